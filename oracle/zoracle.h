@@ -1,0 +1,55 @@
+/*
+ * zoracle.h — TEST INFRASTRUCTURE ONLY (never linked into the product path).
+ *
+ * Plain-C restatement of the reference's compression hot path
+ * (discere-os/zlib.wasm @ zlib 1.3.1.1-motley: deflate.c, trees.c, crc32.c,
+ * adler32.c, compress.c).  Two formulations of deflate live here:
+ *
+ *   zo_compress()     sequential restatement of deflate_fast/deflate_slow over
+ *                     absolute input positions (the reference's algorithm);
+ *   zo_pp_*()         the position-parallel formulation the GPU kernels
+ *                     implement: per-position hash links,
+ *                     per-position longest_match results for both chain budgets,
+ *                     then a sequential parse.  Used to check each GPU stage.
+ *
+ * Parity of this oracle is pinned against the compiled reference
+ * (oracle/_ref/libzref.so, built in the build container only) by
+ * tests/test_oracle.py and by the committed fixtures in tests/golden/.
+ */
+#ifndef ZORACLE_H
+#define ZORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#define ZO_OK            0
+#define ZO_STREAM_ERROR (-2)
+#define ZO_MEM_ERROR    (-4)
+#define ZO_BUF_ERROR    (-5)
+
+/* wrap: 0 = raw deflate (windowBits -15), 1 = zlib (windowBits 15),
+ *       2 = gzip (windowBits 31) */
+unsigned long zo_compress_bound(unsigned long n);
+int zo_compress(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
+                int level, int wrap);
+
+uint32_t zo_crc32(uint32_t crc, const uint8_t *buf, size_t len);
+uint32_t zo_adler32(uint32_t adler, const uint8_t *buf, size_t len);
+uint32_t zo_crc32_combine(uint32_t crc1, uint32_t crc2, int64_t len2);
+uint32_t zo_adler32_combine(uint32_t adler1, uint32_t adler2, int64_t len2);
+
+/* ---- position-parallel formulation (GPU spec) ---- */
+/* link[p] = p - q for the most recent q < p (q <= n-3, q != 0) with
+ * hash3(q) == hash3(p) and p - q <= 32767; 0 when there is none or p > n-3. */
+void zo_pp_links(const uint8_t *src, size_t n, uint16_t *link);
+/* For every p <= n-3 whose head link is within MAX_DIST: the longest_match
+ * result for the level's full chain budget and for the quartered budget,
+ * packed (len << 16) | dist; 0 when no candidate survives the quick reject
+ * or there is no valid head.  Levels 4..9 (all positions inserted). */
+void zo_pp_match(const uint8_t *src, size_t n, int level, const uint16_t *link,
+                 uint32_t *full, uint32_t *quarter);
+/* Whole-stream compression through the position-parallel formulation
+ * (levels 1..9; levels 1..3 use the inserted-set walk of Appendix B.2). */
+int zo_pp_compress(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
+                   int level, int wrap);
+
+#endif

@@ -1,0 +1,174 @@
+"""ctypes helpers for the test suite (TEST INFRASTRUCTURE).
+
+* ``Oracle``    — oracle/liboracle.so, our C restatement of the reference path.
+* ``Reference`` — oracle/_ref/libzref.so, the reference compiled from
+  /root/reference.  It exists only in the build container (it never travels to
+  the GPU box), so tests that need it skip when it is absent.
+"""
+import ctypes as C
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
+REF_SO = os.path.join(ORACLE_DIR, "_ref", "libzref.so")
+
+Z_OK, Z_STREAM_END, Z_STREAM_ERROR, Z_MEM_ERROR, Z_BUF_ERROR = 0, 1, -2, -4, -5
+
+
+def build_oracle():
+    """(Re)build the oracle checker library; cheap when up to date."""
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR, "liboracle.so"], check=True)
+
+
+def compress_bound(n):
+    return n + (n >> 12) + (n >> 14) + (n >> 25) + 13
+
+
+class Oracle:
+    def __init__(self, path=ORACLE_SO):
+        if not os.path.exists(path):
+            build_oracle()
+        L = C.CDLL(path)
+        L.zo_compress.restype = C.c_int
+        L.zo_compress.argtypes = [C.c_void_p, C.POINTER(C.c_size_t), C.c_void_p,
+                                  C.c_size_t, C.c_int, C.c_int]
+        L.zo_pp_compress.restype = C.c_int
+        L.zo_pp_compress.argtypes = L.zo_compress.argtypes
+        for f in ("zo_crc32", "zo_adler32"):
+            getattr(L, f).restype = C.c_uint32
+            getattr(L, f).argtypes = [C.c_uint32, C.c_void_p, C.c_size_t]
+        for f in ("zo_crc32_combine", "zo_adler32_combine"):
+            getattr(L, f).restype = C.c_uint32
+            getattr(L, f).argtypes = [C.c_uint32, C.c_uint32, C.c_int64]
+        L.zo_pp_links.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
+        L.zo_pp_match.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_void_p,
+                                  C.c_void_p, C.c_void_p]
+        self.L = L
+
+    def _compress(self, fn, data, level, wrap, cap):
+        data = bytes(data)
+        if cap is None:
+            cap = compress_bound(len(data)) + 32
+        out = C.create_string_buffer(max(cap, 1))
+        n = C.c_size_t(cap)
+        rc = fn(out, C.byref(n), data, len(data), level, wrap)
+        return rc, out.raw[: n.value]
+
+    def compress(self, data, level=6, wrap=1, cap=None):
+        return self._compress(self.L.zo_compress, data, level, wrap, cap)
+
+    def pp_compress(self, data, level=6, wrap=1, cap=None):
+        return self._compress(self.L.zo_pp_compress, data, level, wrap, cap)
+
+    def crc32(self, data, crc=0):
+        data = bytes(data)
+        return self.L.zo_crc32(crc, data, len(data))
+
+    def adler32(self, data, adler=1):
+        data = bytes(data)
+        return self.L.zo_adler32(adler, data, len(data))
+
+    def links(self, data):
+        import numpy as np
+        data = bytes(data)
+        out = np.zeros(len(data), dtype=np.uint16)
+        self.L.zo_pp_links(data, len(data), out.ctypes.data)
+        return out
+
+    def match(self, data, level, links):
+        import numpy as np
+        data = bytes(data)
+        full = np.zeros(len(data), dtype=np.uint32)
+        quarter = np.zeros(len(data), dtype=np.uint32)
+        self.L.zo_pp_match(data, len(data), level, links.ctypes.data,
+                           full.ctypes.data, quarter.ctypes.data)
+        return full, quarter
+
+
+class ZStream(C.Structure):
+    """z_stream as laid out by zlib.h:90-110 on LP64."""
+    _fields_ = [("next_in", C.c_void_p), ("avail_in", C.c_uint), ("total_in", C.c_ulong),
+                ("next_out", C.c_void_p), ("avail_out", C.c_uint), ("total_out", C.c_ulong),
+                ("msg", C.c_char_p), ("state", C.c_void_p), ("zalloc", C.c_void_p),
+                ("zfree", C.c_void_p), ("opaque", C.c_void_p), ("data_type", C.c_int),
+                ("adler", C.c_ulong), ("reserved", C.c_ulong)]
+
+
+class Reference:
+    """The compiled reference (build container only)."""
+
+    def __init__(self, path=REF_SO):
+        L = C.CDLL(path)
+        L.compress2.restype = C.c_int
+        L.compress2.argtypes = [C.c_void_p, C.POINTER(C.c_ulong), C.c_void_p, C.c_ulong, C.c_int]
+        L.crc32.restype = C.c_ulong
+        L.crc32.argtypes = [C.c_ulong, C.c_void_p, C.c_uint]
+        L.adler32.restype = C.c_ulong
+        L.adler32.argtypes = [C.c_ulong, C.c_void_p, C.c_uint]
+        L.crc32_combine.restype = C.c_ulong
+        L.crc32_combine.argtypes = [C.c_ulong, C.c_ulong, C.c_long]
+        L.adler32_combine.restype = C.c_ulong
+        L.adler32_combine.argtypes = [C.c_ulong, C.c_ulong, C.c_long]
+        L.zlibVersion.restype = C.c_char_p
+        L.deflateInit2_.restype = C.c_int
+        L.deflateInit2_.argtypes = [C.POINTER(ZStream), C.c_int, C.c_int, C.c_int, C.c_int,
+                                    C.c_int, C.c_char_p, C.c_int]
+        L.deflate.restype = C.c_int
+        L.deflate.argtypes = [C.POINTER(ZStream), C.c_int]
+        L.deflateEnd.restype = C.c_int
+        L.deflateEnd.argtypes = [C.POINTER(ZStream)]
+        self.L = L
+        self.version = L.zlibVersion()
+
+    def compress2(self, data, level=6, cap=None):
+        data = bytes(data)
+        if cap is None:
+            cap = compress_bound(len(data))
+        out = C.create_string_buffer(max(cap, 1))
+        n = C.c_ulong(cap)
+        rc = self.L.compress2(out, C.byref(n), data, len(data), level)
+        return rc, out.raw[: n.value]
+
+    def deflate(self, data, level=6, wbits=15, chunk=None):
+        """deflateInit2 + deflate; wbits -15 raw, 15 zlib, 31 gzip.  ``chunk``
+        feeds the input in pieces with Z_NO_FLUSH before Z_FINISH."""
+        data = bytes(data)
+        strm = ZStream()
+        rc = self.L.deflateInit2_(C.byref(strm), level, 8, wbits, 8, 0, self.version,
+                                  C.sizeof(ZStream))
+        assert rc == Z_OK, rc
+        cap = compress_bound(len(data)) + 64
+        out = C.create_string_buffer(cap)
+        inbuf = C.create_string_buffer(data, max(len(data), 1))
+        base_in = C.addressof(inbuf)
+        strm.next_out = C.addressof(out)
+        strm.avail_out = cap
+        pos = 0
+        step = chunk or max(len(data), 1)
+        while True:
+            take = min(step, len(data) - pos)
+            strm.next_in = base_in + pos
+            strm.avail_in = take
+            pos += take
+            flush = 4 if pos >= len(data) else 0
+            rc = self.L.deflate(C.byref(strm), flush)
+            if flush == 4:
+                break
+        assert rc == Z_STREAM_END, rc
+        total = strm.total_out
+        self.L.deflateEnd(C.byref(strm))
+        return out.raw[:total]
+
+    def crc32(self, data, crc=0):
+        data = bytes(data)
+        return self.L.crc32(crc, data, len(data))
+
+    def adler32(self, data, adler=1):
+        data = bytes(data)
+        return self.L.adler32(adler, data, len(data))
+
+
+def reference_available():
+    return os.path.exists(REF_SO)
