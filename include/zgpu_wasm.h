@@ -1,0 +1,45 @@
+/*
+ * zgpu_wasm.h — the reference's WASM front-end exports, re-exported by
+ * libzgpu.so with the same names and C signatures so the existing
+ * compress()/compressSIMD() callers (src/lib/index.ts:120,250,267) bind
+ * unchanged.  All of them route to the GPU path.
+ */
+#ifndef ZGPU_WASM_H
+#define ZGPU_WASM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* src/wasm_module.c:34-46 — compress2 with level clamp; NULL/empty -> Z_STREAM_ERROR */
+int zlib_compress_buffer(const unsigned char *src, unsigned long src_len,
+                         unsigned char *dest, unsigned long *dest_len, int level);
+/* src/wasm_module.c:65-84 */
+unsigned long zlib_crc32(unsigned long crc, const unsigned char *buf, unsigned int len);
+unsigned long zlib_adler32(unsigned long adler, const unsigned char *buf, unsigned int len);
+unsigned long zlib_compress_bound(unsigned long source_len);
+const char *zlib_get_version(void);
+
+/* src/zlib_simd_compression.c:280 and src/zlib_simd_optimized.c:354-383:
+ * raw deflate (windowBits -15).  Deviation: a too-small output returns
+ * Z_BUF_ERROR instead of the reference's Z_OK-with-unchanged-length. */
+int zlib_compress_simd(const uint8_t *input, size_t input_len,
+                       uint8_t *output, size_t *output_len, int level);
+int zlib_compress_simd_full(const uint8_t *input, size_t input_len,
+                            uint8_t *output, size_t *output_len, int level);
+/* src/wasm_module_side.c:61-70: raw deflate for src_len >= 8192, else compress2 */
+int zlib_compress_simd_buffer(const uint8_t *src, size_t src_len,
+                              uint8_t *dest, size_t *dest_len, int level);
+/* src/zlib_simd_compression.c:342, src/zlib_simd_optimized.c:387 */
+uint32_t zlib_crc32_simd_optimized(uint32_t crc, const uint8_t *data, size_t len);
+uint32_t zlib_crc32_simd_enhanced(uint32_t crc, const uint8_t *data, size_t len);
+/* src/zlib_simd_optimized.c:116, with zlib-correct Adler-32 semantics */
+uint32_t zlib_adler32_simd(uint32_t adler, const uint8_t *buf, size_t len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZGPU_WASM_H */

@@ -1,0 +1,110 @@
+/*
+ * zgpu_zlib.h — zlib.h-compatible compression ABI exported by libzgpu.so.
+ *
+ * A program built against the reference's zlib.h (zlib 1.3.1.1-motley) for the
+ * compression side can link libzgpu.so instead of libz: same symbol names, same
+ * signatures, same z_stream layout, same return codes.  Each declaration cites
+ * the reference prototype it replaces.  Decompression (inflate*) is not part of
+ * this library.
+ *
+ * deflate() semantics: deflateInit2_ accepts windowBits 15 / -15 / 31 (zlib /
+ * raw / gzip wrappers), memLevel 8 and Z_DEFAULT_STRATEGY — the configuration
+ * compress2() and the reference's compressSIMD path use
+ * (compress.c:36, src/zlib_simd_optimized.c:365).  Input is gathered across
+ * Z_NO_FLUSH calls and compressed on the GPU at Z_FINISH; the stream is then
+ * drained through next_out/avail_out across as many calls as needed.  Other
+ * parameters, and Z_SYNC_FLUSH/Z_FULL_FLUSH/Z_BLOCK mid-stream, return
+ * Z_STREAM_ERROR (documented gap).
+ */
+#ifndef ZGPU_ZLIB_H
+#define ZGPU_ZLIB_H
+
+#include "zgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef unsigned char Bytef;
+typedef unsigned int uInt;
+typedef unsigned long uLong;
+typedef uLong uLongf;
+typedef void *voidpf;
+typedef voidpf (*alloc_func)(voidpf opaque, uInt items, uInt size);
+typedef void (*free_func)(voidpf opaque, voidpf address);
+
+/* z_stream, field for field as zlib.h:90-110 */
+typedef struct z_stream_s {
+    const Bytef *next_in;
+    uInt avail_in;
+    uLong total_in;
+    Bytef *next_out;
+    uInt avail_out;
+    uLong total_out;
+    const char *msg;
+    struct internal_state *state;
+    alloc_func zalloc;
+    free_func zfree;
+    voidpf opaque;
+    int data_type;
+    uLong adler;
+    uLong reserved;
+} z_stream;
+typedef z_stream *z_streamp;
+
+/* zlib.h:172-204 */
+#define Z_NO_FLUSH      0
+#define Z_PARTIAL_FLUSH 1
+#define Z_SYNC_FLUSH    2
+#define Z_FULL_FLUSH    3
+#define Z_FINISH        4
+#define Z_BLOCK         5
+#define Z_OK            0
+#define Z_STREAM_END    1
+#define Z_STREAM_ERROR (-2)
+#define Z_MEM_ERROR    (-4)
+#define Z_BUF_ERROR    (-5)
+#define Z_VERSION_ERROR (-6)
+#define Z_DEFAULT_COMPRESSION (-1)
+#define Z_DEFAULT_STRATEGY 0
+#define Z_DEFLATED 8
+#define Z_UNKNOWN 2
+
+#define ZGPU_ZLIB_VERSION "1.3.1.1-motley"
+
+const char *zlibVersion(void);                                          /* zlib.h:224 */
+int deflateInit_(z_streamp strm, int level, const char *version,
+                 int stream_size);                                      /* zlib.h:1803 */
+int deflateInit2_(z_streamp strm, int level, int method, int windowBits,
+                  int memLevel, int strategy, const char *version,
+                  int stream_size);                                     /* zlib.h:1807 */
+int deflate(z_streamp strm, int flush);                                 /* zlib.h:254 */
+int deflateEnd(z_streamp strm);                                         /* zlib.h:367 */
+uLong deflateBound(z_streamp strm, uLong sourceLen);                    /* zlib.h:694 */
+int compress(Bytef *dest, uLongf *destLen, const Bytef *source,
+             uLong sourceLen);                                          /* zlib.h:1251 */
+int compress2(Bytef *dest, uLongf *destLen, const Bytef *source,
+              uLong sourceLen, int level);                              /* zlib.h:1266 */
+uLong compressBound(uLong sourceLen);                                   /* zlib.h:1282 */
+uLong adler32(uLong adler, const Bytef *buf, uInt len);                 /* zlib.h:1711 */
+uLong adler32_z(uLong adler, const Bytef *buf, size_t len);             /* zlib.h:1731 */
+uLong adler32_combine(uLong adler1, uLong adler2, long len2);           /* zlib.h:1738 */
+uLong adler32_combine64(uLong adler1, uLong adler2, int64_t len2);
+uLong crc32(uLong crc, const Bytef *buf, uInt len);                     /* zlib.h:1749 */
+uLong crc32_z(uLong crc, const Bytef *buf, size_t len);                 /* zlib.h:1767 */
+uLong crc32_combine(uLong crc1, uLong crc2, long len2);                 /* zlib.h:1774 */
+uLong crc32_combine64(uLong crc1, uLong crc2, int64_t len2);
+uLong crc32_combine_gen(long len2);                                     /* zlib.h:1784 */
+uLong crc32_combine_gen64(int64_t len2);
+uLong crc32_combine_op(uLong crc1, uLong crc2, uLong op);               /* zlib.h:1790 */
+
+#define deflateInit(strm, level) \
+    deflateInit_((strm), (level), ZGPU_ZLIB_VERSION, (int)sizeof(z_stream))
+#define deflateInit2(strm, level, method, windowBits, memLevel, strategy) \
+    deflateInit2_((strm), (level), (method), (windowBits), (memLevel), \
+                  (strategy), ZGPU_ZLIB_VERSION, (int)sizeof(z_stream))
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZGPU_ZLIB_H */

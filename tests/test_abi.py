@@ -1,0 +1,81 @@
+"""CPU tests of the C-ABI library: it loads, exports every symbol the headers
+declare, and the headers and the Python mirror agree.  No compute calls (there
+is no GPU here)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "zlib.wasm_amd", "libzgpu.so")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("zgpu.h", "zgpu_zlib.h", "zgpu_wasm.h")]
+
+
+def declared_functions():
+    names = set()
+    for h in HEADERS:
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        src = re.sub(r"#define[^\n]*(\\\n[^\n]*)*", "", src)
+        src = re.sub(r"typedef[^;]*;", "", src)
+        for m in re.finditer(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\([^;{]*\)\s*;", src):
+            name = m.group(1)
+            if name not in ("sizeof", "alloc_func", "free_func") and not name.startswith("("):
+                names.add(name)
+    return names
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        import subprocess
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "zlib.wasm_amd")], check=True)
+    import torch  # noqa: F401  (share torch's HIP runtime)
+    return C.CDLL(LIB)
+
+
+def test_headers_declare_expected_surface():
+    names = declared_functions()
+    for must in ("compress2", "compressBound", "deflateInit2_", "deflate", "crc32", "crc32_z",
+                 "adler32", "crc32_combine", "zgpu_deflate_batch_dev", "zgpu_crc32_batch_dev",
+                 "zlib_compress_buffer", "zlib_compress_simd", "zlib_crc32_simd_optimized"):
+        assert must in names, must
+
+
+def test_library_exports_every_declared_symbol(lib):
+    missing = [n for n in sorted(declared_functions()) if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_python_mirror_symbol_list_matches_headers():
+    import zgpu
+    assert set(zgpu.EXPORTED_SYMBOLS) == declared_functions()
+
+
+def test_pure_host_entry_points(lib):
+    """Entry points with no device work: bounds, version, combine math."""
+    lib.compressBound.restype = C.c_ulong
+    lib.compressBound.argtypes = [C.c_ulong]
+    for n in (0, 1, 1 << 20, 16 << 20):
+        assert lib.compressBound(n) == n + (n >> 12) + (n >> 14) + (n >> 25) + 13
+    lib.zlibVersion.restype = C.c_char_p
+    assert lib.zlibVersion() == b"1.3.1.1-motley"
+    from zhelpers import Oracle
+    o = Oracle()
+    lib.crc32_combine64.restype = C.c_ulong
+    lib.crc32_combine64.argtypes = [C.c_ulong, C.c_ulong, C.c_int64]
+    lib.adler32_combine64.restype = C.c_ulong
+    lib.adler32_combine64.argtypes = [C.c_ulong, C.c_ulong, C.c_int64]
+    a, b = b"hello world " * 50, bytes(range(256)) * 7
+    assert lib.crc32_combine64(o.crc32(a), o.crc32(b), len(b)) == o.crc32(a + b)
+    assert lib.adler32_combine64(o.adler32(a), o.adler32(b), len(b)) == o.adler32(a + b)
+
+
+def test_no_oracle_linkage():
+    """The product library must not depend on or embed the oracle."""
+    import subprocess
+    out = subprocess.run(["readelf", "-d", LIB], capture_output=True, text=True).stdout
+    assert "oracle" not in out and "zref" not in out
+    syms = subprocess.run(["nm", "-D", LIB], capture_output=True, text=True).stdout
+    assert "zo_" not in syms

@@ -1,0 +1,199 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle and the
+golden fixtures generated from the compiled reference.  Bit-exact everywhere:
+deflate streams byte for byte, CRC-32 / Adler-32 values exactly."""
+import ctypes as C
+import hashlib
+import zlib as pyzlib
+
+import numpy as np
+import pytest
+
+import datagen
+
+pytestmark = pytest.mark.gpu
+
+
+# ----------------------------- checksums -----------------------------
+
+def test_crc_adler_golden(zg, golden):
+    bufs = [datagen.make(c["kind"], c["n"], c["seed"]) for c in golden["cases"]]
+    crcs = zg.crc32_batch(bufs)
+    adls = zg.adler32_batch(bufs)
+    for c, cr, ad in zip(golden["cases"], crcs, adls):
+        assert cr == c["crc32"], (c["kind"], c["n"])
+        assert ad == c["adler32"], (c["kind"], c["n"])
+    assert zg.crc32(b"123456789") == 0xCBF43926
+    assert zg.adler32(b"123456789") == 0x091E01DE
+
+
+def test_crc_adler_ragged_with_init(zg, oracle):
+    rng = np.random.default_rng(5)
+    lens = [0, 1, 2, 3, 4, 5, 15, 16, 17, 31, 63, 64, 65, 1023, 1024, 1025, 4095, 4096, 4097]
+    lens += [int(x) for x in rng.integers(0, 70000, 60)] + [1 << 20, (1 << 20) + 3, 3 * (1 << 20) + 5]
+    bufs = [datagen.random_bytes(n, i) for i, n in enumerate(lens)]
+    inits = [int(x) for x in rng.integers(0, 1 << 32, len(bufs), dtype=np.uint64)]
+    ainit = [int(a) % 65521 | ((int(b) % 65521) << 16) for a, b in
+             zip(rng.integers(0, 65521, len(bufs)), rng.integers(0, 65521, len(bufs)))]
+    got_c = zg.crc32_batch(bufs, inits)
+    got_a = zg.adler32_batch(bufs, ainit)
+    for b, ic, ia, gc, ga in zip(bufs, inits, ainit, got_c, got_a):
+        assert gc == oracle.crc32(b, ic), len(b)
+        assert ga == oracle.adler32(b, ia), len(b)
+
+
+def test_checksum_device_api_unaligned(zg, oracle):
+    import torch
+    rng = np.random.default_rng(7)
+    lens = [int(x) for x in rng.integers(0, 9000, 500)]
+    offs, pos = [], 3
+    for n in lens:
+        offs.append(pos)
+        pos += n + int(rng.integers(0, 5))          # arbitrary alignment
+    host = np.frombuffer(datagen.random_bytes(pos + 16, 1), dtype=np.uint8)
+    src = torch.from_numpy(host.copy()).cuda()
+    off = torch.tensor(offs, dtype=torch.int64).cuda()
+    ln = torch.tensor(lens, dtype=torch.int64).cuda()
+    out = torch.zeros(len(lens), dtype=torch.int32).cuda()
+    zg.crc32_batch_dev(src, off, ln, out)
+    outa = torch.zeros(len(lens), dtype=torch.int32).cuda()
+    zg.adler32_batch_dev(src, off, ln, outa)
+    torch.cuda.synchronize()
+    oc = out.cpu().numpy().view(np.uint32)
+    oa = outa.cpu().numpy().view(np.uint32)
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        b = host[o:o + n].tobytes()
+        assert oc[i] == oracle.crc32(b), (i, n, o)
+        assert oa[i] == oracle.adler32(b), (i, n, o)
+
+
+# ----------------------------- deflate -----------------------------
+
+@pytest.mark.parametrize("level", list(range(10)))
+def test_deflate_golden(zg, golden, level):
+    cases = [c for c in golden["cases"] if c["n"] <= (1 << 20)]
+    bufs = [datagen.make(c["kind"], c["n"], c["seed"]) for c in cases]
+    res = zg.compress_batch(bufs, level=level)
+    for c, (st, z) in zip(cases, res):
+        want = c["levels"][str(level)]
+        assert st == 0
+        assert len(z) == want["len"] and hashlib.sha256(z).hexdigest() == want["sha256"], \
+            (c["kind"], c["n"], level)
+
+
+def test_deflate_wrappers_golden(zg, golden):
+    cases = [c for c in golden["cases"] if c["n"] <= 70000]
+    bufs = [datagen.make(c["kind"], c["n"], c["seed"]) for c in cases]
+    raw = zg.compress_batch(bufs, level=6, wrap=0)
+    gz = zg.compress_batch(bufs, level=6, wrap=2)
+    for c, (s1, r), (s2, g) in zip(cases, raw, gz):
+        assert hashlib.sha256(r).hexdigest() == c["raw6"]["sha256"], (c["kind"], c["n"])
+        assert hashlib.sha256(g).hexdigest() == c["gzip6"]["sha256"], (c["kind"], c["n"])
+
+
+@pytest.mark.parametrize("level", [1, 2, 3, 4, 5, 6, 7, 8, 9])
+def test_deflate_random_sweep_vs_oracle(zg, oracle, level):
+    rng = np.random.default_rng(100 + level)
+    bufs = []
+    for t in range(48):
+        kind = ["text", "runs", "four", "random", "mix", "markup", "records"][t % 7]
+        n = int(rng.choice([int(rng.integers(0, 700)), int(rng.integers(700, 70000)),
+                            int(rng.integers(70000, 400000))]))
+        bufs.append(datagen.make(kind, n, int(rng.integers(0, 1 << 30))))
+    res = zg.compress_batch(bufs, level=level)
+    for b, (st, z) in zip(bufs, res):
+        rc, want = oracle.compress(b, level)
+        assert st == 0 and z == want, (len(b), level)
+
+
+def test_deflate_short_output(zg, oracle):
+    data = datagen.mix(60000, 3)
+    _, full = oracle.compress(data, 6)
+    caps = [0, 1, 2, 9, len(full) // 2, len(full) - 1, len(full), len(full) + 100]
+    res = zg.compress_batch([data] * len(caps), level=6, caps=caps)
+    for cap, (st, z) in zip(caps, res):
+        if cap < len(full):
+            assert st == -5 and z == full[:cap], cap
+        else:
+            assert st == 0 and z == full
+
+
+def test_deflate_device_generated_silesia(zg, oracle):
+    """Device-generated benchmark input (Silesia-style mix): GPU vs oracle."""
+    import torch
+    n, count = 1 << 20, 6
+    src = torch.empty(n * count, dtype=torch.uint8, device="cuda")
+    zg.generate_dev(src, n, count, zg.KIND_SILESIA, seed=42)
+    cap = zg.compress_bound(n)
+    cap = (cap + 15) // 16 * 16
+    off = torch.arange(count, dtype=torch.int64, device="cuda") * n
+    ln = torch.full((count,), n, dtype=torch.int64, device="cuda")
+    dst = torch.zeros(cap * count, dtype=torch.uint8, device="cuda")
+    doff = torch.arange(count, dtype=torch.int64, device="cuda") * cap
+    dcap = torch.full((count,), cap, dtype=torch.int64, device="cuda")
+    dlen = torch.zeros(count, dtype=torch.int64, device="cuda")
+    st = torch.zeros(count, dtype=torch.int32, device="cuda")
+    zg.deflate_batch_dev(src, off, ln, dst, doff, dcap, dlen, st, level=6)
+    torch.cuda.synchronize()
+    h_src, h_dst = src.cpu().numpy(), dst.cpu().numpy()
+    dl, sts = dlen.cpu().numpy(), st.cpu().numpy()
+    ratios = []
+    for i in range(count):
+        data = h_src[i * n:(i + 1) * n].tobytes()
+        z = h_dst[i * cap: i * cap + dl[i]].tobytes()
+        assert sts[i] == 0
+        assert z == oracle.compress(data, 6)[1], i
+        assert pyzlib.decompress(z) == data
+        ratios.append(n / len(z))
+    assert 2.0 < float(np.mean(ratios)) < 6.0, ratios
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+def test_generator_kinds_roundtrip_l1_l9(zg, oracle, kind):
+    import torch
+    n, count = 300000, 2
+    src = torch.empty(n * count, dtype=torch.uint8, device="cuda")
+    zg.generate_dev(src, n, count, kind, seed=7)
+    h = src.cpu().numpy()
+    bufs = [h[i * n:(i + 1) * n].tobytes() for i in range(count)]
+    for level in (1, 9):
+        for b, (st, z) in zip(bufs, zg.compress_batch(bufs, level=level)):
+            assert st == 0 and z == oracle.compress(b, level)[1]
+
+
+def test_dropin_zlib_names(zg, oracle):
+    L = zg.load()
+    data = datagen.text(12345, 9)
+    rc, z = zg.compress2(data, 9)
+    assert rc == 0 and z == oracle.compress(data, 9)[1]
+    # zlib_compress_simd: raw deflate (src/zlib_simd_optimized.c:365)
+    out = C.create_string_buffer(zg.compress_bound(len(data)))
+    olen = C.c_size_t(len(out))
+    assert L.zlib_compress_simd(data, len(data), out, C.byref(olen), 6) == 0
+    assert out.raw[:olen.value] == oracle.compress(data, 6, wrap=0)[1]
+    # streaming deflate(): Z_NO_FLUSH chunks then Z_FINISH, drained 1000 B at a time
+    from zhelpers import ZStream
+    L.deflateInit2_.argtypes = [C.POINTER(ZStream), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                C.c_char_p, C.c_int]
+    L.deflate.argtypes = [C.POINTER(ZStream), C.c_int]
+    L.deflateEnd.argtypes = [C.POINTER(ZStream)]
+    s = ZStream()
+    assert L.deflateInit2_(C.byref(s), 6, 8, 31, 8, 0, b"1.3.1.1-motley", C.sizeof(ZStream)) == 0
+    inbuf = C.create_string_buffer(data, len(data))
+    outbuf = C.create_string_buffer(1000)
+    got = b""
+    for k in range(0, len(data), 4000):
+        s.next_in = C.addressof(inbuf) + k
+        s.avail_in = min(4000, len(data) - k)
+        s.next_out, s.avail_out = C.addressof(outbuf), 1000
+        assert L.deflate(C.byref(s), 0) == 0
+    while True:
+        s.next_out, s.avail_out = C.addressof(outbuf), 1000
+        rc = L.deflate(C.byref(s), 4)
+        got += outbuf.raw[:1000 - s.avail_out]
+        if rc == 1:
+            break
+        assert rc == 0
+    assert L.deflateEnd(C.byref(s)) == 0
+    assert got == oracle.compress(data, 6, wrap=2)[1]
+    z = zg.Zlib().compress(data, level=6)
+    assert z.data == oracle.compress(data, 6)[1] and z.originalSize == len(data)

@@ -1,0 +1,127 @@
+"""CPU tests: pin the oracle (our C restatement) to the reference.
+
+* against the committed golden fixtures (generated from the compiled reference
+  by tests/golden/make_golden.py) — always;
+* against the compiled reference itself — in the build container only, where
+  oracle/_ref/libzref.so exists;
+* the position-parallel formulation (the GPU's spec) against both.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import datagen
+from zhelpers import Reference, reference_available
+
+
+def _cases(golden, maxn=None):
+    for c in golden["cases"]:
+        if maxn is None or c["n"] <= maxn:
+            yield c
+
+
+def test_golden_inputs_regenerate(golden):
+    for c in _cases(golden):
+        data = datagen.make(c["kind"], c["n"], c["seed"])
+        assert hashlib.sha256(data).hexdigest() == c["sha256"], (c["kind"], c["n"])
+
+
+@pytest.mark.parametrize("pp", [False, True], ids=["sequential", "position-parallel"])
+def test_oracle_matches_golden_all_levels(oracle, golden, pp):
+    fn = oracle.pp_compress if pp else oracle.compress
+    for c in _cases(golden, maxn=1 << 20):
+        data = datagen.make(c["kind"], c["n"], c["seed"])
+        levels = range(10) if c["n"] <= 70000 else (1, 4, 6, 9)
+        for lvl in levels:
+            rc, z = fn(data, lvl)
+            want = c["levels"][str(lvl)]
+            assert rc == 0
+            assert len(z) == want["len"], (c["kind"], c["n"], lvl)
+            assert hashlib.sha256(z).hexdigest() == want["sha256"], (c["kind"], c["n"], lvl)
+            if "hex" in want:
+                assert z.hex() == want["hex"]
+
+
+def test_oracle_wrappers_golden(oracle, golden):
+    for c in _cases(golden, maxn=70000):
+        data = datagen.make(c["kind"], c["n"], c["seed"])
+        _, raw = oracle.compress(data, 6, wrap=0)
+        _, gz = oracle.compress(data, 6, wrap=2)
+        assert hashlib.sha256(raw).hexdigest() == c["raw6"]["sha256"]
+        assert hashlib.sha256(gz).hexdigest() == c["gzip6"]["sha256"]
+
+
+def test_oracle_checksums_golden(oracle, golden):
+    for c in _cases(golden):
+        data = datagen.make(c["kind"], c["n"], c["seed"])
+        assert oracle.crc32(data) == c["crc32"]
+        assert oracle.adler32(data) == c["adler32"]
+    for hexs, k in golden["known"].items():
+        s = bytes.fromhex(hexs)
+        assert oracle.crc32(s) == k["crc32"]
+        assert oracle.adler32(s) == k["adler32"]
+        for lvl in (1, 6, 9):
+            assert oracle.compress(s, lvl)[1].hex() == k[f"z{lvl}"]
+    # public known answers
+    assert oracle.crc32(b"123456789") == 0xCBF43926
+    assert oracle.adler32(b"123456789") == 0x091E01DE
+    assert oracle.crc32(b"Hello, World!") == 0xEC4AC3D0
+
+
+def test_oracle_combine(oracle):
+    a, b = datagen.text(5000, 1), datagen.random_bytes(7777, 2)
+    L = oracle.L
+    assert L.zo_crc32_combine(oracle.crc32(a), oracle.crc32(b), len(b)) == oracle.crc32(a + b)
+    assert L.zo_adler32_combine(oracle.adler32(a), oracle.adler32(b), len(b)) == oracle.adler32(a + b)
+
+
+def test_oracle_short_output(oracle):
+    """compress2 with a short destination: Z_BUF_ERROR and a prefix (compress.c:44-58)."""
+    data = datagen.text(20000, 5)
+    _, full = oracle.compress(data, 6)
+    for cap in (0, 1, 2, 7, len(full) // 2, len(full) - 1):
+        rc, z = oracle.compress(data, 6, cap=cap)
+        assert rc == -5 and z == full[:cap]
+    rc, z = oracle.compress(data, 6, cap=len(full))
+    assert rc == 0 and z == full
+
+
+@pytest.mark.skipif(not reference_available(), reason="compiled reference only in build container")
+def test_oracle_vs_reference_random_sweep(oracle):
+    ref = Reference()
+    rng = np.random.default_rng(2024)
+    for t in range(60):
+        kind = ["text", "runs", "four", "random", "mix", "markup", "records"][t % 7]
+        n = int(rng.choice([int(rng.integers(0, 600)), int(rng.integers(600, 40000)),
+                            int(rng.integers(40000, 200000))]))
+        data = datagen.make(kind, n, int(rng.integers(0, 1 << 30)))
+        for lvl in (0, 1, 2, 3, 4, 5, 6, 7, 8, 9):
+            rc, want = ref.compress2(data, lvl)
+            assert oracle.compress(data, lvl)[1] == want, (kind, n, lvl)
+            assert oracle.pp_compress(data, lvl)[1] == want, (kind, n, lvl)
+
+
+@pytest.mark.skipif(not reference_available(), reason="compiled reference only in build container")
+def test_oracle_vs_reference_short_output():
+    from zhelpers import Oracle
+    ref, o = Reference(), Oracle()
+    data = datagen.mix(50000, 9)
+    for lvl in (1, 6, 9):
+        _, full = ref.compress2(data, lvl)
+        for cap in (0, 1, 5, len(full) // 3, len(full) - 1):
+            rc, z = ref.compress2(data, lvl, cap=cap)
+            rc2, z2 = o.compress(data, lvl, cap=cap)
+            assert (rc, z) == (rc2, z2)
+
+
+@pytest.mark.skipif(not reference_available(), reason="compiled reference only in build container")
+def test_reference_chunked_input_equals_one_shot():
+    """Feeding deflate() with Z_NO_FLUSH chunks gives the one-shot stream, which
+    is what lets the drop-in deflate() gather input until Z_FINISH."""
+    ref = Reference()
+    data = datagen.mix(200000, 4)
+    for lvl in (1, 6, 9):
+        one = ref.deflate(data, lvl, 15)
+        for chunk in (1000, 4096, 65536):
+            assert ref.deflate(data, lvl, 15, chunk=chunk) == one

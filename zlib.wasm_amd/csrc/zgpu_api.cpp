@@ -1,0 +1,721 @@
+// zgpu_api.cpp — host side of libzgpu.so: device bring-up, static tables,
+// sub-batch orchestration of the deflate pipeline, and the three exported
+// C ABIs (batched zgpu_*, zlib.h names, the reference's WASM front-end names).
+//
+// Every compute path runs on the GPU.  There is deliberately no CPU fallback:
+// with no usable device every entry point fails (ZGPU_ENODEV / Z_MEM_ERROR)
+// after printing one diagnostic.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "zgpu_internal.h"
+#include "../../include/zgpu.h"
+#include "../../include/zgpu_zlib.h"
+#include "../../include/zgpu_wasm.h"
+
+using namespace zgpu;
+
+namespace {
+
+// ------------------------------------------------------------------------
+// host restatement of the table derivations (trees.c:303-396, crc32.c)
+// ------------------------------------------------------------------------
+constexpr uint32_t kPoly = 0xedb88320u;
+
+uint32_t multmodp(uint32_t a, uint32_t b) {                  // crc32.c:155-170
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+        if (a & m) { p ^= b; if ((a & (m - 1)) == 0) break; }
+        m >>= 1;
+        b = (b & 1u) ? (b >> 1) ^ kPoly : b >> 1;
+    }
+    return p;
+}
+uint32_t x2nmodp(int64_t n, unsigned k) {                     // crc32.c:176-187
+    static uint32_t x2n[32];
+    static std::once_flag once;
+    std::call_once(once, [] {
+        uint32_t p = 1u << 30;
+        x2n[0] = p;
+        for (int i = 1; i < 32; i++) x2n[i] = p = multmodp(p, p);
+    });
+    uint32_t p = 1u << 31;
+    while (n) {
+        if (n & 1) p = multmodp(x2n[k & 31], p);
+        n >>= 1;
+        k++;
+    }
+    return p;
+}
+
+unsigned bitrev(unsigned code, int len) {
+    unsigned r = 0;
+    while (len-- > 0) { r = (r << 1) | (code & 1u); code >>= 1; }
+    return r;
+}
+
+void build_code_tables(CodeTables &t) {
+    std::memset(&t, 0, sizeof t);
+    static const uint8_t xl[29] = {0,0,0,0,0,0,0,0,1,1,1,1,2,2,2,2,3,3,3,3,4,4,4,4,5,5,5,5,0};
+    static const uint8_t xd[30] = {0,0,0,0,1,1,2,2,3,3,4,4,5,5,6,6,7,7,8,8,9,9,10,10,11,11,12,12,13,13};
+    static const uint8_t xb[19] = {0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,2,3,7};
+    static const uint8_t bo[19] = {16,17,18,0,8,7,9,6,10,5,11,4,12,3,13,2,14,1,15};
+    std::memcpy(t.xlbits, xl, 29);
+    std::memcpy(t.xdbits, xd, 30);
+    std::memcpy(t.xblbits, xb, 19);
+    std::memcpy(t.bl_order, bo, 19);
+    int length = 0, code;
+    for (code = 0; code < 28; code++) {
+        t.len_base[code] = (uint16_t)length;
+        for (int k = 0; k < (1 << xl[code]); k++) t.len_code[length++] = (uint8_t)code;
+    }
+    t.len_code[255] = 28;
+    t.len_base[28] = 0;
+    int dist = 0;
+    for (code = 0; code < 16; code++) {
+        t.dist_base[code] = (uint16_t)dist;
+        for (int k = 0; k < (1 << xd[code]); k++) t.dist_code[dist++] = (uint8_t)code;
+    }
+    dist >>= 7;
+    for (; code < 30; code++) {
+        t.dist_base[code] = (uint16_t)(dist << 7);
+        for (int k = 0; k < (1 << (xd[code] - 7)); k++) t.dist_code[256 + dist++] = (uint8_t)code;
+    }
+    uint16_t cnt[16] = {0};
+    for (int n = 0; n < 288; n++) {
+        t.stat_llen[n] = (uint8_t)(n < 144 ? 8 : n < 256 ? 9 : n < 280 ? 7 : 8);
+        cnt[t.stat_llen[n]]++;
+    }
+    uint16_t next[16];
+    unsigned c = 0;
+    for (int b = 1; b <= 15; b++) { c = (c + cnt[b - 1]) << 1; next[b] = (uint16_t)c; }
+    for (int n = 0; n < 288; n++) t.stat_lcode[n] = (uint16_t)bitrev(next[t.stat_llen[n]]++, t.stat_llen[n]);
+    for (int n = 0; n < 30; n++) t.stat_dcode[n] = (uint16_t)bitrev((unsigned)n, 5);
+    static const LevelCfg cfg[10] = {{0, 0, 0, 0},      {4, 4, 8, 4},       {4, 5, 16, 8},
+                                     {4, 6, 32, 32},    {4, 4, 16, 16},    {8, 16, 32, 32},
+                                     {8, 16, 128, 128}, {8, 32, 128, 256}, {32, 128, 258, 1024},
+                                     {32, 258, 258, 4096}};
+    std::memcpy(t.cfg, cfg, sizeof cfg);
+}
+
+void build_crc_tables(CrcTables &t) {
+    for (uint32_t v = 0; v < 256; v++) {
+        uint32_t c = v;
+        for (int k = 0; k < 8; k++) c = (c & 1u) ? kPoly ^ (c >> 1) : c >> 1;
+        t.byte[v] = c;
+    }
+    auto raw_crc = [&](const uint8_t *m, int len) {
+        uint32_t c = 0;
+        for (int i = 0; i < len; i++) c = (c >> 8) ^ t.byte[(c ^ m[i]) & 0xffu];
+        return c;
+    };
+    for (int j = 0; j < 32; j++)
+        for (uint32_t v = 0; v < 16; v++) {
+            uint8_t msg[16] = {0};
+            msg[j >> 1] = (uint8_t)(v << (4 * (j & 1)));
+            t.nib[j][v] = raw_crc(msg, 16);
+        }
+    const uint64_t amounts[kCrcShiftTabs] = {16, 32, 64, 128, 256, 512, 1024, kCrcSegment};
+    for (int k = 0; k < kCrcShiftTabs; k++) {
+        const uint32_t op = x2nmodp((int64_t)amounts[k], 3);
+        for (int j = 0; j < 8; j++)
+            for (uint32_t v = 0; v < 16; v++) t.shift[k][j][v] = multmodp(op, v << (4 * j));
+    }
+}
+
+// ------------------------------------------------------------------------
+// device context
+// ------------------------------------------------------------------------
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    bool ensure(size_t bytes) {
+        if (bytes <= cap) return true;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes + bytes / 8 + 4096;
+        if (hipMalloc(&p, want) != hipSuccess) { p = nullptr; return false; }
+        cap = want;
+        return true;
+    }
+    template <typename T> T *as() const { return static_cast<T *>(p); }
+};
+
+struct Ctx {
+    std::mutex mu;
+    int state = 0;            // 0 uninit, 1 ok, -1 failed
+    int device = 0;
+    std::string info;
+    CrcTables *d_crc = nullptr;
+    size_t inflight = size_t(1) << 30;
+    DevBuf ws_link, ws_rf, ws_rq, ws_sym, ws_blk, ws_meta, ws_heads, ws_io, ws_io2, ws_small;
+};
+
+Ctx &ctx() {
+    static Ctx c;
+    return c;
+}
+
+const CrcTables *g_dev_crc = nullptr;
+
+int init_locked(Ctx &c) {
+    if (c.state == 1) return ZGPU_OK;
+    if (c.state == -1) return ZGPU_ENODEV;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        std::fprintf(stderr, "libzgpu: no HIP device available; the GPU path cannot run\n");
+        c.state = -1;
+        return ZGPU_ENODEV;
+    }
+    (void)hipGetDevice(&c.device);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c.device) != hipSuccess) { c.state = -1; return ZGPU_ENODEV; }
+    c.info = std::string("libzgpu gfx950 build; device ") + std::to_string(c.device) + ": " +
+             prop.name + " (" + prop.gcnArchName + "), " + std::to_string(prop.multiProcessorCount) +
+             " CUs";
+    CodeTables ct;
+    build_code_tables(ct);
+    static CrcTables crc;
+    build_crc_tables(crc);
+    if (launch_tables_upload(&ct, &crc) != 0) { c.state = -1; return ZGPU_ENODEV; }
+    if (hipMalloc(&c.d_crc, sizeof(CrcTables)) != hipSuccess) { c.state = -1; return ZGPU_ENODEV; }
+    if (hipMemcpy(c.d_crc, &crc, sizeof(CrcTables), hipMemcpyHostToDevice) != hipSuccess) {
+        c.state = -1;
+        return ZGPU_ENODEV;
+    }
+    g_dev_crc = c.d_crc;
+    if (const char *e = std::getenv("ZGPU_INFLIGHT_MB")) c.inflight = size_t(std::atoll(e)) << 20;
+    c.state = 1;
+    return ZGPU_OK;
+}
+
+int ensure_init() {
+    Ctx &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    return init_locked(c);
+}
+
+inline int hip_ok(hipError_t e) { return e == hipSuccess ? ZGPU_OK : ZGPU_MEM_ERROR; }
+
+// ------------------------------------------------------------------------
+// deflate orchestration (caller holds ctx().mu)
+// ------------------------------------------------------------------------
+int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
+                       uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
+                       uint64_t *dst_len, int32_t *status, uint32_t count, int level, int wrap,
+                       hipStream_t st) {
+    if (level == -1) level = 6;
+    if (level < 0 || level > 9 || wrap < 0 || wrap > 2) return ZGPU_STREAM_ERROR;
+    if (count == 0) return ZGPU_OK;
+    std::vector<uint64_t> lens(count);
+    if (hipMemcpyAsync(lens.data(), src_len, 8ull * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return ZGPU_MEM_ERROR;
+
+    // plan sub-batches: Σ n <= inflight (a single larger buffer runs alone)
+    std::vector<uint32_t> cuts{0};
+    {
+        uint64_t acc = 0;
+        for (uint32_t i = 0; i < count; i++) {
+            if (acc > 0 && acc + lens[i] > c.inflight) { cuts.push_back(i); acc = 0; }
+            acc += lens[i];
+        }
+        cuts.push_back(count);
+    }
+    uint64_t max_pos = 0, max_blk = 0;
+    uint32_t max_cnt = 0;
+    std::vector<uint64_t> meta(2ull * count);   // [ws_off | blk_off] per buffer, sub-batch relative
+    for (size_t s = 0; s + 1 < cuts.size(); s++) {
+        uint64_t pos = 0, blk = 0;
+        const uint32_t a = cuts[s], b = cuts[s + 1];
+        for (uint32_t i = a; i < b; i++) {
+            meta[i] = pos;
+            meta[count + i] = blk;
+            pos += (lens[i] + 63) & ~63ull;
+            blk += lens[i] / kSymLimit + 2;
+        }
+        max_pos = std::max(max_pos, pos);
+        max_blk = std::max(max_blk, blk);
+        max_cnt = std::max(max_cnt, b - a);
+    }
+    const bool slow = level >= 4, quarter = level >= 5;
+    if (!c.ws_meta.ensure(16ull * count + 8ull * max_cnt * 2)) return ZGPU_MEM_ERROR;
+    if (!c.ws_link.ensure(2 * max_pos + 64)) return ZGPU_MEM_ERROR;
+    if (!c.ws_sym.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
+    if (!c.ws_blk.ensure(sizeof(BlockRec) * max_blk)) return ZGPU_MEM_ERROR;
+    if (slow && !c.ws_rf.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
+    if (quarter && !c.ws_rq.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
+    if (level >= 1 && level <= 3 && !c.ws_heads.ensure(4ull * 32768 * max_cnt)) return ZGPU_MEM_ERROR;
+    uint64_t *d_meta = c.ws_meta.as<uint64_t>();
+    uint32_t *d_nblk = reinterpret_cast<uint32_t *>(d_meta + 2ull * count);
+    uint32_t *d_check = d_nblk + max_cnt;
+    if (hipMemcpyAsync(d_meta, meta.data(), 16ull * count, hipMemcpyHostToDevice, st) != hipSuccess)
+        return ZGPU_MEM_ERROR;
+
+    for (size_t s = 0; s + 1 < cuts.size(); s++) {
+        const uint32_t a = cuts[s], b = cuts[s + 1];
+        DeflateJob job{};
+        job.src = src; job.src_off = src_off; job.src_len = src_len;
+        job.dst = dst; job.dst_off = dst_off; job.dst_cap = dst_cap;
+        job.dst_len = dst_len; job.status = status;
+        job.first = a; job.count = b - a; job.level = level; job.wrap = wrap;
+        job.ws_off = d_meta + a;
+        job.blk_off = d_meta + count + a;
+        job.link = c.ws_link.as<uint16_t>();
+        job.rfull = slow ? c.ws_rf.as<uint32_t>() : nullptr;
+        job.rquart = quarter ? c.ws_rq.as<uint32_t>() : c.ws_rf.as<uint32_t>();
+        job.sym = c.ws_sym.as<uint32_t>();
+        job.blocks = c.ws_blk.as<BlockRec>();
+        job.nblocks = d_nblk;
+        job.check = d_check;
+        int rc = 0;
+        if (wrap == 1) rc = launch_adler32(src, src_off + a, src_len + a, nullptr, d_check, b - a, nullptr, 0, st);
+        else if (wrap == 2) rc = launch_crc32(src, src_off + a, src_len + a, nullptr, d_check, b - a, nullptr, 0, st);
+        if (rc) return ZGPU_MEM_ERROR;
+        if (level >= 4) {
+            if (launch_deflate_stage(0, job, nullptr, st)) return ZGPU_MEM_ERROR;
+            if (launch_deflate_stage(1, job, nullptr, st)) return ZGPU_MEM_ERROR;
+            if (launch_deflate_stage(2, job, nullptr, st)) return ZGPU_MEM_ERROR;
+        } else if (level >= 1) {
+            if (launch_deflate_stage(3, job, c.ws_heads.as<uint32_t>(), st)) return ZGPU_MEM_ERROR;
+        }
+        if (launch_deflate_stage(4, job, nullptr, st)) return ZGPU_MEM_ERROR;
+    }
+    return hip_ok(hipStreamSynchronize(st));
+}
+
+// host-buffer batch: pack, upload, run, download
+int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
+                         size_t *dst_len, int *status, size_t count, int level, int wrap) {
+    if (count == 0) return ZGPU_OK;
+    std::vector<uint64_t> so(count), sl(count), dofs(count), dcap(count);
+    uint64_t in_total = 0, out_total = 0;
+    for (size_t i = 0; i < count; i++) {
+        so[i] = in_total;
+        sl[i] = src_len[i];
+        in_total += (src_len[i] + 15) & ~15ull;
+        dofs[i] = out_total;
+        dcap[i] = dst_len[i];
+        out_total += (dst_len[i] + 15) & ~15ull;
+    }
+    const size_t meta_bytes = 8 * 4 * count + 16 * count;
+    if (!c.ws_io.ensure(in_total + 64) || !c.ws_io2.ensure(out_total + 64) ||
+        !c.ws_small.ensure(meta_bytes + 64))
+        return ZGPU_MEM_ERROR;
+    uint8_t *d_in = c.ws_io.as<uint8_t>(), *d_out = c.ws_io2.as<uint8_t>();
+    uint64_t *d_so = c.ws_small.as<uint64_t>();
+    uint64_t *d_sl = d_so + count, *d_do = d_sl + count, *d_dc = d_do + count, *d_dl = d_dc + count;
+    int32_t *d_st = reinterpret_cast<int32_t *>(d_dl + count);
+    hipStream_t st = nullptr;
+    for (size_t i = 0; i < count; i++)
+        if (src_len[i] && hipMemcpyAsync(d_in + so[i], src[i], src_len[i], hipMemcpyHostToDevice, st) != hipSuccess)
+            return ZGPU_MEM_ERROR;
+    if (hipMemcpyAsync(d_so, so.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_sl, sl.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_do, dofs.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_dc, dcap.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess)
+        return ZGPU_MEM_ERROR;
+    int rc = deflate_dev_locked(c, d_in, d_so, d_sl, d_out, d_do, d_dc, d_dl, d_st, (uint32_t)count,
+                                level, wrap, st);
+    if (rc) return rc;
+    std::vector<uint64_t> ol(count);
+    std::vector<int32_t> os(count);
+    if (hipMemcpy(ol.data(), d_dl, 8 * count, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(os.data(), d_st, 4 * count, hipMemcpyDeviceToHost) != hipSuccess)
+        return ZGPU_MEM_ERROR;
+    for (size_t i = 0; i < count; i++) {
+        if (ol[i] && hipMemcpy(dst[i], d_out + dofs[i], ol[i], hipMemcpyDeviceToHost) != hipSuccess)
+            return ZGPU_MEM_ERROR;
+        dst_len[i] = ol[i];
+        if (status) status[i] = os[i];
+    }
+    return ZGPU_OK;
+}
+
+// host-buffer checksum batch.  Large buffers are cut into 1 MiB pieces so a
+// single huge buffer still spreads over the whole GPU; pieces are joined with
+// crc32_combine / adler32_combine (crc32.c:1021, adler32.c:133).
+uint32_t adler_combine(uint32_t a1, uint32_t a2, int64_t len2);
+uint32_t crc_combine(uint32_t c1, uint32_t c2, int64_t len2) {
+    return multmodp(x2nmodp(len2, 3), c1) ^ c2;
+}
+
+int checksum_host_locked(Ctx &c, bool is_crc, const uint8_t *const *src, const size_t *len,
+                         const uint32_t *init, uint32_t *out, size_t count) {
+    constexpr uint64_t kPiece = 1ull << 20;
+    struct Piece { size_t buf; uint64_t off, len; };
+    std::vector<Piece> pieces;
+    std::vector<size_t> first(count + 1);
+    for (size_t i = 0; i < count; i++) {
+        first[i] = pieces.size();
+        uint64_t L = len[i];
+        if (L == 0) { pieces.push_back({i, 0, 0}); continue; }
+        for (uint64_t o = 0; o < L; o += kPiece) pieces.push_back({i, o, std::min(kPiece, L - o)});
+    }
+    first[count] = pieces.size();
+    const size_t np = pieces.size();
+    std::vector<uint64_t> po(np), pl(np);
+    uint64_t total = 0;
+    for (size_t k = 0; k < np; k++) {
+        po[k] = total;
+        pl[k] = pieces[k].len;
+        total += (pieces[k].len + 15) & ~15ull;
+    }
+    if (!c.ws_io.ensure(total + 64) || !c.ws_small.ensure(8 * 2 * np + 8 * np + 64)) return ZGPU_MEM_ERROR;
+    uint8_t *d_in = c.ws_io.as<uint8_t>();
+    uint64_t *d_po = c.ws_small.as<uint64_t>(), *d_pl = d_po + np;
+    uint32_t *d_init = reinterpret_cast<uint32_t *>(d_pl + np), *d_out = d_init + np;
+    std::vector<uint32_t> pinit(np, is_crc ? 0u : 1u);
+    for (size_t i = 0; i < count; i++)
+        if (init) pinit[first[i]] = init[i];
+    hipStream_t st = nullptr;
+    for (size_t k = 0; k < np; k++)
+        if (pieces[k].len &&
+            hipMemcpyAsync(d_in + po[k], src[pieces[k].buf] + pieces[k].off, pieces[k].len,
+                           hipMemcpyHostToDevice, st) != hipSuccess)
+            return ZGPU_MEM_ERROR;
+    if (hipMemcpyAsync(d_po, po.data(), 8 * np, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_pl, pl.data(), 8 * np, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_init, pinit.data(), 4 * np, hipMemcpyHostToDevice, st) != hipSuccess)
+        return ZGPU_MEM_ERROR;
+    int rc = is_crc ? launch_crc32(d_in, d_po, d_pl, d_init, d_out, (uint32_t)np, nullptr, 0, st)
+                    : launch_adler32(d_in, d_po, d_pl, d_init, d_out, (uint32_t)np, nullptr, 0, st);
+    if (rc) return ZGPU_MEM_ERROR;
+    std::vector<uint32_t> res(np);
+    if (hipMemcpy(res.data(), d_out, 4 * np, hipMemcpyDeviceToHost) != hipSuccess) return ZGPU_MEM_ERROR;
+    for (size_t i = 0; i < count; i++) {
+        uint32_t v = res[first[i]];
+        for (size_t k = first[i] + 1; k < first[i + 1]; k++)
+            v = is_crc ? crc_combine(v, res[k], (int64_t)pieces[k].len)
+                       : adler_combine(v, res[k], (int64_t)pieces[k].len);
+        out[i] = v;
+    }
+    return ZGPU_OK;
+}
+
+constexpr uint32_t kBase = 65521u;
+uint32_t adler_combine(uint32_t adler1, uint32_t adler2, int64_t len2) {   // adler32.c:133-155
+    if (len2 < 0) return 0xffffffffu;
+    uint32_t rem = (uint32_t)(len2 % kBase);
+    uint32_t s1 = adler1 & 0xffffu;
+    uint32_t s2 = (uint32_t)(((uint64_t)rem * s1) % kBase);
+    s1 += (adler2 & 0xffffu) + kBase - 1;
+    s2 += ((adler1 >> 16) & 0xffffu) + ((adler2 >> 16) & 0xffffu) + kBase - rem;
+    if (s1 >= kBase) s1 -= kBase;
+    if (s1 >= kBase) s1 -= kBase;
+    if (s2 >= (kBase << 1)) s2 -= (kBase << 1);
+    if (s2 >= kBase) s2 -= kBase;
+    return s1 | (s2 << 16);
+}
+
+uint64_t compress_bound64(uint64_t n) {                      // compress.c:72-75
+    return n + (n >> 12) + (n >> 14) + (n >> 25) + 13;
+}
+
+}  // namespace
+
+namespace zgpu {
+const CrcTables *device_crc_tables() { return g_dev_crc; }
+}  // namespace zgpu
+
+// ==========================================================================
+// exported C ABI
+// ==========================================================================
+extern "C" {
+
+int zgpu_init(void) { return ensure_init(); }
+
+const char *zgpu_info(void) {
+    Ctx &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    if (init_locked(c) != ZGPU_OK) return "libzgpu: no GPU";
+    return c.info.c_str();
+}
+
+size_t zgpu_set_inflight_bytes(size_t bytes) {
+    Ctx &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    size_t old = c.inflight;
+    if (bytes >= (1u << 20)) c.inflight = bytes;
+    return old;
+}
+
+int zgpu_deflate_batch_dev(const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
+                           uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
+                           uint64_t *dst_len, int32_t *status, uint32_t count, int level, int wrap,
+                           void *stream) {
+    Ctx &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    int rc = init_locked(c);
+    if (rc) return rc;
+    return deflate_dev_locked(c, src, src_off, src_len, dst, dst_off, dst_cap, dst_len, status,
+                              count, level, wrap, static_cast<hipStream_t>(stream));
+}
+
+int zgpu_crc32_batch_dev(const uint8_t *src, const uint64_t *off, const uint64_t *len,
+                         const uint32_t *init, uint32_t *out, uint32_t count, void *stream) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    return launch_crc32(src, off, len, init, out, count, nullptr, 0, static_cast<hipStream_t>(stream))
+               ? ZGPU_MEM_ERROR : ZGPU_OK;
+}
+
+int zgpu_adler32_batch_dev(const uint8_t *src, const uint64_t *off, const uint64_t *len,
+                           const uint32_t *init, uint32_t *out, uint32_t count, void *stream) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    return launch_adler32(src, off, len, init, out, count, nullptr, 0, static_cast<hipStream_t>(stream))
+               ? ZGPU_MEM_ERROR : ZGPU_OK;
+}
+
+int zgpu_compress_batch(const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
+                        size_t *dst_len, int *status, size_t count, int level, int wrap) {
+    Ctx &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    int rc = init_locked(c);
+    if (rc) return rc;
+    return compress_host_locked(c, src, src_len, dst, dst_len, status, count, level, wrap);
+}
+
+int zgpu_crc32_batch(const uint8_t *const *src, const size_t *len, const uint32_t *init,
+                     uint32_t *out, size_t count) {
+    Ctx &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    int rc = init_locked(c);
+    if (rc) return rc;
+    return checksum_host_locked(c, true, src, len, init, out, count);
+}
+
+int zgpu_adler32_batch(const uint8_t *const *src, const size_t *len, const uint32_t *init,
+                       uint32_t *out, size_t count) {
+    Ctx &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    int rc = init_locked(c);
+    if (rc) return rc;
+    return checksum_host_locked(c, false, src, len, init, out, count);
+}
+
+int zgpu_generate_dev(uint8_t *dst, uint64_t len, uint32_t count, int kind, uint64_t seed,
+                      uint64_t first_index, void *stream) {
+    int rc = ensure_init();
+    if (rc) return rc;
+    return launch_generate(dst, len, count, kind, seed, first_index, static_cast<hipStream_t>(stream))
+               ? ZGPU_STREAM_ERROR : ZGPU_OK;
+}
+
+// ---------------------------- zlib.h names ----------------------------
+
+const char *zlibVersion(void) { return ZGPU_ZLIB_VERSION; }
+
+uLong compressBound(uLong sourceLen) { return (uLong)compress_bound64(sourceLen); }
+
+int compress2(Bytef *dest, uLongf *destLen, const Bytef *source, uLong sourceLen, int level) {
+    if (!destLen) return Z_STREAM_ERROR;
+    if (level != Z_DEFAULT_COMPRESSION && (level < 0 || level > 9)) { *destLen = 0; return Z_STREAM_ERROR; }
+    if (!dest || (sourceLen && !source)) { *destLen = 0; return Z_STREAM_ERROR; }
+    size_t cap = *destLen;
+    const uint8_t *s = source;
+    uint8_t *d = dest;
+    size_t sl = sourceLen;
+    int st = 0;
+    int rc = zgpu_compress_batch(&s, &sl, &d, &cap, &st, 1, level, ZGPU_WRAP_ZLIB);
+    if (rc == ZGPU_ENODEV) { *destLen = 0; return Z_MEM_ERROR; }
+    if (rc) { *destLen = 0; return rc; }
+    *destLen = cap;
+    return st;
+}
+
+int compress(Bytef *dest, uLongf *destLen, const Bytef *source, uLong sourceLen) {
+    return compress2(dest, destLen, source, sourceLen, Z_DEFAULT_COMPRESSION);
+}
+
+static uint32_t checksum_one(bool is_crc, uint32_t init, const Bytef *buf, size_t len) {
+    const uint8_t *p = buf;
+    uint32_t out = 0;
+    int rc = is_crc ? zgpu_crc32_batch(&p, &len, &init, &out, 1) : zgpu_adler32_batch(&p, &len, &init, &out, 1);
+    if (rc) {
+        std::fprintf(stderr, "libzgpu: %s failed on the GPU (rc %d)\n", is_crc ? "crc32" : "adler32", rc);
+        std::abort();       // no CPU fallback: fail loudly
+    }
+    return out;
+}
+
+uLong crc32_z(uLong crc, const Bytef *buf, size_t len) {
+    if (buf == nullptr) return 0;                      // crc32.c:700
+    return checksum_one(true, (uint32_t)crc, buf, len);
+}
+uLong crc32(uLong crc, const Bytef *buf, uInt len) { return crc32_z(crc, buf, len); }
+uLong adler32_z(uLong adler, const Bytef *buf, size_t len) {
+    if (buf == nullptr) return 1;                      // adler32.c:83-84
+    return checksum_one(false, (uint32_t)adler, buf, len);
+}
+uLong adler32(uLong adler, const Bytef *buf, uInt len) { return adler32_z(adler, buf, len); }
+
+uLong crc32_combine64(uLong crc1, uLong crc2, int64_t len2) {
+    return crc_combine((uint32_t)crc1, (uint32_t)crc2, len2);
+}
+uLong crc32_combine(uLong crc1, uLong crc2, long len2) { return crc32_combine64(crc1, crc2, len2); }
+uLong crc32_combine_gen64(int64_t len2) { return x2nmodp(len2, 3); }
+uLong crc32_combine_gen(long len2) { return crc32_combine_gen64(len2); }
+uLong crc32_combine_op(uLong crc1, uLong crc2, uLong op) {
+    return multmodp((uint32_t)op, (uint32_t)crc1) ^ (uint32_t)crc2;
+}
+uLong adler32_combine64(uLong adler1, uLong adler2, int64_t len2) {
+    return adler_combine((uint32_t)adler1, (uint32_t)adler2, len2);
+}
+uLong adler32_combine(uLong adler1, uLong adler2, long len2) { return adler32_combine64(adler1, adler2, len2); }
+
+// z_stream deflate: gather input, compress on the GPU at Z_FINISH, drain.
+struct internal_state {
+    int level, wrap;
+    std::vector<uint8_t> in, out;
+    size_t out_pos;
+    int finished;     // 0 gathering, 1 compressed
+};
+
+int deflateInit2_(z_streamp strm, int level, int method, int windowBits, int memLevel, int strategy,
+                  const char *version, int stream_size) {
+    if (!version || version[0] != ZGPU_ZLIB_VERSION[0] || stream_size != (int)sizeof(z_stream))
+        return Z_VERSION_ERROR;                         // deflate.c:386-389
+    if (!strm) return Z_STREAM_ERROR;
+    strm->msg = nullptr;
+    if (level == Z_DEFAULT_COMPRESSION) level = 6;
+    int wrap;
+    if (windowBits == 15) wrap = 1;
+    else if (windowBits == -15) wrap = 0;
+    else if (windowBits == 31) wrap = 2;
+    else return Z_STREAM_ERROR;
+    if (method != Z_DEFLATED || memLevel != 8 || strategy != Z_DEFAULT_STRATEGY || level < 0 || level > 9)
+        return Z_STREAM_ERROR;
+    internal_state *s = new (std::nothrow) internal_state();
+    if (!s) return Z_MEM_ERROR;
+    s->level = level;
+    s->wrap = wrap;
+    s->out_pos = 0;
+    s->finished = 0;
+    strm->state = s;
+    strm->total_in = strm->total_out = 0;
+    strm->data_type = Z_UNKNOWN;
+    strm->adler = wrap == 2 ? 0 : 1;
+    return Z_OK;
+}
+
+int deflateInit_(z_streamp strm, int level, const char *version, int stream_size) {
+    return deflateInit2_(strm, level, Z_DEFLATED, 15, 8, Z_DEFAULT_STRATEGY, version, stream_size);
+}
+
+int deflate(z_streamp strm, int flush) {
+    if (!strm || !strm->state || flush < 0 || flush > Z_BLOCK) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    if (!strm->next_out || (strm->avail_in && !strm->next_in)) return Z_STREAM_ERROR;
+    if (flush != Z_NO_FLUSH && flush != Z_FINISH) return Z_STREAM_ERROR;   // documented gap
+    if (strm->avail_out == 0) return Z_BUF_ERROR;
+    if (s->finished && strm->avail_in) return Z_BUF_ERROR;
+    if (strm->avail_in) {
+        s->in.insert(s->in.end(), strm->next_in, strm->next_in + strm->avail_in);
+        strm->total_in += strm->avail_in;
+        strm->next_in += strm->avail_in;
+        strm->avail_in = 0;
+    }
+    if (flush == Z_FINISH && !s->finished) {
+        size_t cap = (size_t)compress_bound64(s->in.size()) + 32;
+        s->out.resize(cap);
+        const uint8_t *sp = s->in.data();
+        uint8_t *dp = s->out.data();
+        size_t sl = s->in.size();
+        int st = 0;
+        int rc = zgpu_compress_batch(&sp, &sl, &dp, &cap, &st, 1, s->level, s->wrap);
+        if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
+        s->out.resize(cap);
+        s->finished = 1;
+        strm->adler = s->wrap == 2 ? crc32_z(0, sp, sl) : (s->wrap == 1 ? adler32_z(1, sp, sl) : 0);
+        s->in.clear();
+        s->in.shrink_to_fit();
+    }
+    if (!s->finished) return Z_OK;
+    size_t take = std::min<size_t>(strm->avail_out, s->out.size() - s->out_pos);
+    std::memcpy(strm->next_out, s->out.data() + s->out_pos, take);
+    s->out_pos += take;
+    strm->next_out += take;
+    strm->avail_out -= (uInt)take;
+    strm->total_out += take;
+    return s->out_pos == s->out.size() ? Z_STREAM_END : Z_OK;
+}
+
+int deflateEnd(z_streamp strm) {
+    if (!strm || !strm->state) return Z_STREAM_ERROR;
+    delete strm->state;
+    strm->state = nullptr;
+    return Z_OK;
+}
+
+uLong deflateBound(z_streamp strm, uLong sourceLen) {          // deflate.c:842-905
+    const uLong fixedlen = sourceLen + (sourceLen >> 3) + (sourceLen >> 8) + (sourceLen >> 9) + 4;
+    const uLong storelen = sourceLen + (sourceLen >> 5) + (sourceLen >> 7) + (sourceLen >> 11) + 7;
+    if (!strm || !strm->state) return (fixedlen > storelen ? fixedlen : storelen) + 18;
+    const int w = strm->state->wrap;
+    const uLong wraplen = w == 0 ? 0 : w == 1 ? 6 : 18;
+    return sourceLen + (sourceLen >> 12) + (sourceLen >> 14) + (sourceLen >> 25) + 13 - 6 + wraplen;
+}
+
+// ----------------------- reference WASM front-end -----------------------
+
+int zlib_compress_buffer(const unsigned char *src, unsigned long src_len, unsigned char *dest,
+                         unsigned long *dest_len, int level) {         // src/wasm_module.c:34-46
+    if (!src || !dest || !dest_len || src_len == 0) return Z_STREAM_ERROR;
+    if (level < 0 || level > 9) level = Z_DEFAULT_COMPRESSION;
+    return compress2(dest, dest_len, src, src_len, level);
+}
+unsigned long zlib_crc32(unsigned long crc, const unsigned char *buf, unsigned int len) {
+    return crc32(crc, buf, len);                                      // src/wasm_module.c:65-68
+}
+unsigned long zlib_adler32(unsigned long adler, const unsigned char *buf, unsigned int len) {
+    return adler32(adler, buf, len);                                  // src/wasm_module.c:73-76
+}
+unsigned long zlib_compress_bound(unsigned long source_len) { return compressBound(source_len); }
+const char *zlib_get_version(void) { return zlibVersion(); }
+
+int zlib_compress_simd_full(const uint8_t *input, size_t input_len, uint8_t *output,
+                            size_t *output_len, int level) {         // src/zlib_simd_optimized.c:354-383
+    if (!input || !output || !output_len) return Z_STREAM_ERROR;
+    if (level < 0 || level > 9) level = Z_DEFAULT_COMPRESSION;
+    size_t cap = *output_len;
+    int st = 0;
+    int rc = zgpu_compress_batch(&input, &input_len, &output, &cap, &st, 1, level, ZGPU_WRAP_RAW);
+    if (rc) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : rc;
+    if (st) return st;      // Z_BUF_ERROR (documented deviation: the reference returns Z_OK)
+    *output_len = cap;
+    return Z_OK;
+}
+int zlib_compress_simd(const uint8_t *input, size_t input_len, uint8_t *output, size_t *output_len,
+                       int level) {                                   // src/zlib_simd_compression.c:280
+    return zlib_compress_simd_full(input, input_len, output, output_len, level);
+}
+uint32_t zlib_crc32_simd_enhanced(uint32_t crc, const uint8_t *data, size_t len) {
+    return (uint32_t)crc32_z(crc, data, len);                         // src/zlib_simd_optimized.c:387
+}
+uint32_t zlib_crc32_simd_optimized(uint32_t crc, const uint8_t *data, size_t len) {
+    return (uint32_t)crc32_z(crc, data, len);                         // src/zlib_simd_compression.c:342
+}
+uint32_t zlib_adler32_simd(uint32_t adler, const uint8_t *buf, size_t len) {
+    return (uint32_t)adler32_z(adler, buf, len);   // zlib-correct, unlike src/zlib_simd_optimized.c:116
+}
+int zlib_compress_simd_buffer(const uint8_t *src, size_t src_len, uint8_t *dest, size_t *dest_len,
+                              int level) {                            // src/wasm_module_side.c:61-70
+    if (src_len >= 8192) return zlib_compress_simd(src, src_len, dest, dest_len, level);
+    unsigned long dl = *dest_len;
+    int rc = compress2(dest, &dl, src, src_len, level);
+    *dest_len = dl;
+    return rc;
+}
+
+}  // extern "C"

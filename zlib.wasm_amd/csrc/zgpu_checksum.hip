@@ -1,0 +1,220 @@
+// zgpu_checksum.hip — batched CRC-32 and Adler-32 for gfx950.
+//
+// One wave (64 lanes) per buffer.  The buffer is viewed as left-padded with
+// zeros to a multiple of 1 KiB ("rows"); lane i owns the 16-byte chunk at
+// 16*i of every row.  Zero padding in front leaves a zero-init CRC and the
+// Adler sums unchanged, so no lane ever handles a ragged tail.
+//
+// CRC-32 (crc32.c:694-1010): the init value is folded in by XOR-ing ~init into
+// the first four data bytes (for len >= 4 the register state after a message
+// M from init s equals the zero-init state of M ^ s), so the whole buffer is a
+// single linear (zero-init) CRC R and crc32(init, M) = ~R.  A chunk's CRC is
+// 32 lookups in conflict-free 16-entry nibble tables in LDS; rows are combined
+// per lane by Horner (advance by 1024 zero bytes, 8 lookups), lanes by a 6-level
+// shuffle tree (advance by 16<<l bytes) — crc32_combine (crc32.c:1021) with the
+// x^(8n) multipliers pre-tabulated.
+//
+// Adler-32 (adler32.c:61-125): per chunk the byte sum and the position-weighted
+// sum via v_dot4_u32_u8; weights are distances to the (virtual) end of the
+// buffer, so A = a0 + Σx and B = b0 + L*a0 + Σ (L-j+1) x_j with one modulo at the
+// end.  Tiny buffers (len < 16, len == 1 paths of adler32.c; len < 4 for CRC)
+// take the reference's scalar path in lane 0.
+#include "zgpu_internal.h"
+
+namespace zgpu {
+
+constexpr int kCkBlock = 256;                 // 4 waves per workgroup
+constexpr uint32_t kAdlerBase = 65521u;
+
+__device__ inline void load_chunk16(const uint8_t *buf, int64_t x, uint64_t L, uint32_t w[4]) {
+    // bytes buf[x .. x+16), zero where x+j < 0; never reads outside [buf, buf+L)
+    if (x >= 0) {
+        const uint8_t *p = buf + x;
+        uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        uint32_t sh = (uint32_t)(a & 3u);
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+        if (sh == 0) {
+            if ((a & 15u) == 0) {
+                uint4 v = *reinterpret_cast<const uint4 *>(p);
+                w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+            } else {
+                w[0] = q[0]; w[1] = q[1]; w[2] = q[2]; w[3] = q[3];
+            }
+        } else {
+            uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
+            w[0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
+            w[1] = __builtin_amdgcn_alignbyte(d2, d1, sh);
+            w[2] = __builtin_amdgcn_alignbyte(d3, d2, sh);
+            w[3] = __builtin_amdgcn_alignbyte(d4, d3, sh);
+        }
+        (void)L;
+        return;
+    }
+    w[0] = w[1] = w[2] = w[3] = 0;
+    if (x + 16 <= 0) return;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        int64_t o = x + j;
+        if (o >= 0) w[j >> 2] |= (uint32_t)buf[o] << (8 * (j & 3));
+    }
+}
+
+__device__ inline uint32_t crc_shift(uint32_t x, const uint32_t (*t)[16]) {
+    uint32_t y = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) y ^= t[j][(x >> (4 * j)) & 15u];
+    return y;
+}
+
+__global__ __launch_bounds__(kCkBlock) void k_crc32(const uint8_t *__restrict__ src,
+                                                    const uint64_t *__restrict__ off,
+                                                    const uint64_t *__restrict__ len,
+                                                    const uint32_t *__restrict__ init,
+                                                    uint32_t *__restrict__ out, uint32_t count,
+                                                    const CrcTables *__restrict__ tab) {
+    __shared__ uint32_t s_nib[32][16];
+    __shared__ uint32_t s_sh[7][8][16];
+    __shared__ uint32_t s_byte[256];
+    for (int i = threadIdx.x; i < 32 * 16; i += kCkBlock) (&s_nib[0][0])[i] = (&tab->nib[0][0])[i];
+    for (int i = threadIdx.x; i < 7 * 8 * 16; i += kCkBlock) (&s_sh[0][0][0])[i] = (&tab->shift[0][0][0])[i];
+    for (int i = threadIdx.x; i < 256; i += kCkBlock) s_byte[i] = tab->byte[i];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = threadIdx.x >> 6;
+    for (uint32_t b = blockIdx.x * (kCkBlock / 64) + wave; b < count; b += gridDim.x * (kCkBlock / 64)) {
+        const uint64_t L = len[b];
+        const uint8_t *buf = src + off[b];
+        const uint32_t c0 = init ? init[b] : 0u;
+        if (L < 4) {                                   // crc32.c byte loop (tiny input)
+            if (lane == 0) {
+                uint32_t c = ~c0;
+                for (uint64_t i = 0; i < L; i++) c = (c >> 8) ^ s_byte[(c ^ buf[i]) & 0xffu];
+                out[b] = ~c;
+            }
+            continue;
+        }
+        const uint64_t V = (L + 1023) & ~(uint64_t)1023;
+        const int64_t pad = (int64_t)(V - L);
+        const uint32_t xv = ~c0;
+        uint32_t acc = 0;
+        for (uint64_t row = 0; row < V; row += 1024) {
+            const int64_t x = (int64_t)row + 16 * lane - pad;
+            uint32_t w[4];
+            load_chunk16(buf, x, L, w);
+            if (x < 4 && x + 16 > 0) {                 // fold ~init into data bytes 0..3
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    int64_t o = x + j;
+                    if (o >= 0 && o < 4) w[j >> 2] ^= ((xv >> (8 * o)) & 0xffu) << (8 * (j & 3));
+                }
+            }
+            uint32_t c = 0;
+#pragma unroll
+            for (int j = 0; j < 32; j++) c ^= s_nib[j][(w[j >> 3] >> (4 * (j & 7))) & 15u];
+            acc = crc_shift(acc, s_sh[6]) ^ c;
+        }
+#pragma unroll
+        for (int l = 0; l < 6; l++) {
+            uint32_t other = __shfl_down(acc, 1 << l, 64);
+            acc = crc_shift(acc, s_sh[l]) ^ other;
+        }
+        if (lane == 0) out[b] = ~acc;
+    }
+}
+
+__device__ inline uint32_t dot4(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_udot4(a, b, c, false);
+}
+
+__global__ __launch_bounds__(kCkBlock) void k_adler32(const uint8_t *__restrict__ src,
+                                                      const uint64_t *__restrict__ off,
+                                                      const uint64_t *__restrict__ len,
+                                                      const uint32_t *__restrict__ init,
+                                                      uint32_t *__restrict__ out, uint32_t count) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = threadIdx.x >> 6;
+    for (uint32_t b = blockIdx.x * (kCkBlock / 64) + wave; b < count; b += gridDim.x * (kCkBlock / 64)) {
+        const uint64_t L = len[b];
+        const uint8_t *buf = src + off[b];
+        const uint32_t a0 = init ? init[b] : 1u;
+        if (L < 16) {                                  // adler32.c:71-94 verbatim semantics
+            if (lane == 0) {
+                uint32_t a = a0 & 0xffffu, s2 = (a0 >> 16) & 0xffffu;
+                if (L == 1) {
+                    a += buf[0];
+                    if (a >= kAdlerBase) a -= kAdlerBase;
+                    s2 += a;
+                    if (s2 >= kAdlerBase) s2 -= kAdlerBase;
+                } else {
+                    for (uint64_t i = 0; i < L; i++) { a += buf[i]; s2 += a; }
+                    if (a >= kAdlerBase) a -= kAdlerBase;
+                    s2 %= kAdlerBase;
+                }
+                out[b] = a | (s2 << 16);
+            }
+            continue;
+        }
+        const uint64_t V = (L + 1023) & ~(uint64_t)1023;
+        const int64_t pad = (int64_t)(V - L);
+        uint64_t s1 = 0, s2 = 0;
+        for (uint64_t row = 0; row < V; row += 1024) {
+            const int64_t x = (int64_t)row + 16 * lane - pad;
+            uint32_t w[4];
+            load_chunk16(buf, x, L, w);
+            uint32_t sx = dot4(w[0], 0x01010101u, 0);
+            sx = dot4(w[1], 0x01010101u, sx);
+            sx = dot4(w[2], 0x01010101u, sx);
+            sx = dot4(w[3], 0x01010101u, sx);
+            uint32_t sj = dot4(w[0], 0x03020100u, 0);
+            sj = dot4(w[1], 0x07060504u, sj);
+            sj = dot4(w[2], 0x0b0a0908u, sj);
+            sj = dot4(w[3], 0x0f0e0d0cu, sj);
+            // weight of chunk byte j = V - (row + 16*lane) - j
+            const uint64_t wt = (V - row - 16u * (uint64_t)lane) % kAdlerBase;
+            s1 += sx;
+            s2 += wt * sx + kAdlerBase - sj;
+        }
+#pragma unroll
+        for (int l = 32; l >= 1; l >>= 1) {
+            s1 += __shfl_down(s1, l, 64);
+            s2 += __shfl_down(s2, l, 64);
+        }
+        if (lane == 0) {
+            const uint64_t A0 = a0 & 0xffffu, B0 = (a0 >> 16) & 0xffffu;
+            uint64_t A = (A0 + s1) % kAdlerBase;
+            uint64_t B = (B0 + (L % kAdlerBase) * A0 + s2 % kAdlerBase) % kAdlerBase;
+            out[b] = (uint32_t)A | ((uint32_t)B << 16);
+        }
+    }
+}
+
+static int grid_for(uint32_t count) {
+    uint32_t waves = count;
+    uint32_t blocks = (waves + (kCkBlock / 64) - 1) / (kCkBlock / 64);
+    if (blocks > 4096) blocks = 4096;
+    if (blocks == 0) blocks = 1;
+    return (int)blocks;
+}
+
+int launch_crc32(const uint8_t *src, const uint64_t *off, const uint64_t *len,
+                 const uint32_t *init, uint32_t *out, uint32_t count,
+                 void *, size_t, hipStream_t st) {
+    if (count == 0) return 0;
+    hipLaunchKernelGGL(k_crc32, dim3(grid_for(count)), dim3(kCkBlock), 0, st, src, off, len, init,
+                       out, count, device_crc_tables());
+    return (int)hipGetLastError();
+}
+
+int launch_adler32(const uint8_t *src, const uint64_t *off, const uint64_t *len,
+                   const uint32_t *init, uint32_t *out, uint32_t count,
+                   void *, size_t, hipStream_t st) {
+    if (count == 0) return 0;
+    hipLaunchKernelGGL(k_adler32, dim3(grid_for(count)), dim3(kCkBlock), 0, st, src, off, len,
+                       init, out, count);
+    return (int)hipGetLastError();
+}
+
+size_t checksum_scratch_bytes(uint32_t) { return 0; }
+
+}  // namespace zgpu

@@ -1,0 +1,929 @@
+// zgpu_deflate.hip — batched deflate for gfx950, bit-identical to the
+// reference deflate.c/trees.c (zlib 1.3.1.1-motley) at the same level.
+//
+// Pipeline per sub-batch of independent buffers:
+//   k_links      wave/buffer   hash-chain links: link[p] = distance to the most
+//                              recent earlier position with the same 3-byte
+//                              hash (UPDATE_HASH/INSERT_STRING, deflate.c:141,160)
+//   k_match      1024 thr/buf  levels 4..9: longest_match (deflate.c:1356-1497) at
+//                              EVERY position for the full and the quartered chain
+//                              budget, 32 KiB window + links staged in LDS
+//   k_parse_slow wave/buffer   deflate_slow's lazy parse (deflate.c:1923-2043) over
+//                              the per-position results -> symbols + block cuts
+//   k_parse_fast wave/buffer   deflate_fast (deflate.c:1824-1915), levels 1..3,
+//                              whose insertions depend on the parse
+//   k_encode     256 thr/buf   per block: histogram, zlib's Huffman construction
+//                              (trees.c:499-706), block-type choice
+//                              (trees.c:997-1089), parallel bit packing through an
+//                              LDS staging window; zlib/gzip framing + trailer
+#include "zgpu_internal.h"
+
+namespace zgpu {
+
+__constant__ CodeTables c_ct;
+
+// ------------------------------------------------------------------------
+// small helpers
+// ------------------------------------------------------------------------
+__device__ inline uint32_t hash3(uint32_t b0, uint32_t b1, uint32_t b2) {
+    return ((b0 & 31u) << 10) ^ (b1 << 5) ^ b2;        // UPDATE_HASH x3, hash_shift 5
+}
+
+// unaligned 4-byte read from an LDS byte array (two aligned dwords + alignbyte)
+__device__ inline uint32_t lds32u(const uint8_t *base, int off) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(base + (off & ~3));
+    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(off & 3));
+}
+
+// ------------------------------------------------------------------------
+// k_links — one wave per buffer.  head[] holds the low 16 bits of the most
+// recent position per hash; every 32 KiB it is swept like slide_hash
+// (deflate.c:187-209) so no live entry is ever 64 Ki positions old.
+// Within a 64-position chunk the nearest earlier lane with the same hash is
+// found with a shuffle scan; only the last lane of each hash updates head[].
+// ------------------------------------------------------------------------
+constexpr int kLinkStage = 4096;
+
+__global__ __launch_bounds__(64) void k_links(DeflateJob job) {
+    __shared__ uint16_t head[32768];
+    __shared__ uint8_t stage[kLinkStage + 8];
+    __shared__ uint8_t mark[64];
+    const int lane = threadIdx.x;
+    const uint32_t bi = blockIdx.x;
+    const uint32_t g = job.first + bi;
+    const int64_t n = (int64_t)job.src_len[g];
+    const uint8_t *in = job.src + job.src_off[g];
+    uint16_t *out = job.link + job.ws_off[bi];
+
+    for (int i = lane; i < 32768; i += 64) head[i] = 32768;   // "position -32768"
+    for (int64_t t0 = 0; t0 < n; t0 += kLinkStage) {
+        __syncthreads();
+        const int64_t tl = (n - t0 < kLinkStage + 2) ? n - t0 : kLinkStage + 2;
+        for (int j = lane; j < kLinkStage + 2; j += 64) stage[j] = j < tl ? in[t0 + j] : 0;
+        __syncthreads();
+        const int64_t tend = (t0 + kLinkStage < n) ? t0 + kLinkStage : n;
+        for (int64_t c0 = t0; c0 < tend; c0 += 64) {
+            if ((c0 & 32767) == 0 && c0 > 0) {                // slide sweep
+                const uint32_t now = (uint32_t)c0;
+                for (int i = lane; i < 32768; i += 64) {
+                    uint32_t age = (now - head[i]) & 0xffffu;
+                    if (age == 0 || age >= 32768u) head[i] = (uint16_t)((now - 32768u) & 0xffffu);
+                }
+                __syncthreads();
+            }
+            const int64_t p = c0 + lane;
+            const bool valid = p + 3 <= n;
+            const int j = (int)(p - t0);
+            uint32_t h = valid ? hash3(stage[j], stage[j + 1], stage[j + 2]) : (0x10000u + lane);
+            int pred = -1;
+            for (int d = 1; d < 64; d++) {
+                uint32_t v = __shfl_up(h, d, 64);
+                if (pred < 0 && lane >= d && v == h) pred = lane - d;
+            }
+            mark[lane] = 0;
+            __syncthreads();
+            if (pred >= 0) mark[pred] = 1;
+            uint32_t link = 0;
+            if (valid) {
+                uint32_t d;
+                if (pred >= 0) d = (uint32_t)(lane - pred);
+                else d = ((uint32_t)p - head[h]) & 0xffffu;
+                if (d != 0 && d <= 32767u && (int64_t)d != p) link = d;   // position 0 is NIL
+            }
+            __syncthreads();
+            if (valid && mark[lane] == 0) head[h] = (uint16_t)(p & 0xffff);
+            if (p < n) out[p] = (uint16_t)link;
+            __syncthreads();
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
+// k_match — levels 4..9.  One 1024-thread workgroup per buffer walks tiles of
+// kMT positions.  LDS holds input bytes [ts-32768, ts+kMT+272) and links
+// [ts-32768, ts+kMT); between tiles both slide down by kMT.  Every position's
+// walk follows longest_match exactly (quick reject, first strictly longer
+// match wins, stop at nice, chain budget, limit = max(p-MAX_DIST, 0)), records
+// the result after chain/4 candidates too, and stores (len<<16 | dist).
+// ------------------------------------------------------------------------
+constexpr int kMW = 32768, kMT = 4096, kMPad = 272;
+constexpr int kMDat = kMW + kMT + kMPad;                   // 37136 bytes
+constexpr int kMLnk = kMW + kMT;                            // 36864 entries
+constexpr int kMatchThreads = 1024;
+
+__device__ inline void match_walk(const uint8_t *dat, const uint16_t *lnk, int64_t p, int64_t B,
+                                  int64_t n, LevelCfg cfg, uint32_t &rf, uint32_t &rq) {
+    rf = rq = 0;
+    const int s = (int)(p - B);
+    const uint32_t d0 = lnk[s];
+    if (d0 == 0 || d0 > (uint32_t)kMaxDist) return;
+    const int64_t labs = p > kMaxDist ? p - kMaxDist : 0;
+    const int limit = (int)(labs - B);
+    const int64_t rem = n - p;
+    const int nice = rem < cfg.nice ? (int)rem : cfg.nice;
+    const int maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
+    const uint32_t chain = cfg.chain, bq = cfg.chain >> 2;
+    const uint32_t scan0 = lds32u(dat, s) & 0xffffu;
+    int best = kMinMatch - 1, bpos = 0, bestq = 0, bposq = 0;
+    bool snapped = false;
+    uint32_t scan_end = lds32u(dat, s + best - 1) & 0xffffu;
+    int m = s - (int)d0;
+    uint32_t count = 0;
+    for (;;) {
+        count++;
+        bool stop = false;
+        if ((lds32u(dat, m) & 0xffffu) == scan0 && (lds32u(dat, m + best - 1) & 0xffffu) == scan_end) {
+            int k = 0;
+            for (;;) {
+                uint32_t x = lds32u(dat, s + k) ^ lds32u(dat, m + k);
+                if (x) { k += __builtin_ctz(x) >> 3; break; }
+                k += 4;
+                if (k >= maxcmp) break;
+            }
+            const int len = k < maxcmp ? k : maxcmp;
+            if (len > best) {
+                best = len;
+                bpos = m;
+                if (len >= nice) stop = true;
+                else scan_end = lds32u(dat, s + best - 1) & 0xffffu;
+            }
+        }
+        if (count == bq) { bestq = best; bposq = bpos; snapped = true; }
+        if (stop || count >= chain) break;
+        const uint32_t d = lnk[m];
+        if (d == 0) break;
+        m -= (int)d;
+        if (m <= limit) break;
+    }
+    if (!snapped) { bestq = best; bposq = bpos; }
+    if (best >= kMinMatch) rf = ((uint32_t)best << 16) | (uint32_t)(s - bpos);
+    if (bestq >= kMinMatch) rq = ((uint32_t)bestq << 16) | (uint32_t)(s - bposq);
+}
+
+__global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int want_q) {
+    __shared__ __attribute__((aligned(16))) uint8_t dat[kMDat];
+    __shared__ __attribute__((aligned(16))) uint16_t lnk[kMLnk];
+    __shared__ int next_i;
+    const int tid = threadIdx.x;
+    const uint32_t bi = blockIdx.x;
+    const uint32_t g = job.first + bi;
+    const int64_t n = (int64_t)job.src_len[g];
+    const uint8_t *in = job.src + job.src_off[g];
+    const uint16_t *L = job.link + job.ws_off[bi];
+    uint32_t *rf = job.rfull + job.ws_off[bi];
+    uint32_t *rq = job.rquart + job.ws_off[bi];
+    const LevelCfg cfg = c_ct.cfg[job.level];
+
+    for (int64_t ts = 0; ts < n; ts += kMT) {
+        const int64_t B = ts - kMW;
+        if (ts == 0) {
+            for (int i = tid; i < kMDat; i += kMatchThreads) {
+                int64_t q = B + i;
+                dat[i] = (q >= 0 && q < n) ? in[q] : 0;
+            }
+            for (int i = tid; i < kMLnk; i += kMatchThreads) {
+                int64_t q = B + i;
+                lnk[i] = (q >= 0 && q < n) ? L[q] : 0;
+            }
+        } else {
+            // slide both windows down by kMT (register round trip)
+            constexpr int kDatChunks = (kMDat - kMT) / 16;          // 2065
+            constexpr int kLnkChunks = (kMW * 2) / 16;              // 4096
+            uint4 td[3], tl[4];
+            const uint4 *sd = reinterpret_cast<const uint4 *>(dat + kMT);
+            const uint4 *sl = reinterpret_cast<const uint4 *>(lnk + kMT);
+#pragma unroll
+            for (int k = 0; k < 3; k++) { int c = tid + k * kMatchThreads; if (c < kDatChunks) td[k] = sd[c]; }
+#pragma unroll
+            for (int k = 0; k < 4; k++) { int c = tid + k * kMatchThreads; tl[k] = sl[c]; }
+            __syncthreads();
+            uint4 *dd = reinterpret_cast<uint4 *>(dat);
+            uint4 *dl = reinterpret_cast<uint4 *>(lnk);
+#pragma unroll
+            for (int k = 0; k < 3; k++) { int c = tid + k * kMatchThreads; if (c < kDatChunks) dd[c] = td[k]; }
+#pragma unroll
+            for (int k = 0; k < 4; k++) { int c = tid + k * kMatchThreads; dl[c] = tl[k]; }
+            for (int i = tid; i < kMT; i += kMatchThreads) {
+                int64_t q = B + (kMDat - kMT) + i;
+                dat[kMDat - kMT + i] = (q < n) ? in[q] : 0;
+                int64_t r = ts + i;
+                lnk[kMW + i] = (r < n) ? L[r] : 0;
+            }
+        }
+        if (tid == 0) next_i = 0;
+        __syncthreads();
+        for (;;) {
+            const int i = atomicAdd(&next_i, 1);
+            const int64_t p = ts + i;
+            if (i >= kMT || p >= n) break;
+            uint32_t a, b;
+            match_walk(dat, lnk, p, B, n, cfg, a, b);
+            rf[p] = a;
+            if (want_q) rq[p] = b;
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------
+// block bookkeeping shared by both parses (lane 0 only)
+// ------------------------------------------------------------------------
+struct ParseOut {
+    uint32_t *sym;
+    BlockRec *blk;
+    uint32_t nsym, blk_nsym, blk_sym_start, nblk;
+    int64_t block_start, S, E;
+
+    __device__ inline bool tally(uint32_t v) {          // _tr_tally_*: returns bflush
+        sym[nsym++] = v;
+        return ++blk_nsym == (uint32_t)kSymLimit;
+    }
+    __device__ inline void flush(int64_t strstart, bool last) {   // FLUSH_BLOCK_ONLY
+        BlockRec r;
+        r.sym_start = blk_sym_start;
+        r.nsym = blk_nsym;
+        r.in_start = (uint64_t)block_start;
+        r.in_end = (uint64_t)strstart;
+        r.flags = (last ? 1u : 0u) | (block_start >= S ? 2u : 0u);
+        r.pad = 0;
+        blk[nblk++] = r;
+        block_start = strstart;
+        blk_sym_start = nsym;
+        blk_nsym = 0;
+    }
+    // fill_window (deflate.c:251-368), bookkeeping only
+    __device__ inline void fill(int64_t p, int64_t n) {
+        if (p - S >= (int64_t)(kWSize + kMaxDist)) S += kWSize;
+        if (E < n) { int64_t e = S + 2 * kWSize; E = e < n ? e : n; }
+    }
+};
+
+// ------------------------------------------------------------------------
+// k_parse_slow — deflate_slow over precomputed per-position results.
+// One wave per buffer; the wave stages tiles of results and input bytes into
+// LDS, lane 0 runs the sequential lazy-evaluation state machine.
+// ------------------------------------------------------------------------
+constexpr int kPT = 2048;
+
+__global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job) {
+    __shared__ uint32_t s_rf[kPT];
+    __shared__ uint32_t s_rq[kPT];
+    __shared__ uint8_t s_in[kPT + 4];
+    __shared__ int64_t s_next;
+    __shared__ int s_done;
+    const int lane = threadIdx.x;
+    const uint32_t bi = blockIdx.x;
+    const uint32_t g = job.first + bi;
+    const int64_t n = (int64_t)job.src_len[g];
+    const uint8_t *in = job.src + job.src_off[g];
+    const uint32_t *rf = job.rfull + job.ws_off[bi];
+    const uint32_t *rq = job.rquart + job.ws_off[bi];
+    const LevelCfg cfg = c_ct.cfg[job.level];
+    const bool use_q = cfg.good < cfg.lazy;
+
+    ParseOut po;
+    po.sym = job.sym + job.ws_off[bi];
+    po.blk = job.blocks + job.blk_off[bi];
+    po.nsym = po.blk_nsym = po.blk_sym_start = po.nblk = 0;
+    po.block_start = 0; po.S = 0; po.E = 0;
+    int64_t p = 0, match_start = 0, prev_match = 0;
+    uint32_t match_length = kMinMatch - 1, prev_length = 0;
+    bool match_available = false;
+
+    int64_t t0 = 0;
+    for (;;) {
+        for (int j = lane; j < kPT; j += 64) {
+            int64_t q = t0 + j;
+            s_rf[j] = q < n ? rf[q] : 0;
+            if (use_q) s_rq[j] = q < n ? rq[q] : 0;
+        }
+        for (int j = lane; j < kPT + 1; j += 64) {
+            int64_t q = t0 - 1 + j;
+            s_in[j] = (q >= 0 && q < n) ? in[q] : 0;
+        }
+        __syncthreads();
+        if (lane == 0) {
+            int done = 0;
+            for (;;) {
+                if (p >= t0 + kPT) break;
+                if (po.E - p < kMinLookahead) {
+                    po.fill(p, n);
+                    if (po.E == p) { done = 1; break; }
+                }
+                const int64_t lookahead = po.E - p;
+                prev_length = match_length;
+                prev_match = match_start;
+                match_length = kMinMatch - 1;
+                if (lookahead >= kMinMatch && prev_length < cfg.lazy) {
+                    const uint32_t r = (use_q && prev_length >= cfg.good) ? s_rq[p - t0] : s_rf[p - t0];
+                    const uint32_t rl = r >> 16;
+                    if (rl > prev_length) {
+                        match_length = rl;
+                        match_start = p - (int64_t)(r & 0xffffu);
+                        if (match_length == kMinMatch && p - match_start > kTooFar) match_length = kMinMatch - 1;
+                    }
+                }
+                if (prev_length >= kMinMatch && match_length <= prev_length) {
+                    const uint32_t dist = (uint32_t)(p - 1 - prev_match);
+                    const bool bflush = po.tally((dist << 8) | (prev_length - kMinMatch));
+                    p += prev_length - 1;
+                    match_available = false;
+                    match_length = kMinMatch - 1;
+                    if (bflush) po.flush(p, false);
+                } else if (match_available) {
+                    if (po.tally(s_in[p - t0])) po.flush(p, false);
+                    p++;
+                } else {
+                    match_available = true;
+                    p++;
+                }
+            }
+            if (done) {
+                if (match_available) po.tally(s_in[p - t0]);
+                po.flush(p, true);
+                job.nblocks[bi] = po.nblk;
+            }
+            s_next = p;
+            s_done = done;
+        }
+        __syncthreads();
+        if (s_done) break;
+        t0 = s_next;
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------
+// k_parse_fast — levels 1..3 (deflate_fast).  Insertion inside a match depends
+// on its length (deflate.c:1873-1897), so hash chains are maintained exactly
+// as zlib does it, sequentially: head[] (absolute positions, per buffer, in
+// global memory) and prev[] as 16-bit distances.  Lane 0 of one wave per
+// buffer; the chain walk is longest_match with prev_length == MIN_MATCH-1.
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *heads) {
+    const int lane = threadIdx.x;
+    const uint32_t bi = blockIdx.x;
+    const uint32_t g = job.first + bi;
+    const int64_t n = (int64_t)job.src_len[g];
+    const uint8_t *in = job.src + job.src_off[g];
+    uint16_t *prev = job.link + job.ws_off[bi];
+    uint32_t *head = heads + (size_t)bi * 32768;
+    const LevelCfg cfg = c_ct.cfg[job.level];
+    for (int i = lane; i < 32768; i += 64) head[i] = 0;
+    __syncthreads();
+    if (lane != 0) return;
+
+    ParseOut po;
+    po.sym = job.sym + job.ws_off[bi];
+    po.blk = job.blocks + job.blk_off[bi];
+    po.nsym = po.blk_nsym = po.blk_sym_start = po.nblk = 0;
+    po.block_start = 0; po.S = 0; po.E = 0;
+
+    auto insert = [&](int64_t q) -> int64_t {           // INSERT_STRING
+        const uint32_t h = hash3(in[q], in[q + 1], in[q + 2]);
+        const int64_t hh = head[h];
+        const int64_t d = q - hh;
+        prev[q] = (hh != 0 && d <= 32767) ? (uint16_t)d : 0;
+        head[h] = (uint32_t)q;
+        return hh;
+    };
+
+    int64_t p = 0, match_start = 0;
+    uint32_t match_length = kMinMatch - 1;
+    for (;;) {
+        if (po.E - p < kMinLookahead) {
+            po.fill(p, n);
+            if (po.E == p) break;
+        }
+        int64_t lookahead = po.E - p;
+        int64_t hh = 0;
+        if (lookahead >= kMinMatch) hh = insert(p);
+        if (hh > po.S && p - hh <= kMaxDist) {
+            // longest_match (deflate.c:1356-1497), prev_length == 2
+            uint32_t chain = cfg.chain;
+            int nice = lookahead < cfg.nice ? (int)lookahead : cfg.nice;
+            const int64_t limit = (p - po.S) > kMaxDist ? p - kMaxDist : po.S;
+            const int64_t rem = n - p;
+            const int maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
+            int best = kMinMatch - 1;
+            const uint8_t *scan = in + p;
+            int64_t cur = hh;
+            for (;;) {
+                const uint8_t *m = in + cur;
+                if (m[best] == scan[best] && m[best - 1] == scan[best - 1] && m[0] == scan[0] && m[1] == scan[1]) {
+                    int k = 2;
+                    while (k < maxcmp && m[k] == scan[k]) k++;
+                    if (k > best) {
+                        match_start = cur;
+                        best = k;
+                        if (k >= nice) break;
+                    }
+                }
+                const uint32_t d = prev[cur];
+                if (d == 0) break;
+                cur -= d;
+                if (cur <= limit || --chain == 0) break;
+            }
+            match_length = (int64_t)best <= lookahead ? (uint32_t)best : (uint32_t)lookahead;
+        }
+        bool bflush;
+        if (match_length >= kMinMatch) {
+            bflush = po.tally(((uint32_t)(p - match_start) << 8) | (match_length - kMinMatch));
+            lookahead -= match_length;
+            if (match_length <= cfg.lazy && lookahead >= kMinMatch) {
+                for (uint32_t k = 1; k < match_length; k++) insert(p + k);
+            }
+            p += match_length;
+            match_length = 0;
+        } else {
+            bflush = po.tally(in[p]);
+            p++;
+        }
+        if (bflush) po.flush(p, false);
+    }
+    po.flush(p, true);
+    job.nblocks[bi] = po.nblk;
+}
+
+// ------------------------------------------------------------------------
+// k_encode — one 256-thread workgroup per buffer.
+// ------------------------------------------------------------------------
+constexpr int kEncThreads = 256;
+constexpr int kStgWords = 4096;                 // 16 KiB output staging window
+constexpr int kStgBits = kStgWords * 32;
+
+struct TreeLDS {
+    uint16_t lfreq[kHeapSize], ldad[kHeapSize], lcode[kHeapSize];
+    uint8_t llen[kHeapSize + 1];
+    uint16_t dfreq[2 * kDCodes + 1], ddad[2 * kDCodes + 1], dcode[2 * kDCodes + 1];
+    uint8_t dlen[2 * kDCodes + 2];
+    uint16_t bfreq[2 * kBLCodes + 1], bdad[2 * kBLCodes + 1], bcode[2 * kBLCodes + 1];
+    uint8_t blen[2 * kBLCodes + 2];
+    int heap[kHeapSize + 1];
+    uint8_t depth[kHeapSize];
+    uint16_t bl_count[kMaxBits + 1];
+    int heap_len, heap_max;
+    int64_t opt_len, static_len;
+};
+
+struct TreeRef {
+    uint16_t *freq, *dad, *code;
+    uint8_t *len;
+    int max_code;
+};
+
+__device__ inline bool t_smaller(const TreeRef &t, const TreeLDS &h, int n, int m) {
+    return t.freq[n] < t.freq[m] || (t.freq[n] == t.freq[m] && h.depth[n] <= h.depth[m]);
+}
+
+__device__ void t_downheap(const TreeRef &t, TreeLDS &h, int k) {        // pqdownheap
+    int v = h.heap[k];
+    int j = k << 1;
+    while (j <= h.heap_len) {
+        if (j < h.heap_len && t_smaller(t, h, h.heap[j + 1], h.heap[j])) j++;
+        if (t_smaller(t, h, v, h.heap[j])) break;
+        h.heap[k] = h.heap[j];
+        k = j;
+        j <<= 1;
+    }
+    h.heap[k] = v;
+}
+
+__device__ void t_gen_codes(TreeRef &t, const uint16_t *bl_count) {       // gen_codes
+    uint16_t next[kMaxBits + 1];
+    uint32_t c = 0;
+    for (int b = 1; b <= kMaxBits; b++) { c = (c + bl_count[b - 1]) << 1; next[b] = (uint16_t)c; }
+    for (int n = 0; n <= t.max_code; n++) {
+        int len = t.len[n];
+        if (!len) continue;
+        uint32_t code = next[len]++, r = 0;
+        for (int i = 0; i < len; i++) { r = (r << 1) | (code & 1u); code >>= 1; }
+        t.code[n] = (uint16_t)r;
+    }
+}
+
+// build_tree + gen_bitlen (trees.c:540-706); slen == nullptr for the bl tree
+__device__ void t_build(TreeRef &t, TreeLDS &h, int elems, const uint8_t *slen,
+                        const uint8_t *extra, int xbase, int max_length) {
+    int max_code = -1;
+    h.heap_len = 0;
+    h.heap_max = kHeapSize;
+    for (int n = 0; n < elems; n++) {
+        if (t.freq[n] != 0) { h.heap[++h.heap_len] = max_code = n; h.depth[n] = 0; }
+        else t.len[n] = 0;
+    }
+    while (h.heap_len < 2) {
+        int node = h.heap[++h.heap_len] = (max_code < 2 ? ++max_code : 0);
+        t.freq[node] = 1;
+        h.depth[node] = 0;
+        h.opt_len--;
+        if (slen) h.static_len -= slen[node];
+    }
+    t.max_code = max_code;
+    for (int n = h.heap_len / 2; n >= 1; n--) t_downheap(t, h, n);
+    int node = elems;
+    do {
+        int n = h.heap[1];
+        h.heap[1] = h.heap[h.heap_len--];
+        t_downheap(t, h, 1);
+        int m = h.heap[1];
+        h.heap[--h.heap_max] = n;
+        h.heap[--h.heap_max] = m;
+        t.freq[node] = (uint16_t)(t.freq[n] + t.freq[m]);
+        h.depth[node] = (uint8_t)((h.depth[n] >= h.depth[m] ? h.depth[n] : h.depth[m]) + 1);
+        t.dad[n] = t.dad[m] = (uint16_t)node;
+        h.heap[1] = node++;
+        t_downheap(t, h, 1);
+    } while (h.heap_len >= 2);
+    h.heap[--h.heap_max] = h.heap[1];
+
+    // gen_bitlen
+    int overflow = 0;
+    for (int b = 0; b <= kMaxBits; b++) h.bl_count[b] = 0;
+    t.len[h.heap[h.heap_max]] = 0;
+    int hh;
+    for (hh = h.heap_max + 1; hh < kHeapSize; hh++) {
+        int n = h.heap[hh];
+        int bits = t.len[t.dad[n]] + 1;
+        if (bits > max_length) { bits = max_length; overflow++; }
+        t.len[n] = (uint8_t)bits;
+        if (n > t.max_code) continue;
+        h.bl_count[bits]++;
+        int xb = n >= xbase ? extra[n - xbase] : 0;
+        h.opt_len += (int64_t)t.freq[n] * (bits + xb);
+        if (slen) h.static_len += (int64_t)t.freq[n] * (slen[n] + xb);
+    }
+    if (overflow != 0) {
+        do {
+            int bits = max_length - 1;
+            while (h.bl_count[bits] == 0) bits--;
+            h.bl_count[bits]--;
+            h.bl_count[bits + 1] += 2;
+            h.bl_count[max_length]--;
+            overflow -= 2;
+        } while (overflow > 0);
+        hh = kHeapSize;
+        for (int bits = max_length; bits != 0; bits--) {
+            int n = h.bl_count[bits];
+            while (n != 0) {
+                int m = h.heap[--hh];
+                if (m > t.max_code) continue;
+                if (t.len[m] != bits) {
+                    h.opt_len += ((int64_t)bits - t.len[m]) * t.freq[m];
+                    t.len[m] = (uint8_t)bits;
+                }
+                n--;
+            }
+        }
+    }
+    t_gen_codes(t, h.bl_count);
+}
+
+// code-length RLE walk of scan_tree/send_tree (trees.c:712-794)
+template <typename Sink>
+__device__ void t_rle(const uint8_t *len, int max_code, Sink sink) {
+    int prevlen = -1, curlen, nextlen = len[0], count = 0;
+    int max_count = 7, min_count = 4;
+    if (nextlen == 0) { max_count = 138; min_count = 3; }
+    for (int n = 0; n <= max_code; n++) {
+        curlen = nextlen;
+        nextlen = n + 1 <= max_code ? len[n + 1] : 0xffff;
+        if (++count < max_count && curlen == nextlen) continue;
+        if (count < min_count) {
+            while (count--) sink(curlen, 0, 0);
+        } else if (curlen != 0) {
+            if (curlen != prevlen) { sink(curlen, 0, 0); count--; }
+            sink(16, count - 3, 2);
+        } else if (count <= 10) {
+            sink(17, count - 3, 3);
+        } else {
+            sink(18, count - 11, 7);
+        }
+        count = 0;
+        prevlen = curlen;
+        if (nextlen == 0) { max_count = 138; min_count = 3; }
+        else if (curlen == nextlen) { max_count = 6; min_count = 3; }
+        else { max_count = 7; min_count = 4; }
+    }
+}
+
+// Output bit stream, staged in LDS: stg[] holds output bits
+// [sbase, sbase + kStgBits); everything below sbase is in global memory.
+struct Stage {
+    uint32_t *stg;
+    uint8_t *out;          // buffer's output
+    uint64_t cap;          // bytes writable
+    int64_t sbase;         // bit offset of stg[0] (multiple of 32)
+};
+
+__device__ inline void stg_or(uint32_t *stg, int64_t rel, uint64_t v) {  // v < 2^49
+    const int w = (int)(rel >> 5), sh = (int)(rel & 31);
+    const uint32_t lo = (uint32_t)(v << sh);
+    const uint32_t mid = sh ? (uint32_t)(v >> (32 - sh)) : (uint32_t)(v >> 32);
+    const uint32_t hi = sh > 16 ? (uint32_t)(v >> (64 - sh)) : 0u;
+    if (lo) atomicOr(&stg[w], lo);
+    if (mid) atomicOr(&stg[w + 1], mid);
+    if (hi) atomicOr(&stg[w + 2], hi);
+}
+
+// write completed words below bit `upto` to global, keep the partial word
+__device__ void stg_flush(Stage &st, int64_t upto, bool final_flush) {
+    const int tid = threadIdx.x;
+    const int64_t rel = upto - st.sbase;
+    const int full = (int)(rel >> 5);
+    const int nwords = final_flush ? (int)((rel + 31) >> 5) : full;
+    const uint64_t byte0 = (uint64_t)st.sbase >> 3;
+    const uint64_t endbyte = final_flush ? (uint64_t)((upto + 7) >> 3) : byte0 + 4ull * (uint64_t)full;
+    for (int w = tid; w < nwords; w += kEncThreads) {
+        const uint32_t v = st.stg[w];
+        const uint64_t b = byte0 + 4ull * w;
+        uint8_t *o = st.out + b;
+        if (((reinterpret_cast<uintptr_t>(o) & 3) == 0) && b + 4 <= endbyte && b + 4 <= st.cap) {
+            *reinterpret_cast<uint32_t *>(o) = v;
+        } else {
+            for (int k = 0; k < 4; k++)
+                if (b + k < endbyte && b + k < st.cap) o[k] = (uint8_t)(v >> (8 * k));
+        }
+    }
+    __syncthreads();
+    if (!final_flush) {
+        const uint32_t keep = st.stg[full];
+        __syncthreads();
+        for (int w = tid; w < kStgWords; w += kEncThreads) st.stg[w] = 0;
+        __syncthreads();
+        if (tid == 0) st.stg[0] = keep;
+        st.sbase += 32ll * full;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
+    __shared__ uint32_t stg[kStgWords];
+    __shared__ TreeLDS T;
+    __shared__ uint32_t hl[kLCodes], hd[kDCodes];
+    __shared__ uint32_t wsum[kEncThreads / 64];
+    __shared__ int64_t s_obit;
+    __shared__ int s_type, s_maxbl;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t bi = blockIdx.x;
+    const uint32_t g = job.first + bi;
+    const int64_t n = (int64_t)job.src_len[g];
+    const uint8_t *in = job.src + job.src_off[g];
+    const uint32_t *sym = job.sym + job.ws_off[bi];
+    const BlockRec *blk = job.blocks + job.blk_off[bi];
+    const int level = job.level;
+
+    Stage st;
+    st.stg = stg;
+    st.out = job.dst + job.dst_off[g];
+    st.cap = job.dst_cap[g];
+    st.sbase = 0;
+    for (int w = tid; w < kStgWords; w += kEncThreads) stg[w] = 0;
+    __syncthreads();
+
+    // single-lane bit writer into the staging window
+    auto put = [&](uint64_t v, int nb) {      // caller ensures room
+        stg_or(stg, s_obit - st.sbase, v);
+        s_obit += nb;
+    };
+
+    if (tid == 0) {
+        s_obit = 0;
+        if (job.wrap == 1) {                    // zlib header (deflate.c:1004-1037)
+            uint32_t header = (8u + ((15u - 8u) << 4)) << 8;
+            uint32_t flags = level < 2 ? 0u : level < 6 ? 1u : level == 6 ? 2u : 3u;
+            header |= flags << 6;
+            header += 31 - (header % 31);
+            put(header >> 8, 8);
+            put(header & 0xffu, 8);
+        } else if (job.wrap == 2) {             // gzip header (deflate.c:1060-1073)
+            const uint32_t xfl = level == 9 ? 2u : level < 2 ? 4u : 0u;
+            put(31, 8); put(139, 8); put(8, 8); put(0, 8);
+            put(0, 32);
+            put(xfl, 8); put(3, 8);             // OS_CODE (zutil.h:184)
+        }
+    }
+    __syncthreads();
+
+    if (level == 0) {
+        // deflate_stored (deflate.c:1635-1815) with a compressBound()-sized
+        // output: MAX_STORED-byte stored blocks, last one final.
+        int64_t done = 0;
+        do {
+            const int64_t left = n - done;
+            const int64_t len = left < 65535 ? left : 65535;
+            const bool last = len == left;
+            if (s_obit - st.sbase + 128 > kStgBits) stg_flush(st, s_obit, false);
+            if (tid == 0) {
+                put(last ? 1u : 0u, 3);
+                s_obit = (s_obit + 7) & ~7ll;
+                put((uint32_t)len & 0xffffu, 16);
+                put((~(uint32_t)len) & 0xffffu, 16);
+            }
+            __syncthreads();
+            int64_t copied = 0;
+            while (copied < len) {
+                const int64_t room = (st.sbase + kStgBits - 64 - s_obit) >> 3;
+                const int64_t take = (len - copied) < room ? (len - copied) : room;
+                const int64_t ob = s_obit - st.sbase;
+                for (int64_t k = tid; k < take; k += kEncThreads)
+                    stg_or(stg, ob + 8 * k, in[done + copied + k]);
+                __syncthreads();
+                if (tid == 0) s_obit += 8 * take;
+                __syncthreads();
+                copied += take;
+                stg_flush(st, s_obit, false);
+            }
+            done += len;
+            if (last) break;
+        } while (true);
+    } else {
+        const uint32_t nblk = job.nblocks[bi];
+        for (uint32_t k = 0; k < nblk; k++) {
+            const BlockRec br = blk[k];
+            const bool last = br.flags & 1u;
+            // --- histogram (_tr_tally freq updates, deflate.h:354-372) ---
+            for (int i = tid; i < kLCodes; i += kEncThreads) hl[i] = 0;
+            for (int i = tid; i < kDCodes; i += kEncThreads) hd[i] = 0;
+            __syncthreads();
+            for (uint32_t i = tid; i < br.nsym; i += kEncThreads) {
+                const uint32_t v = sym[br.sym_start + i];
+                const uint32_t dist = v >> 8, lc = v & 0xffu;
+                if (dist == 0) atomicAdd(&hl[lc], 1u);
+                else {
+                    atomicAdd(&hl[c_ct.len_code[lc] + 257], 1u);
+                    const uint32_t d = dist - 1;
+                    atomicAdd(&hd[d < 256 ? c_ct.dist_code[d] : c_ct.dist_code[256 + (d >> 7)]], 1u);
+                }
+            }
+            __syncthreads();
+            // room for the largest block header (dynamic trees: < 5000 bits)
+            if (s_obit - st.sbase + 6144 > kStgBits) stg_flush(st, s_obit, false);
+            // --- trees and block type (single lane) ---
+            if (tid == 0) {
+                for (int i = 0; i < kLCodes; i++) T.lfreq[i] = (uint16_t)hl[i];
+                T.lfreq[kEndBlock] = 1;
+                for (int i = 0; i < kDCodes; i++) T.dfreq[i] = (uint16_t)hd[i];
+                for (int i = 0; i < kBLCodes; i++) T.bfreq[i] = 0;
+                T.opt_len = T.static_len = 0;
+                TreeRef lt{T.lfreq, T.ldad, T.lcode, T.llen, 0};
+                TreeRef dt{T.dfreq, T.ddad, T.dcode, T.dlen, 0};
+                TreeRef bt{T.bfreq, T.bdad, T.bcode, T.blen, 0};
+                t_build(lt, T, kLCodes, c_ct.stat_llen, c_ct.xlbits, 257, kMaxBits);
+                uint8_t sdl[kDCodes];
+                for (int i = 0; i < kDCodes; i++) sdl[i] = 5;
+                t_build(dt, T, kDCodes, sdl, c_ct.xdbits, 0, kMaxBits);
+                auto cnt = [&](int s, int, int) { T.bfreq[s]++; };
+                t_rle(T.llen, lt.max_code, cnt);
+                t_rle(T.dlen, dt.max_code, cnt);
+                t_build(bt, T, kBLCodes, nullptr, c_ct.xblbits, 0, kMaxBLBits);
+                int max_blindex;
+                for (max_blindex = kBLCodes - 1; max_blindex >= 3; max_blindex--)
+                    if (T.blen[c_ct.bl_order[max_blindex]] != 0) break;
+                T.opt_len += 3 * ((int64_t)max_blindex + 1) + 5 + 5 + 4;
+                uint64_t opt_lenb = ((uint64_t)T.opt_len + 3 + 7) >> 3;
+                const uint64_t static_lenb = ((uint64_t)T.static_len + 3 + 7) >> 3;
+                if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+                const uint64_t stored_len = br.in_end - br.in_start;
+                int type;
+                if (stored_len + 4 <= opt_lenb && (br.flags & 2u)) type = 0;
+                else if (static_lenb == opt_lenb) type = 1;
+                else type = 2;
+                s_type = type;
+                s_maxbl = max_blindex;
+                // block header
+                put((uint32_t)(type << 1) + (last ? 1u : 0u), 3);
+                if (type == 0) {
+                    s_obit = (s_obit + 7) & ~7ll;
+                    put((uint32_t)stored_len & 0xffffu, 16);
+                    put((~(uint32_t)stored_len) & 0xffffu, 16);
+                } else if (type == 2) {
+                    const int lcodes = lt.max_code + 1, dcodes = dt.max_code + 1;
+                    put((uint32_t)(lcodes - 257), 5);
+                    put((uint32_t)(dcodes - 1), 5);
+                    put((uint32_t)(max_blindex + 1 - 4), 4);
+                    for (int r = 0; r <= max_blindex; r++) put(T.blen[c_ct.bl_order[r]], 3);
+                    auto snd = [&](int s, int xv, int xb) {
+                        put(T.bcode[s], T.blen[s]);
+                        if (xb) put((uint32_t)xv, xb);
+                    };
+                    t_rle(T.llen, lcodes - 1, snd);
+                    t_rle(T.dlen, dcodes - 1, snd);
+                }
+            }
+            __syncthreads();
+            const int type = s_type;
+            if (type == 0) {
+                // stored: raw bytes (byte aligned)
+                const int64_t len = (int64_t)(br.in_end - br.in_start);
+                int64_t copied = 0;
+                while (copied < len) {
+                    stg_flush(st, s_obit, false);
+                    const int64_t room = (st.sbase + kStgBits - 64 - s_obit) >> 3;
+                    const int64_t take = (len - copied) < room ? (len - copied) : room;
+                    const int64_t ob = s_obit - st.sbase;
+                    for (int64_t i = tid; i < take; i += kEncThreads)
+                        stg_or(stg, ob + 8 * i, in[br.in_start + copied + i]);
+                    __syncthreads();
+                    if (tid == 0) s_obit += 8 * take;
+                    __syncthreads();
+                    copied += take;
+                }
+            } else {
+                const uint16_t *lcode = type == 1 ? c_ct.stat_lcode : T.lcode;
+                const uint8_t *llen = type == 1 ? c_ct.stat_llen : T.llen;
+                for (uint32_t base = 0; base < br.nsym + 1; base += kEncThreads) {
+                    // +1: the END_BLOCK code rides in the last batch
+                    const uint32_t i = base + tid;
+                    uint64_t v = 0;
+                    int nb = 0;
+                    if (i < br.nsym) {
+                        const uint32_t s = sym[br.sym_start + i];
+                        const uint32_t dist = s >> 8, lc = s & 0xffu;
+                        if (dist == 0) {
+                            v = lcode[lc]; nb = llen[lc];
+                        } else {
+                            const uint32_t code = c_ct.len_code[lc];
+                            v = lcode[code + 257]; nb = llen[code + 257];
+                            const int xl = c_ct.xlbits[code];
+                            if (xl) { v |= (uint64_t)(lc - c_ct.len_base[code]) << nb; nb += xl; }
+                            const uint32_t d = dist - 1;
+                            const uint32_t dc = d < 256 ? c_ct.dist_code[d] : c_ct.dist_code[256 + (d >> 7)];
+                            const uint32_t dcv = type == 1 ? c_ct.stat_dcode[dc] : T.dcode[dc];
+                            const int dl = type == 1 ? 5 : T.dlen[dc];
+                            v |= (uint64_t)dcv << nb; nb += dl;
+                            const int xd = c_ct.xdbits[dc];
+                            if (xd) { v |= (uint64_t)(d - c_ct.dist_base[dc]) << nb; nb += xd; }
+                        }
+                    } else if (i == br.nsym) {
+                        v = lcode[kEndBlock]; nb = llen[kEndBlock];
+                    }
+                    // block-wide exclusive scan of nb
+                    int incl = nb;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) {
+                        int t = __shfl_up(incl, o, 64);
+                        if (lane >= o) incl += t;
+                    }
+                    if (lane == 63) wsum[wave] = (uint32_t)incl;
+                    __syncthreads();
+                    int wpre = 0, total = 0;
+                    for (int w = 0; w < kEncThreads / 64; w++) {
+                        if (w < wave) wpre += (int)wsum[w];
+                        total += (int)wsum[w];
+                    }
+                    const int excl = wpre + incl - nb;
+                    if (s_obit - st.sbase + total + 64 > kStgBits) stg_flush(st, s_obit, false);
+                    if (nb) stg_or(stg, s_obit - st.sbase + excl, v);
+                    __syncthreads();
+                    if (tid == 0) s_obit += total;
+                    __syncthreads();
+                }
+            }
+            if (last && tid == 0) s_obit = (s_obit + 7) & ~7ll;   // bi_windup
+            __syncthreads();
+        }
+    }
+    // trailer
+    __syncthreads();
+    if (s_obit - st.sbase + 96 > kStgBits) stg_flush(st, s_obit, false);
+    if (tid == 0) {
+        const uint32_t ck = job.check[bi];
+        if (job.wrap == 1) {                    // Adler-32, big-endian (deflate.c:1253-1256)
+            put(ck >> 24, 8); put((ck >> 16) & 0xffu, 8); put((ck >> 8) & 0xffu, 8); put(ck & 0xffu, 8);
+        } else if (job.wrap == 2) {             // CRC-32 + ISIZE, little-endian
+            put(ck, 32);
+            put((uint32_t)n, 32);
+        }
+    }
+    __syncthreads();
+    stg_flush(st, s_obit, true);
+    if (tid == 0) {
+        const uint64_t total = (uint64_t)(s_obit >> 3);
+        job.dst_len[g] = total <= st.cap ? total : st.cap;
+        job.status[g] = total <= st.cap ? 0 : -5;
+    }
+}
+
+// ------------------------------------------------------------------------
+// host-side launch
+// ------------------------------------------------------------------------
+int launch_tables_upload(const CodeTables *ct, const CrcTables *) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(c_ct), ct, sizeof(CodeTables));
+}
+
+int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipStream_t st) {
+    const dim3 grid(job.count);
+    switch (stage) {
+    case 0: hipLaunchKernelGGL(k_links, grid, dim3(64), 0, st, job); break;
+    case 1: hipLaunchKernelGGL(k_match, grid, dim3(kMatchThreads), 0, st, job,
+                               (int)(job.level >= 5)); break;
+    case 2: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job); break;
+    case 3: hipLaunchKernelGGL(k_parse_fast, grid, dim3(64), 0, st, job, heads); break;
+    case 4: hipLaunchKernelGGL(k_encode, grid, dim3(kEncThreads), 0, st, job); break;
+    default: return -1;
+    }
+    return (int)hipGetLastError();
+}
+
+}  // namespace zgpu

@@ -1,0 +1,108 @@
+// zgpu_internal.h — constants, tables and launch entry points shared by the
+// HIP translation units of libzgpu.so.  gfx950 only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+namespace zgpu {
+
+// ---- deflate constants (zutil.h:77-89, deflate.h:33-55,293-303) ----
+constexpr int kWSize = 32768;
+constexpr int kMinMatch = 3;
+constexpr int kMaxMatch = 258;
+constexpr int kMinLookahead = kMaxMatch + kMinMatch + 1;   // 262
+constexpr int kMaxDist = kWSize - kMinLookahead;            // 32506
+constexpr int kTooFar = 4096;                               // deflate.c:88-90
+constexpr int kSymLimit = 16383;                            // lit_bufsize - 1
+constexpr int kLCodes = 286, kDCodes = 30, kBLCodes = 19;
+constexpr int kHeapSize = 2 * kLCodes + 1;                  // 573
+constexpr int kMaxBits = 15, kMaxBLBits = 7;
+constexpr int kEndBlock = 256;
+
+// configuration_table (deflate.c:112-125)
+struct LevelCfg { uint16_t good, lazy, nice, chain; };
+
+// Static code tables (RFC 1951 §3.2.5-3.2.6), derived on the host at init the
+// way tr_static_init (trees.c:303-396) derives them, copied to __constant__.
+struct CodeTables {
+    uint8_t  len_code[256];     // normalized match length -> length code 0..28
+    uint8_t  dist_code[512];    // d<256: [d]; else [256 + (d>>7)]
+    uint16_t len_base[29];
+    uint16_t dist_base[30];
+    uint8_t  xlbits[29];
+    uint8_t  xdbits[30];
+    uint8_t  xblbits[19];
+    uint8_t  bl_order[19];
+    uint16_t stat_lcode[288];
+    uint8_t  stat_llen[288];
+    uint16_t stat_dcode[30];
+    LevelCfg cfg[10];
+};
+
+// CRC-32 tables (reflected poly 0xedb88320, crc32.c), built on the host:
+//   nib[j][v]  raw CRC (zero init, no final xor) of a 16-byte chunk whose
+//              nibble j (byte j/2, low nibble first) is v, all else zero;
+//   shift[k][j][v] advance-by-zero-bytes operators as 8 nibble tables:
+//              k = 0..5 -> 16<<k bytes, k = 6 -> 1024 bytes,
+//              k = 7 -> kCrcSegment bytes (segment Horner);
+//   byte[v]    the classic byte table (tiny-buffer path).
+constexpr int kCrcShiftTabs = 8;
+struct CrcTables {
+    uint32_t nib[32][16];
+    uint32_t shift[kCrcShiftTabs][8][16];
+    uint32_t byte[256];
+};
+constexpr uint64_t kCrcSegment = 64 * 1024;   // bytes per checksum work item
+
+// Per-buffer deflate block record written by the parse, read by the encoder.
+struct BlockRec {
+    uint32_t sym_start;   // index of first symbol (relative to buffer's sym base)
+    uint32_t nsym;
+    uint64_t in_start;    // block_start (absolute input position)
+    uint64_t in_end;      // strstart at flush
+    uint32_t flags;       // bit0 last, bit1 stored-eligible (block_start still in window)
+    uint32_t pad;
+};
+
+// Per-buffer workspace layout for one deflate sub-batch (device arrays).
+struct DeflateJob {
+    const uint8_t *src;      // batch input base
+    const uint64_t *src_off;
+    const uint64_t *src_len;
+    uint8_t *dst;
+    const uint64_t *dst_off;
+    const uint64_t *dst_cap;
+    uint64_t *dst_len;
+    int32_t *status;
+    uint32_t first;          // first buffer index of this sub-batch
+    uint32_t count;          // buffers in this sub-batch
+    int level, wrap;
+    // workspace, indexed by position relative to ws_off[i]
+    const uint64_t *ws_off;  // per sub-batch buffer: start in the position-indexed arrays
+    const uint64_t *blk_off; // per sub-batch buffer: start in the block array
+    uint16_t *link;          // [Σn]
+    uint32_t *rfull;         // [Σn]
+    uint32_t *rquart;        // [Σn] (levels 5..9)
+    uint32_t *sym;           // [Σn]
+    BlockRec *blocks;        // [Σ(n/16383 + 2)]
+    uint32_t *nblocks;       // [count]
+    uint32_t *check;         // [count] adler32 / crc32 of the input (trailer)
+};
+
+// launchers (return hipError_t as int)
+int launch_tables_upload(const CodeTables *ct, const CrcTables *crc);
+const CrcTables *device_crc_tables();
+int launch_crc32(const uint8_t *src, const uint64_t *off, const uint64_t *len,
+                 const uint32_t *init, uint32_t *out, uint32_t count,
+                 void *scratch, size_t scratch_bytes, hipStream_t st);
+int launch_adler32(const uint8_t *src, const uint64_t *off, const uint64_t *len,
+                   const uint32_t *init, uint32_t *out, uint32_t count,
+                   void *scratch, size_t scratch_bytes, hipStream_t st);
+size_t checksum_scratch_bytes(uint32_t count);
+// stage: 0 links, 1 match, 2 lazy parse, 3 greedy parse (heads: 128 KiB/buffer), 4 encode
+int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipStream_t st);
+int launch_generate(uint8_t *dst, uint64_t len, uint32_t count, int kind, uint64_t seed,
+                    uint64_t first_index, hipStream_t st);
+
+}  // namespace zgpu

@@ -1,0 +1,267 @@
+"""Python mirror of the reference's front-end over libzgpu.so.
+
+The reference's host API is the TypeScript ``Zlib`` class (src/lib/index.ts:88-271)
+sitting on the WASM exports of src/wasm_module.c.  Here the same surface sits on
+the C ABI of libzgpu.so (include/zgpu.h): ``Zlib.compress`` returns the same
+result record (data, originalSize, compressedSize, compressionRatio,
+processingTime, plus ``gpuAccelerated`` in place of ``simdAccelerated``) and
+raises ``ZlibCompressionError`` on failure; ``crc32``/``adler32`` take
+``(data, init)`` — the reference's TS wrappers pass (ptr, len) to a
+(crc, buf, len) export (SURVEY §0 finding 3), which is not reproduced.
+
+Batched and device-resident entry points (``compress_batch``,
+``deflate_batch_dev``, ``crc32_batch_dev``, ...) are the new extension.
+
+torch is imported before the library is loaded so that libzgpu.so binds to the
+same HIP runtime (libamdhip64.so.7) torch uses; device buffers are torch tensors.
+"""
+import ctypes as C
+import os
+import time
+from dataclasses import dataclass
+
+try:  # share torch's HIP runtime (must precede loading libzgpu.so)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is part of the image
+    torch = None
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libzgpu.so")
+
+Z_OK, Z_STREAM_END, Z_STREAM_ERROR, Z_MEM_ERROR, Z_BUF_ERROR = 0, 1, -2, -4, -5
+ZGPU_ENODEV = -100
+WRAP_RAW, WRAP_ZLIB, WRAP_GZIP = 0, 1, 2
+KIND_RANDOM, KIND_SILESIA, KIND_ENWIK, KIND_SMALLVOCAB = 0, 1, 2, 3
+
+EXPORTED_SYMBOLS = (
+    # include/zgpu.h
+    "zgpu_init", "zgpu_info", "zgpu_set_inflight_bytes", "zgpu_deflate_batch_dev",
+    "zgpu_crc32_batch_dev", "zgpu_adler32_batch_dev", "zgpu_compress_batch",
+    "zgpu_crc32_batch", "zgpu_adler32_batch", "zgpu_generate_dev",
+    # include/zgpu_zlib.h
+    "zlibVersion", "compress", "compress2", "compressBound", "deflateInit_",
+    "deflateInit2_", "deflate", "deflateEnd", "deflateBound", "crc32", "crc32_z",
+    "crc32_combine", "crc32_combine64", "crc32_combine_gen", "crc32_combine_gen64",
+    "crc32_combine_op", "adler32", "adler32_z", "adler32_combine", "adler32_combine64",
+    # include/zgpu_wasm.h
+    "zlib_compress_buffer", "zlib_crc32", "zlib_adler32", "zlib_compress_bound",
+    "zlib_get_version", "zlib_compress_simd", "zlib_compress_simd_full",
+    "zlib_compress_simd_buffer", "zlib_crc32_simd_optimized", "zlib_crc32_simd_enhanced",
+    "zlib_adler32_simd",
+)
+
+
+class ZlibError(Exception):
+    pass
+
+
+class ZlibCompressionError(ZlibError):
+    pass
+
+
+def compress_bound(n):
+    """compressBound (compress.c:72-75)."""
+    return n + (n >> 12) + (n >> 14) + (n >> 25) + 13
+
+
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load libzgpu.so (raises if it was not built: no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ZlibError(f"{path} missing: run __graft_entry__.build() (no CPU fallback exists)")
+    L = C.CDLL(path)
+    P, U64, U32, I32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
+    L.zgpu_init.restype = I32
+    L.zgpu_info.restype = C.c_char_p
+    L.zgpu_set_inflight_bytes.restype = C.c_size_t
+    L.zgpu_set_inflight_bytes.argtypes = [C.c_size_t]
+    L.zgpu_deflate_batch_dev.restype = I32
+    L.zgpu_deflate_batch_dev.argtypes = [P, P, P, P, P, P, P, P, U32, I32, I32, P]
+    for f in ("zgpu_crc32_batch_dev", "zgpu_adler32_batch_dev"):
+        getattr(L, f).restype = I32
+        getattr(L, f).argtypes = [P, P, P, P, P, U32, P]
+    L.zgpu_compress_batch.restype = I32
+    L.zgpu_compress_batch.argtypes = [P, P, P, P, P, C.c_size_t, I32, I32]
+    for f in ("zgpu_crc32_batch", "zgpu_adler32_batch"):
+        getattr(L, f).restype = I32
+        getattr(L, f).argtypes = [P, P, P, P, C.c_size_t]
+    L.zgpu_generate_dev.restype = I32
+    L.zgpu_generate_dev.argtypes = [P, U64, U32, I32, U64, U64, P]
+    L.compress2.restype = I32
+    L.compress2.argtypes = [P, C.POINTER(C.c_ulong), P, C.c_ulong, I32]
+    L.compressBound.restype = C.c_ulong
+    L.compressBound.argtypes = [C.c_ulong]
+    for f in ("crc32_z", "adler32_z"):
+        getattr(L, f).restype = C.c_ulong
+        getattr(L, f).argtypes = [C.c_ulong, P, C.c_size_t]
+    for f in ("crc32_combine64", "adler32_combine64"):
+        getattr(L, f).restype = C.c_ulong
+        getattr(L, f).argtypes = [C.c_ulong, C.c_ulong, C.c_int64]
+    L.zlibVersion.restype = C.c_char_p
+    L.zlib_compress_simd.restype = I32
+    L.zlib_compress_simd.argtypes = [P, C.c_size_t, P, C.POINTER(C.c_size_t), I32]
+    _lib = L
+    return L
+
+
+def _ptr_array(bufs):
+    arr = (C.c_void_p * len(bufs))()
+    keep = []
+    for i, b in enumerate(bufs):
+        cb = C.create_string_buffer(bytes(b), max(len(b), 1))
+        keep.append(cb)
+        arr[i] = C.addressof(cb)
+    return arr, keep
+
+
+def compress_batch(bufs, level=6, wrap=WRAP_ZLIB, caps=None):
+    """Compress independent host buffers on the GPU; returns [(status, bytes)]."""
+    L = load()
+    n = len(bufs)
+    src, keep = _ptr_array(bufs)
+    lens = (C.c_size_t * n)(*[len(b) for b in bufs])
+    caps = caps or [compress_bound(len(b)) for b in bufs]
+    outs = [C.create_string_buffer(max(c, 1)) for c in caps]
+    dst = (C.c_void_p * n)(*[C.addressof(o) for o in outs])
+    dlen = (C.c_size_t * n)(*caps)
+    st = (C.c_int * n)()
+    rc = L.zgpu_compress_batch(src, lens, dst, dlen, st, n, level, wrap)
+    if rc:
+        raise ZlibCompressionError(f"zgpu_compress_batch failed: {rc}")
+    del keep
+    return [(st[i], outs[i].raw[: dlen[i]]) for i in range(n)]
+
+
+def _checksum_batch(fn, bufs, inits):
+    L = load()
+    n = len(bufs)
+    src, keep = _ptr_array(bufs)
+    lens = (C.c_size_t * n)(*[len(b) for b in bufs])
+    init = (C.c_uint32 * n)(*inits) if inits is not None else None
+    out = (C.c_uint32 * n)()
+    rc = getattr(L, fn)(src, lens, init, out, n)
+    if rc:
+        raise ZlibError(f"{fn} failed: {rc}")
+    del keep
+    return list(out)
+
+
+def crc32_batch(bufs, inits=None):
+    return _checksum_batch("zgpu_crc32_batch", bufs, inits)
+
+
+def adler32_batch(bufs, inits=None):
+    return _checksum_batch("zgpu_adler32_batch", bufs, inits)
+
+
+def compress2(data, level=6, cap=None):
+    """zlib compress2() through the drop-in symbol; returns (rc, bytes)."""
+    L = load()
+    data = bytes(data)
+    cap = compress_bound(len(data)) if cap is None else cap
+    out = C.create_string_buffer(max(cap, 1))
+    n = C.c_ulong(cap)
+    rc = L.compress2(out, C.byref(n), data, len(data), level)
+    return rc, out.raw[: n.value]
+
+
+def crc32(data, crc=0):
+    data = bytes(data)
+    return load().crc32_z(crc, data, len(data))
+
+
+def adler32(data, adler=1):
+    data = bytes(data)
+    return load().adler32_z(adler, data, len(data))
+
+
+# ---------------- device-resident (torch tensors as HBM buffers) ----------------
+
+def _dp(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(stream):
+    if stream is None:
+        return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    return C.c_void_p(stream)
+
+
+def deflate_batch_dev(src, src_off, src_len, dst, dst_off, dst_cap, dst_len, status,
+                      level=6, wrap=WRAP_ZLIB, stream=None):
+    rc = load().zgpu_deflate_batch_dev(_dp(src), _dp(src_off), _dp(src_len), _dp(dst),
+                                       _dp(dst_off), _dp(dst_cap), _dp(dst_len), _dp(status),
+                                       src_len.numel(), level, wrap, _stream(stream))
+    if rc:
+        raise ZlibCompressionError(f"zgpu_deflate_batch_dev failed: {rc}")
+
+
+def crc32_batch_dev(src, off, length, out, init=None, stream=None):
+    rc = load().zgpu_crc32_batch_dev(_dp(src), _dp(off), _dp(length), _dp(init), _dp(out),
+                                     length.numel(), _stream(stream))
+    if rc:
+        raise ZlibError(f"zgpu_crc32_batch_dev failed: {rc}")
+
+
+def adler32_batch_dev(src, off, length, out, init=None, stream=None):
+    rc = load().zgpu_adler32_batch_dev(_dp(src), _dp(off), _dp(length), _dp(init), _dp(out),
+                                       length.numel(), _stream(stream))
+    if rc:
+        raise ZlibError(f"zgpu_adler32_batch_dev failed: {rc}")
+
+
+def generate_dev(dst, length, count, kind, seed=1, first_index=0, stream=None):
+    rc = load().zgpu_generate_dev(_dp(dst), length, count, kind, seed, first_index, _stream(stream))
+    if rc:
+        raise ZlibError(f"zgpu_generate_dev failed: {rc}")
+
+
+def set_inflight_bytes(n):
+    return load().zgpu_set_inflight_bytes(n)
+
+
+def info():
+    return load().zgpu_info().decode()
+
+
+# ---------------- the reference's TS surface ----------------
+
+@dataclass
+class ZlibResult:
+    """src/lib/types.ts:71-78."""
+    data: bytes
+    originalSize: int
+    compressedSize: int
+    compressionRatio: float
+    processingTime: float
+    gpuAccelerated: bool = True
+
+
+class Zlib:
+    """src/lib/index.ts ``Zlib`` — compress / crc32 / adler32 / getVersion."""
+
+    def __init__(self):
+        load()
+
+    def compress(self, data, level=6):
+        t0 = time.perf_counter()
+        data = bytes(data)
+        rc, out = compress2(data, level if level is not None else 6)
+        if rc != Z_OK:
+            raise ZlibCompressionError(f"Compression failed with code: {rc}")
+        ms = (time.perf_counter() - t0) * 1e3
+        return ZlibResult(out, len(data), len(out), len(data) / max(len(out), 1), ms)
+
+    def crc32(self, data, crc=0):
+        return crc32(data, crc)
+
+    def adler32(self, data, adler=1):
+        return adler32(data, adler)
+
+    def getVersion(self):
+        return load().zlibVersion().decode()
