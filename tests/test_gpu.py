@@ -86,6 +86,7 @@ def test_deflate_wrappers_golden(zg, golden):
     raw = zg.compress_batch(bufs, level=6, wrap=0)
     gz = zg.compress_batch(bufs, level=6, wrap=2)
     for c, (s1, r), (s2, g) in zip(cases, raw, gz):
+        assert s1 == 0 and s2 == 0
         assert hashlib.sha256(r).hexdigest() == c["raw6"]["sha256"], (c["kind"], c["n"])
         assert hashlib.sha256(g).hexdigest() == c["gzip6"]["sha256"], (c["kind"], c["n"])
 

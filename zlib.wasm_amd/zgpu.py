@@ -125,7 +125,8 @@ def compress_batch(bufs, level=6, wrap=WRAP_ZLIB, caps=None):
     n = len(bufs)
     src, keep = _ptr_array(bufs)
     lens = (C.c_size_t * n)(*[len(b) for b in bufs])
-    caps = caps or [compress_bound(len(b)) for b in bufs]
+    extra = 12 if wrap == WRAP_GZIP else 0        # deflateBound wraplen 18 vs 6
+    caps = caps or [compress_bound(len(b)) + extra for b in bufs]
     outs = [C.create_string_buffer(max(c, 1)) for c in caps]
     dst = (C.c_void_p * n)(*[C.addressof(o) for o in outs])
     dlen = (C.c_size_t * n)(*caps)
