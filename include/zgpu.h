@@ -58,6 +58,15 @@ const char *zgpu_info(void);
  * byte).  Default 1 GiB.  Returns the previous value. */
 size_t zgpu_set_inflight_bytes(size_t bytes);
 
+/* Per-stage device timing for profiling: HIP events recorded on the launch
+ * stream around every kernel of zgpu_deflate_batch_dev.  enable != 0 resets the
+ * totals and starts collecting; enable == 0 stops.  zgpu_stage_timing_read
+ * copies total milliseconds and launch counts for up to `nstages` stages:
+ * 0 checksum (trailer), 1 links, 2 match, 3 lazy parse, 4 greedy parse,
+ * 5 encode.  Returns the number of stages written. */
+void zgpu_stage_timing(int enable);
+int zgpu_stage_timing_read(double *ms, uint64_t *launches, int nstages);
+
 /* ---------------- batched, device-resident ---------------- */
 
 /* Compress `count` independent buffers.  Buffer i is src[src_off[i] ..

@@ -150,8 +150,50 @@ struct DevBuf {
     template <typename T> T *as() const { return static_cast<T *>(p); }
 };
 
+constexpr int kStages = 6;
+
+struct StageTimer {
+    bool on = false;
+    double ms[kStages] = {0};
+    uint64_t n[kStages] = {0};
+    std::vector<hipEvent_t> pool;
+    std::vector<std::pair<int, int>> pending;   // (stage, event pair index)
+    size_t used = 0;
+    hipEvent_t ev(size_t i) {
+        while (pool.size() <= i) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            pool.push_back(e);
+        }
+        return pool[i];
+    }
+    // wraps one launch; returns the launcher's result
+    template <typename F> int run(int stage, hipStream_t st, F &&launch) {
+        if (!on) return launch();
+        hipEvent_t a = ev(used), b = ev(used + 1);
+        if (a) (void)hipEventRecord(a, st);
+        int rc = launch();
+        if (b) (void)hipEventRecord(b, st);
+        if (a && b) pending.push_back({stage, (int)used});
+        used += 2;
+        return rc;
+    }
+    void collect() {     // after the stream has been synchronised
+        for (auto &pe : pending) {
+            float t = 0;
+            if (hipEventElapsedTime(&t, pool[pe.second], pool[pe.second + 1]) == hipSuccess) {
+                ms[pe.first] += t;
+                n[pe.first]++;
+            }
+        }
+        pending.clear();
+        used = 0;
+    }
+};
+
 struct Ctx {
     std::mutex mu;
+    StageTimer timer;
     int state = 0;            // 0 uninit, 1 ok, -1 failed
     int device = 0;
     std::string info;
@@ -277,20 +319,26 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         job.blocks = c.ws_blk.as<BlockRec>();
         job.nblocks = d_nblk;
         job.check = d_check;
+        StageTimer &T = c.timer;
         int rc = 0;
-        if (wrap == 1) rc = launch_adler32(src, src_off + a, src_len + a, nullptr, d_check, b - a, nullptr, 0, st);
-        else if (wrap == 2) rc = launch_crc32(src, src_off + a, src_len + a, nullptr, d_check, b - a, nullptr, 0, st);
+        if (wrap == 1)
+            rc = T.run(0, st, [&] { return launch_adler32(src, src_off + a, src_len + a, nullptr, d_check, b - a, nullptr, 0, st); });
+        else if (wrap == 2)
+            rc = T.run(0, st, [&] { return launch_crc32(src, src_off + a, src_len + a, nullptr, d_check, b - a, nullptr, 0, st); });
         if (rc) return ZGPU_MEM_ERROR;
         if (level >= 4) {
-            if (launch_deflate_stage(0, job, nullptr, st)) return ZGPU_MEM_ERROR;
-            if (launch_deflate_stage(1, job, nullptr, st)) return ZGPU_MEM_ERROR;
-            if (launch_deflate_stage(2, job, nullptr, st)) return ZGPU_MEM_ERROR;
+            if (T.run(1, st, [&] { return launch_deflate_stage(0, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+            if (T.run(2, st, [&] { return launch_deflate_stage(1, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+            if (T.run(3, st, [&] { return launch_deflate_stage(2, job, nullptr, st); })) return ZGPU_MEM_ERROR;
         } else if (level >= 1) {
-            if (launch_deflate_stage(3, job, c.ws_heads.as<uint32_t>(), st)) return ZGPU_MEM_ERROR;
+            uint32_t *heads = c.ws_heads.as<uint32_t>();
+            if (T.run(4, st, [&] { return launch_deflate_stage(3, job, heads, st); })) return ZGPU_MEM_ERROR;
         }
-        if (launch_deflate_stage(4, job, nullptr, st)) return ZGPU_MEM_ERROR;
+        if (T.run(5, st, [&] { return launch_deflate_stage(4, job, nullptr, st); })) return ZGPU_MEM_ERROR;
     }
-    return hip_ok(hipStreamSynchronize(st));
+    int rc = hip_ok(hipStreamSynchronize(st));
+    c.timer.collect();
+    return rc;
 }
 
 // host-buffer batch: pack, upload, run, download
@@ -447,6 +495,28 @@ size_t zgpu_set_inflight_bytes(size_t bytes) {
     size_t old = c.inflight;
     if (bytes >= (1u << 20)) c.inflight = bytes;
     return old;
+}
+
+void zgpu_stage_timing(int enable) {
+    Ctx &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    c.timer.on = enable != 0;
+    if (enable) {
+        for (int i = 0; i < kStages; i++) { c.timer.ms[i] = 0; c.timer.n[i] = 0; }
+        c.timer.pending.clear();
+        c.timer.used = 0;
+    }
+}
+
+int zgpu_stage_timing_read(double *ms, uint64_t *launches, int nstages) {
+    Ctx &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    int k = nstages < kStages ? nstages : kStages;
+    for (int i = 0; i < k; i++) {
+        if (ms) ms[i] = c.timer.ms[i];
+        if (launches) launches[i] = c.timer.n[i];
+    }
+    return k;
 }
 
 int zgpu_deflate_batch_dev(const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,

@@ -37,7 +37,8 @@ EXPORTED_SYMBOLS = (
     # include/zgpu.h
     "zgpu_init", "zgpu_info", "zgpu_set_inflight_bytes", "zgpu_deflate_batch_dev",
     "zgpu_crc32_batch_dev", "zgpu_adler32_batch_dev", "zgpu_compress_batch",
-    "zgpu_crc32_batch", "zgpu_adler32_batch", "zgpu_generate_dev",
+    "zgpu_crc32_batch", "zgpu_adler32_batch", "zgpu_generate_dev", "zgpu_stage_timing",
+    "zgpu_stage_timing_read",
     # include/zgpu_zlib.h
     "zlibVersion", "compress", "compress2", "compressBound", "deflateInit_",
     "deflateInit2_", "deflate", "deflateEnd", "deflateBound", "crc32", "crc32_z",
@@ -92,6 +93,10 @@ def load(path=LIB_PATH):
         getattr(L, f).argtypes = [P, P, P, P, C.c_size_t]
     L.zgpu_generate_dev.restype = I32
     L.zgpu_generate_dev.argtypes = [P, U64, U32, I32, U64, U64, P]
+    L.zgpu_stage_timing.restype = None
+    L.zgpu_stage_timing.argtypes = [I32]
+    L.zgpu_stage_timing_read.restype = I32
+    L.zgpu_stage_timing_read.argtypes = [P, P, I32]
     L.compress2.restype = I32
     L.compress2.argtypes = [P, C.POINTER(C.c_ulong), P, C.c_ulong, I32]
     L.compressBound.restype = C.c_ulong
@@ -220,6 +225,21 @@ def generate_dev(dst, length, count, kind, seed=1, first_index=0, stream=None):
     rc = load().zgpu_generate_dev(_dp(dst), length, count, kind, seed, first_index, _stream(stream))
     if rc:
         raise ZlibError(f"zgpu_generate_dev failed: {rc}")
+
+
+STAGES = ("checksum", "links", "match", "parse_lazy", "parse_greedy", "encode")
+
+
+def stage_timing(enable=True):
+    load().zgpu_stage_timing(1 if enable else 0)
+
+
+def stage_timing_read():
+    """{stage: (total_ms, launches)} for the stages of zgpu_deflate_batch_dev."""
+    ms = (C.c_double * len(STAGES))()
+    n = (C.c_uint64 * len(STAGES))()
+    load().zgpu_stage_timing_read(ms, n, len(STAGES))
+    return {s: (ms[i], n[i]) for i, s in enumerate(STAGES)}
 
 
 def set_inflight_bytes(n):
