@@ -9,7 +9,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "zlib.wasm_amd", "libzgpu.so")
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("zgpu.h", "zgpu_zlib.h", "zgpu_wasm.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("zgpu.h", "zgpu_zlib.h", "zgpu_wasm.h", "zgpu_debug.h")]
 
 
 def declared_functions():

@@ -68,6 +68,24 @@ def test_checksum_device_api_unaligned(zg, oracle):
 
 # ----------------------------- deflate -----------------------------
 
+@pytest.mark.parametrize("level", [4, 6, 9])
+@pytest.mark.parametrize("kind,n", [("text", 16383), ("mix", 200000), ("runs", 70000),
+                                    ("records", 100000), ("four", 50000)])
+def test_stage_links_and_match_vs_oracle(zg, oracle, level, kind, n):
+    """Per-position intermediates of the GPU pipeline == the oracle's
+    position-parallel formulation (zo_pp_links / zo_pp_match)."""
+    data = datagen.make(kind, n, 17)
+    link, rf, rq = zg.debug_stages(data, level)
+    olink = oracle.links(data)
+    bad = np.nonzero(link != olink)[0]
+    assert bad.size == 0, f"links differ at {bad[:10]}"
+    of, oq = oracle.match(data, level, olink)
+    bad = np.nonzero(rf != of)[0]
+    assert bad.size == 0, f"rfull differ at {bad[:5]}: gpu {rf[bad[:5]]} oracle {of[bad[:5]]}"
+    if level >= 5:
+        bad = np.nonzero(rq != oq)[0]
+        assert bad.size == 0, f"rquart differ at {bad[:5]}: gpu {rq[bad[:5]]} oracle {oq[bad[:5]]}"
+
 @pytest.mark.parametrize("level", list(range(10)))
 def test_deflate_golden(zg, golden, level):
     cases = [c for c in golden["cases"] if c["n"] <= (1 << 20)]

@@ -20,6 +20,7 @@
 #include "../../include/zgpu.h"
 #include "../../include/zgpu_zlib.h"
 #include "../../include/zgpu_wasm.h"
+#include "../../include/zgpu_debug.h"
 
 using namespace zgpu;
 
@@ -580,6 +581,40 @@ int zgpu_generate_dev(uint8_t *dst, uint64_t len, uint32_t count, int kind, uint
     if (rc) return rc;
     return launch_generate(dst, len, count, kind, seed, first_index, static_cast<hipStream_t>(stream))
                ? ZGPU_STREAM_ERROR : ZGPU_OK;
+}
+
+int zgpu_debug_stages(const uint8_t *src, size_t n, int level, uint16_t *link, uint32_t *rfull,
+                      uint32_t *rquart) {
+    Ctx &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    int rc = init_locked(c);
+    if (rc) return rc;
+    if (level < 4 || level > 9) return ZGPU_STREAM_ERROR;
+    const size_t nn = n ? n : 1;
+    if (!c.ws_io.ensure(nn + 64) || !c.ws_link.ensure(2 * nn + 64) || !c.ws_rf.ensure(4 * nn + 64) ||
+        !c.ws_rq.ensure(4 * nn + 64) || !c.ws_small.ensure(64))
+        return ZGPU_MEM_ERROR;
+    uint64_t *d_meta = c.ws_small.as<uint64_t>();   // off, len, ws_off
+    const uint64_t meta[3] = {0, (uint64_t)n, 0};
+    hipStream_t st = nullptr;
+    if (hipMemcpy(d_meta, meta, sizeof meta, hipMemcpyHostToDevice) != hipSuccess ||
+        (n && hipMemcpy(c.ws_io.p, src, n, hipMemcpyHostToDevice) != hipSuccess))
+        return ZGPU_MEM_ERROR;
+    DeflateJob job{};
+    job.src = c.ws_io.as<uint8_t>(); job.src_off = d_meta; job.src_len = d_meta + 1;
+    job.first = 0; job.count = 1; job.level = level; job.wrap = 1;
+    job.ws_off = d_meta + 2;
+    job.link = c.ws_link.as<uint16_t>();
+    job.rfull = c.ws_rf.as<uint32_t>();
+    job.rquart = c.ws_rq.as<uint32_t>();
+    if (launch_deflate_stage(0, job, nullptr, st) || launch_deflate_stage(1, job, nullptr, st) ||
+        hipDeviceSynchronize() != hipSuccess)
+        return ZGPU_MEM_ERROR;
+    if (link && n && hipMemcpy(link, job.link, 2 * n, hipMemcpyDeviceToHost) != hipSuccess) return ZGPU_MEM_ERROR;
+    if (rfull && n && hipMemcpy(rfull, job.rfull, 4 * n, hipMemcpyDeviceToHost) != hipSuccess) return ZGPU_MEM_ERROR;
+    if (rquart && n && level >= 5 && hipMemcpy(rquart, job.rquart, 4 * n, hipMemcpyDeviceToHost) != hipSuccess)
+        return ZGPU_MEM_ERROR;
+    return ZGPU_OK;
 }
 
 // ---------------------------- zlib.h names ----------------------------

@@ -107,62 +107,19 @@ __global__ __launch_bounds__(64) void k_links(DeflateJob job) {
 // the result after chain/4 candidates too, and stores (len<<16 | dist).
 // ------------------------------------------------------------------------
 constexpr int kMW = 32768, kMT = 4096, kMPad = 272;
-constexpr int kMDat = kMW + kMT + kMPad;                   // 37136 bytes
-constexpr int kMLnk = kMW + kMT;                            // 36864 entries
+constexpr int kME = kMW + kMT + kMPad;                     // 37136 words = 148.5 KiB
 constexpr int kMatchThreads = 1024;
 
-__device__ inline void match_walk(const uint8_t *dat, const uint16_t *lnk, int64_t p, int64_t B,
-                                  int64_t n, LevelCfg cfg, uint32_t &rf, uint32_t &rq) {
-    rf = rq = 0;
-    const int s = (int)(p - B);
-    const uint32_t d0 = lnk[s];
-    if (d0 == 0 || d0 > (uint32_t)kMaxDist) return;
-    const int64_t labs = p > kMaxDist ? p - kMaxDist : 0;
-    const int limit = (int)(labs - B);
-    const int64_t rem = n - p;
-    const int nice = rem < cfg.nice ? (int)rem : cfg.nice;
-    const int maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
-    const uint32_t chain = cfg.chain, bq = cfg.chain >> 2;
-    const uint32_t scan0 = lds32u(dat, s) & 0xffffu;
-    int best = kMinMatch - 1, bpos = 0, bestq = 0, bposq = 0;
-    bool snapped = false;
-    uint32_t scan_end = lds32u(dat, s + best - 1) & 0xffffu;
-    int m = s - (int)d0;
-    uint32_t count = 0;
-    for (;;) {
-        count++;
-        bool stop = false;
-        if ((lds32u(dat, m) & 0xffffu) == scan0 && (lds32u(dat, m + best - 1) & 0xffffu) == scan_end) {
-            int k = 0;
-            for (;;) {
-                uint32_t x = lds32u(dat, s + k) ^ lds32u(dat, m + k);
-                if (x) { k += __builtin_ctz(x) >> 3; break; }
-                k += 4;
-                if (k >= maxcmp) break;
-            }
-            const int len = k < maxcmp ? k : maxcmp;
-            if (len > best) {
-                best = len;
-                bpos = m;
-                if (len >= nice) stop = true;
-                else scan_end = lds32u(dat, s + best - 1) & 0xffffu;
-            }
-        }
-        if (count == bq) { bestq = best; bposq = bpos; snapped = true; }
-        if (stop || count >= chain) break;
-        const uint32_t d = lnk[m];
-        if (d == 0) break;
-        m -= (int)d;
-        if (m <= limit) break;
-    }
-    if (!snapped) { bestq = best; bposq = bpos; }
-    if (best >= kMinMatch) rf = ((uint32_t)best << 16) | (uint32_t)(s - bpos);
-    if (bestq >= kMinMatch) rq = ((uint32_t)bestq << 16) | (uint32_t)(s - bposq);
+// LDS word for window position q:  link(q) | byte[q] << 16 | byte[q+1] << 24.
+// One ds_read_b32 yields both the chain link and the first two bytes of a
+// candidate; the quick-reject pair at best-1 is the high half of word best-1.
+__device__ inline uint32_t get4(const uint32_t *E, int i) {      // bytes i..i+3
+    return (E[i] >> 16) | (E[i + 2] & 0xffff0000u);
 }
 
+template <int kVariant>
 __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int want_q) {
-    __shared__ __attribute__((aligned(16))) uint8_t dat[kMDat];
-    __shared__ __attribute__((aligned(16))) uint16_t lnk[kMLnk];
+    __shared__ __attribute__((aligned(16))) uint32_t E[kME];
     __shared__ int next_i;
     const int tid = threadIdx.x;
     const uint32_t bi = blockIdx.x;
@@ -173,53 +130,104 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
     uint32_t *rf = job.rfull + job.ws_off[bi];
     uint32_t *rq = job.rquart + job.ws_off[bi];
     const LevelCfg cfg = c_ct.cfg[job.level];
+    const uint32_t chain = cfg.chain, bq = cfg.chain >> 2;
+
+    auto word = [&](int64_t q, bool with_link) -> uint32_t {
+        uint32_t w = 0;
+        if (q >= 0 && q < n) {
+            w = (uint32_t)in[q] << 16;
+            if (q + 1 < n) w |= (uint32_t)in[q + 1] << 24;
+            if (with_link) w |= L[q];
+        }
+        return w;
+    };
 
     for (int64_t ts = 0; ts < n; ts += kMT) {
         const int64_t B = ts - kMW;
         if (ts == 0) {
-            for (int i = tid; i < kMDat; i += kMatchThreads) {
-                int64_t q = B + i;
-                dat[i] = (q >= 0 && q < n) ? in[q] : 0;
-            }
-            for (int i = tid; i < kMLnk; i += kMatchThreads) {
-                int64_t q = B + i;
-                lnk[i] = (q >= 0 && q < n) ? L[q] : 0;
-            }
+            for (int i = tid; i < kME; i += kMatchThreads) E[i] = word(B + i, i < kMW + kMT);
         } else {
-            // slide both windows down by kMT (register round trip)
-            constexpr int kDatChunks = (kMDat - kMT) / 16;          // 2065
-            constexpr int kLnkChunks = (kMW * 2) / 16;              // 4096
-            uint4 td[3], tl[4];
-            const uint4 *sd = reinterpret_cast<const uint4 *>(dat + kMT);
-            const uint4 *sl = reinterpret_cast<const uint4 *>(lnk + kMT);
-#pragma unroll
-            for (int k = 0; k < 3; k++) { int c = tid + k * kMatchThreads; if (c < kDatChunks) td[k] = sd[c]; }
-#pragma unroll
-            for (int k = 0; k < 4; k++) { int c = tid + k * kMatchThreads; tl[k] = sl[c]; }
+            // slide down by kMT words.  kMT/4 uint4 chunks == kMatchThreads, so
+            // thread t only ever touches chunks = t (mod kMatchThreads): moving
+            // them in increasing order needs no barrier and no staging.
+            static_assert(kMT / 4 == kMatchThreads, "slide assumes kMT/4 == threads");
+            constexpr int kChunks = (kME - kMT) / 4;
+            uint4 *dE = reinterpret_cast<uint4 *>(E);
+            for (int c = tid; c < kChunks; c += kMatchThreads) dE[c] = dE[c + kMT / 4];
             __syncthreads();
-            uint4 *dd = reinterpret_cast<uint4 *>(dat);
-            uint4 *dl = reinterpret_cast<uint4 *>(lnk);
-#pragma unroll
-            for (int k = 0; k < 3; k++) { int c = tid + k * kMatchThreads; if (c < kDatChunks) dd[c] = td[k]; }
-#pragma unroll
-            for (int k = 0; k < 4; k++) { int c = tid + k * kMatchThreads; dl[c] = tl[k]; }
-            for (int i = tid; i < kMT; i += kMatchThreads) {
-                int64_t q = B + (kMDat - kMT) + i;
-                dat[kMDat - kMT + i] = (q < n) ? in[q] : 0;
-                int64_t r = ts + i;
-                lnk[kMW + i] = (r < n) ? L[r] : 0;
+            // words [kMW, kME): the slid part (pad of the last tile) still needs
+            // its links, [kME-kMT, kME) are new; one pass, no overlap race
+            for (int i = tid; i < kME - kMW; i += kMatchThreads) {
+                const int idx = kMW + i;
+                const int64_t q = ts + i;
+                if (idx >= kME - kMT) E[idx] = word(q, i < kMT);
+                else if (i < kMT && q < n) E[idx] |= L[q];
             }
         }
         if (tid == 0) next_i = 0;
         __syncthreads();
+
         for (;;) {
             const int i = atomicAdd(&next_i, 1);
             const int64_t p = ts + i;
             if (i >= kMT || p >= n) break;
-            uint32_t a, b;
-            match_walk(dat, lnk, p, B, n, cfg, a, b);
-            rf[p] = a;
-            if (want_q) rq[p] = b;
+            const int s = (int)(p - B);
+            const uint32_t e0 = E[s];
+            const uint32_t d0 = e0 & 0xffffu;
+            uint32_t r_full = 0, r_q = 0;
+            if (d0 != 0 && d0 <= (uint32_t)kMaxDist) {
+                const int64_t labs = p > kMaxDist ? p - kMaxDist : 0;
+                const int limit = (int)(labs - B);
+                const int64_t rem = n - p;
+                const int nice = rem < cfg.nice ? (int)rem : cfg.nice;
+                const int maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
+                const uint32_t S0 = get4(E, s), S1 = get4(E, s + 4), S2 = get4(E, s + 8), S3 = get4(E, s + 12);
+                const uint32_t scan01 = e0 >> 16;
+                int best = kMinMatch - 1, bpos = 0, bestq = 0, bposq = 0;
+                bool snapped = false;
+                uint32_t scan_end = (S0 >> 8) & 0xffffu;
+                int m = s - (int)d0;
+                uint32_t count = 0;
+                for (;;) {
+                    const uint32_t em = E[m];                       // link + bytes m, m+1
+                    const uint32_t eb = E[m + best - 1] >> 16;      // bytes m+best-1, m+best
+                    count++;
+                    bool stop = false;
+                    if ((em >> 16) == scan01 && eb == scan_end) {
+                        int k;
+                        uint32_t x = get4(E, m) ^ S0;
+                        if (x) k = __builtin_ctz(x) >> 3;
+                        else if ((x = get4(E, m + 4) ^ S1)) k = 4 + (__builtin_ctz(x) >> 3);
+                        else if ((x = get4(E, m + 8) ^ S2)) k = 8 + (__builtin_ctz(x) >> 3);
+                        else if ((x = get4(E, m + 12) ^ S3)) k = 12 + (__builtin_ctz(x) >> 3);
+                        else {
+                            k = 16;
+                            while (k < maxcmp) {
+                                x = get4(E, s + k) ^ get4(E, m + k);
+                                if (x) { k += __builtin_ctz(x) >> 3; break; }
+                                k += 4;
+                            }
+                        }
+                        const int len = k < maxcmp ? k : maxcmp;
+                        if (len > best) {
+                            best = len;
+                            bpos = m;
+                            if (len >= nice) stop = true;
+                            else scan_end = E[s + best - 1] >> 16;
+                        }
+                    }
+                    if (count == bq) { bestq = best; bposq = bpos; snapped = true; }
+                    const uint32_t d = em & 0xffffu;
+                    const int nm = m - (int)d;
+                    if (stop || count >= chain || d == 0 || nm <= limit) break;
+                    m = nm;
+                }
+                if (!snapped) { bestq = best; bposq = bpos; }
+                if (best >= kMinMatch) r_full = ((uint32_t)best << 16) | (uint32_t)(s - bpos);
+                if (bestq >= kMinMatch) r_q = ((uint32_t)bestq << 16) | (uint32_t)(s - bposq);
+            }
+            rf[p] = r_full;
+            if (want_q) rq[p] = r_q;
         }
         __syncthreads();
     }
@@ -260,95 +268,149 @@ struct ParseOut {
 
 // ------------------------------------------------------------------------
 // k_parse_slow — deflate_slow over precomputed per-position results.
-// One wave per buffer; the wave stages tiles of results and input bytes into
-// LDS, lane 0 runs the sequential lazy-evaluation state machine.
+// One wave per buffer, executed wave-uniformly: every lane runs the same
+// state machine on scalar (SGPR) state, values read from LDS are made uniform
+// with readfirstlane, and only lane 0 stores.  Runs of positions with no usable
+// match (the literal branch of deflate.c:2007-2019 repeated) are detected 64
+// at a time with a ballot and emitted in bulk.
 // ------------------------------------------------------------------------
-constexpr int kPT = 2048;
+constexpr int kPT = 4096;
+
+__device__ inline uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+struct ParseU {                     // wave-uniform parse output state
+    uint32_t *sym;
+    BlockRec *blk;
+    uint32_t nsym, blk_nsym, blk_sym_start, nblk;
+    uint32_t block_start, S, E;
+    __device__ inline void flush(uint32_t strstart, bool last, int lane) {   // FLUSH_BLOCK_ONLY
+        if (lane == 0) {
+            BlockRec r;
+            r.sym_start = blk_sym_start;
+            r.nsym = blk_nsym;
+            r.in_start = block_start;
+            r.in_end = strstart;
+            r.flags = (last ? 1u : 0u) | (block_start >= S ? 2u : 0u);
+            r.pad = 0;
+            blk[nblk] = r;
+        }
+        nblk++;
+        block_start = strstart;
+        blk_sym_start = nsym;
+        blk_nsym = 0;
+    }
+    __device__ inline bool tally1(uint32_t v, int lane) {                   // _tr_tally_*
+        if (lane == 0) sym[nsym] = v;
+        nsym++;
+        return ++blk_nsym == (uint32_t)kSymLimit;
+    }
+    __device__ inline void fill(uint32_t p, uint32_t n) {                   // fill_window bookkeeping
+        if (p - S >= (uint32_t)(kWSize + kMaxDist)) S += kWSize;
+        if (E < n) { uint32_t e = S + 2 * kWSize; E = e < n ? e : n; }
+    }
+};
 
 __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job) {
     __shared__ uint32_t s_rf[kPT];
     __shared__ uint32_t s_rq[kPT];
     __shared__ uint8_t s_in[kPT + 4];
-    __shared__ int64_t s_next;
-    __shared__ int s_done;
     const int lane = threadIdx.x;
     const uint32_t bi = blockIdx.x;
     const uint32_t g = job.first + bi;
-    const int64_t n = (int64_t)job.src_len[g];
+    const uint32_t n = (uint32_t)job.src_len[g];
     const uint8_t *in = job.src + job.src_off[g];
     const uint32_t *rf = job.rfull + job.ws_off[bi];
     const uint32_t *rq = job.rquart + job.ws_off[bi];
     const LevelCfg cfg = c_ct.cfg[job.level];
     const bool use_q = cfg.good < cfg.lazy;
+    const uint32_t lazy = cfg.lazy, good = cfg.good;
 
-    ParseOut po;
+    ParseU po;
     po.sym = job.sym + job.ws_off[bi];
     po.blk = job.blocks + job.blk_off[bi];
     po.nsym = po.blk_nsym = po.blk_sym_start = po.nblk = 0;
     po.block_start = 0; po.S = 0; po.E = 0;
-    int64_t p = 0, match_start = 0, prev_match = 0;
-    uint32_t match_length = kMinMatch - 1, prev_length = 0;
-    bool match_available = false;
+    uint32_t p = 0, match_start = 0, match_length = kMinMatch - 1;
+    bool avail = false, done = false;
 
-    int64_t t0 = 0;
-    for (;;) {
+    uint32_t t0 = 0;
+    while (!done) {
         for (int j = lane; j < kPT; j += 64) {
-            int64_t q = t0 + j;
+            const uint32_t q = t0 + j;
             s_rf[j] = q < n ? rf[q] : 0;
             if (use_q) s_rq[j] = q < n ? rq[q] : 0;
         }
         for (int j = lane; j < kPT + 1; j += 64) {
-            int64_t q = t0 - 1 + j;
-            s_in[j] = (q >= 0 && q < n) ? in[q] : 0;
+            const int64_t q = (int64_t)t0 - 1 + j;
+            s_in[j] = (q >= 0 && q < (int64_t)n) ? in[q] : 0;
         }
         __syncthreads();
-        if (lane == 0) {
-            int done = 0;
-            for (;;) {
-                if (p >= t0 + kPT) break;
-                if (po.E - p < kMinLookahead) {
-                    po.fill(p, n);
-                    if (po.E == p) { done = 1; break; }
-                }
-                const int64_t lookahead = po.E - p;
-                prev_length = match_length;
-                prev_match = match_start;
-                match_length = kMinMatch - 1;
-                if (lookahead >= kMinMatch && prev_length < cfg.lazy) {
-                    const uint32_t r = (use_q && prev_length >= cfg.good) ? s_rq[p - t0] : s_rf[p - t0];
-                    const uint32_t rl = r >> 16;
-                    if (rl > prev_length) {
-                        match_length = rl;
-                        match_start = p - (int64_t)(r & 0xffffu);
-                        if (match_length == kMinMatch && p - match_start > kTooFar) match_length = kMinMatch - 1;
+        const bool tile_to_end = (uint64_t)t0 + kPT >= n;
+        for (;;) {
+            if (!tile_to_end && p + 64 > t0 + kPT) break;         // reload, keep 64 lookahead
+            if (po.E - p < (uint32_t)kMinLookahead) {
+                po.fill(p, n);
+                if (po.E == p) { done = true; break; }
+            }
+            const uint32_t lookahead = po.E - p;
+            // ---- bulk literals: no pending match, far from the window end ----
+            if (match_length < kMinMatch && p + 64 + kMinLookahead <= po.E) {
+                const uint32_t r = s_rf[p - t0 + lane];
+                const uint32_t rl = r >> 16;
+                const bool hit = rl >= kMinMatch && !(rl == kMinMatch && (r & 0xffffu) > (uint32_t)kTooFar);
+                const uint64_t mask = __ballot(hit);
+                const uint32_t k = mask ? (uint32_t)__builtin_ctzll(mask) : 64u;
+                if (k > 0) {
+                    uint32_t a = avail ? p - 1 : p;
+                    const uint32_t b = p + k - 1;
+                    while (a < b) {
+                        const uint32_t room = kSymLimit - po.blk_nsym;
+                        const uint32_t take = (b - a) < room ? (b - a) : room;
+                        if ((uint32_t)lane < take) po.sym[po.nsym + lane] = s_in[a + lane - t0 + 1];
+                        po.nsym += take;
+                        po.blk_nsym += take;
+                        a += take;
+                        if (po.blk_nsym == (uint32_t)kSymLimit) po.flush(a, false, lane);
                     }
-                }
-                if (prev_length >= kMinMatch && match_length <= prev_length) {
-                    const uint32_t dist = (uint32_t)(p - 1 - prev_match);
-                    const bool bflush = po.tally((dist << 8) | (prev_length - kMinMatch));
-                    p += prev_length - 1;
-                    match_available = false;
-                    match_length = kMinMatch - 1;
-                    if (bflush) po.flush(p, false);
-                } else if (match_available) {
-                    if (po.tally(s_in[p - t0])) po.flush(p, false);
-                    p++;
-                } else {
-                    match_available = true;
-                    p++;
+                    avail = true;
+                    p += k;
+                    continue;
                 }
             }
-            if (done) {
-                if (match_available) po.tally(s_in[p - t0]);
-                po.flush(p, true);
-                job.nblocks[bi] = po.nblk;
+            // ---- one deflate_slow step (deflate.c:1946-2027) ----
+            const uint32_t prev_length = match_length, prev_match = match_start;
+            match_length = kMinMatch - 1;
+            if (lookahead >= kMinMatch && prev_length < lazy) {
+                const uint32_t r = ufl((use_q && prev_length >= good) ? s_rq[p - t0] : s_rf[p - t0]);
+                const uint32_t rl = r >> 16;
+                if (rl > prev_length) {
+                    match_length = rl;
+                    match_start = p - (r & 0xffffu);
+                    if (match_length == kMinMatch && p - match_start > (uint32_t)kTooFar) match_length = kMinMatch - 1;
+                }
             }
-            s_next = p;
-            s_done = done;
+            if (prev_length >= kMinMatch && match_length <= prev_length) {
+                const uint32_t dist = p - 1 - prev_match;
+                const bool bflush = po.tally1((dist << 8) | (prev_length - kMinMatch), lane);
+                p += prev_length - 1;
+                avail = false;
+                match_length = kMinMatch - 1;
+                if (bflush) po.flush(p, false, lane);
+            } else if (avail) {
+                const uint32_t lit = ufl(s_in[p - t0]);
+                if (po.tally1(lit, lane)) po.flush(p, false, lane);
+                p++;
+            } else {
+                avail = true;
+                p++;
+            }
         }
-        __syncthreads();
-        if (s_done) break;
-        t0 = s_next;
+        if (done) {
+            if (avail) po.tally1(ufl(s_in[p - t0]), lane);
+            po.flush(p, true, lane);
+            if (lane == 0) job.nblocks[bi] = po.nblk;
+        }
+        t0 = p;
         __syncthreads();
     }
 }
@@ -916,7 +978,7 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     const dim3 grid(job.count);
     switch (stage) {
     case 0: hipLaunchKernelGGL(k_links, grid, dim3(64), 0, st, job); break;
-    case 1: hipLaunchKernelGGL(k_match, grid, dim3(kMatchThreads), 0, st, job,
+    case 1: hipLaunchKernelGGL(k_match<0>, grid, dim3(kMatchThreads), 0, st, job,
                                (int)(job.level >= 5)); break;
     case 2: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job); break;
     case 3: hipLaunchKernelGGL(k_parse_fast, grid, dim3(64), 0, st, job, heads); break;

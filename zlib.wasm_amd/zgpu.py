@@ -49,6 +49,8 @@ EXPORTED_SYMBOLS = (
     "zlib_get_version", "zlib_compress_simd", "zlib_compress_simd_full",
     "zlib_compress_simd_buffer", "zlib_crc32_simd_optimized", "zlib_crc32_simd_enhanced",
     "zlib_adler32_simd",
+    # include/zgpu_debug.h (test-only)
+    "zgpu_debug_stages",
 )
 
 
@@ -240,6 +242,23 @@ def stage_timing_read():
     n = (C.c_uint64 * len(STAGES))()
     load().zgpu_stage_timing_read(ms, n, len(STAGES))
     return {s: (ms[i], n[i]) for i, s in enumerate(STAGES)}
+
+
+def debug_stages(data, level):
+    """Test-only: (link u16[n], rfull u32[n], rquart u32[n]) from the GPU stages."""
+    import numpy as np
+    data = bytes(data)
+    n = len(data)
+    link = np.zeros(max(n, 1), dtype=np.uint16)
+    rf = np.zeros(max(n, 1), dtype=np.uint32)
+    rq = np.zeros(max(n, 1), dtype=np.uint32)
+    L = load()
+    L.zgpu_debug_stages.restype = C.c_int
+    L.zgpu_debug_stages.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+    rc = L.zgpu_debug_stages(data, n, level, link.ctypes.data, rf.ctypes.data, rq.ctypes.data)
+    if rc:
+        raise ZlibError(f"zgpu_debug_stages failed: {rc}")
+    return link[:n], rf[:n], rq[:n]
 
 
 def set_inflight_bytes(n):
