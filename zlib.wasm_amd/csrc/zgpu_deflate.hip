@@ -35,6 +35,79 @@ __device__ inline uint32_t lds32u(const uint8_t *base, int off) {
     return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(off & 3));
 }
 
+
+// Stage bytes src[start .. start+count) of a buffer of length n into LDS
+// (dst[0..count)), zero outside [0, n).  count % 16 == 0, dst 16-B aligned.
+// Every lane issues all of its loads before any LDS store, so a tile costs
+// about one memory latency instead of one per element.
+template <int kThreads, int kMaxChunksPerThread>
+__device__ inline void stage_bytes(uint8_t *dst, const uint8_t *src, int64_t start, int count,
+                                   int64_t n, int tid) {
+    const int nchunks = count >> 4;
+    uint4 v[kMaxChunksPerThread];
+#pragma unroll
+    for (int k = 0; k < kMaxChunksPerThread; k++) {
+        const int c = tid + k * kThreads;
+        v[k] = make_uint4(0, 0, 0, 0);
+        if (c >= nchunks) continue;
+        const int64_t x = start + 16ll * c;
+        if (x >= 0 && x + 16 <= n) {
+            const uintptr_t a = reinterpret_cast<uintptr_t>(src + x);
+            const uint32_t sh = (uint32_t)(a & 3u);
+            const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+            if (sh == 0) {
+                v[k].x = q[0]; v[k].y = q[1]; v[k].z = q[2]; v[k].w = q[3];
+            } else {
+                const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
+                v[k].x = __builtin_amdgcn_alignbyte(d1, d0, sh);
+                v[k].y = __builtin_amdgcn_alignbyte(d2, d1, sh);
+                v[k].z = __builtin_amdgcn_alignbyte(d3, d2, sh);
+                v[k].w = __builtin_amdgcn_alignbyte(d4, d3, sh);
+            }
+        } else if (x + 16 > 0 && x < n) {
+            uint32_t w[4] = {0, 0, 0, 0};
+            for (int j = 0; j < 16; j++) {
+                const int64_t o = x + j;
+                if (o >= 0 && o < n) w[j >> 2] |= (uint32_t)src[o] << (8 * (j & 3));
+            }
+            v[k] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxChunksPerThread; k++) {
+        const int c = tid + k * kThreads;
+        if (c < nchunks) reinterpret_cast<uint4 *>(dst)[c] = v[k];
+    }
+}
+
+// Stage u32 words src[start .. start+count) (start % 4 == 0, count % 4 == 0)
+// into LDS, zero at or beyond `limit`.
+template <int kThreads, int kMaxChunksPerThread>
+__device__ inline void stage_words(uint32_t *dst, const uint32_t *src, int64_t start, int count,
+                                   int64_t limit, int tid) {
+    const int nchunks = count >> 2;
+    uint4 v[kMaxChunksPerThread];
+#pragma unroll
+    for (int k = 0; k < kMaxChunksPerThread; k++) {
+        const int c = tid + k * kThreads;
+        const int64_t x = start + 4ll * c;
+        v[k] = make_uint4(0, 0, 0, 0);
+        if (c < nchunks && x < limit) {
+            if (x + 4 <= limit) v[k] = *reinterpret_cast<const uint4 *>(src + x);
+            else {
+                v[k].x = src[x];
+                if (x + 1 < limit) v[k].y = src[x + 1];
+                if (x + 2 < limit) v[k].z = src[x + 2];
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxChunksPerThread; k++) {
+        const int c = tid + k * kThreads;
+        if (c < nchunks) reinterpret_cast<uint4 *>(dst)[c] = v[k];
+    }
+}
+
 // ------------------------------------------------------------------------
 // k_links — one wave per buffer.  head[] holds the low 16 bits of the most
 // recent position per hash; every 32 KiB it is swept like slide_hash
@@ -43,10 +116,13 @@ __device__ inline uint32_t lds32u(const uint8_t *base, int off) {
 // found with a shuffle scan; only the last lane of each hash updates head[].
 // ------------------------------------------------------------------------
 constexpr int kLinkStage = 4096;
+constexpr int kLinkSlots = 256;
 
 __global__ __launch_bounds__(64) void k_links(DeflateJob job) {
     __shared__ uint16_t head[32768];
-    __shared__ uint8_t stage[kLinkStage + 8];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kLinkStage + 16];
+    __shared__ unsigned long long smask[kLinkSlots];
+    __shared__ uint32_t sh_h[64];
     __shared__ uint8_t mark[64];
     const int lane = threadIdx.x;
     const uint32_t bi = blockIdx.x;
@@ -54,16 +130,16 @@ __global__ __launch_bounds__(64) void k_links(DeflateJob job) {
     const int64_t n = (int64_t)job.src_len[g];
     const uint8_t *in = job.src + job.src_off[g];
     uint16_t *out = job.link + job.ws_off[bi];
+    const unsigned long long below_mask = (1ull << lane) - 1ull;
 
     for (int i = lane; i < 32768; i += 64) head[i] = 32768;   // "position -32768"
     for (int64_t t0 = 0; t0 < n; t0 += kLinkStage) {
         __syncthreads();
-        const int64_t tl = (n - t0 < kLinkStage + 2) ? n - t0 : kLinkStage + 2;
-        for (int j = lane; j < kLinkStage + 2; j += 64) stage[j] = j < tl ? in[t0 + j] : 0;
+        stage_bytes<64, (kLinkStage + 16) / 16 / 64 + 1>(stage, in, t0, kLinkStage + 16, n, lane);
         __syncthreads();
         const int64_t tend = (t0 + kLinkStage < n) ? t0 + kLinkStage : n;
         for (int64_t c0 = t0; c0 < tend; c0 += 64) {
-            if ((c0 & 32767) == 0 && c0 > 0) {                // slide sweep
+            if ((c0 & 32767) == 0 && c0 > 0) {                // slide sweep (slide_hash analogue)
                 const uint32_t now = (uint32_t)c0;
                 for (int i = lane; i < 32768; i += 64) {
                     uint32_t age = (now - head[i]) & 0xffffu;
@@ -74,14 +150,24 @@ __global__ __launch_bounds__(64) void k_links(DeflateJob job) {
             const int64_t p = c0 + lane;
             const bool valid = p + 3 <= n;
             const int j = (int)(p - t0);
-            uint32_t h = valid ? hash3(stage[j], stage[j + 1], stage[j + 2]) : (0x10000u + lane);
-            int pred = -1;
-            for (int d = 1; d < 64; d++) {
-                uint32_t v = __shfl_up(h, d, 64);
-                if (pred < 0 && lane >= d && v == h) pred = lane - d;
-            }
+            const uint32_t h = valid ? hash3(stage[j], stage[j + 1], stage[j + 2]) : (0x10000u + lane);
+            // nearest earlier lane with the same hash: lanes OR their bit into a
+            // slot keyed by the low hash bits (order independent), then the
+            // candidates below are verified against the true hash
+            const int slot = (int)(h & (kLinkSlots - 1));
+            smask[slot] = 0ull;
+            sh_h[lane] = h;
             mark[lane] = 0;
             __syncthreads();
+            atomicOr(&smask[slot], 1ull << lane);
+            __syncthreads();
+            unsigned long long cand = smask[slot] & below_mask;
+            int pred = -1;
+            while (cand) {
+                const int jl = 63 - __builtin_clzll(cand);
+                if (sh_h[jl] == h) { pred = jl; break; }
+                cand &= ~(1ull << jl);
+            }
             if (pred >= 0) mark[pred] = 1;
             uint32_t link = 0;
             if (valid) {
@@ -311,9 +397,9 @@ struct ParseU {                     // wave-uniform parse output state
 };
 
 __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job) {
-    __shared__ uint32_t s_rf[kPT];
-    __shared__ uint32_t s_rq[kPT];
-    __shared__ uint8_t s_in[kPT + 4];
+    __shared__ __attribute__((aligned(16))) uint32_t s_rf[kPT];
+    __shared__ __attribute__((aligned(16))) uint32_t s_rq[kPT];
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[kPT + 16];   // in[t0-16 .. t0+kPT)
     const int lane = threadIdx.x;
     const uint32_t bi = blockIdx.x;
     const uint32_t g = job.first + bi;
@@ -335,15 +421,9 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job) {
 
     uint32_t t0 = 0;
     while (!done) {
-        for (int j = lane; j < kPT; j += 64) {
-            const uint32_t q = t0 + j;
-            s_rf[j] = q < n ? rf[q] : 0;
-            if (use_q) s_rq[j] = q < n ? rq[q] : 0;
-        }
-        for (int j = lane; j < kPT + 1; j += 64) {
-            const int64_t q = (int64_t)t0 - 1 + j;
-            s_in[j] = (q >= 0 && q < (int64_t)n) ? in[q] : 0;
-        }
+        stage_words<64, kPT / 4 / 64>(s_rf, rf, t0, kPT, n, lane);
+        if (use_q) stage_words<64, kPT / 4 / 64>(s_rq, rq, t0, kPT, n, lane);
+        stage_bytes<64, (kPT + 16) / 16 / 64 + 1>(s_in, in, (int64_t)t0 - 16, kPT + 16, n, lane);
         __syncthreads();
         const bool tile_to_end = (uint64_t)t0 + kPT >= n;
         for (;;) {
@@ -366,7 +446,7 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job) {
                     while (a < b) {
                         const uint32_t room = kSymLimit - po.blk_nsym;
                         const uint32_t take = (b - a) < room ? (b - a) : room;
-                        if ((uint32_t)lane < take) po.sym[po.nsym + lane] = s_in[a + lane - t0 + 1];
+                        if ((uint32_t)lane < take) po.sym[po.nsym + lane] = s_in[a + lane - t0 + 16];
                         po.nsym += take;
                         po.blk_nsym += take;
                         a += take;
@@ -397,7 +477,7 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job) {
                 match_length = kMinMatch - 1;
                 if (bflush) po.flush(p, false, lane);
             } else if (avail) {
-                const uint32_t lit = ufl(s_in[p - t0]);
+                const uint32_t lit = ufl(s_in[p - 1 - t0 + 16]);
                 if (po.tally1(lit, lane)) po.flush(p, false, lane);
                 p++;
             } else {
@@ -406,11 +486,11 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job) {
             }
         }
         if (done) {
-            if (avail) po.tally1(ufl(s_in[p - t0]), lane);
+            if (avail) po.tally1(ufl(s_in[p - 1 - t0 + 16]), lane);
             po.flush(p, true, lane);
             if (lane == 0) job.nblocks[bi] = po.nblk;
         }
-        t0 = p;
+        t0 = p & ~15u;
         __syncthreads();
     }
 }
