@@ -200,7 +200,7 @@ struct Ctx {
     std::string info;
     CrcTables *d_crc = nullptr;
     size_t inflight = size_t(1) << 30;
-    DevBuf ws_link, ws_rf, ws_rq, ws_sym, ws_blk, ws_meta, ws_heads, ws_io, ws_io2, ws_small;
+    DevBuf ws_link, ws_rf, ws_rq, ws_sym, ws_blk, ws_meta, ws_heads, ws_io, ws_io2, ws_small, ws_bits;
 };
 
 Ctx &ctx() {
@@ -296,6 +296,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     if (!c.ws_sym.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
     if (!c.ws_blk.ensure(sizeof(BlockRec) * max_blk)) return ZGPU_MEM_ERROR;
     if (slow && !c.ws_rf.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
+    if (slow && !c.ws_bits.ensure(max_pos + 64)) return ZGPU_MEM_ERROR;
     if (quarter && !c.ws_rq.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
     if (level >= 1 && level <= 3 && !c.ws_heads.ensure(4ull * 32768 * max_cnt)) return ZGPU_MEM_ERROR;
     uint64_t *d_meta = c.ws_meta.as<uint64_t>();
@@ -320,6 +321,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         job.blocks = c.ws_blk.as<BlockRec>();
         job.nblocks = d_nblk;
         job.check = d_check;
+        job.pbits = c.ws_bits.as<uint32_t>();
         StageTimer &T = c.timer;
         int rc = 0;
         if (wrap == 1)
@@ -330,7 +332,8 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         if (level >= 4) {
             if (T.run(1, st, [&] { return launch_deflate_stage(0, job, nullptr, st); })) return ZGPU_MEM_ERROR;
             if (T.run(2, st, [&] { return launch_deflate_stage(1, job, nullptr, st); })) return ZGPU_MEM_ERROR;
-            if (T.run(3, st, [&] { return launch_deflate_stage(2, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+            if (T.run(3, st, [&] { return launch_deflate_stage(5, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+            if (T.run(3, st, [&] { return launch_deflate_stage(6, job, nullptr, st); })) return ZGPU_MEM_ERROR;
         } else if (level >= 1) {
             uint32_t *heads = c.ws_heads.as<uint32_t>();
             if (T.run(4, st, [&] { return launch_deflate_stage(3, job, heads, st); })) return ZGPU_MEM_ERROR;

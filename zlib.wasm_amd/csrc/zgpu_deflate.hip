@@ -17,10 +17,14 @@
 //                              (trees.c:997-1089), parallel bit packing through an
 //                              LDS staging window; zlib/gzip framing + trailer
 #include "zgpu_internal.h"
+#include <cstdlib>
 
 namespace zgpu {
 
 __constant__ CodeTables c_ct;
+
+// nblocks value a segmented parse leaves for buffers it hands to k_parse_slow
+constexpr uint32_t kParseFallback = 0xffffffffu;
 
 // ------------------------------------------------------------------------
 // small helpers
@@ -203,6 +207,126 @@ __device__ inline uint32_t get4(const uint32_t *E, int i) {      // bytes i..i+3
     return (E[i] >> 16) | (E[i + 2] & 0xffff0000u);
 }
 
+// Tile load: E[i] for window positions [ts-kMW, ts+kMT+kMPad); the first
+// tile loads everything, later tiles slide the window down by kMT words.
+__device__ __attribute__((always_inline)) inline void match_tile_load(uint32_t *E, int64_t ts, int64_t n,
+                                                                      const uint8_t *in, const uint16_t *L,
+                                                                      int tid) {
+    const int64_t B = ts - kMW;
+    auto word = [&](int64_t q, bool with_link) -> uint32_t {
+        uint32_t w = 0;
+        if (q >= 0 && q < n) {
+            w = (uint32_t)in[q] << 16;
+            if (q + 1 < n) w |= (uint32_t)in[q + 1] << 24;
+            if (with_link) w |= L[q];
+        }
+        return w;
+    };
+    if (ts == 0) {
+        for (int i = tid; i < kME; i += kMatchThreads) E[i] = word(B + i, i < kMW + kMT);
+        return;
+    }
+    // kMT/4 uint4 chunks == kMatchThreads, so thread t only ever touches
+    // chunks = t (mod kMatchThreads): moving them in increasing order needs no
+    // barrier and no staging.
+    static_assert(kMT / 4 == kMatchThreads, "slide assumes kMT/4 == threads");
+    constexpr int kChunks = (kME - kMT) / 4;
+    uint4 *dE = reinterpret_cast<uint4 *>(E);
+    for (int c = tid; c < kChunks; c += kMatchThreads) dE[c] = dE[c + kMT / 4];
+    __syncthreads();
+    // words [kMW, kME): the slid part (pad of the last tile) still needs its
+    // links, [kME-kMT, kME) are new; one pass, no overlap race
+    for (int i = tid; i < kME - kMW; i += kMatchThreads) {
+        const int idx = kMW + i;
+        const int64_t q = ts + i;
+        if (idx >= kME - kMT) E[idx] = word(q, i < kMT);
+        else if (i < kMT && q < n) E[idx] |= L[q];
+    }
+}
+
+// One position's longest_match walk (deflate.c:1356-1497) over the packed
+// window, split into init / candidate-load / candidate-step so that several
+// walks per lane can have their LDS reads in flight together.
+struct MWalk {
+    int64_t p;
+    int s, m, best, bpos, bestq, bposq, limit, nice, maxcmp;
+    uint32_t count, scan01, scan_end, S0, S1, S2, S3;
+    bool snapped;
+};
+
+// false: no valid hash head (results already stored)
+__device__ __attribute__((always_inline)) inline bool mwalk_init(MWalk &w, const uint32_t *E, int64_t p,
+                                                                 int64_t B, int64_t n, const LevelCfg &cfg,
+                                                                 uint32_t *rf, uint32_t *rq, int want_q) {
+    w.p = p;
+    w.s = (int)(p - B);
+    const uint32_t e0 = E[w.s];
+    const uint32_t d0 = e0 & 0xffffu;
+    if (d0 == 0 || d0 > (uint32_t)kMaxDist) {
+        rf[p] = 0;
+        if (want_q) rq[p] = 0;
+        return false;
+    }
+    const int64_t labs = p > kMaxDist ? p - kMaxDist : 0;
+    w.limit = (int)(labs - B);
+    const int64_t rem = n - p;
+    w.nice = rem < cfg.nice ? (int)rem : cfg.nice;
+    w.maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
+    w.S0 = get4(E, w.s); w.S1 = get4(E, w.s + 4); w.S2 = get4(E, w.s + 8); w.S3 = get4(E, w.s + 12);
+    w.scan01 = e0 >> 16;
+    w.best = kMinMatch - 1; w.bpos = 0; w.bestq = 0; w.bposq = 0; w.snapped = false;
+    w.scan_end = (w.S0 >> 8) & 0xffffu;
+    w.m = w.s - (int)d0;
+    w.count = 0;
+    return true;
+}
+
+// consume one candidate whose two words were loaded; true when the walk ends
+__device__ __attribute__((always_inline)) inline bool mwalk_step(MWalk &w, const uint32_t *E, uint32_t em,
+                                                                 uint32_t eb, const LevelCfg &cfg,
+                                                                 uint32_t *rf, uint32_t *rq, int want_q) {
+    w.count++;
+    bool stop = false;
+    if ((em >> 16) == w.scan01 && eb == w.scan_end) {
+        const int m = w.m, s = w.s;
+        int k;
+        uint32_t x = get4(E, m) ^ w.S0;
+        if (x) k = __builtin_ctz(x) >> 3;
+        else if ((x = get4(E, m + 4) ^ w.S1)) k = 4 + (__builtin_ctz(x) >> 3);
+        else if ((x = get4(E, m + 8) ^ w.S2)) k = 8 + (__builtin_ctz(x) >> 3);
+        else if ((x = get4(E, m + 12) ^ w.S3)) k = 12 + (__builtin_ctz(x) >> 3);
+        else {
+            k = 16;
+            while (k < w.maxcmp) {
+                x = get4(E, s + k) ^ get4(E, m + k);
+                if (x) { k += __builtin_ctz(x) >> 3; break; }
+                k += 4;
+            }
+        }
+        const int len = k < w.maxcmp ? k : w.maxcmp;
+        if (len > w.best) {
+            w.best = len;
+            w.bpos = m;
+            if (len >= w.nice) stop = true;
+            else w.scan_end = E[s + w.best - 1] >> 16;
+        }
+    }
+    if (w.count == (uint32_t)(cfg.chain >> 2)) { w.bestq = w.best; w.bposq = w.bpos; w.snapped = true; }
+    const uint32_t d = em & 0xffffu;
+    const int nm = w.m - (int)d;
+    if (stop || w.count >= cfg.chain || d == 0 || nm <= w.limit) {
+        if (!w.snapped) { w.bestq = w.best; w.bposq = w.bpos; }
+        rf[w.p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)(w.s - w.bpos)) : 0u;
+        if (want_q) rq[w.p] = w.bestq >= kMinMatch ? (((uint32_t)w.bestq << 16) | (uint32_t)(w.s - w.bposq)) : 0u;
+        return true;
+    }
+    w.m = nm;
+    return false;
+}
+
+// kVariant 0: one walk per position, lanes take positions from a ticket.
+// kVariant 1: candidate-flattened, 1 walk per lane, refill on completion.
+// kVariant 2: candidate-flattened, 2 interleaved walks per lane.
 template <int kVariant>
 __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int want_q) {
     __shared__ __attribute__((aligned(16))) uint32_t E[kME];
@@ -216,104 +340,87 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
     uint32_t *rf = job.rfull + job.ws_off[bi];
     uint32_t *rq = job.rquart + job.ws_off[bi];
     const LevelCfg cfg = c_ct.cfg[job.level];
-    const uint32_t chain = cfg.chain, bq = cfg.chain >> 2;
-
-    auto word = [&](int64_t q, bool with_link) -> uint32_t {
-        uint32_t w = 0;
-        if (q >= 0 && q < n) {
-            w = (uint32_t)in[q] << 16;
-            if (q + 1 < n) w |= (uint32_t)in[q + 1] << 24;
-            if (with_link) w |= L[q];
-        }
-        return w;
-    };
 
     for (int64_t ts = 0; ts < n; ts += kMT) {
         const int64_t B = ts - kMW;
-        if (ts == 0) {
-            for (int i = tid; i < kME; i += kMatchThreads) E[i] = word(B + i, i < kMW + kMT);
-        } else {
-            // slide down by kMT words.  kMT/4 uint4 chunks == kMatchThreads, so
-            // thread t only ever touches chunks = t (mod kMatchThreads): moving
-            // them in increasing order needs no barrier and no staging.
-            static_assert(kMT / 4 == kMatchThreads, "slide assumes kMT/4 == threads");
-            constexpr int kChunks = (kME - kMT) / 4;
-            uint4 *dE = reinterpret_cast<uint4 *>(E);
-            for (int c = tid; c < kChunks; c += kMatchThreads) dE[c] = dE[c + kMT / 4];
-            __syncthreads();
-            // words [kMW, kME): the slid part (pad of the last tile) still needs
-            // its links, [kME-kMT, kME) are new; one pass, no overlap race
-            for (int i = tid; i < kME - kMW; i += kMatchThreads) {
-                const int idx = kMW + i;
-                const int64_t q = ts + i;
-                if (idx >= kME - kMT) E[idx] = word(q, i < kMT);
-                else if (i < kMT && q < n) E[idx] |= L[q];
-            }
-        }
+        match_tile_load(E, ts, n, in, L, tid);
         if (tid == 0) next_i = 0;
         __syncthreads();
-
-        for (;;) {
-            const int i = atomicAdd(&next_i, 1);
-            const int64_t p = ts + i;
-            if (i >= kMT || p >= n) break;
-            const int s = (int)(p - B);
-            const uint32_t e0 = E[s];
-            const uint32_t d0 = e0 & 0xffffu;
-            uint32_t r_full = 0, r_q = 0;
-            if (d0 != 0 && d0 <= (uint32_t)kMaxDist) {
-                const int64_t labs = p > kMaxDist ? p - kMaxDist : 0;
-                const int limit = (int)(labs - B);
-                const int64_t rem = n - p;
-                const int nice = rem < cfg.nice ? (int)rem : cfg.nice;
-                const int maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
-                const uint32_t S0 = get4(E, s), S1 = get4(E, s + 4), S2 = get4(E, s + 8), S3 = get4(E, s + 12);
-                const uint32_t scan01 = e0 >> 16;
-                int best = kMinMatch - 1, bpos = 0, bestq = 0, bposq = 0;
-                bool snapped = false;
-                uint32_t scan_end = (S0 >> 8) & 0xffffu;
-                int m = s - (int)d0;
-                uint32_t count = 0;
+        if (kVariant == 0) {
+            for (;;) {
+                const int i = atomicAdd(&next_i, 1);
+                const int64_t p = ts + i;
+                if (i >= kMT || p >= n) break;
+                MWalk w;
+                if (!mwalk_init(w, E, p, B, n, cfg, rf, rq, want_q)) continue;
                 for (;;) {
-                    const uint32_t em = E[m];                       // link + bytes m, m+1
-                    const uint32_t eb = E[m + best - 1] >> 16;      // bytes m+best-1, m+best
-                    count++;
-                    bool stop = false;
-                    if ((em >> 16) == scan01 && eb == scan_end) {
-                        int k;
-                        uint32_t x = get4(E, m) ^ S0;
-                        if (x) k = __builtin_ctz(x) >> 3;
-                        else if ((x = get4(E, m + 4) ^ S1)) k = 4 + (__builtin_ctz(x) >> 3);
-                        else if ((x = get4(E, m + 8) ^ S2)) k = 8 + (__builtin_ctz(x) >> 3);
-                        else if ((x = get4(E, m + 12) ^ S3)) k = 12 + (__builtin_ctz(x) >> 3);
-                        else {
-                            k = 16;
-                            while (k < maxcmp) {
-                                x = get4(E, s + k) ^ get4(E, m + k);
-                                if (x) { k += __builtin_ctz(x) >> 3; break; }
-                                k += 4;
-                            }
-                        }
-                        const int len = k < maxcmp ? k : maxcmp;
-                        if (len > best) {
-                            best = len;
-                            bpos = m;
-                            if (len >= nice) stop = true;
-                            else scan_end = E[s + best - 1] >> 16;
-                        }
-                    }
-                    if (count == bq) { bestq = best; bposq = bpos; snapped = true; }
-                    const uint32_t d = em & 0xffffu;
-                    const int nm = m - (int)d;
-                    if (stop || count >= chain || d == 0 || nm <= limit) break;
-                    m = nm;
+                    const uint32_t em = E[w.m];
+                    const uint32_t eb = E[w.m + w.best - 1] >> 16;
+                    if (mwalk_step(w, E, em, eb, cfg, rf, rq, want_q)) break;
                 }
-                if (!snapped) { bestq = best; bposq = bpos; }
-                if (best >= kMinMatch) r_full = ((uint32_t)best << 16) | (uint32_t)(s - bpos);
-                if (bestq >= kMinMatch) r_q = ((uint32_t)bestq << 16) | (uint32_t)(s - bposq);
             }
-            rf[p] = r_full;
-            if (want_q) rq[p] = r_q;
+        } else if (kVariant == 1) {
+            MWalk w;
+            bool have = false, exhausted = false;
+            for (;;) {
+                while (!have && !exhausted) {
+                    const int i = atomicAdd(&next_i, 1);
+                    if (i >= kMT || ts + i >= n) { exhausted = true; break; }
+                    have = mwalk_init(w, E, ts + i, B, n, cfg, rf, rq, want_q);
+                }
+                if (!__any(have)) break;
+                if (have) {
+                    const uint32_t em = E[w.m];
+                    const uint32_t eb = E[w.m + w.best - 1] >> 16;
+                    if (mwalk_step(w, E, em, eb, cfg, rf, rq, want_q)) have = false;
+                }
+            }
+        } else if (kVariant >= 10) {
+            // batched refill: walks stay in lockstep; idle lanes take new
+            // (consecutive) positions only once at most kVariant lanes are busy
+            MWalk w;
+            bool have = false, exhausted = false;
+            for (;;) {
+                if (!have && !exhausted) {
+                    const int i = atomicAdd(&next_i, 1);
+                    if (i >= kMT || ts + i >= n) exhausted = true;
+                    else have = mwalk_init(w, E, ts + i, B, n, cfg, rf, rq, want_q);
+                }
+                if (!__any(have)) {
+                    if (__all(exhausted)) break;
+                    continue;
+                }
+                for (;;) {
+                    if (have) {
+                        const uint32_t em = E[w.m];
+                        const uint32_t eb = E[w.m + w.best - 1] >> 16;
+                        if (mwalk_step(w, E, em, eb, cfg, rf, rq, want_q)) have = false;
+                    }
+                    const int busy = __popcll(__ballot(have));
+                    if (busy == 0 || (busy <= kVariant && !__all(exhausted || have))) break;
+                }
+            }
+        } else {
+            MWalk a, b;
+            bool ha = false, hb = false, exhausted = false;
+            for (;;) {
+                while (!ha && !exhausted) {
+                    const int i = atomicAdd(&next_i, 1);
+                    if (i >= kMT || ts + i >= n) { exhausted = true; break; }
+                    ha = mwalk_init(a, E, ts + i, B, n, cfg, rf, rq, want_q);
+                }
+                while (!hb && !exhausted) {
+                    const int i = atomicAdd(&next_i, 1);
+                    if (i >= kMT || ts + i >= n) { exhausted = true; break; }
+                    hb = mwalk_init(b, E, ts + i, B, n, cfg, rf, rq, want_q);
+                }
+                if (!__any(ha || hb)) break;
+                const int ma = ha ? a.m : 0, mb = hb ? b.m : 0;
+                const uint32_t ema = E[ma], eba = E[ma + (ha ? a.best - 1 : 0)] >> 16;
+                const uint32_t emb = E[mb], ebb = E[mb + (hb ? b.best - 1 : 0)] >> 16;
+                if (ha && mwalk_step(a, E, ema, eba, cfg, rf, rq, want_q)) ha = false;
+                if (hb && mwalk_step(b, E, emb, ebb, cfg, rf, rq, want_q)) hb = false;
+            }
         }
         __syncthreads();
     }
@@ -396,7 +503,7 @@ struct ParseU {                     // wave-uniform parse output state
     }
 };
 
-__global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job) {
+__global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flagged) {
     __shared__ __attribute__((aligned(16))) uint32_t s_rf[kPT];
     __shared__ __attribute__((aligned(16))) uint32_t s_rq[kPT];
     __shared__ __attribute__((aligned(16))) uint8_t s_in[kPT + 16];   // in[t0-16 .. t0+kPT)
@@ -410,6 +517,7 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job) {
     const LevelCfg cfg = c_ct.cfg[job.level];
     const bool use_q = cfg.good < cfg.lazy;
     const uint32_t lazy = cfg.lazy, good = cfg.good;
+    if (only_flagged && job.nblocks[bi] != kParseFallback) return;
 
     ParseU po;
     po.sym = job.sym + job.ws_off[bi];
@@ -493,6 +601,278 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job) {
         t0 = p & ~15u;
         __syncthreads();
     }
+}
+
+// ------------------------------------------------------------------------
+// k_parse_seg — deflate_slow parsed by 64 lanes at once (levels 4..9).
+//
+// The lazy parse is a deterministic state machine over decision points whose
+// state is (match_length, match_start, match_available).  Whenever
+// match_length < MIN_MATCH the state is "simple" and fully described by
+// match_available.  The buffer is cut into <= 64 segments; lane i parses its
+// segment from the simple state (.., avail=0), recording in a bitmap every
+// position where it stood in a simple state (per lane parity).  Lane i then
+// runs on into segment i+1 until it stands at a position in the same simple
+// state lane i+1 recorded there: from that point the two parses coincide, so
+// the true parse is lane 0 on [0,y0), lane 1 on [y0,y1), ...  A count pass and
+// a wave prefix sum give each lane its first symbol index; an emit pass writes
+// the symbols in place, the block cuts (every 16383 symbols, deflate.h:371)
+// and the fill_window slide points needed for the stored-block test
+// (FLUSH_BLOCK_ONLY's block_start >= 0, deflate.c:1597-1600).  A buffer whose
+// lanes fail to meet is flagged (nblocks = ~0) for k_parse_slow.
+// ------------------------------------------------------------------------
+constexpr int kSegMin = 4096;
+constexpr int kSegMaxBlk = 1100;      // buffers up to ~18 MB; larger use k_parse_slow
+constexpr int kSegMaxThr = 1024;
+constexpr uint32_t kEnd = 0xffffffffu;
+
+struct WCache {
+    uint32_t base;
+    uint32_t x, y, z, w;       // four separate registers: no indexable array
+};
+__device__ __attribute__((always_inline)) inline uint32_t sel4(uint32_t x, uint32_t y, uint32_t z,
+                                                               uint32_t w, uint32_t k) {
+    const uint32_t lo = (k & 1u) ? y : x, hi = (k & 1u) ? w : z;
+    return (k & 2u) ? hi : lo;
+}
+__device__ __attribute__((always_inline)) inline uint32_t wget(const uint32_t *a, uint32_t p, WCache &c) {
+    const uint32_t b = p & ~3u;
+    if (b != c.base) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(a + b);
+        c.x = v.x; c.y = v.y; c.z = v.z; c.w = v.w;
+        c.base = b;
+    }
+    return sel4(c.x, c.y, c.z, c.w, p & 3u);
+}
+struct BCache {
+    uintptr_t base;
+    uint32_t x, y, z, w;
+};
+__device__ __attribute__((always_inline)) inline uint32_t bget(const uint8_t *in, uint32_t x, BCache &c) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(in + x);
+    const uintptr_t b = a & ~(uintptr_t)15;
+    if (b != c.base) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(b);
+        c.x = v.x; c.y = v.y; c.z = v.z; c.w = v.w;
+        c.base = b;
+    }
+    const uint32_t o = (uint32_t)(a - b);
+    return (sel4(c.x, c.y, c.z, c.w, o >> 2) >> (8 * (o & 3u))) & 0xffu;
+}
+
+struct SlowLane {
+    uint32_t p, ml, ms, avail;
+    WCache cf, cq;
+    BCache cb;
+};
+
+// one deflate_slow decision (deflate.c:1946-2027) on precomputed results.
+// Returns 0 (no symbol), 1 (literal at spos), 2 (match starting at spos, len).
+__device__ __attribute__((always_inline)) inline int slow_step(SlowLane &L, uint32_t n, const uint32_t *rf, const uint32_t *rq,
+                                const uint8_t *in, const LevelCfg &cfg, bool use_q, uint32_t &sym,
+                                uint32_t &spos, uint32_t &slen) {
+    const uint32_t p = L.p;
+    const uint32_t prev_length = L.ml, prev_match = L.ms;
+    uint32_t ml = kMinMatch - 1;
+    if (n - p >= (uint32_t)kMinMatch && prev_length < cfg.lazy) {
+        const uint32_t r = (use_q && prev_length >= cfg.good) ? wget(rq, p, L.cq) : wget(rf, p, L.cf);
+        const uint32_t rl = r >> 16;
+        if (rl > prev_length) {
+            ml = rl;
+            L.ms = p - (r & 0xffffu);
+            if (ml == (uint32_t)kMinMatch && p - L.ms > (uint32_t)kTooFar) ml = kMinMatch - 1;
+        }
+    }
+    if (prev_length >= (uint32_t)kMinMatch && ml <= prev_length) {
+        sym = ((p - 1 - prev_match) << 8) | (prev_length - kMinMatch);
+        spos = p - 1;
+        slen = prev_length;
+        L.p = p + prev_length - 1;
+        L.avail = 0;
+        L.ml = kMinMatch - 1;
+        return 2;
+    }
+    L.ml = ml;
+    if (L.avail) {
+        sym = bget(in, p - 1, L.cb);
+        spos = p - 1;
+        slen = 1;
+        L.p = p + 1;
+        return 1;
+    }
+    L.avail = 1;
+    L.p = p + 1;
+    return 0;
+}
+
+// p at which the k-th window slide (k >= 1) becomes due: fill_window is called
+// when lookahead < MIN_LOOKAHEAD and slides when strstart >= WSIZE+MAX_DIST
+// (deflate.c:277); with all input present the window end is min(n, S + 64K).
+__device__ inline int64_t slide_threshold(uint32_t k, uint32_t n) {
+    const int64_t S = (int64_t)kWSize * (k - 1);
+    if ((int64_t)n > S + 2 * kWSize) return S + kWSize + kMaxDist + 1;
+    const int64_t a = (int64_t)n - (kMinLookahead - 1), b = S + kWSize + kMaxDist;
+    return a > b ? a : b;
+}
+
+__device__ __attribute__((always_inline)) inline void lane_init(SlowLane &L, uint32_t p, uint32_t avail) {
+    L.p = p; L.ml = kMinMatch - 1; L.ms = 0; L.avail = avail;
+    L.cf.base = L.cq.base = 0xffffffffu;
+    L.cb.base = ~(uintptr_t)0;
+}
+
+__global__ __launch_bounds__(64) void k_parse_seg(DeflateJob job) {
+    __shared__ uint32_t s_y[65], s_sig[65], s_cnt[64];
+    __shared__ int s_fail, s_final_lit;
+    __shared__ uint32_t s_blk_end[kSegMaxBlk], s_blk_pd[kSegMaxBlk];
+    __shared__ uint32_t s_trig[kSegMaxThr];
+    const int lane = threadIdx.x;
+    const uint32_t bi = blockIdx.x;
+    const uint32_t g = job.first + bi;
+    const uint32_t n = (uint32_t)job.src_len[g];
+    const uint8_t *in = job.src + job.src_off[g];
+    const uint32_t *rf = job.rfull + job.ws_off[bi];
+    const uint32_t *rq = job.rquart + job.ws_off[bi];
+    uint32_t *bits = job.pbits + (job.ws_off[bi] >> 2);
+    uint32_t *sym = job.sym + job.ws_off[bi];
+    BlockRec *blk = job.blocks + job.blk_off[bi];
+    const LevelCfg cfg = c_ct.cfg[job.level];
+    const bool use_q = cfg.good < cfg.lazy;
+
+    if ((uint64_t)n / kSymLimit + 2 > (uint64_t)kSegMaxBlk || (uint64_t)n / kWSize + 2 > (uint64_t)kSegMaxThr) {
+        if (lane == 0) job.nblocks[bi] = kParseFallback;
+        return;
+    }
+    uint32_t nseg = (n + kSegMin - 1) / kSegMin;
+    nseg = nseg < 1 ? 1 : nseg > 64 ? 64 : nseg;
+    const uint32_t seg = (((n + nseg - 1) / nseg) + 15u) & ~15u;
+    auto xb = [&](uint32_t i) -> uint32_t { uint64_t v = (uint64_t)i * seg; return v < n ? (uint32_t)v : n; };
+    const bool active = (uint32_t)lane < nseg;
+    const uint32_t par = lane & 1;
+
+    for (uint32_t w = lane; w < (n >> 2) + 1; w += 64) bits[w] = 0;
+    if (lane == 0) { s_fail = 0; s_final_lit = 0; }
+    __threadfence();
+    __syncthreads();
+
+    // ---- pass 1: speculative parse of the own segment, record simple states
+    SlowLane L;
+    uint32_t sym_v, spos, slen;
+    lane_init(L, xb(lane), 0);
+    const uint32_t seg_end = (uint32_t)lane + 1 >= nseg ? n : xb(lane + 1);
+    if (active) {
+        while (L.p < seg_end) {
+            if (L.ml < (uint32_t)kMinMatch)
+                atomicOr(&bits[L.p >> 2], 1u << (8 * (L.p & 3u) + 2 * par + L.avail));
+            slow_step(L, n, rf, rq, in, cfg, use_q, sym_v, spos, slen);
+        }
+    }
+    __threadfence();
+    __syncthreads();
+
+    // ---- pass 2: run on until the parse meets lane+1's recorded state
+    uint32_t y = kEnd, sig = 0;
+    if (active && (uint32_t)lane + 1 < nseg) {
+        const uint32_t next_start = xb(lane + 1);
+        const uint32_t stop = (uint32_t)lane + 2 >= nseg ? n : xb(lane + 2);
+        for (;;) {
+            if (L.p >= n) { y = kEnd; break; }
+            if (L.p >= stop) { atomicOr(&s_fail, 1); break; }
+            if (L.p >= next_start && L.ml < (uint32_t)kMinMatch) {
+                const uint32_t wv = __hip_atomic_load(&bits[L.p >> 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((wv >> (8 * (L.p & 3u) + 2 * (par ^ 1u) + L.avail)) & 1u) { y = L.p; sig = L.avail; break; }
+            }
+            slow_step(L, n, rf, rq, in, cfg, use_q, sym_v, spos, slen);
+        }
+    }
+    s_y[lane] = active ? y : kEnd;
+    s_sig[lane] = sig;
+    __syncthreads();
+    if (s_fail) {
+        if (lane == 0) job.nblocks[bi] = kParseFallback;
+        return;
+    }
+    // lane i parses [start, end): start = y[i-1] (lane 0: 0), end = y[i] (kEnd: to n)
+    bool mine = active;
+    uint32_t start = 0, start_av = 0;
+    if (lane > 0) {
+        for (int j = 0; j < lane; j++) if (s_y[j] == kEnd) mine = false;
+        start = s_y[lane - 1];
+        start_av = s_sig[lane - 1];
+    }
+    const uint32_t yend = s_y[lane];
+    const uint32_t end = yend == kEnd ? n : yend;
+
+    // ---- pass 3: count symbols
+    uint32_t cnt = 0;
+    if (mine) {
+        lane_init(L, start, start_av);
+        while (L.p < end)
+            if (slow_step(L, n, rf, rq, in, cfg, use_q, sym_v, spos, slen)) cnt++;
+        if (yend == kEnd && L.avail) cnt++;
+    }
+    // exclusive wave prefix sum
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    const uint32_t base = incl - cnt;
+    const uint32_t total = __shfl(incl, 63, 64);
+
+    // ---- pass 4: emit symbols at their final index, block ends, slide points
+    uint32_t nthr = 0;
+    while (nthr < (uint32_t)kSegMaxThr && slide_threshold(nthr + 1, n) <= (int64_t)n) nthr++;
+    if (mine) {
+        lane_init(L, start, start_av);
+        uint32_t gidx = base;
+        uint32_t k = 0;
+        while (k < nthr && slide_threshold(k + 1, n) < (int64_t)start) k++;
+        while (L.p < end) {
+            while (k < nthr && slide_threshold(k + 1, n) <= (int64_t)L.p) s_trig[k++] = L.p;
+            const int t = slow_step(L, n, rf, rq, in, cfg, use_q, sym_v, spos, slen);
+            if (t) {
+                sym[gidx] = sym_v;
+                if ((gidx + 1) % (uint32_t)kSymLimit == 0) {
+                    const uint32_t b = (gidx + 1) / kSymLimit - 1;
+                    s_blk_end[b] = spos + slen;
+                    s_blk_pd[b] = spos + 1;
+                }
+                gidx++;
+            }
+        }
+        if (yend == kEnd) {
+            while (k < nthr && slide_threshold(k + 1, n) <= (int64_t)n) s_trig[k++] = n;
+            if (L.avail) {                      // final pending literal: no flush test
+                sym[gidx++] = bget(in, n - 1, L.cb);
+                s_final_lit = 1;
+            }
+        } else {
+            while (k < nthr && slide_threshold(k + 1, n) < (int64_t)end) s_trig[k++] = end;
+        }
+    }
+    __syncthreads();
+
+    // ---- block records
+    const uint32_t ncut = total / kSymLimit - ((s_final_lit && total % kSymLimit == 0) ? 1u : 0u);
+    for (uint32_t b = lane; b <= ncut; b += 64) {
+        const bool last = b == ncut;
+        const uint32_t in_end = last ? n : s_blk_end[b];
+        const uint32_t pd = last ? n : s_blk_pd[b];
+        const uint32_t in_start = b == 0 ? 0 : s_blk_end[b - 1];
+        uint32_t slides = 0;
+        for (uint32_t j = 0; j < nthr; j++) slides += s_trig[j] <= pd ? 1u : 0u;
+        BlockRec r;
+        r.sym_start = b * kSymLimit;
+        r.nsym = last ? total - b * kSymLimit : (uint32_t)kSymLimit;
+        r.in_start = in_start;
+        r.in_end = in_end;
+        r.flags = (last ? 1u : 0u) | ((uint64_t)in_start >= (uint64_t)kWSize * slides ? 2u : 0u);
+        r.pad = 0;
+        blk[b] = r;
+    }
+    if (lane == 0) job.nblocks[bi] = ncut + 1;
 }
 
 // ------------------------------------------------------------------------
@@ -1058,9 +1438,23 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     const dim3 grid(job.count);
     switch (stage) {
     case 0: hipLaunchKernelGGL(k_links, grid, dim3(64), 0, st, job); break;
-    case 1: hipLaunchKernelGGL(k_match<0>, grid, dim3(kMatchThreads), 0, st, job,
-                               (int)(job.level >= 5)); break;
-    case 2: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job); break;
+    case 1: {
+        static const int variant = [] {
+            const char *e = getenv("ZGPU_MATCH_VARIANT");
+            return e ? atoi(e) : 0;
+        }();
+        const int wq = (int)(job.level >= 5);
+        if (variant == 1) hipLaunchKernelGGL(k_match<1>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        else if (variant == 2) hipLaunchKernelGGL(k_match<2>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        else if (variant == 16) hipLaunchKernelGGL(k_match<16>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        else if (variant == 32) hipLaunchKernelGGL(k_match<32>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        else if (variant == 48) hipLaunchKernelGGL(k_match<48>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        else hipLaunchKernelGGL(k_match<0>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        break;
+    }
+    case 2: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 0); break;
+    case 5: hipLaunchKernelGGL(k_parse_seg, grid, dim3(64), 0, st, job); break;
+    case 6: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 1); break;
     case 3: hipLaunchKernelGGL(k_parse_fast, grid, dim3(64), 0, st, job, heads); break;
     case 4: hipLaunchKernelGGL(k_encode, grid, dim3(kEncThreads), 0, st, job); break;
     default: return -1;

@@ -87,6 +87,7 @@ struct DeflateJob {
     uint32_t *sym;           // [Σn]
     BlockRec *blocks;        // [Σ(n/16383 + 2)]
     uint32_t *nblocks;       // [count]
+    uint32_t *pbits;         // [Σn/4] segmented-parse state bitmap
     uint32_t *check;         // [count] adler32 / crc32 of the input (trailer)
 };
 
@@ -100,7 +101,8 @@ int launch_adler32(const uint8_t *src, const uint64_t *off, const uint64_t *len,
                    const uint32_t *init, uint32_t *out, uint32_t count,
                    void *scratch, size_t scratch_bytes, hipStream_t st);
 size_t checksum_scratch_bytes(uint32_t count);
-// stage: 0 links, 1 match, 2 lazy parse, 3 greedy parse (heads: 128 KiB/buffer), 4 encode
+// stage: 0 links, 1 match, 2 lazy parse (sequential), 3 greedy parse (heads: 128 KiB/buffer),
+//        4 encode, 5 lazy parse (segmented), 6 lazy parse fallback for buffers flagged by 5
 int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipStream_t st);
 int launch_generate(uint8_t *dst, uint64_t len, uint32_t count, int kind, uint64_t seed,
                     uint64_t first_index, hipStream_t st);
