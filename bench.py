@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verify", type=int, default=8, help="outputs checked vs oracle")
+    ap.add_argument("--inflight-mb", type=int, default=4096,
+                    help="input bytes per deflate sub-batch (workspace ~15 B per byte)")
     return ap.parse_args()
 
 
@@ -94,11 +96,18 @@ def reduce_sum(x, world):
     return float(t.item())
 
 
+def shard(rank, world, per_gpu):
+    """Global buffer indices owned by `rank`: a contiguous block of `per_gpu`
+    (weak scaling: per-GPU work is fixed, the job grows with N)."""
+    return rank * per_gpu, (rank + 1) * per_gpu
+
+
 def deflate_leg(a, world, rank):
     n, B = a.buffer_bytes, a.buffers
+    first, _ = shard(rank, world, B)
     cap = (zgpu.compress_bound(n) + 15) // 16 * 16
     src = torch.empty(n * B, dtype=torch.uint8, device="cuda")
-    zgpu.generate_dev(src, n, B, zgpu.KIND_SILESIA, seed=2025, first_index=rank * B)
+    zgpu.generate_dev(src, n, B, zgpu.KIND_SILESIA, seed=2025, first_index=first)
     off = torch.arange(B, dtype=torch.int64, device="cuda") * n
     ln = torch.full((B,), n, dtype=torch.int64, device="cuda")
     dst = torch.empty(cap * B, dtype=torch.uint8, device="cuda")
@@ -130,8 +139,9 @@ def deflate_leg(a, world, rank):
 
 def crc_leg(a, world, rank):
     n, B = a.crc_bytes, a.crc_buffers
+    first, _ = shard(rank, world, B)
     src = torch.empty(n * B, dtype=torch.uint8, device="cuda")
-    zgpu.generate_dev(src, n, B, zgpu.KIND_RANDOM, seed=77, first_index=rank * B)
+    zgpu.generate_dev(src, n, B, zgpu.KIND_RANDOM, seed=77, first_index=first)
     off = torch.arange(B, dtype=torch.int64, device="cuda") * n
     ln = torch.full((B,), n, dtype=torch.int64, device="cuda")
     out = torch.zeros(B, dtype=torch.int32, device="cuda")
@@ -180,6 +190,7 @@ def main():
     world, rank = dist_setup()
     zgpu.load()
     assert zgpu.load().zgpu_init() == 0, "libzgpu: GPU init failed"
+    zgpu.set_inflight_bytes(a.inflight_mb << 20)
 
     d = deflate_leg(a, world, rank)
     c = crc_leg(a, world, rank)
@@ -245,7 +256,7 @@ def main():
             "config": {"workload": f"C4 per-GPU shard: {a.buffers} x {a.buffer_bytes} B buffers, "
                                    f"deflate level {a.level}, zlib wrapper, inputs+outputs in HBM",
                        "level": a.level, "buffer_bytes": a.buffer_bytes,
-                       "buffers_per_gpu": a.buffers,
+                       "buffers_per_gpu": a.buffers, "inflight_mb": a.inflight_mb,
                        "parallelism": f"{world} GPU(s), buffers sharded by index, no data-path collective"},
             "compression_ratio": round(ratio, 4),
             "roofline": {"bound": "hbm", "kernel": "k_match",

@@ -1,0 +1,84 @@
+"""Multi-process (gloo, CPU) test of the benchmark's multi-GPU decomposition:
+buffers are sharded by global index with no data-path collective, and the
+only collectives are the final max(elapsed) / sum(bytes) reductions.  Compute
+is done with the oracle on tiny inputs (no GPU here)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import datagen
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, per_gpu, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from zhelpers import Oracle
+    o = Oracle()
+    lo, hi = bench.shard(rank, world, per_gpu)
+    in_bytes = out_bytes = 0
+    crcs = []
+    for gidx in range(lo, hi):
+        data = datagen.mix(3000 + 17 * gidx, gidx)
+        z = o.compress(data, 6)[1]
+        in_bytes += len(data)
+        out_bytes += len(z)
+        crcs.append(o.crc32(z))
+    t = torch.tensor([float(in_bytes), float(out_bytes)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    el = torch.tensor([0.1 * (rank + 1)], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, (lo, hi, crcs))
+    if rank == 0:
+        q.put((t.tolist(), float(el.item()), gathered))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_batch_matches_single_process(world):
+    per_gpu = 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, per_gpu, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    (tot_in, tot_out), el, gathered = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # shards are disjoint and cover [0, world*per_gpu)
+    idx = sorted(i for lo, hi, _ in gathered for i in range(lo, hi))
+    assert idx == list(range(world * per_gpu))
+    # aggregate equals a single-process pass over the same global batch
+    from zhelpers import Oracle
+    o = Oracle()
+    want_in = want_out = 0
+    want_crc = []
+    for gidx in range(world * per_gpu):
+        data = datagen.mix(3000 + 17 * gidx, gidx)
+        z = o.compress(data, 6)[1]
+        want_in += len(data)
+        want_out += len(z)
+        want_crc.append(o.crc32(z))
+    assert (tot_in, tot_out) == (want_in, want_out)
+    assert [c for _, _, cs in gathered for c in cs] == want_crc
+    assert abs(el - 0.1 * world) < 1e-9
