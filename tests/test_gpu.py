@@ -216,3 +216,22 @@ def test_dropin_zlib_names(zg, oracle):
     assert got == oracle.compress(data, 6, wrap=2)[1]
     z = zg.Zlib().compress(data, level=6)
     assert z.data == oracle.compress(data, 6)[1] and z.originalSize == len(data)
+
+
+def test_crc_adler_many_small_ragged(zg, oracle):
+    """>= 16384 buffers selects the 16-lanes-per-buffer CRC kernel."""
+    rng = np.random.default_rng(11)
+    lens = [int(x) for x in rng.integers(0, 3000, 20000)]
+    lens[:8] = [0, 1, 3, 4, 255, 256, 257, 4096]
+    pool = datagen.random_bytes(sum(lens) + 16, 3)
+    bufs, p = [], 0
+    for n in lens:
+        bufs.append(pool[p:p + n])
+        p += n
+    inits = [int(x) for x in rng.integers(0, 1 << 32, len(bufs), dtype=np.uint64)]
+    got = zg.crc32_batch(bufs, inits)
+    for b, ic, g in zip(bufs, inits, got):
+        assert g == oracle.crc32(b, ic), len(b)
+    got = zg.adler32_batch(bufs)
+    for b, g in zip(bufs, got):
+        assert g == oracle.adler32(b), len(b)

@@ -1,8 +1,8 @@
 // zgpu_checksum.hip — batched CRC-32 and Adler-32 for gfx950.
 //
-// One wave (64 lanes) per buffer.  The buffer is viewed as left-padded with
-// zeros to a multiple of 1 KiB ("rows"); lane i owns the 16-byte chunk at
-// 16*i of every row.  Zero padding in front leaves a zero-init CRC and the
+// G lanes per buffer (64, or 16 for batches of many buffers).  The buffer is
+// viewed as left-padded with zeros to a multiple of 16*G bytes ("rows"); lane i
+// owns the 16-byte chunk at 16*i of every row.  Zero padding in front leaves a zero-init CRC and the
 // Adler sums unchanged, so no lane ever handles a ragged tail.
 //
 // CRC-32 (crc32.c:694-1010): the init value is folded in by XOR-ing ~init into
@@ -10,8 +10,9 @@
 // M from init s equals the zero-init state of M ^ s), so the whole buffer is a
 // single linear (zero-init) CRC R and crc32(init, M) = ~R.  A chunk's CRC is
 // 32 lookups in conflict-free 16-entry nibble tables in LDS; rows are combined
-// per lane by Horner (advance by 1024 zero bytes, 8 lookups), lanes by a 6-level
-// shuffle tree (advance by 16<<l bytes) — crc32_combine (crc32.c:1021) with the
+// per lane by Horner (advance by one row of zero bytes, 8 lookups), lanes by a
+// log2(G)-level shuffle tree (advance by 16<<l bytes) — crc32_combine
+// (crc32.c:1021) with the
 // x^(8n) multipliers pre-tabulated.
 //
 // Adler-32 (adler32.c:61-125): per chunk the byte sum and the position-weighted
@@ -59,19 +60,40 @@ __device__ inline void load_chunk16(const uint8_t *buf, int64_t x, uint64_t L, u
     }
 }
 
-__device__ inline uint32_t crc_shift(uint32_t x, const uint32_t (*t)[16]) {
-    uint32_t y = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) y ^= t[j][(x >> (4 * j)) & 15u];
-    return y;
+// Nibble-table lookups with byte addresses pre-masked: lo/hi hold 4*nibble for
+// the low/high nibble of each byte, so every lookup address is one byte extract.
+__device__ inline uint32_t nib_at(const uint32_t *t, uint32_t addr4) {
+    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(t) + addr4);
 }
 
+// acc ^ XOR of the 8 nibble lookups of word x in tables t[0..7] (16 entries each)
+__device__ inline uint32_t crc_word(uint32_t x, const uint32_t *t, uint32_t acc = 0) {
+    uint32_t lo = (x << 2) & 0x3c3c3c3cu, hi = (x >> 2) & 0x3c3c3c3cu;
+    asm volatile("" : "+v"(lo), "+v"(hi));   // keep the masks: 1 extract per address
+    uint32_t a = nib_at(t + 0 * 16, lo & 0xffu), b = nib_at(t + 1 * 16, hi & 0xffu);
+    uint32_t c = nib_at(t + 2 * 16, (lo >> 8) & 0xffu), d = nib_at(t + 3 * 16, (hi >> 8) & 0xffu);
+    uint32_t e = nib_at(t + 4 * 16, (lo >> 16) & 0xffu), f = nib_at(t + 5 * 16, (hi >> 16) & 0xffu);
+    uint32_t g = nib_at(t + 6 * 16, lo >> 24), h = nib_at(t + 7 * 16, hi >> 24);
+    return ((acc ^ a) ^ (b ^ c)) ^ ((d ^ e) ^ (f ^ g)) ^ h;
+}
+
+__device__ inline uint32_t crc_shift(uint32_t x, const uint32_t (*t)[16]) {
+    return crc_word(x, &t[0][0]);
+}
+
+// G lanes per buffer (16 or 64): a row is 16*G bytes; 64/G buffers per wave.
+// G = 16 halves the lane-combine tree (4 levels, shared by 4 buffers) and is
+// used for batches of many small buffers; G = 64 for few large ones.
+template <int G>
 __global__ __launch_bounds__(kCkBlock) void k_crc32(const uint8_t *__restrict__ src,
                                                     const uint64_t *__restrict__ off,
                                                     const uint64_t *__restrict__ len,
                                                     const uint32_t *__restrict__ init,
                                                     uint32_t *__restrict__ out, uint32_t count,
                                                     const CrcTables *__restrict__ tab) {
+    constexpr int kLog = G == 64 ? 6 : 4;
+    constexpr uint64_t kRow = 16u * G;
+    constexpr uint32_t kPerWave = 64 / G;
     __shared__ uint32_t s_nib[32][16];
     __shared__ uint32_t s_sh[7][8][16];
     __shared__ uint32_t s_byte[256];
@@ -80,9 +102,10 @@ __global__ __launch_bounds__(kCkBlock) void k_crc32(const uint8_t *__restrict__ 
     for (int i = threadIdx.x; i < 256; i += kCkBlock) s_byte[i] = tab->byte[i];
     __syncthreads();
 
-    const int lane = threadIdx.x & 63;
-    const uint32_t wave = threadIdx.x >> 6;
-    for (uint32_t b = blockIdx.x * (kCkBlock / 64) + wave; b < count; b += gridDim.x * (kCkBlock / 64)) {
+    const int lane = threadIdx.x & (G - 1);
+    const uint32_t grp = (threadIdx.x >> 6) * kPerWave + ((threadIdx.x & 63) >> kLog);
+    const uint32_t stride = gridDim.x * (kCkBlock / 64) * kPerWave;
+    for (uint32_t b = blockIdx.x * (kCkBlock / 64) * kPerWave + grp; b < count; b += stride) {
         const uint64_t L = len[b];
         const uint8_t *buf = src + off[b];
         const uint32_t c0 = init ? init[b] : 0u;
@@ -94,11 +117,11 @@ __global__ __launch_bounds__(kCkBlock) void k_crc32(const uint8_t *__restrict__ 
             }
             continue;
         }
-        const uint64_t V = (L + 1023) & ~(uint64_t)1023;
+        const uint64_t V = (L + kRow - 1) & ~(kRow - 1);
         const int64_t pad = (int64_t)(V - L);
         const uint32_t xv = ~c0;
         uint32_t acc = 0;
-        for (uint64_t row = 0; row < V; row += 1024) {
+        for (uint64_t row = 0; row < V; row += kRow) {
             const int64_t x = (int64_t)row + 16 * lane - pad;
             uint32_t w[4];
             load_chunk16(buf, x, L, w);
@@ -109,15 +132,15 @@ __global__ __launch_bounds__(kCkBlock) void k_crc32(const uint8_t *__restrict__ 
                     if (o >= 0 && o < 4) w[j >> 2] ^= ((xv >> (8 * o)) & 0xffu) << (8 * (j & 3));
                 }
             }
-            uint32_t c = 0;
-#pragma unroll
-            for (int j = 0; j < 32; j++) c ^= s_nib[j][(w[j >> 3] >> (4 * (j & 7))) & 15u];
-            acc = crc_shift(acc, s_sh[6]) ^ c;
+            uint32_t c = crc_word(w[0], s_nib[0], crc_shift(acc, s_sh[kLog]));
+            c = crc_word(w[1], s_nib[8], c);
+            c = crc_word(w[2], s_nib[16], c);
+            acc = crc_word(w[3], s_nib[24], c);
         }
 #pragma unroll
-        for (int l = 0; l < 6; l++) {
-            uint32_t other = __shfl_down(acc, 1 << l, 64);
-            acc = crc_shift(acc, s_sh[l]) ^ other;
+        for (int l = 0; l < kLog; l++) {
+            uint32_t other = __shfl_down(acc, 1 << l, G);
+            acc = crc_word(acc, &s_sh[l][0][0], other);
         }
         if (lane == 0) out[b] = ~acc;
     }
@@ -189,8 +212,8 @@ __global__ __launch_bounds__(kCkBlock) void k_adler32(const uint8_t *__restrict_
     }
 }
 
-static int grid_for(uint32_t count) {
-    uint32_t waves = count;
+static int grid_for(uint32_t count, uint32_t per_wave = 1) {
+    uint32_t waves = (count + per_wave - 1) / per_wave;
     uint32_t blocks = (waves + (kCkBlock / 64) - 1) / (kCkBlock / 64);
     if (blocks > 4096) blocks = 4096;
     if (blocks == 0) blocks = 1;
@@ -201,8 +224,13 @@ int launch_crc32(const uint8_t *src, const uint64_t *off, const uint64_t *len,
                  const uint32_t *init, uint32_t *out, uint32_t count,
                  void *, size_t, hipStream_t st) {
     if (count == 0) return 0;
-    hipLaunchKernelGGL(k_crc32, dim3(grid_for(count)), dim3(kCkBlock), 0, st, src, off, len, init,
-                       out, count, device_crc_tables());
+    // 16-lane groups once there are enough buffers to fill the chip 4x over
+    if (count >= 4u * 256u * (kCkBlock / 64) * 4u)
+        hipLaunchKernelGGL(k_crc32<16>, dim3(grid_for(count, 4)), dim3(kCkBlock), 0, st, src, off,
+                           len, init, out, count, device_crc_tables());
+    else
+        hipLaunchKernelGGL(k_crc32<64>, dim3(grid_for(count)), dim3(kCkBlock), 0, st, src, off,
+                           len, init, out, count, device_crc_tables());
     return (int)hipGetLastError();
 }
 
