@@ -15,7 +15,10 @@ buffers, 1/2/4/8 GPU".
 * cpu_baseline: the oracle port (oracle/liboracle.so, our C restatement of the
   reference deflate.c/trees.c) timed on this host's cores on a bounded sample of
   the same buffers; kind "port" (the compiled reference never leaves the build
-  container).
+  container); plus host system zlib on the same sample
+  (`system_zlib`), checked byte-identical first.
+* roofline.traffic: HBM bytes per launch from the committed rocprofv3 PMC
+  passes of the same launch shape (profiles/), FETCH_SIZE x2 + WRITE_SIZE.
 * After timing, a sample of outputs is checked bit-exact against the oracle and
   every status is checked.
 
@@ -162,6 +165,12 @@ def crc_leg(a, world, rank):
     return dict(src=src, out=out, elapsed=el, kernel_ms=kms, bytes=n * B)
 
 
+def launches_tag(a):
+    """Shape of one deflate launch (sub-batch): buffers x bytes."""
+    per = max(1, min(a.buffers, (a.inflight_mb << 20) // a.buffer_bytes))
+    return f"{per}x{a.buffer_bytes}"
+
+
 def cpu_baseline(a, sample, level):
     """Oracle port timed on host cores over a bounded, repeated sample."""
     from zhelpers import Oracle
@@ -185,6 +194,60 @@ def cpu_baseline(a, sample, level):
     return total / el / 1e6, threads, total
 
 
+def system_zlib_baseline(a, sample, level, want):
+    """Host zlib (Python's zlib module: the system libz, GIL released) on the
+    same sample; its output is checked against the GPU streams first."""
+    import zlib
+    for b, z in zip(sample, want):
+        if zlib.compress(b, level) != z:
+            return {"value": None, "version": zlib.ZLIB_RUNTIME_VERSION,
+                    "note": "system zlib output differs from the reference stream; not timed"}
+    threads = max(1, min(a.cpu_threads, os.cpu_count() or 1))
+    deadline = time.perf_counter() + a.cpu_seconds
+
+    def work(tid):
+        done, k = 0, tid
+        while time.perf_counter() < deadline:
+            b = sample[k % len(sample)]
+            zlib.compress(b, level)
+            done += len(b)
+            k += threads
+        return done
+
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as ex:
+        total = sum(ex.map(work, range(threads)))
+    el = time.perf_counter() - t0
+    return {"value": round(total / el / 1e6, 2), "unit": "MB/s", "cores": threads,
+            "version": zlib.ZLIB_RUNTIME_VERSION, "bit_identical_on_sample": True,
+            "sample": f"same {len(sample)} buffers, ~{a.cpu_seconds:.0f} s, {total / 1e6:.0f} MB"}
+
+
+def pmc_traffic(kernel, launch_bytes_hint):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/*_pmc_fetch_*.csv, *_pmc_write_*.csv; FETCH_SIZE doubled per the
+    gfx950 streaming-read correction, units KiB).  Only for profiles taken on
+    this launch's shape (file name carries the shape tag)."""
+    import csv
+    import glob
+    tag = launch_bytes_hint
+    fetch = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_fetch_*{tag}*.csv")))
+    write = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_write_*{tag}*.csv")))
+    if not fetch or not write:
+        return None, None
+
+    def per_launch(path, counter):
+        vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+                if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]]
+        return sum(vals) / len(vals) * 1024.0 if vals else None
+
+    f = per_launch(fetch[-1], "FETCH_SIZE")
+    w = per_launch(write[-1], "WRITE_SIZE")
+    if f is None or w is None:
+        return None, None
+    return 2.0 * f + w, os.path.basename(fetch[-1]) + " + " + os.path.basename(write[-1])
+
+
 def main():
     a = parse()
     world, rank = dist_setup()
@@ -201,12 +264,13 @@ def main():
     h_dlen = d["dlen"].cpu().numpy()
     n = a.buffer_bytes
     idx = sorted(set(int(i) for i in torch.linspace(0, a.buffers - 1, max(1, a.verify)).tolist()))
-    sample = []
+    sample, want = [], []
     for i in idx:
         raw = d["src"][i * n:(i + 1) * n].cpu().numpy().tobytes()
         z = d["dst"][i * d["cap"]: i * d["cap"] + int(h_dlen[i])].cpu().numpy().tobytes()
         assert z == o.compress(raw, a.level)[1], f"buffer {i}: GPU stream != oracle"
         sample.append(raw)
+        want.append(z)
     crc_h = c["out"][:64].cpu().numpy().view("uint32")
     for i in range(64):
         raw = c["src"][i * a.crc_bytes:(i + 1) * a.crc_bytes].cpu().numpy().tobytes()
@@ -233,12 +297,15 @@ def main():
         crc_alg = (a.crc_bytes + 4) * a.crc_buffers
         crc_gbs_kernel = crc_alg / (c["kernel_ms"] / 1e3) / 1e9
         cpu = None
+        m_traffic, m_src = pmc_traffic("k_match", f"L{a.level}_{launches_tag(a)}")
+        c_traffic, c_src = pmc_traffic("k_crc32", f"C2_{a.crc_buffers}x{a.crc_bytes}")
         if not a.no_cpu:
             v, threads, tot = cpu_baseline(a, sample, a.level)
             cpu = {"value": round(v, 2), "unit": "MB/s", "cores": threads, "kind": "port",
                    "sample": f"{len(sample)} distinct 1 MiB Silesia-mix buffers of this batch, "
                              f"compressed repeatedly at level {a.level} for ~{a.cpu_seconds:.0f} s "
-                             f"({tot / 1e6:.0f} MB) by oracle/liboracle.so on {threads} host threads"}
+                             f"({tot / 1e6:.0f} MB) by oracle/liboracle.so on {threads} host threads",
+                   "system_zlib": system_zlib_baseline(a, sample, a.level, want)}
         line = {
             "metric": METRIC,
             "value": round(mbps, 1),
@@ -261,7 +328,9 @@ def main():
             "compression_ratio": round(ratio, 4),
             "roofline": {"bound": "hbm", "kernel": "k_match",
                          "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 6),
+                         "traffic": None if m_traffic is None else int(m_traffic),
+                         "traffic_source": m_src,
                          "alg_bytes_per_launch": int(alg_per_launch),
                          "avg_launch_ms": round(m_avg_ms, 3)},
             "stage_ms_per_step": {k: round(v[0] / max(1, a.steps), 2) for k, v in st.items()},
@@ -270,7 +339,10 @@ def main():
                       "roofline": {"bound": "hbm", "kernel": "k_crc32",
                                    "achieved": round(crc_gbs_kernel, 1), "peak": HBM_PEAK_GBS,
                                    "unit": "GB/s", "frac": round(crc_gbs_kernel / HBM_PEAK_GBS, 4),
-                                   "traffic": None, "avg_launch_ms": round(c["kernel_ms"], 4)}},
+                                   "traffic": None if c_traffic is None else int(c_traffic),
+                                   "traffic_source": c_src,
+                                   "alg_bytes_per_launch": crc_alg,
+                                   "avg_launch_ms": round(c["kernel_ms"], 4)}},
             "verified": {"deflate_buffers_bit_exact_vs_oracle": len(sample),
                          "crc32_values_checked": 64, "all_status_ok": True},
             "cpu_baseline": cpu,
