@@ -207,6 +207,10 @@ __device__ inline uint32_t get4(const uint32_t *E, int i) {      // bytes i..i+3
     return (E[i] >> 16) | (E[i + 2] & 0xffff0000u);
 }
 
+// "no predecessor" (link 0) is stored as 0xffff in LDS: m - 0xffff is always
+// <= the walk's limit, so the chain-end test folds into the limit test.
+__device__ inline uint32_t nil_link(uint32_t l) { return l ? l : 0xffffu; }
+
 // Tile load: E[i] for window positions [ts-kMW, ts+kMT+kMPad); the first
 // tile loads everything, later tiles slide the window down by kMT words.
 __device__ __attribute__((always_inline)) inline void match_tile_load(uint32_t *E, int64_t ts, int64_t n,
@@ -218,7 +222,7 @@ __device__ __attribute__((always_inline)) inline void match_tile_load(uint32_t *
         if (q >= 0 && q < n) {
             w = (uint32_t)in[q] << 16;
             if (q + 1 < n) w |= (uint32_t)in[q + 1] << 24;
-            if (with_link) w |= L[q];
+            if (with_link) w |= nil_link(L[q]);
         }
         return w;
     };
@@ -240,7 +244,7 @@ __device__ __attribute__((always_inline)) inline void match_tile_load(uint32_t *
         const int idx = kMW + i;
         const int64_t q = ts + i;
         if (idx >= kME - kMT) E[idx] = word(q, i < kMT);
-        else if (i < kMT && q < n) E[idx] |= L[q];
+        else if (i < kMT && q < n) E[idx] |= nil_link(L[q]);
     }
 }
 
@@ -324,9 +328,101 @@ __device__ __attribute__((always_inline)) inline bool mwalk_step(MWalk &w, const
     return false;
 }
 
-// kVariant 0: one walk per position, lanes take positions from a ticket.
-// kVariant 1: candidate-flattened, 1 walk per lane, refill on completion.
-// kVariant 2: candidate-flattened, 2 interleaved walks per lane.
+// Variant 3 walk: the candidate loop of longest_match with byte addresses, no
+// chain-end test (nil_link) and the chain/4 snapshot between two loops, so a
+// step is 2 LDS reads, the quick reject, and the link/limit/budget tests.
+struct MW3 {
+    int s4, m4, be4, best, bpos4, limit4, nice, maxcmp;
+    uint32_t count, scan01, scanE;
+};
+
+// The walk used by default (variants 6/7): byte addresses into the packed
+// window, no chain-end test (nil_link), the chain/4 snapshot between two loops
+// (no per-step snapshot test), the next candidate's word loaded before the
+// current one is tested, and both quick-reject pairs tested as one predicate so
+// both loads precede the single branch.  A nice-length stop is folded into the
+// limit test (limit4 = INT_MAX).  Variant 7 unrolls the step loop twice.
+template <int kUnroll>
+__device__ __attribute__((always_inline)) inline bool mw6_loop(MW3 &w, uint32_t &em, const uint32_t *E,
+                                                               uint32_t end) {
+    const char *Eb = reinterpret_cast<const char *>(E);
+#pragma unroll kUnroll
+    for (;;) {
+        const int m4n = w.m4 - (int)((em & 0xffffu) << 2);
+        const uint32_t eb = *reinterpret_cast<const uint32_t *>(Eb + w.m4 + w.be4);
+        const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + (m4n > 0 ? m4n : 0));
+        // one predicate for both quick-reject pairs: both loads precede the branch
+        const uint32_t miss = ((em >> 16) ^ w.scan01) | ((eb >> 16) ^ w.scanE);
+        if (__builtin_expect(miss == 0, 0)) {
+            const int m = w.m4 >> 2, s = w.s4 >> 2;
+            int k;
+            uint32_t x = get4(E, m) ^ get4(E, s);
+            if (x) k = __builtin_ctz(x) >> 3;
+            else {
+                k = 4;
+                for (;;) {
+                    if (k >= w.maxcmp) break;
+                    x = get4(E, s + k) ^ get4(E, m + k);
+                    if (x) { k += __builtin_ctz(x) >> 3; break; }
+                    k += 4;
+                }
+            }
+            const int len = k < w.maxcmp ? k : w.maxcmp;
+            if (len > w.best) {
+                w.best = len;
+                w.bpos4 = w.m4;
+                if (len >= w.nice) w.limit4 = 0x7fffffff;
+                w.be4 = (len - 1) * 4;
+                w.scanE = E[s + len - 1] >> 16;
+            }
+        }
+        w.count++;
+        w.m4 = m4n;
+        em = emn;
+        if (m4n <= w.limit4) return true;
+        if (w.count >= end) return false;
+    }
+}
+
+template <int kUnroll>
+__device__ __attribute__((always_inline)) inline void mw6_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
+                                                               const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
+                                                               int want_q) {
+    const int s = (int)(p - B);
+    const uint32_t e0 = E[s];
+    const uint32_t d0 = e0 & 0xffffu;
+    if (d0 > (uint32_t)kMaxDist) {
+        rf[p] = 0;
+        if (want_q) rq[p] = 0;
+        return;
+    }
+    MW3 w;
+    const int64_t labs = p > kMaxDist ? p - kMaxDist : 0;
+    w.limit4 = (int)(labs - B) * 4;
+    const int64_t rem = n - p;
+    w.nice = rem < cfg.nice ? (int)rem : cfg.nice;
+    w.maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
+    w.s4 = s * 4;
+    w.m4 = (s - (int)d0) * 4;
+    w.best = kMinMatch - 1;
+    w.bpos4 = 0;
+    w.be4 = (kMinMatch - 2) * 4;
+    w.scan01 = e0 >> 16;
+    w.scanE = E[s + 1] >> 16;
+    w.count = 0;
+    uint32_t em = E[s - (int)d0];
+    const uint32_t qc = want_q ? (uint32_t)(cfg.chain >> 2) : (uint32_t)cfg.chain;
+    const bool done = mw6_loop<kUnroll>(w, em, E, qc);
+    if (want_q) {
+        rq[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
+        if (!done) mw6_loop<kUnroll>(w, em, E, (uint32_t)cfg.chain);
+    }
+    rf[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
+}
+
+// Lanes take positions from an LDS ticket; each walks one position at a time.
+// kVariant 0: the plain walk (MWalk), kept as the readable reference form;
+// 6 / 7: mw6_walk (default 7).  ZGPU_MATCH_VARIANT selects one for A/B runs.
 template <int kVariant>
 __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int want_q) {
     __shared__ __attribute__((aligned(16))) uint32_t E[kME];
@@ -346,7 +442,14 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
         match_tile_load(E, ts, n, in, L, tid);
         if (tid == 0) next_i = 0;
         __syncthreads();
-        if (kVariant == 0) {
+        if (kVariant == 6 || kVariant == 7) {
+            for (;;) {
+                const int i = atomicAdd(&next_i, 1);
+                const int64_t p = ts + i;
+                if (i >= kMT || p >= n) break;
+                mw6_walk<kVariant == 7 ? 2 : 1>(E, p, B, n, cfg, rf, rq, want_q);
+            }
+        } else {
             for (;;) {
                 const int i = atomicAdd(&next_i, 1);
                 const int64_t p = ts + i;
@@ -358,68 +461,6 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
                     const uint32_t eb = E[w.m + w.best - 1] >> 16;
                     if (mwalk_step(w, E, em, eb, cfg, rf, rq, want_q)) break;
                 }
-            }
-        } else if (kVariant == 1) {
-            MWalk w;
-            bool have = false, exhausted = false;
-            for (;;) {
-                while (!have && !exhausted) {
-                    const int i = atomicAdd(&next_i, 1);
-                    if (i >= kMT || ts + i >= n) { exhausted = true; break; }
-                    have = mwalk_init(w, E, ts + i, B, n, cfg, rf, rq, want_q);
-                }
-                if (!__any(have)) break;
-                if (have) {
-                    const uint32_t em = E[w.m];
-                    const uint32_t eb = E[w.m + w.best - 1] >> 16;
-                    if (mwalk_step(w, E, em, eb, cfg, rf, rq, want_q)) have = false;
-                }
-            }
-        } else if (kVariant >= 10) {
-            // batched refill: walks stay in lockstep; idle lanes take new
-            // (consecutive) positions only once at most kVariant lanes are busy
-            MWalk w;
-            bool have = false, exhausted = false;
-            for (;;) {
-                if (!have && !exhausted) {
-                    const int i = atomicAdd(&next_i, 1);
-                    if (i >= kMT || ts + i >= n) exhausted = true;
-                    else have = mwalk_init(w, E, ts + i, B, n, cfg, rf, rq, want_q);
-                }
-                if (!__any(have)) {
-                    if (__all(exhausted)) break;
-                    continue;
-                }
-                for (;;) {
-                    if (have) {
-                        const uint32_t em = E[w.m];
-                        const uint32_t eb = E[w.m + w.best - 1] >> 16;
-                        if (mwalk_step(w, E, em, eb, cfg, rf, rq, want_q)) have = false;
-                    }
-                    const int busy = __popcll(__ballot(have));
-                    if (busy == 0 || (busy <= kVariant && !__all(exhausted || have))) break;
-                }
-            }
-        } else {
-            MWalk a, b;
-            bool ha = false, hb = false, exhausted = false;
-            for (;;) {
-                while (!ha && !exhausted) {
-                    const int i = atomicAdd(&next_i, 1);
-                    if (i >= kMT || ts + i >= n) { exhausted = true; break; }
-                    ha = mwalk_init(a, E, ts + i, B, n, cfg, rf, rq, want_q);
-                }
-                while (!hb && !exhausted) {
-                    const int i = atomicAdd(&next_i, 1);
-                    if (i >= kMT || ts + i >= n) { exhausted = true; break; }
-                    hb = mwalk_init(b, E, ts + i, B, n, cfg, rf, rq, want_q);
-                }
-                if (!__any(ha || hb)) break;
-                const int ma = ha ? a.m : 0, mb = hb ? b.m : 0;
-                const uint32_t ema = E[ma], eba = E[ma + (ha ? a.best - 1 : 0)] >> 16;
-                const uint32_t emb = E[mb], ebb = E[mb + (hb ? b.best - 1 : 0)] >> 16;
-                if (ha && mwalk_step(a, E, ema, eba, cfg, rf, rq, want_q)) ha = false;
-                if (hb && mwalk_step(b, E, emb, ebb, cfg, rf, rq, want_q)) hb = false;
             }
         }
         __syncthreads();
@@ -722,7 +763,7 @@ __device__ __attribute__((always_inline)) inline void lane_init(SlowLane &L, uin
 }
 
 __global__ __launch_bounds__(64) void k_parse_seg(DeflateJob job) {
-    __shared__ uint32_t s_y[65], s_sig[65], s_cnt[64];
+    __shared__ uint32_t s_y[65], s_sig[65];
     __shared__ int s_fail, s_final_lit;
     __shared__ uint32_t s_blk_end[kSegMaxBlk], s_blk_pd[kSegMaxBlk];
     __shared__ uint32_t s_trig[kSegMaxThr];
@@ -1185,7 +1226,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
     __shared__ uint32_t hl[kLCodes], hd[kDCodes];
     __shared__ uint32_t wsum[kEncThreads / 64];
     __shared__ int64_t s_obit;
-    __shared__ int s_type, s_maxbl;
+    __shared__ int s_type;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t bi = blockIdx.x;
     const uint32_t g = job.first + bi;
@@ -1312,7 +1353,6 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
                 else if (static_lenb == opt_lenb) type = 1;
                 else type = 2;
                 s_type = type;
-                s_maxbl = max_blindex;
                 // block header
                 put((uint32_t)(type << 1) + (last ? 1u : 0u), 3);
                 if (type == 0) {
@@ -1441,15 +1481,12 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     case 1: {
         static const int variant = [] {
             const char *e = getenv("ZGPU_MATCH_VARIANT");
-            return e ? atoi(e) : 0;
+            return e ? atoi(e) : 7;
         }();
         const int wq = (int)(job.level >= 5);
-        if (variant == 1) hipLaunchKernelGGL(k_match<1>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        else if (variant == 2) hipLaunchKernelGGL(k_match<2>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        else if (variant == 16) hipLaunchKernelGGL(k_match<16>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        else if (variant == 32) hipLaunchKernelGGL(k_match<32>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        else if (variant == 48) hipLaunchKernelGGL(k_match<48>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        else hipLaunchKernelGGL(k_match<0>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        if (variant == 0) hipLaunchKernelGGL(k_match<0>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        else if (variant == 6) hipLaunchKernelGGL(k_match<6>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        else hipLaunchKernelGGL(k_match<7>, grid, dim3(kMatchThreads), 0, st, job, wq);
         break;
     }
     case 2: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 0); break;
