@@ -384,6 +384,90 @@ __device__ __attribute__((always_inline)) inline bool mw6_loop(MW3 &w, uint32_t 
     }
 }
 
+// Variant 8: both words of candidate k+1 (link word and end-bytes word at the
+// current best) are loaded while candidate k is tested; a best-length change
+// (rare) reloads the end-bytes word.
+template <int kUnroll>
+__device__ __attribute__((always_inline)) inline bool mw8_loop(MW3 &w, uint32_t &em, uint32_t &eb,
+                                                               const uint32_t *E, uint32_t end) {
+    const char *Eb = reinterpret_cast<const char *>(E);
+#pragma unroll kUnroll
+    for (;;) {
+        const int m4n = w.m4 - (int)((em & 0xffffu) << 2);
+        const int a = m4n > 0 ? m4n : 0;
+        const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + a);
+        uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
+        const uint32_t miss = ((em >> 16) ^ w.scan01) | ((eb >> 16) ^ w.scanE);
+        if (__builtin_expect(miss == 0, 0)) {
+            const int m = w.m4 >> 2, s = w.s4 >> 2;
+            int k;
+            uint32_t x = get4(E, m) ^ get4(E, s);
+            if (x) k = __builtin_ctz(x) >> 3;
+            else {
+                k = 4;
+                for (;;) {
+                    if (k >= w.maxcmp) break;
+                    x = get4(E, s + k) ^ get4(E, m + k);
+                    if (x) { k += __builtin_ctz(x) >> 3; break; }
+                    k += 4;
+                }
+            }
+            const int len = k < w.maxcmp ? k : w.maxcmp;
+            if (len > w.best) {
+                w.best = len;
+                w.bpos4 = w.m4;
+                if (len >= w.nice) w.limit4 = 0x7fffffff;
+                w.be4 = (len - 1) * 4;
+                w.scanE = E[s + len - 1] >> 16;
+                ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
+            }
+        }
+        w.count++;
+        w.m4 = m4n;
+        em = emn;
+        eb = ebn;
+        if (m4n <= w.limit4) return true;
+        if (w.count >= end) return false;
+    }
+}
+
+template <int kUnroll>
+__device__ __attribute__((always_inline)) inline void mw8_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
+                                                               const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
+                                                               int want_q) {
+    const int s = (int)(p - B);
+    const uint32_t e0 = E[s];
+    const uint32_t d0 = e0 & 0xffffu;
+    if (d0 > (uint32_t)kMaxDist) {
+        rf[p] = 0;
+        if (want_q) rq[p] = 0;
+        return;
+    }
+    MW3 w;
+    const int64_t labs = p > kMaxDist ? p - kMaxDist : 0;
+    w.limit4 = (int)(labs - B) * 4;
+    const int64_t rem = n - p;
+    w.nice = rem < cfg.nice ? (int)rem : cfg.nice;
+    w.maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
+    w.s4 = s * 4;
+    w.m4 = (s - (int)d0) * 4;
+    w.best = kMinMatch - 1;
+    w.bpos4 = 0;
+    w.be4 = (kMinMatch - 2) * 4;
+    w.scan01 = e0 >> 16;
+    w.scanE = E[s + 1] >> 16;
+    w.count = 0;
+    uint32_t em = E[s - (int)d0];
+    uint32_t eb = E[s - (int)d0 + 1];
+    const uint32_t qc = want_q ? (uint32_t)(cfg.chain >> 2) : (uint32_t)cfg.chain;
+    const bool done = mw8_loop<kUnroll>(w, em, eb, E, qc);
+    if (want_q) {
+        rq[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
+        if (!done) mw8_loop<kUnroll>(w, em, eb, E, (uint32_t)cfg.chain);
+    }
+    rf[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
+}
+
 template <int kUnroll>
 __device__ __attribute__((always_inline)) inline void mw6_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
                                                                const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
@@ -422,7 +506,8 @@ __device__ __attribute__((always_inline)) inline void mw6_walk(const uint32_t *E
 
 // Lanes take positions from an LDS ticket; each walks one position at a time.
 // kVariant 0: the plain walk (MWalk), kept as the readable reference form;
-// 6 / 7: mw6_walk (default 7).  ZGPU_MATCH_VARIANT selects one for A/B runs.
+// 6 / 7: mw6_walk; 8 / 9: mw8_walk (default 9; 7 and 9 unroll the step loop
+// twice).  ZGPU_MATCH_VARIANT selects one for A/B runs.
 template <int kVariant>
 __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int want_q) {
     __shared__ __attribute__((aligned(16))) uint32_t E[kME];
@@ -442,7 +527,14 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
         match_tile_load(E, ts, n, in, L, tid);
         if (tid == 0) next_i = 0;
         __syncthreads();
-        if (kVariant == 6 || kVariant == 7) {
+        if (kVariant == 8 || kVariant == 9) {
+            for (;;) {
+                const int i = atomicAdd(&next_i, 1);
+                const int64_t p = ts + i;
+                if (i >= kMT || p >= n) break;
+                mw8_walk<kVariant == 9 ? 2 : 1>(E, p, B, n, cfg, rf, rq, want_q);
+            }
+        } else if (kVariant == 6 || kVariant == 7) {
             for (;;) {
                 const int i = atomicAdd(&next_i, 1);
                 const int64_t p = ts + i;
@@ -1481,12 +1573,15 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     case 1: {
         static const int variant = [] {
             const char *e = getenv("ZGPU_MATCH_VARIANT");
-            return e ? atoi(e) : 7;
+            return e ? atoi(e) : 9;
         }();
         const int wq = (int)(job.level >= 5);
         if (variant == 0) hipLaunchKernelGGL(k_match<0>, grid, dim3(kMatchThreads), 0, st, job, wq);
         else if (variant == 6) hipLaunchKernelGGL(k_match<6>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        else hipLaunchKernelGGL(k_match<7>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        else if (variant == 8) hipLaunchKernelGGL(k_match<8>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        else if (variant == 9) hipLaunchKernelGGL(k_match<9>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        else if (variant == 7) hipLaunchKernelGGL(k_match<7>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        else hipLaunchKernelGGL(k_match<9>, grid, dim3(kMatchThreads), 0, st, job, wq);
         break;
     }
     case 2: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 0); break;
