@@ -200,7 +200,7 @@ struct Ctx {
     std::string info;
     CrcTables *d_crc = nullptr;
     size_t inflight = size_t(1) << 30;
-    DevBuf ws_link, ws_rf, ws_rq, ws_sym, ws_blk, ws_meta, ws_heads, ws_io, ws_io2, ws_small, ws_bits;
+    DevBuf ws_link, ws_rf, ws_rq, ws_sym, ws_blk, ws_meta, ws_heads, ws_io, ws_io2, ws_small, ws_state;
 };
 
 Ctx &ctx() {
@@ -290,14 +290,15 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         max_blk = std::max(max_blk, blk);
         max_cnt = std::max(max_cnt, b - a);
     }
-    const bool slow = level >= 4, quarter = level >= 5;
+    const bool slow = level >= 4;
     if (!c.ws_meta.ensure(16ull * count + 8ull * max_cnt * 2)) return ZGPU_MEM_ERROR;
     if (!c.ws_link.ensure(2 * max_pos + 64)) return ZGPU_MEM_ERROR;
     if (!c.ws_sym.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
     if (!c.ws_blk.ensure(sizeof(BlockRec) * max_blk)) return ZGPU_MEM_ERROR;
     if (slow && !c.ws_rf.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
-    if (slow && !c.ws_bits.ensure(max_pos + 64)) return ZGPU_MEM_ERROR;
-    if (quarter && !c.ws_rq.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
+    // rquart: quarter-budget results (L5-9) and the lazy parse's symbol-start staging (L4-9)
+    if (slow && !c.ws_rq.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
+    if (slow && !c.ws_state.ensure(max_pos / 4 + 64)) return ZGPU_MEM_ERROR;
     if (level >= 1 && level <= 3 && !c.ws_heads.ensure(4ull * 32768 * max_cnt)) return ZGPU_MEM_ERROR;
     uint64_t *d_meta = c.ws_meta.as<uint64_t>();
     uint32_t *d_nblk = reinterpret_cast<uint32_t *>(d_meta + 2ull * count);
@@ -316,12 +317,12 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         job.blk_off = d_meta + count + a;
         job.link = c.ws_link.as<uint16_t>();
         job.rfull = slow ? c.ws_rf.as<uint32_t>() : nullptr;
-        job.rquart = quarter ? c.ws_rq.as<uint32_t>() : c.ws_rf.as<uint32_t>();
+        job.rquart = slow ? c.ws_rq.as<uint32_t>() : nullptr;
         job.sym = c.ws_sym.as<uint32_t>();
+        job.pstate = slow ? c.ws_state.as<uint32_t>() : nullptr;
         job.blocks = c.ws_blk.as<BlockRec>();
         job.nblocks = d_nblk;
         job.check = d_check;
-        job.pbits = c.ws_bits.as<uint32_t>();
         StageTimer &T = c.timer;
         int rc = 0;
         if (wrap == 1)

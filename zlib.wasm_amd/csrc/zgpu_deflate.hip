@@ -742,21 +742,32 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
 // The lazy parse is a deterministic state machine over decision points whose
 // state is (match_length, match_start, match_available).  Whenever
 // match_length < MIN_MATCH the state is "simple" and fully described by
-// match_available.  The buffer is cut into <= 64 segments; lane i parses its
-// segment from the simple state (.., avail=0), recording in a bitmap every
-// position where it stood in a simple state (per lane parity).  Lane i then
-// runs on into segment i+1 until it stands at a position in the same simple
-// state lane i+1 recorded there: from that point the two parses coincide, so
-// the true parse is lane 0 on [0,y0), lane 1 on [y0,y1), ...  A count pass and
-// a wave prefix sum give each lane its first symbol index; an emit pass writes
-// the symbols in place, the block cuts (every 16383 symbols, deflate.h:371)
-// and the fill_window slide points needed for the stored-block test
-// (FLUSH_BLOCK_ONLY's block_start >= 0, deflate.c:1597-1600).  A buffer whose
-// lanes fail to meet is flagged (nblocks = ~0) for k_parse_slow.
+// match_available.  The buffer is cut into <= kParseLanes segments of >= 4 KiB,
+// one lane each (several independent load chains per buffer hide latency).
+//  pass 1  lane i parses its segment from the simple state (.., avail=0) and
+//          records (2 bits per position, lane-private words in global memory)
+//          the simple states it stands in;
+//  pass 2  lane i runs on into segment i+1 until it stands at a position in the
+//          same simple state lane i+1 recorded there: from that point the two
+//          parses coincide, so the true parse is lane 0 on [0,y0), lane 1 on
+//          [y0,y1), ...  (measured: they meet within ~20 positions on average,
+//          ~500 at most on byte runs);
+//  pass 3  lane i parses [y(i-1), y(i)) and stages its k-th symbol at
+//          rquart[y(i-1) + k] and the symbol's start at rfull[y(i-1) + k] (both
+//          dead behind the parse: a lane's k-th symbol starts at or after
+//          y(i-1) + k - 1, and a lane reads nothing before its position);
+//  compact a block prefix sum of the counts gives each lane its first symbol
+//          index; the symbols are copied into sym[] and every 16383rd symbol
+//          records its end (the block cut of _tr_tally, deflate.h:371);
+//  blocks  block records from the cuts; the fill_window slides before a flush
+//          at decision point d are #{k : T_k <= d} (the k-th slide happens at
+//          the first decision point >= T_k), which is the block_start >= 0 test
+//          of the stored-block choice (deflate.c:1597-1600).
+// A buffer whose lanes fail to meet within the next segment is flagged
+// (nblocks = ~0) for k_parse_slow.
 // ------------------------------------------------------------------------
 constexpr int kSegMin = 4096;
-constexpr int kSegMaxBlk = 1100;      // buffers up to ~18 MB; larger use k_parse_slow
-constexpr int kSegMaxThr = 1024;
+constexpr int kParseLanes = 256;                  // segments (lanes) per buffer
 constexpr uint32_t kEnd = 0xffffffffu;
 
 struct WCache {
@@ -854,53 +865,57 @@ __device__ __attribute__((always_inline)) inline void lane_init(SlowLane &L, uin
     L.cb.base = ~(uintptr_t)0;
 }
 
-__global__ __launch_bounds__(64) void k_parse_seg(DeflateJob job) {
-    __shared__ uint32_t s_y[65], s_sig[65];
-    __shared__ int s_fail, s_final_lit;
-    __shared__ uint32_t s_blk_end[kSegMaxBlk], s_blk_pd[kSegMaxBlk];
-    __shared__ uint32_t s_trig[kSegMaxThr];
+__global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
+    __shared__ uint32_t s_y[kParseLanes], s_sig[kParseLanes];
+    __shared__ uint32_t s_wsum[kParseLanes / 64];
+    __shared__ int s_fail;
+    __shared__ uint32_t s_first_end, s_final;
     const int lane = threadIdx.x;
+    const int wl = lane & 63, wv = lane >> 6;
     const uint32_t bi = blockIdx.x;
     const uint32_t g = job.first + bi;
     const uint32_t n = (uint32_t)job.src_len[g];
     const uint8_t *in = job.src + job.src_off[g];
-    const uint32_t *rf = job.rfull + job.ws_off[bi];
-    const uint32_t *rq = job.rquart + job.ws_off[bi];
-    uint32_t *bits = job.pbits + (job.ws_off[bi] >> 2);
+    uint32_t *rf = job.rfull + job.ws_off[bi];
+    uint32_t *rq = job.rquart + job.ws_off[bi];
     uint32_t *sym = job.sym + job.ws_off[bi];
+    uint32_t *sst = job.pstate + (job.ws_off[bi] >> 4);      // 2 bits per position
     BlockRec *blk = job.blocks + job.blk_off[bi];
     const LevelCfg cfg = c_ct.cfg[job.level];
     const bool use_q = cfg.good < cfg.lazy;
 
-    if ((uint64_t)n / kSymLimit + 2 > (uint64_t)kSegMaxBlk || (uint64_t)n / kWSize + 2 > (uint64_t)kSegMaxThr) {
-        if (lane == 0) job.nblocks[bi] = kParseFallback;
-        return;
-    }
     uint32_t nseg = (n + kSegMin - 1) / kSegMin;
-    nseg = nseg < 1 ? 1 : nseg > 64 ? 64 : nseg;
-    const uint32_t seg = (((n + nseg - 1) / nseg) + 15u) & ~15u;
+    nseg = nseg < 1 ? 1 : nseg > (uint32_t)kParseLanes ? (uint32_t)kParseLanes : nseg;
+    const uint32_t seg = (((n + nseg - 1) / nseg) + 15u) & ~15u;      // lanes never share a state word
     auto xb = [&](uint32_t i) -> uint32_t { uint64_t v = (uint64_t)i * seg; return v < n ? (uint32_t)v : n; };
     const bool active = (uint32_t)lane < nseg;
-    const uint32_t par = lane & 1;
+    if (lane == 0) { s_fail = 0; s_first_end = kParseLanes; s_final = 0; }
 
-    for (uint32_t w = lane; w < (n >> 2) + 1; w += 64) bits[w] = 0;
-    if (lane == 0) { s_fail = 0; s_final_lit = 0; }
-    __threadfence();
-    __syncthreads();
-
-    // ---- pass 1: speculative parse of the own segment, record simple states
+    // ---- pass 1: speculative parse of the own segment; the simple states it
+    // stands in go to sst[] one 16-position word at a time (words it jumps
+    // over are zeroed), lane-private, no atomics
     SlowLane L;
     uint32_t sym_v, spos, slen;
-    lane_init(L, xb(lane), 0);
+    const uint32_t x0 = xb(lane);
+    lane_init(L, x0, 0);
     const uint32_t seg_end = (uint32_t)lane + 1 >= nseg ? n : xb(lane + 1);
-    if (active) {
+    if (active && x0 < seg_end) {
+        uint32_t widx = x0 >> 4, wcur = 0;
         while (L.p < seg_end) {
-            if (L.ml < (uint32_t)kMinMatch)
-                atomicOr(&bits[L.p >> 2], 1u << (8 * (L.p & 3u) + 2 * par + L.avail));
+            const uint32_t wi = L.p >> 4;
+            if (wi != widx) {
+                sst[widx] = wcur;
+                for (uint32_t z = widx + 1; z < wi; z++) sst[z] = 0;
+                widx = wi;
+                wcur = 0;
+            }
+            if (L.ml < (uint32_t)kMinMatch) wcur |= 1u << (2 * (L.p & 15u) + L.avail);
             slow_step(L, n, rf, rq, in, cfg, use_q, sym_v, spos, slen);
         }
+        sst[widx] = wcur;
+        for (uint32_t z = widx + 1; z <= (seg_end - 1) >> 4; z++) sst[z] = 0;
     }
-    __threadfence();
+    __threadfence_block();
     __syncthreads();
 
     // ---- pass 2: run on until the parse meets lane+1's recorded state
@@ -908,102 +923,138 @@ __global__ __launch_bounds__(64) void k_parse_seg(DeflateJob job) {
     if (active && (uint32_t)lane + 1 < nseg) {
         const uint32_t next_start = xb(lane + 1);
         const uint32_t stop = (uint32_t)lane + 2 >= nseg ? n : xb(lane + 2);
+        uint32_t ridx = 0xffffffffu, rw = 0;
         for (;;) {
             if (L.p >= n) { y = kEnd; break; }
             if (L.p >= stop) { atomicOr(&s_fail, 1); break; }
             if (L.p >= next_start && L.ml < (uint32_t)kMinMatch) {
-                const uint32_t wv = __hip_atomic_load(&bits[L.p >> 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((wv >> (8 * (L.p & 3u) + 2 * (par ^ 1u) + L.avail)) & 1u) { y = L.p; sig = L.avail; break; }
+                if ((L.p >> 4) != ridx) { ridx = L.p >> 4; rw = sst[ridx]; }
+                if ((rw >> (2 * (L.p & 15u) + L.avail)) & 1u) { y = L.p; sig = L.avail; break; }
             }
             slow_step(L, n, rf, rq, in, cfg, use_q, sym_v, spos, slen);
         }
     }
-    s_y[lane] = active ? y : kEnd;
+    if (active && y == kEnd) atomicMin(&s_first_end, (uint32_t)lane);
+    s_y[lane] = y;
     s_sig[lane] = sig;
     __syncthreads();
     if (s_fail) {
         if (lane == 0) job.nblocks[bi] = kParseFallback;
         return;
     }
-    // lane i parses [start, end): start = y[i-1] (lane 0: 0), end = y[i] (kEnd: to n)
-    bool mine = active;
-    uint32_t start = 0, start_av = 0;
-    if (lane > 0) {
-        for (int j = 0; j < lane; j++) if (s_y[j] == kEnd) mine = false;
-        start = s_y[lane - 1];
-        start_av = s_sig[lane - 1];
-    }
+    // lane i parses [start, end): start = y[i-1] (lane 0: 0), end = y[i] (kEnd: to n);
+    // lanes after the first one that reached n have nothing to do
+    const bool mine = active && (uint32_t)lane <= s_first_end;
+    const uint32_t start = lane > 0 ? s_y[lane - 1] : 0u;
+    const uint32_t start_av = lane > 0 ? s_sig[lane - 1] : 0u;
     const uint32_t yend = s_y[lane];
     const uint32_t end = yend == kEnd ? n : yend;
+    __syncthreads();
 
-    // ---- pass 3: count symbols
+    // ---- pass 3: the true parse of [start, end); the k-th symbol is staged at
+    // rq[start + k] and its start position at rf[start + k] (both behind the
+    // lane: symbol k starts at or after start + k - 1, and a lane reads only
+    // at and ahead of its own position, inside its own range)
     uint32_t cnt = 0;
     if (mine) {
         lane_init(L, start, start_av);
-        while (L.p < end)
-            if (slow_step(L, n, rf, rq, in, cfg, use_q, sym_v, spos, slen)) cnt++;
-        if (yend == kEnd && L.avail) cnt++;
+        while (L.p < end) {
+            if (slow_step(L, n, rf, rq, in, cfg, use_q, sym_v, spos, slen)) {
+                rq[start + cnt] = sym_v;
+                rf[start + cnt] = spos;
+                cnt++;
+            }
+        }
+        if (yend == kEnd && L.avail) {                 // final pending literal: no flush test
+            rq[start + cnt] = bget(in, n - 1, L.cb);
+            rf[start + cnt] = n - 1;
+            cnt++;
+            s_final = 1;
+        }
     }
-    // exclusive wave prefix sum
+    // exclusive block prefix sum of cnt
     uint32_t incl = cnt;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
+        if (wl >= o) incl += t;
     }
-    const uint32_t base = incl - cnt;
-    const uint32_t total = __shfl(incl, 63, 64);
+    if (wl == 63) s_wsum[wv] = incl;
+    __threadfence_block();
+    __syncthreads();
+    uint32_t woff = 0, total = 0;
+    for (int k = 0; k < kParseLanes / 64; k++) {
+        const uint32_t t = s_wsum[k];
+        if (k < wv) woff += t;
+        total += t;
+    }
+    const uint32_t base = woff + incl - cnt;
+    const uint32_t ncut = total / kSymLimit - ((s_final && total % kSymLimit == 0) ? 1u : 0u);
 
-    // ---- pass 4: emit symbols at their final index, block ends, slide points
-    uint32_t nthr = 0;
-    while (nthr < (uint32_t)kSegMaxThr && slide_threshold(nthr + 1, n) <= (int64_t)n) nthr++;
-    if (mine) {
-        lane_init(L, start, start_av);
-        uint32_t gidx = base;
-        uint32_t k = 0;
-        while (k < nthr && slide_threshold(k + 1, n) < (int64_t)start) k++;
-        while (L.p < end) {
-            while (k < nthr && slide_threshold(k + 1, n) <= (int64_t)L.p) s_trig[k++] = L.p;
-            const int t = slow_step(L, n, rf, rq, in, cfg, use_q, sym_v, spos, slen);
-            if (t) {
-                sym[gidx] = sym_v;
-                if ((gidx + 1) % (uint32_t)kSymLimit == 0) {
-                    const uint32_t b = (gidx + 1) / kSymLimit - 1;
-                    s_blk_end[b] = spos + slen;
-                    s_blk_pd[b] = spos + 1;
+    // ---- compaction: every wave copies its own lanes' symbols (stage and
+    // destination are different arrays); 16383rd symbols record their block
+    // cut in blk[b].in_end / .pad
+    for (int j = 0; j < 64; j++) {
+        const uint32_t jc = __shfl(cnt, j, 64), jb = __shfl(base, j, 64), js = __shfl(start, j, 64);
+        if (jc == 0) continue;
+        for (uint32_t c = 0; c < jc; c += 64 * 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint32_t idx = c + 64u * u + (uint32_t)wl;
+                v[u] = idx < jc ? rq[js + idx] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint32_t idx = c + 64u * u + (uint32_t)wl;
+                if (idx < jc) {
+                    const uint32_t gi = jb + idx;
+                    sym[gi] = v[u];
+                    if ((gi + 1) % (uint32_t)kSymLimit == 0 && (gi + 1) / (uint32_t)kSymLimit <= ncut) {
+                        const uint32_t b = (gi + 1) / (uint32_t)kSymLimit - 1;
+                        const uint32_t sp = rf[js + idx];
+                        const uint32_t sl = v[u] < 256u ? 1u : (v[u] & 0xffu) + (uint32_t)kMinMatch;
+                        blk[b].in_end = (uint64_t)(sp + sl);
+                        blk[b].pad = sp + 1;                        // decision point of the flush
+                    }
                 }
-                gidx++;
             }
-        }
-        if (yend == kEnd) {
-            while (k < nthr && slide_threshold(k + 1, n) <= (int64_t)n) s_trig[k++] = n;
-            if (L.avail) {                      // final pending literal: no flush test
-                sym[gidx++] = bget(in, n - 1, L.cb);
-                s_final_lit = 1;
-            }
-        } else {
-            while (k < nthr && slide_threshold(k + 1, n) < (int64_t)end) s_trig[k++] = end;
         }
     }
+    __threadfence_block();
     __syncthreads();
 
-    // ---- block records
-    const uint32_t ncut = total / kSymLimit - ((s_final_lit && total % kSymLimit == 0) ? 1u : 0u);
-    for (uint32_t b = lane; b <= ncut; b += 64) {
-        const bool last = b == ncut;
-        const uint32_t in_end = last ? n : s_blk_end[b];
-        const uint32_t pd = last ? n : s_blk_pd[b];
-        const uint32_t in_start = b == 0 ? 0 : s_blk_end[b - 1];
-        uint32_t slides = 0;
-        for (uint32_t j = 0; j < nthr; j++) slides += s_trig[j] <= pd ? 1u : 0u;
-        BlockRec r;
-        r.sym_start = b * kSymLimit;
-        r.nsym = last ? total - b * kSymLimit : (uint32_t)kSymLimit;
-        r.in_start = in_start;
-        r.in_end = in_end;
-        r.flags = (last ? 1u : 0u) | ((uint64_t)in_start >= (uint64_t)kWSize * slides ? 2u : 0u);
-        r.pad = 0;
-        blk[b] = r;
+    // ---- block records (all cut fields read before any record is written)
+    uint32_t nthr = 0;
+    while (slide_threshold(nthr + 1, n) <= (int64_t)n) nthr++;
+    constexpr int kRecs = 8;
+    BlockRec r[kRecs];
+    for (uint32_t b0 = 0; b0 <= ncut; b0 += kParseLanes * kRecs) {
+#pragma unroll
+        for (int u = 0; u < kRecs; u++) {
+            const uint32_t b = b0 + (uint32_t)u * kParseLanes + (uint32_t)lane;
+            if (b > ncut) continue;
+            const bool last = b == ncut;
+            const uint64_t in_end = last ? n : blk[b].in_end;
+            const uint64_t pd = last ? n : blk[b].pad;
+            const uint64_t in_start = b == 0 ? 0 : blk[b - 1].in_end;
+            uint32_t slides = 0;
+            while (slides < nthr && slide_threshold(slides + 1, n) <= (int64_t)pd) slides++;
+            r[u].sym_start = b * kSymLimit;
+            r[u].nsym = last ? total - b * kSymLimit : (uint32_t)kSymLimit;
+            r[u].in_start = in_start;
+            r[u].in_end = in_end;
+            r[u].flags = (last ? 1u : 0u) | (in_start >= (uint64_t)kWSize * slides ? 2u : 0u);
+            r[u].pad = 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kRecs; u++) {
+            const uint32_t b = b0 + (uint32_t)u * kParseLanes + (uint32_t)lane;
+            if (b <= ncut) blk[b] = r[u];
+        }
+        __threadfence_block();
+        __syncthreads();
     }
     if (lane == 0) job.nblocks[bi] = ncut + 1;
 }
@@ -1585,7 +1636,7 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         break;
     }
     case 2: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 0); break;
-    case 5: hipLaunchKernelGGL(k_parse_seg, grid, dim3(64), 0, st, job); break;
+    case 5: hipLaunchKernelGGL(k_parse_seg, grid, dim3(kParseLanes), 0, st, job); break;
     case 6: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 1); break;
     case 3: hipLaunchKernelGGL(k_parse_fast, grid, dim3(64), 0, st, job, heads); break;
     case 4: hipLaunchKernelGGL(k_encode, grid, dim3(kEncThreads), 0, st, job); break;

@@ -84,10 +84,10 @@ struct DeflateJob {
     uint16_t *link;          // [Σn]
     uint32_t *rfull;         // [Σn]
     uint32_t *rquart;        // [Σn] (levels 5..9)
+    uint32_t *pstate;        // [Σn/16] lazy-parse sync states, 2 bits per position
     uint32_t *sym;           // [Σn]
     BlockRec *blocks;        // [Σ(n/16383 + 2)]
     uint32_t *nblocks;       // [count]
-    uint32_t *pbits;         // [Σn/4] segmented-parse state bitmap
     uint32_t *check;         // [count] adler32 / crc32 of the input (trailer)
 };
 
