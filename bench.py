@@ -263,7 +263,7 @@ def main():
     o = Oracle()
     h_dlen = d["dlen"].cpu().numpy()
     n = a.buffer_bytes
-    idx = sorted(set(int(i) for i in torch.linspace(0, a.buffers - 1, max(1, a.verify)).tolist()))
+    idx = sorted(set(int(i) for i in torch.linspace(0, a.buffers - 1, a.verify).tolist())) if a.verify > 0 else []
     sample, want = [], []
     for i in idx:
         raw = d["src"][i * n:(i + 1) * n].cpu().numpy().tobytes()
@@ -299,7 +299,7 @@ def main():
         cpu = None
         m_traffic, m_src = pmc_traffic("k_match", f"L{a.level}_{launches_tag(a)}")
         c_traffic, c_src = pmc_traffic("k_crc32", f"C2_{a.crc_buffers}x{a.crc_bytes}")
-        if not a.no_cpu:
+        if not a.no_cpu and sample:
             v, threads, tot = cpu_baseline(a, sample, a.level)
             cpu = {"value": round(v, 2), "unit": "MB/s", "cores": threads, "kind": "port",
                    "sample": f"{len(sample)} distinct 1 MiB Silesia-mix buffers of this batch, "

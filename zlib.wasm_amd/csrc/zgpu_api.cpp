@@ -100,6 +100,7 @@ void build_code_tables(CodeTables &t) {
     for (int b = 1; b <= 15; b++) { c = (c + cnt[b - 1]) << 1; next[b] = (uint16_t)c; }
     for (int n = 0; n < 288; n++) t.stat_lcode[n] = (uint16_t)bitrev(next[t.stat_llen[n]]++, t.stat_llen[n]);
     for (int n = 0; n < 30; n++) t.stat_dcode[n] = (uint16_t)bitrev((unsigned)n, 5);
+    for (int n = 0; n < 30; n++) t.stat_dlen[n] = 5;
     static const LevelCfg cfg[10] = {{0, 0, 0, 0},      {4, 4, 8, 4},       {4, 5, 16, 8},
                                      {4, 6, 32, 32},    {4, 4, 16, 16},    {8, 16, 32, 32},
                                      {8, 16, 128, 128}, {8, 32, 128, 256}, {32, 128, 258, 1024},

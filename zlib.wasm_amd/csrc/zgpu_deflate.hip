@@ -1165,11 +1165,8 @@ struct TreeLDS {
     uint8_t dlen[2 * kDCodes + 2];
     uint16_t bfreq[2 * kBLCodes + 1], bdad[2 * kBLCodes + 1], bcode[2 * kBLCodes + 1];
     uint8_t blen[2 * kBLCodes + 2];
-    int heap[kHeapSize + 1];
-    uint8_t depth[kHeapSize];
+    uint32_t heap[kHeapSize + 1];        // packed keys, see hkey()
     uint16_t bl_count[kMaxBits + 1];
-    int heap_len, heap_max;
-    int64_t opt_len, static_len;
 };
 
 struct TreeRef {
@@ -1178,86 +1175,101 @@ struct TreeRef {
     int max_code;
 };
 
-__device__ inline bool t_smaller(const TreeRef &t, const TreeLDS &h, int n, int m) {
-    return t.freq[n] < t.freq[m] || (t.freq[n] == t.freq[m] && h.depth[n] <= h.depth[m]);
+// Heap entries carry their own sort key: freq (16 bits) | depth (6) | node (10).
+// zlib's smaller(n, m) (trees.c:499-501: freq, then depth, ties "<=") is then
+// hkey(n) >> 10 <= hkey(m) >> 10, and a heap level costs one LDS round trip.
+__device__ inline uint32_t hkey(uint32_t freq, uint32_t depth, uint32_t node) {
+    return (freq << 16) | (depth << 10) | node;
 }
+__device__ inline bool hle(uint32_t a, uint32_t b) { return (a >> 10) <= (b >> 10); }
 
-__device__ void t_downheap(const TreeRef &t, TreeLDS &h, int k) {        // pqdownheap
-    int v = h.heap[k];
+__device__ void t_downheap(uint32_t *heap, int heap_len, int k) {        // pqdownheap
+    const uint32_t v = heap[k];
     int j = k << 1;
-    while (j <= h.heap_len) {
-        if (j < h.heap_len && t_smaller(t, h, h.heap[j + 1], h.heap[j])) j++;
-        if (t_smaller(t, h, v, h.heap[j])) break;
-        h.heap[k] = h.heap[j];
+    while (j <= heap_len) {
+        uint32_t hj = heap[j];
+        if (j < heap_len) {
+            const uint32_t hj1 = heap[j + 1];
+            if (hle(hj1, hj)) { j++; hj = hj1; }
+        }
+        if (hle(v, hj)) break;
+        heap[k] = hj;
         k = j;
         j <<= 1;
     }
-    h.heap[k] = v;
+    heap[k] = v;
 }
 
 __device__ void t_gen_codes(TreeRef &t, const uint16_t *bl_count) {       // gen_codes
-    uint16_t next[kMaxBits + 1];
+    uint32_t next[kMaxBits + 1];
     uint32_t c = 0;
-    for (int b = 1; b <= kMaxBits; b++) { c = (c + bl_count[b - 1]) << 1; next[b] = (uint16_t)c; }
+#pragma unroll
+    for (int b = 1; b <= kMaxBits; b++) { c = (c + bl_count[b - 1]) << 1; next[b] = c; }
     for (int n = 0; n <= t.max_code; n++) {
-        int len = t.len[n];
+        const int len = t.len[n];
         if (!len) continue;
-        uint32_t code = next[len]++, r = 0;
-        for (int i = 0; i < len; i++) { r = (r << 1) | (code & 1u); code >>= 1; }
-        t.code[n] = (uint16_t)r;
+        uint32_t code = 0;
+#pragma unroll
+        for (int b = 1; b <= kMaxBits; b++)            // register-resident next[] (no scratch)
+            if (b == len) code = next[b]++;
+        t.code[n] = (uint16_t)(__brev(code) >> (32 - len));
     }
 }
 
-// build_tree + gen_bitlen (trees.c:540-706); slen == nullptr for the bl tree
-__device__ void t_build(TreeRef &t, TreeLDS &h, int elems, const uint8_t *slen,
-                        const uint8_t *extra, int xbase, int max_length) {
-    int max_code = -1;
-    h.heap_len = 0;
-    h.heap_max = kHeapSize;
+// build_tree + gen_bitlen (trees.c:540-706); slen == nullptr for the bl tree.
+// Single lane; opt_len/static_len accumulate in registers.
+__device__ void t_build(TreeRef &t, TreeLDS &h, int elems, const uint8_t *slen, const uint8_t *extra,
+                        int xbase, int max_length, int64_t &opt_len, int64_t &static_len) {
+    uint32_t *heap = h.heap;
+    int max_code = -1, heap_len = 0, heap_max = kHeapSize;
     for (int n = 0; n < elems; n++) {
-        if (t.freq[n] != 0) { h.heap[++h.heap_len] = max_code = n; h.depth[n] = 0; }
+        const uint32_t f = t.freq[n];
+        if (f != 0) { heap[++heap_len] = hkey(f, 0, (uint32_t)n); max_code = n; }
         else t.len[n] = 0;
     }
-    while (h.heap_len < 2) {
-        int node = h.heap[++h.heap_len] = (max_code < 2 ? ++max_code : 0);
+    while (heap_len < 2) {
+        const int node = max_code < 2 ? ++max_code : 0;
+        heap[++heap_len] = hkey(1, 0, (uint32_t)node);
         t.freq[node] = 1;
-        h.depth[node] = 0;
-        h.opt_len--;
-        if (slen) h.static_len -= slen[node];
+        opt_len--;
+        if (slen) static_len -= slen[node];
     }
     t.max_code = max_code;
-    for (int n = h.heap_len / 2; n >= 1; n--) t_downheap(t, h, n);
-    int node = elems;
+    for (int n = heap_len / 2; n >= 1; n--) t_downheap(heap, heap_len, n);
+    uint32_t node = (uint32_t)elems;
     do {
-        int n = h.heap[1];
-        h.heap[1] = h.heap[h.heap_len--];
-        t_downheap(t, h, 1);
-        int m = h.heap[1];
-        h.heap[--h.heap_max] = n;
-        h.heap[--h.heap_max] = m;
-        t.freq[node] = (uint16_t)(t.freq[n] + t.freq[m]);
-        h.depth[node] = (uint8_t)((h.depth[n] >= h.depth[m] ? h.depth[n] : h.depth[m]) + 1);
-        t.dad[n] = t.dad[m] = (uint16_t)node;
-        h.heap[1] = node++;
-        t_downheap(t, h, 1);
-    } while (h.heap_len >= 2);
-    h.heap[--h.heap_max] = h.heap[1];
+        const uint32_t kn = heap[1];
+        heap[1] = heap[heap_len--];
+        t_downheap(heap, heap_len, 1);
+        const uint32_t km = heap[1];
+        heap[--heap_max] = kn;
+        heap[--heap_max] = km;
+        const uint32_t f = (kn >> 16) + (km >> 16);
+        const uint32_t dn = (kn >> 10) & 63u, dm = (km >> 10) & 63u;
+        t.freq[node] = (uint16_t)f;
+        t.dad[kn & 1023u] = t.dad[km & 1023u] = (uint16_t)node;
+        heap[1] = hkey(f, (dn >= dm ? dn : dm) + 1, node);
+        node++;
+        t_downheap(heap, heap_len, 1);
+    } while (heap_len >= 2);
+    heap[--heap_max] = heap[1];
 
     // gen_bitlen
     int overflow = 0;
     for (int b = 0; b <= kMaxBits; b++) h.bl_count[b] = 0;
-    t.len[h.heap[h.heap_max]] = 0;
-    int hh;
-    for (hh = h.heap_max + 1; hh < kHeapSize; hh++) {
-        int n = h.heap[hh];
+    t.len[heap[heap_max] & 1023u] = 0;
+    for (int hh = heap_max + 1; hh < kHeapSize; hh++) {
+        const uint32_t key = heap[hh];
+        const int n = (int)(key & 1023u);
         int bits = t.len[t.dad[n]] + 1;
         if (bits > max_length) { bits = max_length; overflow++; }
         t.len[n] = (uint8_t)bits;
-        if (n > t.max_code) continue;
+        if (n > max_code) continue;
         h.bl_count[bits]++;
-        int xb = n >= xbase ? extra[n - xbase] : 0;
-        h.opt_len += (int64_t)t.freq[n] * (bits + xb);
-        if (slen) h.static_len += (int64_t)t.freq[n] * (slen[n] + xb);
+        const int xb = n >= xbase ? extra[n - xbase] : 0;
+        const int64_t f = (int64_t)(key >> 16);
+        opt_len += f * (bits + xb);
+        if (slen) static_len += f * (slen[n] + xb);
     }
     if (overflow != 0) {
         do {
@@ -1268,14 +1280,14 @@ __device__ void t_build(TreeRef &t, TreeLDS &h, int elems, const uint8_t *slen,
             h.bl_count[max_length]--;
             overflow -= 2;
         } while (overflow > 0);
-        hh = kHeapSize;
+        int hh = kHeapSize;
         for (int bits = max_length; bits != 0; bits--) {
             int n = h.bl_count[bits];
             while (n != 0) {
-                int m = h.heap[--hh];
-                if (m > t.max_code) continue;
+                const int m = (int)(heap[--hh] & 1023u);
+                if (m > max_code) continue;
                 if (t.len[m] != bits) {
-                    h.opt_len += ((int64_t)bits - t.len[m]) * t.freq[m];
+                    opt_len += ((int64_t)bits - t.len[m]) * t.freq[m];
                     t.len[m] = (uint8_t)bits;
                 }
                 n--;
@@ -1466,29 +1478,27 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
             // room for the largest block header (dynamic trees: < 5000 bits)
             if (s_obit - st.sbase + 6144 > kStgBits) stg_flush(st, s_obit, false);
             // --- trees and block type (single lane) ---
+            for (int i = tid; i < kLCodes; i += kEncThreads) T.lfreq[i] = i == kEndBlock ? 1 : (uint16_t)hl[i];
+            if (tid < kDCodes) T.dfreq[tid] = (uint16_t)hd[tid];
+            if (tid < kBLCodes) T.bfreq[tid] = 0;
+            __syncthreads();
             if (tid == 0) {
-                for (int i = 0; i < kLCodes; i++) T.lfreq[i] = (uint16_t)hl[i];
-                T.lfreq[kEndBlock] = 1;
-                for (int i = 0; i < kDCodes; i++) T.dfreq[i] = (uint16_t)hd[i];
-                for (int i = 0; i < kBLCodes; i++) T.bfreq[i] = 0;
-                T.opt_len = T.static_len = 0;
+                int64_t opt_len = 0, static_len = 0;
                 TreeRef lt{T.lfreq, T.ldad, T.lcode, T.llen, 0};
                 TreeRef dt{T.dfreq, T.ddad, T.dcode, T.dlen, 0};
                 TreeRef bt{T.bfreq, T.bdad, T.bcode, T.blen, 0};
-                t_build(lt, T, kLCodes, c_ct.stat_llen, c_ct.xlbits, 257, kMaxBits);
-                uint8_t sdl[kDCodes];
-                for (int i = 0; i < kDCodes; i++) sdl[i] = 5;
-                t_build(dt, T, kDCodes, sdl, c_ct.xdbits, 0, kMaxBits);
+                t_build(lt, T, kLCodes, c_ct.stat_llen, c_ct.xlbits, 257, kMaxBits, opt_len, static_len);
+                t_build(dt, T, kDCodes, c_ct.stat_dlen, c_ct.xdbits, 0, kMaxBits, opt_len, static_len);
                 auto cnt = [&](int s, int, int) { T.bfreq[s]++; };
                 t_rle(T.llen, lt.max_code, cnt);
                 t_rle(T.dlen, dt.max_code, cnt);
-                t_build(bt, T, kBLCodes, nullptr, c_ct.xblbits, 0, kMaxBLBits);
+                t_build(bt, T, kBLCodes, nullptr, c_ct.xblbits, 0, kMaxBLBits, opt_len, static_len);
                 int max_blindex;
                 for (max_blindex = kBLCodes - 1; max_blindex >= 3; max_blindex--)
                     if (T.blen[c_ct.bl_order[max_blindex]] != 0) break;
-                T.opt_len += 3 * ((int64_t)max_blindex + 1) + 5 + 5 + 4;
-                uint64_t opt_lenb = ((uint64_t)T.opt_len + 3 + 7) >> 3;
-                const uint64_t static_lenb = ((uint64_t)T.static_len + 3 + 7) >> 3;
+                opt_len += 3 * ((int64_t)max_blindex + 1) + 5 + 5 + 4;
+                uint64_t opt_lenb = ((uint64_t)opt_len + 3 + 7) >> 3;
+                const uint64_t static_lenb = ((uint64_t)static_len + 3 + 7) >> 3;
                 if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
                 const uint64_t stored_len = br.in_end - br.in_start;
                 int type;

@@ -37,6 +37,7 @@ struct CodeTables {
     uint16_t stat_lcode[288];
     uint8_t  stat_llen[288];
     uint16_t stat_dcode[30];
+    uint8_t  stat_dlen[30];     // all 5 (static_dtree, trees.c:292)
     LevelCfg cfg[10];
 };
 
