@@ -1155,15 +1155,17 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
 // k_encode — one 256-thread workgroup per buffer.
 // ------------------------------------------------------------------------
 constexpr int kEncThreads = 256;
-constexpr int kStgWords = 4096;                 // 16 KiB output staging window
+constexpr int kStgWords = 2048;                 // 8 KiB output staging window
+constexpr int kEncGroup = kEncThreads / 64;     // blocks whose trees are built at once (one per wave)
 constexpr int kStgBits = kStgWords * 32;
 
 struct TreeLDS {
-    uint16_t lfreq[kHeapSize], ldad[kHeapSize], lcode[kHeapSize];
+    // leaves: freq/code; all nodes: dad/len (internal-node freqs live in heap keys)
+    uint16_t lfreq[kLCodes], lcode[kLCodes], ldad[kHeapSize];
     uint8_t llen[kHeapSize + 1];
-    uint16_t dfreq[2 * kDCodes + 1], ddad[2 * kDCodes + 1], dcode[2 * kDCodes + 1];
+    uint16_t dfreq[kDCodes], dcode[kDCodes], ddad[2 * kDCodes + 1];
     uint8_t dlen[2 * kDCodes + 2];
-    uint16_t bfreq[2 * kBLCodes + 1], bdad[2 * kBLCodes + 1], bcode[2 * kBLCodes + 1];
+    uint16_t bfreq[kBLCodes], bcode[kBLCodes], bdad[2 * kBLCodes + 1];
     uint8_t blen[2 * kBLCodes + 2];
     uint32_t heap[kHeapSize + 1];        // packed keys, see hkey()
     uint16_t bl_count[kMaxBits + 1];
@@ -1246,7 +1248,6 @@ __device__ void t_build(TreeRef &t, TreeLDS &h, int elems, const uint8_t *slen, 
         heap[--heap_max] = km;
         const uint32_t f = (kn >> 16) + (km >> 16);
         const uint32_t dn = (kn >> 10) & 63u, dm = (km >> 10) & 63u;
-        t.freq[node] = (uint16_t)f;
         t.dad[kn & 1023u] = t.dad[km & 1023u] = (uint16_t)node;
         heap[1] = hkey(f, (dn >= dm ? dn : dm) + 1, node);
         node++;
@@ -1377,11 +1378,11 @@ __device__ void stg_flush(Stage &st, int64_t upto, bool final_flush) {
 
 __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
     __shared__ uint32_t stg[kStgWords];
-    __shared__ TreeLDS T;
-    __shared__ uint32_t hl[kLCodes], hd[kDCodes];
+    __shared__ TreeLDS TT[kEncGroup];
+    __shared__ uint32_t HL[kEncGroup][kLCodes], HD[kEncGroup][kDCodes];
     __shared__ uint32_t wsum[kEncThreads / 64];
     __shared__ int64_t s_obit;
-    __shared__ int s_type;
+    __shared__ struct { int type, lmax, dmax, blmax; } s_hdr[kEncGroup];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t bi = blockIdx.x;
     const uint32_t g = job.first + bi;
@@ -1457,63 +1458,82 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
         } while (true);
     } else {
         const uint32_t nblk = job.nblocks[bi];
-        for (uint32_t k = 0; k < nblk; k++) {
-            const BlockRec br = blk[k];
-            const bool last = br.flags & 1u;
-            // --- histogram (_tr_tally freq updates, deflate.h:354-372) ---
-            for (int i = tid; i < kLCodes; i += kEncThreads) hl[i] = 0;
-            for (int i = tid; i < kDCodes; i += kEncThreads) hd[i] = 0;
-            __syncthreads();
-            for (uint32_t i = tid; i < br.nsym; i += kEncThreads) {
-                const uint32_t v = sym[br.sym_start + i];
-                const uint32_t dist = v >> 8, lc = v & 0xffu;
-                if (dist == 0) atomicAdd(&hl[lc], 1u);
-                else {
-                    atomicAdd(&hl[c_ct.len_code[lc] + 257], 1u);
-                    const uint32_t d = dist - 1;
-                    atomicAdd(&hd[d < 256 ? c_ct.dist_code[d] : c_ct.dist_code[256 + (d >> 7)]], 1u);
+        for (uint32_t g0 = 0; g0 < nblk; g0 += kEncGroup) {
+            // ---- trees of kEncGroup blocks at once: wave w owns block g0 + w ----
+            {
+                const uint32_t kb = g0 + (uint32_t)wave;
+                TreeLDS &T = TT[wave];
+                uint32_t *hl = HL[wave], *hd = HD[wave];
+                if (kb < nblk) {
+                    const BlockRec br = blk[kb];
+                    // histogram (_tr_tally freq updates, deflate.h:354-372)
+                    for (int i = lane; i < kLCodes; i += 64) hl[i] = 0;
+                    if (lane < kDCodes) hd[lane] = 0;
+                    __builtin_amdgcn_wave_barrier();
+                    for (uint32_t i = lane; i < br.nsym; i += 64) {
+                        const uint32_t v = sym[br.sym_start + i];
+                        const uint32_t dist = v >> 8, lc = v & 0xffu;
+                        if (dist == 0) atomicAdd(&hl[lc], 1u);
+                        else {
+                            atomicAdd(&hl[c_ct.len_code[lc] + 257], 1u);
+                            const uint32_t d = dist - 1;
+                            atomicAdd(&hd[d < 256 ? c_ct.dist_code[d] : c_ct.dist_code[256 + (d >> 7)]], 1u);
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    for (int i = lane; i < kLCodes; i += 64) T.lfreq[i] = i == kEndBlock ? 1 : (uint16_t)hl[i];
+                    if (lane < kDCodes) T.dfreq[lane] = (uint16_t)hd[lane];
+                    if (lane < kBLCodes) T.bfreq[lane] = 0;
+                    __builtin_amdgcn_wave_barrier();
+                    if (lane == 0) {
+                        int64_t opt_len = 0, static_len = 0;
+                        TreeRef lt{T.lfreq, T.ldad, T.lcode, T.llen, 0};
+                        TreeRef dt{T.dfreq, T.ddad, T.dcode, T.dlen, 0};
+                        TreeRef bt{T.bfreq, T.bdad, T.bcode, T.blen, 0};
+                        t_build(lt, T, kLCodes, c_ct.stat_llen, c_ct.xlbits, 257, kMaxBits, opt_len, static_len);
+                        t_build(dt, T, kDCodes, c_ct.stat_dlen, c_ct.xdbits, 0, kMaxBits, opt_len, static_len);
+                        auto cnt = [&](int s, int, int) { T.bfreq[s]++; };
+                        t_rle(T.llen, lt.max_code, cnt);
+                        t_rle(T.dlen, dt.max_code, cnt);
+                        t_build(bt, T, kBLCodes, nullptr, c_ct.xblbits, 0, kMaxBLBits, opt_len, static_len);
+                        int max_blindex;
+                        for (max_blindex = kBLCodes - 1; max_blindex >= 3; max_blindex--)
+                            if (T.blen[c_ct.bl_order[max_blindex]] != 0) break;
+                        opt_len += 3 * ((int64_t)max_blindex + 1) + 5 + 5 + 4;
+                        uint64_t opt_lenb = ((uint64_t)opt_len + 3 + 7) >> 3;
+                        const uint64_t static_lenb = ((uint64_t)static_len + 3 + 7) >> 3;
+                        if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+                        const uint64_t stored_len = br.in_end - br.in_start;
+                        int type;                                   // trees.c:1027-1074
+                        if (stored_len + 4 <= opt_lenb && (br.flags & 2u)) type = 0;
+                        else if (static_lenb == opt_lenb) type = 1;
+                        else type = 2;
+                        s_hdr[wave].type = type;
+                        s_hdr[wave].lmax = lt.max_code;
+                        s_hdr[wave].dmax = dt.max_code;
+                        s_hdr[wave].blmax = max_blindex;
+                    }
                 }
             }
             __syncthreads();
+          for (int w = 0; w < kEncGroup && g0 + (uint32_t)w < nblk; w++) {
+            const uint32_t k = g0 + (uint32_t)w;
+            const BlockRec br = blk[k];
+            const bool last = br.flags & 1u;
+            TreeLDS &T = TT[w];
             // room for the largest block header (dynamic trees: < 5000 bits)
             if (s_obit - st.sbase + 6144 > kStgBits) stg_flush(st, s_obit, false);
-            // --- trees and block type (single lane) ---
-            for (int i = tid; i < kLCodes; i += kEncThreads) T.lfreq[i] = i == kEndBlock ? 1 : (uint16_t)hl[i];
-            if (tid < kDCodes) T.dfreq[tid] = (uint16_t)hd[tid];
-            if (tid < kBLCodes) T.bfreq[tid] = 0;
-            __syncthreads();
             if (tid == 0) {
-                int64_t opt_len = 0, static_len = 0;
-                TreeRef lt{T.lfreq, T.ldad, T.lcode, T.llen, 0};
-                TreeRef dt{T.dfreq, T.ddad, T.dcode, T.dlen, 0};
-                TreeRef bt{T.bfreq, T.bdad, T.bcode, T.blen, 0};
-                t_build(lt, T, kLCodes, c_ct.stat_llen, c_ct.xlbits, 257, kMaxBits, opt_len, static_len);
-                t_build(dt, T, kDCodes, c_ct.stat_dlen, c_ct.xdbits, 0, kMaxBits, opt_len, static_len);
-                auto cnt = [&](int s, int, int) { T.bfreq[s]++; };
-                t_rle(T.llen, lt.max_code, cnt);
-                t_rle(T.dlen, dt.max_code, cnt);
-                t_build(bt, T, kBLCodes, nullptr, c_ct.xblbits, 0, kMaxBLBits, opt_len, static_len);
-                int max_blindex;
-                for (max_blindex = kBLCodes - 1; max_blindex >= 3; max_blindex--)
-                    if (T.blen[c_ct.bl_order[max_blindex]] != 0) break;
-                opt_len += 3 * ((int64_t)max_blindex + 1) + 5 + 5 + 4;
-                uint64_t opt_lenb = ((uint64_t)opt_len + 3 + 7) >> 3;
-                const uint64_t static_lenb = ((uint64_t)static_len + 3 + 7) >> 3;
-                if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+                const int type = s_hdr[w].type;
                 const uint64_t stored_len = br.in_end - br.in_start;
-                int type;
-                if (stored_len + 4 <= opt_lenb && (br.flags & 2u)) type = 0;
-                else if (static_lenb == opt_lenb) type = 1;
-                else type = 2;
-                s_type = type;
-                // block header
                 put((uint32_t)(type << 1) + (last ? 1u : 0u), 3);
                 if (type == 0) {
                     s_obit = (s_obit + 7) & ~7ll;
                     put((uint32_t)stored_len & 0xffffu, 16);
                     put((~(uint32_t)stored_len) & 0xffffu, 16);
                 } else if (type == 2) {
-                    const int lcodes = lt.max_code + 1, dcodes = dt.max_code + 1;
+                    const int lcodes = s_hdr[w].lmax + 1, dcodes = s_hdr[w].dmax + 1;
+                    const int max_blindex = s_hdr[w].blmax;
                     put((uint32_t)(lcodes - 257), 5);
                     put((uint32_t)(dcodes - 1), 5);
                     put((uint32_t)(max_blindex + 1 - 4), 4);
@@ -1527,7 +1547,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
                 }
             }
             __syncthreads();
-            const int type = s_type;
+            const int type = s_hdr[w].type;
             if (type == 0) {
                 // stored: raw bytes (byte aligned)
                 const int64_t len = (int64_t)(br.in_end - br.in_start);
@@ -1597,6 +1617,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
             }
             if (last && tid == 0) s_obit = (s_obit + 7) & ~7ll;   // bi_windup
             __syncthreads();
+          }
         }
     }
     // trailer
