@@ -202,6 +202,12 @@ struct Ctx {
     CrcTables *d_crc = nullptr;
     size_t inflight = size_t(1) << 30;
     DevBuf ws_link, ws_rf, ws_rq, ws_sym, ws_blk, ws_meta, ws_heads, ws_io, ws_io2, ws_small, ws_state;
+    // second workspace slot and stream for the L4-9 pipeline (k_match of
+    // sub-batch i+1 runs on `aux` while links/parse/encode run on the caller's
+    // stream)
+    DevBuf ws_link2, ws_rf2, ws_rq2, ws_state2;
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_links[2] = {nullptr, nullptr}, ev_match[2] = {nullptr, nullptr};
 };
 
 Ctx &ctx() {
@@ -292,6 +298,9 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         max_cnt = std::max(max_cnt, b - a);
     }
     const bool slow = level >= 4;
+    const size_t nsub = cuts.size() - 1;
+    static const bool no_pipe = std::getenv("ZGPU_NO_PIPELINE") != nullptr;
+    const bool piped = slow && nsub > 1 && !no_pipe;
     if (!c.ws_meta.ensure(16ull * count + 8ull * max_cnt * 2)) return ZGPU_MEM_ERROR;
     if (!c.ws_link.ensure(2 * max_pos + 64)) return ZGPU_MEM_ERROR;
     if (!c.ws_sym.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
@@ -300,6 +309,21 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     // rquart: quarter-budget results (L5-9) and the lazy parse's symbol-start staging (L4-9)
     if (slow && !c.ws_rq.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
     if (slow && !c.ws_state.ensure(max_pos / 4 + 64)) return ZGPU_MEM_ERROR;
+    if (piped) {
+        if (!c.ws_link2.ensure(2 * max_pos + 64) || !c.ws_rf2.ensure(4 * max_pos + 64) ||
+            !c.ws_rq2.ensure(4 * max_pos + 64) || !c.ws_state2.ensure(max_pos / 4 + 64))
+            return ZGPU_MEM_ERROR;
+        if (!c.aux && hipStreamCreateWithFlags(&c.aux, hipStreamNonBlocking) != hipSuccess) {
+            c.aux = nullptr;
+            return ZGPU_MEM_ERROR;
+        }
+        for (int k = 0; k < 2; k++) {
+            if (!c.ev_links[k] && hipEventCreateWithFlags(&c.ev_links[k], hipEventDisableTiming) != hipSuccess)
+                return ZGPU_MEM_ERROR;
+            if (!c.ev_match[k] && hipEventCreateWithFlags(&c.ev_match[k], hipEventDisableTiming) != hipSuccess)
+                return ZGPU_MEM_ERROR;
+        }
+    }
     if (level >= 1 && level <= 3 && !c.ws_heads.ensure(4ull * 32768 * max_cnt)) return ZGPU_MEM_ERROR;
     uint64_t *d_meta = c.ws_meta.as<uint64_t>();
     uint32_t *d_nblk = reinterpret_cast<uint32_t *>(d_meta + 2ull * count);
@@ -307,8 +331,10 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     if (hipMemcpyAsync(d_meta, meta.data(), 16ull * count, hipMemcpyHostToDevice, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
 
-    for (size_t s = 0; s + 1 < cuts.size(); s++) {
+    StageTimer &T = c.timer;
+    auto make_job = [&](size_t s) {
         const uint32_t a = cuts[s], b = cuts[s + 1];
+        const int slot = piped ? (int)(s & 1) : 0;
         DeflateJob job{};
         job.src = src; job.src_off = src_off; job.src_len = src_len;
         job.dst = dst; job.dst_off = dst_off; job.dst_cap = dst_cap;
@@ -316,15 +342,19 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         job.first = a; job.count = b - a; job.level = level; job.wrap = wrap;
         job.ws_off = d_meta + a;
         job.blk_off = d_meta + count + a;
-        job.link = c.ws_link.as<uint16_t>();
-        job.rfull = slow ? c.ws_rf.as<uint32_t>() : nullptr;
-        job.rquart = slow ? c.ws_rq.as<uint32_t>() : nullptr;
+        job.link = (slot ? c.ws_link2 : c.ws_link).as<uint16_t>();
+        job.rfull = slow ? (slot ? c.ws_rf2 : c.ws_rf).as<uint32_t>() : nullptr;
+        job.rquart = slow ? (slot ? c.ws_rq2 : c.ws_rq).as<uint32_t>() : nullptr;
         job.sym = c.ws_sym.as<uint32_t>();
-        job.pstate = slow ? c.ws_state.as<uint32_t>() : nullptr;
+        job.pstate = slow ? (slot ? c.ws_state2 : c.ws_state).as<uint32_t>() : nullptr;
         job.blocks = c.ws_blk.as<BlockRec>();
         job.nblocks = d_nblk;
         job.check = d_check;
-        StageTimer &T = c.timer;
+        return job;
+    };
+    // trailer check value, parse, encode of sub-batch s on the caller's stream
+    auto tail = [&](size_t s, const DeflateJob &job) -> int {
+        const uint32_t a = cuts[s], b = cuts[s + 1];
         int rc = 0;
         if (wrap == 1)
             rc = T.run(0, st, [&] { return launch_adler32(src, src_off + a, src_len + a, nullptr, d_check, b - a, nullptr, 0, st); });
@@ -332,8 +362,6 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             rc = T.run(0, st, [&] { return launch_crc32(src, src_off + a, src_len + a, nullptr, d_check, b - a, nullptr, 0, st); });
         if (rc) return ZGPU_MEM_ERROR;
         if (level >= 4) {
-            if (T.run(1, st, [&] { return launch_deflate_stage(0, job, nullptr, st); })) return ZGPU_MEM_ERROR;
-            if (T.run(2, st, [&] { return launch_deflate_stage(1, job, nullptr, st); })) return ZGPU_MEM_ERROR;
             if (T.run(3, st, [&] { return launch_deflate_stage(5, job, nullptr, st); })) return ZGPU_MEM_ERROR;
             if (T.run(3, st, [&] { return launch_deflate_stage(6, job, nullptr, st); })) return ZGPU_MEM_ERROR;
         } else if (level >= 1) {
@@ -341,8 +369,43 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             if (T.run(4, st, [&] { return launch_deflate_stage(3, job, heads, st); })) return ZGPU_MEM_ERROR;
         }
         if (T.run(5, st, [&] { return launch_deflate_stage(4, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+        return ZGPU_OK;
+    };
+
+    if (!piped) {
+        for (size_t s = 0; s < nsub; s++) {
+            const DeflateJob job = make_job(s);
+            if (level >= 4) {
+                if (T.run(1, st, [&] { return launch_deflate_stage(0, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+                if (T.run(2, st, [&] { return launch_deflate_stage(1, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+            }
+            if (int rc = tail(s, job)) return rc;
+        }
+    } else {
+        // caller's stream: links(0), then per s: links(s+1), [wait match(s)] tail(s)
+        // aux stream:      per s: [wait links(s)] match(s)
+        // Slot s%2 is reused by s+2: links(s+2) follows tail(s) on the caller's
+        // stream, and match(s+2) waits for links(s+2), so neither overwrites a
+        // slot still being read.
+        hipStream_t ax = c.aux;
+        auto links = [&](size_t s) -> int {
+            const DeflateJob job = make_job(s);
+            if (T.run(1, st, [&] { return launch_deflate_stage(0, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+            if (hipEventRecord(c.ev_links[s & 1], st) != hipSuccess) return ZGPU_MEM_ERROR;
+            if (hipStreamWaitEvent(ax, c.ev_links[s & 1], 0) != hipSuccess) return ZGPU_MEM_ERROR;
+            if (T.run(2, ax, [&] { return launch_deflate_stage(1, job, nullptr, ax); })) return ZGPU_MEM_ERROR;
+            if (hipEventRecord(c.ev_match[s & 1], ax) != hipSuccess) return ZGPU_MEM_ERROR;
+            return ZGPU_OK;
+        };
+        if (int rc = links(0)) return rc;
+        for (size_t s = 0; s < nsub; s++) {
+            if (s + 1 < nsub) if (int rc = links(s + 1)) return rc;
+            if (hipStreamWaitEvent(st, c.ev_match[s & 1], 0) != hipSuccess) return ZGPU_MEM_ERROR;
+            if (int rc = tail(s, make_job(s))) return rc;
+        }
     }
     int rc = hip_ok(hipStreamSynchronize(st));
+    if (piped && rc == ZGPU_OK) rc = hip_ok(hipStreamSynchronize(c.aux));
     c.timer.collect();
     return rc;
 }
