@@ -387,7 +387,7 @@ __device__ __attribute__((always_inline)) inline bool mw6_loop(MW3 &w, uint32_t 
 // Variant 8: both words of candidate k+1 (link word and end-bytes word at the
 // current best) are loaded while candidate k is tested; a best-length change
 // (rare) reloads the end-bytes word.
-template <int kUnroll>
+template <int kUnroll, bool kNoCmp = false>
 __device__ __attribute__((always_inline)) inline bool mw8_loop(MW3 &w, uint32_t &em, uint32_t &eb,
                                                                const uint32_t *E, uint32_t end) {
     const char *Eb = reinterpret_cast<const char *>(E);
@@ -398,7 +398,10 @@ __device__ __attribute__((always_inline)) inline bool mw8_loop(MW3 &w, uint32_t 
         const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + a);
         uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
         const uint32_t miss = ((em >> 16) ^ w.scan01) | ((eb >> 16) ^ w.scanE);
-        if (__builtin_expect(miss == 0, 0)) {
+        if (kNoCmp && miss == 0) {           // timing stub: valid but fake lengths
+            if (w.best < 8 && w.best < w.maxcmp) { w.best++; w.bpos4 = w.m4; }
+        }
+        else if (__builtin_expect(miss == 0, 0)) {
             const int m = w.m4 >> 2, s = w.s4 >> 2;
             int k;
             uint32_t x = get4(E, m) ^ get4(E, s);
@@ -431,7 +434,107 @@ __device__ __attribute__((always_inline)) inline bool mw8_loop(MW3 &w, uint32_t 
     }
 }
 
+// Variant 14: mw8's walk with a 16-byte-per-round-trip compare.  The first 16
+// scan bytes are held in registers (loaded once per walk); a hit reads the
+// candidate's first 16 bytes with 4 independent ds_read2 (one LDS round trip)
+// and longer matches continue 16 bytes (both sides) per round trip.
+struct Scan16 { uint32_t s0, s1, s2, s3; };
+
+__device__ __attribute__((always_inline)) inline int cmp16(const uint32_t *E, int m, int s, const Scan16 &S,
+                                                           int maxcmp) {
+    const uint32_t x0 = get4(E, m) ^ S.s0, x1 = get4(E, m + 4) ^ S.s1;
+    const uint32_t x2 = get4(E, m + 8) ^ S.s2, x3 = get4(E, m + 12) ^ S.s3;
+    if (x0) return __builtin_ctz(x0) >> 3;
+    if (x1) return 4 + (__builtin_ctz(x1) >> 3);
+    if (x2) return 8 + (__builtin_ctz(x2) >> 3);
+    if (x3) return 12 + (__builtin_ctz(x3) >> 3);
+    int k = 16;
+    while (k < maxcmp) {
+        const uint32_t y0 = get4(E, m + k) ^ get4(E, s + k);
+        const uint32_t y1 = get4(E, m + k + 4) ^ get4(E, s + k + 4);
+        const uint32_t y2 = get4(E, m + k + 8) ^ get4(E, s + k + 8);
+        const uint32_t y3 = get4(E, m + k + 12) ^ get4(E, s + k + 12);
+        if (y0) return k + (__builtin_ctz(y0) >> 3);
+        if (y1) return k + 4 + (__builtin_ctz(y1) >> 3);
+        if (y2) return k + 8 + (__builtin_ctz(y2) >> 3);
+        if (y3) return k + 12 + (__builtin_ctz(y3) >> 3);
+        k += 16;
+    }
+    return k;
+}
+
 template <int kUnroll>
+__device__ __attribute__((always_inline)) inline bool mw14_loop(MW3 &w, uint32_t &em, uint32_t &eb,
+                                                                const Scan16 &S, const uint32_t *E, uint32_t end) {
+    const char *Eb = reinterpret_cast<const char *>(E);
+#pragma unroll kUnroll
+    for (;;) {
+        const int m4n = w.m4 - (int)((em & 0xffffu) << 2);
+        const int a = m4n > 0 ? m4n : 0;
+        const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + a);
+        uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
+        const uint32_t miss = ((em >> 16) ^ w.scan01) | ((eb >> 16) ^ w.scanE);
+        if (__builtin_expect(miss == 0, 0)) {
+            const int m = w.m4 >> 2, s = w.s4 >> 2;
+            const int k = cmp16(E, m, s, S, w.maxcmp);
+            const int len = k < w.maxcmp ? k : w.maxcmp;
+            if (len > w.best) {
+                w.best = len;
+                w.bpos4 = w.m4;
+                if (len >= w.nice) w.limit4 = 0x7fffffff;
+                w.be4 = (len - 1) * 4;
+                w.scanE = E[s + len - 1] >> 16;
+                ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
+            }
+        }
+        w.count++;
+        w.m4 = m4n;
+        em = emn;
+        eb = ebn;
+        if (m4n <= w.limit4) return true;
+        if (w.count >= end) return false;
+    }
+}
+
+template <int kUnroll>
+__device__ __attribute__((always_inline)) inline void mw14_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
+                                                                const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
+                                                                int want_q) {
+    const int s = (int)(p - B);
+    const uint32_t e0 = E[s];
+    const uint32_t d0 = e0 & 0xffffu;
+    if (d0 > (uint32_t)kMaxDist) {
+        rf[p] = 0;
+        if (want_q) rq[p] = 0;
+        return;
+    }
+    MW3 w;
+    const int64_t labs = p > kMaxDist ? p - kMaxDist : 0;
+    w.limit4 = (int)(labs - B) * 4;
+    const int64_t rem = n - p;
+    w.nice = rem < cfg.nice ? (int)rem : cfg.nice;
+    w.maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
+    w.s4 = s * 4;
+    w.m4 = (s - (int)d0) * 4;
+    w.best = kMinMatch - 1;
+    w.bpos4 = 0;
+    w.be4 = (kMinMatch - 2) * 4;
+    w.scan01 = e0 >> 16;
+    w.scanE = E[s + 1] >> 16;
+    w.count = 0;
+    Scan16 S{get4(E, s), get4(E, s + 4), get4(E, s + 8), get4(E, s + 12)};
+    uint32_t em = E[s - (int)d0];
+    uint32_t eb = E[s - (int)d0 + 1];
+    const uint32_t qc = want_q ? (uint32_t)(cfg.chain >> 2) : (uint32_t)cfg.chain;
+    const bool done = mw14_loop<kUnroll>(w, em, eb, S, E, qc);
+    if (want_q) {
+        rq[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
+        if (!done) mw14_loop<kUnroll>(w, em, eb, S, E, (uint32_t)cfg.chain);
+    }
+    rf[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
+}
+
+template <int kUnroll, bool kNoCmp = false>
 __device__ __attribute__((always_inline)) inline void mw8_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
                                                                const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
                                                                int want_q) {
@@ -460,12 +563,238 @@ __device__ __attribute__((always_inline)) inline void mw8_walk(const uint32_t *E
     uint32_t em = E[s - (int)d0];
     uint32_t eb = E[s - (int)d0 + 1];
     const uint32_t qc = want_q ? (uint32_t)(cfg.chain >> 2) : (uint32_t)cfg.chain;
-    const bool done = mw8_loop<kUnroll>(w, em, eb, E, qc);
+    const bool done = mw8_loop<kUnroll, kNoCmp>(w, em, eb, E, qc);
     if (want_q) {
         rq[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
-        if (!done) mw8_loop<kUnroll>(w, em, eb, E, (uint32_t)cfg.chain);
+        if (!done) mw8_loop<kUnroll, kNoCmp>(w, em, eb, E, (uint32_t)cfg.chain);
     }
     rf[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
+}
+
+// Variant 10: mw8's step without per-lane loop exits.  All lanes of the wave
+// start their walks together, so the candidate count is wave-uniform; a lane
+// whose walk has ended keeps a `done` flag and stops committing state, and the
+// wave leaves the loop when all lanes are done (tested every kU steps) or the
+// count reaches `end`.  The only divergent branch left is the full compare.
+template <int kU>
+__device__ __attribute__((always_inline)) inline void mw10_loop(MW3 &w, uint32_t &em, uint32_t &eb, bool &done,
+                                                                const uint32_t *E, uint32_t &count, uint32_t end) {
+    const char *Eb = reinterpret_cast<const char *>(E);
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int m4n = w.m4 - (int)((em & 0xffffu) << 2);
+            const int a = m4n > 0 ? m4n : 0;
+            const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + a);
+            uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
+            const uint32_t miss = ((em >> 16) ^ w.scan01) | ((eb >> 16) ^ w.scanE) | (uint32_t)done;
+            if (__builtin_expect(miss == 0, 0)) {
+                const int m = w.m4 >> 2, s = w.s4 >> 2;
+                int k;
+                uint32_t x = get4(E, m) ^ get4(E, s);
+                if (x) k = __builtin_ctz(x) >> 3;
+                else {
+                    k = 4;
+                    for (;;) {
+                        if (k >= w.maxcmp) break;
+                        x = get4(E, s + k) ^ get4(E, m + k);
+                        if (x) { k += __builtin_ctz(x) >> 3; break; }
+                        k += 4;
+                    }
+                }
+                const int len = k < w.maxcmp ? k : w.maxcmp;
+                if (len > w.best) {
+                    w.best = len;
+                    w.bpos4 = w.m4;
+                    if (len >= w.nice) w.limit4 = 0x7fffffff;
+                    w.be4 = (len - 1) * 4;
+                    w.scanE = E[s + len - 1] >> 16;
+                    ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
+                }
+            }
+            // a finished lane keeps walking garbage (addresses stay clamped into
+            // the window) but never compares again, so no state is frozen and
+            // the next words are not waited for here
+            count++;
+            done = done || m4n <= w.limit4;
+            w.m4 = m4n;
+            em = emn;
+            eb = ebn;
+            if (count >= end) return;
+        }
+        if (__all(done)) return;
+    }
+}
+
+template <int kU>
+__device__ __attribute__((always_inline)) inline void mw10_walk(const uint32_t *E, int64_t p, bool have,
+                                                                int64_t B, int64_t n, const LevelCfg &cfg,
+                                                                uint32_t *rf, uint32_t *rq, int want_q) {
+    const int s = have ? (int)(p - B) : 0;
+    const uint32_t e0 = E[s];
+    const uint32_t d0 = e0 & 0xffffu;
+    bool done = !have || d0 > (uint32_t)kMaxDist;
+    if (have && done) {
+        rf[p] = 0;
+        if (want_q) rq[p] = 0;
+    }
+    MW3 w;
+    const int64_t labs = p > kMaxDist ? p - kMaxDist : 0;
+    w.limit4 = (int)(labs - B) * 4;
+    const int64_t rem = n - p;
+    w.nice = rem < cfg.nice ? (int)rem : cfg.nice;
+    w.maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
+    w.s4 = s * 4;
+    const int m0 = done ? s : s - (int)d0;
+    w.m4 = m0 * 4;
+    w.best = kMinMatch - 1;
+    w.bpos4 = 0;
+    w.be4 = (kMinMatch - 2) * 4;
+    w.scan01 = e0 >> 16;
+    w.scanE = E[s + 1] >> 16;
+    uint32_t em = E[m0];
+    uint32_t eb = E[m0 + 1];
+    const bool skip = done;
+    if (__all(done)) return;
+    uint32_t count = 0;
+    const uint32_t qc = want_q ? (uint32_t)(cfg.chain >> 2) : (uint32_t)cfg.chain;
+    mw10_loop<kU>(w, em, eb, done, E, count, qc);
+    if (want_q) {
+        if (!skip)
+            rq[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
+        if (!__all(done)) mw10_loop<kU>(w, em, eb, done, E, count, (uint32_t)cfg.chain);
+    }
+    if (!skip) rf[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
+}
+
+// Variant 11: kW independent walks per lane in lockstep (mw10's step), so a
+// lane keeps kW LDS pointer chases in flight.
+struct MW11 {
+    MW3 w;
+    uint32_t em, eb;
+    bool done, skip;
+    int64_t p;
+};
+
+__device__ __attribute__((always_inline)) inline void mw11_step(MW11 &x, const uint32_t *E) {
+    const char *Eb = reinterpret_cast<const char *>(E);
+    MW3 &w = x.w;
+    const int m4n = w.m4 - (int)((x.em & 0xffffu) << 2);
+    const int a = m4n > 0 ? m4n : 0;
+    const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + a);
+    uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
+    const uint32_t miss = ((x.em >> 16) ^ w.scan01) | ((x.eb >> 16) ^ w.scanE) | (uint32_t)x.done;
+    if (__builtin_expect(miss == 0, 0)) {
+        const int m = w.m4 >> 2, s = w.s4 >> 2;
+        int k;
+        uint32_t xx = get4(E, m) ^ get4(E, s);
+        if (xx) k = __builtin_ctz(xx) >> 3;
+        else {
+            k = 4;
+            for (;;) {
+                if (k >= w.maxcmp) break;
+                xx = get4(E, s + k) ^ get4(E, m + k);
+                if (xx) { k += __builtin_ctz(xx) >> 3; break; }
+                k += 4;
+            }
+        }
+        const int len = k < w.maxcmp ? k : w.maxcmp;
+        if (len > w.best) {
+            w.best = len;
+            w.bpos4 = w.m4;
+            if (len >= w.nice) w.limit4 = 0x7fffffff;
+            w.be4 = (len - 1) * 4;
+            w.scanE = E[s + len - 1] >> 16;
+            ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
+        }
+    }
+    x.done = x.done || m4n <= w.limit4;
+    w.m4 = m4n;
+    x.em = emn;
+    x.eb = ebn;
+}
+
+__device__ __attribute__((always_inline)) inline void mw11_init(MW11 &x, const uint32_t *E, int64_t p, bool have,
+                                                                int64_t B, int64_t n, const LevelCfg &cfg,
+                                                                uint32_t *rf, uint32_t *rq, int want_q) {
+    const int s = have ? (int)(p - B) : 0;
+    const uint32_t e0 = E[s];
+    const uint32_t d0 = e0 & 0xffffu;
+    x.p = p;
+    x.done = !have || d0 > (uint32_t)kMaxDist;
+    x.skip = x.done;
+    if (have && x.done) {
+        rf[p] = 0;
+        if (want_q) rq[p] = 0;
+    }
+    MW3 &w = x.w;
+    const int64_t labs = p > kMaxDist ? p - kMaxDist : 0;
+    w.limit4 = (int)(labs - B) * 4;
+    const int64_t rem = n - p;
+    w.nice = rem < cfg.nice ? (int)rem : cfg.nice;
+    w.maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
+    w.s4 = s * 4;
+    const int m0 = x.done ? s : s - (int)d0;
+    w.m4 = m0 * 4;
+    w.best = kMinMatch - 1;
+    w.bpos4 = 0;
+    w.be4 = (kMinMatch - 2) * 4;
+    w.scan01 = e0 >> 16;
+    w.scanE = E[s + 1] >> 16;
+    x.em = E[m0];
+    x.eb = E[m0 + 1];
+}
+
+__device__ __attribute__((always_inline)) inline uint32_t mw11_result(const MW11 &x) {
+    return x.w.best >= kMinMatch ? (((uint32_t)x.w.best << 16) | (uint32_t)((x.w.s4 - x.w.bpos4) >> 2)) : 0u;
+}
+
+template <int kW, int kU>
+__device__ __attribute__((always_inline)) inline void mw11_loop(MW11 (&x)[kW], const uint32_t *E, uint32_t &count,
+                                                                uint32_t end) {
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+#pragma unroll
+            for (int k = 0; k < kW; k++) mw11_step(x[k], E);
+            count++;
+            if (count >= end) return;
+        }
+        bool all = true;
+#pragma unroll
+        for (int k = 0; k < kW; k++) all = all && x[k].done;
+        if (__all(all)) return;
+    }
+}
+
+template <int kW, int kU>
+__device__ __attribute__((always_inline)) inline void mw11_walks(const uint32_t *E, int64_t p0, int64_t lim,
+                                                                 int64_t B, int64_t n, const LevelCfg &cfg,
+                                                                 uint32_t *rf, uint32_t *rq, int want_q) {
+    MW11 x[kW];
+    bool all = true;
+#pragma unroll
+    for (int k = 0; k < kW; k++) {
+        const int64_t p = p0 + 64 * k;
+        mw11_init(x[k], E, p, p < lim, B, n, cfg, rf, rq, want_q);
+        all = all && x[k].done;
+    }
+    if (__all(all)) return;
+    uint32_t count = 0;
+    const uint32_t qc = want_q ? (uint32_t)(cfg.chain >> 2) : (uint32_t)cfg.chain;
+    mw11_loop<kW, kU>(x, E, count, qc);
+    if (want_q) {
+        all = true;
+#pragma unroll
+        for (int k = 0; k < kW; k++) {
+            if (!x[k].skip) rq[x[k].p] = mw11_result(x[k]);
+            all = all && x[k].done;
+        }
+        if (!__all(all)) mw11_loop<kW, kU>(x, E, count, (uint32_t)cfg.chain);
+    }
+#pragma unroll
+    for (int k = 0; k < kW; k++)
+        if (!x[k].skip) rf[x[k].p] = mw11_result(x[k]);
 }
 
 template <int kUnroll>
@@ -527,7 +856,44 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
         match_tile_load(E, ts, n, in, L, tid);
         if (tid == 0) next_i = 0;
         __syncthreads();
-        if (kVariant == 8 || kVariant == 9) {
+        if (kVariant == 14) {
+            for (;;) {
+                const int i = atomicAdd(&next_i, 1);
+                const int64_t p = ts + i;
+                if (i >= kMT || p >= n) break;
+                mw14_walk<2>(E, p, B, n, cfg, rf, rq, want_q);
+            }
+        } else if (kVariant == 13) {
+            for (;;) {
+                const int i = atomicAdd(&next_i, 1);
+                const int64_t p = ts + i;
+                if (i >= kMT || p >= n) break;
+                mw8_walk<2, true>(E, p, B, n, cfg, rf, rq, want_q);
+            }
+        } else if (kVariant == 11 || kVariant == 12) {
+            constexpr int kW = kVariant == 11 ? 2 : 3;
+            const int lane = tid & 63;
+            const int64_t lim = (ts + kMT < n) ? ts + kMT : n;
+            for (;;) {
+                int i0 = 0;
+                if (lane == 0) i0 = atomicAdd(&next_i, 64 * kW);
+                i0 = __shfl(i0, 0, 64);
+                if (i0 >= kMT || ts + i0 >= n) break;
+                mw11_walks<kW, 2>(E, ts + i0 + lane, lim, B, n, cfg, rf, rq, want_q);
+            }
+        } else if (kVariant == 10) {
+            // wave-synchronous: a wave takes 64 consecutive positions at a time
+            const int lane = tid & 63;
+            for (;;) {
+                int i0 = 0;
+                if (lane == 0) i0 = atomicAdd(&next_i, 64);
+                i0 = __shfl(i0, 0, 64);
+                if (i0 >= kMT || ts + i0 >= n) break;
+                const int64_t p = ts + i0 + lane;
+                const bool have = i0 + lane < kMT && p < n;
+                mw10_walk<4>(E, p, have, B, n, cfg, rf, rq, want_q);
+            }
+        } else if (kVariant == 8 || kVariant == 9) {
             for (;;) {
                 const int i = atomicAdd(&next_i, 1);
                 const int64_t p = ts + i;
@@ -1655,15 +2021,20 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     case 1: {
         static const int variant = [] {
             const char *e = getenv("ZGPU_MATCH_VARIANT");
-            return e ? atoi(e) : 9;
+            return e ? atoi(e) : 14;
         }();
         const int wq = (int)(job.level >= 5);
         if (variant == 0) hipLaunchKernelGGL(k_match<0>, grid, dim3(kMatchThreads), 0, st, job, wq);
         else if (variant == 6) hipLaunchKernelGGL(k_match<6>, grid, dim3(kMatchThreads), 0, st, job, wq);
         else if (variant == 8) hipLaunchKernelGGL(k_match<8>, grid, dim3(kMatchThreads), 0, st, job, wq);
         else if (variant == 9) hipLaunchKernelGGL(k_match<9>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        else if (variant == 10) hipLaunchKernelGGL(k_match<10>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        else if (variant == 11) hipLaunchKernelGGL(k_match<11>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        else if (variant == 13) hipLaunchKernelGGL(k_match<13>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        else if (variant == 14) hipLaunchKernelGGL(k_match<14>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        else if (variant == 12) hipLaunchKernelGGL(k_match<12>, grid, dim3(kMatchThreads), 0, st, job, wq);
         else if (variant == 7) hipLaunchKernelGGL(k_match<7>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        else hipLaunchKernelGGL(k_match<9>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        else hipLaunchKernelGGL(k_match<14>, grid, dim3(kMatchThreads), 0, st, job, wq);
         break;
     }
     case 2: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 0); break;
