@@ -45,6 +45,14 @@ import zgpu  # noqa: E402
 
 METRIC = "compress MB/s @ level 6 + CRC32 GB/s, batched 1 MB buffers, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+KIND_DATA = {
+    "silesia": "synthetic: device-generated seeded Silesia-style 64 KiB-segment mix "
+               "(40% text, 20% markup, 20% binary records, 10% random, 10% runs)",
+    "enwik": "synthetic: device-generated seeded enwik-style 4 KiB segments (70% word text, 30% markup)",
+    "vocab": "synthetic: device-generated seeded small-vocabulary text",
+    "random": "synthetic: device-generated uniform random bytes",
+}
+KIND_CONFIG = {"silesia": "C4 per-GPU shard", "enwik": "C3-style", "vocab": "C5-style", "random": "random"}
 
 
 def parse():
@@ -56,6 +64,8 @@ def parse():
                     help="1 MiB buffers per GPU (C4 shard = 32768)")
     ap.add_argument("--buffer-bytes", type=int, default=1 << 20)
     ap.add_argument("--level", type=int, default=6)
+    ap.add_argument("--kind", default="silesia", choices=["random", "silesia", "enwik", "vocab"],
+                    help="device generator: silesia (C4, default), enwik (C3), vocab (C5)")
     ap.add_argument("--crc-buffers", type=int, default=1 << 20)
     ap.add_argument("--crc-bytes", type=int, default=4096)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -110,7 +120,8 @@ def deflate_leg(a, world, rank):
     first, _ = shard(rank, world, B)
     cap = (zgpu.compress_bound(n) + 15) // 16 * 16
     src = torch.empty(n * B, dtype=torch.uint8, device="cuda")
-    zgpu.generate_dev(src, n, B, zgpu.KIND_SILESIA, seed=2025, first_index=first)
+    kind = {"random": 0, "silesia": 1, "enwik": 2, "vocab": 3}[a.kind]
+    zgpu.generate_dev(src, n, B, kind, seed=2025, first_index=first)
     off = torch.arange(B, dtype=torch.int64, device="cuda") * n
     ln = torch.full((B,), n, dtype=torch.int64, device="cuda")
     dst = torch.empty(cap * B, dtype=torch.uint8, device="cuda")
@@ -318,9 +329,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic: device-generated seeded Silesia-style 64 KiB-segment mix "
-                    "(40% text, 20% markup, 20% binary records, 10% random, 10% runs)",
-            "config": {"workload": f"C4 per-GPU shard: {a.buffers} x {a.buffer_bytes} B buffers, "
+            "data": KIND_DATA[a.kind],
+            "config": {"workload": f"{KIND_CONFIG[a.kind]}: {a.buffers} x {a.buffer_bytes} B buffers, "
                                    f"deflate level {a.level}, zlib wrapper, inputs+outputs in HBM",
                        "level": a.level, "buffer_bytes": a.buffer_bytes,
                        "buffers_per_gpu": a.buffers, "inflight_mb": a.inflight_mb,
