@@ -235,3 +235,36 @@ def test_crc_adler_many_small_ragged(zg, oracle):
     got = zg.adler32_batch(bufs)
     for b, g in zip(bufs, got):
         assert g == oracle.adler32(b), len(b)
+
+
+@pytest.mark.parametrize("level", [4, 6, 9])
+def test_pipeline_many_subbatches(zg, oracle, level):
+    """A small in-flight budget splits the batch into many sub-batches, so the
+    two-stream L4-9 pipeline runs and reuses both workspace slots."""
+    rng = np.random.default_rng(200 + level)
+    bufs = []
+    for t in range(40):
+        kind = ["text", "runs", "four", "random", "mix", "markup", "records"][t % 7]
+        n = int(rng.choice([0, 1, 300, int(rng.integers(300, 120000)), int(rng.integers(120000, 300000))]))
+        bufs.append(datagen.make(kind, n, int(rng.integers(0, 1 << 30))))
+    old = zg.set_inflight_bytes(300 * 1024)
+    try:
+        for wrap in (0, 1, 2):
+            res = zg.compress_batch(bufs, level=level, wrap=wrap)
+            for b, (st, z) in zip(bufs, res):
+                assert st == 0 and z == oracle.compress(b, level, wrap=wrap)[1], (len(b), level, wrap)
+    finally:
+        zg.set_inflight_bytes(old)
+
+
+def test_deflate_pathological_sync(zg, oracle):
+    """Inputs where speculative lazy-parse segments may never meet (runs,
+    short and long periods), plus the k_parse_slow fallback they can take."""
+    n = 1 << 20
+    pat3 = (b"abc" * (n // 3 + 1))[:n]
+    pat257 = (bytes(range(256)) + b"!") * (n // 257 + 1)
+    bufs = [bytes(n), pat3, pat257[:n], datagen.make("runs", n, 9), (b"\x00" * 258 + b"\x01") * 4000]
+    for level in (4, 6, 9):
+        for b, (st, z) in zip(bufs, zg.compress_batch(bufs, level=level)):
+            assert st == 0 and z == oracle.compress(b, level)[1], (len(b), level)
+            assert pyzlib.decompress(z) == b
