@@ -313,7 +313,7 @@ def main():
         if not a.no_cpu and sample:
             v, threads, tot = cpu_baseline(a, sample, a.level)
             cpu = {"value": round(v, 2), "unit": "MB/s", "cores": threads, "kind": "port",
-                   "sample": f"{len(sample)} distinct 1 MiB Silesia-mix buffers of this batch, "
+                   "sample": f"{len(sample)} distinct 1 MiB {a.kind} buffers of this batch, "
                              f"compressed repeatedly at level {a.level} for ~{a.cpu_seconds:.0f} s "
                              f"({tot / 1e6:.0f} MB) by oracle/liboracle.so on {threads} host threads",
                    "system_zlib": system_zlib_baseline(a, sample, a.level, want)}

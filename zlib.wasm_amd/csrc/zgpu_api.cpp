@@ -271,12 +271,16 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         hipStreamSynchronize(st) != hipSuccess)
         return ZGPU_MEM_ERROR;
 
-    // plan sub-batches: Σ n <= inflight (a single larger buffer runs alone)
+    // plan sub-batches: Σ n <= budget (a single larger buffer runs alone).  L1-3
+    // keep ~6 B of workspace per in-flight byte (L4-9: ~25) and their parse is
+    // one sequential lane per buffer, so they get 4x the budget: more buffers
+    // in flight is what their throughput scales with.
+    const uint64_t budget = (level >= 1 && level <= 3) ? 4 * (uint64_t)c.inflight : (uint64_t)c.inflight;
     std::vector<uint32_t> cuts{0};
     {
         uint64_t acc = 0;
         for (uint32_t i = 0; i < count; i++) {
-            if (acc > 0 && acc + lens[i] > c.inflight) { cuts.push_back(i); acc = 0; }
+            if (acc > 0 && acc + lens[i] > budget) { cuts.push_back(i); acc = 0; }
             acc += lens[i];
         }
         cuts.push_back(count);
