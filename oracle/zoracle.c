@@ -393,6 +393,7 @@ typedef struct {
     uint16_t *link;
     uint32_t *rfull, *rquart;
     uint8_t  *ins;             /* inserted-set bitmap (levels 1..3, pp) */
+    int strategy;              /* Z_DEFAULT_STRATEGY 0, Z_FILTERED 1, Z_HUFFMAN_ONLY 2, Z_RLE 3, Z_FIXED 4 */
     /* window schedule: S = slide offset, E = end of data read so far */
     size_t S, E;
     size_t block_start;
@@ -474,7 +475,7 @@ static void flush_block(zs_t *s, size_t strstart, int last) {
 
     uint64_t opt_lenb = ((uint64_t)h->opt_len + 3 + 7) >> 3;
     uint64_t static_lenb = ((uint64_t)h->static_len + 3 + 7) >> 3;
-    if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+    if (static_lenb <= opt_lenb || s->strategy == ZO_FIXED) opt_lenb = static_lenb;   /* trees.c:1035 */
 
     bw_t *w = &s->bw;
     if (stored_len + 4 <= opt_lenb && have_buf) {      /* _tr_stored_block, trees.c:860-875 */
@@ -665,7 +666,8 @@ static void run_slow(zs_t *s) {
             } else {
                 match_length = longest_match_seq(s, p, hh, prev_length, &match_start);
             }
-            if (match_length <= 5 && match_length == MIN_MATCH && p - match_start > TOO_FAR)
+            if (match_length <= 5 && (s->strategy == ZO_FILTERED ||          /* deflate.c:1964-1975 */
+                                      (match_length == MIN_MATCH && p - match_start > TOO_FAR)))
                 match_length = MIN_MATCH - 1;
         }
         if (prev_length >= MIN_MATCH && match_length <= prev_length) {
@@ -686,6 +688,54 @@ static void run_slow(zs_t *s) {
         }
     }
     if (match_available) tally_lit(s, s->in[p - 1]);
+    flush_block(s, p, 1);
+}
+
+/* deflate_rle (deflate.c:2051-2116): runs of the previous byte at distance 1.
+ * fill_window when lookahead <= MAX_MATCH. */
+static void run_rle(zs_t *s) {
+    size_t p = 0;
+    for (;;) {
+        if (s->E - p <= MAX_MATCH) {
+            fill(s, p);
+            if (s->E == p) break;
+        }
+        const size_t lookahead = s->E - p;
+        unsigned match_length = 0;
+        if (lookahead >= MIN_MATCH && p > 0) {
+            const uint8_t prev = s->in[p - 1];
+            if (s->in[p] == prev && s->in[p + 1] == prev && s->in[p + 2] == prev) {
+                unsigned len = 3;                          /* run length, capped at MAX_MATCH */
+                while (len < MAX_MATCH && p + len < s->n && s->in[p + len] == prev) len++;
+                match_length = len <= lookahead ? len : (unsigned)lookahead;
+            }
+        }
+        int bflush;
+        if (match_length >= MIN_MATCH) {
+            bflush = tally_dist(s, 1, match_length - MIN_MATCH);
+            p += match_length;
+        } else {
+            bflush = tally_lit(s, s->in[p]);
+            p++;
+        }
+        if (bflush) flush_block(s, p, 0);
+    }
+    flush_block(s, p, 1);
+}
+
+/* deflate_huff (deflate.c:2122-2152): literals only; fill_window when the
+ * lookahead is 0. */
+static void run_huff(zs_t *s) {
+    size_t p = 0;
+    for (;;) {
+        if (s->E == p) {
+            fill(s, p);
+            if (s->E == p) break;
+        }
+        const int bflush = tally_lit(s, s->in[p]);
+        p++;
+        if (bflush) flush_block(s, p, 0);
+    }
     flush_block(s, p, 1);
 }
 
@@ -777,7 +827,8 @@ static int assemble(zs_t *s, uint8_t *dst, size_t *dst_len, int wrap) {
     size_t hlen = 0;
     if (wrap == 1) {
         unsigned header = (8u + ((15u - 8u) << 4)) << 8;
-        unsigned flags = s->level < 2 ? 0u : s->level < 6 ? 1u : s->level == 6 ? 2u : 3u;
+        unsigned flags = (s->strategy >= ZO_HUFFMAN_ONLY || s->level < 2) ? 0u  /* deflate.c:1009-1016 */
+                         : s->level < 6 ? 1u : s->level == 6 ? 2u : 3u;
         header |= flags << 6;
         header += 31 - (header % 31);
         hdr[0] = (uint8_t)(header >> 8);
@@ -786,7 +837,7 @@ static int assemble(zs_t *s, uint8_t *dst, size_t *dst_len, int wrap) {
     } else if (wrap == 2) {
         static const uint8_t g[10] = {31, 139, 8, 0, 0, 0, 0, 0, 0, 3};
         memcpy(hdr, g, 10);
-        hdr[8] = s->level == 9 ? 2 : s->level < 2 ? 4 : 0;
+        hdr[8] = s->level == 9 ? 2 : (s->strategy >= ZO_HUFFMAN_ONLY || s->level < 2) ? 4 : 0;  /* :1052 */
         hlen = 10;
     }
     uint8_t trl[8];
@@ -813,10 +864,11 @@ static int assemble(zs_t *s, uint8_t *dst, size_t *dst_len, int wrap) {
 }
 
 static int compress_common(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
-                           int level, int wrap, int pp) {
+                           int level, int wrap, int pp, int strategy) {
     init_tables();
     if (level == -1) level = 6;
     if (level < 0 || level > 9 || wrap < 0 || wrap > 2 || !dst_len) return ZO_STREAM_ERROR;
+    if (strategy < 0 || strategy > ZO_FIXED) return ZO_STREAM_ERROR;
     if (n && !src) return ZO_STREAM_ERROR;
     if (!dst) { *dst_len = 0; return ZO_STREAM_ERROR; }
     zs_t *s = (zs_t *)calloc(1, sizeof(zs_t));
@@ -826,6 +878,7 @@ static int compress_common(uint8_t *dst, size_t *dst_len, const uint8_t *src, si
     s->level = level;
     s->cfg = CFG[level];
     s->pp = pp;
+    s->strategy = strategy;
     int rc = ZO_MEM_ERROR;
     size_t nn = n ? n : 1;
     if (pp) {
@@ -845,7 +898,10 @@ static int compress_common(uint8_t *dst, size_t *dst_len, const uint8_t *src, si
         if (!s->head || !s->prev) goto out;
     }
     block_reset(s);
+    /* deflate.c:1190-1193 */
     if (level == 0) run_stored(s);
+    else if (strategy == ZO_HUFFMAN_ONLY) run_huff(s);
+    else if (strategy == ZO_RLE) run_rle(s);
     else if (level <= 3) run_fast(s);
     else run_slow(s);
     rc = assemble(s, dst, dst_len, wrap);
@@ -858,10 +914,15 @@ out:
 
 int zo_compress(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
                 int level, int wrap) {
-    return compress_common(dst, dst_len, src, n, level, wrap, 0);
+    return compress_common(dst, dst_len, src, n, level, wrap, 0, 0);
+}
+
+int zo_compress2(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
+                 int level, int wrap, int strategy) {
+    return compress_common(dst, dst_len, src, n, level, wrap, 0, strategy);
 }
 
 int zo_pp_compress(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
                    int level, int wrap) {
-    return compress_common(dst, dst_len, src, n, level, wrap, 1);
+    return compress_common(dst, dst_len, src, n, level, wrap, 1, 0);
 }

@@ -31,6 +31,13 @@
 unsigned long zo_compress_bound(unsigned long n);
 int zo_compress(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
                 int level, int wrap);
+/* strategies (zlib.h:197-201): deflateInit2_(strategy) semantics */
+#define ZO_FILTERED     1
+#define ZO_HUFFMAN_ONLY 2
+#define ZO_RLE          3
+#define ZO_FIXED        4
+int zo_compress2(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
+                 int level, int wrap, int strategy);
 
 uint32_t zo_crc32(uint32_t crc, const uint8_t *buf, size_t len);
 uint32_t zo_adler32(uint32_t adler, const uint8_t *buf, size_t len);

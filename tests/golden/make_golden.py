@@ -10,7 +10,8 @@ The fixture holds, per case, the input's sha256 (inputs are regenerated from
 tests/datagen.py with the recorded kind/size/seed), the reference's
 compress2() output length + sha256 for levels 0..9, the full output bytes for
 small cases, raw-deflate (windowBits -15) and gzip (31) outputs for level 6,
-and crc32/adler32 values, plus a few public known answers.
+deflateInit2_ strategy outputs (1..4 at levels 1/4/6/9), and crc32/adler32
+values, plus a few public known answers.
 """
 import hashlib
 import json
@@ -38,6 +39,9 @@ CASES.append(("runs", 1 << 20, 13))
 FULL_BYTES_MAX = 4096
 
 
+STRATEGY_MAX_N = 1 << 20
+
+
 def main():
     ref = Reference()
     out = {"reference": ref.version.decode(), "cases": [], "known": {}}
@@ -57,6 +61,15 @@ def main():
         for name, wbits in (("raw6", -15), ("gzip6", 31)):
             z = ref.deflate(data, 6, wbits)
             case[name] = {"len": len(z), "sha256": hashlib.sha256(z).hexdigest()}
+        # deflateInit2_ strategies 1..4 (Z_FILTERED, Z_HUFFMAN_ONLY, Z_RLE,
+        # Z_FIXED), zlib wrapper, levels 1/4/6/9
+        if n <= STRATEGY_MAX_N:
+            case["strategies"] = {}
+            for strategy in (1, 2, 3, 4):
+                for level in (1, 4, 6, 9):
+                    z = ref.deflate(data, level, 15, strategy=strategy)
+                    case["strategies"][f"{strategy}/{level}"] = {
+                        "len": len(z), "sha256": hashlib.sha256(z).hexdigest()}
         out["cases"].append(case)
     for s in (b"", b"123456789", b"Hello, World!", b"a"):
         out["known"][s.hex()] = {"crc32": ref.crc32(s), "adler32": ref.adler32(s),

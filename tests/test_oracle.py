@@ -125,3 +125,34 @@ def test_reference_chunked_input_equals_one_shot():
         one = ref.deflate(data, lvl, 15)
         for chunk in (1000, 4096, 65536):
             assert ref.deflate(data, lvl, 15, chunk=chunk) == one
+
+
+@pytest.mark.skipif(not reference_available(), reason="compiled reference only in the build container")
+@pytest.mark.parametrize("strategy", [1, 2, 3, 4], ids=["filtered", "huffman_only", "rle", "fixed"])
+def test_oracle_strategies_vs_reference(oracle, strategy):
+    """deflateInit2_(strategy) of the compiled reference (deflate.c:1190-1193,
+    1964, 2051-2152, trees.c:1035) against the oracle, all levels and wrappers,
+    including sizes around the window slides of each parser."""
+    ref = Reference()
+    rng = np.random.default_rng(300 + strategy)
+    sizes = [0, 1, 2, 3, 4, 258, 259, 262, 16383, 16384, 65273, 65274, 65275, 65278, 65536,
+             65537, 98304, 200000]
+    for t, n in enumerate(sizes):
+        kind = ["runs", "text", "mix", "random", "records", "four"][t % 6]
+        data = datagen.make(kind, n, int(rng.integers(0, 1 << 30)))
+        for level in (0, 1, 4, 6, 9):
+            for wbits, wrap in ((15, 1), (-15, 0), (31, 2)):
+                want = ref.deflate(data, level, wbits=wbits, strategy=strategy)
+                rc, got = oracle.compress(data, level, wrap=wrap, strategy=strategy)
+                assert rc == 0 and got == want, (kind, n, level, wrap, strategy)
+
+
+def test_oracle_strategies_golden(oracle, golden):
+    """Oracle vs the committed strategy fixtures (compiled-reference outputs)."""
+    for c in _cases(golden, maxn=70000):
+        data = datagen.make(c["kind"], c["n"], c["seed"])
+        for key, want in c["strategies"].items():
+            strategy, level = (int(x) for x in key.split("/"))
+            rc, z = oracle.compress(data, level, wrap=1, strategy=strategy)
+            assert rc == 0 and len(z) == want["len"] and hashlib.sha256(z).hexdigest() == want["sha256"], \
+                (c["kind"], c["n"], key)

@@ -36,6 +36,8 @@ class Oracle:
                                   C.c_size_t, C.c_int, C.c_int]
         L.zo_pp_compress.restype = C.c_int
         L.zo_pp_compress.argtypes = L.zo_compress.argtypes
+        L.zo_compress2.restype = C.c_int
+        L.zo_compress2.argtypes = L.zo_compress.argtypes + [C.c_int]
         for f in ("zo_crc32", "zo_adler32"):
             getattr(L, f).restype = C.c_uint32
             getattr(L, f).argtypes = [C.c_uint32, C.c_void_p, C.c_size_t]
@@ -56,7 +58,10 @@ class Oracle:
         rc = fn(out, C.byref(n), data, len(data), level, wrap)
         return rc, out.raw[: n.value]
 
-    def compress(self, data, level=6, wrap=1, cap=None):
+    def compress(self, data, level=6, wrap=1, cap=None, strategy=0):
+        if strategy:
+            return self._compress(lambda o, n, d, ln, lv, w: self.L.zo_compress2(o, n, d, ln, lv, w, strategy),
+                                  data, level, wrap, cap)
         return self._compress(self.L.zo_compress, data, level, wrap, cap)
 
     def pp_compress(self, data, level=6, wrap=1, cap=None):
@@ -131,12 +136,12 @@ class Reference:
         rc = self.L.compress2(out, C.byref(n), data, len(data), level)
         return rc, out.raw[: n.value]
 
-    def deflate(self, data, level=6, wbits=15, chunk=None):
+    def deflate(self, data, level=6, wbits=15, chunk=None, strategy=0):
         """deflateInit2 + deflate; wbits -15 raw, 15 zlib, 31 gzip.  ``chunk``
         feeds the input in pieces with Z_NO_FLUSH before Z_FINISH."""
         data = bytes(data)
         strm = ZStream()
-        rc = self.L.deflateInit2_(C.byref(strm), level, 8, wbits, 8, 0, self.version,
+        rc = self.L.deflateInit2_(C.byref(strm), level, 8, wbits, 8, strategy, self.version,
                                   C.sizeof(ZStream))
         assert rc == Z_OK, rc
         cap = compress_bound(len(data)) + 64
