@@ -74,12 +74,23 @@ int zgpu_stage_timing_read(double *ms, uint64_t *launches, int nstages);
  * On completion dst_len[i] = bytes written and status[i] = Z_OK, or
  * Z_BUF_ERROR with dst_len[i] = dst_cap[i] and the stream prefix written
  * (compress2 semantics, compress.c:44-58).  level: -1 (=6) or 0..9.
- * All arrays are device pointers.  Asynchronous on `stream`. */
+ * All arrays are device pointers; `stream` orders the work, and the call returns
+ * once it is complete (the sub-batch planning reads src_len to the host). */
 int zgpu_deflate_batch_dev(const uint8_t *src, const uint64_t *src_off,
                            const uint64_t *src_len, uint8_t *dst,
                            const uint64_t *dst_off, const uint64_t *dst_cap,
                            uint64_t *dst_len, int32_t *status, uint32_t count,
                            int level, int wrap, void *stream);
+
+/* zgpu_deflate_batch_dev with a deflateInit2_ strategy (zlib.h:197-201):
+ * 0 default, 1 Z_FILTERED, 2 Z_HUFFMAN_ONLY, 3 Z_RLE, 4 Z_FIXED; per buffer the
+ * output equals deflateInit2_(level, Z_DEFLATED, windowBits of `wrap`, 8,
+ * strategy) + deflate(Z_FINISH). */
+int zgpu_deflate_batch_dev_ex(const uint8_t *src, const uint64_t *src_off,
+                              const uint64_t *src_len, uint8_t *dst,
+                              const uint64_t *dst_off, const uint64_t *dst_cap,
+                              uint64_t *dst_len, int32_t *status, uint32_t count,
+                              int level, int wrap, int strategy, void *stream);
 
 /* crc32(init[i], buffer i) for each buffer (init == NULL: 0).  Device ptrs. */
 int zgpu_crc32_batch_dev(const uint8_t *src, const uint64_t *off, const uint64_t *len,
@@ -97,6 +108,10 @@ int zgpu_adler32_batch_dev(const uint8_t *src, const uint64_t *off, const uint64
 int zgpu_compress_batch(const uint8_t *const *src, const size_t *src_len,
                         uint8_t *const *dst, size_t *dst_len, int *status,
                         size_t count, int level, int wrap);
+/* Host-memory form with a strategy (see zgpu_deflate_batch_dev_ex). */
+int zgpu_compress_batch_ex(const uint8_t *const *src, const size_t *src_len,
+                           uint8_t *const *dst, size_t *dst_len, int *status,
+                           size_t count, int level, int wrap, int strategy);
 int zgpu_crc32_batch(const uint8_t *const *src, const size_t *len,
                      const uint32_t *init, uint32_t *out, size_t count);
 int zgpu_adler32_batch(const uint8_t *const *src, const size_t *len,

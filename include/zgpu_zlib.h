@@ -8,9 +8,10 @@
  * this library.
  *
  * deflate() semantics: deflateInit2_ accepts windowBits 15 / -15 / 31 (zlib /
- * raw / gzip wrappers), memLevel 8 and Z_DEFAULT_STRATEGY — the configuration
- * compress2() and the reference's compressSIMD path use
- * (compress.c:36, src/zlib_simd_optimized.c:365).  Input is gathered across
+ * raw / gzip wrappers), memLevel 8 and every strategy (Z_DEFAULT_STRATEGY,
+ * Z_FILTERED, Z_HUFFMAN_ONLY, Z_RLE, Z_FIXED; deflate.c:1190-1193,1964,
+ * 2051-2152, trees.c:1035) — compress2() and the reference's compressSIMD
+ * path use the default (compress.c:36, src/zlib_simd_optimized.c:365).  Input is gathered across
  * Z_NO_FLUSH calls and compressed on the GPU at Z_FINISH; the stream is then
  * drained through next_out/avail_out across as many calls as needed.  Other
  * parameters, and Z_SYNC_FLUSH/Z_FULL_FLUSH/Z_BLOCK mid-stream, return
@@ -66,7 +67,11 @@ typedef z_stream *z_streamp;
 #define Z_BUF_ERROR    (-5)
 #define Z_VERSION_ERROR (-6)
 #define Z_DEFAULT_COMPRESSION (-1)
-#define Z_DEFAULT_STRATEGY 0
+#define Z_FILTERED            1                                        /* zlib.h:197-201 */
+#define Z_HUFFMAN_ONLY        2
+#define Z_RLE                 3
+#define Z_FIXED               4
+#define Z_DEFAULT_STRATEGY    0
 #define Z_DEFLATED 8
 #define Z_UNKNOWN 2
 

@@ -926,3 +926,8 @@ int zo_pp_compress(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
                    int level, int wrap) {
     return compress_common(dst, dst_len, src, n, level, wrap, 1, 0);
 }
+
+int zo_pp_compress2(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
+                    int level, int wrap, int strategy) {
+    return compress_common(dst, dst_len, src, n, level, wrap, 1, strategy);
+}

@@ -59,4 +59,6 @@ void zo_pp_match(const uint8_t *src, size_t n, int level, const uint16_t *link,
 int zo_pp_compress(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
                    int level, int wrap);
 
+int zo_pp_compress2(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
+                    int level, int wrap, int strategy);
 #endif

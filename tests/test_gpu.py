@@ -268,3 +268,72 @@ def test_deflate_pathological_sync(zg, oracle):
         for b, (st, z) in zip(bufs, zg.compress_batch(bufs, level=level)):
             assert st == 0 and z == oracle.compress(b, level)[1], (len(b), level)
             assert pyzlib.decompress(z) == b
+
+
+def test_deflate_literal_tail_neighbours(zg, oracle):
+    """All-literal buffers whose length is a multiple of 64 (the workspace
+    rounding) packed between compressible ones: the lazy parse stages such a
+    buffer's final pending literal at index n, which must stay inside its own
+    workspace region (it once overwrote the neighbour's first staged symbol,
+    depending on timing)."""
+    bufs = []
+    for t in range(96):
+        n = 64 * int(np.random.default_rng(t).integers(1, 2048))
+        bufs.append(datagen.make("random", n, 7000 + t))
+        bufs.append(datagen.make("text", 65536, 8000 + t))
+    for level in (4, 6, 9):
+        for strategy in (0, 1):
+            res = zg.compress_batch(bufs, level=level, strategy=strategy)
+            for b, (st, z) in zip(bufs, res):
+                assert st == 0 and z == oracle.compress(b, level, strategy=strategy)[1], (len(b), level, strategy)
+
+
+@pytest.mark.parametrize("strategy", [1, 2, 3, 4], ids=["filtered", "huffman_only", "rle", "fixed"])
+def test_deflate_strategies_golden(zg, golden, strategy):
+    """deflateInit2_ strategies vs the compiled reference's outputs (fixtures)."""
+    cases = [c for c in golden["cases"] if c["n"] <= (1 << 20)]
+    bufs = [datagen.make(c["kind"], c["n"], c["seed"]) for c in cases]
+    for level in (1, 4, 6, 9):
+        res = zg.compress_batch(bufs, level=level, strategy=strategy)
+        for c, (st, z) in zip(cases, res):
+            want = c["strategies"][f"{strategy}/{level}"]
+            assert st == 0 and len(z) == want["len"] and hashlib.sha256(z).hexdigest() == want["sha256"], \
+                (c["kind"], c["n"], level, strategy)
+
+
+@pytest.mark.parametrize("strategy", [1, 2, 3, 4])
+def test_deflate_strategies_sweep_vs_oracle(zg, oracle, strategy):
+    rng = np.random.default_rng(400 + strategy)
+    bufs = [datagen.make(["runs", "text", "mix", "random", "records"][t % 5],
+                         int(rng.choice([0, 5, 300, int(rng.integers(300, 300000))])),
+                         int(rng.integers(0, 1 << 30))) for t in range(30)]
+    old = zg.set_inflight_bytes(400 * 1024)            # several sub-batches (and the L4-9 pipeline)
+    try:
+        for level in (0, 2, 5, 8):
+            for wrap in (0, 1, 2):
+                for b, (st, z) in zip(bufs, zg.compress_batch(bufs, level=level, wrap=wrap, strategy=strategy)):
+                    assert st == 0 and z == oracle.compress(b, level, wrap=wrap, strategy=strategy)[1], \
+                        (len(b), level, wrap, strategy)
+    finally:
+        zg.set_inflight_bytes(old)
+
+
+def test_deflateinit2_strategy_stream(zg, oracle):
+    L = zg.load()
+    from zhelpers import ZStream
+    L.deflateInit2_.argtypes = [C.POINTER(ZStream), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                C.c_char_p, C.c_int]
+    L.deflate.argtypes = [C.POINTER(ZStream), C.c_int]
+    L.deflateEnd.argtypes = [C.POINTER(ZStream)]
+    data = datagen.mix(150000, 4)
+    for strategy in range(5):
+        s = ZStream()
+        assert L.deflateInit2_(C.byref(s), 6, 8, 15, 8, strategy, b"1.3.1.1-motley", C.sizeof(ZStream)) == 0
+        inbuf = C.create_string_buffer(data, len(data))
+        out = C.create_string_buffer(len(data) * 2 + 100)
+        s.next_in, s.avail_in = C.addressof(inbuf), len(data)
+        s.next_out, s.avail_out = C.addressof(out), len(out)
+        assert L.deflate(C.byref(s), 4) == 1
+        got = out.raw[:s.total_out]
+        assert L.deflateEnd(C.byref(s)) == 0
+        assert got == oracle.compress(data, 6, wrap=1, strategy=strategy)[1], strategy

@@ -262,9 +262,10 @@ inline int hip_ok(hipError_t e) { return e == hipSuccess ? ZGPU_OK : ZGPU_MEM_ER
 int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
                        uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
                        uint64_t *dst_len, int32_t *status, uint32_t count, int level, int wrap,
-                       hipStream_t st) {
+                       int strategy, hipStream_t st) {
     if (level == -1) level = 6;
-    if (level < 0 || level > 9 || wrap < 0 || wrap > 2) return ZGPU_STREAM_ERROR;
+    if (level < 0 || level > 9 || wrap < 0 || wrap > 2 || strategy < 0 || strategy > 4)
+        return ZGPU_STREAM_ERROR;
     if (count == 0) return ZGPU_OK;
     std::vector<uint64_t> lens(count);
     if (hipMemcpyAsync(lens.data(), src_len, 8ull * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -275,7 +276,8 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     // keep ~6 B of workspace per in-flight byte (L4-9: ~25) and their parse is
     // one sequential lane per buffer, so they get 4x the budget: more buffers
     // in flight is what their throughput scales with.
-    const uint64_t budget = (level >= 1 && level <= 3) ? 4 * (uint64_t)c.inflight : (uint64_t)c.inflight;
+    const uint64_t budget = (level >= 1 && level <= 3) || strategy == 2 || strategy == 3
+                                ? 4 * (uint64_t)c.inflight : (uint64_t)c.inflight;
     std::vector<uint32_t> cuts{0};
     {
         uint64_t acc = 0;
@@ -294,14 +296,20 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         for (uint32_t i = a; i < b; i++) {
             meta[i] = pos;
             meta[count + i] = blk;
-            pos += (lens[i] + 63) & ~63ull;
+            // n + 1 rounded up: k_parse_seg may stage a buffer's final pending
+            // literal at index n (a run of literals up to the end), which must
+            // not land in the next buffer's region
+            pos += (lens[i] + 64) & ~63ull;
             blk += lens[i] / kSymLimit + 2;
         }
         max_pos = std::max(max_pos, pos);
         max_blk = std::max(max_blk, blk);
         max_cnt = std::max(max_cnt, b - a);
     }
-    const bool slow = level >= 4;
+    // deflate.c:1190-1193: level 0 stores; Z_HUFFMAN_ONLY / Z_RLE replace the
+    // level's parser; the other strategies change the lazy parse / tree choice
+    const bool huff = level >= 1 && strategy == 2, rle = level >= 1 && strategy == 3;
+    const bool slow = level >= 4 && !huff && !rle;
     const size_t nsub = cuts.size() - 1;
     static const bool no_pipe = std::getenv("ZGPU_NO_PIPELINE") != nullptr;
     const bool piped = slow && nsub > 1 && !no_pipe;
@@ -309,7 +317,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     if (!c.ws_link.ensure(2 * max_pos + 64)) return ZGPU_MEM_ERROR;
     if (!c.ws_sym.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
     if (!c.ws_blk.ensure(sizeof(BlockRec) * max_blk)) return ZGPU_MEM_ERROR;
-    if (slow && !c.ws_rf.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
+    if ((slow || huff || rle) && !c.ws_rf.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
     // rquart: quarter-budget results (L5-9) and the lazy parse's symbol-start staging (L4-9)
     if (slow && !c.ws_rq.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
     if (slow && !c.ws_state.ensure(max_pos / 4 + 64)) return ZGPU_MEM_ERROR;
@@ -328,12 +336,24 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
                 return ZGPU_MEM_ERROR;
         }
     }
-    if (level >= 1 && level <= 3 && !c.ws_heads.ensure(4ull * 32768 * max_cnt)) return ZGPU_MEM_ERROR;
+    if (level >= 1 && level <= 3 && !huff && !rle && !c.ws_heads.ensure(4ull * 32768 * max_cnt))
+        return ZGPU_MEM_ERROR;
     uint64_t *d_meta = c.ws_meta.as<uint64_t>();
     uint32_t *d_nblk = reinterpret_cast<uint32_t *>(d_meta + 2ull * count);
     uint32_t *d_check = d_nblk + max_cnt;
     if (hipMemcpyAsync(d_meta, meta.data(), 16ull * count, hipMemcpyHostToDevice, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
+    // ZGPU_POISON (debug): fill every workspace with a per-call byte pattern so
+    // a kernel that reads a word it did not write shows up as a mismatch
+    static const bool poison = std::getenv("ZGPU_POISON") != nullptr;
+    if (poison) {
+        static int round = 0;
+        const int v = 0x5a ^ (round++ * 0x3b);
+        for (DevBuf *b : {&c.ws_link, &c.ws_sym, &c.ws_blk, &c.ws_rf, &c.ws_rq, &c.ws_state, &c.ws_heads,
+                          &c.ws_link2, &c.ws_rf2, &c.ws_rq2, &c.ws_state2})
+            if (b->p && hipMemsetAsync(b->p, v & 0xff, b->cap, st) != hipSuccess) return ZGPU_MEM_ERROR;
+        if (hipMemsetAsync(d_nblk, v & 0xff, 8ull * max_cnt, st) != hipSuccess) return ZGPU_MEM_ERROR;
+    }
 
     StageTimer &T = c.timer;
     auto make_job = [&](size_t s) {
@@ -343,11 +363,11 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         job.src = src; job.src_off = src_off; job.src_len = src_len;
         job.dst = dst; job.dst_off = dst_off; job.dst_cap = dst_cap;
         job.dst_len = dst_len; job.status = status;
-        job.first = a; job.count = b - a; job.level = level; job.wrap = wrap;
+        job.first = a; job.count = b - a; job.level = level; job.wrap = wrap; job.strategy = strategy;
         job.ws_off = d_meta + a;
         job.blk_off = d_meta + count + a;
         job.link = (slot ? c.ws_link2 : c.ws_link).as<uint16_t>();
-        job.rfull = slow ? (slot ? c.ws_rf2 : c.ws_rf).as<uint32_t>() : nullptr;
+        job.rfull = (slow || huff || rle) ? (slot ? c.ws_rf2 : c.ws_rf).as<uint32_t>() : nullptr;
         job.rquart = slow ? (slot ? c.ws_rq2 : c.ws_rq).as<uint32_t>() : nullptr;
         job.sym = c.ws_sym.as<uint32_t>();
         job.pstate = slow ? (slot ? c.ws_state2 : c.ws_state).as<uint32_t>() : nullptr;
@@ -365,7 +385,11 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         else if (wrap == 2)
             rc = T.run(0, st, [&] { return launch_crc32(src, src_off + a, src_len + a, nullptr, d_check, b - a, nullptr, 0, st); });
         if (rc) return ZGPU_MEM_ERROR;
-        if (level >= 4) {
+        if (huff) {
+            if (T.run(4, st, [&] { return launch_deflate_stage(7, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+        } else if (rle) {
+            if (T.run(4, st, [&] { return launch_deflate_stage(8, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+        } else if (level >= 4) {
             if (T.run(3, st, [&] { return launch_deflate_stage(5, job, nullptr, st); })) return ZGPU_MEM_ERROR;
             if (T.run(3, st, [&] { return launch_deflate_stage(6, job, nullptr, st); })) return ZGPU_MEM_ERROR;
         } else if (level >= 1) {
@@ -379,7 +403,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     if (!piped) {
         for (size_t s = 0; s < nsub; s++) {
             const DeflateJob job = make_job(s);
-            if (level >= 4) {
+            if (slow) {
                 if (T.run(1, st, [&] { return launch_deflate_stage(0, job, nullptr, st); })) return ZGPU_MEM_ERROR;
                 if (T.run(2, st, [&] { return launch_deflate_stage(1, job, nullptr, st); })) return ZGPU_MEM_ERROR;
             }
@@ -416,7 +440,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
 
 // host-buffer batch: pack, upload, run, download
 int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
-                         size_t *dst_len, int *status, size_t count, int level, int wrap) {
+                         size_t *dst_len, int *status, size_t count, int level, int wrap, int strategy) {
     if (count == 0) return ZGPU_OK;
     std::vector<uint64_t> so(count), sl(count), dofs(count), dcap(count);
     uint64_t in_total = 0, out_total = 0;
@@ -437,6 +461,14 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
     uint64_t *d_sl = d_so + count, *d_do = d_sl + count, *d_dc = d_do + count, *d_dl = d_dc + count;
     int32_t *d_st = reinterpret_cast<int32_t *>(d_dl + count);
     hipStream_t st = nullptr;
+    static const bool poison = std::getenv("ZGPU_POISON") != nullptr;   // debug, see deflate_dev_locked
+    if (poison) {
+        static int round = 0;
+        const int v = (0xc3 ^ (round++ * 0x29)) & 0xff;
+        if (hipMemsetAsync(d_in, v, c.ws_io.cap, st) != hipSuccess ||
+            hipMemsetAsync(d_out, v ^ 0xff, c.ws_io2.cap, st) != hipSuccess)
+            return ZGPU_MEM_ERROR;
+    }
     for (size_t i = 0; i < count; i++)
         if (src_len[i] && hipMemcpyAsync(d_in + so[i], src[i], src_len[i], hipMemcpyHostToDevice, st) != hipSuccess)
             return ZGPU_MEM_ERROR;
@@ -446,7 +478,7 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
         hipMemcpyAsync(d_dc, dcap.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
     int rc = deflate_dev_locked(c, d_in, d_so, d_sl, d_out, d_do, d_dc, d_dl, d_st, (uint32_t)count,
-                                level, wrap, st);
+                                level, wrap, strategy, st);
     if (rc) return rc;
     std::vector<uint64_t> ol(count);
     std::vector<int32_t> os(count);
@@ -592,16 +624,24 @@ int zgpu_stage_timing_read(double *ms, uint64_t *launches, int nstages) {
     return k;
 }
 
-int zgpu_deflate_batch_dev(const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
-                           uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
-                           uint64_t *dst_len, int32_t *status, uint32_t count, int level, int wrap,
-                           void *stream) {
+int zgpu_deflate_batch_dev_ex(const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
+                              uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
+                              uint64_t *dst_len, int32_t *status, uint32_t count, int level, int wrap,
+                              int strategy, void *stream) {
     Ctx &c = ctx();
     std::lock_guard<std::mutex> g(c.mu);
     int rc = init_locked(c);
     if (rc) return rc;
     return deflate_dev_locked(c, src, src_off, src_len, dst, dst_off, dst_cap, dst_len, status,
-                              count, level, wrap, static_cast<hipStream_t>(stream));
+                              count, level, wrap, strategy, static_cast<hipStream_t>(stream));
+}
+
+int zgpu_deflate_batch_dev(const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
+                           uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
+                           uint64_t *dst_len, int32_t *status, uint32_t count, int level, int wrap,
+                           void *stream) {
+    return zgpu_deflate_batch_dev_ex(src, src_off, src_len, dst, dst_off, dst_cap, dst_len, status,
+                                     count, level, wrap, 0, stream);
 }
 
 int zgpu_crc32_batch_dev(const uint8_t *src, const uint64_t *off, const uint64_t *len,
@@ -620,13 +660,18 @@ int zgpu_adler32_batch_dev(const uint8_t *src, const uint64_t *off, const uint64
                ? ZGPU_MEM_ERROR : ZGPU_OK;
 }
 
-int zgpu_compress_batch(const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
-                        size_t *dst_len, int *status, size_t count, int level, int wrap) {
+int zgpu_compress_batch_ex(const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
+                           size_t *dst_len, int *status, size_t count, int level, int wrap, int strategy) {
     Ctx &c = ctx();
     std::lock_guard<std::mutex> g(c.mu);
     int rc = init_locked(c);
     if (rc) return rc;
-    return compress_host_locked(c, src, src_len, dst, dst_len, status, count, level, wrap);
+    return compress_host_locked(c, src, src_len, dst, dst_len, status, count, level, wrap, strategy);
+}
+
+int zgpu_compress_batch(const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
+                        size_t *dst_len, int *status, size_t count, int level, int wrap) {
+    return zgpu_compress_batch_ex(src, src_len, dst, dst_len, status, count, level, wrap, 0);
 }
 
 int zgpu_crc32_batch(const uint8_t *const *src, const size_t *len, const uint32_t *init,
@@ -753,7 +798,7 @@ uLong adler32_combine(uLong adler1, uLong adler2, long len2) { return adler32_co
 
 // z_stream deflate: gather input, compress on the GPU at Z_FINISH, drain.
 struct internal_state {
-    int level, wrap;
+    int level, wrap, strategy;
     std::vector<uint8_t> in, out;
     size_t out_pos;
     int finished;     // 0 gathering, 1 compressed
@@ -771,12 +816,13 @@ int deflateInit2_(z_streamp strm, int level, int method, int windowBits, int mem
     else if (windowBits == -15) wrap = 0;
     else if (windowBits == 31) wrap = 2;
     else return Z_STREAM_ERROR;
-    if (method != Z_DEFLATED || memLevel != 8 || strategy != Z_DEFAULT_STRATEGY || level < 0 || level > 9)
+    if (method != Z_DEFLATED || memLevel != 8 || strategy < 0 || strategy > Z_FIXED || level < 0 || level > 9)
         return Z_STREAM_ERROR;
     internal_state *s = new (std::nothrow) internal_state();
     if (!s) return Z_MEM_ERROR;
     s->level = level;
     s->wrap = wrap;
+    s->strategy = strategy;
     s->out_pos = 0;
     s->finished = 0;
     strm->state = s;
@@ -810,7 +856,7 @@ int deflate(z_streamp strm, int flush) {
         uint8_t *dp = s->out.data();
         size_t sl = s->in.size();
         int st = 0;
-        int rc = zgpu_compress_batch(&sp, &sl, &dp, &cap, &st, 1, s->level, s->wrap);
+        int rc = zgpu_compress_batch_ex(&sp, &sl, &dp, &cap, &st, 1, s->level, s->wrap, s->strategy);
         if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
         s->out.resize(cap);
         s->finished = 1;

@@ -440,30 +440,42 @@ __device__ __attribute__((always_inline)) inline bool mw8_loop(MW3 &w, uint32_t 
 // and longer matches continue 16 bytes (both sides) per round trip.
 struct Scan16 { uint32_t s0, s1, s2, s3; };
 
+// first mismatching byte of a 4-byte xor word at byte offset `at`, or 99 if none
+__device__ __attribute__((always_inline)) inline int mism(uint32_t x, int at) {
+    return x ? at + (int)(__builtin_ctz(x) >> 3) : 99;
+}
+
+template <bool kBatch>
 __device__ __attribute__((always_inline)) inline int cmp16(const uint32_t *E, int m, int s, const Scan16 &S,
                                                            int maxcmp) {
-    const uint32_t x0 = get4(E, m) ^ S.s0, x1 = get4(E, m + 4) ^ S.s1;
-    const uint32_t x2 = get4(E, m + 8) ^ S.s2, x3 = get4(E, m + 12) ^ S.s3;
-    if (x0) return __builtin_ctz(x0) >> 3;
-    if (x1) return 4 + (__builtin_ctz(x1) >> 3);
-    if (x2) return 8 + (__builtin_ctz(x2) >> 3);
-    if (x3) return 12 + (__builtin_ctz(x3) >> 3);
+    if (kBatch) {
+        // all four candidate words loaded before anything is tested
+        const uint32_t x0 = get4(E, m) ^ S.s0, x1 = get4(E, m + 4) ^ S.s1;
+        const uint32_t x2 = get4(E, m + 8) ^ S.s2, x3 = get4(E, m + 12) ^ S.s3;
+        const int k16 = min(min(mism(x0, 0), mism(x1, 4)), min(mism(x2, 8), mism(x3, 12)));
+        if (k16 < 16 || maxcmp <= 16) return k16 < 16 ? k16 : 16;
+    } else {
+        // word by word: most compares end in the first 4-8 bytes
+        uint32_t x = get4(E, m) ^ S.s0;
+        if (x) return __builtin_ctz(x) >> 3;
+        if ((x = get4(E, m + 4) ^ S.s1)) return 4 + (__builtin_ctz(x) >> 3);
+        if ((x = get4(E, m + 8) ^ S.s2)) return 8 + (__builtin_ctz(x) >> 3);
+        if ((x = get4(E, m + 12) ^ S.s3)) return 12 + (__builtin_ctz(x) >> 3);
+    }
     int k = 16;
     while (k < maxcmp) {
         const uint32_t y0 = get4(E, m + k) ^ get4(E, s + k);
         const uint32_t y1 = get4(E, m + k + 4) ^ get4(E, s + k + 4);
         const uint32_t y2 = get4(E, m + k + 8) ^ get4(E, s + k + 8);
         const uint32_t y3 = get4(E, m + k + 12) ^ get4(E, s + k + 12);
-        if (y0) return k + (__builtin_ctz(y0) >> 3);
-        if (y1) return k + 4 + (__builtin_ctz(y1) >> 3);
-        if (y2) return k + 8 + (__builtin_ctz(y2) >> 3);
-        if (y3) return k + 12 + (__builtin_ctz(y3) >> 3);
+        const int r = min(min(mism(y0, 0), mism(y1, 4)), min(mism(y2, 8), mism(y3, 12)));
+        if (r < 16) return k + r;
         k += 16;
     }
     return k;
 }
 
-template <int kUnroll>
+template <int kUnroll, bool kBatch>
 __device__ __attribute__((always_inline)) inline bool mw14_loop(MW3 &w, uint32_t &em, uint32_t &eb,
                                                                 const Scan16 &S, const uint32_t *E, uint32_t end) {
     const char *Eb = reinterpret_cast<const char *>(E);
@@ -476,7 +488,7 @@ __device__ __attribute__((always_inline)) inline bool mw14_loop(MW3 &w, uint32_t
         const uint32_t miss = ((em >> 16) ^ w.scan01) | ((eb >> 16) ^ w.scanE);
         if (__builtin_expect(miss == 0, 0)) {
             const int m = w.m4 >> 2, s = w.s4 >> 2;
-            const int k = cmp16(E, m, s, S, w.maxcmp);
+            const int k = cmp16<kBatch>(E, m, s, S, w.maxcmp);
             const int len = k < w.maxcmp ? k : w.maxcmp;
             if (len > w.best) {
                 w.best = len;
@@ -496,7 +508,7 @@ __device__ __attribute__((always_inline)) inline bool mw14_loop(MW3 &w, uint32_t
     }
 }
 
-template <int kUnroll>
+template <int kUnroll, bool kBatch>
 __device__ __attribute__((always_inline)) inline void mw14_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
                                                                 const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
                                                                 int want_q) {
@@ -526,10 +538,10 @@ __device__ __attribute__((always_inline)) inline void mw14_walk(const uint32_t *
     uint32_t em = E[s - (int)d0];
     uint32_t eb = E[s - (int)d0 + 1];
     const uint32_t qc = want_q ? (uint32_t)(cfg.chain >> 2) : (uint32_t)cfg.chain;
-    const bool done = mw14_loop<kUnroll>(w, em, eb, S, E, qc);
+    const bool done = mw14_loop<kUnroll, kBatch>(w, em, eb, S, E, qc);
     if (want_q) {
         rq[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
-        if (!done) mw14_loop<kUnroll>(w, em, eb, S, E, (uint32_t)cfg.chain);
+        if (!done) mw14_loop<kUnroll, kBatch>(w, em, eb, S, E, (uint32_t)cfg.chain);
     }
     rf[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
 }
@@ -856,12 +868,12 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
         match_tile_load(E, ts, n, in, L, tid);
         if (tid == 0) next_i = 0;
         __syncthreads();
-        if (kVariant == 14) {
+        if (kVariant == 14 || kVariant == 15) {
             for (;;) {
                 const int i = atomicAdd(&next_i, 1);
                 const int64_t p = ts + i;
                 if (i >= kMT || p >= n) break;
-                mw14_walk<2>(E, p, B, n, cfg, rf, rq, want_q);
+                mw14_walk<2, kVariant == 15>(E, p, B, n, cfg, rf, rq, want_q);
             }
         } else if (kVariant == 13) {
             for (;;) {
@@ -1015,6 +1027,7 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
     const uint32_t *rq = job.rquart + job.ws_off[bi];
     const LevelCfg cfg = c_ct.cfg[job.level];
     const bool use_q = cfg.good < cfg.lazy;
+    const bool filtered = job.strategy == 1;
     const uint32_t lazy = cfg.lazy, good = cfg.good;
     if (only_flagged && job.nblocks[bi] != kParseFallback) return;
 
@@ -1044,7 +1057,8 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
             if (match_length < kMinMatch && p + 64 + kMinLookahead <= po.E) {
                 const uint32_t r = s_rf[p - t0 + lane];
                 const uint32_t rl = r >> 16;
-                const bool hit = rl >= kMinMatch && !(rl == kMinMatch && (r & 0xffffu) > (uint32_t)kTooFar);
+                const bool hit = rl >= kMinMatch &&
+                                 !(rl <= 5u && (filtered || (rl == kMinMatch && (r & 0xffffu) > (uint32_t)kTooFar)));
                 const uint64_t mask = __ballot(hit);
                 const uint32_t k = mask ? (uint32_t)__builtin_ctzll(mask) : 64u;
                 if (k > 0) {
@@ -1073,7 +1087,8 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
                 if (rl > prev_length) {
                     match_length = rl;
                     match_start = p - (r & 0xffffu);
-                    if (match_length == kMinMatch && p - match_start > (uint32_t)kTooFar) match_length = kMinMatch - 1;
+                    if (match_length <= 5u && (filtered || (match_length == kMinMatch && p - match_start > (uint32_t)kTooFar)))
+                        match_length = kMinMatch - 1;                  // deflate.c:1964-1975
                 }
             }
             if (prev_length >= kMinMatch && match_length <= prev_length) {
@@ -1179,8 +1194,8 @@ struct SlowLane {
 // one deflate_slow decision (deflate.c:1946-2027) on precomputed results.
 // Returns 0 (no symbol), 1 (literal at spos), 2 (match starting at spos, len).
 __device__ __attribute__((always_inline)) inline int slow_step(SlowLane &L, uint32_t n, const uint32_t *rf, const uint32_t *rq,
-                                const uint8_t *in, const LevelCfg &cfg, bool use_q, uint32_t &sym,
-                                uint32_t &spos, uint32_t &slen) {
+                                const uint8_t *in, const LevelCfg &cfg, bool use_q, bool filtered,
+                                uint32_t &sym, uint32_t &spos, uint32_t &slen) {
     const uint32_t p = L.p;
     const uint32_t prev_length = L.ml, prev_match = L.ms;
     uint32_t ml = kMinMatch - 1;
@@ -1190,7 +1205,8 @@ __device__ __attribute__((always_inline)) inline int slow_step(SlowLane &L, uint
         if (rl > prev_length) {
             ml = rl;
             L.ms = p - (r & 0xffffu);
-            if (ml == (uint32_t)kMinMatch && p - L.ms > (uint32_t)kTooFar) ml = kMinMatch - 1;
+            if (ml <= 5u && (filtered || (ml == (uint32_t)kMinMatch && p - L.ms > (uint32_t)kTooFar)))
+                ml = kMinMatch - 1;                        // deflate.c:1964-1975
         }
     }
     if (prev_length >= (uint32_t)kMinMatch && ml <= prev_length) {
@@ -1218,10 +1234,14 @@ __device__ __attribute__((always_inline)) inline int slow_step(SlowLane &L, uint
 // p at which the k-th window slide (k >= 1) becomes due: fill_window is called
 // when lookahead < MIN_LOOKAHEAD and slides when strstart >= WSIZE+MAX_DIST
 // (deflate.c:277); with all input present the window end is min(n, S + 64K).
-__device__ inline int64_t slide_threshold(uint32_t k, uint32_t n) {
+__device__ inline int64_t slide_threshold(uint32_t k, uint32_t n, int64_t refill = kMinLookahead - 1) {
+    // fill_window runs at a decision point p with lookahead E - p <= refill
+    // (261 for deflate_slow/fast, 258 for deflate_rle, 0 for deflate_huff) and
+    // slides when p - S >= WSIZE + MAX_DIST (deflate.c:277); all input is
+    // present, so the window end is E = min(n, S + 64K).
     const int64_t S = (int64_t)kWSize * (k - 1);
-    if ((int64_t)n > S + 2 * kWSize) return S + kWSize + kMaxDist + 1;
-    const int64_t a = (int64_t)n - (kMinLookahead - 1), b = S + kWSize + kMaxDist;
+    const int64_t E = (int64_t)n > S + 2 * kWSize ? S + 2 * kWSize : (int64_t)n;
+    const int64_t a = E - refill, b = S + kWSize + kMaxDist;
     return a > b ? a : b;
 }
 
@@ -1249,6 +1269,7 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
     BlockRec *blk = job.blocks + job.blk_off[bi];
     const LevelCfg cfg = c_ct.cfg[job.level];
     const bool use_q = cfg.good < cfg.lazy;
+    const bool filtered = job.strategy == 1;
 
     uint32_t nseg = (n + kSegMin - 1) / kSegMin;
     nseg = nseg < 1 ? 1 : nseg > (uint32_t)kParseLanes ? (uint32_t)kParseLanes : nseg;
@@ -1276,7 +1297,7 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
                 wcur = 0;
             }
             if (L.ml < (uint32_t)kMinMatch) wcur |= 1u << (2 * (L.p & 15u) + L.avail);
-            slow_step(L, n, rf, rq, in, cfg, use_q, sym_v, spos, slen);
+            slow_step(L, n, rf, rq, in, cfg, use_q, filtered, sym_v, spos, slen);
         }
         sst[widx] = wcur;
         for (uint32_t z = widx + 1; z <= (seg_end - 1) >> 4; z++) sst[z] = 0;
@@ -1297,7 +1318,7 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
                 if ((L.p >> 4) != ridx) { ridx = L.p >> 4; rw = sst[ridx]; }
                 if ((rw >> (2 * (L.p & 15u) + L.avail)) & 1u) { y = L.p; sig = L.avail; break; }
             }
-            slow_step(L, n, rf, rq, in, cfg, use_q, sym_v, spos, slen);
+            slow_step(L, n, rf, rq, in, cfg, use_q, filtered, sym_v, spos, slen);
         }
     }
     if (active && y == kEnd) atomicMin(&s_first_end, (uint32_t)lane);
@@ -1320,12 +1341,13 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
     // ---- pass 3: the true parse of [start, end); the k-th symbol is staged at
     // rq[start + k] and its start position at rf[start + k] (both behind the
     // lane: symbol k starts at or after start + k - 1, and a lane reads only
-    // at and ahead of its own position, inside its own range)
+    // at and ahead of its own position, inside its own range).  The last lane's
+    // final pending literal can take index n: buffer regions hold n + 1 words.
     uint32_t cnt = 0;
     if (mine) {
         lane_init(L, start, start_av);
         while (L.p < end) {
-            if (slow_step(L, n, rf, rq, in, cfg, use_q, sym_v, spos, slen)) {
+            if (slow_step(L, n, rf, rq, in, cfg, use_q, filtered, sym_v, spos, slen)) {
                 rq[start + cnt] = sym_v;
                 rf[start + cnt] = spos;
                 cnt++;
@@ -1423,6 +1445,111 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
         __syncthreads();
     }
     if (lane == 0) job.nblocks[bi] = ncut + 1;
+}
+
+// ------------------------------------------------------------------------
+// Block records of a parse whose every symbol is flush-tested (deflate_huff,
+// deflate_rle): block b ends after symbol 16383(b+1)-1; its flush happens at
+// the decision point of that symbol (its start), so the slides before it are
+// #{k : T_k <= start} with the parser's refill threshold; the last block is
+// flushed at n.  cut_end/cut_pd: per cut, the end and decision point.
+// ------------------------------------------------------------------------
+__device__ void cut_blocks(BlockRec *blk, uint32_t n, uint32_t total, const uint32_t *cut_end,
+                           const uint32_t *cut_pd, int64_t refill, int tid, int nthreads) {
+    const uint32_t ncut = total / kSymLimit;
+    uint32_t nthr = 0;
+    while (slide_threshold(nthr + 1, n, refill) <= (int64_t)n) nthr++;
+    for (uint32_t b = tid; b <= ncut; b += nthreads) {
+        const bool last = b == ncut;
+        const uint64_t in_end = last ? n : cut_end[b];
+        const uint64_t pd = last ? n : cut_pd[b];
+        const uint64_t in_start = b == 0 ? 0 : cut_end[b - 1];
+        uint32_t slides = 0;
+        while (slides < nthr && slide_threshold(slides + 1, n, refill) <= (int64_t)pd) slides++;
+        BlockRec r;
+        r.sym_start = b * kSymLimit;
+        r.nsym = last ? total - b * kSymLimit : (uint32_t)kSymLimit;
+        r.in_start = in_start;
+        r.in_end = in_end;
+        r.flags = (last ? 1u : 0u) | (in_start >= (uint64_t)kWSize * slides ? 2u : 0u);
+        r.pad = 0;
+        blk[b] = r;
+    }
+}
+
+// k_parse_huff — Z_HUFFMAN_ONLY (deflate_huff, deflate.c:2122-2152): every byte
+// is a literal; the window refills when the lookahead is 0.
+constexpr int kHuffThreads = 256;
+__global__ __launch_bounds__(kHuffThreads) void k_parse_huff(DeflateJob job) {
+    const int tid = threadIdx.x;
+    const uint32_t bi = blockIdx.x;
+    const uint32_t g = job.first + bi;
+    const uint32_t n = (uint32_t)job.src_len[g];
+    const uint8_t *in = job.src + job.src_off[g];
+    uint32_t *sym = job.sym + job.ws_off[bi];
+    BlockRec *blk = job.blocks + job.blk_off[bi];
+    for (uint32_t i = tid; i < n; i += kHuffThreads) sym[i] = in[i];
+    // cut ends / decision points live in the rfull workspace (unused here)
+    uint32_t *cut_end = job.rfull + job.ws_off[bi];
+    uint32_t *cut_pd = cut_end + (n / kSymLimit + 1);
+    const uint32_t ncut = n / kSymLimit;
+    for (uint32_t b = tid; b < ncut; b += kHuffThreads) {
+        cut_end[b] = (b + 1) * kSymLimit;
+        cut_pd[b] = (b + 1) * kSymLimit - 1;
+    }
+    __threadfence_block();
+    __syncthreads();
+    cut_blocks(blk, n, n, cut_end, cut_pd, 0, tid, kHuffThreads);
+    if (tid == 0) job.nblocks[bi] = ncut + 1;
+}
+
+// k_parse_rle — Z_RLE (deflate_rle, deflate.c:2051-2116): a run of the previous
+// byte of length >= 3 (capped at 258 and at the lookahead) becomes a match at
+// distance 1; the window refills when the lookahead is <= 258.  One lane per
+// buffer walks the input; symbols and cut points go to the workspace.
+__global__ __launch_bounds__(64) void k_parse_rle(DeflateJob job) {
+    const int lane = threadIdx.x;
+    const uint32_t bi = blockIdx.x;
+    const uint32_t g = job.first + bi;
+    const uint32_t n = (uint32_t)job.src_len[g];
+    const uint8_t *in = job.src + job.src_off[g];
+    uint32_t *sym = job.sym + job.ws_off[bi];
+    BlockRec *blk = job.blocks + job.blk_off[bi];
+    uint32_t *cut_end = job.rfull + job.ws_off[bi];
+    uint32_t *cut_pd = cut_end + (n / kSymLimit + 1);
+    __shared__ uint32_t s_total;
+    if (lane == 0) {
+        BCache cb;
+        cb.base = ~(uintptr_t)0;
+        uint32_t p = 0, cnt = 0;
+        while (p < n) {
+            uint32_t len = 0;
+            if (n - p >= (uint32_t)kMinMatch && p > 0) {
+                const uint32_t prev = bget(in, p - 1, cb);
+                if (bget(in, p, cb) == prev && bget(in, p + 1, cb) == prev && bget(in, p + 2, cb) == prev) {
+                    len = 3;
+                    const uint32_t cap = n - p < (uint32_t)kMaxMatch ? n - p : (uint32_t)kMaxMatch;
+                    while (len < cap && bget(in, p + len, cb) == prev) len++;
+                }
+            }
+            uint32_t v, sl;
+            if (len >= (uint32_t)kMinMatch) { v = (1u << 8) | (len - kMinMatch); sl = len; }
+            else { v = bget(in, p, cb); sl = 1; }
+            sym[cnt] = v;
+            if ((cnt + 1) % (uint32_t)kSymLimit == 0) {
+                cut_end[cnt / kSymLimit] = p + sl;
+                cut_pd[cnt / kSymLimit] = p;
+            }
+            cnt++;
+            p += sl;
+        }
+        s_total = cnt;
+    }
+    __threadfence_block();
+    __syncthreads();
+    const uint32_t total = s_total;
+    cut_blocks(blk, n, total, cut_end, cut_pd, kMaxMatch, lane, 64);
+    if (lane == 0) job.nblocks[bi] = total / kSymLimit + 1;
 }
 
 // ------------------------------------------------------------------------
@@ -1776,13 +1903,13 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
         s_obit = 0;
         if (job.wrap == 1) {                    // zlib header (deflate.c:1004-1037)
             uint32_t header = (8u + ((15u - 8u) << 4)) << 8;
-            uint32_t flags = level < 2 ? 0u : level < 6 ? 1u : level == 6 ? 2u : 3u;
+            uint32_t flags = (job.strategy >= 2 || level < 2) ? 0u : level < 6 ? 1u : level == 6 ? 2u : 3u;
             header |= flags << 6;
             header += 31 - (header % 31);
             put(header >> 8, 8);
             put(header & 0xffu, 8);
         } else if (job.wrap == 2) {             // gzip header (deflate.c:1060-1073)
-            const uint32_t xfl = level == 9 ? 2u : level < 2 ? 4u : 0u;
+            const uint32_t xfl = level == 9 ? 2u : (job.strategy >= 2 || level < 2) ? 4u : 0u;   // deflate.c:1052
             put(31, 8); put(139, 8); put(8, 8); put(0, 8);
             put(0, 32);
             put(xfl, 8); put(3, 8);             // OS_CODE (zutil.h:184)
@@ -1868,7 +1995,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
                         opt_len += 3 * ((int64_t)max_blindex + 1) + 5 + 5 + 4;
                         uint64_t opt_lenb = ((uint64_t)opt_len + 3 + 7) >> 3;
                         const uint64_t static_lenb = ((uint64_t)static_len + 3 + 7) >> 3;
-                        if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+                        if (static_lenb <= opt_lenb || job.strategy == 4) opt_lenb = static_lenb;   // trees.c:1035
                         const uint64_t stored_len = br.in_end - br.in_start;
                         int type;                                   // trees.c:1027-1074
                         if (stored_len + 4 <= opt_lenb && (br.flags & 2u)) type = 0;
@@ -2032,6 +2159,7 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         else if (variant == 11) hipLaunchKernelGGL(k_match<11>, grid, dim3(kMatchThreads), 0, st, job, wq);
         else if (variant == 13) hipLaunchKernelGGL(k_match<13>, grid, dim3(kMatchThreads), 0, st, job, wq);
         else if (variant == 14) hipLaunchKernelGGL(k_match<14>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        else if (variant == 15) hipLaunchKernelGGL(k_match<15>, grid, dim3(kMatchThreads), 0, st, job, wq);
         else if (variant == 12) hipLaunchKernelGGL(k_match<12>, grid, dim3(kMatchThreads), 0, st, job, wq);
         else if (variant == 7) hipLaunchKernelGGL(k_match<7>, grid, dim3(kMatchThreads), 0, st, job, wq);
         else hipLaunchKernelGGL(k_match<14>, grid, dim3(kMatchThreads), 0, st, job, wq);
@@ -2042,6 +2170,8 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     case 6: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 1); break;
     case 3: hipLaunchKernelGGL(k_parse_fast, grid, dim3(64), 0, st, job, heads); break;
     case 4: hipLaunchKernelGGL(k_encode, grid, dim3(kEncThreads), 0, st, job); break;
+    case 7: hipLaunchKernelGGL(k_parse_huff, grid, dim3(kHuffThreads), 0, st, job); break;
+    case 8: hipLaunchKernelGGL(k_parse_rle, grid, dim3(64), 0, st, job); break;
     default: return -1;
     }
     return (int)hipGetLastError();

@@ -79,6 +79,7 @@ struct DeflateJob {
     uint32_t first;          // first buffer index of this sub-batch
     uint32_t count;          // buffers in this sub-batch
     int level, wrap;
+    int strategy;            // deflateInit2_ strategy: 0 default, 1 filtered, 2 huffman only, 3 rle, 4 fixed
     // workspace, indexed by position relative to ws_off[i]
     const uint64_t *ws_off;  // per sub-batch buffer: start in the position-indexed arrays
     const uint64_t *blk_off; // per sub-batch buffer: start in the block array

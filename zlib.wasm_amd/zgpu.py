@@ -36,6 +36,7 @@ KIND_RANDOM, KIND_SILESIA, KIND_ENWIK, KIND_SMALLVOCAB = 0, 1, 2, 3
 EXPORTED_SYMBOLS = (
     # include/zgpu.h
     "zgpu_init", "zgpu_info", "zgpu_set_inflight_bytes", "zgpu_deflate_batch_dev",
+    "zgpu_deflate_batch_dev_ex", "zgpu_compress_batch_ex",
     "zgpu_crc32_batch_dev", "zgpu_adler32_batch_dev", "zgpu_compress_batch",
     "zgpu_crc32_batch", "zgpu_adler32_batch", "zgpu_generate_dev", "zgpu_stage_timing",
     "zgpu_stage_timing_read",
@@ -85,11 +86,15 @@ def load(path=LIB_PATH):
     L.zgpu_set_inflight_bytes.argtypes = [C.c_size_t]
     L.zgpu_deflate_batch_dev.restype = I32
     L.zgpu_deflate_batch_dev.argtypes = [P, P, P, P, P, P, P, P, U32, I32, I32, P]
+    L.zgpu_deflate_batch_dev_ex.restype = I32
+    L.zgpu_deflate_batch_dev_ex.argtypes = [P, P, P, P, P, P, P, P, U32, I32, I32, I32, P]
     for f in ("zgpu_crc32_batch_dev", "zgpu_adler32_batch_dev"):
         getattr(L, f).restype = I32
         getattr(L, f).argtypes = [P, P, P, P, P, U32, P]
     L.zgpu_compress_batch.restype = I32
     L.zgpu_compress_batch.argtypes = [P, P, P, P, P, C.c_size_t, I32, I32]
+    L.zgpu_compress_batch_ex.restype = I32
+    L.zgpu_compress_batch_ex.argtypes = [P, P, P, P, P, C.c_size_t, I32, I32, I32]
     for f in ("zgpu_crc32_batch", "zgpu_adler32_batch"):
         getattr(L, f).restype = I32
         getattr(L, f).argtypes = [P, P, P, P, C.c_size_t]
@@ -126,19 +131,34 @@ def _ptr_array(bufs):
     return arr, keep
 
 
-def compress_batch(bufs, level=6, wrap=WRAP_ZLIB, caps=None):
-    """Compress independent host buffers on the GPU; returns [(status, bytes)]."""
+STRATEGY_DEFAULT, STRATEGY_FILTERED, STRATEGY_HUFFMAN_ONLY, STRATEGY_RLE, STRATEGY_FIXED = 0, 1, 2, 3, 4
+
+
+def conservative_bound(n):
+    """deflateBound's bound for non-default parameters (deflate.c:887-897):
+    valid for every strategy."""
+    return n + ((n + 7) >> 3) + ((n + 63) >> 6) + 5
+
+
+def compress_batch(bufs, level=6, wrap=WRAP_ZLIB, caps=None, strategy=0):
+    """Compress independent host buffers on the GPU; returns [(status, bytes)].
+    ``strategy`` is deflateInit2_'s (0 default, 1 filtered, 2 huffman only,
+    3 rle, 4 fixed)."""
     L = load()
     n = len(bufs)
     src, keep = _ptr_array(bufs)
     lens = (C.c_size_t * n)(*[len(b) for b in bufs])
     extra = 12 if wrap == WRAP_GZIP else 0        # deflateBound wraplen 18 vs 6
-    caps = caps or [compress_bound(len(b)) + extra for b in bufs]
+    if caps is None:
+        if strategy == 0:
+            caps = [compress_bound(len(b)) + extra for b in bufs]
+        else:                                        # + deflateBound's wraplen
+            caps = [conservative_bound(len(b)) + (18 if wrap == WRAP_GZIP else 6) for b in bufs]
     outs = [C.create_string_buffer(max(c, 1)) for c in caps]
     dst = (C.c_void_p * n)(*[C.addressof(o) for o in outs])
     dlen = (C.c_size_t * n)(*caps)
     st = (C.c_int * n)()
-    rc = L.zgpu_compress_batch(src, lens, dst, dlen, st, n, level, wrap)
+    rc = L.zgpu_compress_batch_ex(src, lens, dst, dlen, st, n, level, wrap, strategy)
     if rc:
         raise ZlibCompressionError(f"zgpu_compress_batch failed: {rc}")
     del keep
@@ -201,10 +221,10 @@ def _stream(stream):
 
 
 def deflate_batch_dev(src, src_off, src_len, dst, dst_off, dst_cap, dst_len, status,
-                      level=6, wrap=WRAP_ZLIB, stream=None):
-    rc = load().zgpu_deflate_batch_dev(_dp(src), _dp(src_off), _dp(src_len), _dp(dst),
-                                       _dp(dst_off), _dp(dst_cap), _dp(dst_len), _dp(status),
-                                       src_len.numel(), level, wrap, _stream(stream))
+                      level=6, wrap=WRAP_ZLIB, stream=None, strategy=0):
+    rc = load().zgpu_deflate_batch_dev_ex(_dp(src), _dp(src_off), _dp(src_len), _dp(dst),
+                                          _dp(dst_off), _dp(dst_cap), _dp(dst_len), _dp(status),
+                                          src_len.numel(), level, wrap, strategy, _stream(stream))
     if rc:
         raise ZlibCompressionError(f"zgpu_deflate_batch_dev failed: {rc}")
 
