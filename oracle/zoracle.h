@@ -23,6 +23,7 @@
 
 #define ZO_OK            0
 #define ZO_STREAM_ERROR (-2)
+#define ZO_DATA_ERROR   (-3)
 #define ZO_MEM_ERROR    (-4)
 #define ZO_BUF_ERROR    (-5)
 
@@ -61,4 +62,16 @@ int zo_pp_compress(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
 
 int zo_pp_compress2(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
                     int level, int wrap, int strategy);
+/* ---- inflate (zinflate.c): inflate.c / inftrees.c / uncompr.c ----
+ * wrap: 0 raw, 1 zlib, 2 gzip, 3 zlib or gzip (windowBits 15+32).
+ * zo_inflate_run stops at the stream end (0), a data error (1), a preset
+ * dictionary request (2), a full output (3) or the end of the input (4);
+ * out_len = bytes written, consumed = input bytes inflate() has taken. */
+int zo_inflate_run(const uint8_t *src, size_t n, uint8_t *dst, size_t cap, int wrap,
+                   size_t *out_len, size_t *consumed);
+/* uncompress2 (uncompr.c:24-80) for any wrapper: ZO_OK / ZO_DATA_ERROR /
+ * ZO_BUF_ERROR; *dst_len in: capacity, out: bytes written; *src_len in: input
+ * length, out: bytes consumed */
+int zo_uncompress3(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t *src_len, int wrap);
+int zo_uncompress2(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t *src_len);
 #endif

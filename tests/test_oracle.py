@@ -156,3 +156,61 @@ def test_oracle_strategies_golden(oracle, golden):
             rc, z = oracle.compress(data, level, wrap=1, strategy=strategy)
             assert rc == 0 and len(z) == want["len"] and hashlib.sha256(z).hexdigest() == want["sha256"], \
                 (c["kind"], c["n"], key)
+
+
+# ----------------------------- inflate -----------------------------
+
+@pytest.fixture(scope="module")
+def inflate_golden():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "inflate_golden.json")) as f:
+        return json.load(f)
+
+
+def _oracle_compress(oracle):
+    return lambda d, level, wrap, strategy: oracle.compress(d, level, wrap=wrap, strategy=strategy)[1]
+
+
+def test_oracle_inflate_golden(oracle, inflate_golden):
+    """uncompress2 status / output / consumed of the reference on 2427 streams:
+    valid ones at every level, wrapper and strategy, truncated, bit-flipped,
+    with garbage tails, short outputs, the destLen == 0 probe, and crafted
+    headers / block headers / code sets."""
+    import inflate_cases as ic
+    comp = _oracle_compress(oracle)
+    bases = {}
+    for c in inflate_golden["cases"]:
+        if "hex" in c:
+            src = bytes.fromhex(c["hex"])
+        else:
+            key = (c["kind"], c["n"], c["seed"], c["level"], c["wrap"], c["strategy"])
+            if key not in bases:
+                bases[key] = ic.base_stream(c, comp)[1]
+                assert ic.sha(bases[key]) == c["base_sha256"], key   # the oracle compressor too
+            src = ic.mutate(bases[key], c["mut"])
+        rc, out, used = oracle.uncompress(src, c["cap"], c["dwrap"])
+        e = c["expect"]
+        assert (rc, len(out), ic.sha(out), used) == (e["status"], e["len"], e["sha256"], e["consumed"]), c
+
+
+@pytest.mark.skipif(not reference_available(), reason="compiled reference only in build container")
+def test_oracle_inflate_vs_reference_fuzz(oracle):
+    import inflate_cases as ic
+    ref = Reference()
+    rng = np.random.default_rng(77)
+    for c in ic.crafted(seed=31, count=1500):
+        src = bytes.fromhex(c["hex"])
+        assert oracle.uncompress(src, c["cap"], c["dwrap"]) == ref.uncompress(src, c["cap"], c["dwrap"]), c
+    for t in range(60):
+        data = datagen.make(["text", "mix", "runs", "random"][t % 4], int(rng.integers(0, 50000)), t)
+        wrap = t % 3
+        z = oracle.compress(data, int(rng.integers(0, 10)), wrap=wrap)[1]
+        for _ in range(10):
+            zz = bytearray(z)
+            i = int(rng.integers(0, len(zz) * 8))
+            zz[i >> 3] ^= 1 << (i & 7)
+            cut = int(rng.integers(0, len(zz) + 1))
+            for src in (bytes(zz), z[:cut]):
+                cap = int(rng.integers(0, len(data) + 2))
+                assert oracle.uncompress(src, cap, wrap) == ref.uncompress(src, cap, wrap), (t, i, cut)

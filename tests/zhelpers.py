@@ -44,6 +44,9 @@ class Oracle:
         for f in ("zo_crc32_combine", "zo_adler32_combine"):
             getattr(L, f).restype = C.c_uint32
             getattr(L, f).argtypes = [C.c_uint32, C.c_uint32, C.c_int64]
+        L.zo_uncompress3.restype = C.c_int
+        L.zo_uncompress3.argtypes = [C.c_void_p, C.POINTER(C.c_size_t), C.c_void_p,
+                                     C.POINTER(C.c_size_t), C.c_int]
         L.zo_pp_links.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
         L.zo_pp_match.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_void_p,
                                   C.c_void_p, C.c_void_p]
@@ -66,6 +69,14 @@ class Oracle:
 
     def pp_compress(self, data, level=6, wrap=1, cap=None):
         return self._compress(self.L.zo_pp_compress, data, level, wrap, cap)
+
+    def uncompress(self, src, cap, wrap=1):
+        """uncompress2 semantics for any wrapper: (status, output, consumed)."""
+        src = bytes(src)
+        out = C.create_string_buffer(max(cap, 1))
+        dl, sl = C.c_size_t(cap), C.c_size_t(len(src))
+        rc = self.L.zo_uncompress3(out, C.byref(dl), src, C.byref(sl), wrap)
+        return rc, out.raw[: dl.value], sl.value
 
     def crc32(self, data, crc=0):
         data = bytes(data)
@@ -124,8 +135,58 @@ class Reference:
         L.deflate.argtypes = [C.POINTER(ZStream), C.c_int]
         L.deflateEnd.restype = C.c_int
         L.deflateEnd.argtypes = [C.POINTER(ZStream)]
+        L.uncompress2.restype = C.c_int
+        L.uncompress2.argtypes = [C.c_void_p, C.POINTER(C.c_ulong), C.c_void_p, C.POINTER(C.c_ulong)]
+        L.inflateInit2_.restype = C.c_int
+        L.inflateInit2_.argtypes = [C.POINTER(ZStream), C.c_int, C.c_char_p, C.c_int]
+        L.inflate.restype = C.c_int
+        L.inflate.argtypes = [C.POINTER(ZStream), C.c_int]
+        L.inflateEnd.restype = C.c_int
+        L.inflateEnd.argtypes = [C.POINTER(ZStream)]
         self.L = L
         self.version = L.zlibVersion()
+
+    def uncompress(self, src, cap, wrap=1):
+        """(status, output, consumed).  wrap 1 calls the reference's own
+        uncompress2; the other wrappers run uncompress2's loop (uncompr.c:24-80)
+        over the reference's inflateInit2_/inflate (windowBits -15, 31, 47)."""
+        src = bytes(src)
+        out = C.create_string_buffer(max(cap, 1))
+        if wrap == 1:
+            dl, sl = C.c_ulong(cap), C.c_ulong(len(src))
+            rc = self.L.uncompress2(out, C.byref(dl), src, C.byref(sl))
+            return rc, out.raw[: dl.value], sl.value
+        inbuf = C.create_string_buffer(src, max(len(src), 1))
+        strm = ZStream()
+        wbits = {0: -15, 2: 31, 3: 47}[wrap]
+        assert self.L.inflateInit2_(C.byref(strm), wbits, self.version, C.sizeof(ZStream)) == Z_OK
+        probe = cap == 0
+        buf1 = C.create_string_buffer(1)
+        left = 1 if probe else cap
+        strm.next_in = C.addressof(inbuf)
+        strm.avail_in = len(src)
+        strm.next_out = C.addressof(buf1) if probe else C.addressof(out)
+        strm.avail_out = left
+        left = 0
+        while True:
+            err = self.L.inflate(C.byref(strm), 0)
+            if err != Z_OK:
+                break
+        consumed = len(src) - strm.avail_in
+        total = strm.total_out
+        if probe and total and err == -5:
+            left = 1
+        avail_out = strm.avail_out
+        self.L.inflateEnd(C.byref(strm))
+        if err == 1:
+            rc = Z_OK
+        elif err == 2:
+            rc = -3
+        elif err == -5 and left + avail_out:
+            rc = -3
+        else:
+            rc = err
+        return rc, (b"" if probe else out.raw[:total]), consumed
 
     def compress2(self, data, level=6, cap=None):
         data = bytes(data)
