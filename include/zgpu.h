@@ -14,10 +14,10 @@
  *       host    : host buffers; staged over PCIe by the library.
  *
  *  2. zlib.h drop-in names (zgpu_zlib.h): compress2, compress, compressBound,
- *     deflateInit_/deflateInit2_/deflate/deflateEnd/deflateBound, crc32,
- *     crc32_z, crc32_combine*, adler32, adler32_z, adler32_combine*,
- *     zlibVersion — replacing zlib.h:224-1836 of the reference for the
- *     compression side.
+ *     deflateInit_/deflateInit2_/deflate/deflateEnd/deflateBound, uncompress,
+ *     uncompress2, inflateInit_/inflateInit2_/inflate/inflateEnd/inflateReset,
+ *     crc32, crc32_z, crc32_combine*, adler32, adler32_z, adler32_combine*,
+ *     zlibVersion — replacing zlib.h:224-1836 of the reference.
  *
  *  3. The reference's WASM front-end exports (src/wasm_module.c:34-84,
  *     src/zlib_simd_compression.c:280,342, src/zlib_simd_optimized.c:27-409):
@@ -63,7 +63,8 @@ size_t zgpu_set_inflight_bytes(size_t bytes);
  * totals and starts collecting; enable == 0 stops.  zgpu_stage_timing_read
  * copies total milliseconds and launch counts for up to `nstages` stages:
  * 0 checksum (trailer), 1 links, 2 match, 3 lazy parse, 4 greedy parse,
- * 5 encode.  Returns the number of stages written. */
+ * 5 encode; for zgpu_inflate_batch_dev 3 decode, 4 match copy, 5 finish.
+ * Returns the number of stages written. */
 void zgpu_stage_timing(int enable);
 int zgpu_stage_timing_read(double *ms, uint64_t *launches, int nstages);
 
@@ -101,6 +102,27 @@ int zgpu_adler32_batch_dev(const uint8_t *src, const uint64_t *off, const uint64
                            const uint32_t *init, uint32_t *out, uint32_t count,
                            void *stream);
 
+/* Decompress `count` independent streams (the other half of the wire format,
+ * SURVEY §8f row 2).  Stream i is src[src_off[i] .. +src_len[i]) and is
+ * inflated into dst[dst_off[i] .. +dst_cap[i]).  Per stream the result is what
+ * the reference's uncompress2 (uncompr.c:24-85) returns for that input and
+ * capacity, for wrap 1 (zlib) exactly, and for the other wrappers with
+ * inflateInit2_(-15 raw / 31 gzip / 47 zlib-or-gzip) in the same loop:
+ *   status[i]   Z_OK, Z_DATA_ERROR (corrupt, truncated, preset dictionary) or
+ *               Z_BUF_ERROR (the output filled up before the stream ended);
+ *   dst_len[i]  bytes written (the decodable prefix on errors; 0 when
+ *               dst_cap[i] == 0, uncompress2's 1-byte probe);
+ *   src_used[i] input bytes consumed (may be NULL).
+ * wrap: ZGPU_WRAP_RAW / _ZLIB / _GZIP, or ZGPU_WRAP_AUTO (zlib or gzip header).
+ * Each stream's src_len and dst_cap must be < 4 GiB (else ZGPU_STREAM_ERROR).
+ * Device pointers, ordered on `stream`; returns when complete. */
+#define ZGPU_WRAP_AUTO 3
+int zgpu_inflate_batch_dev(const uint8_t *src, const uint64_t *src_off,
+                           const uint64_t *src_len, uint8_t *dst,
+                           const uint64_t *dst_off, const uint64_t *dst_cap,
+                           uint64_t *dst_len, uint64_t *src_used, int32_t *status,
+                           uint32_t count, int wrap, void *stream);
+
 /* ---------------- batched, host buffers ---------------- */
 
 /* Host-memory form of zgpu_deflate_batch_dev; dst_len[i] is in: capacity,
@@ -112,6 +134,11 @@ int zgpu_compress_batch(const uint8_t *const *src, const size_t *src_len,
 int zgpu_compress_batch_ex(const uint8_t *const *src, const size_t *src_len,
                            uint8_t *const *dst, size_t *dst_len, int *status,
                            size_t count, int level, int wrap, int strategy);
+/* Host-memory form of zgpu_inflate_batch_dev: dst_len[i] in: capacity, out:
+ * bytes written; src_used may be NULL.  Synchronous. */
+int zgpu_uncompress_batch(const uint8_t *const *src, const size_t *src_len,
+                          uint8_t *const *dst, size_t *dst_len, size_t *src_used,
+                          int *status, size_t count, int wrap);
 int zgpu_crc32_batch(const uint8_t *const *src, const size_t *len,
                      const uint32_t *init, uint32_t *out, size_t count);
 int zgpu_adler32_batch(const uint8_t *const *src, const size_t *len,

@@ -1,8 +1,8 @@
 /*
  * zgpu_wasm.h — the reference's WASM front-end exports, re-exported by
  * libzgpu.so with the same names and C signatures so the existing
- * compress()/compressSIMD() callers (src/lib/index.ts:120,250,267) bind
- * unchanged.  All of them route to the GPU path.
+ * compress()/decompress()/compressSIMD() callers (src/lib/index.ts:120,170,
+ * 250,267) bind unchanged.  All of them route to the GPU path.
  */
 #ifndef ZGPU_WASM_H
 #define ZGPU_WASM_H
@@ -17,6 +17,34 @@ extern "C" {
 /* src/wasm_module.c:34-46 — compress2 with level clamp; NULL/empty -> Z_STREAM_ERROR */
 int zlib_compress_buffer(const unsigned char *src, unsigned long src_len,
                          unsigned char *dest, unsigned long *dest_len, int level);
+/* src/wasm_module.c:53-60 — uncompress; NULL/empty -> Z_STREAM_ERROR */
+int zlib_decompress_buffer(const unsigned char *src, unsigned long src_len,
+                           unsigned char *dest, unsigned long *dest_len);
+/* src/wasm_module_simd.c:425-456 — the same under the SIMD module's names */
+int zlib_decompress_optimized(const unsigned char *input, unsigned long input_len,
+                              unsigned char *output, unsigned long *output_len);
+int zlib_decompress(const unsigned char *input, unsigned long input_len,
+                    unsigned char *output, unsigned long *output_len);
+int zlib_compress_optimized(const unsigned char *input, unsigned long input_len,
+                            unsigned char *output, unsigned long *output_len, int level);
+int zlib_compress(const unsigned char *input, unsigned long input_len,
+                  unsigned char *output, unsigned long *output_len, int level);
+
+/* src/wasm_module.c:160-291 — stream contexts over deflate() / inflate() */
+typedef struct zlib_stream_s zlib_stream_t;
+zlib_stream_t *zlib_deflate_init(int level, int window_bits, int mem_level, int strategy);
+int zlib_deflate_process(zlib_stream_t *ctx, const unsigned char *input, unsigned int input_len,
+                         unsigned char *output, unsigned int output_len, int flush);
+void zlib_deflate_end(zlib_stream_t *ctx);
+zlib_stream_t *zlib_inflate_init(int window_bits);
+int zlib_inflate_process(zlib_stream_t *ctx, const unsigned char *input, unsigned int input_len,
+                         unsigned char *output, unsigned int output_len);
+void zlib_inflate_end(zlib_stream_t *ctx);
+unsigned int zlib_stream_avail_in(zlib_stream_t *ctx);
+unsigned int zlib_stream_avail_out(zlib_stream_t *ctx);
+unsigned long zlib_stream_total_in(zlib_stream_t *ctx);
+unsigned long zlib_stream_total_out(zlib_stream_t *ctx);
+
 /* src/wasm_module.c:65-84 */
 unsigned long zlib_crc32(unsigned long crc, const unsigned char *buf, unsigned int len);
 unsigned long zlib_adler32(unsigned long adler, const unsigned char *buf, unsigned int len);

@@ -4,8 +4,17 @@
  * A program built against the reference's zlib.h (zlib 1.3.1.1-motley) for the
  * compression side can link libzgpu.so instead of libz: same symbol names, same
  * signatures, same z_stream layout, same return codes.  Each declaration cites
- * the reference prototype it replaces.  Decompression (inflate*) is not part of
- * this library.
+ * the reference prototype it replaces.
+ *
+ * uncompress()/uncompress2() return what the reference returns for every input
+ * (valid, corrupt, truncated, short output), with the same output and the same
+ * consumed length.  inflate() gathers input across calls and decodes on the
+ * GPU once the gathered input holds a whole stream (checked when the input has
+ * doubled since the last attempt, when a call brings no new input, and at
+ * Z_FINISH); the output is then drained through next_out/avail_out.  The bytes
+ * and the final return code equal the reference's; output arrives once per
+ * stream instead of progressively.  inflateSetDictionary is not provided: a
+ * stream that needs a preset dictionary returns Z_NEED_DICT.
  *
  * deflate() semantics: deflateInit2_ accepts windowBits 15 / -15 / 31 (zlib /
  * raw / gzip wrappers), memLevel 8 and every strategy (Z_DEFAULT_STRATEGY,
@@ -62,6 +71,8 @@ typedef z_stream *z_streamp;
 #define Z_BLOCK         5
 #define Z_OK            0
 #define Z_STREAM_END    1
+#define Z_NEED_DICT     2                                                  /* zlib.h:183 */
+#define Z_DATA_ERROR   (-3)
 #define Z_STREAM_ERROR (-2)
 #define Z_MEM_ERROR    (-4)
 #define Z_BUF_ERROR    (-5)
@@ -103,6 +114,22 @@ uLong crc32_combine_gen(long len2);                                     /* zlib.
 uLong crc32_combine_gen64(int64_t len2);
 uLong crc32_combine_op(uLong crc1, uLong crc2, uLong op);               /* zlib.h:1790 */
 
+int uncompress(Bytef *dest, uLongf *destLen, const Bytef *source,
+               uLong sourceLen);                                        /* zlib.h:1289 */
+int uncompress2(Bytef *dest, uLongf *destLen, const Bytef *source,
+                uLong *sourceLen);                                      /* zlib.h:1307 */
+int inflateInit_(z_streamp strm, const char *version, int stream_size); /* zlib.h:1805 */
+/* windowBits 8..15 zlib, -8..-15 raw, +16 gzip, +32 zlib or gzip (zlib.h:853) */
+int inflateInit2_(z_streamp strm, int windowBits, const char *version,
+                  int stream_size);                                     /* zlib.h:1811 */
+int inflate(z_streamp strm, int flush);                                 /* zlib.h:405 */
+int inflateEnd(z_streamp strm);                                         /* zlib.h:525 */
+int inflateReset(z_streamp strm);                                       /* zlib.h:980 */
+
+#define inflateInit(strm) \
+    inflateInit_((strm), ZGPU_ZLIB_VERSION, (int)sizeof(z_stream))
+#define inflateInit2(strm, windowBits) \
+    inflateInit2_((strm), (windowBits), ZGPU_ZLIB_VERSION, (int)sizeof(z_stream))
 #define deflateInit(strm, level) \
     deflateInit_((strm), (level), ZGPU_ZLIB_VERSION, (int)sizeof(z_stream))
 #define deflateInit2(strm, level, method, windowBits, memLevel, strategy) \

@@ -206,6 +206,8 @@ struct Ctx {
     // sub-batch i+1 runs on `aux` while links/parse/encode run on the caller's
     // stream)
     DevBuf ws_link2, ws_rf2, ws_rq2, ws_state2;
+    // inflate: match records, per-stream results, checks, offsets, stop codes
+    DevBuf ws_mrec, ws_irec, ws_ick, ws_imeta, ws_istop;
     hipStream_t aux = nullptr;
     hipEvent_t ev_links[2] = {nullptr, nullptr}, ev_match[2] = {nullptr, nullptr};
 };
@@ -494,6 +496,137 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
     return ZGPU_OK;
 }
 
+// ------------------------------------------------------------------------
+// inflate orchestration (caller holds ctx().mu).  Sub-batches keep the sum of
+// output capacities within the in-flight budget; each stream gets cap/3 + 2
+// match records (a match writes >= 3 bytes, the last one may be cut short).
+// stop_out (device, optional): InflateStop per stream.
+// ------------------------------------------------------------------------
+int inflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
+                       uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap, uint64_t *dst_len,
+                       uint64_t *src_used, int32_t *status, uint32_t *stop_out, uint32_t count, int wrap,
+                       int wbits, hipStream_t st) {
+    if (wrap < 0 || wrap > 3) return ZGPU_STREAM_ERROR;
+    if (count == 0) return ZGPU_OK;
+    std::vector<uint64_t> lens(count), caps(count);
+    if (hipMemcpyAsync(lens.data(), src_len, 8ull * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(caps.data(), dst_cap, 8ull * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return ZGPU_MEM_ERROR;
+    for (uint32_t i = 0; i < count; i++)
+        if (lens[i] >= (1ull << 32) || caps[i] >= (1ull << 32)) return ZGPU_STREAM_ERROR;   // per-stream limit
+    const uint64_t budget = c.inflight;
+    std::vector<uint32_t> cuts{0};
+    {
+        uint64_t acc = 0;
+        for (uint32_t i = 0; i < count; i++) {
+            const uint64_t w = caps[i] + lens[i];
+            if (acc > 0 && acc + w > budget) { cuts.push_back(i); acc = 0; }
+            acc += w;
+        }
+        cuts.push_back(count);
+    }
+    std::vector<uint64_t> moff(count);
+    uint64_t max_rec = 0;
+    uint32_t max_cnt = 0;
+    for (size_t s = 0; s + 1 < cuts.size(); s++) {
+        uint64_t acc = 0;
+        for (uint32_t i = cuts[s]; i < cuts[s + 1]; i++) { moff[i] = acc; acc += caps[i] / 3 + 2; }
+        max_rec = std::max(max_rec, acc);
+        max_cnt = std::max(max_cnt, cuts[s + 1] - cuts[s]);
+    }
+    if (!c.ws_mrec.ensure(8 * max_rec + 64) || !c.ws_irec.ensure(sizeof(InflateRec) * max_cnt + 64) ||
+        !c.ws_ick.ensure(8ull * max_cnt + 64) || !c.ws_imeta.ensure(8ull * count + 64))
+        return ZGPU_MEM_ERROR;
+    uint64_t *d_moff = c.ws_imeta.as<uint64_t>();
+    if (hipMemcpyAsync(d_moff, moff.data(), 8ull * count, hipMemcpyHostToDevice, st) != hipSuccess)
+        return ZGPU_MEM_ERROR;
+    StageTimer &T = c.timer;
+    for (size_t s = 0; s + 1 < cuts.size(); s++) {
+        const uint32_t a = cuts[s], b = cuts[s + 1];
+        InflateJob job{};
+        job.src = src; job.src_off = src_off; job.src_len = src_len;
+        job.dst = dst; job.dst_off = dst_off; job.dst_cap = dst_cap; job.dst_len = dst_len;
+        job.src_used = src_used; job.status = status; job.stop_out = stop_out;
+        job.first = a; job.count = b - a; job.wrap = wrap; job.wbits = wbits;
+        job.mrec_off = d_moff + a;
+        job.mrec = c.ws_mrec.as<uint64_t>();
+        job.rec = c.ws_irec.as<InflateRec>();
+        job.adler = c.ws_ick.as<uint32_t>();
+        job.crc = job.adler + max_cnt;
+        job.crc_byte = device_crc_tables()->byte;
+        if (T.run(3, st, [&] { return launch_inflate_stage(0, job, st); })) return ZGPU_MEM_ERROR;
+        if (T.run(4, st, [&] { return launch_inflate_stage(1, job, st); })) return ZGPU_MEM_ERROR;
+        if ((wrap & 1) && T.run(0, st, [&] {
+                return launch_adler32(dst, dst_off + a, dst_len + a, nullptr, job.adler, b - a, nullptr, 0, st); }))
+            return ZGPU_MEM_ERROR;
+        if ((wrap & 2) && T.run(0, st, [&] {
+                return launch_crc32(dst, dst_off + a, dst_len + a, nullptr, job.crc, b - a, nullptr, 0, st); }))
+            return ZGPU_MEM_ERROR;
+        if (T.run(5, st, [&] { return launch_inflate_stage(2, job, st); })) return ZGPU_MEM_ERROR;
+    }
+    int rc = hip_ok(hipStreamSynchronize(st));
+    c.timer.collect();
+    return rc;
+}
+
+// host-buffer inflate batch: pack, upload, run, download.  dst_len in:
+// capacity, out: bytes written; src_used / stop optional.
+int uncompress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
+                           size_t *dst_len, size_t *src_used, int *status, int *stop, size_t count, int wrap,
+                           int wbits) {
+    if (count == 0) return ZGPU_OK;
+    std::vector<uint64_t> so(count), sl(count), dofs(count), dcap(count);
+    uint64_t in_total = 0, out_total = 0;
+    for (size_t i = 0; i < count; i++) {
+        so[i] = in_total;
+        sl[i] = src_len[i];
+        in_total += (src_len[i] + 15) & ~15ull;
+        dofs[i] = out_total;
+        dcap[i] = dst_len[i];
+        out_total += (dst_len[i] + 15) & ~15ull;
+    }
+    const size_t meta_bytes = 8 * 6 * count + 8 * count;
+    if (!c.ws_io.ensure(in_total + 64) || !c.ws_io2.ensure(out_total + 64) ||
+        !c.ws_small.ensure(meta_bytes + 64) || !c.ws_istop.ensure(4ull * count + 64))
+        return ZGPU_MEM_ERROR;
+    uint8_t *d_in = c.ws_io.as<uint8_t>(), *d_out = c.ws_io2.as<uint8_t>();
+    uint64_t *d_so = c.ws_small.as<uint64_t>();
+    uint64_t *d_sl = d_so + count, *d_do = d_sl + count, *d_dc = d_do + count, *d_dl = d_dc + count;
+    uint64_t *d_used = d_dl + count;
+    int32_t *d_st = reinterpret_cast<int32_t *>(d_used + count);
+    uint32_t *d_stop = c.ws_istop.as<uint32_t>();
+    hipStream_t st = nullptr;
+    for (size_t i = 0; i < count; i++)
+        if (src_len[i] && hipMemcpyAsync(d_in + so[i], src[i], src_len[i], hipMemcpyHostToDevice, st) != hipSuccess)
+            return ZGPU_MEM_ERROR;
+    if (hipMemcpyAsync(d_so, so.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_sl, sl.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_do, dofs.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_dc, dcap.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess)
+        return ZGPU_MEM_ERROR;
+    int rc = inflate_dev_locked(c, d_in, d_so, d_sl, d_out, d_do, d_dc, d_dl, d_used, d_st, d_stop,
+                                (uint32_t)count, wrap, wbits, st);
+    if (rc) return rc;
+    std::vector<uint64_t> ol(count), ou(count);
+    std::vector<int32_t> os(count);
+    std::vector<uint32_t> ostop(count);
+    if (hipMemcpy(ol.data(), d_dl, 8 * count, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(ou.data(), d_used, 8 * count, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(os.data(), d_st, 4 * count, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(ostop.data(), d_stop, 4 * count, hipMemcpyDeviceToHost) != hipSuccess)
+        return ZGPU_MEM_ERROR;
+    for (size_t i = 0; i < count; i++) {
+        if (ol[i] && hipMemcpy(dst[i], d_out + dofs[i], ol[i], hipMemcpyDeviceToHost) != hipSuccess)
+            return ZGPU_MEM_ERROR;
+        dst_len[i] = ol[i];
+        if (src_used) src_used[i] = ou[i];
+        if (status) status[i] = os[i];
+        if (stop) stop[i] = (int)ostop[i];
+    }
+    return ZGPU_OK;
+}
+
 // host-buffer checksum batch.  Large buffers are cut into 1 MiB pieces so a
 // single huge buffer still spreads over the whole GPU; pieces are joined with
 // crc32_combine / adler32_combine (crc32.c:1021, adler32.c:133).
@@ -674,6 +807,28 @@ int zgpu_compress_batch(const uint8_t *const *src, const size_t *src_len, uint8_
     return zgpu_compress_batch_ex(src, src_len, dst, dst_len, status, count, level, wrap, 0);
 }
 
+int zgpu_inflate_batch_dev(const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
+                           uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
+                           uint64_t *dst_len, uint64_t *src_used, int32_t *status, uint32_t count,
+                           int wrap, void *stream) {
+    Ctx &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    int rc = init_locked(c);
+    if (rc) return rc;
+    return inflate_dev_locked(c, src, src_off, src_len, dst, dst_off, dst_cap, dst_len, src_used, status,
+                              nullptr, count, wrap, 15, static_cast<hipStream_t>(stream));
+}
+
+int zgpu_uncompress_batch(const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
+                          size_t *dst_len, size_t *src_used, int *status, size_t count, int wrap) {
+    if (wrap < 0 || wrap > 3) return ZGPU_STREAM_ERROR;
+    Ctx &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    int rc = init_locked(c);
+    if (rc) return rc;
+    return uncompress_host_locked(c, src, src_len, dst, dst_len, src_used, status, nullptr, count, wrap, 15);
+}
+
 int zgpu_crc32_batch(const uint8_t *const *src, const size_t *len, const uint32_t *init,
                      uint32_t *out, size_t count) {
     Ctx &c = ctx();
@@ -801,7 +956,13 @@ struct internal_state {
     int level, wrap, strategy;
     std::vector<uint8_t> in, out;
     size_t out_pos;
-    int finished;     // 0 gathering, 1 compressed
+    int finished;     // 0 gathering, 1 compressed / decoded
+    // inflate streams
+    int inflating = 0;
+    int wbits = 15;
+    size_t tried = 0;       // gathered input at the last decode attempt that ran out of input
+    size_t cap = 0;         // output capacity of the next attempt
+    int result = Z_OK;      // once decoded: Z_STREAM_END, Z_DATA_ERROR or Z_NEED_DICT
 };
 
 int deflateInit2_(z_streamp strm, int level, int method, int windowBits, int memLevel, int strategy,
@@ -837,7 +998,7 @@ int deflateInit_(z_streamp strm, int level, const char *version, int stream_size
 }
 
 int deflate(z_streamp strm, int flush) {
-    if (!strm || !strm->state || flush < 0 || flush > Z_BLOCK) return Z_STREAM_ERROR;
+    if (!strm || !strm->state || strm->state->inflating || flush < 0 || flush > Z_BLOCK) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
     if (!strm->next_out || (strm->avail_in && !strm->next_in)) return Z_STREAM_ERROR;
     if (flush != Z_NO_FLUSH && flush != Z_FINISH) return Z_STREAM_ERROR;   // documented gap
@@ -875,7 +1036,7 @@ int deflate(z_streamp strm, int flush) {
 }
 
 int deflateEnd(z_streamp strm) {
-    if (!strm || !strm->state) return Z_STREAM_ERROR;
+    if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
     delete strm->state;
     strm->state = nullptr;
     return Z_OK;
@@ -890,7 +1051,236 @@ uLong deflateBound(z_streamp strm, uLong sourceLen) {          // deflate.c:842-
     return sourceLen + (sourceLen >> 12) + (sourceLen >> 14) + (sourceLen >> 25) + 13 - 6 + wraplen;
 }
 
+// ------------------------------- inflate -------------------------------
+
+int uncompress2(Bytef *dest, uLongf *destLen, const Bytef *source, uLong *sourceLen) {   // uncompr.c:24-80
+    if (!destLen || !sourceLen || (*sourceLen && !source) || (*destLen && !dest)) return Z_STREAM_ERROR;
+    const uint8_t *s = source;
+    uint8_t *d = dest;
+    size_t sl = *sourceLen, cap = *destLen, used = 0;
+    int st = 0;
+    int rc = zgpu_uncompress_batch(&s, &sl, &d, &cap, &used, &st, 1, ZGPU_WRAP_ZLIB);
+    if (rc == ZGPU_ENODEV) return Z_MEM_ERROR;
+    if (rc) return rc;
+    *destLen = cap;
+    *sourceLen = used;
+    return st;
+}
+
+int uncompress(Bytef *dest, uLongf *destLen, const Bytef *source, uLong sourceLen) {    // uncompr.c:82-85
+    return uncompress2(dest, destLen, source, &sourceLen);
+}
+
+// z_stream inflate: gather input, decode on the GPU once the gathered input
+// holds a whole stream, drain.
+int inflateInit2_(z_streamp strm, int windowBits, const char *version, int stream_size) {
+    if (!version || version[0] != ZGPU_ZLIB_VERSION[0] || stream_size != (int)sizeof(z_stream))
+        return Z_VERSION_ERROR;                                       // inflate.c:203-206
+    if (!strm) return Z_STREAM_ERROR;
+    int wrap;                                                         // inflateReset2, inflate.c:161-185
+    if (windowBits < 0) {
+        if (windowBits < -15) return Z_STREAM_ERROR;
+        wrap = 0;
+        windowBits = -windowBits;
+    } else {
+        wrap = ((windowBits >> 4) + 5) & 3;                           // 1 zlib, 2 gzip, 3 either
+        if (windowBits < 48) windowBits &= 15;
+    }
+    if (windowBits && (windowBits < 8 || windowBits > 15)) return Z_STREAM_ERROR;
+    internal_state *s = new (std::nothrow) internal_state();
+    if (!s) return Z_MEM_ERROR;
+    s->inflating = 1;
+    s->wrap = wrap;
+    s->wbits = windowBits;
+    s->out_pos = 0;
+    s->finished = 0;
+    strm->msg = nullptr;
+    strm->state = s;
+    strm->total_in = strm->total_out = 0;
+    strm->adler = wrap & 1;
+    return Z_OK;
+}
+
+int inflateInit_(z_streamp strm, const char *version, int stream_size) {
+    return inflateInit2_(strm, 15, version, stream_size);
+}
+
+int inflateReset(z_streamp strm) {
+    if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    s->in.clear(); s->out.clear();
+    s->out_pos = 0; s->finished = 0; s->tried = 0; s->cap = 0; s->result = Z_OK;
+    strm->total_in = strm->total_out = 0;
+    strm->msg = nullptr;
+    strm->adler = s->wrap & 1;
+    return Z_OK;
+}
+
+int inflate(z_streamp strm, int flush) {
+    if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    if (!strm->next_out || (strm->avail_in && !strm->next_in)) return Z_STREAM_ERROR;   // inflate.c:610-612
+    if (flush == Z_BLOCK || flush == 6 /* Z_TREES */) return Z_STREAM_ERROR;           // documented gap
+    const size_t took = s->finished ? 0 : strm->avail_in;
+    if (took) {
+        s->in.insert(s->in.end(), strm->next_in, strm->next_in + took);
+        strm->next_in += took;
+        strm->avail_in = 0;
+        strm->total_in += took;
+    }
+    if (!s->finished && (took == 0 || flush == Z_FINISH || s->in.size() >= 2 * s->tried)) {
+        if (s->cap == 0) s->cap = std::max<size_t>(4 * s->in.size(), 1 << 16);
+        for (;;) {
+            s->out.resize(s->cap);
+            const uint8_t *sp = s->in.data();
+            uint8_t *dp = s->out.data();
+            size_t sl = s->in.size(), dl = s->cap, used = 0;
+            int st = 0, stop = 0;
+            Ctx &c = ctx();
+            int rc;
+            {
+                std::lock_guard<std::mutex> g(c.mu);
+                rc = init_locked(c);
+                if (!rc) rc = uncompress_host_locked(c, &sp, &sl, &dp, &dl, &used, &st, &stop, 1, s->wrap, s->wbits);
+            }
+            if (rc) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : rc;
+            if (stop == kIFull) {                                     // grow the output and decode again
+                if (s->cap >= (size_t(1) << 31)) return Z_MEM_ERROR;
+                s->cap *= 2;
+                continue;
+            }
+            if (stop == kIInEnd) { s->tried = s->in.size(); s->out.clear(); break; }
+            s->out.resize(dl);
+            s->finished = 1;
+            if (stop == kIEnd) {
+                s->result = Z_STREAM_END;
+                const size_t extra = s->in.size() - used;             // give back input past the stream end
+                const size_t back = std::min(extra, took);
+                strm->next_in -= back;
+                strm->avail_in += (uInt)back;
+                strm->total_in = used;
+                if (s->wrap) strm->adler = s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b
+                                               ? crc32_z(0, s->out.data(), s->out.size())
+                                               : adler32_z(1, s->out.data(), s->out.size());
+            } else if (stop == kIDict) {
+                s->result = Z_NEED_DICT;
+                strm->adler = ((uLong)s->in[2] << 24) | ((uLong)s->in[3] << 16) | ((uLong)s->in[4] << 8) | s->in[5];
+            } else {
+                s->result = Z_DATA_ERROR;
+                strm->msg = const_cast<char *>("invalid or corrupt deflate stream");
+            }
+            s->in.clear();
+            s->in.shrink_to_fit();
+            break;
+        }
+    }
+    size_t give = 0;
+    if (s->finished) {
+        give = std::min<size_t>(strm->avail_out, s->out.size() - s->out_pos);
+        std::memcpy(strm->next_out, s->out.data() + s->out_pos, give);
+        s->out_pos += give;
+        strm->next_out += give;
+        strm->avail_out -= (uInt)give;
+        strm->total_out += give;
+        if (s->out_pos == s->out.size()) return s->result;
+    }
+    if (took || give) return Z_OK;
+    return Z_BUF_ERROR;                                                // inflate.c:1265-1266: no progress
+}
+
+int inflateEnd(z_streamp strm) {
+    if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
+    delete strm->state;
+    strm->state = nullptr;
+    return Z_OK;
+}
+
 // ----------------------- reference WASM front-end -----------------------
+
+int zlib_decompress_buffer(const unsigned char *src, unsigned long src_len, unsigned char *dest,
+                           unsigned long *dest_len) {                // src/wasm_module.c:53-60
+    if (!src || !dest || !dest_len || src_len == 0) return Z_STREAM_ERROR;
+    return uncompress(dest, dest_len, src, src_len);
+}
+int zlib_decompress_optimized(const unsigned char *input, unsigned long input_len, unsigned char *output,
+                              unsigned long *output_len) {           // src/wasm_module_simd.c:425-428
+    return zlib_decompress_buffer(input, input_len, output, output_len);
+}
+int zlib_decompress(const unsigned char *input, unsigned long input_len, unsigned char *output,
+                    unsigned long *output_len) {                     // src/wasm_module_simd.c:453-456
+    return zlib_decompress_buffer(input, input_len, output, output_len);
+}
+
+struct zlib_stream_s {                                                // src/wasm_module.c:160-163
+    z_stream stream;
+    int initialized;
+};
+
+zlib_stream_t *zlib_deflate_init(int level, int window_bits, int mem_level, int strategy) {
+    if (level < 0 || level > 9) level = Z_DEFAULT_COMPRESSION;        // src/wasm_module.c:168-186
+    if (window_bits < 8 || window_bits > 15) window_bits = 15;
+    if (mem_level < 1 || mem_level > 9) mem_level = 8;
+    zlib_stream_t *ctx = static_cast<zlib_stream_t *>(std::calloc(1, sizeof(zlib_stream_t)));
+    if (!ctx) return nullptr;
+    if (deflateInit2_(&ctx->stream, level, Z_DEFLATED, window_bits, mem_level, strategy, ZGPU_ZLIB_VERSION,
+                      (int)sizeof(z_stream)) != Z_OK) {
+        std::free(ctx);                                               // windowBits < 15 / memLevel != 8
+        return nullptr;
+    }
+    ctx->initialized = 1;
+    return ctx;
+}
+int zlib_deflate_process(zlib_stream_t *ctx, const unsigned char *input, unsigned int input_len,
+                         unsigned char *output, unsigned int output_len, int flush) {
+    if (!ctx || !ctx->initialized) return Z_STREAM_ERROR;             // src/wasm_module.c:192-203
+    ctx->stream.next_in = const_cast<Bytef *>(input);
+    ctx->stream.avail_in = input_len;
+    ctx->stream.next_out = output;
+    ctx->stream.avail_out = output_len;
+    return deflate(&ctx->stream, flush);
+}
+void zlib_deflate_end(zlib_stream_t *ctx) {                           // src/wasm_module.c:209-215
+    if (!ctx) return;
+    if (ctx->initialized) deflateEnd(&ctx->stream);
+    std::free(ctx);
+}
+zlib_stream_t *zlib_inflate_init(int window_bits) {                  // src/wasm_module.c:209-226
+    if (window_bits < 8 || window_bits > 15) window_bits = 15;
+    zlib_stream_t *ctx = static_cast<zlib_stream_t *>(std::calloc(1, sizeof(zlib_stream_t)));
+    if (!ctx) return nullptr;
+    if (inflateInit2_(&ctx->stream, window_bits, ZGPU_ZLIB_VERSION, (int)sizeof(z_stream)) != Z_OK) {
+        std::free(ctx);
+        return nullptr;
+    }
+    ctx->initialized = 1;
+    return ctx;
+}
+int zlib_inflate_process(zlib_stream_t *ctx, const unsigned char *input, unsigned int input_len,
+                         unsigned char *output, unsigned int output_len) {   // src/wasm_module.c:232-243
+    if (!ctx || !ctx->initialized) return Z_STREAM_ERROR;
+    ctx->stream.next_in = const_cast<Bytef *>(input);
+    ctx->stream.avail_in = input_len;
+    ctx->stream.next_out = output;
+    ctx->stream.avail_out = output_len;
+    return inflate(&ctx->stream, Z_NO_FLUSH);
+}
+void zlib_inflate_end(zlib_stream_t *ctx) {                           // src/wasm_module.c:249-255
+    if (!ctx) return;
+    if (ctx->initialized) inflateEnd(&ctx->stream);
+    std::free(ctx);
+}
+unsigned int zlib_stream_avail_in(zlib_stream_t *ctx) { return ctx ? ctx->stream.avail_in : 0; }
+unsigned int zlib_stream_avail_out(zlib_stream_t *ctx) { return ctx ? ctx->stream.avail_out : 0; }
+unsigned long zlib_stream_total_in(zlib_stream_t *ctx) { return ctx ? ctx->stream.total_in : 0; }
+unsigned long zlib_stream_total_out(zlib_stream_t *ctx) { return ctx ? ctx->stream.total_out : 0; }
+int zlib_compress_optimized(const unsigned char *input, unsigned long input_len, unsigned char *output,
+                            unsigned long *output_len, int level) {  // src/wasm_module_simd.c:419-422
+    return zlib_compress_buffer(input, input_len, output, output_len, level);
+}
+int zlib_compress(const unsigned char *input, unsigned long input_len, unsigned char *output,
+                  unsigned long *output_len, int level) {            // src/wasm_module_simd.c:447-450
+    return zlib_compress_buffer(input, input_len, output, output_len, level);
+}
 
 int zlib_compress_buffer(const unsigned char *src, unsigned long src_len, unsigned char *dest,
                          unsigned long *dest_len, int level) {         // src/wasm_module.c:34-46

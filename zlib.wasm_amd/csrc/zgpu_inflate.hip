@@ -1,0 +1,610 @@
+// zgpu_inflate.hip — batched inflate for gfx950: output, status and bytes
+// consumed identical to the reference's uncompress2 (uncompr.c:24-85) over
+// inflate() (inflate.c:622-1221) on every stream, valid or not.
+//
+// Per sub-batch of independent streams:
+//   k_inflate_decode  wave/stream  the inflate state machine: headers, block
+//                                  headers, code tables (built in LDS by all 64
+//                                  lanes), symbol decode.  Decoder state is
+//                                  wave-uniform (every lane computes the same,
+//                                  LDS reads are broadcasts made scalar with
+//                                  readfirstlane), so staging the input, building
+//                                  tables and flushing output use the whole wave
+//                                  without divergence.  Literals and stored bytes
+//                                  go to the output; each match becomes a record
+//                                  (pos, len, dist) in HBM.
+//   k_inflate_copy    wave/stream  resolves the matches in order through a 40 KiB
+//                                  LDS window (32 KiB history + a 4 KiB output
+//                                  chunk + one match of overhang), one lane per
+//                                  byte of a match.
+//   checksums                      k_adler32 / k_crc32 over the output (trailer)
+//   k_inflate_finish  thread/stream  trailer checks and uncompress2's status map.
+#include "zgpu_internal.h"
+
+namespace zgpu {
+
+constexpr int kIRing = 2048;          // staged input bytes
+constexpr int kOBuf = 1024;           // staged literal bytes
+constexpr int kMBuf = 64;             // staged match records
+constexpr int kLRoot = 10, kDRoot = 8, kCRoot = 7;
+constexpr uint32_t kSymBad = 0x1ff;   // table entry symbol of an invalid code (1 bit)
+constexpr uint32_t kLong = 0x8000;    // table entry flag: code longer than the root
+constexpr uint32_t kBadEntry = kSymBad | (1u << 9);
+
+struct Canon {                        // canonical decode of codes longer than the root
+    uint16_t count[16], first[16], offs[16];
+    uint16_t sorted[288];
+};
+
+struct InfLDS {
+    union { uint8_t b[kIRing + 16]; uint32_t w[(kIRing + 16) / 4]; } ring;
+    uint8_t obuf[kOBuf];
+    uint64_t mbuf[kMBuf];
+    uint16_t lt[1 << kLRoot], dt[1 << kDRoot], ct[1 << kCRoot];
+    Canon lcan, dcan;
+    uint16_t lens[320];
+};
+
+__device__ __constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
+                                                 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__device__ __constant__ uint8_t c_lext[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2,
+                                               3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__device__ __constant__ uint16_t c_dbase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129,
+                                                 193, 257, 385, 513, 769, 1025, 1537, 2049, 3073,
+                                                 4097, 6145, 8193, 12289, 16385, 24577};
+__device__ __constant__ uint8_t c_dext[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7,
+                                               8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__device__ __constant__ uint8_t c_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+__device__ __attribute__((always_inline)) inline uint32_t uni(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __attribute__((always_inline)) inline uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+enum { kCodes = 0, kLens = 1, kDists = 2 };
+
+// inflate_table's acceptance rules (inftrees.c:100-134,297-301) and a decode
+// table: root entries sym | len << 9 for codes up to `root` bits, kLong at the
+// root prefix of longer codes (canonical decode from `can`), kBadEntry where no
+// code lands (an empty or a single-1-bit code).  Wave-uniform; returns false on
+// an over-subscribed or forbidden incomplete set.
+template <int kRoot>
+__device__ bool build_code(const uint16_t *lens, int n, int type, uint16_t *T, Canon *can, int lane) {
+    uint32_t cnt[16];
+#pragma unroll
+    for (int l = 0; l < 16; l++) cnt[l] = 0;
+    for (int c = 0; c < n; c += 64) {
+        const int s = c + lane;
+        const uint32_t l = s < n ? lens[s] : 0u;
+#pragma unroll
+        for (int lv = 1; lv <= 15; lv++) cnt[lv] += (uint32_t)__builtin_popcountll(__ballot(l == (uint32_t)lv));
+    }
+    int max = 0;
+#pragma unroll
+    for (int lv = 1; lv <= 15; lv++)
+        if (cnt[lv]) max = lv;
+    for (int e = lane; e < (1 << kRoot); e += 64) T[e] = (uint16_t)kBadEntry;
+    if (max == 0) { __syncthreads(); return true; }
+    int left = 1;
+#pragma unroll
+    for (int lv = 1; lv <= 15; lv++) {
+        left = 2 * left - (int)cnt[lv];
+        if (left < 0) return false;                  // over-subscribed (uniform)
+    }
+    if (left > 0 && (type == kCodes || max != 1)) return false;
+    uint32_t first[16], offs[16];
+    {
+        uint32_t code = 0, off = 0;
+        first[0] = 0; offs[0] = 0;
+#pragma unroll
+        for (int lv = 1; lv <= 15; lv++) {
+            code = (code + cnt[lv - 1]) << 1;
+            first[lv] = code;
+            offs[lv] = off;
+            off += cnt[lv];
+        }
+    }
+    const bool longs = max > kRoot;
+    if (longs && lane < 16) {
+        uint32_t f = 0, o = 0, k = 0;
+#pragma unroll
+        for (int lv = 0; lv < 16; lv++)
+            if (lane == lv) { f = first[lv]; o = offs[lv]; k = cnt[lv]; }
+        can->first[lane] = (uint16_t)f;
+        can->offs[lane] = (uint16_t)o;
+        can->count[lane] = (uint16_t)k;
+    }
+    __syncthreads();
+    uint32_t rc[16];
+#pragma unroll
+    for (int l = 0; l < 16; l++) rc[l] = 0;
+    for (int c = 0; c < n; c += 64) {
+        const int s = c + lane;
+        const uint32_t l = s < n ? lens[s] : 0u;
+        uint32_t code = 0, off = 0;
+#pragma unroll
+        for (int lv = 1; lv <= 15; lv++) {
+            const uint64_t m = __ballot(l == (uint32_t)lv);
+            if (l == (uint32_t)lv) {
+                const uint32_t rank = rc[lv] + lanes_below(m);
+                code = first[lv] + rank;
+                off = offs[lv] + rank;
+            }
+            rc[lv] += (uint32_t)__builtin_popcountll(m);
+        }
+        if (l) {
+            const uint32_t rev = __brev(code) >> (32 - l);
+            if (longs) can->sorted[off] = (uint16_t)s;
+            if (l <= (uint32_t)kRoot) {
+                for (uint32_t e = rev; e < (1u << kRoot); e += 1u << l) T[e] = (uint16_t)(s | (l << 9));
+            } else {
+                T[rev & ((1u << kRoot) - 1)] = (uint16_t)kLong;
+            }
+        }
+    }
+    __syncthreads();
+    return true;
+}
+
+// one code from `hold` (>= 15 bits in hand or zero padded); returns the symbol
+// (kSymBad for an invalid code) and its length
+template <int kRoot>
+__device__ __attribute__((always_inline)) inline uint32_t dec_code(const uint16_t *T, const Canon *can,
+                                                                   uint64_t hold, uint32_t &len) {
+    const uint32_t e = uni(T[(uint32_t)hold & ((1u << kRoot) - 1)]);
+    if (!(e & kLong)) { len = (e >> 9) & 15u; return e & 0x1ffu; }
+    const uint32_t c = __brev((uint32_t)hold);
+    for (uint32_t l = kRoot + 1; l <= 15; l++) {
+        const uint32_t code = c >> (32 - l);
+        const uint32_t f = uni(can->first[l]), k = uni(can->count[l]);
+        if (code - f < k) { len = l; return uni(can->sorted[uni(can->offs[l]) + code - f]); }
+    }
+    len = 1;
+    return kSymBad;
+}
+
+struct Rd {                           // wave-uniform bit reader over the LDS input ring
+    uint64_t hold;
+    uint32_t bits, ipos, rbase;
+};
+
+__device__ __attribute__((always_inline)) inline void ring_stage(InfLDS &S, Rd &r, const uint8_t *in,
+                                                                 uint32_t n, uint32_t base, int lane) {
+    __syncthreads();
+    for (uint32_t i = (uint32_t)lane; i < (uint32_t)(kIRing + 16) / 4; i += 64) {
+        uint32_t w = 0;
+        const uint32_t x = base + 4 * i;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (x + k < n) w |= (uint32_t)in[x + k] << (8 * k);
+        S.ring.w[i] = w;
+    }
+    r.rbase = base;
+    __syncthreads();
+}
+
+// NEEDBITS-style: at least 32 bits in `hold` (zeros beyond the input)
+__device__ __attribute__((always_inline)) inline void refill(InfLDS &S, Rd &r, const uint8_t *in, uint32_t n,
+                                                             int lane) {
+    if (r.bits >= 32) return;
+    uint32_t o = r.ipos - r.rbase;
+    if (r.ipos < r.rbase || o + 8 > (uint32_t)kIRing) {
+        ring_stage(S, r, in, n, r.ipos & ~3u, lane);
+        o = r.ipos - r.rbase;
+    }
+    const uint32_t w0 = uni(S.ring.w[o >> 2]), w1 = uni(S.ring.w[(o >> 2) + 1]);
+    const uint32_t v = __builtin_amdgcn_alignbyte(w1, w0, o & 3u);
+    r.hold |= (uint64_t)v << r.bits;
+    r.bits += 32;
+    r.ipos += 4;
+}
+
+__device__ __attribute__((always_inline)) inline uint64_t bitpos(const Rd &r) {
+    return (uint64_t)r.ipos * 8 - r.bits;
+}
+__device__ __attribute__((always_inline)) inline void dropb(Rd &r, uint32_t k) { r.hold >>= k; r.bits -= k; }
+__device__ __attribute__((always_inline)) inline void seek(Rd &r, uint32_t byte) { r.hold = 0; r.bits = 0; r.ipos = byte; }
+
+__global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
+    __shared__ InfLDS S;
+    const int lane = threadIdx.x;
+    const uint32_t bi = blockIdx.x, g = job.first + bi;
+    const uint32_t n = (uint32_t)job.src_len[g];
+    const uint8_t *in = job.src + job.src_off[g];
+    const uint64_t cap0 = job.dst_cap[g];
+    const bool probe = cap0 == 0;
+    const uint32_t cap = probe ? 1u : (uint32_t)cap0;
+    uint8_t *out = job.dst + job.dst_off[g];
+    uint64_t *mrec = job.mrec + job.mrec_off[bi];
+    const uint64_t inbits = (uint64_t)n * 8;
+    const int wrap = job.wrap;
+
+    Rd r;
+    r.hold = 0; r.bits = 0; r.ipos = 0; r.rbase = 0;
+    ring_stage(S, r, in, n, 0, lane);
+
+    uint32_t put = 0, ob = 0, nm = 0, pbyte = 0;
+    uint32_t stop = kIEnd;
+    uint64_t used = 0, used_bad = 0;
+    uint32_t chk_kind = 0, chk_want = 0, isize = 0;
+    bool gz = false;
+
+    auto ceil_used = [&]() -> uint64_t { return (bitpos(r) + 7) >> 3; };
+    auto flush_obuf = [&](uint32_t upto) {          // output bytes [ob, upto), upto <= ob + kOBuf
+        __syncthreads();
+        if (!probe)
+            for (uint32_t i = (uint32_t)lane; i < upto - ob; i += 64) out[ob + i] = S.obuf[i];
+        __syncthreads();
+    };
+    auto flush_mbuf = [&](uint32_t k) {             // the last k staged records
+        __syncthreads();
+        if ((uint32_t)lane < k) mrec[nm - k + (uint32_t)lane] = S.mbuf[lane];
+        __syncthreads();
+    };
+
+    // ---------------- HEAD (inflate.c:622-669) / gzip header (:629-807) ----------------
+    if (wrap) {
+        refill(S, r, in, n, lane);
+        if (bitpos(r) + 16 > inbits) { stop = kIInEnd; used = n; goto done; }
+        const uint32_t h16 = (uint32_t)r.hold & 0xffffu;
+        if ((wrap & 2) && h16 == 0x8b1fu) {
+            gz = true;
+            // header fields straight from global memory (a few bytes)
+            if (n < 4) { stop = kIInEnd; used = n; goto done; }
+            const uint32_t flags = in[2] | ((uint32_t)in[3] << 8);
+            if ((flags & 0xffu) != 8u || (flags & 0xe000u)) { stop = kIData; used = 4; goto done; }
+            uint32_t p = 10;
+            if (n < p) { stop = kIInEnd; used = n; goto done; }
+            if (flags & 0x0400u) {                                   // FEXTRA
+                if (n < p + 2) { stop = kIInEnd; used = n; goto done; }
+                const uint32_t xlen = in[p] | ((uint32_t)in[p + 1] << 8);
+                p += 2;
+                if (n - p < xlen) { stop = kIInEnd; used = n; goto done; }
+                p += xlen;
+            }
+            for (uint32_t f = 0x0800u; f <= 0x1000u; f <<= 1) {      // FNAME, FCOMMENT
+                if (!(flags & f)) continue;
+                uint32_t z = 0xffffffffu;
+                for (uint32_t q = p; q < n && z == 0xffffffffu; q += 64) {
+                    const uint32_t x = q + (uint32_t)lane;
+                    const uint64_t m = __ballot(x < n && in[x] == 0);
+                    if (m) z = q + (uint32_t)__builtin_ctzll(m);
+                }
+                if (z == 0xffffffffu) { stop = kIInEnd; used = n; goto done; }
+                p = z + 1;
+            }
+            if (flags & 0x0200u) {                                   // FHCRC
+                if (n < p + 2) { stop = kIInEnd; used = n; goto done; }
+                uint32_t c = 0xffffffffu;
+                for (uint32_t q = 0; q < p; q++) c = job.crc_byte[(c ^ in[q]) & 0xffu] ^ (c >> 8);
+                c = ~c;
+                const uint32_t want = in[p] | ((uint32_t)in[p + 1] << 8);
+                p += 2;
+                if (want != (c & 0xffffu)) { stop = kIData; used = p; goto done; }
+            }
+            seek(r, p);
+        } else {
+            const uint32_t wlen = ((h16 >> 4) & 15u) + 8u;
+            if (!(wrap & 1) || ((((h16 & 0xffu) << 8) + (h16 >> 8)) % 31u) || (h16 & 15u) != 8u ||
+                wlen > 15u || (job.wbits && wlen > (uint32_t)job.wbits)) {
+                stop = kIData; used = 2; goto done;
+            }
+            dropb(r, 16);
+            if (h16 & 0x2000u) {                                     // FDICT: DICTID, Z_NEED_DICT
+                if (n < 6) { stop = kIInEnd; used = n; } else { stop = kIDict; used = 6; }
+                goto done;
+            }
+        }
+    }
+
+    // ---------------- blocks (inflate.c:827-1181) ----------------
+    for (;;) {
+        refill(S, r, in, n, lane);
+        if (bitpos(r) + 3 > inbits) { stop = kIInEnd; used = n; goto done; }
+        const uint32_t last = (uint32_t)r.hold & 1u, type = ((uint32_t)r.hold >> 1) & 3u;
+        dropb(r, 3);
+        if (type == 3) { stop = kIData; used = ceil_used(); goto done; }
+        if (type == 0) {                                             // STORED, COPY
+            dropb(r, r.bits & 7u);
+            refill(S, r, in, n, lane);
+            if (bitpos(r) + 32 > inbits) { stop = kIInEnd; used = n; goto done; }
+            const uint32_t len = (uint32_t)r.hold & 0xffffu, nlen = ((uint32_t)r.hold >> 16) & 0xffffu;
+            if (len != (nlen ^ 0xffffu)) { stop = kIData; used = (bitpos(r) >> 3) + 4; goto done; }
+            dropb(r, 32);
+            const uint32_t bp = (uint32_t)(bitpos(r) >> 3);
+            flush_obuf(put);
+            uint32_t cnt = len;
+            if (cnt > n - bp) cnt = n - bp;
+            if (cnt > cap - put) cnt = cap - put;
+            if (probe) { if (cnt) pbyte = in[bp]; }
+            else for (uint32_t i = (uint32_t)lane; i < cnt; i += 64) out[put + i] = in[bp + i];
+            put += cnt;
+            ob = put;
+            seek(r, bp + cnt);
+            if (cnt < len) {
+                if (put == cap) { stop = kIFull; used = bp + cnt; } else { stop = kIInEnd; used = n; }
+                goto done;
+            }
+        } else {
+            if (type == 1) {                                         // fixedtables (inflate.c:255-285)
+                for (int i = lane; i < 288; i += 64)
+                    S.lens[i] = (uint16_t)(i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8);
+                __syncthreads();
+                build_code<kLRoot>(S.lens, 288, kLens, S.lt, &S.lcan, lane);
+                for (int i = lane; i < 32; i += 64) S.lens[i] = 5;
+                __syncthreads();
+                build_code<kDRoot>(S.lens, 32, kDists, S.dt, &S.dcan, lane);
+            } else {                                                 // TABLE, LENLENS, CODELENS
+                refill(S, r, in, n, lane);
+                if (bitpos(r) + 14 > inbits) { stop = kIInEnd; used = n; goto done; }
+                const uint32_t nlen = ((uint32_t)r.hold & 31u) + 257;
+                const uint32_t ndist = (((uint32_t)r.hold >> 5) & 31u) + 1;
+                const uint32_t ncode = (((uint32_t)r.hold >> 10) & 15u) + 4;
+                dropb(r, 14);
+                if (nlen > 286 || ndist > 30) { stop = kIData; used = ceil_used(); goto done; }
+                uint32_t cl = 0;                                     // lane i: length of code-length code i
+                {
+                    uint32_t have = 0;
+                    while (have < ncode) {
+                        refill(S, r, in, n, lane);
+                        if (bitpos(r) + 3 > inbits) { stop = kIInEnd; used = n; goto done; }
+                        const uint32_t v = (uint32_t)r.hold & 7u;
+                        if ((uint32_t)lane == c_order[have]) cl = v;
+                        dropb(r, 3);
+                        have++;
+                    }
+                }
+                if (lane < 19) S.lens[lane] = (uint16_t)cl;
+                __syncthreads();
+                if (!build_code<kCRoot>(S.lens, 19, kCodes, S.ct, nullptr, lane)) {
+                    stop = kIData; used = ceil_used(); goto done;
+                }
+                uint32_t have = 0;
+                const uint32_t total = nlen + ndist;
+                while (have < total) {
+                    refill(S, r, in, n, lane);
+                    const uint32_t e = uni(S.ct[(uint32_t)r.hold & 127u]);
+                    const uint32_t L = (e >> 9) & 15u, sym = e & 0x1ffu;
+                    if (bitpos(r) + L > inbits) { stop = kIInEnd; used = n; goto done; }
+                    dropb(r, L);
+                    if (sym == kSymBad || sym < 16) {                // empty code-length code: 0 per bit
+                        if (lane == 0) S.lens[have] = (uint16_t)(sym == kSymBad ? 0 : sym);
+                        have++;
+                        continue;
+                    }
+                    uint32_t len, rep;
+                    if (sym == 16) {
+                        if (bitpos(r) + 2 > inbits) { stop = kIInEnd; used = n; goto done; }
+                        if (have == 0) { stop = kIData; used = (bitpos(r) + 2 + 7) >> 3; goto done; }
+                        __syncthreads();
+                        len = uni(S.lens[have - 1]);
+                        rep = 3 + ((uint32_t)r.hold & 3u);
+                        dropb(r, 2);
+                    } else if (sym == 17) {
+                        if (bitpos(r) + 3 > inbits) { stop = kIInEnd; used = n; goto done; }
+                        len = 0;
+                        rep = 3 + ((uint32_t)r.hold & 7u);
+                        dropb(r, 3);
+                    } else {
+                        if (bitpos(r) + 7 > inbits) { stop = kIInEnd; used = n; goto done; }
+                        len = 0;
+                        rep = 11 + ((uint32_t)r.hold & 127u);
+                        dropb(r, 7);
+                    }
+                    if (have + rep > total) { stop = kIData; used = ceil_used(); goto done; }
+                    for (uint32_t k = (uint32_t)lane; k < rep; k += 64) S.lens[have + k] = (uint16_t)len;
+                    have += rep;
+                }
+                __syncthreads();
+                if (uni(S.lens[256]) == 0) { stop = kIData; used = ceil_used(); goto done; }
+                if (!build_code<kLRoot>(S.lens, (int)nlen, kLens, S.lt, &S.lcan, lane)) {
+                    stop = kIData; used = ceil_used(); goto done;
+                }
+                if (!build_code<kDRoot>(S.lens + nlen, (int)ndist, kDists, S.dt, &S.dcan, lane)) {
+                    stop = kIData; used = ceil_used(); goto done;
+                }
+            }
+            // ---------------- LEN .. MATCH / LIT ----------------
+            for (;;) {
+                refill(S, r, in, n, lane);
+                uint32_t L;
+                const uint32_t sym = dec_code<kLRoot>(S.lt, &S.lcan, r.hold, L);
+                if (bitpos(r) + L > inbits) { stop = kIInEnd; used = n; goto done; }
+                dropb(r, L);
+                if (sym < 256) {
+                    if (put == cap) { stop = kIFull; used = ceil_used(); goto done; }
+                    if (probe) pbyte = sym;
+                    else if (lane == 0) S.obuf[put - ob] = (uint8_t)sym;
+                    put++;
+                    if (put - ob == (uint32_t)kOBuf) { flush_obuf(put); ob = put; }
+                    continue;
+                }
+                if (sym == 256) break;
+                if (sym > 285) { stop = kIData; used = ceil_used(); goto done; }   // kSymBad, 286, 287
+                const uint32_t ls = sym - 257, xl = c_lext[ls];
+                if (bitpos(r) + xl > inbits) { stop = kIInEnd; used = n; goto done; }
+                const uint32_t len = c_lbase[ls] + ((uint32_t)r.hold & ((1u << xl) - 1u));
+                dropb(r, xl);
+                refill(S, r, in, n, lane);
+                uint32_t DL;
+                const uint32_t ds = dec_code<kDRoot>(S.dt, &S.dcan, r.hold, DL);
+                if (bitpos(r) + DL > inbits) { stop = kIInEnd; used = n; goto done; }
+                dropb(r, DL);
+                if (ds > 29) { stop = kIData; used = ceil_used(); goto done; }
+                const uint32_t xd = c_dext[ds];
+                if (bitpos(r) + xd > inbits) { stop = kIInEnd; used = n; goto done; }
+                const uint32_t dist = c_dbase[ds] + ((uint32_t)r.hold & ((1u << xd) - 1u));
+                dropb(r, xd);
+                if (put == cap) { stop = kIFull; used = ceil_used(); goto done; }    // MATCH: room first
+                if (dist > put) { stop = kIData; used = ceil_used(); goto done; }    // too far back
+                const uint32_t copy = len < cap - put ? len : cap - put;
+                if (lane == 0) S.mbuf[nm & (kMBuf - 1)] = (uint64_t)put | ((uint64_t)copy << 32) | ((uint64_t)dist << 41);
+                nm++;
+                if ((nm & (kMBuf - 1)) == 0) flush_mbuf(kMBuf);
+                put += copy;
+                while (put - ob >= (uint32_t)kOBuf) { flush_obuf(ob + kOBuf); ob += kOBuf; }
+                if (copy < len) { stop = kIFull; used = ceil_used(); goto done; }
+            }
+        }
+        if (last) break;
+    }
+
+    // ---------------- CHECK, LENGTH (inflate.c:1183-1221) ----------------
+    dropb(r, r.bits & 7u);
+    if (wrap && !gz) {
+        refill(S, r, in, n, lane);
+        if (bitpos(r) + 32 > inbits) { stop = kIInEnd; used = n; goto done; }
+        const uint32_t h = (uint32_t)r.hold;
+        chk_want = (h >> 24) | ((h >> 8) & 0xff00u) | ((h << 8) & 0xff0000u) | (h << 24);
+        dropb(r, 32);
+        chk_kind = 1;
+        used = used_bad = bitpos(r) >> 3;
+    } else if (gz) {
+        refill(S, r, in, n, lane);
+        if (bitpos(r) + 32 > inbits) { stop = kIInEnd; used = n; goto done; }
+        chk_want = (uint32_t)r.hold;
+        dropb(r, 32);
+        chk_kind = 2;
+        used_bad = bitpos(r) >> 3;
+        refill(S, r, in, n, lane);
+        if (bitpos(r) + 32 > inbits) {
+            isize = 3;
+            used = n;
+        } else {
+            isize = (uint32_t)r.hold == put ? 1 : 2;
+            dropb(r, 32);
+            used = bitpos(r) >> 3;
+        }
+    } else {
+        used = bitpos(r) >> 3;
+    }
+    stop = kIEnd;
+
+done:
+    flush_obuf(put);
+    if (nm & (kMBuf - 1)) flush_mbuf(nm & (kMBuf - 1));
+    if (lane == 0) {
+        InflateRec rc;
+        rc.put = put;
+        rc.used = used;
+        rc.used_bad = used_bad;
+        rc.stop = stop;
+        rc.nmatch = nm;
+        rc.chk_kind = chk_kind;
+        rc.chk_want = chk_want;
+        rc.isize = isize;
+        rc.pbyte = pbyte;
+        job.rec[bi] = rc;
+        job.dst_len[g] = probe ? 0 : put;            // the checksum kernels read this
+    }
+}
+
+// ------------------------------------------------------------------------
+// k_inflate_copy — matches in stream order through an LDS window.
+// ------------------------------------------------------------------------
+constexpr uint32_t kWin = 40960;       // >= 32768 + kChunk + 258
+constexpr uint32_t kChunk = 4096;
+
+__device__ __attribute__((always_inline)) inline uint32_t wslot(uint32_t p) { return p % kWin; }
+
+__global__ __launch_bounds__(64) void k_inflate_copy(InflateJob job) {
+    __shared__ uint8_t W[kWin];
+    const int lane = threadIdx.x;
+    const uint32_t bi = blockIdx.x, g = job.first + bi;
+    const InflateRec rc = job.rec[bi];
+    if (job.dst_cap[g] == 0 || rc.nmatch == 0) return;
+    const uint32_t put = (uint32_t)rc.put, nm = rc.nmatch;
+    uint8_t *out = job.dst + job.dst_off[g];
+    const uint64_t *M = job.mrec + job.mrec_off[bi];
+    uint32_t loaded = 0, mi = 0, mbase = 0;
+    uint64_t mreg = (uint32_t)lane < nm ? M[lane] : 0;
+    // the first chunk that holds a match; earlier output is final already
+    const uint32_t p0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)mreg);
+    uint32_t c0 = p0 >= 32768u + kChunk ? ((p0 - 32768u) / kChunk) * kChunk : 0u;
+    loaded = c0 >= 32768u ? c0 - 32768u : 0u;
+    for (; c0 < put && mi < nm; c0 += kChunk) {
+        const uint32_t c1 = c0 + kChunk < put ? c0 + kChunk : put;
+        const uint32_t want = c1 + 258 < put ? c1 + 258 : put;
+        for (uint32_t p = loaded + (uint32_t)lane; p < want; p += 64) W[wslot(p)] = out[p];
+        loaded = want;
+        __syncthreads();
+        while (mi < nm) {
+            if (mi - mbase >= 64) {
+                mbase = mi;
+                mreg = mbase + (uint32_t)lane < nm ? M[mbase + lane] : 0;
+            }
+            const int k = (int)(mi - mbase);
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mreg, k);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mreg >> 32), k);
+            const uint32_t pos = lo;
+            if (pos >= c1) break;
+            const uint32_t len = hi & 511u, dist = hi >> 9;
+            const uint32_t s0 = pos - dist;
+            if (dist >= len) {
+                for (uint32_t j = (uint32_t)lane; j < len; j += 64) W[wslot(pos + j)] = W[wslot(s0 + j)];
+            } else {
+                for (uint32_t j = (uint32_t)lane; j < len; j += 64) W[wslot(pos + j)] = W[wslot(s0 + j % dist)];
+            }
+            mi++;
+        }
+        __syncthreads();
+        // [c0, want): final below c1; the overhang holds literals, the tails of
+        // matches that started in this chunk and (harmless) unresolved bytes
+        // that a later chunk rewrites
+        for (uint32_t p = c0 + (uint32_t)lane; p < want; p += 64) out[p] = W[wslot(p)];
+        __syncthreads();
+    }
+    // output after the last chunk holding a match is literal-only and final
+}
+
+// ------------------------------------------------------------------------
+// k_inflate_finish — trailer checks and uncompress2's result (uncompr.c:62-84)
+// ------------------------------------------------------------------------
+__global__ void k_inflate_finish(InflateJob job) {
+    const uint32_t bi = blockIdx.x * blockDim.x + threadIdx.x;
+    if (bi >= job.count) return;
+    const uint32_t g = job.first + bi;
+    const InflateRec rc = job.rec[bi];
+    const uint64_t cap0 = job.dst_cap[g];
+    const bool probe = cap0 == 0;
+    uint32_t stop = rc.stop;
+    uint64_t used = rc.used;
+    if (stop == kIEnd && rc.chk_kind) {
+        uint32_t got;
+        if (probe) {                               // at most one byte was produced
+            if (rc.chk_kind == 1) {
+                got = rc.put ? ((1u + rc.pbyte) | ((1u + rc.pbyte) << 16)) : 1u;
+            } else {
+                got = rc.put ? ~(job.crc_byte[(0xffffffffu ^ rc.pbyte) & 0xffu] ^ 0x00ffffffu) : 0u;
+            }
+        } else {
+            got = rc.chk_kind == 1 ? job.adler[bi] : job.crc[bi];
+        }
+        if (got != rc.chk_want) { stop = kIData; used = rc.used_bad; }
+        else if (rc.chk_kind == 2 && rc.isize == 2) stop = kIData;
+        else if (rc.chk_kind == 2 && rc.isize == 3) stop = kIInEnd;
+    }
+    int32_t status;
+    if (stop == kIEnd) status = 0;                                    // Z_OK
+    else if (stop == kIData || stop == kIDict) status = -3;          // Z_DATA_ERROR
+    else status = (probe || rc.put < cap0) ? -3 : -5;                // Z_BUF_ERROR only when full
+    job.status[g] = status;
+    if (job.stop_out) job.stop_out[g] = stop;
+    job.dst_len[g] = probe ? 0 : rc.put;
+    if (job.src_used) job.src_used[g] = used;
+}
+
+int launch_inflate_stage(int stage, const InflateJob &job, hipStream_t st) {
+    if (job.count == 0) return 0;
+    switch (stage) {
+    case 0: hipLaunchKernelGGL(k_inflate_decode, dim3(job.count), dim3(64), 0, st, job); break;
+    case 1: hipLaunchKernelGGL(k_inflate_copy, dim3(job.count), dim3(64), 0, st, job); break;
+    case 2: hipLaunchKernelGGL(k_inflate_finish, dim3((job.count + 255) / 256), dim3(256), 0, st, job); break;
+    default: return -1;
+    }
+    return (int)hipGetLastError();
+}
+
+}  // namespace zgpu

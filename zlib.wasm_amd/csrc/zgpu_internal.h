@@ -93,6 +93,44 @@ struct DeflateJob {
     uint32_t *check;         // [count] adler32 / crc32 of the input (trailer)
 };
 
+// ---- inflate ----
+// where k_inflate_decode stopped (zo_inflate_run's codes)
+enum InflateStop : uint32_t { kIEnd = 0, kIData = 1, kIDict = 2, kIFull = 3, kIInEnd = 4 };
+
+struct InflateRec {          // per stream, written by k_inflate_decode
+    uint64_t put;            // output bytes produced
+    uint64_t used;           // input bytes consumed at the stop (check passed)
+    uint64_t used_bad;       // consumed when the trailer check fails
+    uint32_t stop;           // InflateStop; kIEnd may still fail its check
+    uint32_t nmatch;         // match records for k_inflate_copy
+    uint32_t chk_kind;       // 0 none, 1 Adler-32 (zlib), 2 CRC-32 (gzip)
+    uint32_t chk_want;       // trailer value
+    uint32_t isize;          // gzip ISIZE: 0 n/a, 1 equal, 2 differs, 3 input ended
+    uint32_t pbyte;          // probe mode (capacity 0): the byte produced, if any
+};
+
+struct InflateJob {
+    const uint8_t *src;
+    const uint64_t *src_off;
+    const uint64_t *src_len;
+    uint8_t *dst;
+    const uint64_t *dst_off;
+    const uint64_t *dst_cap;
+    uint64_t *dst_len;
+    uint64_t *src_used;      // may be null
+    int32_t *status;
+    uint32_t *stop_out;      // may be null: InflateStop after the checks
+    uint32_t first, count;
+    int wrap;                // 0 raw, 1 zlib, 2 gzip, 3 zlib or gzip
+    int wbits;               // inflateInit2_ window bits (8..15; 0: the header's)
+    const uint64_t *mrec_off;   // per sub-batch stream: first match record
+    uint64_t *mrec;          // match records: pos | len << 32 | dist << 41
+    InflateRec *rec;         // [count]
+    uint32_t *adler, *crc;   // [count] checks of the produced output
+    const uint32_t *crc_byte;   // CRC-32 byte table (device)
+};
+int launch_inflate_stage(int stage, const InflateJob &job, hipStream_t st);
+
 // launchers (return hipError_t as int)
 int launch_tables_upload(const CodeTables *ct, const CrcTables *crc);
 const CrcTables *device_crc_tables();

@@ -39,17 +39,23 @@ EXPORTED_SYMBOLS = (
     "zgpu_deflate_batch_dev_ex", "zgpu_compress_batch_ex",
     "zgpu_crc32_batch_dev", "zgpu_adler32_batch_dev", "zgpu_compress_batch",
     "zgpu_crc32_batch", "zgpu_adler32_batch", "zgpu_generate_dev", "zgpu_stage_timing",
-    "zgpu_stage_timing_read",
+    "zgpu_stage_timing_read", "zgpu_inflate_batch_dev", "zgpu_uncompress_batch",
     # include/zgpu_zlib.h
     "zlibVersion", "compress", "compress2", "compressBound", "deflateInit_",
     "deflateInit2_", "deflate", "deflateEnd", "deflateBound", "crc32", "crc32_z",
     "crc32_combine", "crc32_combine64", "crc32_combine_gen", "crc32_combine_gen64",
     "crc32_combine_op", "adler32", "adler32_z", "adler32_combine", "adler32_combine64",
+    "uncompress", "uncompress2", "inflateInit_", "inflateInit2_", "inflate", "inflateEnd",
+    "inflateReset",
     # include/zgpu_wasm.h
     "zlib_compress_buffer", "zlib_crc32", "zlib_adler32", "zlib_compress_bound",
     "zlib_get_version", "zlib_compress_simd", "zlib_compress_simd_full",
     "zlib_compress_simd_buffer", "zlib_crc32_simd_optimized", "zlib_crc32_simd_enhanced",
-    "zlib_adler32_simd",
+    "zlib_adler32_simd", "zlib_decompress_buffer", "zlib_decompress_optimized",
+    "zlib_decompress", "zlib_compress_optimized", "zlib_compress", "zlib_deflate_init",
+    "zlib_deflate_process", "zlib_deflate_end", "zlib_inflate_init", "zlib_inflate_process",
+    "zlib_inflate_end", "zlib_stream_avail_in", "zlib_stream_avail_out", "zlib_stream_total_in",
+    "zlib_stream_total_out",
     # include/zgpu_debug.h (test-only)
     "zgpu_debug_stages",
 )
@@ -117,6 +123,14 @@ def load(path=LIB_PATH):
     L.zlibVersion.restype = C.c_char_p
     L.zlib_compress_simd.restype = I32
     L.zlib_compress_simd.argtypes = [P, C.c_size_t, P, C.POINTER(C.c_size_t), I32]
+    L.zgpu_inflate_batch_dev.restype = I32
+    L.zgpu_inflate_batch_dev.argtypes = [P, P, P, P, P, P, P, P, P, U32, I32, P]
+    L.zgpu_uncompress_batch.restype = I32
+    L.zgpu_uncompress_batch.argtypes = [P, P, P, P, P, P, C.c_size_t, I32]
+    L.uncompress2.restype = I32
+    L.uncompress2.argtypes = [P, C.POINTER(C.c_ulong), P, C.POINTER(C.c_ulong)]
+    L.uncompress.restype = I32
+    L.uncompress.argtypes = [P, C.POINTER(C.c_ulong), P, C.c_ulong]
     _lib = L
     return L
 
@@ -163,6 +177,47 @@ def compress_batch(bufs, level=6, wrap=WRAP_ZLIB, caps=None, strategy=0):
         raise ZlibCompressionError(f"zgpu_compress_batch failed: {rc}")
     del keep
     return [(st[i], outs[i].raw[: dlen[i]]) for i in range(n)]
+
+
+WRAP_AUTO = 3
+
+
+def uncompress_batch(bufs, caps, wrap=WRAP_ZLIB):
+    """Inflate independent host streams on the GPU: [(status, bytes, consumed)]
+    with uncompress2 semantics per stream (``caps[i]`` = output capacity)."""
+    L = load()
+    n = len(bufs)
+    src, keep = _ptr_array(bufs)
+    lens = (C.c_size_t * n)(*[len(b) for b in bufs])
+    outs = [C.create_string_buffer(max(c, 1)) for c in caps]
+    dst = (C.c_void_p * n)(*[C.addressof(o) for o in outs])
+    dlen = (C.c_size_t * n)(*caps)
+    used = (C.c_size_t * n)()
+    st = (C.c_int * n)()
+    rc = L.zgpu_uncompress_batch(src, lens, dst, dlen, used, st, n, wrap)
+    if rc:
+        raise ZlibError(f"zgpu_uncompress_batch failed: {rc}")
+    del keep
+    return [(st[i], outs[i].raw[: dlen[i]], used[i]) for i in range(n)]
+
+
+def uncompress2(data, cap):
+    """zlib uncompress2() through the drop-in symbol: (rc, bytes, consumed)."""
+    L = load()
+    data = bytes(data)
+    out = C.create_string_buffer(max(cap, 1))
+    dl, sl = C.c_ulong(cap), C.c_ulong(len(data))
+    rc = L.uncompress2(out, C.byref(dl), data, C.byref(sl))
+    return rc, out.raw[: dl.value], sl.value
+
+
+def inflate_batch_dev(src, src_off, src_len, dst, dst_off, dst_cap, dst_len, status, src_used=None,
+                      wrap=WRAP_ZLIB, stream=None):
+    rc = load().zgpu_inflate_batch_dev(_dp(src), _dp(src_off), _dp(src_len), _dp(dst), _dp(dst_off),
+                                       _dp(dst_cap), _dp(dst_len), _dp(src_used), _dp(status),
+                                       src_len.numel(), wrap, _stream(stream))
+    if rc:
+        raise ZlibError(f"zgpu_inflate_batch_dev failed: {rc}")
 
 
 def _checksum_batch(fn, bufs, inits):
