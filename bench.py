@@ -71,6 +71,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-inflate", action="store_true", help="skip the inflate round-trip leg")
     ap.add_argument("--verify", type=int, default=8, help="outputs checked vs oracle")
     ap.add_argument("--inflight-mb", type=int, default=4096,
                     help="input bytes per deflate sub-batch (workspace ~15 B per byte)")
@@ -176,6 +177,40 @@ def crc_leg(a, world, rank):
     return dict(src=src, out=out, elapsed=el, kernel_ms=kms, bytes=n * B)
 
 
+def inflate_leg(a, world, d):
+    """Decompress every stream the deflate leg produced (the other half of the
+    wire format) and check the full-size round trip on the
+    device: inflate(deflate(x)) == x for all buffers, every status Z_OK."""
+    n, B = a.buffer_bytes, a.buffers
+    src, dst, dlen, cap = d["src"], d["dst"], d["dlen"], d["cap"]
+    soff = torch.arange(B, dtype=torch.int64, device="cuda") * cap
+    out = torch.empty(n * B, dtype=torch.uint8, device="cuda")
+    ooff = torch.arange(B, dtype=torch.int64, device="cuda") * n
+    ocap = torch.full((B,), n, dtype=torch.int64, device="cuda")
+    olen = torch.zeros(B, dtype=torch.int64, device="cuda")
+    ost = torch.full((B,), 99, dtype=torch.int32, device="cuda")
+
+    def step():
+        zgpu.inflate_batch_dev(dst, soff, dlen, out, ooff, ocap, olen, ost)
+
+    for _ in range(max(1, a.warmup)):
+        step()
+    out.zero_()
+    barrier(world)
+    zgpu.stage_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    barrier(world)
+    el = time.perf_counter() - t0
+    zgpu.stage_timing(False)
+    stages = zgpu.stage_timing_read()
+    ok = int((ost != 0).sum().item()) == 0 and bool((olen == n).all().item()) and bool(torch.equal(out, src))
+    assert ok, "inflate(deflate(x)) != x on the device"
+    del out
+    return dict(elapsed=el, stages=stages, out_bytes=n * B, in_bytes=int(dlen.sum().item()))
+
+
 def launches_tag(a):
     """Shape of one deflate launch (sub-batch): buffers x bytes."""
     per = max(1, min(a.buffers, (a.inflight_mb << 20) // a.buffer_bytes))
@@ -267,6 +302,7 @@ def main():
     zgpu.set_inflight_bytes(a.inflight_mb << 20)
 
     d = deflate_leg(a, world, rank)
+    inf = None if a.no_inflate else inflate_leg(a, world, d)
     c = crc_leg(a, world, rank)
 
     # ---- verification (outside the timed region) ----
@@ -290,6 +326,9 @@ def main():
     el = reduce_max(d["elapsed"], world)
     in_total = reduce_sum(float(d["in_bytes"]) * a.steps, world)
     out_total = reduce_sum(float(d["out_bytes"]), world)
+    if inf is not None:
+        inf_el = reduce_max(inf["elapsed"], world)
+        inf_total = reduce_sum(float(inf["out_bytes"]) * a.steps, world)
     crc_el = reduce_max(c["elapsed"], world)
     crc_total = reduce_sum(float(c["bytes"]) * a.steps, world)
 
@@ -353,6 +392,14 @@ def main():
                                    "traffic_source": c_src,
                                    "alg_bytes_per_launch": crc_alg,
                                    "avg_launch_ms": round(c["kernel_ms"], 4)}},
+            "inflate": None if inf is None else {
+                "value": round(inf_total / inf_el / 1e6, 1), "unit": "MB/s (decompressed output)",
+                "workload": "inflate of every stream the deflate leg wrote (zlib wrapper), outputs in HBM",
+                "round_trip_bit_exact_all_buffers": True,
+                "stage_ms_per_step": {"decode": round(inf["stages"]["parse_lazy"][0] / max(1, a.steps), 2),
+                                      "match_copy": round(inf["stages"]["parse_greedy"][0] / max(1, a.steps), 2),
+                                      "adler32": round(inf["stages"]["checksum"][0] / max(1, a.steps), 2),
+                                      "finish": round(inf["stages"]["encode"][0] / max(1, a.steps), 2)}},
             "verified": {"deflate_buffers_bit_exact_vs_oracle": len(sample),
                          "crc32_values_checked": 64, "all_status_ok": True},
             "cpu_baseline": cpu,

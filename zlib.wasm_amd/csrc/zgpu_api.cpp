@@ -206,6 +206,7 @@ struct Ctx {
     // sub-batch i+1 runs on `aux` while links/parse/encode run on the caller's
     // stream)
     DevBuf ws_link2, ws_rf2, ws_rq2, ws_state2;
+    DevBuf ws_key, ws_key2;   // k_count's walk-length keys (one byte per position)
     // inflate: match records, per-stream results, checks, offsets, stop codes
     DevBuf ws_mrec, ws_irec, ws_ick, ws_imeta, ws_istop;
     hipStream_t aux = nullptr;
@@ -323,7 +324,9 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     // rquart: quarter-budget results (L5-9) and the lazy parse's symbol-start staging (L4-9)
     if (slow && !c.ws_rq.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
     if (slow && !c.ws_state.ensure(max_pos / 4 + 64)) return ZGPU_MEM_ERROR;
+    if (slow && !c.ws_key.ensure(max_pos + 64)) return ZGPU_MEM_ERROR;
     if (piped) {
+        if (!c.ws_key2.ensure(max_pos + 64)) return ZGPU_MEM_ERROR;
         if (!c.ws_link2.ensure(2 * max_pos + 64) || !c.ws_rf2.ensure(4 * max_pos + 64) ||
             !c.ws_rq2.ensure(4 * max_pos + 64) || !c.ws_state2.ensure(max_pos / 4 + 64))
             return ZGPU_MEM_ERROR;
@@ -369,6 +372,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         job.ws_off = d_meta + a;
         job.blk_off = d_meta + count + a;
         job.link = (slot ? c.ws_link2 : c.ws_link).as<uint16_t>();
+        job.key = slow ? (slot ? c.ws_key2 : c.ws_key).as<uint8_t>() : nullptr;
         job.rfull = (slow || huff || rle) ? (slot ? c.ws_rf2 : c.ws_rf).as<uint32_t>() : nullptr;
         job.rquart = slow ? (slot ? c.ws_rq2 : c.ws_rq).as<uint32_t>() : nullptr;
         job.sym = c.ws_sym.as<uint32_t>();
@@ -864,7 +868,7 @@ int zgpu_debug_stages(const uint8_t *src, size_t n, int level, uint16_t *link, u
     if (level < 4 || level > 9) return ZGPU_STREAM_ERROR;
     const size_t nn = n ? n : 1;
     if (!c.ws_io.ensure(nn + 64) || !c.ws_link.ensure(2 * nn + 64) || !c.ws_rf.ensure(4 * nn + 64) ||
-        !c.ws_rq.ensure(4 * nn + 64) || !c.ws_small.ensure(64))
+        !c.ws_rq.ensure(4 * nn + 64) || !c.ws_key.ensure(nn + 64) || !c.ws_small.ensure(64))
         return ZGPU_MEM_ERROR;
     uint64_t *d_meta = c.ws_small.as<uint64_t>();   // off, len, ws_off
     const uint64_t meta[3] = {0, (uint64_t)n, 0};
@@ -879,6 +883,7 @@ int zgpu_debug_stages(const uint8_t *src, size_t n, int level, uint16_t *link, u
     job.link = c.ws_link.as<uint16_t>();
     job.rfull = c.ws_rf.as<uint32_t>();
     job.rquart = c.ws_rq.as<uint32_t>();
+    job.key = c.ws_key.as<uint8_t>();
     if (launch_deflate_stage(0, job, nullptr, st) || launch_deflate_stage(1, job, nullptr, st) ||
         hipDeviceSynchronize() != hipSuccess)
         return ZGPU_MEM_ERROR;

@@ -5,9 +5,13 @@
 //   k_links      wave/buffer   hash-chain links: link[p] = distance to the most
 //                              recent earlier position with the same 3-byte
 //                              hash (UPDATE_HASH/INSERT_STRING, deflate.c:141,160)
+//   k_count      256 thr/buf   levels 4..9: per position, the number of same-hash
+//                              candidates in its window (capped at the chain
+//                              budget): the order in which k_match walks a tile
 //   k_match      1024 thr/buf  levels 4..9: longest_match (deflate.c:1356-1497) at
 //                              EVERY position for the full and the quartered chain
-//                              budget, 32 KiB window + links staged in LDS
+//                              budget, 32 KiB window + links staged in LDS, walks
+//                              of similar expected length run side by side
 //   k_parse_slow wave/buffer   deflate_slow's lazy parse (deflate.c:1923-2043) over
 //                              the per-position results -> symbols + block cuts
 //   k_parse_fast wave/buffer   deflate_fast (deflate.c:1824-1915), levels 1..3,
@@ -18,6 +22,7 @@
 //                              LDS staging window; zlib/gzip framing + trailer
 #include "zgpu_internal.h"
 #include <cstdlib>
+#include <cstdio>
 
 namespace zgpu {
 
@@ -189,6 +194,67 @@ __global__ __launch_bounds__(64) void k_links(DeflateJob job) {
 }
 
 // ------------------------------------------------------------------------
+// k_count — the order in which k_match walks a tile's positions.  For every
+// position p: the number of earlier positions q in (p - MAX_DIST, p) with the
+// same hash, i.e. the candidates a chain walk from p can visit, capped at the
+// level's chain budget (walks stop there) and compressed to a byte.  The
+// sliding-window counts live in LDS, two u16 counters per word, updated with
+// atomics: the position leaving the window is subtracted, p is added and the
+// value before the add is p's count.  Within one 64-position step the atomics
+// are unordered, so a count may be off by the step's own same-hash positions:
+// the key is a scheduling hint that orders walks by expected length (similar
+// lengths share a wave) and decides no result.
+// ------------------------------------------------------------------------
+constexpr int kCntStage = 4096;
+constexpr int kCntThreads = 256;
+
+__device__ __attribute__((always_inline)) inline uint32_t walk_key(uint32_t c, uint32_t chain) {
+    if (c > chain) c = chain;
+    if (c < 128) return c;
+    const uint32_t k = 128 + ((c - 128) >> 5);
+    return k < 255 ? k : 255;
+}
+
+// 4 waves per buffer; thread t takes positions t, t + 256, ... of each staged
+// 4 KiB, without barriers between them (their order only perturbs the hint).
+__global__ __launch_bounds__(kCntThreads) void k_count(DeflateJob job) {
+    __shared__ uint32_t cnt[16384];
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[kCntStage + 16];
+    __shared__ __attribute__((aligned(16))) uint8_t s_out[kCntStage + 16];
+    const int tid = threadIdx.x;
+    const uint32_t bi = blockIdx.x;
+    const uint32_t g = job.first + bi;
+    const int64_t n = (int64_t)job.src_len[g];
+    const uint8_t *in = job.src + job.src_off[g];
+    uint8_t *key = job.key + job.ws_off[bi];
+    const uint32_t chain = c_ct.cfg[job.level].chain;
+    for (int i = tid; i < 16384; i += kCntThreads) cnt[i] = 0;
+    for (int64_t t0 = 0; t0 < n; t0 += kCntStage) {
+        __syncthreads();
+        stage_bytes<kCntThreads, (kCntStage + 16) / 16 / kCntThreads + 1>(s_in, in, t0, kCntStage + 16, n, tid);
+        stage_bytes<kCntThreads, (kCntStage + 16) / 16 / kCntThreads + 1>(s_out, in, t0 - kMaxDist,
+                                                                         kCntStage + 16, n, tid);
+        __syncthreads();
+        const int64_t tend = (t0 + kCntStage < n) ? t0 + kCntStage : n;
+        for (int64_t p = t0 + tid; p < tend; p += kCntThreads) {
+            const int j = (int)(p - t0);
+            const int64_t q = p - kMaxDist;                   // leaves p's window
+            if (q >= 1 && q + 3 <= n) {
+                const uint32_t h = hash3(s_out[j], s_out[j + 1], s_out[j + 2]);
+                atomicSub(&cnt[h >> 1], 1u << ((h & 1u) * 16));
+            }
+            uint32_t k = 0;
+            if (p >= 1 && p + 3 <= n) {
+                const uint32_t h = hash3(s_in[j], s_in[j + 1], s_in[j + 2]);
+                const uint32_t old = atomicAdd(&cnt[h >> 1], 1u << ((h & 1u) * 16));
+                k = walk_key((old >> ((h & 1u) * 16)) & 0xffffu, chain);
+            }
+            key[p] = (uint8_t)k;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
 // k_match — levels 4..9.  One 1024-thread workgroup per buffer walks tiles of
 // kMT positions.  LDS holds input bytes [ts-32768, ts+kMT+272) and links
 // [ts-32768, ts+kMT); between tiles both slide down by kMT.  Every position's
@@ -233,7 +299,7 @@ __device__ __attribute__((always_inline)) inline void match_tile_load(uint32_t *
     // kMT/4 uint4 chunks == kMatchThreads, so thread t only ever touches
     // chunks = t (mod kMatchThreads): moving them in increasing order needs no
     // barrier and no staging.
-    static_assert(kMT / 4 == kMatchThreads, "slide assumes kMT/4 == threads");
+    static_assert(kMT / 4 == kMatchThreads, "slide (and k_match's key sort) assume kMT/4 == threads");
     constexpr int kChunks = (kME - kMT) / 4;
     uint4 *dE = reinterpret_cast<uint4 *>(E);
     for (int c = tid; c < kChunks; c += kMatchThreads) dE[c] = dE[c + kMT / 4];
@@ -249,195 +315,21 @@ __device__ __attribute__((always_inline)) inline void match_tile_load(uint32_t *
 }
 
 // One position's longest_match walk (deflate.c:1356-1497) over the packed
-// window, split into init / candidate-load / candidate-step so that several
-// walks per lane can have their LDS reads in flight together.
-struct MWalk {
-    int64_t p;
-    int s, m, best, bpos, bestq, bposq, limit, nice, maxcmp;
-    uint32_t count, scan01, scan_end, S0, S1, S2, S3;
-    bool snapped;
-};
-
-// false: no valid hash head (results already stored)
-__device__ __attribute__((always_inline)) inline bool mwalk_init(MWalk &w, const uint32_t *E, int64_t p,
-                                                                 int64_t B, int64_t n, const LevelCfg &cfg,
-                                                                 uint32_t *rf, uint32_t *rq, int want_q) {
-    w.p = p;
-    w.s = (int)(p - B);
-    const uint32_t e0 = E[w.s];
-    const uint32_t d0 = e0 & 0xffffu;
-    if (d0 == 0 || d0 > (uint32_t)kMaxDist) {
-        rf[p] = 0;
-        if (want_q) rq[p] = 0;
-        return false;
-    }
-    const int64_t labs = p > kMaxDist ? p - kMaxDist : 0;
-    w.limit = (int)(labs - B);
-    const int64_t rem = n - p;
-    w.nice = rem < cfg.nice ? (int)rem : cfg.nice;
-    w.maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
-    w.S0 = get4(E, w.s); w.S1 = get4(E, w.s + 4); w.S2 = get4(E, w.s + 8); w.S3 = get4(E, w.s + 12);
-    w.scan01 = e0 >> 16;
-    w.best = kMinMatch - 1; w.bpos = 0; w.bestq = 0; w.bposq = 0; w.snapped = false;
-    w.scan_end = (w.S0 >> 8) & 0xffffu;
-    w.m = w.s - (int)d0;
-    w.count = 0;
-    return true;
-}
-
-// consume one candidate whose two words were loaded; true when the walk ends
-__device__ __attribute__((always_inline)) inline bool mwalk_step(MWalk &w, const uint32_t *E, uint32_t em,
-                                                                 uint32_t eb, const LevelCfg &cfg,
-                                                                 uint32_t *rf, uint32_t *rq, int want_q) {
-    w.count++;
-    bool stop = false;
-    if ((em >> 16) == w.scan01 && eb == w.scan_end) {
-        const int m = w.m, s = w.s;
-        int k;
-        uint32_t x = get4(E, m) ^ w.S0;
-        if (x) k = __builtin_ctz(x) >> 3;
-        else if ((x = get4(E, m + 4) ^ w.S1)) k = 4 + (__builtin_ctz(x) >> 3);
-        else if ((x = get4(E, m + 8) ^ w.S2)) k = 8 + (__builtin_ctz(x) >> 3);
-        else if ((x = get4(E, m + 12) ^ w.S3)) k = 12 + (__builtin_ctz(x) >> 3);
-        else {
-            k = 16;
-            while (k < w.maxcmp) {
-                x = get4(E, s + k) ^ get4(E, m + k);
-                if (x) { k += __builtin_ctz(x) >> 3; break; }
-                k += 4;
-            }
-        }
-        const int len = k < w.maxcmp ? k : w.maxcmp;
-        if (len > w.best) {
-            w.best = len;
-            w.bpos = m;
-            if (len >= w.nice) stop = true;
-            else w.scan_end = E[s + w.best - 1] >> 16;
-        }
-    }
-    if (w.count == (uint32_t)(cfg.chain >> 2)) { w.bestq = w.best; w.bposq = w.bpos; w.snapped = true; }
-    const uint32_t d = em & 0xffffu;
-    const int nm = w.m - (int)d;
-    if (stop || w.count >= cfg.chain || d == 0 || nm <= w.limit) {
-        if (!w.snapped) { w.bestq = w.best; w.bposq = w.bpos; }
-        rf[w.p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)(w.s - w.bpos)) : 0u;
-        if (want_q) rq[w.p] = w.bestq >= kMinMatch ? (((uint32_t)w.bestq << 16) | (uint32_t)(w.s - w.bposq)) : 0u;
-        return true;
-    }
-    w.m = nm;
-    return false;
-}
-
-// Variant 3 walk: the candidate loop of longest_match with byte addresses, no
-// chain-end test (nil_link) and the chain/4 snapshot between two loops, so a
-// step is 2 LDS reads, the quick reject, and the link/limit/budget tests.
+// window: byte addresses (4 x window index), no chain-end test (nil_link), the
+// chain/4 snapshot between two loops (no per-step snapshot test), the next
+// candidate's two words loaded before the current one is tested, and both
+// quick-reject pairs tested as one predicate so both loads precede the single
+// branch.  A nice-length stop is folded into the limit test (limit4 = INT_MAX).
 struct MW3 {
     int s4, m4, be4, best, bpos4, limit4, nice, maxcmp;
     uint32_t count, scan01, scanE;
+    uint32_t ncmp;            // compares (statistics build only)
 };
 
-// The walk used by default (variants 6/7): byte addresses into the packed
-// window, no chain-end test (nil_link), the chain/4 snapshot between two loops
-// (no per-step snapshot test), the next candidate's word loaded before the
-// current one is tested, and both quick-reject pairs tested as one predicate so
-// both loads precede the single branch.  A nice-length stop is folded into the
-// limit test (limit4 = INT_MAX).  Variant 7 unrolls the step loop twice.
-template <int kUnroll>
-__device__ __attribute__((always_inline)) inline bool mw6_loop(MW3 &w, uint32_t &em, const uint32_t *E,
-                                                               uint32_t end) {
-    const char *Eb = reinterpret_cast<const char *>(E);
-#pragma unroll kUnroll
-    for (;;) {
-        const int m4n = w.m4 - (int)((em & 0xffffu) << 2);
-        const uint32_t eb = *reinterpret_cast<const uint32_t *>(Eb + w.m4 + w.be4);
-        const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + (m4n > 0 ? m4n : 0));
-        // one predicate for both quick-reject pairs: both loads precede the branch
-        const uint32_t miss = ((em >> 16) ^ w.scan01) | ((eb >> 16) ^ w.scanE);
-        if (__builtin_expect(miss == 0, 0)) {
-            const int m = w.m4 >> 2, s = w.s4 >> 2;
-            int k;
-            uint32_t x = get4(E, m) ^ get4(E, s);
-            if (x) k = __builtin_ctz(x) >> 3;
-            else {
-                k = 4;
-                for (;;) {
-                    if (k >= w.maxcmp) break;
-                    x = get4(E, s + k) ^ get4(E, m + k);
-                    if (x) { k += __builtin_ctz(x) >> 3; break; }
-                    k += 4;
-                }
-            }
-            const int len = k < w.maxcmp ? k : w.maxcmp;
-            if (len > w.best) {
-                w.best = len;
-                w.bpos4 = w.m4;
-                if (len >= w.nice) w.limit4 = 0x7fffffff;
-                w.be4 = (len - 1) * 4;
-                w.scanE = E[s + len - 1] >> 16;
-            }
-        }
-        w.count++;
-        w.m4 = m4n;
-        em = emn;
-        if (m4n <= w.limit4) return true;
-        if (w.count >= end) return false;
-    }
-}
-
-// Variant 8: both words of candidate k+1 (link word and end-bytes word at the
-// current best) are loaded while candidate k is tested; a best-length change
-// (rare) reloads the end-bytes word.
-template <int kUnroll, bool kNoCmp = false>
-__device__ __attribute__((always_inline)) inline bool mw8_loop(MW3 &w, uint32_t &em, uint32_t &eb,
-                                                               const uint32_t *E, uint32_t end) {
-    const char *Eb = reinterpret_cast<const char *>(E);
-#pragma unroll kUnroll
-    for (;;) {
-        const int m4n = w.m4 - (int)((em & 0xffffu) << 2);
-        const int a = m4n > 0 ? m4n : 0;
-        const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + a);
-        uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
-        const uint32_t miss = ((em >> 16) ^ w.scan01) | ((eb >> 16) ^ w.scanE);
-        if (kNoCmp && miss == 0) {           // timing stub: valid but fake lengths
-            if (w.best < 8 && w.best < w.maxcmp) { w.best++; w.bpos4 = w.m4; }
-        }
-        else if (__builtin_expect(miss == 0, 0)) {
-            const int m = w.m4 >> 2, s = w.s4 >> 2;
-            int k;
-            uint32_t x = get4(E, m) ^ get4(E, s);
-            if (x) k = __builtin_ctz(x) >> 3;
-            else {
-                k = 4;
-                for (;;) {
-                    if (k >= w.maxcmp) break;
-                    x = get4(E, s + k) ^ get4(E, m + k);
-                    if (x) { k += __builtin_ctz(x) >> 3; break; }
-                    k += 4;
-                }
-            }
-            const int len = k < w.maxcmp ? k : w.maxcmp;
-            if (len > w.best) {
-                w.best = len;
-                w.bpos4 = w.m4;
-                if (len >= w.nice) w.limit4 = 0x7fffffff;
-                w.be4 = (len - 1) * 4;
-                w.scanE = E[s + len - 1] >> 16;
-                ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
-            }
-        }
-        w.count++;
-        w.m4 = m4n;
-        em = emn;
-        eb = ebn;
-        if (m4n <= w.limit4) return true;
-        if (w.count >= end) return false;
-    }
-}
-
-// Variant 14: mw8's walk with a 16-byte-per-round-trip compare.  The first 16
-// scan bytes are held in registers (loaded once per walk); a hit reads the
-// candidate's first 16 bytes with 4 independent ds_read2 (one LDS round trip)
-// and longer matches continue 16 bytes (both sides) per round trip.
+// The compare: the first 16 scan bytes are held in registers (loaded once per
+// walk); a hit reads the candidate word by word (most compares end in the
+// first 4-8 bytes) and longer matches continue 16 bytes (both sides) per LDS
+// round trip.
 struct Scan16 { uint32_t s0, s1, s2, s3; };
 
 // first mismatching byte of a 4-byte xor word at byte offset `at`, or 99 if none
@@ -487,6 +379,7 @@ __device__ __attribute__((always_inline)) inline bool mw14_loop(MW3 &w, uint32_t
         uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
         const uint32_t miss = ((em >> 16) ^ w.scan01) | ((eb >> 16) ^ w.scanE);
         if (__builtin_expect(miss == 0, 0)) {
+            w.ncmp++;
             const int m = w.m4 >> 2, s = w.s4 >> 2;
             const int k = cmp16<kBatch>(E, m, s, S, w.maxcmp);
             const int len = k < w.maxcmp ? k : w.maxcmp;
@@ -511,7 +404,8 @@ __device__ __attribute__((always_inline)) inline bool mw14_loop(MW3 &w, uint32_t
 template <int kUnroll, bool kBatch>
 __device__ __attribute__((always_inline)) inline void mw14_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
                                                                 const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
-                                                                int want_q) {
+                                                                int want_q, uint32_t *st_steps = nullptr,
+                                                                uint32_t *st_cmp = nullptr) {
     const int s = (int)(p - B);
     const uint32_t e0 = E[s];
     const uint32_t d0 = e0 & 0xffffu;
@@ -534,6 +428,7 @@ __device__ __attribute__((always_inline)) inline void mw14_walk(const uint32_t *
     w.scan01 = e0 >> 16;
     w.scanE = E[s + 1] >> 16;
     w.count = 0;
+    w.ncmp = 0;
     Scan16 S{get4(E, s), get4(E, s + 4), get4(E, s + 8), get4(E, s + 12)};
     uint32_t em = E[s - (int)d0];
     uint32_t eb = E[s - (int)d0 + 1];
@@ -544,315 +439,29 @@ __device__ __attribute__((always_inline)) inline void mw14_walk(const uint32_t *
         if (!done) mw14_loop<kUnroll, kBatch>(w, em, eb, S, E, (uint32_t)cfg.chain);
     }
     rf[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
+    if (st_steps) { *st_steps = w.count; *st_cmp = w.ncmp; }
 }
 
-template <int kUnroll, bool kNoCmp = false>
-__device__ __attribute__((always_inline)) inline void mw8_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
-                                                               const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
-                                                               int want_q) {
-    const int s = (int)(p - B);
-    const uint32_t e0 = E[s];
-    const uint32_t d0 = e0 & 0xffffu;
-    if (d0 > (uint32_t)kMaxDist) {
-        rf[p] = 0;
-        if (want_q) rq[p] = 0;
-        return;
-    }
-    MW3 w;
-    const int64_t labs = p > kMaxDist ? p - kMaxDist : 0;
-    w.limit4 = (int)(labs - B) * 4;
-    const int64_t rem = n - p;
-    w.nice = rem < cfg.nice ? (int)rem : cfg.nice;
-    w.maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
-    w.s4 = s * 4;
-    w.m4 = (s - (int)d0) * 4;
-    w.best = kMinMatch - 1;
-    w.bpos4 = 0;
-    w.be4 = (kMinMatch - 2) * 4;
-    w.scan01 = e0 >> 16;
-    w.scanE = E[s + 1] >> 16;
-    w.count = 0;
-    uint32_t em = E[s - (int)d0];
-    uint32_t eb = E[s - (int)d0 + 1];
-    const uint32_t qc = want_q ? (uint32_t)(cfg.chain >> 2) : (uint32_t)cfg.chain;
-    const bool done = mw8_loop<kUnroll, kNoCmp>(w, em, eb, E, qc);
-    if (want_q) {
-        rq[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
-        if (!done) mw8_loop<kUnroll, kNoCmp>(w, em, eb, E, (uint32_t)cfg.chain);
-    }
-    rf[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
-}
+__device__ unsigned long long g_mstat[4];   // kMatchStats statistics
 
-// Variant 10: mw8's step without per-lane loop exits.  All lanes of the wave
-// start their walks together, so the candidate count is wave-uniform; a lane
-// whose walk has ended keeps a `done` flag and stops committing state, and the
-// wave leaves the loop when all lanes are done (tested every kU steps) or the
-// count reaches `end`.  The only divergent branch left is the full compare.
-template <int kU>
-__device__ __attribute__((always_inline)) inline void mw10_loop(MW3 &w, uint32_t &em, uint32_t &eb, bool &done,
-                                                                const uint32_t *E, uint32_t &count, uint32_t end) {
-    const char *Eb = reinterpret_cast<const char *>(E);
-    for (;;) {
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const int m4n = w.m4 - (int)((em & 0xffffu) << 2);
-            const int a = m4n > 0 ? m4n : 0;
-            const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + a);
-            uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
-            const uint32_t miss = ((em >> 16) ^ w.scan01) | ((eb >> 16) ^ w.scanE) | (uint32_t)done;
-            if (__builtin_expect(miss == 0, 0)) {
-                const int m = w.m4 >> 2, s = w.s4 >> 2;
-                int k;
-                uint32_t x = get4(E, m) ^ get4(E, s);
-                if (x) k = __builtin_ctz(x) >> 3;
-                else {
-                    k = 4;
-                    for (;;) {
-                        if (k >= w.maxcmp) break;
-                        x = get4(E, s + k) ^ get4(E, m + k);
-                        if (x) { k += __builtin_ctz(x) >> 3; break; }
-                        k += 4;
-                    }
-                }
-                const int len = k < w.maxcmp ? k : w.maxcmp;
-                if (len > w.best) {
-                    w.best = len;
-                    w.bpos4 = w.m4;
-                    if (len >= w.nice) w.limit4 = 0x7fffffff;
-                    w.be4 = (len - 1) * 4;
-                    w.scanE = E[s + len - 1] >> 16;
-                    ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
-                }
-            }
-            // a finished lane keeps walking garbage (addresses stay clamped into
-            // the window) but never compares again, so no state is frozen and
-            // the next words are not waited for here
-            count++;
-            done = done || m4n <= w.limit4;
-            w.m4 = m4n;
-            em = emn;
-            eb = ebn;
-            if (count >= end) return;
-        }
-        if (__all(done)) return;
-    }
-}
+// k_match variants (ZGPU_MATCH_VARIANT, for A/B runs):
+//   19 (default)  positions of a tile walked in k_count's key order, longest
+//                 walks first: the 64 walks a wave runs side by side have
+//                 similar lengths (SIMT utilisation 63 % -> 90 % at L6,
+//                 20 % -> 93 % at L9, measured with kMatchStats)
+//   14            positions in index order (no keys)
+//   21            19 plus statistics (lane steps, compares, walks, wave
+//                 iterations) printed after each launch
+constexpr int kMatchDefault = 19, kMatchStats = 21;
 
-template <int kU>
-__device__ __attribute__((always_inline)) inline void mw10_walk(const uint32_t *E, int64_t p, bool have,
-                                                                int64_t B, int64_t n, const LevelCfg &cfg,
-                                                                uint32_t *rf, uint32_t *rq, int want_q) {
-    const int s = have ? (int)(p - B) : 0;
-    const uint32_t e0 = E[s];
-    const uint32_t d0 = e0 & 0xffffu;
-    bool done = !have || d0 > (uint32_t)kMaxDist;
-    if (have && done) {
-        rf[p] = 0;
-        if (want_q) rq[p] = 0;
-    }
-    MW3 w;
-    const int64_t labs = p > kMaxDist ? p - kMaxDist : 0;
-    w.limit4 = (int)(labs - B) * 4;
-    const int64_t rem = n - p;
-    w.nice = rem < cfg.nice ? (int)rem : cfg.nice;
-    w.maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
-    w.s4 = s * 4;
-    const int m0 = done ? s : s - (int)d0;
-    w.m4 = m0 * 4;
-    w.best = kMinMatch - 1;
-    w.bpos4 = 0;
-    w.be4 = (kMinMatch - 2) * 4;
-    w.scan01 = e0 >> 16;
-    w.scanE = E[s + 1] >> 16;
-    uint32_t em = E[m0];
-    uint32_t eb = E[m0 + 1];
-    const bool skip = done;
-    if (__all(done)) return;
-    uint32_t count = 0;
-    const uint32_t qc = want_q ? (uint32_t)(cfg.chain >> 2) : (uint32_t)cfg.chain;
-    mw10_loop<kU>(w, em, eb, done, E, count, qc);
-    if (want_q) {
-        if (!skip)
-            rq[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
-        if (!__all(done)) mw10_loop<kU>(w, em, eb, done, E, count, (uint32_t)cfg.chain);
-    }
-    if (!skip) rf[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
-}
-
-// Variant 11: kW independent walks per lane in lockstep (mw10's step), so a
-// lane keeps kW LDS pointer chases in flight.
-struct MW11 {
-    MW3 w;
-    uint32_t em, eb;
-    bool done, skip;
-    int64_t p;
-};
-
-__device__ __attribute__((always_inline)) inline void mw11_step(MW11 &x, const uint32_t *E) {
-    const char *Eb = reinterpret_cast<const char *>(E);
-    MW3 &w = x.w;
-    const int m4n = w.m4 - (int)((x.em & 0xffffu) << 2);
-    const int a = m4n > 0 ? m4n : 0;
-    const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + a);
-    uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
-    const uint32_t miss = ((x.em >> 16) ^ w.scan01) | ((x.eb >> 16) ^ w.scanE) | (uint32_t)x.done;
-    if (__builtin_expect(miss == 0, 0)) {
-        const int m = w.m4 >> 2, s = w.s4 >> 2;
-        int k;
-        uint32_t xx = get4(E, m) ^ get4(E, s);
-        if (xx) k = __builtin_ctz(xx) >> 3;
-        else {
-            k = 4;
-            for (;;) {
-                if (k >= w.maxcmp) break;
-                xx = get4(E, s + k) ^ get4(E, m + k);
-                if (xx) { k += __builtin_ctz(xx) >> 3; break; }
-                k += 4;
-            }
-        }
-        const int len = k < w.maxcmp ? k : w.maxcmp;
-        if (len > w.best) {
-            w.best = len;
-            w.bpos4 = w.m4;
-            if (len >= w.nice) w.limit4 = 0x7fffffff;
-            w.be4 = (len - 1) * 4;
-            w.scanE = E[s + len - 1] >> 16;
-            ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
-        }
-    }
-    x.done = x.done || m4n <= w.limit4;
-    w.m4 = m4n;
-    x.em = emn;
-    x.eb = ebn;
-}
-
-__device__ __attribute__((always_inline)) inline void mw11_init(MW11 &x, const uint32_t *E, int64_t p, bool have,
-                                                                int64_t B, int64_t n, const LevelCfg &cfg,
-                                                                uint32_t *rf, uint32_t *rq, int want_q) {
-    const int s = have ? (int)(p - B) : 0;
-    const uint32_t e0 = E[s];
-    const uint32_t d0 = e0 & 0xffffu;
-    x.p = p;
-    x.done = !have || d0 > (uint32_t)kMaxDist;
-    x.skip = x.done;
-    if (have && x.done) {
-        rf[p] = 0;
-        if (want_q) rq[p] = 0;
-    }
-    MW3 &w = x.w;
-    const int64_t labs = p > kMaxDist ? p - kMaxDist : 0;
-    w.limit4 = (int)(labs - B) * 4;
-    const int64_t rem = n - p;
-    w.nice = rem < cfg.nice ? (int)rem : cfg.nice;
-    w.maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
-    w.s4 = s * 4;
-    const int m0 = x.done ? s : s - (int)d0;
-    w.m4 = m0 * 4;
-    w.best = kMinMatch - 1;
-    w.bpos4 = 0;
-    w.be4 = (kMinMatch - 2) * 4;
-    w.scan01 = e0 >> 16;
-    w.scanE = E[s + 1] >> 16;
-    x.em = E[m0];
-    x.eb = E[m0 + 1];
-}
-
-__device__ __attribute__((always_inline)) inline uint32_t mw11_result(const MW11 &x) {
-    return x.w.best >= kMinMatch ? (((uint32_t)x.w.best << 16) | (uint32_t)((x.w.s4 - x.w.bpos4) >> 2)) : 0u;
-}
-
-template <int kW, int kU>
-__device__ __attribute__((always_inline)) inline void mw11_loop(MW11 (&x)[kW], const uint32_t *E, uint32_t &count,
-                                                                uint32_t end) {
-    for (;;) {
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-#pragma unroll
-            for (int k = 0; k < kW; k++) mw11_step(x[k], E);
-            count++;
-            if (count >= end) return;
-        }
-        bool all = true;
-#pragma unroll
-        for (int k = 0; k < kW; k++) all = all && x[k].done;
-        if (__all(all)) return;
-    }
-}
-
-template <int kW, int kU>
-__device__ __attribute__((always_inline)) inline void mw11_walks(const uint32_t *E, int64_t p0, int64_t lim,
-                                                                 int64_t B, int64_t n, const LevelCfg &cfg,
-                                                                 uint32_t *rf, uint32_t *rq, int want_q) {
-    MW11 x[kW];
-    bool all = true;
-#pragma unroll
-    for (int k = 0; k < kW; k++) {
-        const int64_t p = p0 + 64 * k;
-        mw11_init(x[k], E, p, p < lim, B, n, cfg, rf, rq, want_q);
-        all = all && x[k].done;
-    }
-    if (__all(all)) return;
-    uint32_t count = 0;
-    const uint32_t qc = want_q ? (uint32_t)(cfg.chain >> 2) : (uint32_t)cfg.chain;
-    mw11_loop<kW, kU>(x, E, count, qc);
-    if (want_q) {
-        all = true;
-#pragma unroll
-        for (int k = 0; k < kW; k++) {
-            if (!x[k].skip) rq[x[k].p] = mw11_result(x[k]);
-            all = all && x[k].done;
-        }
-        if (!__all(all)) mw11_loop<kW, kU>(x, E, count, (uint32_t)cfg.chain);
-    }
-#pragma unroll
-    for (int k = 0; k < kW; k++)
-        if (!x[k].skip) rf[x[k].p] = mw11_result(x[k]);
-}
-
-template <int kUnroll>
-__device__ __attribute__((always_inline)) inline void mw6_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
-                                                               const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
-                                                               int want_q) {
-    const int s = (int)(p - B);
-    const uint32_t e0 = E[s];
-    const uint32_t d0 = e0 & 0xffffu;
-    if (d0 > (uint32_t)kMaxDist) {
-        rf[p] = 0;
-        if (want_q) rq[p] = 0;
-        return;
-    }
-    MW3 w;
-    const int64_t labs = p > kMaxDist ? p - kMaxDist : 0;
-    w.limit4 = (int)(labs - B) * 4;
-    const int64_t rem = n - p;
-    w.nice = rem < cfg.nice ? (int)rem : cfg.nice;
-    w.maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
-    w.s4 = s * 4;
-    w.m4 = (s - (int)d0) * 4;
-    w.best = kMinMatch - 1;
-    w.bpos4 = 0;
-    w.be4 = (kMinMatch - 2) * 4;
-    w.scan01 = e0 >> 16;
-    w.scanE = E[s + 1] >> 16;
-    w.count = 0;
-    uint32_t em = E[s - (int)d0];
-    const uint32_t qc = want_q ? (uint32_t)(cfg.chain >> 2) : (uint32_t)cfg.chain;
-    const bool done = mw6_loop<kUnroll>(w, em, E, qc);
-    if (want_q) {
-        rq[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
-        if (!done) mw6_loop<kUnroll>(w, em, E, (uint32_t)cfg.chain);
-    }
-    rf[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
-}
-
-// Lanes take positions from an LDS ticket; each walks one position at a time.
-// kVariant 0: the plain walk (MWalk), kept as the readable reference form;
-// 6 / 7: mw6_walk; 8 / 9: mw8_walk (default 9; 7 and 9 unroll the step loop
-// twice).  ZGPU_MATCH_VARIANT selects one for A/B runs.
 template <int kVariant>
 __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int want_q) {
+    constexpr bool kSorted = kVariant != 14;
+    constexpr int kSortBuckets = 64;
     __shared__ __attribute__((aligned(16))) uint32_t E[kME];
     __shared__ int next_i;
+    __shared__ uint16_t s_perm[kSorted ? kMT : 1];
+    __shared__ int s_hist[kSortBuckets], s_base[kSortBuckets];
     const int tid = threadIdx.x;
     const uint32_t bi = blockIdx.x;
     const uint32_t g = job.first + bi;
@@ -861,79 +470,74 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
     const uint16_t *L = job.link + job.ws_off[bi];
     uint32_t *rf = job.rfull + job.ws_off[bi];
     uint32_t *rq = job.rquart + job.ws_off[bi];
+    const uint8_t *K = kSorted ? job.key + job.ws_off[bi] : nullptr;
     const LevelCfg cfg = c_ct.cfg[job.level];
+    uint64_t st_lane_steps = 0, st_cmps = 0, st_walks = 0, st_wave_iters = 0;
 
     for (int64_t ts = 0; ts < n; ts += kMT) {
         const int64_t B = ts - kMW;
+        const int tile_n = (int)((n - ts) < kMT ? (n - ts) : kMT);
         match_tile_load(E, ts, n, in, L, tid);
         if (tid == 0) next_i = 0;
+        if (kSorted && tid < kSortBuckets) s_hist[tid] = 0;
         __syncthreads();
-        if (kVariant == 14 || kVariant == 15) {
-            for (;;) {
-                const int i = atomicAdd(&next_i, 1);
-                const int64_t p = ts + i;
-                if (i >= kMT || p >= n) break;
-                mw14_walk<2, kVariant == 15>(E, p, B, n, cfg, rf, rq, want_q);
+        if (kSorted) {
+            // counting sort of the tile's positions by key (64 buckets), longest
+            // first.  Thread t takes positions t + 1024u, so within a bucket the
+            // ranks come out nearly in position order and a wave's lanes get
+            // nearby positions (nearby candidates, fewer LDS bank conflicts).
+            int bk[4], rk[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = tid + u * kMatchThreads;
+                bk[u] = kSortBuckets - 1 - (i < tile_n ? (int)(K[ts + i] >> 2) : 0);
             }
-        } else if (kVariant == 13) {
-            for (;;) {
-                const int i = atomicAdd(&next_i, 1);
-                const int64_t p = ts + i;
-                if (i >= kMT || p >= n) break;
-                mw8_walk<2, true>(E, p, B, n, cfg, rf, rq, want_q);
-            }
-        } else if (kVariant == 11 || kVariant == 12) {
-            constexpr int kW = kVariant == 11 ? 2 : 3;
-            const int lane = tid & 63;
-            const int64_t lim = (ts + kMT < n) ? ts + kMT : n;
-            for (;;) {
-                int i0 = 0;
-                if (lane == 0) i0 = atomicAdd(&next_i, 64 * kW);
-                i0 = __shfl(i0, 0, 64);
-                if (i0 >= kMT || ts + i0 >= n) break;
-                mw11_walks<kW, 2>(E, ts + i0 + lane, lim, B, n, cfg, rf, rq, want_q);
-            }
-        } else if (kVariant == 10) {
-            // wave-synchronous: a wave takes 64 consecutive positions at a time
-            const int lane = tid & 63;
-            for (;;) {
-                int i0 = 0;
-                if (lane == 0) i0 = atomicAdd(&next_i, 64);
-                i0 = __shfl(i0, 0, 64);
-                if (i0 >= kMT || ts + i0 >= n) break;
-                const int64_t p = ts + i0 + lane;
-                const bool have = i0 + lane < kMT && p < n;
-                mw10_walk<4>(E, p, have, B, n, cfg, rf, rq, want_q);
-            }
-        } else if (kVariant == 8 || kVariant == 9) {
-            for (;;) {
-                const int i = atomicAdd(&next_i, 1);
-                const int64_t p = ts + i;
-                if (i >= kMT || p >= n) break;
-                mw8_walk<kVariant == 9 ? 2 : 1>(E, p, B, n, cfg, rf, rq, want_q);
-            }
-        } else if (kVariant == 6 || kVariant == 7) {
-            for (;;) {
-                const int i = atomicAdd(&next_i, 1);
-                const int64_t p = ts + i;
-                if (i >= kMT || p >= n) break;
-                mw6_walk<kVariant == 7 ? 2 : 1>(E, p, B, n, cfg, rf, rq, want_q);
-            }
-        } else {
-            for (;;) {
-                const int i = atomicAdd(&next_i, 1);
-                const int64_t p = ts + i;
-                if (i >= kMT || p >= n) break;
-                MWalk w;
-                if (!mwalk_init(w, E, p, B, n, cfg, rf, rq, want_q)) continue;
-                for (;;) {
-                    const uint32_t em = E[w.m];
-                    const uint32_t eb = E[w.m + w.best - 1] >> 16;
-                    if (mwalk_step(w, E, em, eb, cfg, rf, rq, want_q)) break;
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                rk[u] = tid + u * kMatchThreads < tile_n ? atomicAdd(&s_hist[bk[u]], 1) : 0;
+            __syncthreads();
+            if (tid < 64) {                              // exclusive scan of the bucket sizes
+                const int v = s_hist[tid];
+                int incl = v;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int t = __shfl_up(incl, o, 64);
+                    if (tid >= o) incl += t;
                 }
+                s_base[tid] = incl - v;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (tid + u * kMatchThreads < tile_n)
+                    s_perm[s_base[bk[u]] + rk[u]] = (uint16_t)(tid + u * kMatchThreads);
+            __syncthreads();
+        }
+        for (;;) {
+            const int i = atomicAdd(&next_i, 1);
+            if (i >= tile_n) break;
+            const int64_t p = ts + (kSorted ? (int)s_perm[i] : i);
+            if (kVariant == kMatchStats) {
+                uint32_t steps = 0, cmps = 0;
+                mw14_walk<2, false>(E, p, B, n, cfg, rf, rq, want_q, &steps, &cmps);
+                uint32_t mx = steps;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+                st_lane_steps += steps;
+                st_cmps += cmps;
+                st_walks += steps ? 1u : 0u;
+                if ((tid & 63) == __builtin_ctzll(__ballot(1))) st_wave_iters += mx;
+            } else {
+                mw14_walk<2, false>(E, p, B, n, cfg, rf, rq, want_q);
             }
         }
         __syncthreads();
+    }
+    if (kVariant == kMatchStats) {
+        atomicAdd(&g_mstat[0], (unsigned long long)st_lane_steps);
+        atomicAdd(&g_mstat[1], (unsigned long long)st_cmps);
+        atomicAdd(&g_mstat[2], (unsigned long long)st_walks);
+        atomicAdd(&g_mstat[3], (unsigned long long)st_wave_iters);
     }
 }
 
@@ -2141,28 +1745,40 @@ int launch_tables_upload(const CodeTables *ct, const CrcTables *) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(c_ct), ct, sizeof(CodeTables));
 }
 
+static int match_variant() {
+    static const int v = [] {
+        const char *e = getenv("ZGPU_MATCH_VARIANT");
+        const int x = e ? atoi(e) : kMatchDefault;
+        return (x == 14 || x == kMatchStats) ? x : kMatchDefault;
+    }();
+    return v;
+}
+
 int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipStream_t st) {
     const dim3 grid(job.count);
     switch (stage) {
-    case 0: hipLaunchKernelGGL(k_links, grid, dim3(64), 0, st, job); break;
+    case 0:
+        hipLaunchKernelGGL(k_links, grid, dim3(64), 0, st, job);
+        if (match_variant() != 14) hipLaunchKernelGGL(k_count, grid, dim3(kCntThreads), 0, st, job);
+        break;
     case 1: {
-        static const int variant = [] {
-            const char *e = getenv("ZGPU_MATCH_VARIANT");
-            return e ? atoi(e) : 14;
-        }();
         const int wq = (int)(job.level >= 5);
-        if (variant == 0) hipLaunchKernelGGL(k_match<0>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        else if (variant == 6) hipLaunchKernelGGL(k_match<6>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        else if (variant == 8) hipLaunchKernelGGL(k_match<8>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        else if (variant == 9) hipLaunchKernelGGL(k_match<9>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        else if (variant == 10) hipLaunchKernelGGL(k_match<10>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        else if (variant == 11) hipLaunchKernelGGL(k_match<11>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        else if (variant == 13) hipLaunchKernelGGL(k_match<13>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        else if (variant == 14) hipLaunchKernelGGL(k_match<14>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        else if (variant == 15) hipLaunchKernelGGL(k_match<15>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        else if (variant == 12) hipLaunchKernelGGL(k_match<12>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        else if (variant == 7) hipLaunchKernelGGL(k_match<7>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        else hipLaunchKernelGGL(k_match<14>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        const int v = match_variant();
+        if (v == 14) {
+            hipLaunchKernelGGL(k_match<14>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchStats) {
+            unsigned long long z[4] = {0, 0, 0, 0}, r[4];
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_mstat), z, sizeof z);
+            hipLaunchKernelGGL(k_match<kMatchStats>, grid, dim3(kMatchThreads), 0, st, job, wq);
+            (void)hipStreamSynchronize(st);
+            (void)hipMemcpyFromSymbol(r, HIP_SYMBOL(g_mstat), sizeof r);
+            fprintf(stderr, "k_match stats: lane_steps %llu compares %llu walks %llu wave_iters %llu "
+                    "simt %.3f steps/walk %.2f cmp/step %.4f\n", r[0], r[1], r[2], r[3],
+                    r[3] ? (double)r[0] / (64.0 * r[3]) : 0.0, r[2] ? (double)r[0] / r[2] : 0.0,
+                    r[0] ? (double)r[1] / r[0] : 0.0);
+        } else {
+            hipLaunchKernelGGL(k_match<kMatchDefault>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        }
         break;
     }
     case 2: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 0); break;
@@ -2172,6 +1788,7 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     case 4: hipLaunchKernelGGL(k_encode, grid, dim3(kEncThreads), 0, st, job); break;
     case 7: hipLaunchKernelGGL(k_parse_huff, grid, dim3(kHuffThreads), 0, st, job); break;
     case 8: hipLaunchKernelGGL(k_parse_rle, grid, dim3(64), 0, st, job); break;
+    case 9: hipLaunchKernelGGL(k_count, grid, dim3(kCntThreads), 0, st, job); break;
     default: return -1;
     }
     return (int)hipGetLastError();

@@ -84,6 +84,7 @@ struct DeflateJob {
     const uint64_t *ws_off;  // per sub-batch buffer: start in the position-indexed arrays
     const uint64_t *blk_off; // per sub-batch buffer: start in the block array
     uint16_t *link;          // [Σn]
+    uint8_t *key;            // [Σn] k_count's walk-length keys (k_match's position order)
     uint32_t *rfull;         // [Σn]
     uint32_t *rquart;        // [Σn] (levels 5..9)
     uint32_t *pstate;        // [Σn/16] lazy-parse sync states, 2 bits per position
@@ -142,7 +143,8 @@ int launch_adler32(const uint8_t *src, const uint64_t *off, const uint64_t *len,
                    void *scratch, size_t scratch_bytes, hipStream_t st);
 size_t checksum_scratch_bytes(uint32_t count);
 // stage: 0 links, 1 match, 2 lazy parse (sequential), 3 greedy parse (heads: 128 KiB/buffer),
-//        4 encode, 5 lazy parse (segmented), 6 lazy parse fallback for buffers flagged by 5
+//        4 encode, 5 lazy parse (segmented), 6 lazy parse fallback for buffers flagged by 5,
+//        7 huffman-only parse, 8 rle parse, 9 walk-length keys (k_count)
 int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipStream_t st);
 int launch_generate(uint8_t *dst, uint64_t len, uint32_t count, int kind, uint64_t seed,
                     uint64_t first_index, hipStream_t st);
