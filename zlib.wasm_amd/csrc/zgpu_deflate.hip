@@ -2,9 +2,10 @@
 // reference deflate.c/trees.c (zlib 1.3.1.1-motley) at the same level.
 //
 // Pipeline per sub-batch of independent buffers:
-//   k_links      wave/buffer   hash-chain links: link[p] = distance to the most
+//   k_links      1024 thr/buf  hash-chain links: link[p] = distance to the most
 //                              recent earlier position with the same 3-byte
-//                              hash (UPDATE_HASH/INSERT_STRING, deflate.c:141,160)
+//                              hash (UPDATE_HASH/INSERT_STRING, deflate.c:141,160),
+//                              from 8 Ki-position chunks radix-sorted by hash in LDS
 //   k_count      256 thr/buf   levels 4..9: per position, the number of same-hash
 //                              candidates in its window (capped at the chain
 //                              budget): the order in which k_match walks a tile
@@ -118,78 +119,140 @@ __device__ inline void stage_words(uint32_t *dst, const uint32_t *src, int64_t s
 }
 
 // ------------------------------------------------------------------------
-// k_links — one wave per buffer.  head[] holds the low 16 bits of the most
-// recent position per hash; every 32 KiB it is swept like slide_hash
-// (deflate.c:187-209) so no live entry is ever 64 Ki positions old.
-// Within a 64-position chunk the nearest earlier lane with the same hash is
-// found with a shuffle scan; only the last lane of each hash updates head[].
+// k_links — link[p] = p - q for the most recent q < p (q != 0, q <= n-3) with
+// the same hash, 0 when there is none, the distance exceeds 32767 or p > n-3:
+// the chain prev[] would hold.  One 1024-thread workgroup per buffer.
+// Positions are taken kLC at a time.  Each chunk's keys (hash << 13 | index)
+// are radix-sorted in LDS (two stable 8-bit passes over the 15-bit hash; the
+// index in the low bits keeps equal hashes in position order), so the previous
+// position with p's hash is the previous key in sorted order, or, for the
+// first of its hash in the chunk, head[hash]: INSERT_STRING's head[]
+// (deflate.c:160-163) as it stands at the chunk boundary.  head[] holds the
+// low 16 bits of positions and is swept every 32 Ki positions like slide_hash
+// (deflate.c:187-209), so no live entry is ever 64 Ki positions old.
 // ------------------------------------------------------------------------
-constexpr int kLinkStage = 4096;
-constexpr int kLinkSlots = 256;
+constexpr int kLC = 8192;
+constexpr int kLThreads = 1024;
+constexpr int kLWaves = kLThreads / 64;
+constexpr int kLPer = kLC / kLThreads;
 
-__global__ __launch_bounds__(64) void k_links(DeflateJob job) {
+// One stable counting-sort pass of src[0..m) into dst by the 8-bit digit at
+// `shift`.  Wave w owns elements w*512 + j*64 + lane; equal digits within a
+// wave step are ranked with ballots, counts are scanned digit-major across
+// waves, so the scatter keeps element order within a digit.
+__device__ __attribute__((always_inline)) inline void links_radix_pass(const uint32_t *src, uint32_t *dst, int m,
+                                                                       int shift, uint16_t (*wcnt)[256],
+                                                                       int *wsum, int tid) {
+    const int lane = tid & 63, wave = tid >> 6;
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (int k = tid; k < kLWaves * 256; k += kLThreads) (&wcnt[0][0])[k] = 0;
+    __syncthreads();
+    uint32_t key[kLPer], rank[kLPer];
+    const uint64_t all = __ballot(1);
+    (void)all;
+#pragma unroll
+    for (int j = 0; j < kLPer; j++) {
+        const int e = wave * (64 * kLPer) + j * 64 + lane;
+        const bool valid = e < m;
+        key[j] = valid ? src[e] : 0u;
+        const uint32_t d = (key[j] >> shift) & 0xffu;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const uint64_t bb = __ballot((d >> b) & 1u);
+            peers &= ((d >> b) & 1u) ? bb : ~bb;
+        }
+        rank[j] = 0;
+        if (valid) {
+            const uint32_t base = wcnt[wave][d];
+            rank[j] = base + (uint32_t)__popcll(peers & below);
+            if ((peers & below) == 0) wcnt[wave][d] = (uint16_t)(base + __popcll(peers));
+        }
+    }
+    __syncthreads();
+    // exclusive scan over (digit, wave), digit-major: thread t owns 4 entries
+    int v[4], tot = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int idx = tid * 4 + k;
+        v[k] = wcnt[idx & (kLWaves - 1)][idx >> 4];
+        tot += v[k];
+    }
+    int incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int wbase = 0;
+    for (int w = 0; w < wave; w++) wbase += wsum[w];
+    int run = wbase + incl - tot;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int idx = tid * 4 + k;
+        wcnt[idx & (kLWaves - 1)][idx >> 4] = (uint16_t)run;
+        run += v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kLPer; j++) {
+        const int e = wave * (64 * kLPer) + j * 64 + lane;
+        if (e < m) dst[wcnt[wave][(key[j] >> shift) & 0xffu] + rank[j]] = key[j];
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kLThreads) void k_links(DeflateJob job) {
     __shared__ uint16_t head[32768];
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kLinkStage + 16];
-    __shared__ unsigned long long smask[kLinkSlots];
-    __shared__ uint32_t sh_h[64];
-    __shared__ uint8_t mark[64];
-    const int lane = threadIdx.x;
+    __shared__ uint32_t ka[kLC], kb[kLC];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kLC + 16];
+    __shared__ uint16_t wcnt[kLWaves][256];
+    __shared__ int wsum[kLWaves];
+    const int tid = threadIdx.x;
     const uint32_t bi = blockIdx.x;
     const uint32_t g = job.first + bi;
     const int64_t n = (int64_t)job.src_len[g];
     const uint8_t *in = job.src + job.src_off[g];
     uint16_t *out = job.link + job.ws_off[bi];
-    const unsigned long long below_mask = (1ull << lane) - 1ull;
 
-    for (int i = lane; i < 32768; i += 64) head[i] = 32768;   // "position -32768"
-    for (int64_t t0 = 0; t0 < n; t0 += kLinkStage) {
+    for (int i = tid; i < 32768; i += kLThreads) head[i] = 32768;   // "position -32768"
+    for (int64_t c0 = 0; c0 < n; c0 += kLC) {
         __syncthreads();
-        stage_bytes<64, (kLinkStage + 16) / 16 / 64 + 1>(stage, in, t0, kLinkStage + 16, n, lane);
-        __syncthreads();
-        const int64_t tend = (t0 + kLinkStage < n) ? t0 + kLinkStage : n;
-        for (int64_t c0 = t0; c0 < tend; c0 += 64) {
-            if ((c0 & 32767) == 0 && c0 > 0) {                // slide sweep (slide_hash analogue)
-                const uint32_t now = (uint32_t)c0;
-                for (int i = lane; i < 32768; i += 64) {
-                    uint32_t age = (now - head[i]) & 0xffffu;
-                    if (age == 0 || age >= 32768u) head[i] = (uint16_t)((now - 32768u) & 0xffffu);
-                }
-                __syncthreads();
+        if ((c0 & 32767) == 0 && c0 > 0) {                   // slide sweep (slide_hash analogue)
+            const uint32_t now = (uint32_t)c0;
+            for (int i = tid; i < 32768; i += kLThreads) {
+                const uint32_t age = (now - head[i]) & 0xffffu;
+                if (age == 0 || age >= 32768u) head[i] = (uint16_t)((now - 32768u) & 0xffffu);
             }
-            const int64_t p = c0 + lane;
-            const bool valid = p + 3 <= n;
-            const int j = (int)(p - t0);
-            const uint32_t h = valid ? hash3(stage[j], stage[j + 1], stage[j + 2]) : (0x10000u + lane);
-            // nearest earlier lane with the same hash: lanes OR their bit into a
-            // slot keyed by the low hash bits (order independent), then the
-            // candidates below are verified against the true hash
-            const int slot = (int)(h & (kLinkSlots - 1));
-            smask[slot] = 0ull;
-            sh_h[lane] = h;
-            mark[lane] = 0;
-            __syncthreads();
-            atomicOr(&smask[slot], 1ull << lane);
-            __syncthreads();
-            unsigned long long cand = smask[slot] & below_mask;
-            int pred = -1;
-            while (cand) {
-                const int jl = 63 - __builtin_clzll(cand);
-                if (sh_h[jl] == h) { pred = jl; break; }
-                cand &= ~(1ull << jl);
-            }
-            if (pred >= 0) mark[pred] = 1;
-            uint32_t link = 0;
-            if (valid) {
-                uint32_t d;
-                if (pred >= 0) d = (uint32_t)(lane - pred);
-                else d = ((uint32_t)p - head[h]) & 0xffffu;
-                if (d != 0 && d <= 32767u && (int64_t)d != p) link = d;   // position 0 is NIL
-            }
-            __syncthreads();
-            if (valid && mark[lane] == 0) head[h] = (uint16_t)(p & 0xffff);
-            if (p < n) out[p] = (uint16_t)link;
-            __syncthreads();
         }
+        stage_bytes<kLThreads, (kLC + 16) / 16 / kLThreads + 1>(stage, in, c0, kLC + 16, n, tid);
+        __syncthreads();
+        const int cnt = (int)((n - c0) < kLC ? (n - c0) : kLC);          // positions in the chunk
+        const int m = (int)((n - 2 - c0) < kLC ? ((n - 2 - c0) > 0 ? n - 2 - c0 : 0) : kLC);   // p <= n-3
+        for (int e = tid; e < m; e += kLThreads)
+            ka[e] = hash3(stage[e], stage[e + 1], stage[e + 2]) << 13 | (uint32_t)e;
+        links_radix_pass(ka, kb, m, 13, wcnt, wsum, tid);
+        links_radix_pass(kb, ka, m, 21, wcnt, wsum, tid);
+        // sorted: ka[i] = hash << 13 | e, hashes ascending, e ascending within a hash
+        for (int i = tid; i < m; i += kLThreads) {
+            const uint32_t key = ka[i];
+            const uint32_t h = key >> 13, e = key & (kLC - 1);
+            const uint32_t p = (uint32_t)c0 + e;
+            uint32_t d;
+            if (i > 0 && (ka[i - 1] >> 13) == h) d = e - (ka[i - 1] & (kLC - 1));
+            else d = (p - head[h]) & 0xffffu;
+            kb[e] = (d != 0 && d <= 32767u && d != p) ? d : 0u;               // position 0 is NIL
+        }
+        __syncthreads();
+        for (int i = tid; i < m; i += kLThreads) {
+            const uint32_t key = ka[i];
+            if (i == m - 1 || (ka[i + 1] >> 13) != (key >> 13))
+                head[key >> 13] = (uint16_t)(((uint32_t)c0 + (key & (kLC - 1))) & 0xffffu);
+        }
+        for (int e = tid; e < cnt; e += kLThreads) out[c0 + e] = e < m ? (uint16_t)kb[e] : (uint16_t)0;
     }
 }
 
@@ -1758,7 +1821,7 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     const dim3 grid(job.count);
     switch (stage) {
     case 0:
-        hipLaunchKernelGGL(k_links, grid, dim3(64), 0, st, job);
+        hipLaunchKernelGGL(k_links, grid, dim3(kLThreads), 0, st, job);
         if (match_variant() != 14) hipLaunchKernelGGL(k_count, grid, dim3(kCntThreads), 0, st, job);
         break;
     case 1: {
