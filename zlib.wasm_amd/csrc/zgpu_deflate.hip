@@ -340,41 +340,79 @@ __device__ inline uint32_t get4(const uint32_t *E, int i) {      // bytes i..i+3
 // <= the walk's limit, so the chain-end test folds into the limit test.
 __device__ inline uint32_t nil_link(uint32_t l) { return l ? l : 0xffffu; }
 
-// Tile load: E[i] for window positions [ts-kMW, ts+kMT+kMPad); the first
-// tile loads everything, later tiles slide the window down by kMT words.
-__device__ __attribute__((always_inline)) inline void match_tile_load(uint32_t *E, int64_t ts, int64_t n,
-                                                                      const uint8_t *in, const uint16_t *L,
-                                                                      int tid) {
-    const int64_t B = ts - kMW;
-    auto word = [&](int64_t q, bool with_link) -> uint32_t {
-        uint32_t w = 0;
-        if (q >= 0 && q < n) {
-            w = (uint32_t)in[q] << 16;
-            if (q + 1 < n) w |= (uint32_t)in[q + 1] << 24;
-            if (with_link) w |= nil_link(L[q]);
+// Tile prefetch: what thread t writes into the LDS window for a tile, loaded
+// from HBM into registers one tile ahead (while the previous tile's walks
+// run): bytes ts+4t .. ts+4t+4 (words 4t..4t+3), for t < kMPad/4 the pad
+// words kMT+4t.., the links of positions ts+4t.., and the walk keys of
+// positions ts+t+1024u (u = 0..3).
+static_assert(kMT / 4 == kMatchThreads && kMPad % 4 == 0 && kMPad / 4 <= kMatchThreads && kMW % 4 == 0,
+              "tile prefetch: 4 words per thread");
+struct TilePre {
+    uint32_t b[4];        // packed word bytes (byte[q] | byte[q+1] << 8) for words 4t+u
+    uint32_t pb[4];       // same for pad words kMT + 4t + u (t < kMPad / 4)
+    uint32_t lk[4];       // links (raw, 0 = none)
+    uint32_t key[4];
+};
+
+__device__ __attribute__((always_inline)) inline uint32_t ldb(const uint8_t *in, int64_t q, int64_t n) {
+    return (q >= 0 && q < n) ? (uint32_t)in[q] : 0u;
+}
+
+__device__ __attribute__((always_inline)) inline void tile_prefetch(TilePre &P, int64_t ts, int64_t n,
+                                                                    const uint8_t *in, const uint16_t *L,
+                                                                    const uint8_t *K, int tid) {
+    const int64_t q0 = ts + 4 * tid;
+    uint32_t x[5];
+#pragma unroll
+    for (int u = 0; u < 5; u++) x[u] = ldb(in, q0 + u, n);
+#pragma unroll
+    for (int u = 0; u < 4; u++) P.b[u] = x[u] | x[u + 1] << 8;
+    if (tid < kMPad / 4) {
+        const int64_t q1 = ts + kMT + 4 * tid;
+#pragma unroll
+        for (int u = 0; u < 5; u++) x[u] = ldb(in, q1 + u, n);
+#pragma unroll
+        for (int u = 0; u < 4; u++) P.pb[u] = x[u] | x[u + 1] << 8;
+    }
+    if (q0 + 4 <= n) {
+        const uint2 v = *reinterpret_cast<const uint2 *>(L + q0);   // 8-B aligned: ws_off % 64 == 0
+        P.lk[0] = v.x & 0xffffu; P.lk[1] = v.x >> 16; P.lk[2] = v.y & 0xffffu; P.lk[3] = v.y >> 16;
+    } else {
+#pragma unroll
+        for (int u = 0; u < 4; u++) P.lk[u] = q0 + u < n ? (uint32_t)L[q0 + u] : 0u;
+    }
+    if (K) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int64_t q = ts + tid + u * kMatchThreads;
+            P.key[u] = q < n ? (uint32_t)K[q] : 0u;
         }
-        return w;
-    };
+    }
+}
+
+// Tile load from the prefetched registers: slide the window down by kMT words
+// (later tiles), then write words kMW.. of the new tile and its pad.
+__device__ __attribute__((always_inline)) inline void tile_store(uint32_t *E, const TilePre &P, int64_t ts,
+                                                                 int tid) {
     if (ts == 0) {
-        for (int i = tid; i < kME; i += kMatchThreads) E[i] = word(B + i, i < kMW + kMT);
-        return;
+        for (int i = tid; i < kMW; i += kMatchThreads) E[i] = 0;
+    } else {
+        // kMW/4 uint4 chunks, thread t moves chunks t (mod kMatchThreads) in
+        // increasing order: no chunk is overwritten before it is read
+        uint4 *dE = reinterpret_cast<uint4 *>(E);
+        for (int c = tid; c < kMW / 4; c += kMatchThreads) dE[c] = dE[c + kMT / 4];
+        __syncthreads();
     }
-    // kMT/4 uint4 chunks == kMatchThreads, so thread t only ever touches
-    // chunks = t (mod kMatchThreads): moving them in increasing order needs no
-    // barrier and no staging.
-    static_assert(kMT / 4 == kMatchThreads, "slide (and k_match's key sort) assume kMT/4 == threads");
-    constexpr int kChunks = (kME - kMT) / 4;
-    uint4 *dE = reinterpret_cast<uint4 *>(E);
-    for (int c = tid; c < kChunks; c += kMatchThreads) dE[c] = dE[c + kMT / 4];
-    __syncthreads();
-    // words [kMW, kME): the slid part (pad of the last tile) still needs its
-    // links, [kME-kMT, kME) are new; one pass, no overlap race
-    for (int i = tid; i < kME - kMW; i += kMatchThreads) {
-        const int idx = kMW + i;
-        const int64_t q = ts + i;
-        if (idx >= kME - kMT) E[idx] = word(q, i < kMT);
-        else if (i < kMT && q < n) E[idx] |= nil_link(L[q]);
-    }
+    const int w0 = kMW + 4 * tid;
+    uint4 v;
+    v.x = P.b[0] << 16 | nil_link(P.lk[0]);
+    v.y = P.b[1] << 16 | nil_link(P.lk[1]);
+    v.z = P.b[2] << 16 | nil_link(P.lk[2]);
+    v.w = P.b[3] << 16 | nil_link(P.lk[3]);
+    *reinterpret_cast<uint4 *>(E + w0) = v;
+    if (tid < kMPad / 4)
+        *reinterpret_cast<uint4 *>(E + kMW + kMT + 4 * tid) =
+            make_uint4(P.pb[0] << 16, P.pb[1] << 16, P.pb[2] << 16, P.pb[3] << 16);
 }
 
 // One position's longest_match walk (deflate.c:1356-1497) over the packed
@@ -537,10 +575,12 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
     const LevelCfg cfg = c_ct.cfg[job.level];
     uint64_t st_lane_steps = 0, st_cmps = 0, st_walks = 0, st_wave_iters = 0;
 
+    TilePre P;
+    tile_prefetch(P, 0, n, in, L, K, tid);
     for (int64_t ts = 0; ts < n; ts += kMT) {
         const int64_t B = ts - kMW;
         const int tile_n = (int)((n - ts) < kMT ? (n - ts) : kMT);
-        match_tile_load(E, ts, n, in, L, tid);
+        tile_store(E, P, ts, tid);
         if (tid == 0) next_i = 0;
         if (kSorted && tid < kSortBuckets) s_hist[tid] = 0;
         __syncthreads();
@@ -553,7 +593,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const int i = tid + u * kMatchThreads;
-                bk[u] = kSortBuckets - 1 - (i < tile_n ? (int)(K[ts + i] >> 2) : 0);
+                bk[u] = kSortBuckets - 1 - (i < tile_n ? (int)(P.key[u] >> 2) : 0);
             }
 #pragma unroll
             for (int u = 0; u < 4; u++)
@@ -576,6 +616,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
                     s_perm[s_base[bk[u]] + rk[u]] = (uint16_t)(tid + u * kMatchThreads);
             __syncthreads();
         }
+        if (ts + kMT < n) tile_prefetch(P, ts + kMT, n, in, L, K, tid);   // lands during the walks
         for (;;) {
             const int i = atomicAdd(&next_i, 1);
             if (i >= tile_n) break;
@@ -590,6 +631,15 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
                 st_cmps += cmps;
                 st_walks += steps ? 1u : 0u;
                 if ((tid & 63) == __builtin_ctzll(__ballot(1))) st_wave_iters += mx;
+            } else if (kVariant == 33) {
+                rf[p] = 0;                                  // timing probe: no walks
+                if (want_q) rq[p] = 0;
+            } else if (kVariant == 30) {
+                mw14_walk<1, false>(E, p, B, n, cfg, rf, rq, want_q);
+            } else if (kVariant == 31) {
+                mw14_walk<4, false>(E, p, B, n, cfg, rf, rq, want_q);
+            } else if (kVariant == 32) {
+                mw14_walk<2, true>(E, p, B, n, cfg, rf, rq, want_q);
             } else {
                 mw14_walk<2, false>(E, p, B, n, cfg, rf, rq, want_q);
             }
@@ -1812,7 +1862,7 @@ static int match_variant() {
     static const int v = [] {
         const char *e = getenv("ZGPU_MATCH_VARIANT");
         const int x = e ? atoi(e) : kMatchDefault;
-        return (x == 14 || x == kMatchStats) ? x : kMatchDefault;
+        return (x == 14 || x == kMatchStats || (x >= 30 && x <= 33)) ? x : kMatchDefault;
     }();
     return v;
 }
@@ -1829,6 +1879,14 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         const int v = match_variant();
         if (v == 14) {
             hipLaunchKernelGGL(k_match<14>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == 33) {
+            hipLaunchKernelGGL(k_match<33>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == 30) {
+            hipLaunchKernelGGL(k_match<30>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == 31) {
+            hipLaunchKernelGGL(k_match<31>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == 32) {
+            hipLaunchKernelGGL(k_match<32>, grid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchStats) {
             unsigned long long z[4] = {0, 0, 0, 0}, r[4];
             (void)hipMemcpyToSymbol(HIP_SYMBOL(g_mstat), z, sizeof z);
