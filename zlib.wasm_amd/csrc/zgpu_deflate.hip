@@ -553,7 +553,11 @@ __device__ unsigned long long g_mstat[4];   // kMatchStats statistics
 //   14            positions in index order (no keys)
 //   21            19 plus statistics (lane steps, compares, walks, wave
 //                 iterations) printed after each launch
-constexpr int kMatchDefault = 19, kMatchStats = 21;
+//   33, 35        timing probes (wrong results): 33 no walks (tile staging,
+//                 sort and stores: 33 ms of 351 per 4 GiB at L6); 35 half the
+//                 waves walk (1.6x slower at L6, 1.8x at L9: the walks are
+//                 latency-bound at the 16 waves the LDS window allows)
+constexpr int kMatchDefault = 19, kMatchStats = 21, kMatchProbeNoWalk = 33, kMatchProbeHalf = 35;
 
 template <int kVariant>
 __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int want_q) {
@@ -618,6 +622,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
         }
         if (ts + kMT < n) tile_prefetch(P, ts + kMT, n, in, L, K, tid);   // lands during the walks
         for (;;) {
+            if (kVariant == kMatchProbeHalf && tid >= kMatchThreads / 2) break;   // probe: half the waves walk
             const int i = atomicAdd(&next_i, 1);
             if (i >= tile_n) break;
             const int64_t p = ts + (kSorted ? (int)s_perm[i] : i);
@@ -631,15 +636,9 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
                 st_cmps += cmps;
                 st_walks += steps ? 1u : 0u;
                 if ((tid & 63) == __builtin_ctzll(__ballot(1))) st_wave_iters += mx;
-            } else if (kVariant == 33) {
-                rf[p] = 0;                                  // timing probe: no walks
+            } else if (kVariant == kMatchProbeNoWalk) {
+                rf[p] = 0;                                  // probe: staging, sort and stores only
                 if (want_q) rq[p] = 0;
-            } else if (kVariant == 30) {
-                mw14_walk<1, false>(E, p, B, n, cfg, rf, rq, want_q);
-            } else if (kVariant == 31) {
-                mw14_walk<4, false>(E, p, B, n, cfg, rf, rq, want_q);
-            } else if (kVariant == 32) {
-                mw14_walk<2, true>(E, p, B, n, cfg, rf, rq, want_q);
             } else {
                 mw14_walk<2, false>(E, p, B, n, cfg, rf, rq, want_q);
             }
@@ -1862,7 +1861,7 @@ static int match_variant() {
     static const int v = [] {
         const char *e = getenv("ZGPU_MATCH_VARIANT");
         const int x = e ? atoi(e) : kMatchDefault;
-        return (x == 14 || x == kMatchStats || (x >= 30 && x <= 33)) ? x : kMatchDefault;
+        return (x == 14 || x == kMatchStats || x == kMatchProbeNoWalk || x == kMatchProbeHalf) ? x : kMatchDefault;
     }();
     return v;
 }
@@ -1879,14 +1878,10 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         const int v = match_variant();
         if (v == 14) {
             hipLaunchKernelGGL(k_match<14>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == 33) {
-            hipLaunchKernelGGL(k_match<33>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == 30) {
-            hipLaunchKernelGGL(k_match<30>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == 31) {
-            hipLaunchKernelGGL(k_match<31>, grid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == 32) {
-            hipLaunchKernelGGL(k_match<32>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchProbeNoWalk) {
+            hipLaunchKernelGGL(k_match<kMatchProbeNoWalk>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchProbeHalf) {
+            hipLaunchKernelGGL(k_match<kMatchProbeHalf>, grid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchStats) {
             unsigned long long z[4] = {0, 0, 0, 0}, r[4];
             (void)hipMemcpyToSymbol(HIP_SYMBOL(g_mstat), z, sizeof z);
