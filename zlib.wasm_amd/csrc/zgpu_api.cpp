@@ -207,6 +207,7 @@ struct Ctx {
     // stream)
     DevBuf ws_link2, ws_rf2, ws_rq2, ws_state2;
     DevBuf ws_key, ws_key2;   // k_count's walk-length keys (one byte per position)
+    DevBuf ws_stg;            // k_parse_seg's symbol staging (caller's stream only)
     // inflate: match records, per-stream results, checks, offsets, stop codes
     DevBuf ws_mrec, ws_irec, ws_ick, ws_imeta, ws_istop;
     hipStream_t aux = nullptr;
@@ -325,6 +326,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     if (slow && !c.ws_rq.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
     if (slow && !c.ws_state.ensure(max_pos / 4 + 64)) return ZGPU_MEM_ERROR;
     if (slow && !c.ws_key.ensure(max_pos + 64)) return ZGPU_MEM_ERROR;
+    if (slow && !c.ws_stg.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
     if (piped) {
         if (!c.ws_key2.ensure(max_pos + 64)) return ZGPU_MEM_ERROR;
         if (!c.ws_link2.ensure(2 * max_pos + 64) || !c.ws_rf2.ensure(4 * max_pos + 64) ||
@@ -354,7 +356,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     if (poison) {
         static int round = 0;
         const int v = 0x5a ^ (round++ * 0x3b);
-        for (DevBuf *b : {&c.ws_link, &c.ws_sym, &c.ws_blk, &c.ws_rf, &c.ws_rq, &c.ws_state, &c.ws_heads,
+        for (DevBuf *b : {&c.ws_link, &c.ws_sym, &c.ws_stg, &c.ws_blk, &c.ws_rf, &c.ws_rq, &c.ws_state, &c.ws_heads,
                           &c.ws_link2, &c.ws_rf2, &c.ws_rq2, &c.ws_state2})
             if (b->p && hipMemsetAsync(b->p, v & 0xff, b->cap, st) != hipSuccess) return ZGPU_MEM_ERROR;
         if (hipMemsetAsync(d_nblk, v & 0xff, 8ull * max_cnt, st) != hipSuccess) return ZGPU_MEM_ERROR;
@@ -376,6 +378,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         job.rfull = (slow || huff || rle) ? (slot ? c.ws_rf2 : c.ws_rf).as<uint32_t>() : nullptr;
         job.rquart = slow ? (slot ? c.ws_rq2 : c.ws_rq).as<uint32_t>() : nullptr;
         job.sym = c.ws_sym.as<uint32_t>();
+        job.stage = slow ? c.ws_stg.as<uint32_t>() : nullptr;
         job.pstate = slow ? (slot ? c.ws_state2 : c.ws_state).as<uint32_t>() : nullptr;
         job.blocks = c.ws_blk.as<BlockRec>();
         job.nblocks = d_nblk;

@@ -834,7 +834,7 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
 }
 
 // ------------------------------------------------------------------------
-// k_parse_seg — deflate_slow parsed by 64 lanes at once (levels 4..9).
+// k_parse_seg — deflate_slow parsed by 256 lanes per buffer (levels 4..9).
 //
 // The lazy parse is a deterministic state machine over decision points whose
 // state is (match_length, match_start, match_available).  Whenever
@@ -849,18 +849,21 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
 //          parses coincide, so the true parse is lane 0 on [0,y0), lane 1 on
 //          [y0,y1), ...  (measured: they meet within ~20 positions on average,
 //          ~500 at most on byte runs);
-//  pass 3  lane i parses [y(i-1), y(i)) and stages its k-th symbol at
-//          rquart[y(i-1) + k] and the symbol's start at rfull[y(i-1) + k] (both
-//          dead behind the parse: a lane's k-th symbol starts at or after
-//          y(i-1) + k - 1, and a lane reads nothing before its position);
+//          Pass 1 also stages its symbols at stage[x0 + k] (16-byte stores);
+//  replay  lane i counts the pass-1 symbols of steps before y(i-1) (replaying
+//          its first ~20 positions) and replays its run-on [pass-1 end, y(i)),
+//          staging those symbols in its own (now dead) state words, so every
+//          position is parsed about once;
 //  compact a block prefix sum of the counts gives each lane its first symbol
-//          index; the symbols are copied into sym[] and every 16383rd symbol
+//          index; the symbols are copied into sym[], a wave scan of their
+//          lengths gives their start positions, and every 16383rd symbol
 //          records its end (the block cut of _tr_tally, deflate.h:371);
 //  blocks  block records from the cuts; the fill_window slides before a flush
 //          at decision point d are #{k : T_k <= d} (the k-th slide happens at
 //          the first decision point >= T_k), which is the block_start >= 0 test
 //          of the stored-block choice (deflate.c:1597-1600).
-// A buffer whose lanes fail to meet within the next segment is flagged
+// A buffer whose lanes fail to meet within the next segment, or whose run-on
+// has more symbols than the lane has state words, is flagged
 // (nblocks = ~0) for k_parse_slow.
 // ------------------------------------------------------------------------
 constexpr int kSegMin = 4096;
@@ -967,6 +970,25 @@ __device__ __attribute__((always_inline)) inline void lane_init(SlowLane &L, uin
     L.cb.base = ~(uintptr_t)0;
 }
 
+// Four symbols buffered in registers and stored as one 16-byte word: a lane's
+// staging writes are sequential, so whole 16 B go to memory at a time.
+struct SymBuf {
+    uint32_t v0, v1, v2, v3;
+    uint32_t k;                 // symbols pushed
+    __device__ __attribute__((always_inline)) inline void push(uint32_t *dst, uint32_t v) {
+        const uint32_t j = k & 3u;
+        if (j == 0) v0 = v; else if (j == 1) v1 = v; else if (j == 2) v2 = v; else v3 = v;
+        k++;
+        if ((k & 3u) == 0) *reinterpret_cast<uint4 *>(dst + k - 4) = make_uint4(v0, v1, v2, v3);
+    }
+    __device__ __attribute__((always_inline)) inline void flush(uint32_t *dst) {
+        const uint32_t j = k & 3u, b = k & ~3u;
+        if (j > 0) dst[b] = v0;
+        if (j > 1) dst[b + 1] = v1;
+        if (j > 2) dst[b + 2] = v2;
+    }
+};
+
 __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
     __shared__ uint32_t s_y[kParseLanes], s_sig[kParseLanes];
     __shared__ uint32_t s_wsum[kParseLanes / 64];
@@ -978,9 +1000,10 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
     const uint32_t g = job.first + bi;
     const uint32_t n = (uint32_t)job.src_len[g];
     const uint8_t *in = job.src + job.src_off[g];
-    uint32_t *rf = job.rfull + job.ws_off[bi];
-    uint32_t *rq = job.rquart + job.ws_off[bi];
+    const uint32_t *rf = job.rfull + job.ws_off[bi];
+    const uint32_t *rq = job.rquart + job.ws_off[bi];
     uint32_t *sym = job.sym + job.ws_off[bi];
+    uint32_t *stg = job.stage + job.ws_off[bi];
     uint32_t *sst = job.pstate + (job.ws_off[bi] >> 4);      // 2 bits per position
     BlockRec *blk = job.blocks + job.blk_off[bi];
     const LevelCfg cfg = c_ct.cfg[job.level];
@@ -994,14 +1017,16 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
     const bool active = (uint32_t)lane < nseg;
     if (lane == 0) { s_fail = 0; s_first_end = kParseLanes; s_final = 0; }
 
-    // ---- pass 1: speculative parse of the own segment; the simple states it
-    // stands in go to sst[] one 16-position word at a time (words it jumps
-    // over are zeroed), lane-private, no atomics
+    // ---- pass 1: speculative parse of the own segment [x0, seg_end) from the
+    // simple state.  Its symbols are staged at stg[x0 + k] (a symbol starts
+    // inside the segment, so k < seg); the simple states it stands in go to
+    // sst[] one 16-position word at a time (words it jumps over are zeroed).
     SlowLane L;
     uint32_t sym_v, spos, slen;
     const uint32_t x0 = xb(lane);
     lane_init(L, x0, 0);
     const uint32_t seg_end = (uint32_t)lane + 1 >= nseg ? n : xb(lane + 1);
+    SymBuf sb{0, 0, 0, 0, 0};
     if (active && x0 < seg_end) {
         uint32_t widx = x0 >> 4, wcur = 0;
         while (L.p < seg_end) {
@@ -1013,11 +1038,14 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
                 wcur = 0;
             }
             if (L.ml < (uint32_t)kMinMatch) wcur |= 1u << (2 * (L.p & 15u) + L.avail);
-            slow_step(L, n, rf, rq, in, cfg, use_q, filtered, sym_v, spos, slen);
+            if (slow_step(L, n, rf, rq, in, cfg, use_q, filtered, sym_v, spos, slen)) sb.push(stg + x0, sym_v);
         }
         sst[widx] = wcur;
         for (uint32_t z = widx + 1; z <= (seg_end - 1) >> 4; z++) sst[z] = 0;
+        sb.flush(stg + x0);
     }
+    const uint32_t k1 = sb.k;
+    const uint32_t e_p = L.p, e_ml = L.ml, e_ms = L.ms, e_av = L.avail;   // where pass 1 stopped
     __threadfence_block();
     __syncthreads();
 
@@ -1040,42 +1068,53 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
     if (active && y == kEnd) atomicMin(&s_first_end, (uint32_t)lane);
     s_y[lane] = y;
     s_sig[lane] = sig;
+    __threadfence_block();
     __syncthreads();
     if (s_fail) {
         if (lane == 0) job.nblocks[bi] = kParseFallback;
         return;
     }
-    // lane i parses [start, end): start = y[i-1] (lane 0: 0), end = y[i] (kEnd: to n);
-    // lanes after the first one that reached n have nothing to do
+    // the true parse is lane i's on [y(i-1), y(i)) (lane 0 from 0; y = kEnd: to
+    // n); lanes after the first one that reached n have nothing to do
     const bool mine = active && (uint32_t)lane <= s_first_end;
     const uint32_t start = lane > 0 ? s_y[lane - 1] : 0u;
     const uint32_t start_av = lane > 0 ? s_sig[lane - 1] : 0u;
     const uint32_t yend = s_y[lane];
     const uint32_t end = yend == kEnd ? n : yend;
-    __syncthreads();
 
-    // ---- pass 3: the true parse of [start, end); the k-th symbol is staged at
-    // rq[start + k] and its start position at rf[start + k] (both behind the
-    // lane: symbol k starts at or after start + k - 1, and a lane reads only
-    // at and ahead of its own position, inside its own range).  The last lane's
-    // final pending literal can take index n: buffer regions hold n + 1 words.
-    uint32_t cnt = 0;
+    // ---- prefix: pass 1's symbols from steps before y(i-1) are not lane i's
+    // (the parse meets the true one there); count them by replaying pass 1
+    uint32_t kstart = 0;
+    if (mine && lane > 0) {
+        lane_init(L, x0, 0);
+        while (L.p < start)
+            if (slow_step(L, n, rf, rq, in, cfg, use_q, filtered, sym_v, spos, slen)) kstart++;
+    }
+    // ---- run-on: replay pass 2 from where pass 1 stopped and stage its
+    // symbols in the lane's own (now dead) state words; the last lane's final
+    // pending literal goes there too (tallied without a flush test)
+    uint32_t rcnt = 0;
+    uint32_t *ron = sst + (x0 >> 4);
+    const uint32_t rcap = (seg_end - x0 + 15u) >> 4;
     if (mine) {
-        lane_init(L, start, start_av);
+        L.p = e_p; L.ml = e_ml; L.ms = e_ms; L.avail = e_av;
+        L.cf.base = L.cq.base = 0xffffffffu;
+        L.cb.base = ~(uintptr_t)0;
         while (L.p < end) {
             if (slow_step(L, n, rf, rq, in, cfg, use_q, filtered, sym_v, spos, slen)) {
-                rq[start + cnt] = sym_v;
-                rf[start + cnt] = spos;
-                cnt++;
+                if (rcnt < rcap) ron[rcnt] = sym_v;
+                rcnt++;
             }
         }
-        if (yend == kEnd && L.avail) {                 // final pending literal: no flush test
-            rq[start + cnt] = bget(in, n - 1, L.cb);
-            rf[start + cnt] = n - 1;
-            cnt++;
+        if (yend == kEnd && L.avail) {
+            if (rcnt < rcap) ron[rcnt] = bget(in, n - 1, L.cb);
+            rcnt++;
             s_final = 1;
         }
+        if (rcnt > rcap) atomicOr(&s_fail, 1);
     }
+    const uint32_t c1 = mine ? k1 - kstart : 0u;        // staged pass-1 symbols that are lane i's
+    const uint32_t cnt = c1 + rcnt;
     // exclusive block prefix sum of cnt
     uint32_t incl = cnt;
 #pragma unroll
@@ -1086,6 +1125,10 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
     if (wl == 63) s_wsum[wv] = incl;
     __threadfence_block();
     __syncthreads();
+    if (s_fail) {
+        if (lane == 0) job.nblocks[bi] = kParseFallback;
+        return;
+    }
     uint32_t woff = 0, total = 0;
     for (int k = 0; k < kParseLanes / 64; k++) {
         const uint32_t t = s_wsum[k];
@@ -1094,33 +1137,39 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
     }
     const uint32_t base = woff + incl - cnt;
     const uint32_t ncut = total / kSymLimit - ((s_final && total % kSymLimit == 0) ? 1u : 0u);
+    // the symbols of lane i tile the input from y(i-1) - sig(i-1) (its first
+    // symbol may be the literal pending at y(i-1))
+    const uint32_t pos0 = start - start_av;
 
-    // ---- compaction: every wave copies its own lanes' symbols (stage and
-    // destination are different arrays); 16383rd symbols record their block
-    // cut in blk[b].in_end / .pad
+    // ---- compaction: every wave copies its own lanes' symbols, 64 at a time,
+    // into sym[]; a wave scan of the symbol lengths gives each symbol's start,
+    // and every 16383rd symbol records its block cut in blk[b].in_end / .pad
     for (int j = 0; j < 64; j++) {
-        const uint32_t jc = __shfl(cnt, j, 64), jb = __shfl(base, j, 64), js = __shfl(start, j, 64);
+        const uint32_t jc = __shfl(cnt, j, 64), jb = __shfl(base, j, 64);
         if (jc == 0) continue;
-        for (uint32_t c = 0; c < jc; c += 64 * 8) {
-            uint32_t v[8];
+        const uint32_t jc1 = __shfl(c1, j, 64), jx = __shfl(x0, j, 64), jk = __shfl(kstart, j, 64);
+        uint32_t run = __shfl(pos0, j, 64);
+        const uint32_t *s1 = stg + jx + jk, *s2 = sst + (jx >> 4);
+        for (uint32_t c = 0; c < jc; c += 64) {
+            const uint32_t idx = c + (uint32_t)wl;
+            const bool have = idx < jc;
+            const uint32_t v = have ? (idx < jc1 ? s1[idx] : s2[idx - jc1]) : 0u;
+            const uint32_t len = have ? (v < 256u ? 1u : (v & 0xffu) + (uint32_t)kMinMatch) : 0u;
+            uint32_t li = len;
 #pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const uint32_t idx = c + 64u * u + (uint32_t)wl;
-                v[u] = idx < jc ? rq[js + idx] : 0u;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(li, o, 64);
+                if (wl >= o) li += t;
             }
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const uint32_t idx = c + 64u * u + (uint32_t)wl;
-                if (idx < jc) {
-                    const uint32_t gi = jb + idx;
-                    sym[gi] = v[u];
-                    if ((gi + 1) % (uint32_t)kSymLimit == 0 && (gi + 1) / (uint32_t)kSymLimit <= ncut) {
-                        const uint32_t b = (gi + 1) / (uint32_t)kSymLimit - 1;
-                        const uint32_t sp = rf[js + idx];
-                        const uint32_t sl = v[u] < 256u ? 1u : (v[u] & 0xffu) + (uint32_t)kMinMatch;
-                        blk[b].in_end = (uint64_t)(sp + sl);
-                        blk[b].pad = sp + 1;                        // decision point of the flush
-                    }
+            const uint32_t sp = run + li - len;
+            run += __shfl(li, 63, 64);
+            if (have) {
+                const uint32_t gi = jb + idx;
+                sym[gi] = v;
+                if ((gi + 1) % (uint32_t)kSymLimit == 0 && (gi + 1) / (uint32_t)kSymLimit <= ncut) {
+                    const uint32_t b = (gi + 1) / (uint32_t)kSymLimit - 1;
+                    blk[b].in_end = (uint64_t)(sp + len);
+                    blk[b].pad = sp + 1;                        // decision point of the flush
                 }
             }
         }

@@ -89,6 +89,7 @@ struct DeflateJob {
     uint32_t *rquart;        // [Σn] (levels 5..9)
     uint32_t *pstate;        // [Σn/16] lazy-parse sync states, 2 bits per position
     uint32_t *sym;           // [Σn]
+    uint32_t *stage;         // [Σn] k_parse_seg's pass-1 symbol staging (levels 4..9)
     BlockRec *blocks;        // [Σ(n/16383 + 2)]
     uint32_t *nblocks;       // [count]
     uint32_t *check;         // [count] adler32 / crc32 of the input (trailer)
