@@ -661,9 +661,11 @@ struct ParseOut {
     BlockRec *blk;
     uint32_t nsym, blk_nsym, blk_sym_start, nblk;
     int64_t block_start, S, E;
+    bool lead;               // the lane that stores (the state itself is wave-uniform)
 
     __device__ inline bool tally(uint32_t v) {          // _tr_tally_*: returns bflush
-        sym[nsym++] = v;
+        if (lead) sym[nsym] = v;
+        nsym++;
         return ++blk_nsym == (uint32_t)kSymLimit;
     }
     __device__ inline void flush(int64_t strstart, bool last) {   // FLUSH_BLOCK_ONLY
@@ -674,7 +676,8 @@ struct ParseOut {
         r.in_end = (uint64_t)strstart;
         r.flags = (last ? 1u : 0u) | (block_start >= S ? 2u : 0u);
         r.pad = 0;
-        blk[nblk++] = r;
+        if (lead) blk[nblk] = r;
+        nblk++;
         block_start = strstart;
         blk_sym_start = nsym;
         blk_nsym = 0;
@@ -1321,11 +1324,15 @@ __global__ __launch_bounds__(64) void k_parse_rle(DeflateJob job) {
 // k_parse_fast — levels 1..3 (deflate_fast).  Insertion inside a match depends
 // on its length (deflate.c:1873-1897), so hash chains are maintained exactly
 // as zlib does it, sequentially: head[] (absolute positions, per buffer, in
-// global memory) and prev[] as 16-bit distances.  Lane 0 of one wave per
-// buffer; the chain walk is longest_match with prev_length == MIN_MATCH-1.
+// global memory) and prev[] as 16-bit distances.  One wave per buffer runs the
+// parse wave-uniformly (every lane holds the same state; lane 0 stores), so the
+// chain walk (longest_match with prev_length == MIN_MATCH-1) compares a
+// candidate 64 bytes per memory round trip, one byte per lane, with the next
+// link loaded in the same round trip.
 // ------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *heads) {
     const int lane = threadIdx.x;
+    const bool lead = lane == 0;
     const uint32_t bi = blockIdx.x;
     const uint32_t g = job.first + bi;
     const int64_t n = (int64_t)job.src_len[g];
@@ -1334,22 +1341,62 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     uint32_t *head = heads + (size_t)bi * 32768;
     const LevelCfg cfg = c_ct.cfg[job.level];
     for (int i = lane; i < 32768; i += 64) head[i] = 0;
+    __threadfence_block();
     __syncthreads();
-    if (lane != 0) return;
 
     ParseOut po;
     po.sym = job.sym + job.ws_off[bi];
     po.blk = job.blocks + job.blk_off[bi];
     po.nsym = po.blk_nsym = po.blk_sym_start = po.nblk = 0;
     po.block_start = 0; po.S = 0; po.E = 0;
+    po.lead = lead;
 
+    // input window in registers: lane j holds in[wb + j] (w0) and in[wb + 64 + j]
+    // (w1); it is moved forward 64 bytes at a time, so hashing and the scan side
+    // of a compare need no memory round trip
+    int64_t wb = -128;
+    uint32_t w0 = 0, w1 = 0;
+    auto ld = [&](int64_t x) -> uint32_t { return x < n ? (uint32_t)in[x] : 0u; };
+    auto wsee = [&](int64_t x) {                        // make [x, x + 66) resident
+        if (x >= wb && x + 66 <= wb + 128) return;
+        const int64_t nb = x & ~(int64_t)63;
+        if (nb == wb + 64) { w0 = w1; w1 = ld(nb + 64 + lane); }
+        else { w0 = ld(nb + lane); w1 = ld(nb + 64 + lane); }
+        wb = nb;
+    };
+    auto wbyte = [&](int64_t x) -> uint32_t {           // uniform x in the window
+        const int o = (int)(x - wb);
+        return (uint32_t)__builtin_amdgcn_readlane((int)(o < 64 ? w0 : w1), o & 63);
+    };
+    auto whash = [&](int64_t q) -> uint32_t { return hash3(wbyte(q), wbyte(q + 1), wbyte(q + 2)); };
     auto insert = [&](int64_t q) -> int64_t {           // INSERT_STRING
-        const uint32_t h = hash3(in[q], in[q + 1], in[q + 2]);
-        const int64_t hh = head[h];
+        const uint32_t h = whash(q);
+        const int64_t hh = ufl(head[h]);
         const int64_t d = q - hh;
-        prev[q] = (hh != 0 && d <= 32767) ? (uint16_t)d : 0;
-        head[h] = (uint32_t)q;
+        if (lead) {
+            prev[q] = (hh != 0 && d <= 32767) ? (uint16_t)d : 0;
+            head[h] = (uint32_t)q;
+        }
         return hh;
+    };
+    // common prefix of in[a..] and in[p..], capped at maxcmp (a < p); the scan
+    // side of the first 64 bytes comes from the register window
+    auto common = [&](int64_t a, int64_t pp, int maxcmp) -> int {
+        const int o = (int)(pp - wb) + lane;            // < 128 + 63
+        const uint32_t x0 = (uint32_t)__shfl((int)w0, o & 63, 64), x1 = (uint32_t)__shfl((int)w1, o & 63, 64);
+        const uint32_t sb = o < 64 ? x0 : x1;           // wsee(pp): pp - wb <= 62
+        {
+            const bool diff = lane < maxcmp && ld(a + lane) != sb;
+            const uint64_t m = __ballot(diff);
+            if (m) return __builtin_ctzll(m);
+        }
+        for (int k0 = 64; k0 < maxcmp; k0 += 64) {
+            const int k = k0 + lane;
+            const bool diff = k < maxcmp && ld(a + k) != ld(pp + k);
+            const uint64_t m = __ballot(diff);
+            if (m) return k0 + __builtin_ctzll(m);
+        }
+        return maxcmp;
     };
 
     int64_t p = 0, match_start = 0;
@@ -1359,31 +1406,28 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
             po.fill(p, n);
             if (po.E == p) break;
         }
+        wsee(p);
         int64_t lookahead = po.E - p;
         int64_t hh = 0;
         if (lookahead >= kMinMatch) hh = insert(p);
         if (hh > po.S && p - hh <= kMaxDist) {
-            // longest_match (deflate.c:1356-1497), prev_length == 2
+            // longest_match (deflate.c:1356-1497), prev_length == 2: the first
+            // candidate with the longest prefix wins, stop at nice, chain, limit
             uint32_t chain = cfg.chain;
-            int nice = lookahead < cfg.nice ? (int)lookahead : cfg.nice;
+            const int nice = lookahead < cfg.nice ? (int)lookahead : cfg.nice;
             const int64_t limit = (p - po.S) > kMaxDist ? p - kMaxDist : po.S;
             const int64_t rem = n - p;
             const int maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
             int best = kMinMatch - 1;
-            const uint8_t *scan = in + p;
             int64_t cur = hh;
             for (;;) {
-                const uint8_t *m = in + cur;
-                if (m[best] == scan[best] && m[best - 1] == scan[best - 1] && m[0] == scan[0] && m[1] == scan[1]) {
-                    int k = 2;
-                    while (k < maxcmp && m[k] == scan[k]) k++;
-                    if (k > best) {
-                        match_start = cur;
-                        best = k;
-                        if (k >= nice) break;
-                    }
+                const uint32_t d = ufl(prev[cur]);
+                const int k = common(cur, p, maxcmp);
+                if (k > best) {
+                    match_start = cur;
+                    best = k;
+                    if (k >= nice) break;
                 }
-                const uint32_t d = prev[cur];
                 if (d == 0) break;
                 cur -= d;
                 if (cur <= limit || --chain == 0) break;
@@ -1395,18 +1439,43 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
             bflush = po.tally(((uint32_t)(p - match_start) << 8) | (match_length - kMinMatch));
             lookahead -= match_length;
             if (match_length <= cfg.lazy && lookahead >= kMinMatch) {
-                for (uint32_t k = 1; k < match_length; k++) insert(p + k);
+                // positions p+1 .. p+len-1 (at most 5), one lane each: the head
+                // loads go out together; a position whose hash a lower lane
+                // also inserts takes that lane's position (zlib inserts in order)
+                const uint32_t cntk = match_length - 1;
+                const bool mine = (uint32_t)lane < cntk;
+                const int64_t q = p + 1 + lane;
+                uint32_t h = 0xffffffffu;
+                for (uint32_t k = 0; k < cntk; k++) {
+                    const uint32_t hk = whash(p + 1 + k);
+                    if ((uint32_t)lane == k) h = hk;
+                }
+                const int64_t hh0 = mine ? (int64_t)head[h] : 0;
+                int64_t hq = hh0;
+                bool last = mine;
+                for (uint32_t k = 0; k < cntk; k++) {
+                    const uint32_t hk = (uint32_t)__shfl((int)h, (int)k, 64);
+                    if (mine && hk == h) {
+                        if (k < (uint32_t)lane) hq = p + 1 + k;        // a lower lane's position
+                        if (k > (uint32_t)lane) last = false;          // a higher lane writes head
+                    }
+                }
+                if (mine) {
+                    const int64_t dd = q - hq;
+                    prev[q] = (hq != 0 && dd <= 32767) ? (uint16_t)dd : 0;
+                    if (last) head[h] = (uint32_t)q;
+                }
             }
             p += match_length;
             match_length = 0;
         } else {
-            bflush = po.tally(in[p]);
+            bflush = po.tally(wbyte(p));
             p++;
         }
         if (bflush) po.flush(p, false);
     }
     po.flush(p, true);
-    job.nblocks[bi] = po.nblk;
+    if (lead) job.nblocks[bi] = po.nblk;
 }
 
 // ------------------------------------------------------------------------
