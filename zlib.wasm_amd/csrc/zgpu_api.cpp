@@ -131,6 +131,18 @@ void build_crc_tables(CrcTables &t) {
         for (int j = 0; j < 8; j++)
             for (uint32_t v = 0; v < 16; v++) t.shift[k][j][v] = multmodp(op, v << (4 * j));
     }
+    for (uint32_t v = 0; v < 256; v++) t.s4[0][v] = t.byte[v];
+    for (int k = 1; k < 4; k++)
+        for (uint32_t v = 0; v < 256; v++) {
+            const uint32_t c = t.s4[k - 1][v];
+            t.s4[k][v] = (c >> 8) ^ t.byte[c & 0xffu];
+        }
+    const uint64_t a64[kCrcSh64Tabs] = {64, 128, 256, 512, 1024, 2048, 64 * 15, 64 * 63};
+    for (int k = 0; k < kCrcSh64Tabs; k++) {
+        const uint32_t op = x2nmodp((int64_t)a64[k], 3);
+        for (int j = 0; j < 8; j++)
+            for (uint32_t v = 0; v < 16; v++) t.sh64[k][j][v] = multmodp(op, v << (4 * j));
+    }
 }
 
 // ------------------------------------------------------------------------

@@ -49,10 +49,18 @@ struct CodeTables {
 //              k = 7 -> kCrcSegment bytes (segment Horner);
 //   byte[v]    the classic byte table (tiny-buffer path).
 constexpr int kCrcShiftTabs = 8;
+//   s4[k][v]   slice-by-4 tables: s4[0] = byte, s4[k][v] = s4[k-1][v] advanced
+//              by one zero byte;
+//   sh64[k][j][v] nibble operators advancing by {64,128,...,2048, 960, 4032}
+//              bytes (k_crc32s: the gaps between a lane's chunks and the
+//              lane-combine tree).
+constexpr int kCrcSh64Tabs = 8;
 struct CrcTables {
     uint32_t nib[32][16];
     uint32_t shift[kCrcShiftTabs][8][16];
     uint32_t byte[256];
+    uint32_t s4[4][256];
+    uint32_t sh64[kCrcSh64Tabs][8][16];
 };
 constexpr uint64_t kCrcSegment = 64 * 1024;   // bytes per checksum work item
 
