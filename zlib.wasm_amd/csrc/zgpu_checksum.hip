@@ -16,8 +16,8 @@
 // x^(8n) multipliers pre-tabulated.
 //
 // k_crc32s (the default; k_crc32 above is kept for A/B as ZGPU_CRC_NIBBLE=1)
-// replaces the nibble lookups by slice-by-4 byte tables, conflict-free per
-// lane: 1 LDS lookup per byte instead of 2.5 (4.0 -> 4.3 TB/s on C2, where a
+// replaces the nibble lookups by slice-by-4 byte tables, replicated per lane
+// group: 1 LDS lookup per byte instead of 2.5 (4.0 -> 4.35 TB/s on C2, where a
 // plain 16-byte streaming read of the same 4 GiB reaches 6.0 TB/s).
 //
 // Adler-32 (adler32.c:61-125): per chunk the byte sum and the position-weighted
@@ -160,14 +160,17 @@ __global__ __launch_bounds__(kCkBlock) void k_crc32(const uint8_t *__restrict__ 
 // and runs slice-by-4 through it, rows are joined by advancing the lane's CRC
 // over the (G-1)*64-byte gap, lanes by the shuffle tree (64 << l bytes).
 // Random byte indexes would hit the 32 LDS banks ~3.5-way; every table is
-// therefore stored 32 times, entry e of copy c at word e*32 + c, and lane l
-// reads copy l % 32, which is always bank l % 32: conflict-free, 128 KiB.
+// therefore stored 16 times, entry e of copy c at word e*16 + c, and lane l
+// reads copy l % 16: bank c or c + 16, so at most 2-way (lanes l and l + 16),
+// in 64 KiB, which leaves room for two 1024-thread blocks per CU (32 copies,
+// conflict-free but one block per CU, measured 2 % slower).
 // ------------------------------------------------------------------------
 constexpr int kCsBlock = 1024;
+constexpr int kCsCopyLog = 4;                 // 16 copies per table: 64 KiB, two blocks per CU
 
 __device__ __attribute__((always_inline)) inline uint32_t s4_at(const uint8_t *T, uint32_t t, uint32_t e,
                                                                 uint32_t loff) {
-    return *reinterpret_cast<const uint32_t *>(T + (t << 15) + (e << 7) + loff);
+    return *reinterpret_cast<const uint32_t *>(T + (t << (kCsCopyLog + 10)) + (e << (kCsCopyLog + 2)) + loff);
 }
 
 __device__ __attribute__((always_inline)) inline uint32_t s4_step(uint32_t c, uint32_t w, const uint8_t *T,
@@ -188,15 +191,15 @@ __global__ __launch_bounds__(kCsBlock) void k_crc32s(const uint8_t *__restrict__
     constexpr uint64_t kRow = 64u * G;
     constexpr uint32_t kPerWave = 64 / G;
     constexpr int kGap = G == 64 ? 7 : 6;              // sh64 index of the (G-1)*64-byte gap
-    __shared__ __attribute__((aligned(16))) uint32_t s_t[4 * 256 * 32];
+    __shared__ __attribute__((aligned(16))) uint32_t s_t[4 * 256 << kCsCopyLog];
     __shared__ uint32_t s_sh[kCrcSh64Tabs][8][16];
     __shared__ uint32_t s_byte[256];
-    for (int i = threadIdx.x; i < 4 * 256 * 32; i += kCsBlock) s_t[i] = (&tab->s4[0][0])[i >> 5];
+    for (int i = threadIdx.x; i < (4 * 256 << kCsCopyLog); i += kCsBlock) s_t[i] = (&tab->s4[0][0])[i >> kCsCopyLog];
     for (int i = threadIdx.x; i < kCrcSh64Tabs * 8 * 16; i += kCsBlock) (&s_sh[0][0][0])[i] = (&tab->sh64[0][0][0])[i];
     for (int i = threadIdx.x; i < 256; i += kCsBlock) s_byte[i] = tab->byte[i];
     __syncthreads();
     const uint8_t *T = reinterpret_cast<const uint8_t *>(s_t);
-    const uint32_t loff = (threadIdx.x & 31u) << 2;
+    const uint32_t loff = (threadIdx.x & ((1u << kCsCopyLog) - 1u)) << 2;
 
     const int lane = threadIdx.x & (G - 1);
     const uint32_t grp = (threadIdx.x >> 6) * kPerWave + ((threadIdx.x & 63) >> kLog);
@@ -359,7 +362,7 @@ int launch_crc32(const uint8_t *src, const uint64_t *off, const uint64_t *len,
     auto blocks = [&](uint32_t per_wave) {
         uint32_t waves = (count + per_wave - 1) / per_wave;
         uint32_t b = (waves + (kCsBlock / 64) - 1) / (kCsBlock / 64);
-        return b > 256u ? 256u : (b ? b : 1u);
+        return b > 512u ? 512u : (b ? b : 1u);
     };
     if (count >= 256u * (kCsBlock / 64) * 4u * 2u)
         hipLaunchKernelGGL(k_crc32s<16>, dim3(blocks(4)), dim3(kCsBlock), 0, st, src, off, len, init, out,
