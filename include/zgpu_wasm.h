@@ -67,6 +67,28 @@ uint32_t zlib_crc32_simd_enhanced(uint32_t crc, const uint8_t *data, size_t len)
 /* src/zlib_simd_optimized.c:116, with zlib-correct Adler-32 semantics */
 uint32_t zlib_adler32_simd(uint32_t adler, const uint8_t *buf, size_t len);
 
+/* src/zlib_simd_optimized.c:27,74,210,296 — the build's kernels that have no
+ * caller in the reference, with zlib-correct semantics, run on
+ * the GPU over the caller's host arrays:
+ *  slide_hash: every entry m of head[hash_size] and prev[window_size] becomes
+ *    m >= wsize ? m - wsize : 0 (deflate.c:187-209; the reference leaves a
+ *    remainder of < 16 entries untouched);
+ *  compare256: number of leading equal bytes of src0[0..256) and src1[0..256);
+ *  longest_match: deflate.c:1356-1497 over window[0 .. 2*(wmask+1)) and
+ *    prev[0 .. wmask+1), chain head prev[strstart & wmask], nice = min(258,
+ *    lookahead), limit strstart - (wmask+1-262); returns min(best, lookahead),
+ *    writes *match_start only when a candidate beat prev_length; invalid
+ *    arguments return prev_length;
+ *  chunkmemset: dest[i] = src[i % dist] for i < len (the LZ77 copy; the
+ *    reference's splat is wrong for dist in 3, 5..7, 9..15). */
+void zlib_slide_hash_simd(uint16_t *hash_table, uint16_t *prev_table, uint32_t hash_size,
+                          uint32_t window_size, uint16_t wsize);
+uint32_t zlib_compare256_simd(const uint8_t *src0, const uint8_t *src1);
+uint32_t zlib_longest_match_simd(const uint8_t *window, uint32_t strstart, uint32_t prev_length,
+                                 uint32_t good_match, uint32_t max_chain_length, uint32_t lookahead,
+                                 const uint16_t *prev_table, uint32_t wmask, uint32_t *match_start);
+void zlib_chunkmemset_simd(uint8_t *dest, uint8_t *src, uint32_t dist, uint32_t len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -931,3 +931,51 @@ int zo_pp_compress2(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
                     int level, int wrap, int strategy) {
     return compress_common(dst, dst_len, src, n, level, wrap, 1, strategy);
 }
+
+/* ------------------------------------------------------------------------ */
+/* a18 helpers, zlib-correct                                                 */
+/* ------------------------------------------------------------------------ */
+void zo_slide_hash(uint16_t *head, uint16_t *prev, uint32_t hash_size, uint32_t window_size,
+                   uint32_t wsize) {                          /* deflate.c:187-209 */
+    for (uint32_t i = 0; i < hash_size; i++) head[i] = (uint16_t)(head[i] >= wsize ? head[i] - wsize : 0);
+    for (uint32_t i = 0; i < window_size; i++) prev[i] = (uint16_t)(prev[i] >= wsize ? prev[i] - wsize : 0);
+}
+
+uint32_t zo_compare256(const uint8_t *a, const uint8_t *b) {
+    uint32_t k = 0;
+    while (k < 256 && a[k] == b[k]) k++;
+    return k;
+}
+
+/* deflate.c:1356-1497 with UNALIGNED_OK undefined: quick reject on scan_end,
+ * scan_end1, scan[0], scan[1]; byte 2 is not compared; bytes 3.. up to
+ * MAX_MATCH in the unrolled loop's units (32 groups of 8 end exactly at 258) */
+uint32_t zo_longest_match(const uint8_t *window, uint32_t strstart, uint32_t prev_length,
+                          uint32_t good, uint32_t chain, uint32_t lookahead, const uint16_t *prev,
+                          uint32_t wmask, uint32_t *match_start) {
+    const uint32_t wsize = wmask + 1, max_dist = wsize - MIN_LOOKAHEAD;
+    const uint8_t *scan = window + strstart;
+    uint32_t best = prev_length;
+    uint32_t nice = MAX_MATCH < lookahead ? MAX_MATCH : lookahead;
+    const uint32_t limit = strstart > max_dist ? strstart - max_dist : 0;
+    if (prev_length >= good) chain >>= 2;
+    uint32_t cur = prev[strstart & wmask];
+    if (!(cur > limit) || chain == 0) return best <= lookahead ? best : lookahead;
+    do {
+        const uint8_t *m = window + cur;
+        if (m[best] != scan[best] || m[best - 1] != scan[best - 1] || m[0] != scan[0] || m[1] != scan[1])
+            continue;
+        uint32_t len = 3;
+        while (len < MAX_MATCH && scan[len] == m[len]) len++;
+        if (len > best) {
+            *match_start = cur;
+            best = len;
+            if (len >= nice) break;
+        }
+    } while ((cur = prev[cur & wmask]) > limit && --chain != 0);
+    return best <= lookahead ? best : lookahead;
+}
+
+void zo_chunkmemset(uint8_t *dest, const uint8_t *src, uint32_t dist, uint32_t len) {
+    for (uint32_t i = 0; i < len; i++) dest[i] = src[i % dist];
+}

@@ -62,6 +62,17 @@ int zo_pp_compress(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
 
 int zo_pp_compress2(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
                     int level, int wrap, int strategy);
+/* ---- the a18 helper kernels (src/zlib_simd_optimized.c:27,74,210,296) with
+ * zlib-correct semantics: slide_hash (deflate.c:187-209), a 256-byte common
+ * prefix, longest_match over a caller's window/prev (deflate.c:1356-1497, nice
+ * = min(258, lookahead)), the LZ77 copy dest[i] = src[i % dist]. */
+void zo_slide_hash(uint16_t *head, uint16_t *prev, uint32_t hash_size, uint32_t window_size,
+                   uint32_t wsize);
+uint32_t zo_compare256(const uint8_t *a, const uint8_t *b);
+uint32_t zo_longest_match(const uint8_t *window, uint32_t strstart, uint32_t prev_length,
+                          uint32_t good, uint32_t chain, uint32_t lookahead, const uint16_t *prev,
+                          uint32_t wmask, uint32_t *match_start);
+void zo_chunkmemset(uint8_t *dest, const uint8_t *src, uint32_t dist, uint32_t len);
 /* ---- inflate (zinflate.c): inflate.c / inftrees.c / uncompr.c ----
  * wrap: 0 raw, 1 zlib, 2 gzip, 3 zlib or gzip (windowBits 15+32).
  * zo_inflate_run stops at the stream end (0), a data error (1), a preset

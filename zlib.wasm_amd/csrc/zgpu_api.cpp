@@ -220,6 +220,7 @@ struct Ctx {
     DevBuf ws_link2, ws_rf2, ws_rq2, ws_state2;
     DevBuf ws_key, ws_key2;   // k_count's walk-length keys (one byte per position)
     DevBuf ws_stg;            // k_parse_seg's symbol staging (caller's stream only)
+    DevBuf ws_help;           // the a18 helpers' staging (zlib_*_simd)
     // inflate: match records, per-stream results, checks, offsets, stop codes
     DevBuf ws_mrec, ws_irec, ws_ick, ws_imeta, ws_istop;
     hipStream_t aux = nullptr;
@@ -1349,6 +1350,80 @@ int zlib_compress_simd_buffer(const uint8_t *src, size_t src_len, uint8_t *dest,
     int rc = compress2(dest, &dl, src, src_len, level);
     *dest_len = dl;
     return rc;
+}
+
+// ---- src/zlib_simd_optimized.c kernels without a caller, zlib-
+// correct, on the GPU: the caller's host arrays are staged, the kernel runs,
+// the results come back.  With no GPU they leave their outputs unchanged (and
+// return 0) after libzgpu's one-time diagnostic.
+void zlib_slide_hash_simd(uint16_t *hash_table, uint16_t *prev_table, uint32_t hash_size,
+                          uint32_t window_size, uint16_t wsize) {    // src/zlib_simd_optimized.c:27
+    if ((!hash_table && hash_size) || (!prev_table && window_size)) return;
+    Ctx &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    if (init_locked(c)) return;
+    const size_t hb = 2ull * hash_size, pb = 2ull * window_size;
+    if (!c.ws_help.ensure(hb + pb + 64)) return;
+    uint16_t *dh = c.ws_help.as<uint16_t>(), *dp = dh + hash_size;
+    if ((hb && hipMemcpy(dh, hash_table, hb, hipMemcpyHostToDevice) != hipSuccess) ||
+        (pb && hipMemcpy(dp, prev_table, pb, hipMemcpyHostToDevice) != hipSuccess) ||
+        launch_slide_hash(dh, dp, hash_size, window_size, wsize, nullptr) ||
+        (hb && hipMemcpy(hash_table, dh, hb, hipMemcpyDeviceToHost) != hipSuccess) ||
+        (pb && hipMemcpy(prev_table, dp, pb, hipMemcpyDeviceToHost) != hipSuccess))
+        std::fprintf(stderr, "libzgpu: zlib_slide_hash_simd failed\n");
+}
+uint32_t zlib_compare256_simd(const uint8_t *src0, const uint8_t *src1) {   // src/zlib_simd_optimized.c:74
+    if (!src0 || !src1) return 0;
+    Ctx &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    if (init_locked(c) || !c.ws_help.ensure(512 + 64)) return 0;
+    uint8_t *d = c.ws_help.as<uint8_t>();
+    uint32_t *dr = reinterpret_cast<uint32_t *>(d + 512), r = 0;
+    if (hipMemcpy(d, src0, 256, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d + 256, src1, 256, hipMemcpyHostToDevice) != hipSuccess ||
+        launch_compare256(d, d + 256, dr, nullptr) ||
+        hipMemcpy(&r, dr, 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return 0;
+    return r;
+}
+uint32_t zlib_longest_match_simd(const uint8_t *window, uint32_t strstart, uint32_t prev_length,
+                                 uint32_t good_match, uint32_t max_chain_length, uint32_t lookahead,
+                                 const uint16_t *prev_table, uint32_t wmask,
+                                 uint32_t *match_start) {            // src/zlib_simd_optimized.c:210
+    // zlib's window is 2 * wsize bytes and prev[] wsize entries (wsize = wmask + 1,
+    // a power of two); strstart <= 2 * wsize - MIN_LOOKAHEAD as deflate keeps it
+    const uint64_t wsize = (uint64_t)wmask + 1;
+    if (!window || !prev_table || !match_start || (wsize & wmask) || wsize < 512 || wsize > 32768 ||
+        prev_length < 2 || prev_length > (uint32_t)kMaxMatch ||
+        (uint64_t)strstart + kMinLookahead > 2 * wsize || lookahead > 2 * wsize - strstart)
+        return prev_length;
+    Ctx &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    if (init_locked(c) || !c.ws_help.ensure(2 * wsize + 2 * wsize + 64)) return prev_length;
+    uint8_t *dw = c.ws_help.as<uint8_t>();
+    uint16_t *dp = reinterpret_cast<uint16_t *>(dw + 2 * wsize);
+    uint32_t *dr = reinterpret_cast<uint32_t *>(dw + 4 * wsize), r[3] = {prev_length, 0, 0};
+    if (hipMemcpy(dw, window, 2 * wsize, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(dp, prev_table, 2 * wsize, hipMemcpyHostToDevice) != hipSuccess ||
+        launch_longest_match(dw, strstart, prev_length, good_match, max_chain_length, lookahead, dp, wmask, dr,
+                             nullptr) ||
+        hipMemcpy(r, dr, sizeof r, hipMemcpyDeviceToHost) != hipSuccess)
+        return prev_length;
+    if (r[2]) *match_start = r[1];
+    return r[0];
+}
+void zlib_chunkmemset_simd(uint8_t *dest, uint8_t *src, uint32_t dist,
+                           uint32_t len) {                           // src/zlib_simd_optimized.c:296
+    if (!dest || !src || dist == 0 || len == 0) return;
+    const uint32_t sn = dist < len ? dist : len;
+    Ctx &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    if (init_locked(c) || !c.ws_help.ensure((size_t)sn + len + 64)) return;
+    uint8_t *ds = c.ws_help.as<uint8_t>(), *dd = ds + ((sn + 15) & ~15u);
+    if (hipMemcpy(ds, src, sn, hipMemcpyHostToDevice) != hipSuccess ||
+        launch_chunkmemset(dd, ds, dist, len, nullptr) ||
+        hipMemcpy(dest, dd, len, hipMemcpyDeviceToHost) != hipSuccess)
+        std::fprintf(stderr, "libzgpu: zlib_chunkmemset_simd failed\n");
 }
 
 }  // extern "C"

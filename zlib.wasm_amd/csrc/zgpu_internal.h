@@ -155,6 +155,14 @@ size_t checksum_scratch_bytes(uint32_t count);
 //        4 encode, 5 lazy parse (segmented), 6 lazy parse fallback for buffers flagged by 5,
 //        7 huffman-only parse, 8 rle parse, 9 walk-length keys (k_count)
 int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipStream_t st);
+// a18 helpers (zgpu_helpers.hip)
+int launch_slide_hash(uint16_t *head, uint16_t *prev, uint32_t hash_size, uint32_t window_size, uint32_t wsize,
+                      hipStream_t st);
+int launch_compare256(const uint8_t *a, const uint8_t *b, uint32_t *out, hipStream_t st);
+int launch_longest_match(const uint8_t *window, uint32_t strstart, uint32_t prev_length, uint32_t good,
+                         uint32_t chain, uint32_t lookahead, const uint16_t *prev, uint32_t wmask, uint32_t *out,
+                         hipStream_t st);
+int launch_chunkmemset(uint8_t *dest, const uint8_t *src, uint32_t dist, uint32_t len, hipStream_t st);
 int launch_generate(uint8_t *dst, uint64_t len, uint32_t count, int kind, uint64_t seed,
                     uint64_t first_index, hipStream_t st);
 

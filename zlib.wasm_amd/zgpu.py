@@ -55,7 +55,8 @@ EXPORTED_SYMBOLS = (
     "zlib_decompress", "zlib_compress_optimized", "zlib_compress", "zlib_deflate_init",
     "zlib_deflate_process", "zlib_deflate_end", "zlib_inflate_init", "zlib_inflate_process",
     "zlib_inflate_end", "zlib_stream_avail_in", "zlib_stream_avail_out", "zlib_stream_total_in",
-    "zlib_stream_total_out",
+    "zlib_stream_total_out", "zlib_slide_hash_simd", "zlib_compare256_simd",
+    "zlib_longest_match_simd", "zlib_chunkmemset_simd",
     # include/zgpu_debug.h (test-only)
     "zgpu_debug_stages",
 )
