@@ -397,6 +397,14 @@ typedef struct {
     /* window schedule: S = slide offset, E = end of data read so far */
     size_t S, E;
     size_t block_start;
+    /* deflate() calls with flushes (zo_deflate_flushes): the data available is
+     * [0, avail); flush event fi ends at fpos[fi] with type ftype[fi];
+     * insert = positions before strstart still to be hashed (deflate.c:1944) */
+    size_t avail, insert;
+    const size_t *fpos;
+    const int *ftype;
+    int nf, fi;
+    int open_end;              /* the stream is not finished: no final block, no trailer */
     /* current block */
     uint32_t sym[LIT_BUFSIZE]; /* (dist << 8) | lc  (dist 0 => literal lc) */
     unsigned nsym;
@@ -410,12 +418,51 @@ static inline unsigned hash3(const uint8_t *p) {      /* UPDATE_HASH x3, deflate
 }
 
 /* fill_window (deflate.c:251-368), window bookkeeping only */
+static size_t insert_at(zs_t *s, size_t p);
 static void fill(zs_t *s, size_t p) {
     if (p - s->S >= WSIZE + MAX_DIST) s->S += WSIZE;  /* slide, :277-287 */
-    if (s->E < s->n) {                                  /* read_buf, :306 */
+    if (s->E < s->avail) {                              /* read_buf, :306 */
         size_t e = s->S + WINDOW_SIZE;
-        s->E = e < s->n ? e : s->n;
+        s->E = e < s->avail ? e : s->avail;
+        /* hash the strings a flush left unhashed (:318-335) */
+        if (s->insert && s->E - p + s->insert >= MIN_MATCH) {
+            size_t str = p - s->insert;
+            while (s->insert) {
+                insert_at(s, str);
+                str++;
+                s->insert--;
+                if (s->E - p + s->insert < MIN_MATCH) break;
+            }
+        }
     }
+}
+
+static void flush_block(zs_t *s, size_t strstart, int last);
+/* end of a deflate(flush) call at p (deflate.c:2030-2042 and :1211-1233): the
+ * parser has tallied its pending literal; returns 1 when the event was a
+ * flush (the parse continues), 0 at the end of the stream (Z_FINISH) */
+static int flush_event(zs_t *s, size_t p, size_t ins) {
+    if (s->fi >= s->nf || s->fpos[s->fi] != p) return 0;
+    const int t = s->ftype[s->fi++];
+    s->insert = ins;
+    if (s->nsym) flush_block(s, p, 0);
+    bw_t *w = &s->bw;
+    if (t == 1) {                                       /* Z_PARTIAL_FLUSH: _tr_align, trees.c:900 */
+        bw_bits(w, 1u << 1, 3);
+        bw_bits(w, 0, 7);                               /* static END_BLOCK: 7 zero bits */
+    } else if (t == 2 || t == 3) {                      /* _tr_stored_block(s, 0, 0, 0) */
+        bw_bits(w, 0, 3);
+        bw_align(w);
+        bw_byte(w, 0); bw_byte(w, 0); bw_byte(w, 0xff); bw_byte(w, 0xff);
+        if (t == 3) {                                   /* Z_FULL_FLUSH: CLEAR_HASH, window reset */
+            if (s->head) memset(s->head, 0, 32768 * sizeof(uint32_t));
+            s->S = p;
+            s->block_start = p;
+            s->insert = 0;
+        }
+    }                                                   /* t == 5 (Z_BLOCK): nothing */
+    s->avail = s->fi < s->nf ? s->fpos[s->fi] : s->n;
+    return 1;
 }
 
 static void block_reset(zs_t *s) {                     /* init_block, trees.c:411-422 */
@@ -615,7 +662,10 @@ static void run_fast(zs_t *s) {
     for (;;) {
         if (s->E - p < MIN_LOOKAHEAD) {
             fill(s, p);
-            if (s->E == p) break;
+            if (s->E == p) {
+                if (flush_event(s, p, p - s->S < MIN_MATCH - 1 ? p - s->S : MIN_MATCH - 1)) continue;
+                break;
+            }
         }
         size_t lookahead = s->E - p;
         size_t hh = 0;
@@ -638,7 +688,7 @@ static void run_fast(zs_t *s) {
         }
         if (bflush) flush_block(s, p, 0);
     }
-    flush_block(s, p, 1);
+    if (!s->open_end) flush_block(s, p, 1);
 }
 
 /* deflate_slow (deflate.c:1923-2043) */
@@ -649,7 +699,16 @@ static void run_slow(zs_t *s) {
     for (;;) {
         if (s->E - p < MIN_LOOKAHEAD) {
             fill(s, p);
-            if (s->E == p) break;
+            if (s->E == p) {
+                if (s->fi < s->nf && s->fpos[s->fi] == p) {
+                    if (match_available) tally_lit(s, s->in[p - 1]);   /* no flush test */
+                    match_available = 0;
+                    match_length = MIN_MATCH - 1;
+                    flush_event(s, p, p - s->S < MIN_MATCH - 1 ? p - s->S : MIN_MATCH - 1);
+                    continue;
+                }
+                break;
+            }
         }
         size_t lookahead = s->E - p;
         size_t hh = 0;
@@ -687,6 +746,7 @@ static void run_slow(zs_t *s) {
             p++;
         }
     }
+    if (s->open_end) return;
     if (match_available) tally_lit(s, s->in[p - 1]);
     flush_block(s, p, 1);
 }
@@ -698,11 +758,14 @@ static void run_rle(zs_t *s) {
     for (;;) {
         if (s->E - p <= MAX_MATCH) {
             fill(s, p);
-            if (s->E == p) break;
+            if (s->E == p) {
+                if (flush_event(s, p, 0)) continue;
+                break;
+            }
         }
         const size_t lookahead = s->E - p;
         unsigned match_length = 0;
-        if (lookahead >= MIN_MATCH && p > 0) {
+        if (lookahead >= MIN_MATCH && p > s->S) {       /* strstart > 0 */
             const uint8_t prev = s->in[p - 1];
             if (s->in[p] == prev && s->in[p + 1] == prev && s->in[p + 2] == prev) {
                 unsigned len = 3;                          /* run length, capped at MAX_MATCH */
@@ -720,7 +783,7 @@ static void run_rle(zs_t *s) {
         }
         if (bflush) flush_block(s, p, 0);
     }
-    flush_block(s, p, 1);
+    if (!s->open_end) flush_block(s, p, 1);
 }
 
 /* deflate_huff (deflate.c:2122-2152): literals only; fill_window when the
@@ -730,13 +793,16 @@ static void run_huff(zs_t *s) {
     for (;;) {
         if (s->E == p) {
             fill(s, p);
-            if (s->E == p) break;
+            if (s->E == p) {
+                if (flush_event(s, p, 0)) continue;
+                break;
+            }
         }
         const int bflush = tally_lit(s, s->in[p]);
         p++;
         if (bflush) flush_block(s, p, 0);
     }
-    flush_block(s, p, 1);
+    if (!s->open_end) flush_block(s, p, 1);
 }
 
 /* deflate_stored (deflate.c:1635-1815) for a single deflate(Z_FINISH) call
@@ -842,7 +908,8 @@ static int assemble(zs_t *s, uint8_t *dst, size_t *dst_len, int wrap) {
     }
     uint8_t trl[8];
     size_t tlen = 0;
-    if (wrap == 1) {
+    if (s->open_end) {
+    } else if (wrap == 1) {
         uint32_t a = zo_adler32(1, s->in, s->n);
         if (s->n == 0) a = 1;
         trl[0] = (uint8_t)(a >> 24); trl[1] = (uint8_t)(a >> 16);
@@ -863,8 +930,16 @@ static int assemble(zs_t *s, uint8_t *dst, size_t *dst_len, int wrap) {
     return total <= cap ? ZO_OK : ZO_BUF_ERROR;
 }
 
+static int compress_events(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
+                           int level, int wrap, int pp, int strategy, const size_t *fpos,
+                           const int *ftype, int nf, int finish);
 static int compress_common(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
                            int level, int wrap, int pp, int strategy) {
+    return compress_events(dst, dst_len, src, n, level, wrap, pp, strategy, NULL, NULL, 0, 1);
+}
+static int compress_events(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
+                           int level, int wrap, int pp, int strategy, const size_t *fpos,
+                           const int *ftype, int nf, int finish) {
     init_tables();
     if (level == -1) level = 6;
     if (level < 0 || level > 9 || wrap < 0 || wrap > 2 || !dst_len) return ZO_STREAM_ERROR;
@@ -875,6 +950,12 @@ static int compress_common(uint8_t *dst, size_t *dst_len, const uint8_t *src, si
     if (!s) return ZO_MEM_ERROR;
     s->in = src;
     s->n = n;
+    s->fpos = fpos;
+    s->ftype = ftype;
+    s->nf = nf;
+    s->fi = 0;
+    s->avail = nf ? fpos[0] : n;
+    s->open_end = !finish;
     s->level = level;
     s->cfg = CFG[level];
     s->pp = pp;
@@ -978,4 +1059,18 @@ uint32_t zo_longest_match(const uint8_t *window, uint32_t strstart, uint32_t pre
 
 void zo_chunkmemset(uint8_t *dest, const uint8_t *src, uint32_t dist, uint32_t len) {
     for (uint32_t i = 0; i < len; i++) dest[i] = src[i % dist];
+}
+
+/* deflate() driven by a sequence of calls (see zoracle.h) */
+int zo_deflate_flushes(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n, int level,
+                       int wrap, int strategy, const size_t *fpos, const int *ftype, int nf,
+                       int finish) {
+    if (level == -1) level = 6;
+    if (level == 0 && nf) return ZO_STREAM_ERROR;      /* deflate_stored's blocks follow avail_out */
+    for (int i = 0; i < nf; i++) {
+        if (fpos[i] > n || (i && fpos[i] < fpos[i - 1])) return ZO_STREAM_ERROR;
+        if (ftype[i] != 1 && ftype[i] != 2 && ftype[i] != 3 && ftype[i] != 5) return ZO_STREAM_ERROR;
+    }
+    if (!finish && (nf == 0 || fpos[nf - 1] != n)) return ZO_STREAM_ERROR;
+    return compress_events(dst, dst_len, src, n, level, wrap, 0, strategy, fpos, ftype, nf, finish);
 }

@@ -62,6 +62,17 @@ int zo_pp_compress(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
 
 int zo_pp_compress2(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
                     int level, int wrap, int strategy);
+/* deflate() over a sequence of calls: the input is [0, n); call i ended at
+ * fpos[i] (ascending) with flush ftype[i] in {Z_PARTIAL_FLUSH 1, Z_SYNC_FLUSH 2,
+ * Z_FULL_FLUSH 3, Z_BLOCK 5} (calls zlib turns away, a repeated flush with no
+ * input and no higher rank, are not listed); Z_NO_FLUSH calls in between do not
+ * change the stream.  finish = 1: the last call was Z_FINISH at n (final block,
+ * trailer); finish = 0: fpos[nf-1] == n and the output is every complete byte
+ * written so far (header included).  Levels 1..9 (level 0's stored blocks
+ * follow the caller's avail_out).  deflate.c:954-1263,1923-2043, trees.c:887. */
+int zo_deflate_flushes(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n, int level,
+                       int wrap, int strategy, const size_t *fpos, const int *ftype, int nf,
+                       int finish);
 /* ---- the a18 helper kernels (src/zlib_simd_optimized.c:27,74,210,296) with
  * zlib-correct semantics: slide_hash (deflate.c:187-209), a 256-byte common
  * prefix, longest_match over a caller's window/prev (deflate.c:1356-1497, nice

@@ -7,6 +7,7 @@
 * the position-parallel formulation (the GPU's spec) against both.
 """
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -214,3 +215,77 @@ def test_oracle_inflate_vs_reference_fuzz(oracle):
             for src in (bytes(zz), z[:cut]):
                 cap = int(rng.integers(0, len(data) + 2))
                 assert oracle.uncompress(src, cap, wrap) == ref.uncompress(src, cap, wrap), (t, i, cut)
+
+
+def _flush_plan(rng, n):
+    """A random deflate() call sequence over n bytes: chunk sizes from tiny to
+    window-sized, flush types Z_NO_FLUSH / PARTIAL / SYNC / FULL / BLOCK,
+    repeated flushes with no input, then Z_FINISH."""
+    calls, pos = [], 0
+    while pos < n:
+        take = int(min(n - pos, rng.choice([0, 1, 2, 3, 17, 300, 4000, 40000, 70000])))
+        flush = int(rng.choice([0, 0, 1, 2, 2, 3, 5]))
+        calls.append((take, flush))
+        pos += take
+        if rng.random() < 0.15:
+            calls.append((0, int(rng.choice([1, 2, 3, 5]))))
+    calls.append((0, 4))
+    return calls
+
+
+@pytest.mark.skipif(not reference_available(), reason="compiled reference only in the build container")
+def test_oracle_flushes_vs_reference(oracle):
+    """deflate() call sequences with Z_PARTIAL/SYNC/FULL_FLUSH and Z_BLOCK on
+    the compiled reference (deflate.c:954-1263, flush handling :1211-1233, the
+    parsers' flush tails :1905-1915,2030-2042) against zo_deflate_flushes: the
+    whole stream, and after every flush call the bytes written so far."""
+    from zhelpers import flush_events
+    ref = Reference()
+    rng = np.random.default_rng(int(os.environ.get("ZO_FLUSH_SEED", 11)))
+    for t in range(int(os.environ.get("ZO_FLUSH_CASES", 40))):
+        kind = ["text", "mix", "runs", "random", "four"][t % 5]
+        n = int(rng.choice([0, 5, 1000, 70000, 150000]))
+        data = datagen.make(kind, n, 300 + t)
+        level = int(rng.choice([1, 2, 3, 4, 6, 9]))
+        strategy = int(rng.choice([0, 0, 0, 1, 2, 3, 4]))
+        wbits = int(rng.choice([15, -15, 31]))
+        wrap = {15: 1, -15: 0, 31: 2}[wbits]
+        calls = _flush_plan(rng, n)
+        sts, lens, whole = ref.deflate_calls(data, calls, level, wbits, strategy)
+        ev = flush_events(calls)
+        rc, got = oracle.deflate_flushes(data, ev, level, wrap, strategy)
+        assert rc == 0 and got == whole, (t, kind, n, level, strategy, wbits)
+        pos = 0
+        for i, (take, flush) in enumerate(calls[:-1]):
+            pos += take
+            if flush in (0, 4) or sts[i] != 0:
+                continue
+            pre = flush_events(calls[:i + 1])
+            rc, part = oracle.deflate_flushes(data[:pos], pre, level, wrap, strategy, finish=False)
+            assert rc == 0 and part == whole[:lens[i]], (t, i, pos, flush)
+
+
+def test_oracle_flush_golden(oracle):
+    """zo_deflate_flushes against the reference's deflate() call sequences
+    frozen in tests/golden/flush_golden.json (whole stream and the output
+    after every flush call)."""
+    import json
+    import os as _os
+    from zhelpers import flush_events
+    with open(_os.path.join(_os.path.dirname(__file__), "golden", "flush_golden.json")) as f:
+        cases = json.load(f)["cases"]
+    for c in cases:
+        data = datagen.make(c["kind"], c["n"], c["seed"])
+        assert hashlib.sha256(data).hexdigest() == c["input_sha256"]
+        calls = [tuple(x) for x in c["calls"]]
+        wrap = {15: 1, -15: 0, 31: 2}[c["wbits"]]
+        rc, got = oracle.deflate_flushes(data, flush_events(calls), c["level"], wrap, c["strategy"])
+        assert rc == 0 and len(got) == c["len"] and hashlib.sha256(got).hexdigest() == c["sha256"], c["seed"]
+        pos = 0
+        for i, (take, flush) in enumerate(calls[:-1]):
+            pos += take
+            if flush in (0, 4) or c["status"][i] != 0:
+                continue
+            rc, part = oracle.deflate_flushes(data[:pos], flush_events(calls[:i + 1]), c["level"], wrap,
+                                              c["strategy"], finish=False)
+            assert rc == 0 and part == got[:c["out_len"][i]], (c["seed"], i)

@@ -47,6 +47,10 @@ class Oracle:
         L.zo_uncompress3.restype = C.c_int
         L.zo_uncompress3.argtypes = [C.c_void_p, C.POINTER(C.c_size_t), C.c_void_p,
                                      C.POINTER(C.c_size_t), C.c_int]
+        L.zo_deflate_flushes.restype = C.c_int
+        L.zo_deflate_flushes.argtypes = [C.c_void_p, C.POINTER(C.c_size_t), C.c_void_p, C.c_size_t,
+                                         C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
+                                         C.c_int]
         L.zo_pp_links.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
         L.zo_pp_match.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_void_p,
                                   C.c_void_p, C.c_void_p]
@@ -66,6 +70,19 @@ class Oracle:
             return self._compress(lambda o, n, d, ln, lv, w: self.L.zo_compress2(o, n, d, ln, lv, w, strategy),
                                   data, level, wrap, cap)
         return self._compress(self.L.zo_compress, data, level, wrap, cap)
+
+    def deflate_flushes(self, data, events, level=6, wrap=1, strategy=0, finish=True):
+        """zo_deflate_flushes: (rc, stream) for flush events [(pos, flush)]."""
+        data = bytes(data)
+        nf = len(events)
+        fpos = (C.c_size_t * max(nf, 1))(*[e[0] for e in events])
+        ftyp = (C.c_int * max(nf, 1))(*[e[1] for e in events])
+        cap = compress_bound(len(data)) + 64 + 16 * nf
+        out = C.create_string_buffer(cap)
+        n = C.c_size_t(cap)
+        rc = self.L.zo_deflate_flushes(out, C.byref(n), data, len(data), level, wrap, strategy, fpos, ftyp,
+                                       nf, 1 if finish else 0)
+        return rc, out.raw[: n.value]
 
     def pp_compress(self, data, level=6, wrap=1, cap=None):
         return self._compress(self.L.zo_pp_compress, data, level, wrap, cap)
@@ -227,6 +244,31 @@ class Reference:
         self.L.deflateEnd(C.byref(strm))
         return out.raw[:total]
 
+    def deflate_calls(self, data, calls, level=6, wbits=15, strategy=0):
+        """deflate() over a call sequence [(input_len, flush), ...] (the lengths
+        sum to len(data), the last call is Z_FINISH or not); returns
+        (status per call, output length after each call, whole output)."""
+        data = bytes(data)
+        strm = ZStream()
+        rc = self.L.deflateInit2_(C.byref(strm), level, 8, wbits, 8, strategy, self.version,
+                                  C.sizeof(ZStream))
+        assert rc == Z_OK, rc
+        cap = compress_bound(len(data)) + 64 + 16 * len(calls)
+        out = C.create_string_buffer(cap)
+        inbuf = C.create_string_buffer(data, max(len(data), 1))
+        strm.next_out = C.addressof(out)
+        strm.avail_out = cap
+        pos, sts, lens = 0, [], []
+        for take, flush in calls:
+            strm.next_in = C.addressof(inbuf) + pos
+            strm.avail_in = take
+            pos += take
+            sts.append(self.L.deflate(C.byref(strm), flush))
+            lens.append(strm.total_out)
+        total = strm.total_out
+        self.L.deflateEnd(C.byref(strm))
+        return sts, lens, out.raw[:total]
+
     def crc32(self, data, crc=0):
         data = bytes(data)
         return self.L.crc32(crc, data, len(data))
@@ -234,6 +276,20 @@ class Reference:
     def adler32(self, data, adler=1):
         data = bytes(data)
         return self.L.adler32(adler, data, len(data))
+
+
+def flush_events(calls):
+    """The flush events zlib acts on for a call sequence: a flush call with no
+    new input whose RANK is not above the previous call's is refused with
+    Z_BUF_ERROR (deflate.c:1002-1005).  Returns [(position, flush), ...]."""
+    rank = lambda f: f * 2 - (9 if f > 4 else 0)
+    ev, pos, last = [], 0, -2
+    for take, flush in calls:
+        pos += take
+        if flush not in (0, 4) and not (take == 0 and rank(flush) <= rank(last)):
+            ev.append((pos, flush))
+        last = flush
+    return ev
 
 
 def reference_available():
