@@ -21,10 +21,13 @@
  * Z_FILTERED, Z_HUFFMAN_ONLY, Z_RLE, Z_FIXED; deflate.c:1190-1193,1964,
  * 2051-2152, trees.c:1035) — compress2() and the reference's compressSIMD
  * path use the default (compress.c:36, src/zlib_simd_optimized.c:365).  Input is gathered across
- * Z_NO_FLUSH calls and compressed on the GPU at Z_FINISH; the stream is then
- * drained through next_out/avail_out across as many calls as needed.  Other
- * parameters, and Z_SYNC_FLUSH/Z_FULL_FLUSH/Z_BLOCK mid-stream, return
- * Z_STREAM_ERROR (documented gap).
+ * Z_NO_FLUSH calls and compressed on the GPU at the next flush call or at
+ * Z_FINISH; the stream is then drained through next_out/avail_out across as
+ * many calls as needed.  Z_PARTIAL_FLUSH, Z_SYNC_FLUSH, Z_FULL_FLUSH and
+ * Z_BLOCK act as in deflate.c:763-1265 (markers, full-flush reset, refused
+ * repeats with Z_BUF_ERROR); each flush call hands out the stream up to its
+ * marker.  Flush calls at level 0 and other parameters return Z_STREAM_ERROR
+ * (documented gap).
  */
 #ifndef ZGPU_ZLIB_H
 #define ZGPU_ZLIB_H

@@ -1,0 +1,189 @@
+"""deflate() with flush calls (Z_PARTIAL_FLUSH, Z_SYNC_FLUSH, Z_FULL_FLUSH,
+Z_BLOCK, refused repeats, then Z_FINISH) through libzgpu's z_stream API on the
+GPU, against
+
+  * tests/golden/flush_golden.json -- call sequences run through the compiled
+    reference (deflate.c:763-1265): the status of every call, the output length
+    after every flush call and the sha256 of the whole stream;
+  * the oracle's zo_deflate_flushes (oracle/zoracle.c) on further random call
+    sequences, and on the stream prefix each flush call hands out.
+
+Bit-exact.  Level 0 with flush calls is a documented gap (Z_STREAM_ERROR)."""
+import ctypes as C
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import datagen
+from zhelpers import ZStream, flush_events
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+VERSION = b"1.3.1.1-motley"
+
+
+def _lib(zg):
+    L = zg.load()
+    L.deflateInit2_.restype = C.c_int
+    L.deflateInit2_.argtypes = [C.POINTER(ZStream), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                C.c_char_p, C.c_int]
+    L.deflate.restype = C.c_int
+    L.deflate.argtypes = [C.POINTER(ZStream), C.c_int]
+    L.deflateEnd.restype = C.c_int
+    L.deflateEnd.argtypes = [C.POINTER(ZStream)]
+    return L
+
+
+def replay(L, data, calls, level, wbits, strategy, chunk=None):
+    """Run a call sequence [(input_len, flush)]; with ``chunk`` every call is
+    zpipe's loop (repeat while avail_out == 0 with a fresh ``chunk``-byte
+    buffer).  Returns (status per call, total_out after each call, stream)."""
+    data = bytes(data)
+    s = ZStream()
+    assert L.deflateInit2_(C.byref(s), level, 8, wbits, 8, strategy, VERSION, C.sizeof(ZStream)) == 0
+    inbuf = C.create_string_buffer(data, max(len(data), 1))
+    cap = chunk or (2 * len(data) + 1024 + 16 * len(calls))
+    outbuf = C.create_string_buffer(cap)
+    out, sts, lens, pos = bytearray(), [], [], 0
+    for take, flush in calls:
+        s.next_in = C.addressof(inbuf) + pos
+        s.avail_in = take
+        pos += take
+        rounds = 0
+        while True:
+            s.next_out, s.avail_out = C.addressof(outbuf), cap
+            rc = L.deflate(C.byref(s), flush)
+            out += outbuf.raw[:cap - s.avail_out]
+            rounds += 1
+            assert rounds < 1_000_000
+            if chunk is None or s.avail_out != 0:
+                break
+        sts.append(rc)
+        lens.append(s.total_out)
+        assert s.avail_in == 0
+    assert L.deflateEnd(C.byref(s)) == 0
+    return sts, lens, bytes(out)
+
+
+@pytest.fixture(scope="module")
+def flush_golden():
+    with open(os.path.join(HERE, "golden", "flush_golden.json")) as f:
+        return json.load(f)["cases"]
+
+
+def _case_input(c):
+    data = datagen.make(c["kind"], c["n"], c["seed"])
+    assert hashlib.sha256(bytes(data)).hexdigest() == c["input_sha256"]
+    return data
+
+
+def test_flush_golden_streams(zg, flush_golden):
+    L = _lib(zg)
+    for c in flush_golden:
+        data = _case_input(c)
+        sts, lens, whole = replay(L, data, c["calls"], c["level"], c["wbits"], c["strategy"])
+        tag = (c["kind"], c["n"], c["level"], c["strategy"], c["wbits"])
+        assert sts == c["status"], tag
+        # output after every flush call (Z_NO_FLUSH output is deferred here)
+        for (take, flush), got, want in zip(c["calls"], lens, c["out_len"]):
+            if flush != 0:
+                assert got == want, (tag, take, flush)
+        assert len(whole) == c["len"], tag
+        assert hashlib.sha256(whole).hexdigest() == c["sha256"], tag
+
+
+def _plan(rng, n):
+    calls, pos = [], 0
+    while pos < n:
+        take = int(min(n - pos, rng.choice([0, 1, 2, 3, 5, 250, 3000, 33000, 66000, 140000])))
+        calls.append((take, int(rng.choice([0, 1, 2, 2, 3, 5]))))
+        pos += take
+        if rng.random() < 0.2:
+            calls.append((0, int(rng.choice([1, 2, 3, 5]))))
+    calls.append((0, 4))
+    return calls
+
+
+def test_flush_random_vs_oracle(zg, oracle):
+    """Random call sequences; every flush call's output is the oracle's stream
+    prefix (open end: complete bytes, no trailer), the end is its stream."""
+    L = _lib(zg)
+    rng = np.random.default_rng(int(os.environ.get("ZGPU_FLUSH_SEED", "31")))
+    kinds = ["text", "mix", "runs", "random", "records", "markup"]
+    for t in range(int(os.environ.get("ZGPU_FLUSH_CASES", "24"))):
+        n = int(rng.choice([0, 2, 700, 50000, 200000, 600000]))
+        data = datagen.make(kinds[t % len(kinds)], n, 900 + t)
+        level = 1 + t % 9
+        strategy = int(rng.choice([0, 0, 1, 2, 3, 4]))
+        wbits = int(rng.choice([15, -15, 31]))
+        wrap = {15: 1, -15: 0, 31: 2}[wbits]
+        calls = _plan(rng, n)
+        sts, lens, whole = replay(L, data, calls, level, wbits, strategy)
+        ev = flush_events(calls)
+        rc, want = oracle.deflate_flushes(data, ev, level, wrap, strategy, finish=True)
+        tag = (t, n, level, strategy, wbits)
+        assert rc == 0 and whole == want, tag
+        assert sts[-1] == 1, tag
+        pos = 0
+        for i, (take, flush) in enumerate(calls[:-1]):
+            pos += take
+            if flush == 0 or sts[i] != 0:
+                continue
+            rc, pre = oracle.deflate_flushes(data[:pos], flush_events(calls[:i + 1]), level, wrap, strategy,
+                                             finish=False)
+            assert rc == 0 and lens[i] == len(pre) and whole[:len(pre)] == pre, (tag, i)
+
+
+def test_flush_small_output_buffers(zg, flush_golden):
+    """zpipe-style loops with small output buffers: a flush call that runs
+    out of output before its marker completes it on the repeat call (no second
+    marker); the stream is the golden one whenever no marker ends exactly at the
+    end of a buffer (zlib.h: avail_out greater than six)."""
+    L = _lib(zg)
+    done = 0
+    for c in flush_golden:
+        if c["n"] < 1000 or done >= 12:
+            continue
+        data = _case_input(c)
+        for chunk in (997, 16384):
+            _, _, whole = replay(L, data, c["calls"], c["level"], c["wbits"], c["strategy"], chunk=chunk)
+            _, _, ref = replay(L, data, c["calls"], c["level"], c["wbits"], c["strategy"])
+            if whole != ref:
+                # a repeated marker: the stream must still decode to the input
+                import zlib as pyzlib
+                wb = {15: 15, -15: -15, 31: 31}[c["wbits"]]
+                assert pyzlib.decompress(whole, wb) == bytes(data)
+            else:
+                assert hashlib.sha256(whole).hexdigest() == c["sha256"]
+        done += 1
+    assert done > 0
+
+
+def test_flush_level0_and_errors(zg):
+    L = _lib(zg)
+    s = ZStream()
+    assert L.deflateInit2_(C.byref(s), 0, 8, 15, 8, 0, VERSION, C.sizeof(ZStream)) == 0
+    buf = C.create_string_buffer(b"abc", 3)
+    out = C.create_string_buffer(64)
+    s.next_in, s.avail_in = C.addressof(buf), 3
+    s.next_out, s.avail_out = C.addressof(out), 64
+    assert L.deflate(C.byref(s), 2) == -2          # documented gap: level 0 with flushes
+    assert L.deflate(C.byref(s), 4) == 1
+    assert L.deflateEnd(C.byref(s)) == 0
+    # a repeated flush with no new input is refused (deflate.c:1002-1005)
+    s = ZStream()
+    assert L.deflateInit2_(C.byref(s), 6, 8, 15, 8, 0, VERSION, C.sizeof(ZStream)) == 0
+    s.next_in, s.avail_in = C.addressof(buf), 3
+    s.next_out, s.avail_out = C.addressof(out), 64
+    assert L.deflate(C.byref(s), 2) == 0
+    n1 = s.total_out
+    s.next_out, s.avail_out = C.addressof(out), 64
+    assert L.deflate(C.byref(s), 2) == -5
+    assert L.deflate(C.byref(s), 1) == -5          # lower rank
+    assert L.deflate(C.byref(s), 3) == 0           # higher rank: acted on
+    assert s.total_out == n1 + 5
+    assert L.deflateEnd(C.byref(s)) == 0

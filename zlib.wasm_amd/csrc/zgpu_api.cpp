@@ -276,13 +276,23 @@ inline int hip_ok(hipError_t e) { return e == hipSuccess ? ZGPU_OK : ZGPU_MEM_ER
 // ------------------------------------------------------------------------
 // deflate orchestration (caller holds ctx().mu)
 // ------------------------------------------------------------------------
+// The deflate(flush) calls of a streaming job (device arrays, see DeflateJob).
+struct FlushSpec {
+    const uint64_t *pos;
+    const uint32_t *type;
+    uint32_t n;
+    int open_end;
+    uint64_t *mark_bits;
+};
+
 int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
                        uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
                        uint64_t *dst_len, int32_t *status, uint32_t count, int level, int wrap,
-                       int strategy, hipStream_t st) {
+                       int strategy, hipStream_t st, const FlushSpec *fs = nullptr) {
     if (level == -1) level = 6;
     if (level < 0 || level > 9 || wrap < 0 || wrap > 2 || strategy < 0 || strategy > 4)
         return ZGPU_STREAM_ERROR;
+    if (fs && (count != 1 || level == 0)) return ZGPU_STREAM_ERROR;
     if (count == 0) return ZGPU_OK;
     std::vector<uint64_t> lens(count);
     if (hipMemcpyAsync(lens.data(), src_len, 8ull * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -317,7 +327,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             // literal at index n (a run of literals up to the end), which must
             // not land in the next buffer's region
             pos += (lens[i] + 64) & ~63ull;
-            blk += lens[i] / kSymLimit + 2;
+            blk += lens[i] / kSymLimit + 2 + (fs ? 2ull * fs->n : 0);   // a flush: a block and a marker
         }
         max_pos = std::max(max_pos, pos);
         max_blk = std::max(max_blk, blk);
@@ -396,6 +406,13 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         job.blocks = c.ws_blk.as<BlockRec>();
         job.nblocks = d_nblk;
         job.check = d_check;
+        if (fs) {
+            job.fl_pos = fs->pos;
+            job.fl_type = fs->type;
+            job.nfl = fs->n;
+            job.open_end = fs->open_end;
+            job.mark_bits = fs->mark_bits;
+        }
         return job;
     };
     // trailer check value, parse, encode of sub-batch s on the caller's stream
@@ -407,10 +424,16 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         else if (wrap == 2)
             rc = T.run(0, st, [&] { return launch_crc32(src, src_off + a, src_len + a, nullptr, d_check, b - a, nullptr, 0, st); });
         if (rc) return ZGPU_MEM_ERROR;
-        if (huff) {
+        if ((huff || rle) && fs) {
+            if (T.run(4, st, [&] { return launch_deflate_stage(10, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+        } else if (huff) {
             if (T.run(4, st, [&] { return launch_deflate_stage(7, job, nullptr, st); })) return ZGPU_MEM_ERROR;
         } else if (rle) {
             if (T.run(4, st, [&] { return launch_deflate_stage(8, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+        } else if (level >= 4 && fs) {
+            // flush jobs: the sequential lazy parse (the segmented one assumes
+            // the input is all there)
+            if (T.run(3, st, [&] { return launch_deflate_stage(2, job, nullptr, st); })) return ZGPU_MEM_ERROR;
         } else if (level >= 4) {
             if (T.run(3, st, [&] { return launch_deflate_stage(5, job, nullptr, st); })) return ZGPU_MEM_ERROR;
             if (T.run(3, st, [&] { return launch_deflate_stage(6, job, nullptr, st); })) return ZGPU_MEM_ERROR;
@@ -461,8 +484,18 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
 }
 
 // host-buffer batch: pack, upload, run, download
+// host-side flush calls of one streaming job (positions ascending, see FlushSpec)
+struct FlushHost {
+    const uint64_t *pos;
+    const uint32_t *type;
+    uint32_t n;
+    int open_end;
+    uint64_t mark_bits;     // out: output bits before the last marker
+};
+
 int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
-                         size_t *dst_len, int *status, size_t count, int level, int wrap, int strategy) {
+                         size_t *dst_len, int *status, size_t count, int level, int wrap, int strategy,
+                         FlushHost *fh = nullptr) {
     if (count == 0) return ZGPU_OK;
     std::vector<uint64_t> so(count), sl(count), dofs(count), dcap(count);
     uint64_t in_total = 0, out_total = 0;
@@ -474,7 +507,8 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
         dcap[i] = dst_len[i];
         out_total += (dst_len[i] + 15) & ~15ull;
     }
-    const size_t meta_bytes = 8 * 4 * count + 16 * count;
+    const size_t ev_bytes = fh ? 16ull * fh->n + 32 : 0;
+    const size_t meta_bytes = 8 * 4 * count + 16 * count + ev_bytes;
     if (!c.ws_io.ensure(in_total + 64) || !c.ws_io2.ensure(out_total + 64) ||
         !c.ws_small.ensure(meta_bytes + 64))
         return ZGPU_MEM_ERROR;
@@ -499,9 +533,22 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
         hipMemcpyAsync(d_do, dofs.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(d_dc, dcap.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
+    FlushSpec fs{};
+    if (fh) {
+        uint64_t *d_fp = reinterpret_cast<uint64_t *>(d_st + 2 * count);   // 8-aligned
+        uint32_t *d_ft = reinterpret_cast<uint32_t *>(d_fp + fh->n);
+        if (fh->n && (hipMemcpyAsync(d_fp, fh->pos, 8ull * fh->n, hipMemcpyHostToDevice, st) != hipSuccess ||
+                      hipMemcpyAsync(d_ft, fh->type, 4ull * fh->n, hipMemcpyHostToDevice, st) != hipSuccess))
+            return ZGPU_MEM_ERROR;
+        uint64_t *d_mb = d_fp + fh->n + (fh->n + 1) / 2;
+        if (hipMemsetAsync(d_mb, 0, 8, st) != hipSuccess) return ZGPU_MEM_ERROR;
+        fs = FlushSpec{d_fp, d_ft, fh->n, fh->open_end, d_mb};
+    }
     int rc = deflate_dev_locked(c, d_in, d_so, d_sl, d_out, d_do, d_dc, d_dl, d_st, (uint32_t)count,
-                                level, wrap, strategy, st);
+                                level, wrap, strategy, st, fh ? &fs : nullptr);
     if (rc) return rc;
+    if (fh && hipMemcpy(&fh->mark_bits, fs.mark_bits, 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return ZGPU_MEM_ERROR;
     std::vector<uint64_t> ol(count);
     std::vector<int32_t> os(count);
     if (hipMemcpy(ol.data(), d_dl, 8 * count, hipMemcpyDeviceToHost) != hipSuccess ||
@@ -972,12 +1019,25 @@ uLong adler32_combine64(uLong adler1, uLong adler2, int64_t len2) {
 }
 uLong adler32_combine(uLong adler1, uLong adler2, long len2) { return adler32_combine64(adler1, adler2, len2); }
 
-// z_stream deflate: gather input, compress on the GPU at Z_FINISH, drain.
+// z_stream deflate: gather input, compress on the GPU at a flush call or at
+// Z_FINISH, drain.
 struct internal_state {
     int level, wrap, strategy;
-    std::vector<uint8_t> in, out;
+    std::vector<uint8_t> in, out;   // deflate: the input since the last Z_FULL_FLUSH; output queue
     size_t out_pos;
     int finished;     // 0 gathering, 1 compressed / decoded
+    // deflate(flush) calls (Z_PARTIAL_FLUSH, Z_SYNC_FLUSH, Z_FULL_FLUSH, Z_BLOCK):
+    // the stream is the header, then one raw "part" per Z_FULL_FLUSH-separated
+    // stretch of input (each starts from an empty window and byte aligned,
+    // deflate.c:1225-1231), then the trailer
+    int last_flush = -2;            // deflate.c: s->last_flush (deflateReset)
+    bool flushed = false;           // a flush call was acted on
+    bool header_done = false;
+    std::vector<uint64_t> ev_pos;   // the current part's flush calls (part-relative)
+    std::vector<uint32_t> ev_type;
+    size_t part_out = 0;            // bytes of the current part already queued
+    bool marker_due = false;        // the last flush call ran out of output before its marker
+    uint32_t check = 0;             // adler32 / crc32 of the input before the current part
     // inflate streams
     int inflating = 0;
     int wbits = 15;
@@ -1007,6 +1067,7 @@ int deflateInit2_(z_streamp strm, int level, int method, int windowBits, int mem
     s->strategy = strategy;
     s->out_pos = 0;
     s->finished = 0;
+    s->check = wrap == 2 ? 0 : 1;
     strm->state = s;
     strm->total_in = strm->total_out = 0;
     strm->data_type = Z_UNKNOWN;
@@ -1018,41 +1079,185 @@ int deflateInit_(z_streamp strm, int level, const char *version, int stream_size
     return deflateInit2_(strm, level, Z_DEFLATED, 15, 8, Z_DEFAULT_STRATEGY, version, stream_size);
 }
 
-int deflate(z_streamp strm, int flush) {
-    if (!strm || !strm->state || strm->state->inflating || flush < 0 || flush > Z_BLOCK) return Z_STREAM_ERROR;
-    internal_state *s = strm->state;
-    if (!strm->next_out || (strm->avail_in && !strm->next_in)) return Z_STREAM_ERROR;
-    if (flush != Z_NO_FLUSH && flush != Z_FINISH) return Z_STREAM_ERROR;   // documented gap
-    if (strm->avail_out == 0) return Z_BUF_ERROR;
-    if (s->finished && strm->avail_in) return Z_BUF_ERROR;
-    if (strm->avail_in) {
-        s->in.insert(s->in.end(), strm->next_in, strm->next_in + strm->avail_in);
-        strm->total_in += strm->avail_in;
-        strm->next_in += strm->avail_in;
-        strm->avail_in = 0;
+namespace {
+// deflate(flush) calls: the prefix of the current part up to the flush
+// position, compressed with the part's flush calls as a raw stream that ends
+// open (complete bytes only); its first part_out bytes were queued before.
+int deflate_part(internal_state *s, int open_end, std::vector<uint8_t> &body, uint64_t *mark_bits = nullptr) {
+    const uint32_t nev = (uint32_t)s->ev_pos.size();
+    size_t cap = (size_t)compress_bound64(s->in.size()) + 64 + 16ull * nev;
+    body.resize(cap);
+    const uint8_t *sp = s->in.data();
+    uint8_t *dp = body.data();
+    size_t sl = s->in.size();
+    int st = 0;
+    FlushHost fh{s->ev_pos.data(), s->ev_type.data(), nev, open_end};
+    Ctx &c = ctx();
+    std::lock_guard<std::mutex> g(c.mu);
+    int rc = init_locked(c);
+    if (!rc) rc = compress_host_locked(c, &sp, &sl, &dp, &cap, &st, 1, s->level, ZGPU_WRAP_RAW, s->strategy,
+                                       nev ? &fh : nullptr);
+    if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
+    body.resize(cap);
+    if (mark_bits) *mark_bits = fh.mark_bits;
+    return Z_OK;
+}
+
+uint32_t stream_check(const internal_state *s, uint32_t init, const uint8_t *p, size_t n) {
+    return s->wrap == 2 ? (uint32_t)crc32_z(init, p, n) : (uint32_t)adler32_z(init, p, n);
+}
+
+void queue_header(internal_state *s) {                          // deflate.c:1002-1073
+    if (s->header_done) return;
+    s->header_done = true;
+    if (s->wrap == 1) {
+        uint32_t header = (8u + ((15u - 8u) << 4)) << 8;
+        const uint32_t flags = (s->strategy >= 2 || s->level < 2) ? 0u : s->level < 6 ? 1u : s->level == 6 ? 2u : 3u;
+        header |= flags << 6;
+        header += 31 - (header % 31);
+        s->out.push_back((uint8_t)(header >> 8));
+        s->out.push_back((uint8_t)header);
+    } else if (s->wrap == 2) {
+        const uint8_t xfl = s->level == 9 ? 2 : (s->strategy >= 2 || s->level < 2) ? 4 : 0;
+        const uint8_t g[10] = {31, 139, 8, 0, 0, 0, 0, 0, xfl, 3};
+        s->out.insert(s->out.end(), g, g + 10);
     }
-    if (flush == Z_FINISH && !s->finished) {
-        size_t cap = (size_t)compress_bound64(s->in.size()) + 32;
-        s->out.resize(cap);
-        const uint8_t *sp = s->in.data();
-        uint8_t *dp = s->out.data();
-        size_t sl = s->in.size();
-        int st = 0;
-        int rc = zgpu_compress_batch_ex(&sp, &sl, &dp, &cap, &st, 1, s->level, s->wrap, s->strategy);
-        if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
-        s->out.resize(cap);
-        s->finished = 1;
-        strm->adler = s->wrap == 2 ? crc32_z(0, sp, sl) : (s->wrap == 1 ? adler32_z(1, sp, sl) : 0);
-        s->in.clear();
-        s->in.shrink_to_fit();
-    }
-    if (!s->finished) return Z_OK;
+}
+
+void drain(z_streamp strm, internal_state *s) {
     size_t take = std::min<size_t>(strm->avail_out, s->out.size() - s->out_pos);
     std::memcpy(strm->next_out, s->out.data() + s->out_pos, take);
     s->out_pos += take;
     strm->next_out += take;
     strm->avail_out -= (uInt)take;
     strm->total_out += take;
+    if (s->out_pos == s->out.size() && !s->finished) {
+        s->out.clear();
+        s->out_pos = 0;
+    }
+}
+
+inline int flush_rank(int f) { return f * 2 - (f > 4 ? 9 : 0); }   // deflate.c: RANK
+
+// A flush call whose event is the last of s->ev_*: its blocks and marker are
+// queued.  zlib writes the blocks first and returns need_more when the output
+// space runs out at a block (deflate.c:1685-1690 FLUSH_BLOCK); the marker
+// follows only in a call that got past the last block (the zlib.h contract
+// repeats the flush call while avail_out == 0) -- and a call that ends with
+// avail_out == 0 after the marker makes the next one append another
+// (zlib.h: "avail_out is greater than six to avoid repeated flush markers").
+int emit_flush(z_streamp strm, internal_state *s, int flush) {
+    std::vector<uint8_t> body;
+    uint64_t mb = 0;
+    if (int rc = deflate_part(s, 1, body, &mb)) return rc;
+    queue_header(s);
+    const uint64_t queued = strm->total_out + (s->out.size() - s->out_pos);
+    const uint64_t cap = strm->total_out + strm->avail_out;
+    const size_t q_last = (size_t)(mb >> 3);                  // complete bytes before the marker
+    if (q_last > s->part_out && queued - s->part_out + q_last >= cap) {
+        s->out.insert(s->out.end(), body.begin() + (std::ptrdiff_t)s->part_out, body.begin() + (std::ptrdiff_t)q_last);
+        s->part_out = q_last;
+        s->marker_due = true;
+        drain(strm, s);
+        s->last_flush = -1;
+        return Z_OK;
+    }
+    s->out.insert(s->out.end(), body.begin() + (std::ptrdiff_t)s->part_out, body.end());
+    s->part_out = body.size();
+    if (s->wrap) strm->adler = stream_check(s, s->check, s->in.data(), s->in.size());
+    if (flush == Z_FULL_FLUSH) {                                // the next part starts afresh
+        if (s->wrap) s->check = (uint32_t)strm->adler;
+        s->in.clear();
+        s->ev_pos.clear();
+        s->ev_type.clear();
+        s->part_out = 0;
+    }
+    drain(strm, s);
+    if (strm->avail_out == 0) s->last_flush = -1;
+    return Z_OK;
+}
+}  // namespace
+
+int deflate(z_streamp strm, int flush) {
+    if (!strm || !strm->state || strm->state->inflating || flush < 0 || flush > Z_BLOCK) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    if (!strm->next_out || (strm->avail_in && !strm->next_in) || (s->finished && flush != Z_FINISH))
+        return Z_STREAM_ERROR;
+    const bool is_flush = flush != Z_NO_FLUSH && flush != Z_FINISH;
+    // level 0 with flush calls: deflate_stored's blocks follow avail_out
+    // (deflate.c:1635-1815) -- documented gap
+    if (is_flush && s->level == 0) return Z_STREAM_ERROR;
+    if (strm->avail_out == 0) return Z_BUF_ERROR;
+    const int old_flush = s->last_flush;
+    s->last_flush = flush;
+    if (s->out_pos < s->out.size()) {                           // deflate.c:983-1005
+        drain(strm, s);
+        if (strm->avail_out == 0) {
+            s->last_flush = -1;
+            return Z_OK;
+        }
+    } else if (strm->avail_in == 0 && flush_rank(flush) <= flush_rank(old_flush) && flush != Z_FINISH) {
+        return Z_BUF_ERROR;
+    }
+    if (s->finished && strm->avail_in) return Z_BUF_ERROR;
+    if (s->marker_due) {
+        // the previous flush call cut its block but ran out of output before
+        // the marker: a flush call with no input completes it with its own
+        // kind; anything else leaves the cut without a marker (Z_BLOCK's)
+        s->marker_due = false;
+        if (!strm->avail_in && is_flush) {
+            s->ev_type.back() = (uint32_t)flush;
+            return emit_flush(strm, s, flush);
+        }
+        s->ev_type.back() = Z_BLOCK;
+    }
+    if (strm->avail_in) {
+        s->in.insert(s->in.end(), strm->next_in, strm->next_in + strm->avail_in);
+        strm->total_in += strm->avail_in;
+        strm->next_in += strm->avail_in;
+        strm->avail_in = 0;
+    }
+    if (is_flush) {
+        s->flushed = true;
+        s->ev_pos.push_back(s->in.size());
+        s->ev_type.push_back((uint32_t)flush);
+        return emit_flush(strm, s, flush);
+    }
+    if (flush == Z_FINISH && !s->finished) {
+        if (!s->flushed) {
+            size_t cap = (size_t)compress_bound64(s->in.size()) + 32;
+            s->out.resize(cap);
+            const uint8_t *sp = s->in.data();
+            uint8_t *dp = s->out.data();
+            size_t sl = s->in.size();
+            int st = 0;
+            int rc = zgpu_compress_batch_ex(&sp, &sl, &dp, &cap, &st, 1, s->level, s->wrap, s->strategy);
+            if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
+            s->out.resize(cap);
+            strm->adler = s->wrap == 2 ? crc32_z(0, sp, sl) : (s->wrap == 1 ? adler32_z(1, sp, sl) : 0);
+        } else {
+            std::vector<uint8_t> body;
+            if (int rc = deflate_part(s, 0, body)) return rc;
+            queue_header(s);
+            s->out.insert(s->out.end(), body.begin() + (std::ptrdiff_t)s->part_out, body.end());
+            if (s->wrap) {
+                const uint32_t ck = stream_check(s, s->check, s->in.data(), s->in.size());
+                strm->adler = ck;
+                if (s->wrap == 1) {
+                    for (int i = 3; i >= 0; i--) s->out.push_back((uint8_t)(ck >> (8 * i)));
+                } else {
+                    const uint32_t isz = (uint32_t)strm->total_in;
+                    for (int i = 0; i < 4; i++) s->out.push_back((uint8_t)(ck >> (8 * i)));
+                    for (int i = 0; i < 4; i++) s->out.push_back((uint8_t)(isz >> (8 * i)));
+                }
+            }
+        }
+        s->finished = 1;
+        s->in.clear();
+        s->in.shrink_to_fit();
+    }
+    drain(strm, s);
+    if (flush != Z_FINISH) return Z_OK;
     return s->out_pos == s->out.size() ? Z_STREAM_END : Z_OK;
 }
 

@@ -559,6 +559,40 @@ __device__ unsigned long long g_mstat[4];   // kMatchStats statistics
 //                 latency-bound at the 16 waves the LDS window allows)
 constexpr int kMatchDefault = 19, kMatchStats = 21, kMatchProbeNoWalk = 33, kMatchProbeHalf = 35;
 
+__device__ inline uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+// The deflate(flush) calls of a flush job (DeflateJob::fl_pos/fl_type): the
+// parse runs as if the input ended at the next flush position (deflate() has
+// not seen more), and when it stands there with the window drained the call's
+// flush is acted on (deflate.c:2030-2042, :1211-1233).  Positions are read
+// uniformly (every lane the same value).
+struct FlushEv {
+    const uint64_t *pos;
+    const uint32_t *type;
+    uint32_t n, i;
+    __device__ inline bool at(int64_t p) const { return i < n && (int64_t)ufl64(pos[i]) == p; }
+    __device__ inline uint32_t kind() const { return (uint32_t)__builtin_amdgcn_readfirstlane((int)type[i]); }
+    __device__ inline int64_t limit(int64_t end) const { return i < n ? (int64_t)ufl64(pos[i]) : end; }
+    __device__ static inline uint64_t ufl64(uint64_t v) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+        return ((uint64_t)hi << 32) | lo;
+    }
+};
+__device__ inline FlushEv flush_ev(const DeflateJob &job) { return FlushEv{job.fl_pos, job.fl_type, job.nfl, 0}; }
+
+// first flush position > p: the end of the input deflate() has seen when the
+// parse decides at p (longest_match's nice / lookahead clamp), else n
+__device__ inline int64_t flush_limit(const DeflateJob &job, int64_t p, int64_t n) {
+    uint32_t lo = 0, hi = job.nfl;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((int64_t)job.fl_pos[mid] > p) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo < job.nfl ? (int64_t)job.fl_pos[lo] : n;
+}
+
 template <int kVariant>
 __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int want_q) {
     constexpr bool kSorted = kVariant != 14;
@@ -626,9 +660,12 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
             const int i = atomicAdd(&next_i, 1);
             if (i >= tile_n) break;
             const int64_t p = ts + (kSorted ? (int)s_perm[i] : i);
+            // a flush job's search at p sees the input up to the next flush
+            // position only (nice and the compare length are clamped to it)
+            const int64_t nl = job.nfl ? flush_limit(job, p, n) : n;
             if (kVariant == kMatchStats) {
                 uint32_t steps = 0, cmps = 0;
-                mw14_walk<2, false>(E, p, B, n, cfg, rf, rq, want_q, &steps, &cmps);
+                mw14_walk<2, false>(E, p, B, nl, cfg, rf, rq, want_q, &steps, &cmps);
                 uint32_t mx = steps;
 #pragma unroll
                 for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
@@ -640,7 +677,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
                 rf[p] = 0;                                  // probe: staging, sort and stores only
                 if (want_q) rq[p] = 0;
             } else {
-                mw14_walk<2, false>(E, p, B, n, cfg, rf, rq, want_q);
+                mw14_walk<2, false>(E, p, B, nl, cfg, rf, rq, want_q);
             }
         }
         __syncthreads();
@@ -682,12 +719,25 @@ struct ParseOut {
         blk_sym_start = nsym;
         blk_nsym = 0;
     }
-    // fill_window (deflate.c:251-368), bookkeeping only
+    // the bits a deflate(flush) call appends after its blocks (kBlkMarker)
+    __device__ inline void marker(int64_t strstart, uint32_t kind) {
+        BlockRec r;
+        r.sym_start = blk_sym_start;
+        r.nsym = 0;
+        r.in_start = r.in_end = (uint64_t)strstart;
+        r.flags = kBlkMarker | (kind << 4);
+        r.pad = 0;
+        if (lead) blk[nblk] = r;
+        nblk++;
+    }
+    // fill_window (deflate.c:251-368), bookkeeping only; n = the end of the
+    // input deflate() has been given so far
     __device__ inline void fill(int64_t p, int64_t n) {
         if (p - S >= (int64_t)(kWSize + kMaxDist)) S += kWSize;
         if (E < n) { int64_t e = S + 2 * kWSize; E = e < n ? e : n; }
     }
 };
+
 
 // ------------------------------------------------------------------------
 // k_parse_slow — deflate_slow over precomputed per-position results.
@@ -699,7 +749,6 @@ struct ParseOut {
 // ------------------------------------------------------------------------
 constexpr int kPT = 4096;
 
-__device__ inline uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
 struct ParseU {                     // wave-uniform parse output state
     uint32_t *sym;
@@ -726,6 +775,18 @@ struct ParseU {                     // wave-uniform parse output state
         if (lane == 0) sym[nsym] = v;
         nsym++;
         return ++blk_nsym == (uint32_t)kSymLimit;
+    }
+    __device__ inline void marker(uint32_t strstart, uint32_t kind, int lane) {   // see ParseOut::marker
+        if (lane == 0) {
+            BlockRec r;
+            r.sym_start = blk_sym_start;
+            r.nsym = 0;
+            r.in_start = r.in_end = strstart;
+            r.flags = kBlkMarker | (kind << 4);
+            r.pad = 0;
+            blk[nblk] = r;
+        }
+        nblk++;
     }
     __device__ inline void fill(uint32_t p, uint32_t n) {                   // fill_window bookkeeping
         if (p - S >= (uint32_t)(kWSize + kMaxDist)) S += kWSize;
@@ -757,6 +818,8 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
     po.block_start = 0; po.S = 0; po.E = 0;
     uint32_t p = 0, match_start = 0, match_length = kMinMatch - 1;
     bool avail = false, done = false;
+    FlushEv fe = flush_ev(job);
+    uint32_t lim = (uint32_t)fe.limit(n);      // input deflate() has been given
 
     uint32_t t0 = 0;
     while (!done) {
@@ -768,8 +831,24 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
         for (;;) {
             if (!tile_to_end && p + 64 > t0 + kPT) break;         // reload, keep 64 lookahead
             if (po.E - p < (uint32_t)kMinLookahead) {
-                po.fill(p, n);
-                if (po.E == p) { done = true; break; }
+                po.fill(p, lim);
+                if (po.E == p) {
+                    if (fe.at(p)) {
+                        // a deflate(flush) call ends here (deflate.c:2030-2042): the
+                        // pending literal is tallied without a flush test, the
+                        // block is flushed if it holds symbols, then the marker
+                        if (avail) po.tally1(ufl(s_in[p - 1 - t0 + 16]), lane);
+                        avail = false;
+                        match_length = kMinMatch - 1;
+                        if (po.blk_nsym) po.flush(p, false, lane);
+                        po.marker(p, fe.kind(), lane);
+                        fe.i++;
+                        lim = (uint32_t)fe.limit(n);
+                        continue;
+                    }
+                    done = true;
+                    break;
+                }
             }
             const uint32_t lookahead = po.E - p;
             // ---- bulk literals: no pending match, far from the window end ----
@@ -827,8 +906,10 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
             }
         }
         if (done) {
-            if (avail) po.tally1(ufl(s_in[p - 1 - t0 + 16]), lane);
-            po.flush(p, true, lane);
+            if (!job.open_end) {
+                if (avail) po.tally1(ufl(s_in[p - 1 - t0 + 16]), lane);
+                po.flush(p, true, lane);
+            }
             if (lane == 0) job.nblocks[bi] = po.nblk;
         }
         t0 = p & ~15u;
@@ -1321,6 +1402,67 @@ __global__ __launch_bounds__(64) void k_parse_rle(DeflateJob job) {
 }
 
 // ------------------------------------------------------------------------
+// k_parse_ev — Z_HUFFMAN_ONLY / Z_RLE parse of a flush job (deflate_huff,
+// deflate.c:2122-2152; deflate_rle, :2051-2116), one lane, sequential: the
+// window schedule decides where its blocks end once flush calls cut the input
+// (fill_window at lookahead 0 resp. <= MAX_MATCH), and flush jobs are the
+// streaming API's, one buffer at a time.
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_parse_ev(DeflateJob job) {
+    if (threadIdx.x != 0) return;
+    const uint32_t bi = blockIdx.x;
+    const uint32_t g = job.first + bi;
+    const int64_t n = (int64_t)job.src_len[g];
+    const uint8_t *in = job.src + job.src_off[g];
+    const bool rle = job.strategy == 3;
+    ParseOut po;
+    po.sym = job.sym + job.ws_off[bi];
+    po.blk = job.blocks + job.blk_off[bi];
+    po.nsym = po.blk_nsym = po.blk_sym_start = po.nblk = 0;
+    po.block_start = 0; po.S = 0; po.E = 0;
+    po.lead = true;
+    FlushEv fe = flush_ev(job);
+    int64_t lim = fe.limit(n);
+    int64_t p = 0;
+    for (;;) {
+        if (rle ? po.E - p <= kMaxMatch : po.E == p) {
+            po.fill(p, lim);
+            if (po.E == p) {
+                if (fe.at(p)) {
+                    if (po.blk_nsym) po.flush(p, false);
+                    po.marker(p, fe.kind());
+                    fe.i++;
+                    lim = fe.limit(n);
+                    continue;
+                }
+                break;
+            }
+        }
+        const int64_t lookahead = po.E - p;
+        uint32_t len = 0;
+        if (rle && lookahead >= kMinMatch && p > po.S) {      // strstart > 0
+            const uint8_t c = in[p - 1];
+            if (in[p] == c && in[p + 1] == c && in[p + 2] == c) {
+                len = kMinMatch;
+                while (len < (uint32_t)kMaxMatch && p + len < n && in[p + len] == c) len++;
+                if (len > lookahead) len = (uint32_t)lookahead;
+            }
+        }
+        bool bflush;
+        if (len >= (uint32_t)kMinMatch) {
+            bflush = po.tally((1u << 8) | (len - kMinMatch));
+            p += len;
+        } else {
+            bflush = po.tally(in[p]);
+            p++;
+        }
+        if (bflush) po.flush(p, false);
+    }
+    if (!job.open_end) po.flush(p, true);
+    job.nblocks[bi] = po.nblk;
+}
+
+// ------------------------------------------------------------------------
 // k_parse_fast — levels 1..3 (deflate_fast).  Insertion inside a match depends
 // on its length (deflate.c:1873-1897), so hash chains are maintained exactly
 // as zlib does it, sequentially: head[] (absolute positions, per buffer, in
@@ -1401,10 +1543,37 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
 
     int64_t p = 0, match_start = 0;
     uint32_t match_length = kMinMatch - 1;
+    FlushEv fe = flush_ev(job);
+    int64_t lim = fe.limit(n);                 // input deflate() has been given
+    int64_t pend = 0;                          // s->insert: strings a flush left unhashed
     for (;;) {
         if (po.E - p < kMinLookahead) {
-            po.fill(p, n);
-            if (po.E == p) break;
+            const bool reads = po.E < lim;
+            po.fill(p, lim);
+            // fill_window hashes the strings the last flush left unhashed once
+            // new input is read (deflate.c:318-335)
+            if (reads && pend && po.E - p + pend >= kMinMatch) {
+                int64_t str = p - pend;
+                while (pend) {
+                    wsee(str);
+                    insert(str);
+                    str++;
+                    pend--;
+                    if (po.E - p + pend < kMinMatch) break;
+                }
+            }
+            if (po.E == p) {
+                if (fe.at(p)) {
+                    // a deflate(flush) call ends here (deflate.c:1903-1914, :1211-1233)
+                    pend = p - po.S < kMinMatch - 1 ? p - po.S : kMinMatch - 1;
+                    if (po.blk_nsym) po.flush(p, false);
+                    po.marker(p, fe.kind());
+                    fe.i++;
+                    lim = fe.limit(n);
+                    continue;
+                }
+                break;
+            }
         }
         wsee(p);
         int64_t lookahead = po.E - p;
@@ -1474,7 +1643,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         }
         if (bflush) po.flush(p, false);
     }
-    po.flush(p, true);
+    if (!job.open_end) po.flush(p, true);
     if (lead) job.nblocks[bi] = po.nblk;
 }
 
@@ -1791,7 +1960,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
                 const uint32_t kb = g0 + (uint32_t)wave;
                 TreeLDS &T = TT[wave];
                 uint32_t *hl = HL[wave], *hd = HD[wave];
-                if (kb < nblk) {
+                if (kb < nblk && !(blk[kb].flags & kBlkMarker)) {
                     const BlockRec br = blk[kb];
                     // histogram (_tr_tally freq updates, deflate.h:354-372)
                     for (int i = lane; i < kLCodes; i += 64) hl[i] = 0;
@@ -1832,7 +2001,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
                         if (static_lenb <= opt_lenb || job.strategy == 4) opt_lenb = static_lenb;   // trees.c:1035
                         const uint64_t stored_len = br.in_end - br.in_start;
                         int type;                                   // trees.c:1027-1074
-                        if (stored_len + 4 <= opt_lenb && (br.flags & 2u)) type = 0;
+                        if (stored_len + 4 <= opt_lenb && (br.flags & kBlkStored)) type = 0;
                         else if (static_lenb == opt_lenb) type = 1;
                         else type = 2;
                         s_hdr[wave].type = type;
@@ -1846,8 +2015,27 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
           for (int w = 0; w < kEncGroup && g0 + (uint32_t)w < nblk; w++) {
             const uint32_t k = g0 + (uint32_t)w;
             const BlockRec br = blk[k];
-            const bool last = br.flags & 1u;
+            const bool last = br.flags & kBlkLast;
             TreeLDS &T = TT[w];
+            if (br.flags & kBlkMarker) {
+                // what the deflate(flush) call appends (deflate.c:1211-1233)
+                if (s_obit - st.sbase + 128 > kStgBits) stg_flush(st, s_obit, false);
+                if (tid == 0) {
+                    const uint32_t kind = blk_marker_kind(br.flags);
+                    if (job.mark_bits) job.mark_bits[bi] = (uint64_t)s_obit;
+                    if (kind == 1) {                    // _tr_align (trees.c:900-904)
+                        put(1u << 1, 3);                // STATIC_TREES, not last
+                        put(0, 7);                      // END_BLOCK in the static tree
+                    } else if (kind == 2 || kind == 3) {   // _tr_stored_block(s, 0, 0, 0)
+                        put(0, 3);
+                        s_obit = (s_obit + 7) & ~7ll;
+                        put(0, 16);
+                        put(0xffffu, 16);
+                    }
+                }
+                __syncthreads();
+                continue;
+            }
             // room for the largest block header (dynamic trees: < 5000 bits)
             if (s_obit - st.sbase + 6144 > kStgBits) stg_flush(st, s_obit, false);
             if (tid == 0) {
@@ -2023,6 +2211,7 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     case 7: hipLaunchKernelGGL(k_parse_huff, grid, dim3(kHuffThreads), 0, st, job); break;
     case 8: hipLaunchKernelGGL(k_parse_rle, grid, dim3(64), 0, st, job); break;
     case 9: hipLaunchKernelGGL(k_count, grid, dim3(kCntThreads), 0, st, job); break;
+    case 10: hipLaunchKernelGGL(k_parse_ev, grid, dim3(64), 0, st, job); break;
     default: return -1;
     }
     return (int)hipGetLastError();

@@ -70,9 +70,17 @@ struct BlockRec {
     uint32_t nsym;
     uint64_t in_start;    // block_start (absolute input position)
     uint64_t in_end;      // strstart at flush
-    uint32_t flags;       // bit0 last, bit1 stored-eligible (block_start still in window)
+    uint32_t flags;       // kBlk* below
     uint32_t pad;
 };
+constexpr uint32_t kBlkLast = 1u;     // BFINAL
+constexpr uint32_t kBlkStored = 2u;   // stored-eligible (block_start still in the window)
+// A marker record is no block: it stands for the bits a deflate(flush) call
+// appends after its blocks (deflate.c:1211-1233), its kind in bits 4..6:
+// Z_PARTIAL_FLUSH 1 (_tr_align), Z_SYNC_FLUSH 2 / Z_FULL_FLUSH 3 (an empty
+// stored block), Z_BLOCK 5 (nothing).
+constexpr uint32_t kBlkMarker = 8u;
+__host__ __device__ constexpr uint32_t blk_marker_kind(uint32_t flags) { return (flags >> 4) & 7u; }
 
 // Per-buffer workspace layout for one deflate sub-batch (device arrays).
 struct DeflateJob {
@@ -101,6 +109,16 @@ struct DeflateJob {
     BlockRec *blocks;        // [Σ(n/16383 + 2)]
     uint32_t *nblocks;       // [count]
     uint32_t *check;         // [count] adler32 / crc32 of the input (trailer)
+    // deflate(flush) calls of a streaming job (count == 1, zgpu_api.cpp deflate()):
+    // the input position where each flush call ended (ascending) and its kind
+    // (Z_PARTIAL_FLUSH 1, Z_SYNC_FLUSH 2, Z_FULL_FLUSH 3 -- only as the job's
+    // last event --, Z_BLOCK 5); open_end: the stream goes on after the last
+    // flush (no final block, complete bytes only).  nfl == 0 for batch jobs.
+    const uint64_t *fl_pos;
+    const uint32_t *fl_type;
+    uint32_t nfl;
+    int open_end;
+    uint64_t *mark_bits;     // [count] or null: output bits written before the last marker
 };
 
 // ---- inflate ----
@@ -153,7 +171,8 @@ int launch_adler32(const uint8_t *src, const uint64_t *off, const uint64_t *len,
 size_t checksum_scratch_bytes(uint32_t count);
 // stage: 0 links, 1 match, 2 lazy parse (sequential), 3 greedy parse (heads: 128 KiB/buffer),
 //        4 encode, 5 lazy parse (segmented), 6 lazy parse fallback for buffers flagged by 5,
-//        7 huffman-only parse, 8 rle parse, 9 walk-length keys (k_count)
+//        7 huffman-only parse, 8 rle parse, 9 walk-length keys (k_count),
+//        10 huffman-only / rle parse of a flush job (sequential)
 int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipStream_t st);
 // a18 helpers (zgpu_helpers.hip)
 int launch_slide_hash(uint16_t *head, uint16_t *prev, uint32_t hash_size, uint32_t window_size, uint32_t wsize,
