@@ -468,7 +468,7 @@ __device__ __attribute__((always_inline)) inline int cmp16(const uint32_t *E, in
     return k;
 }
 
-template <int kUnroll, bool kBatch>
+template <int kUnroll, bool kBatch, bool kNoCmp = false>
 __device__ __attribute__((always_inline)) inline bool mw14_loop(MW3 &w, uint32_t &em, uint32_t &eb,
                                                                 const Scan16 &S, const uint32_t *E, uint32_t end) {
     const char *Eb = reinterpret_cast<const char *>(E);
@@ -479,7 +479,7 @@ __device__ __attribute__((always_inline)) inline bool mw14_loop(MW3 &w, uint32_t
         const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + a);
         uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
         const uint32_t miss = ((em >> 16) ^ w.scan01) | ((eb >> 16) ^ w.scanE);
-        if (__builtin_expect(miss == 0, 0)) {
+        if (!kNoCmp && __builtin_expect(miss == 0, 0)) {
             w.ncmp++;
             const int m = w.m4 >> 2, s = w.s4 >> 2;
             const int k = cmp16<kBatch>(E, m, s, S, w.maxcmp);
@@ -502,7 +502,7 @@ __device__ __attribute__((always_inline)) inline bool mw14_loop(MW3 &w, uint32_t
     }
 }
 
-template <int kUnroll, bool kBatch>
+template <int kUnroll, bool kBatch, bool kNoCmp = false>
 __device__ __attribute__((always_inline)) inline void mw14_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
                                                                 const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
                                                                 int want_q, uint32_t *st_steps = nullptr,
@@ -534,12 +534,13 @@ __device__ __attribute__((always_inline)) inline void mw14_walk(const uint32_t *
     uint32_t em = E[s - (int)d0];
     uint32_t eb = E[s - (int)d0 + 1];
     const uint32_t qc = want_q ? (uint32_t)(cfg.chain >> 2) : (uint32_t)cfg.chain;
-    const bool done = mw14_loop<kUnroll, kBatch>(w, em, eb, S, E, qc);
+    const bool done = mw14_loop<kUnroll, kBatch, kNoCmp>(w, em, eb, S, E, qc);
     if (want_q) {
         rq[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
-        if (!done) mw14_loop<kUnroll, kBatch>(w, em, eb, S, E, (uint32_t)cfg.chain);
+        if (!done) mw14_loop<kUnroll, kBatch, kNoCmp>(w, em, eb, S, E, (uint32_t)cfg.chain);
     }
     rf[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
+    if (kNoCmp) rf[p] = (w.count ^ (uint32_t)w.m4) == 0x7fffffffu ? 1u : 0u;   // probe: keep the walk live
     if (st_steps) { *st_steps = w.count; *st_cmp = w.ncmp; }
 }
 
@@ -553,11 +554,17 @@ __device__ unsigned long long g_mstat[4];   // kMatchStats statistics
 //   14            positions in index order (no keys)
 //   21            19 plus statistics (lane steps, compares, walks, wave
 //                 iterations) printed after each launch
+//   37            timing probe (wrong results): walks without compares (every
+//                 quick-reject pass ignored, so no walk stops at nice): 127 ms
+//                 of 355 per 4 GiB at L6 -- the compares, 3.4 % of the steps,
+//                 hold their waves for the rest (in most steps some lane of 64
+//                 compares)
 //   33, 35        timing probes (wrong results): 33 no walks (tile staging,
 //                 sort and stores: 33 ms of 351 per 4 GiB at L6); 35 half the
 //                 waves walk (1.6x slower at L6, 1.8x at L9: the walks are
 //                 latency-bound at the 16 waves the LDS window allows)
-constexpr int kMatchDefault = 19, kMatchStats = 21, kMatchProbeNoWalk = 33, kMatchProbeHalf = 35;
+constexpr int kMatchDefault = 19, kMatchStats = 21, kMatchProbeNoWalk = 33, kMatchProbeHalf = 35,
+              kMatchProbeNoCmp = 37;
 
 __device__ inline uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
@@ -673,6 +680,9 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
                 st_cmps += cmps;
                 st_walks += steps ? 1u : 0u;
                 if ((tid & 63) == __builtin_ctzll(__ballot(1))) st_wave_iters += mx;
+            } else if (kVariant == kMatchProbeNoCmp) {
+                mw14_walk<2, false, true>(E, p, B, nl, cfg, rf, rq, want_q);
+
             } else if (kVariant == kMatchProbeNoWalk) {
                 rf[p] = 0;                                  // probe: staging, sort and stores only
                 if (want_q) rq[p] = 0;
@@ -2167,7 +2177,8 @@ static int match_variant() {
     static const int v = [] {
         const char *e = getenv("ZGPU_MATCH_VARIANT");
         const int x = e ? atoi(e) : kMatchDefault;
-        return (x == 14 || x == kMatchStats || x == kMatchProbeNoWalk || x == kMatchProbeHalf) ? x : kMatchDefault;
+        return (x == 14 || x == kMatchStats || x == kMatchProbeNoWalk || x == kMatchProbeHalf ||
+                x == kMatchProbeNoCmp) ? x : kMatchDefault;
     }();
     return v;
 }
@@ -2188,6 +2199,9 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
             hipLaunchKernelGGL(k_match<kMatchProbeNoWalk>, grid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchProbeHalf) {
             hipLaunchKernelGGL(k_match<kMatchProbeHalf>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchProbeNoCmp) {
+            hipLaunchKernelGGL(k_match<kMatchProbeNoCmp>, grid, dim3(kMatchThreads), 0, st, job, wq);
+
         } else if (v == kMatchStats) {
             unsigned long long z[4] = {0, 0, 0, 0}, r[4];
             (void)hipMemcpyToSymbol(HIP_SYMBOL(g_mstat), z, sizeof z);
