@@ -684,6 +684,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
                 mw14_walk<2, false, true>(E, p, B, nl, cfg, rf, rq, want_q);
 
 
+
             } else if (kVariant == kMatchProbeNoWalk) {
                 rf[p] = 0;                                  // probe: staging, sort and stores only
                 if (want_q) rq[p] = 0;
@@ -2202,6 +2203,7 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
             hipLaunchKernelGGL(k_match<kMatchProbeHalf>, grid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchProbeNoCmp) {
             hipLaunchKernelGGL(k_match<kMatchProbeNoCmp>, grid, dim3(kMatchThreads), 0, st, job, wq);
+
 
 
         } else if (v == kMatchStats) {
