@@ -138,6 +138,31 @@ def test_flush_random_vs_oracle(zg, oracle):
             assert rc == 0 and lens[i] == len(pre) and whole[:len(pre)] == pre, (tag, i)
 
 
+@pytest.mark.parametrize("level,strategy", [(6, 0), (9, 1), (4, 3), (2, 2), (1, 0)])
+def test_flush_many_calls(zg, oracle, level, strategy):
+    """Hundreds of flush calls on a multi-MiB stream: every job after the
+    first resumes at the last flush (levels 4..9, Z_HUFFMAN_ONLY, Z_RLE), so the
+    work stays linear; the stream is the oracle's."""
+    import time
+    L = _lib(zg)
+    n = (3 << 20) if level >= 4 or strategy else (1 << 20)
+    data = datagen.make("mix", n, 77 + level)
+    rng = np.random.default_rng(level)
+    calls, pos = [], 0
+    while pos < n:
+        take = int(min(n - pos, rng.integers(1, 12000)))
+        calls.append((take, int(rng.choice([0, 1, 2, 2, 5]))))
+        pos += take
+    calls.append((0, 4))
+    t0 = time.time()
+    sts, _, whole = replay(L, data, calls, level, 15, strategy)
+    took = time.time() - t0
+    rc, want = oracle.deflate_flushes(data, flush_events(calls), level, 1, strategy, finish=True)
+    assert rc == 0 and whole == want, (level, strategy, len(calls))
+    assert sts[-1] == 1
+    assert took < 60, took
+
+
 def test_flush_small_output_buffers(zg, flush_golden):
     """zpipe-style loops with small output buffers: a flush call that runs
     out of output before its marker completes it on the repeat call (no second

@@ -282,7 +282,8 @@ struct FlushSpec {
     const uint32_t *type;
     uint32_t n;
     int open_end;
-    uint64_t *mark_bits;
+    uint32_t start, bit0, byte0;   // a resumed job (DeflateJob::start/bit0/byte0)
+    uint64_t *out;                 // DeflateJob::flush_out
 };
 
 int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
@@ -411,7 +412,10 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.fl_type = fs->type;
             job.nfl = fs->n;
             job.open_end = fs->open_end;
-            job.mark_bits = fs->mark_bits;
+            job.start = fs->start;
+            job.bit0 = fs->bit0;
+            job.byte0 = fs->byte0;
+            job.flush_out = fs->out;
         }
         return job;
     };
@@ -490,7 +494,8 @@ struct FlushHost {
     const uint32_t *type;
     uint32_t n;
     int open_end;
-    uint64_t mark_bits;     // out: output bits before the last marker
+    uint32_t start, bit0, byte0;   // in: a resumed job (see DeflateJob)
+    uint64_t out[4];               // out: DeflateJob::flush_out
 };
 
 int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
@@ -507,7 +512,7 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
         dcap[i] = dst_len[i];
         out_total += (dst_len[i] + 15) & ~15ull;
     }
-    const size_t ev_bytes = fh ? 16ull * fh->n + 32 : 0;
+    const size_t ev_bytes = fh ? 16ull * fh->n + 64 : 0;
     const size_t meta_bytes = 8 * 4 * count + 16 * count + ev_bytes;
     if (!c.ws_io.ensure(in_total + 64) || !c.ws_io2.ensure(out_total + 64) ||
         !c.ws_small.ensure(meta_bytes + 64))
@@ -541,13 +546,13 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
                       hipMemcpyAsync(d_ft, fh->type, 4ull * fh->n, hipMemcpyHostToDevice, st) != hipSuccess))
             return ZGPU_MEM_ERROR;
         uint64_t *d_mb = d_fp + fh->n + (fh->n + 1) / 2;
-        if (hipMemsetAsync(d_mb, 0, 8, st) != hipSuccess) return ZGPU_MEM_ERROR;
-        fs = FlushSpec{d_fp, d_ft, fh->n, fh->open_end, d_mb};
+        if (hipMemsetAsync(d_mb, 0, 32, st) != hipSuccess) return ZGPU_MEM_ERROR;
+        fs = FlushSpec{d_fp, d_ft, fh->n, fh->open_end, fh->start, fh->bit0, fh->byte0, d_mb};
     }
     int rc = deflate_dev_locked(c, d_in, d_so, d_sl, d_out, d_do, d_dc, d_dl, d_st, (uint32_t)count,
                                 level, wrap, strategy, st, fh ? &fs : nullptr);
     if (rc) return rc;
-    if (fh && hipMemcpy(&fh->mark_bits, fs.mark_bits, 8, hipMemcpyDeviceToHost) != hipSuccess)
+    if (fh && hipMemcpy(fh->out, fs.out, 32, hipMemcpyDeviceToHost) != hipSuccess)
         return ZGPU_MEM_ERROR;
     std::vector<uint64_t> ol(count);
     std::vector<int32_t> os(count);
@@ -1037,7 +1042,18 @@ struct internal_state {
     std::vector<uint32_t> ev_type;
     size_t part_out = 0;            // bytes of the current part already queued
     bool marker_due = false;        // the last flush call ran out of output before its marker
-    uint32_t check = 0;             // adler32 / crc32 of the input before the current part
+    size_t in_base = 0;             // part position of in[0] (input behind the resume point is dropped)
+    uint32_t check = 0;             // adler32 / crc32 of the stream's input before ck_pos
+    size_t ck_pos = 0;              // part position the running check has reached
+    // resume point: the state right after the last flush acted on in this part.
+    // The next job compresses from there (its buffer starts at the window
+    // offset S, the parse at the flush, the output at its bit) instead of from
+    // the part start, so a stream with many flush calls costs linear work.
+    // Levels 1..3 keep exact hash chains sequentially (deflate_fast inserts
+    // selectively, deflate.c:1873-1897) and restart at the part start.
+    size_t res_S = 0, res_pos = 0, res_ev = 0;
+    uint64_t res_bits = 0;
+    uint32_t res_byte = 0;
     // inflate streams
     int inflating = 0;
     int wbits = 15;
@@ -1080,31 +1096,53 @@ int deflateInit_(z_streamp strm, int level, const char *version, int stream_size
 }
 
 namespace {
-// deflate(flush) calls: the prefix of the current part up to the flush
-// position, compressed with the part's flush calls as a raw stream that ends
-// open (complete bytes only); its first part_out bytes were queued before.
-int deflate_part(internal_state *s, int open_end, std::vector<uint8_t> &body, uint64_t *mark_bits = nullptr) {
-    const uint32_t nev = (uint32_t)s->ev_pos.size();
-    size_t cap = (size_t)compress_bound64(s->in.size()) + 64 + 16ull * nev;
+// deflate(flush) calls: the current part from its resume point up to the end
+// of the input given so far, compressed with the flush calls since then as a
+// raw stream; open_end: it stops after the last flush (complete bytes only).
+// body[0] is the part's output byte res_bits / 8; out as FlushHost::out.
+int deflate_part(internal_state *s, int open_end, std::vector<uint8_t> &body, uint64_t *out) {
+    const size_t base = s->res_S, nev = s->ev_pos.size() - s->res_ev;
+    std::vector<uint64_t> pos(nev + 1);
+    for (size_t i = 0; i < nev; i++) pos[i] = s->ev_pos[s->res_ev + i] - base;
+    const uint8_t *sp = s->in.data() + (base - s->in_base);
+    size_t sl = s->in_base + s->in.size() - base;
+    size_t cap = (size_t)compress_bound64(sl) + 64 + 16ull * nev;
     body.resize(cap);
-    const uint8_t *sp = s->in.data();
     uint8_t *dp = body.data();
-    size_t sl = s->in.size();
     int st = 0;
-    FlushHost fh{s->ev_pos.data(), s->ev_type.data(), nev, open_end};
+    FlushHost fh{pos.data(), s->ev_type.data() + s->res_ev, (uint32_t)nev, open_end, (uint32_t)(s->res_pos - base),
+                 (uint32_t)(s->res_bits & 7), s->res_byte & ((1u << (s->res_bits & 7)) - 1u), {0, 0, 0, 0}};
     Ctx &c = ctx();
     std::lock_guard<std::mutex> g(c.mu);
     int rc = init_locked(c);
-    if (!rc) rc = compress_host_locked(c, &sp, &sl, &dp, &cap, &st, 1, s->level, ZGPU_WRAP_RAW, s->strategy,
-                                       nev ? &fh : nullptr);
+    if (!rc) rc = compress_host_locked(c, &sp, &sl, &dp, &cap, &st, 1, s->level, ZGPU_WRAP_RAW, s->strategy, &fh);
     if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
     body.resize(cap);
-    if (mark_bits) *mark_bits = fh.mark_bits;
+    for (int i = 0; i < 4; i++) out[i] = fh.out[i];
     return Z_OK;
 }
 
-uint32_t stream_check(const internal_state *s, uint32_t init, const uint8_t *p, size_t n) {
-    return s->wrap == 2 ? (uint32_t)crc32_z(init, p, n) : (uint32_t)adler32_z(init, p, n);
+// the running Adler-32 / CRC-32 up to the end of the input given so far
+void advance_check(internal_state *s) {
+    const size_t end = s->in_base + s->in.size();
+    if (!s->wrap || s->ck_pos >= end) return;
+    const uint8_t *p = s->in.data() + (s->ck_pos - s->in_base);
+    const size_t n = end - s->ck_pos;
+    s->check = s->wrap == 2 ? (uint32_t)crc32_z(s->check, p, n) : (uint32_t)adler32_z(s->check, p, n);
+    s->ck_pos = end;
+}
+
+// a Z_FULL_FLUSH closes the part: the next starts with an empty window
+void close_part(internal_state *s) {
+    s->in.clear();
+    s->in_base = 0;
+    s->ck_pos = 0;
+    s->ev_pos.clear();
+    s->ev_type.clear();
+    s->part_out = 0;
+    s->res_S = s->res_pos = s->res_ev = 0;
+    s->res_bits = 0;
+    s->res_byte = 0;
 }
 
 void queue_header(internal_state *s) {                          // deflate.c:1002-1073
@@ -1148,29 +1186,41 @@ inline int flush_rank(int f) { return f * 2 - (f > 4 ? 9 : 0); }   // deflate.c:
 // (zlib.h: "avail_out is greater than six to avoid repeated flush markers").
 int emit_flush(z_streamp strm, internal_state *s, int flush) {
     std::vector<uint8_t> body;
-    uint64_t mb = 0;
-    if (int rc = deflate_part(s, 1, body, &mb)) return rc;
+    uint64_t o[4];
+    if (int rc = deflate_part(s, 1, body, o)) return rc;
     queue_header(s);
+    const size_t jb = (size_t)(s->res_bits >> 3);             // part byte of body[0]
     const uint64_t queued = strm->total_out + (s->out.size() - s->out_pos);
     const uint64_t cap = strm->total_out + strm->avail_out;
-    const size_t q_last = (size_t)(mb >> 3);                  // complete bytes before the marker
+    const size_t q_last = jb + (size_t)(o[0] >> 3);           // complete bytes before the marker
+    auto queue = [&](size_t to) {                              // part bytes [part_out, to)
+        s->out.insert(s->out.end(), body.begin() + (std::ptrdiff_t)(s->part_out - jb),
+                      body.begin() + (std::ptrdiff_t)(to - jb));
+        s->part_out = to;
+    };
     if (q_last > s->part_out && queued - s->part_out + q_last >= cap) {
-        s->out.insert(s->out.end(), body.begin() + (std::ptrdiff_t)s->part_out, body.begin() + (std::ptrdiff_t)q_last);
-        s->part_out = q_last;
+        queue(q_last);
         s->marker_due = true;
         drain(strm, s);
         s->last_flush = -1;
         return Z_OK;
     }
-    s->out.insert(s->out.end(), body.begin() + (std::ptrdiff_t)s->part_out, body.end());
-    s->part_out = body.size();
-    if (s->wrap) strm->adler = stream_check(s, s->check, s->in.data(), s->in.size());
-    if (flush == Z_FULL_FLUSH) {                                // the next part starts afresh
-        if (s->wrap) s->check = (uint32_t)strm->adler;
-        s->in.clear();
-        s->ev_pos.clear();
-        s->ev_type.clear();
-        s->part_out = 0;
+    queue(jb + body.size());
+    advance_check(s);
+    if (s->wrap) strm->adler = s->check;
+    if (flush == Z_FULL_FLUSH) {
+        close_part(s);
+    } else if (s->level >= 4 || s->strategy == Z_HUFFMAN_ONLY || s->strategy == Z_RLE) {
+        // the next job resumes here; the input before the window offset is not needed again
+        s->res_S += (size_t)o[2];
+        s->res_pos = s->ev_pos.back();
+        s->res_ev = s->ev_pos.size();
+        s->res_bits = ((uint64_t)jb << 3) + o[1];
+        s->res_byte = (uint32_t)o[3];
+        if (s->res_S > s->in_base) {
+            s->in.erase(s->in.begin(), s->in.begin() + (std::ptrdiff_t)(s->res_S - s->in_base));
+            s->in_base = s->res_S;
+        }
     }
     drain(strm, s);
     if (strm->avail_out == 0) s->last_flush = -1;
@@ -1219,7 +1269,7 @@ int deflate(z_streamp strm, int flush) {
     }
     if (is_flush) {
         s->flushed = true;
-        s->ev_pos.push_back(s->in.size());
+        s->ev_pos.push_back(s->in_base + s->in.size());
         s->ev_type.push_back((uint32_t)flush);
         return emit_flush(strm, s, flush);
     }
@@ -1237,11 +1287,14 @@ int deflate(z_streamp strm, int flush) {
             strm->adler = s->wrap == 2 ? crc32_z(0, sp, sl) : (s->wrap == 1 ? adler32_z(1, sp, sl) : 0);
         } else {
             std::vector<uint8_t> body;
-            if (int rc = deflate_part(s, 0, body)) return rc;
+            uint64_t o[4];
+            if (int rc = deflate_part(s, 0, body, o)) return rc;
             queue_header(s);
-            s->out.insert(s->out.end(), body.begin() + (std::ptrdiff_t)s->part_out, body.end());
+            const size_t jb = (size_t)(s->res_bits >> 3);
+            s->out.insert(s->out.end(), body.begin() + (std::ptrdiff_t)(s->part_out - jb), body.end());
             if (s->wrap) {
-                const uint32_t ck = stream_check(s, s->check, s->in.data(), s->in.size());
+                advance_check(s);
+                const uint32_t ck = s->check;
                 strm->adler = ck;
                 if (s->wrap == 1) {
                     for (int i = 3; i >= 0; i--) s->out.push_back((uint8_t)(ck >> (8 * i)));

@@ -827,13 +827,15 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
     po.sym = job.sym + job.ws_off[bi];
     po.blk = job.blocks + job.blk_off[bi];
     po.nsym = po.blk_nsym = po.blk_sym_start = po.nblk = 0;
-    po.block_start = 0; po.S = 0; po.E = 0;
-    uint32_t p = 0, match_start = 0, match_length = kMinMatch - 1;
+    // a resumed flush job starts at its last flush: window read up to there
+    // (E), nothing pending, a new block (deflate.c state after :2030-2042)
+    uint32_t p = job.start, match_start = 0, match_length = kMinMatch - 1;
+    po.block_start = p; po.S = 0; po.E = p;
     bool avail = false, done = false;
     FlushEv fe = flush_ev(job);
     uint32_t lim = (uint32_t)fe.limit(n);      // input deflate() has been given
 
-    uint32_t t0 = 0;
+    uint32_t t0 = p & ~15u;
     while (!done) {
         stage_words<64, kPT / 4 / 64>(s_rf, rf, t0, kPT, n, lane);
         if (use_q) stage_words<64, kPT / 4 / 64>(s_rq, rq, t0, kPT, n, lane);
@@ -854,6 +856,7 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
                         match_length = kMinMatch - 1;
                         if (po.blk_nsym) po.flush(p, false, lane);
                         po.marker(p, fe.kind(), lane);
+                        if (lane == 0 && job.flush_out) job.flush_out[2] = po.S;
                         fe.i++;
                         lim = (uint32_t)fe.limit(n);
                         continue;
@@ -1431,11 +1434,11 @@ __global__ __launch_bounds__(64) void k_parse_ev(DeflateJob job) {
     po.sym = job.sym + job.ws_off[bi];
     po.blk = job.blocks + job.blk_off[bi];
     po.nsym = po.blk_nsym = po.blk_sym_start = po.nblk = 0;
-    po.block_start = 0; po.S = 0; po.E = 0;
     po.lead = true;
+    int64_t p = job.start;                      // a resumed job: see k_parse_slow
+    po.block_start = p; po.S = 0; po.E = p;
     FlushEv fe = flush_ev(job);
     int64_t lim = fe.limit(n);
-    int64_t p = 0;
     for (;;) {
         if (rle ? po.E - p <= kMaxMatch : po.E == p) {
             po.fill(p, lim);
@@ -1443,6 +1446,7 @@ __global__ __launch_bounds__(64) void k_parse_ev(DeflateJob job) {
                 if (fe.at(p)) {
                     if (po.blk_nsym) po.flush(p, false);
                     po.marker(p, fe.kind());
+                    if (job.flush_out) job.flush_out[2] = (uint64_t)po.S;
                     fe.i++;
                     lim = fe.limit(n);
                     continue;
@@ -1915,7 +1919,8 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
     };
 
     if (tid == 0) {
-        s_obit = 0;
+        s_obit = job.bit0;                      // a resumed flush job: the partial byte's bits
+        stg[0] = job.byte0;
         if (job.wrap == 1) {                    // zlib header (deflate.c:1004-1037)
             uint32_t header = (8u + ((15u - 8u) << 4)) << 8;
             uint32_t flags = (job.strategy >= 2 || level < 2) ? 0u : level < 6 ? 1u : level == 6 ? 2u : 3u;
@@ -2034,7 +2039,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
                 if (s_obit - st.sbase + 128 > kStgBits) stg_flush(st, s_obit, false);
                 if (tid == 0) {
                     const uint32_t kind = blk_marker_kind(br.flags);
-                    if (job.mark_bits) job.mark_bits[bi] = (uint64_t)s_obit;
+                    if (job.flush_out) job.flush_out[0] = (uint64_t)s_obit;
                     if (kind == 1) {                    // _tr_align (trees.c:900-904)
                         put(1u << 1, 3);                // STATIC_TREES, not last
                         put(0, 7);                      // END_BLOCK in the static tree
@@ -2160,6 +2165,11 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
         }
     }
     __syncthreads();
+    if (tid == 0 && job.flush_out) {
+        const int64_t r = s_obit - st.sbase;
+        job.flush_out[1] = (uint64_t)s_obit;
+        job.flush_out[3] = (stg[r >> 5] >> (((r >> 3) & 3) * 8)) & 0xffu;
+    }
     stg_flush(st, s_obit, true);
     if (tid == 0) {
         const uint64_t total = (uint64_t)(s_obit >> 3);

@@ -118,7 +118,14 @@ struct DeflateJob {
     const uint32_t *fl_type;
     uint32_t nfl;
     int open_end;
-    uint64_t *mark_bits;     // [count] or null: output bits written before the last marker
+    // a resumed flush job (zgpu_api.cpp deflate_part): the buffer starts at the
+    // window offset S of the last flush acted on, the parse at that flush
+    // (`start`), and the output at bit `bit0` of a byte whose low bits are byte0
+    uint32_t start, bit0, byte0;
+    // flush jobs' results or null: [0] output bits before the last marker,
+    // [1] output bits at the end, [2] the window offset S at the last flush
+    // (buffer-relative), [3] the last, partial output byte
+    uint64_t *flush_out;
 };
 
 // ---- inflate ----
