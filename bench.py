@@ -381,7 +381,9 @@ def main():
                          "traffic": None if m_traffic is None else int(m_traffic),
                          "traffic_source": m_src,
                          "alg_bytes_per_launch": int(alg_per_launch),
-                         "avg_launch_ms": round(m_avg_ms, 3)},
+                         "avg_launch_ms": round(m_avg_ms, 3),
+                         "limiter": "not HBM: dependent LDS round trips of the chain walks and instruction "
+                                    "issue at the 16 waves/CU the 148.5 KiB LDS window allows (DESIGN.md 4.3)"},
             "stage_ms_per_step": {k: round(v[0] / max(1, a.steps), 2) for k, v in st.items()},
             "crc32": {"value": round(crc_total / crc_el / 1e9, 2), "unit": "GB/s",
                       "workload": f"C2: {a.crc_buffers} x {a.crc_bytes} B uniform random per GPU",
