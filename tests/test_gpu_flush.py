@@ -138,14 +138,14 @@ def test_flush_random_vs_oracle(zg, oracle):
             assert rc == 0 and lens[i] == len(pre) and whole[:len(pre)] == pre, (tag, i)
 
 
-@pytest.mark.parametrize("level,strategy", [(6, 0), (9, 1), (4, 3), (2, 2), (1, 0)])
+@pytest.mark.parametrize("level,strategy", [(6, 0), (9, 1), (4, 3), (2, 2), (1, 0), (3, 4)])
 def test_flush_many_calls(zg, oracle, level, strategy):
     """Hundreds of flush calls on a multi-MiB stream: every job after the
-    first resumes at the last flush (levels 4..9, Z_HUFFMAN_ONLY, Z_RLE), so the
-    work stays linear; the stream is the oracle's."""
+    first resumes at the last flush (levels 1..3 with their hash chains carried
+    over), so the work stays linear; the stream is the oracle's."""
     import time
     L = _lib(zg)
-    n = (3 << 20) if level >= 4 or strategy else (1 << 20)
+    n = 3 << 20
     data = datagen.make("mix", n, 77 + level)
     rng = np.random.default_rng(level)
     calls, pos = [], 0

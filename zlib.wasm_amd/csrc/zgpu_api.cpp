@@ -284,6 +284,11 @@ struct FlushSpec {
     int open_end;
     uint32_t start, bit0, byte0;   // a resumed job (DeflateJob::start/bit0/byte0)
     uint64_t *out;                 // DeflateJob::flush_out
+    // levels 1..3 resumed (host arrays): k_parse_fast's head[32768], rebased to
+    // the job's buffer, and the prev links of its positions [0, prev_n)
+    const uint32_t *head_in;
+    const uint16_t *prev_in;
+    size_t prev_n;
 };
 
 int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
@@ -384,6 +389,13 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
                           &c.ws_link2, &c.ws_rf2, &c.ws_rq2, &c.ws_state2})
             if (b->p && hipMemsetAsync(b->p, v & 0xff, b->cap, st) != hipSuccess) return ZGPU_MEM_ERROR;
         if (hipMemsetAsync(d_nblk, v & 0xff, 8ull * max_cnt, st) != hipSuccess) return ZGPU_MEM_ERROR;
+    }
+    if (fs && fs->head_in) {
+        if (!c.ws_heads.ensure(4ull * 32768) ||
+            hipMemcpyAsync(c.ws_heads.p, fs->head_in, 4ull * 32768, hipMemcpyHostToDevice, st) != hipSuccess ||
+            (fs->prev_n && hipMemcpyAsync(c.ws_link.p, fs->prev_in, 2ull * fs->prev_n, hipMemcpyHostToDevice, st) !=
+                               hipSuccess))
+            return ZGPU_MEM_ERROR;
     }
 
     StageTimer &T = c.timer;
@@ -496,6 +508,13 @@ struct FlushHost {
     int open_end;
     uint32_t start, bit0, byte0;   // in: a resumed job (see DeflateJob)
     uint64_t out[4];               // out: DeflateJob::flush_out
+    // levels 1..3 (see FlushSpec): the chains the job starts from, and where
+    // it leaves them: head[32768] and the prev links of [S, last flush), S = out[2]
+    const uint32_t *head_in = nullptr;
+    const uint16_t *prev_in = nullptr;
+    size_t prev_n = 0;
+    std::vector<uint32_t> *head_out = nullptr;
+    std::vector<uint16_t> *prev_out = nullptr;
 };
 
 int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
@@ -547,13 +566,23 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
             return ZGPU_MEM_ERROR;
         uint64_t *d_mb = d_fp + fh->n + (fh->n + 1) / 2;
         if (hipMemsetAsync(d_mb, 0, 32, st) != hipSuccess) return ZGPU_MEM_ERROR;
-        fs = FlushSpec{d_fp, d_ft, fh->n, fh->open_end, fh->start, fh->bit0, fh->byte0, d_mb};
+        fs = FlushSpec{d_fp, d_ft, fh->n, fh->open_end, fh->start, fh->bit0, fh->byte0, d_mb,
+                       fh->head_in, fh->prev_in, fh->prev_n};
     }
     int rc = deflate_dev_locked(c, d_in, d_so, d_sl, d_out, d_do, d_dc, d_dl, d_st, (uint32_t)count,
                                 level, wrap, strategy, st, fh ? &fs : nullptr);
     if (rc) return rc;
     if (fh && hipMemcpy(fh->out, fs.out, 32, hipMemcpyDeviceToHost) != hipSuccess)
         return ZGPU_MEM_ERROR;
+    if (fh && fh->head_out && fh->n) {
+        const uint64_t S = fh->out[2], end = fh->pos[fh->n - 1];
+        fh->head_out->resize(32768);
+        fh->prev_out->resize(end > S ? end - S : 0);
+        if (hipMemcpy(fh->head_out->data(), c.ws_heads.p, 4ull * 32768, hipMemcpyDeviceToHost) != hipSuccess ||
+            (end > S && hipMemcpy(fh->prev_out->data(), c.ws_link.as<uint16_t>() + S, 2 * (end - S),
+                                  hipMemcpyDeviceToHost) != hipSuccess))
+            return ZGPU_MEM_ERROR;
+    }
     std::vector<uint64_t> ol(count);
     std::vector<int32_t> os(count);
     if (hipMemcpy(ol.data(), d_dl, 8 * count, hipMemcpyDeviceToHost) != hipSuccess ||
@@ -1054,6 +1083,10 @@ struct internal_state {
     size_t res_S = 0, res_pos = 0, res_ev = 0;
     uint64_t res_bits = 0;
     uint32_t res_byte = 0;
+    // levels 1..3: k_parse_fast's hash chains at the resume point (head[] as
+    // part positions, prev links of [res_S, res_pos)) and as the last job left them
+    std::vector<uint32_t> fast_head, job_head;
+    std::vector<uint16_t> fast_prev, job_prev;
     // inflate streams
     int inflating = 0;
     int wbits = 15;
@@ -1112,6 +1145,18 @@ int deflate_part(internal_state *s, int open_end, std::vector<uint8_t> &body, ui
     int st = 0;
     FlushHost fh{pos.data(), s->ev_type.data() + s->res_ev, (uint32_t)nev, open_end, (uint32_t)(s->res_pos - base),
                  (uint32_t)(s->res_bits & 7), s->res_byte & ((1u << (s->res_bits & 7)) - 1u), {0, 0, 0, 0}};
+    std::vector<uint32_t> head_in;
+    if (s->level >= 1 && s->level <= 3 && s->strategy != Z_HUFFMAN_ONLY && s->strategy != Z_RLE) {
+        if (s->res_pos > base) {                               // rebase the saved chains to this buffer
+            head_in.resize(32768);
+            for (size_t i = 0; i < 32768; i++) head_in[i] = s->fast_head[i] > base ? s->fast_head[i] - (uint32_t)base : 0;
+            fh.head_in = head_in.data();
+            fh.prev_in = s->fast_prev.data();
+            fh.prev_n = s->fast_prev.size();
+        }
+        fh.head_out = &s->job_head;
+        fh.prev_out = &s->job_prev;
+    }
     Ctx &c = ctx();
     std::lock_guard<std::mutex> g(c.mu);
     int rc = init_locked(c);
@@ -1143,6 +1188,10 @@ void close_part(internal_state *s) {
     s->res_S = s->res_pos = s->res_ev = 0;
     s->res_bits = 0;
     s->res_byte = 0;
+    s->fast_head.clear();
+    s->fast_prev.clear();
+    s->job_head.clear();
+    s->job_prev.clear();
 }
 
 void queue_header(internal_state *s) {                          // deflate.c:1002-1073
@@ -1210,8 +1259,15 @@ int emit_flush(z_streamp strm, internal_state *s, int flush) {
     if (s->wrap) strm->adler = s->check;
     if (flush == Z_FULL_FLUSH) {
         close_part(s);
-    } else if (s->level >= 4 || s->strategy == Z_HUFFMAN_ONLY || s->strategy == Z_RLE) {
+    } else {
         // the next job resumes here; the input before the window offset is not needed again
+        if (!s->job_head.empty()) {                            // levels 1..3: keep the chains
+            const uint32_t base = (uint32_t)s->res_S;
+            s->fast_head.resize(32768);
+            for (size_t i = 0; i < 32768; i++) s->fast_head[i] = s->job_head[i] ? s->job_head[i] + base : 0;
+            s->fast_prev.swap(s->job_prev);
+            s->job_head.clear();
+        }
         s->res_S += (size_t)o[2];
         s->res_pos = s->ev_pos.back();
         s->res_ev = s->ev_pos.size();

@@ -1498,7 +1498,10 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     uint16_t *prev = job.link + job.ws_off[bi];
     uint32_t *head = heads + (size_t)bi * 32768;
     const LevelCfg cfg = c_ct.cfg[job.level];
-    for (int i = lane; i < 32768; i += 64) head[i] = 0;
+    // a resumed flush job (start > 0) finds head[] and prev[] as the last job
+    // left them, rebased to its buffer (zgpu_api.cpp deflate_part)
+    if (job.start == 0)
+        for (int i = lane; i < 32768; i += 64) head[i] = 0;
     __threadfence_block();
     __syncthreads();
 
@@ -1506,7 +1509,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     po.sym = job.sym + job.ws_off[bi];
     po.blk = job.blocks + job.blk_off[bi];
     po.nsym = po.blk_nsym = po.blk_sym_start = po.nblk = 0;
-    po.block_start = 0; po.S = 0; po.E = 0;
+    po.block_start = job.start; po.S = 0; po.E = job.start;
     po.lead = lead;
 
     // input window in registers: lane j holds in[wb + j] (w0) and in[wb + 64 + j]
@@ -1557,11 +1560,13 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         return maxcmp;
     };
 
-    int64_t p = 0, match_start = 0;
+    int64_t p = job.start, match_start = 0;
     uint32_t match_length = kMinMatch - 1;
     FlushEv fe = flush_ev(job);
     int64_t lim = fe.limit(n);                 // input deflate() has been given
-    int64_t pend = 0;                          // s->insert: strings a flush left unhashed
+    // s->insert: strings a flush left unhashed (a resumed job starts right
+    // after a flush at its window offset + start)
+    int64_t pend = p < kMinMatch - 1 ? p : kMinMatch - 1;
     for (;;) {
         if (po.E - p < kMinLookahead) {
             const bool reads = po.E < lim;
@@ -1584,6 +1589,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
                     pend = p - po.S < kMinMatch - 1 ? p - po.S : kMinMatch - 1;
                     if (po.blk_nsym) po.flush(p, false);
                     po.marker(p, fe.kind());
+                    if (lead && job.flush_out) job.flush_out[2] = (uint64_t)po.S;
                     fe.i++;
                     lim = fe.limit(n);
                     continue;
