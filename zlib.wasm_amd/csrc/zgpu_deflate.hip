@@ -468,7 +468,7 @@ __device__ __attribute__((always_inline)) inline int cmp16(const uint32_t *E, in
     return k;
 }
 
-template <int kUnroll, bool kBatch, bool kNoCmp = false>
+template <int kUnroll, bool kBatch, int kProbe = 0>
 __device__ __attribute__((always_inline)) inline bool mw14_loop(MW3 &w, uint32_t &em, uint32_t &eb,
                                                                 const Scan16 &S, const uint32_t *E, uint32_t end) {
     const char *Eb = reinterpret_cast<const char *>(E);
@@ -479,12 +479,14 @@ __device__ __attribute__((always_inline)) inline bool mw14_loop(MW3 &w, uint32_t
         const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + a);
         uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
         const uint32_t miss = ((em >> 16) ^ w.scan01) | ((eb >> 16) ^ w.scanE);
-        if (!kNoCmp && __builtin_expect(miss == 0, 0)) {
+        if (kProbe != 1 && __builtin_expect(miss == 0, 0)) {
             w.ncmp++;
             const int m = w.m4 >> 2, s = w.s4 >> 2;
             const int k = cmp16<kBatch>(E, m, s, S, w.maxcmp);
             const int len = k < w.maxcmp ? k : w.maxcmp;
-            if (len > w.best) {
+            if (kProbe == 2) {
+                w.ncmp += (uint32_t)len;             // probe 38: compare, keep nothing
+            } else if (len > w.best) {
                 w.best = len;
                 w.bpos4 = w.m4;
                 if (len >= w.nice) w.limit4 = 0x7fffffff;
@@ -502,7 +504,7 @@ __device__ __attribute__((always_inline)) inline bool mw14_loop(MW3 &w, uint32_t
     }
 }
 
-template <int kUnroll, bool kBatch, bool kNoCmp = false>
+template <int kUnroll, bool kBatch, int kProbe = 0>
 __device__ __attribute__((always_inline)) inline void mw14_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
                                                                 const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
                                                                 int want_q, uint32_t *st_steps = nullptr,
@@ -534,13 +536,13 @@ __device__ __attribute__((always_inline)) inline void mw14_walk(const uint32_t *
     uint32_t em = E[s - (int)d0];
     uint32_t eb = E[s - (int)d0 + 1];
     const uint32_t qc = want_q ? (uint32_t)(cfg.chain >> 2) : (uint32_t)cfg.chain;
-    const bool done = mw14_loop<kUnroll, kBatch, kNoCmp>(w, em, eb, S, E, qc);
+    const bool done = mw14_loop<kUnroll, kBatch, kProbe>(w, em, eb, S, E, qc);
     if (want_q) {
         rq[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
-        if (!done) mw14_loop<kUnroll, kBatch, kNoCmp>(w, em, eb, S, E, (uint32_t)cfg.chain);
+        if (!done) mw14_loop<kUnroll, kBatch, kProbe>(w, em, eb, S, E, (uint32_t)cfg.chain);
     }
     rf[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
-    if (kNoCmp) rf[p] = (w.count ^ (uint32_t)w.m4) == 0x7fffffffu ? 1u : 0u;   // probe: keep the walk live
+    if (kProbe) rf[p] = (w.count ^ (uint32_t)w.m4 ^ w.ncmp) == 0x7fffffffu ? 1u : 0u;   // probe: keep the walk live
     if (st_steps) { *st_steps = w.count; *st_cmp = w.ncmp; }
 }
 
@@ -554,6 +556,12 @@ __device__ unsigned long long g_mstat[4];   // kMatchStats statistics
 //   14            positions in index order (no keys)
 //   21            19 plus statistics (lane steps, compares, walks, wave
 //                 iterations) printed after each launch
+//   38            timing probe (wrong results): 37 plus every compare done
+//                 and its length discarded (best, nice and the quick-reject
+//                 offset stay as in 37, so nearly every same-hash candidate
+//                 passes the quick reject): 1624 ms -- with most lanes
+//                 comparing together a compare costs ~1/3 of what a lone
+//                 lane's compare costs its wave
 //   37            timing probe (wrong results): walks without compares (every
 //                 quick-reject pass ignored, so no walk stops at nice): 127 ms
 //                 of 355 per 4 GiB at L6 -- the compares, 3.4 % of the steps,
@@ -564,7 +572,7 @@ __device__ unsigned long long g_mstat[4];   // kMatchStats statistics
 //                 waves walk (1.6x slower at L6, 1.8x at L9: the walks are
 //                 latency-bound at the 16 waves the LDS window allows)
 constexpr int kMatchDefault = 19, kMatchStats = 21, kMatchProbeNoWalk = 33, kMatchProbeHalf = 35,
-              kMatchProbeNoCmp = 37;
+              kMatchProbeNoCmp = 37, kMatchProbeCmpOnly = 38;
 
 __device__ inline uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
@@ -681,7 +689,9 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
                 st_walks += steps ? 1u : 0u;
                 if ((tid & 63) == __builtin_ctzll(__ballot(1))) st_wave_iters += mx;
             } else if (kVariant == kMatchProbeNoCmp) {
-                mw14_walk<2, false, true>(E, p, B, nl, cfg, rf, rq, want_q);
+                mw14_walk<2, false, 1>(E, p, B, nl, cfg, rf, rq, want_q);
+            } else if (kVariant == kMatchProbeCmpOnly) {
+                mw14_walk<2, false, 2>(E, p, B, nl, cfg, rf, rq, want_q);
 
 
 
@@ -2196,7 +2206,7 @@ static int match_variant() {
         const char *e = getenv("ZGPU_MATCH_VARIANT");
         const int x = e ? atoi(e) : kMatchDefault;
         return (x == 14 || x == kMatchStats || x == kMatchProbeNoWalk || x == kMatchProbeHalf ||
-                x == kMatchProbeNoCmp) ? x : kMatchDefault;
+                x == kMatchProbeNoCmp || x == kMatchProbeCmpOnly) ? x : kMatchDefault;
     }();
     return v;
 }
@@ -2219,6 +2229,8 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
             hipLaunchKernelGGL(k_match<kMatchProbeHalf>, grid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchProbeNoCmp) {
             hipLaunchKernelGGL(k_match<kMatchProbeNoCmp>, grid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchProbeCmpOnly) {
+            hipLaunchKernelGGL(k_match<kMatchProbeCmpOnly>, grid, dim3(kMatchThreads), 0, st, job, wq);
 
 
 
