@@ -1498,6 +1498,9 @@ __global__ __launch_bounds__(64) void k_parse_ev(DeflateJob job) {
 // candidate 64 bytes per memory round trip, one byte per lane, with the next
 // link loaded in the same round trip.
 // ------------------------------------------------------------------------
+// kEv: a flush job (events, a resumed start, late hashing); batch jobs run
+// the <false> instance, whose loop carries none of that
+template <bool kEv>
 __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *heads) {
     const int lane = threadIdx.x;
     const bool lead = lane == 0;
@@ -1510,7 +1513,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     const LevelCfg cfg = c_ct.cfg[job.level];
     // a resumed flush job (start > 0) finds head[] and prev[] as the last job
     // left them, rebased to its buffer (zgpu_api.cpp deflate_part)
-    if (job.start == 0)
+    if (!kEv || job.start == 0)
         for (int i = lane; i < 32768; i += 64) head[i] = 0;
     __threadfence_block();
     __syncthreads();
@@ -1519,7 +1522,8 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     po.sym = job.sym + job.ws_off[bi];
     po.blk = job.blocks + job.blk_off[bi];
     po.nsym = po.blk_nsym = po.blk_sym_start = po.nblk = 0;
-    po.block_start = job.start; po.S = 0; po.E = job.start;
+    const int64_t start = kEv ? (int64_t)job.start : 0;
+    po.block_start = start; po.S = 0; po.E = start;
     po.lead = lead;
 
     // input window in registers: lane j holds in[wb + j] (w0) and in[wb + 64 + j]
@@ -1570,16 +1574,16 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         return maxcmp;
     };
 
-    int64_t p = job.start, match_start = 0;
+    int64_t p = start, match_start = 0;
     uint32_t match_length = kMinMatch - 1;
     FlushEv fe = flush_ev(job);
-    int64_t lim = fe.limit(n);                 // input deflate() has been given
+    int64_t lim = kEv ? fe.limit(n) : n;       // input deflate() has been given
     // s->insert: strings a flush left unhashed (a resumed job starts right
     // after a flush at its window offset + start)
     int64_t pend = p < kMinMatch - 1 ? p : kMinMatch - 1;
     for (;;) {
         if (po.E - p < kMinLookahead) {
-            const bool reads = po.E < lim;
+            const bool reads = kEv && po.E < lim;
             po.fill(p, lim);
             // fill_window hashes the strings the last flush left unhashed once
             // new input is read (deflate.c:318-335)
@@ -1594,7 +1598,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
                 }
             }
             if (po.E == p) {
-                if (fe.at(p)) {
+                if (kEv && fe.at(p)) {
                     // a deflate(flush) call ends here (deflate.c:1903-1914, :1211-1233)
                     pend = p - po.S < kMinMatch - 1 ? p - po.S : kMinMatch - 1;
                     if (po.blk_nsym) po.flush(p, false);
@@ -1675,7 +1679,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         }
         if (bflush) po.flush(p, false);
     }
-    if (!job.open_end) po.flush(p, true);
+    if (!kEv || !job.open_end) po.flush(p, true);
     if (lead) job.nblocks[bi] = po.nblk;
 }
 
@@ -2252,7 +2256,10 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     case 2: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 0); break;
     case 5: hipLaunchKernelGGL(k_parse_seg, grid, dim3(kParseLanes), 0, st, job); break;
     case 6: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 1); break;
-    case 3: hipLaunchKernelGGL(k_parse_fast, grid, dim3(64), 0, st, job, heads); break;
+    case 3:
+        if (job.nfl || job.start) hipLaunchKernelGGL(k_parse_fast<true>, grid, dim3(64), 0, st, job, heads);
+        else hipLaunchKernelGGL(k_parse_fast<false>, grid, dim3(64), 0, st, job, heads);
+        break;
     case 4: hipLaunchKernelGGL(k_encode, grid, dim3(kEncThreads), 0, st, job); break;
     case 7: hipLaunchKernelGGL(k_parse_huff, grid, dim3(kHuffThreads), 0, st, job); break;
     case 8: hipLaunchKernelGGL(k_parse_rle, grid, dim3(64), 0, st, job); break;
