@@ -608,7 +608,7 @@ __device__ inline int64_t flush_limit(const DeflateJob &job, int64_t p, int64_t 
     return lo < job.nfl ? (int64_t)job.fl_pos[lo] : n;
 }
 
-template <int kVariant>
+template <int kVariant, bool kEv = false>
 __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int want_q) {
     constexpr bool kSorted = kVariant != 14;
     constexpr int kSortBuckets = 64;
@@ -677,7 +677,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
             const int64_t p = ts + (kSorted ? (int)s_perm[i] : i);
             // a flush job's search at p sees the input up to the next flush
             // position only (nice and the compare length are clamped to it)
-            const int64_t nl = job.nfl ? flush_limit(job, p, n) : n;
+            const int64_t nl = kEv ? flush_limit(job, p, n) : n;
             if (kVariant == kMatchStats) {
                 uint32_t steps = 0, cmps = 0;
                 mw14_walk<2, false>(E, p, B, nl, cfg, rf, rq, want_q, &steps, &cmps);
@@ -2225,7 +2225,9 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     case 1: {
         const int wq = (int)(job.level >= 5);
         const int v = match_variant();
-        if (v == 14) {
+        if (job.nfl) {                                          // a flush job (zgpu_api.cpp deflate())
+            hipLaunchKernelGGL((k_match<kMatchDefault, true>), grid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == 14) {
             hipLaunchKernelGGL(k_match<14>, grid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchProbeNoWalk) {
             hipLaunchKernelGGL(k_match<kMatchProbeNoWalk>, grid, dim3(kMatchThreads), 0, st, job, wq);
