@@ -100,6 +100,9 @@ int deflateInit2_(z_streamp strm, int level, int method, int windowBits,
 int deflate(z_streamp strm, int flush);                                 /* zlib.h:254 */
 int deflateEnd(z_streamp strm);                                         /* zlib.h:367 */
 uLong deflateBound(z_streamp strm, uLong sourceLen);                    /* zlib.h:694 */
+int deflateReset(z_streamp strm);                                       /* zlib.h:621 */
+int deflateCopy(z_streamp dest, z_streamp source);                      /* zlib.h:603 */
+int deflatePending(z_streamp strm, unsigned *pending, int *bits);       /* zlib.h:746 */
 int compress(Bytef *dest, uLongf *destLen, const Bytef *source,
              uLong sourceLen);                                          /* zlib.h:1251 */
 int compress2(Bytef *dest, uLongf *destLen, const Bytef *source,

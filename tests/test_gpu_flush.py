@@ -212,3 +212,75 @@ def test_flush_level0_and_errors(zg):
     assert L.deflate(C.byref(s), 3) == 0           # higher rank: acted on
     assert s.total_out == n1 + 5
     assert L.deflateEnd(C.byref(s)) == 0
+
+
+def test_wasm_stream_api_flushes(zg, oracle):
+    """The WASM front end's streaming names (src/wasm_module.c:168-215) pass
+    the flush value through to deflate(): flush calls included, the stream is
+    the oracle's."""
+    L = zg.load()
+    L.zlib_deflate_init.restype = C.c_void_p
+    L.zlib_deflate_init.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int]
+    L.zlib_deflate_process.restype = C.c_int
+    L.zlib_deflate_process.argtypes = [C.c_void_p, C.c_void_p, C.c_uint, C.c_void_p, C.c_uint, C.c_int]
+    L.zlib_deflate_end.argtypes = [C.c_void_p]
+    L.zlib_stream_total_out.restype = C.c_ulong
+    L.zlib_stream_total_out.argtypes = [C.c_void_p]
+    data = bytes(datagen.make("text", 200000, 5))
+    calls = [(50000, 2), (0, 1), (70000, 0), (30000, 5), (50000, 3), (0, 2), (0, 4)]
+    h = L.zlib_deflate_init(6, 15, 8, 0)
+    assert h
+    inbuf = C.create_string_buffer(data, len(data))
+    out = bytearray()
+    obuf = C.create_string_buffer(1 << 20)
+    pos = 0
+    for take, flush in calls:
+        rc = L.zlib_deflate_process(h, C.addressof(inbuf) + pos, take, obuf, len(obuf), flush)
+        pos += take
+        assert rc in (0, 1, -5), (take, flush, rc)
+        out += obuf.raw[:L.zlib_stream_total_out(h) - len(out)]   # each call writes from the buffer start
+    L.zlib_deflate_end(C.c_void_p(h))
+    rc, want = oracle.deflate_flushes(data, flush_events(calls), 6, 1, 0, finish=True)
+    assert rc == 0 and bytes(out) == want
+
+
+def test_deflate_reset_copy_pending(zg, oracle):
+    L = _lib(zg)
+    L.deflateReset.argtypes = [C.POINTER(ZStream)]
+    L.deflateCopy.argtypes = [C.POINTER(ZStream), C.POINTER(ZStream)]
+    L.deflatePending.argtypes = [C.POINTER(ZStream), C.POINTER(C.c_uint), C.POINTER(C.c_int)]
+    data = bytes(datagen.make("mix", 150000, 8))
+    inbuf = C.create_string_buffer(data, len(data))
+    cap = 2 * len(data) + 4096
+
+    def run(s, start, calls):
+        out, pos = bytearray(), start
+        buf = C.create_string_buffer(cap)
+        for take, flush in calls:
+            s.next_in, s.avail_in = C.addressof(inbuf) + pos, take
+            s.next_out, s.avail_out = C.addressof(buf), cap
+            L.deflate(C.byref(s), flush)
+            out += buf.raw[:cap - s.avail_out]
+            pos += take
+        return bytes(out)
+
+    s = ZStream()
+    assert L.deflateInit2_(C.byref(s), 6, 8, 15, 8, 0, VERSION, C.sizeof(ZStream)) == 0
+    head = run(s, 0, [(60000, 1)])                       # Z_PARTIAL_FLUSH: a partial byte stays
+    pend, bits = C.c_uint(99), C.c_int(99)
+    assert L.deflatePending(C.byref(s), C.byref(pend), C.byref(bits)) == 0
+    assert pend.value == 0 and 0 <= bits.value < 8
+    t = ZStream()
+    assert L.deflateCopy(C.byref(t), C.byref(s)) == 0
+    tail_s = run(s, 60000, [(90000, 4)])
+    tail_t = run(t, 60000, [(90000, 4)])
+    assert tail_s == tail_t
+    rc, want = oracle.deflate_flushes(data, [(60000, 1)], 6, 1, 0, finish=True)
+    assert rc == 0 and head + tail_s == want
+    assert L.deflateEnd(C.byref(t)) == 0
+    # deflateReset: the same stream object compresses afresh
+    assert L.deflateReset(C.byref(s)) == 0
+    assert s.total_in == 0 and s.total_out == 0
+    again = run(s, 0, [(150000, 4)])
+    assert again == oracle.compress(data, 6)[1]
+    assert L.deflateEnd(C.byref(s)) == 0

@@ -1370,6 +1370,44 @@ int deflate(z_streamp strm, int flush) {
     return s->out_pos == s->out.size() ? Z_STREAM_END : Z_OK;
 }
 
+int deflateReset(z_streamp strm) {                              // deflate.c:560-620
+    if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    const int level = s->level, wrap = s->wrap, strategy = s->strategy;
+    *s = internal_state();
+    s->level = level;
+    s->wrap = wrap;
+    s->strategy = strategy;
+    s->out_pos = 0;
+    s->finished = 0;
+    s->check = wrap == 2 ? 0 : 1;
+    strm->total_in = strm->total_out = 0;
+    strm->msg = nullptr;
+    strm->data_type = Z_UNKNOWN;
+    strm->adler = wrap == 2 ? 0 : 1;
+    return Z_OK;
+}
+
+int deflateCopy(z_streamp dest, z_streamp source) {             // deflate.c:1270-1311
+    if (!dest || !source || !source->state || source->state->inflating) return Z_STREAM_ERROR;
+    internal_state *s = new (std::nothrow) internal_state(*source->state);
+    if (!s) return Z_MEM_ERROR;
+    *dest = *source;
+    dest->state = s;
+    return Z_OK;
+}
+
+// Bytes generated and not yet handed out; bits: those of a partial last byte
+// after a Z_PARTIAL_FLUSH / Z_BLOCK (deflate.c:739-747).  Output of Z_NO_FLUSH
+// calls is deferred here, so it is not counted until a flush or Z_FINISH.
+int deflatePending(z_streamp strm, unsigned *pending, int *bits) {
+    if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    if (pending) *pending = (unsigned)(s->out.size() - s->out_pos);
+    if (bits) *bits = s->finished ? 0 : (int)(s->res_bits & 7);
+    return Z_OK;
+}
+
 int deflateEnd(z_streamp strm) {
     if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
     delete strm->state;

@@ -42,7 +42,7 @@ EXPORTED_SYMBOLS = (
     "zgpu_stage_timing_read", "zgpu_inflate_batch_dev", "zgpu_uncompress_batch",
     # include/zgpu_zlib.h
     "zlibVersion", "compress", "compress2", "compressBound", "deflateInit_",
-    "deflateInit2_", "deflate", "deflateEnd", "deflateBound", "crc32", "crc32_z",
+    "deflateInit2_", "deflate", "deflateEnd", "deflateBound", "deflateReset", "deflateCopy", "deflatePending", "crc32", "crc32_z",
     "crc32_combine", "crc32_combine64", "crc32_combine_gen", "crc32_combine_gen64",
     "crc32_combine_op", "adler32", "adler32_z", "adler32_combine", "adler32_combine64",
     "uncompress", "uncompress2", "inflateInit_", "inflateInit2_", "inflate", "inflateEnd",
