@@ -1074,3 +1074,110 @@ int zo_deflate_flushes(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t
     if (!finish && (nf == 0 || fpos[nf - 1] != n)) return ZO_STREAM_ERROR;
     return compress_events(dst, dst_len, src, n, level, wrap, 0, strategy, fpos, ftype, nf, finish);
 }
+
+/* ------------------------------------------------------------------------ */
+/* level 0 driven by deflate() calls (deflate.c:763-1265 over deflate_stored, */
+/* :1635-1815) with an output buffer that always holds a call's output: the  */
+/* first loop of deflate_stored copies stored blocks of up to MAX_STORED     */
+/* bytes straight from the window and the input -- a Z_NO_FLUSH call only    */
+/* while a block of at least min_block (= w_size, 32768) is available, any   */
+/* other call everything; what a Z_NO_FLUSH call leaves (< 32768 bytes) waits */
+/* in the window.  Then deflate()'s markers (block_done) and the trailer.     */
+/* ------------------------------------------------------------------------ */
+static void stored_block(bw_t *w, const uint8_t *a, size_t na, const uint8_t *b, size_t nb, int last) {
+    const size_t len = na + nb;                                  /* _tr_stored_block, trees.c:863-876 */
+    bw_bits(w, (unsigned)last, 3);
+    bw_align(w);
+    bw_byte(w, (uint8_t)len);
+    bw_byte(w, (uint8_t)(len >> 8));
+    bw_byte(w, (uint8_t)~len);
+    bw_byte(w, (uint8_t)(~len >> 8));
+    for (size_t i = 0; i < na; i++) bw_byte(w, a[i]);
+    for (size_t i = 0; i < nb; i++) bw_byte(w, b[i]);
+}
+
+int zo_deflate_stored_calls(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n, int wrap,
+                            const size_t *take, const int *flush, int ncalls, int *status, size_t *out_len) {
+    init_tables();
+    if (!dst || !dst_len || wrap < 0 || wrap > 2 || (n && !src)) return ZO_STREAM_ERROR;
+    bw_t w = {0};
+    /* header (deflate.c:1002-1073): level 0 -> FLEVEL 0 / XFL 4 */
+    uint8_t hdr[10];
+    size_t hlen = 0;
+    if (wrap == 1) {
+        unsigned h = (8u + ((15u - 8u) << 4)) << 8;
+        h += 31 - (h % 31);
+        hdr[0] = (uint8_t)(h >> 8); hdr[1] = (uint8_t)h; hlen = 2;
+    } else if (wrap == 2) {
+        static const uint8_t g[10] = {31, 139, 8, 0, 0, 0, 0, 0, 4, 3};
+        memcpy(hdr, g, 10); hlen = 10;
+    }
+    size_t pos = 0, buf = 0;            /* input consumed; bytes of it still in the window */
+    int last_flush = -2, finished = 0, rc = ZO_OK;
+    for (int i = 0; i < ncalls; i++) {
+        const int f = flush[i];
+        size_t avail = take[i];
+        if (pos + avail > n || f < 0 || f > 5) { rc = ZO_STREAM_ERROR; break; }
+        int st = ZO_OK;
+        const int old = last_flush;
+        last_flush = f;
+        if (finished && f != 4) st = ZO_STREAM_ERROR;              /* :976-979 */
+        else if (avail == 0 && (f * 2 - (f > 4 ? 9 : 0)) <= (old * 2 - (old > 4 ? 9 : 0)) && f != 4)
+            st = ZO_BUF_ERROR;                                     /* :1002-1005 */
+        else if (finished && avail) st = ZO_BUF_ERROR;
+        else if (!finished) {
+            size_t total = buf + avail;
+            int last = 0;
+            const uint8_t *wb = src + pos - buf;                   /* window bytes not yet sent */
+            for (;;) {                                             /* :1652-1725 */
+                const size_t len = total < MAX_STORED ? total : MAX_STORED;
+                if (len < 32768 && ((len == 0 && f != 4) || f == 0)) break;
+                last = f == 4 && len == total;
+                stored_block(&w, wb, len, NULL, 0, last);
+                wb += len;
+                total -= len;
+                if (last) break;
+            }
+            pos += avail;
+            buf = total;
+            if (last) {                                            /* finish_done: trailer */
+                finished = 1;
+                st = 1;                                            /* Z_STREAM_END */
+            } else if (f != 0 && f != 4 && buf == 0) {             /* block_done: :1211-1233 */
+                if (f == 1) { bw_bits(&w, 1u << 1, 3); bw_bits(&w, 0, 7); }
+                else if (f == 2 || f == 3) {
+                    bw_bits(&w, 0, 3); bw_align(&w);
+                    bw_byte(&w, 0); bw_byte(&w, 0); bw_byte(&w, 0xff); bw_byte(&w, 0xff);
+                }
+            }
+        } else {
+            st = 1;                                                /* repeated Z_FINISH */
+        }
+        if (status) status[i] = st;
+        if (out_len) out_len[i] = hlen + w.len + (finished ? (wrap == 1 ? 4 : wrap == 2 ? 8 : 0) : 0);
+    }
+    if (rc == ZO_OK && w.oom) rc = ZO_MEM_ERROR;
+    if (rc == ZO_OK) {
+        uint8_t trl[8];
+        size_t tlen = 0;
+        if (finished && wrap == 1) {
+            const uint32_t a = zo_adler32(1, src, pos);
+            trl[0] = (uint8_t)(a >> 24); trl[1] = (uint8_t)(a >> 16); trl[2] = (uint8_t)(a >> 8); trl[3] = (uint8_t)a;
+            tlen = 4;
+        } else if (finished && wrap == 2) {
+            const uint32_t c = zo_crc32(0, src, pos);
+            for (int k = 0; k < 4; k++) trl[k] = (uint8_t)(c >> (8 * k));
+            for (int k = 0; k < 4; k++) trl[4 + k] = (uint8_t)((uint32_t)pos >> (8 * k));
+            tlen = 8;
+        }
+        size_t k = 0;
+        const size_t cap = *dst_len;
+        for (size_t j = 0; j < hlen && k < cap; j++) dst[k++] = hdr[j];
+        for (size_t j = 0; j < w.len && k < cap; j++) dst[k++] = w.buf[j];
+        for (size_t j = 0; j < tlen && k < cap; j++) dst[k++] = trl[j];
+        if (hlen + w.len + tlen > cap) rc = ZO_BUF_ERROR;
+        *dst_len = k;
+    }
+    free(w.buf);
+    return rc;
+}

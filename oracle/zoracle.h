@@ -73,6 +73,11 @@ int zo_pp_compress2(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n,
 int zo_deflate_flushes(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n, int level,
                        int wrap, int strategy, const size_t *fpos, const int *ftype, int nf,
                        int finish);
+/* level 0 over a deflate() call sequence (take[i] input bytes, flush[i]), each
+ * call's output space large enough: the whole stream, and per call the status
+ * and the total output length after it (deflate.c:763-1265, :1635-1815) */
+int zo_deflate_stored_calls(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t n, int wrap,
+                            const size_t *take, const int *flush, int ncalls, int *status, size_t *out_len);
 /* ---- the a18 helper kernels (src/zlib_simd_optimized.c:27,74,210,296) with
  * zlib-correct semantics: slide_hash (deflate.c:187-209), a 256-byte common
  * prefix, longest_match over a caller's window/prev (deflate.c:1356-1497, nice

@@ -289,3 +289,45 @@ def test_oracle_flush_golden(oracle):
             rc, part = oracle.deflate_flushes(data[:pos], flush_events(calls[:i + 1]), c["level"], wrap,
                                               c["strategy"], finish=False)
             assert rc == 0 and part == got[:c["out_len"][i]], (c["seed"], i)
+
+
+def test_oracle_stored_calls_golden(oracle):
+    """zo_deflate_stored_calls (level 0 over deflate() calls) against the
+    reference's call sequences frozen in tests/golden/stored_golden.json:
+    status and output length after every call, and the stream."""
+    import json
+    import os as _os
+    with open(_os.path.join(_os.path.dirname(__file__), "golden", "stored_golden.json")) as f:
+        cases = json.load(f)["cases"]
+    for c in cases:
+        data = datagen.make(c["kind"], c["n"], c["seed"])
+        assert hashlib.sha256(data).hexdigest() == c["input_sha256"]
+        calls = [tuple(x) for x in c["calls"]]
+        wrap = {15: 1, -15: 0, 31: 2}[c["wbits"]]
+        rc, sts, lens, got = oracle.deflate_stored_calls(data, calls, wrap)
+        assert rc == 0 and sts == c["status"] and lens == c["out_len"], c["seed"]
+        assert len(got) == c["len"] and hashlib.sha256(got).hexdigest() == c["sha256"], c["seed"]
+
+
+@pytest.mark.skipif(not reference_available(), reason="compiled reference not built (build container only)")
+def test_oracle_stored_calls_vs_reference(oracle):
+    """Random level-0 call sequences through the compiled reference."""
+    import os as _os
+    from zhelpers import Reference
+    ref = Reference()
+    rng = np.random.default_rng(int(_os.environ.get("ZO_STORED_SEED", "3")))
+    for t in range(int(_os.environ.get("ZO_STORED_CASES", "60"))):
+        n = int(rng.choice([0, 1, 5, 1000, 40000, 70000, 200000]))
+        data = datagen.make(["text", "mix", "runs", "random"][t % 4], n, 100 + t)
+        calls, pos = [], 0
+        while pos < n:
+            take = int(min(n - pos, rng.choice([0, 1, 17, 4000, 32767, 32768, 65535, 65536, 140000])))
+            calls.append((take, int(rng.choice([0, 0, 0, 1, 2, 3, 5]))))
+            pos += take
+            if rng.random() < 0.15:
+                calls.append((0, int(rng.choice([0, 1, 2, 3, 5]))))
+        calls.append((0, 4))
+        wb = int(rng.choice([15, -15, 31]))
+        sts, lens, whole = ref.deflate_calls(data, calls, 0, wb, 0)
+        rc, osts, olens, got = oracle.deflate_stored_calls(data, calls, {15: 1, -15: 0, 31: 2}[wb])
+        assert rc == 0 and osts == sts and olens == lens and got == whole, (t, n, wb)

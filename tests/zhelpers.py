@@ -51,6 +51,10 @@ class Oracle:
         L.zo_deflate_flushes.argtypes = [C.c_void_p, C.POINTER(C.c_size_t), C.c_void_p, C.c_size_t,
                                          C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
                                          C.c_int]
+        L.zo_deflate_stored_calls.restype = C.c_int
+        L.zo_deflate_stored_calls.argtypes = [C.c_void_p, C.POINTER(C.c_size_t), C.c_void_p, C.c_size_t,
+                                              C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
+                                              C.c_void_p]
         L.zo_pp_links.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
         L.zo_pp_match.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_void_p,
                                   C.c_void_p, C.c_void_p]
@@ -70,6 +74,21 @@ class Oracle:
             return self._compress(lambda o, n, d, ln, lv, w: self.L.zo_compress2(o, n, d, ln, lv, w, strategy),
                                   data, level, wrap, cap)
         return self._compress(self.L.zo_compress, data, level, wrap, cap)
+
+    def deflate_stored_calls(self, data, calls, wrap=1):
+        """zo_deflate_stored_calls: level 0 over [(input_len, flush)] ->
+        (rc, statuses, output length after each call, stream)."""
+        data = bytes(data)
+        nc = len(calls)
+        take = (C.c_size_t * max(nc, 1))(*[c[0] for c in calls])
+        fl = (C.c_int * max(nc, 1))(*[c[1] for c in calls])
+        st = (C.c_int * max(nc, 1))()
+        ol = (C.c_size_t * max(nc, 1))()
+        cap = compress_bound(len(data)) + 64 + 16 * nc
+        out = C.create_string_buffer(cap)
+        n = C.c_size_t(cap)
+        rc = self.L.zo_deflate_stored_calls(out, C.byref(n), data, len(data), wrap, take, fl, nc, st, ol)
+        return rc, list(st[:nc]), list(ol[:nc]), out.raw[: n.value]
 
     def deflate_flushes(self, data, events, level=6, wrap=1, strategy=0, finish=True):
         """zo_deflate_flushes: (rc, stream) for flush events [(pos, flush)]."""
