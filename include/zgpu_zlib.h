@@ -26,8 +26,8 @@
  * many calls as needed.  Z_PARTIAL_FLUSH, Z_SYNC_FLUSH, Z_FULL_FLUSH and
  * Z_BLOCK act as in deflate.c:763-1265 (markers, full-flush reset, refused
  * repeats with Z_BUF_ERROR); each flush call hands out the stream up to its
- * marker.  Flush calls at level 0 and other parameters return Z_STREAM_ERROR
- * (documented gap).
+ * marker (level 0: deflate_stored's blocks, handed out by every call).  Other
+ * parameters return Z_STREAM_ERROR.
  */
 #ifndef ZGPU_ZLIB_H
 #define ZGPU_ZLIB_H

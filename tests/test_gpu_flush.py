@@ -8,7 +8,7 @@ GPU, against
   * the oracle's zo_deflate_flushes (oracle/zoracle.c) on further random call
     sequences, and on the stream prefix each flush call hands out.
 
-Bit-exact.  Level 0 with flush calls is a documented gap (Z_STREAM_ERROR)."""
+Bit-exact, level 0 included (tests/golden/stored_golden.json)."""
 import ctypes as C
 import hashlib
 import json
@@ -188,17 +188,44 @@ def test_flush_small_output_buffers(zg, flush_golden):
     assert done > 0
 
 
-def test_flush_level0_and_errors(zg):
+def test_stored_golden_streams(zg):
+    """Level 0 over deflate() calls (deflate_stored, deflate.c:1635-1815):
+    status and total output after EVERY call (level-0 output is not deferred)
+    and the stream, against tests/golden/stored_golden.json."""
     L = _lib(zg)
-    s = ZStream()
-    assert L.deflateInit2_(C.byref(s), 0, 8, 15, 8, 0, VERSION, C.sizeof(ZStream)) == 0
+    with open(os.path.join(HERE, "golden", "stored_golden.json")) as f:
+        cases = json.load(f)["cases"]
+    for c in cases:
+        data = _case_input(c)
+        sts, lens, whole = replay(L, data, c["calls"], 0, c["wbits"], 0)
+        tag = (c["kind"], c["n"], c["wbits"], c["seed"])
+        assert sts == c["status"], tag
+        assert lens == c["out_len"], tag
+        assert len(whole) == c["len"] and hashlib.sha256(whole).hexdigest() == c["sha256"], tag
+
+
+def test_stored_random_vs_oracle(zg, oracle):
+    L = _lib(zg)
+    rng = np.random.default_rng(int(os.environ.get("ZGPU_STORED_SEED", "9")))
+    for t in range(16):
+        n = int(rng.choice([0, 3, 40000, 70000, 300000]))
+        data = bytes(datagen.make(["text", "random", "mix"][t % 3], n, 40 + t))
+        calls, pos = [], 0
+        while pos < n:
+            take = int(min(n - pos, rng.choice([0, 1, 1000, 32767, 32768, 65535, 65536, 100000])))
+            calls.append((take, int(rng.choice([0, 0, 1, 2, 3, 5]))))
+            pos += take
+        calls.append((0, 4))
+        wbits = int(rng.choice([15, -15, 31]))
+        sts, lens, whole = replay(L, data, calls, 0, wbits, 0)
+        rc, osts, olens, want = oracle.deflate_stored_calls(data, calls, {15: 1, -15: 0, 31: 2}[wbits])
+        assert rc == 0 and sts == osts and lens == olens and whole == want, (t, n, wbits)
+
+
+def test_flush_errors(zg):
+    L = _lib(zg)
     buf = C.create_string_buffer(b"abc", 3)
     out = C.create_string_buffer(64)
-    s.next_in, s.avail_in = C.addressof(buf), 3
-    s.next_out, s.avail_out = C.addressof(out), 64
-    assert L.deflate(C.byref(s), 2) == -2          # documented gap: level 0 with flushes
-    assert L.deflate(C.byref(s), 4) == 1
-    assert L.deflateEnd(C.byref(s)) == 0
     # a repeated flush with no new input is refused (deflate.c:1002-1005)
     s = ZStream()
     assert L.deflateInit2_(C.byref(s), 6, 8, 15, 8, 0, VERSION, C.sizeof(ZStream)) == 0

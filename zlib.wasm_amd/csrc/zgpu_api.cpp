@@ -289,6 +289,10 @@ struct FlushSpec {
     const uint32_t *head_in;
     const uint16_t *prev_in;
     size_t prev_n;
+    // level 0 (host array): the stored blocks and markers, made on the host the
+    // way deflate_stored cuts them (see deflate_stored_call)
+    const BlockRec *plan;
+    uint32_t nplan;
 };
 
 int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
@@ -298,7 +302,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     if (level == -1) level = 6;
     if (level < 0 || level > 9 || wrap < 0 || wrap > 2 || strategy < 0 || strategy > 4)
         return ZGPU_STREAM_ERROR;
-    if (fs && (count != 1 || level == 0)) return ZGPU_STREAM_ERROR;
+    if (fs && (count != 1 || (level == 0) != (fs->plan != nullptr))) return ZGPU_STREAM_ERROR;
     if (count == 0) return ZGPU_OK;
     std::vector<uint64_t> lens(count);
     if (hipMemcpyAsync(lens.data(), src_len, 8ull * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -333,7 +337,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             // literal at index n (a run of literals up to the end), which must
             // not land in the next buffer's region
             pos += (lens[i] + 64) & ~63ull;
-            blk += lens[i] / kSymLimit + 2 + (fs ? 2ull * fs->n : 0);   // a flush: a block and a marker
+            blk += lens[i] / kSymLimit + 2 + (fs ? 2ull * fs->n + fs->nplan : 0);   // a flush: a block and a marker
         }
         max_pos = std::max(max_pos, pos);
         max_blk = std::max(max_blk, blk);
@@ -390,6 +394,10 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             if (b->p && hipMemsetAsync(b->p, v & 0xff, b->cap, st) != hipSuccess) return ZGPU_MEM_ERROR;
         if (hipMemsetAsync(d_nblk, v & 0xff, 8ull * max_cnt, st) != hipSuccess) return ZGPU_MEM_ERROR;
     }
+    if (fs && fs->plan &&
+        (hipMemcpyAsync(c.ws_blk.p, fs->plan, sizeof(BlockRec) * fs->nplan, hipMemcpyHostToDevice, st) != hipSuccess ||
+         hipMemcpyAsync(d_nblk, &fs->nplan, 4, hipMemcpyHostToDevice, st) != hipSuccess))
+        return ZGPU_MEM_ERROR;
     if (fs && fs->head_in) {
         if (!c.ws_heads.ensure(4ull * 32768) ||
             hipMemcpyAsync(c.ws_heads.p, fs->head_in, 4ull * 32768, hipMemcpyHostToDevice, st) != hipSuccess ||
@@ -428,6 +436,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.bit0 = fs->bit0;
             job.byte0 = fs->byte0;
             job.flush_out = fs->out;
+            job.plan = fs->plan != nullptr;
         }
         return job;
     };
@@ -515,6 +524,8 @@ struct FlushHost {
     size_t prev_n = 0;
     std::vector<uint32_t> *head_out = nullptr;
     std::vector<uint16_t> *prev_out = nullptr;
+    const BlockRec *plan = nullptr;    // level 0: see FlushSpec
+    uint32_t nplan = 0;
 };
 
 int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
@@ -567,7 +578,7 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
         uint64_t *d_mb = d_fp + fh->n + (fh->n + 1) / 2;
         if (hipMemsetAsync(d_mb, 0, 32, st) != hipSuccess) return ZGPU_MEM_ERROR;
         fs = FlushSpec{d_fp, d_ft, fh->n, fh->open_end, fh->start, fh->bit0, fh->byte0, d_mb,
-                       fh->head_in, fh->prev_in, fh->prev_n};
+                       fh->head_in, fh->prev_in, fh->prev_n, fh->plan, fh->nplan};
     }
     int rc = deflate_dev_locked(c, d_in, d_so, d_sl, d_out, d_do, d_dc, d_dl, d_st, (uint32_t)count,
                                 level, wrap, strategy, st, fh ? &fs : nullptr);
@@ -1226,6 +1237,98 @@ void drain(z_streamp strm, internal_state *s) {
 
 inline int flush_rank(int f) { return f * 2 - (f > 4 ? 9 : 0); }   // deflate.c: RANK
 
+// Level 0: one deflate() call of deflate_stored (deflate.c:1635-1815) with an
+// output buffer that takes the call's output.  Its first loop sends stored
+// blocks of up to MAX_STORED bytes straight from the window and the input: a
+// Z_NO_FLUSH call while at least min_block (w_size = 32768) bytes are there,
+// any other call all of them (the last one final at Z_FINISH); the rest waits
+// in the window.  The block cuts are made here, the blocks and deflate()'s
+// markers are written by k_encode on the GPU.  zlib cuts smaller blocks when
+// the output space is smaller -- the one way a level-0 stream can differ.
+int deflate_stored_call(z_streamp strm, internal_state *s, int flush) {
+    if (s->finished) {
+        drain(strm, s);
+        return flush == Z_FINISH && s->out_pos == s->out.size() ? Z_STREAM_END : Z_OK;
+    }
+    queue_header(s);                                           // written by the first call
+    if (strm->avail_in) {
+        s->in.insert(s->in.end(), strm->next_in, strm->next_in + strm->avail_in);
+        strm->total_in += strm->avail_in;
+        strm->next_in += strm->avail_in;
+        strm->avail_in = 0;
+    }
+    advance_check(s);
+    std::vector<BlockRec> plan;
+    size_t off = 0, total = s->in.size();
+    bool last = false;
+    for (;;) {                                                 // deflate.c:1652-1725
+        const size_t len = std::min<size_t>(total, 65535);
+        if (len < 32768 && ((len == 0 && flush != Z_FINISH) || flush == Z_NO_FLUSH)) break;
+        last = flush == Z_FINISH && len == total;
+        BlockRec r{};
+        r.in_start = off;
+        r.in_end = off + len;
+        r.flags = last ? kBlkLast : 0u;
+        plan.push_back(r);
+        off += len;
+        total -= len;
+        if (last) break;
+    }
+    if (!last && flush != Z_NO_FLUSH && flush != Z_FINISH && total == 0) {   // block_done: :1211-1233
+        BlockRec r{};
+        r.in_start = r.in_end = off;
+        r.flags = kBlkMarker | ((uint32_t)flush << 4);
+        plan.push_back(r);
+    }
+    if (!plan.empty()) {
+        std::vector<uint8_t> body((size_t)compress_bound64(off) + 64 + 8 * plan.size());
+        const uint8_t *sp = s->in.data();
+        uint8_t *dp = body.data();
+        size_t sl = off, cap = body.size();
+        int st = 0;
+        FlushHost fh{nullptr, nullptr, 0, 1, 0, (uint32_t)(s->res_bits & 7),
+                     s->res_byte & ((1u << (s->res_bits & 7)) - 1u), {0, 0, 0, 0}};
+        fh.plan = plan.data();
+        fh.nplan = (uint32_t)plan.size();
+        {
+            Ctx &c = ctx();
+            std::lock_guard<std::mutex> g(c.mu);
+            int rc = init_locked(c);
+            if (!rc) rc = compress_host_locked(c, &sp, &sl, &dp, &cap, &st, 1, 0, ZGPU_WRAP_RAW, s->strategy, &fh);
+            if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
+        }
+        const size_t jb = (size_t)(s->res_bits >> 3);
+        s->out.insert(s->out.end(), body.begin() + (std::ptrdiff_t)(s->part_out - jb),
+                      body.begin() + (std::ptrdiff_t)cap);
+        s->part_out = jb + cap;
+        s->res_bits = ((uint64_t)jb << 3) + fh.out[1];
+        s->res_byte = (uint32_t)fh.out[3];
+        s->in.erase(s->in.begin(), s->in.begin() + (std::ptrdiff_t)off);
+        s->in_base += off;
+        s->ck_pos = std::max(s->ck_pos, s->in_base);
+    }
+    if (s->wrap) strm->adler = s->check;
+    if (last) {                                                // the trailer (deflate.c:1236-1262)
+        const uint32_t ck = s->check;
+        if (s->wrap == 1) {
+            for (int i = 3; i >= 0; i--) s->out.push_back((uint8_t)(ck >> (8 * i)));
+        } else if (s->wrap == 2) {
+            const uint32_t isz = (uint32_t)strm->total_in;
+            for (int i = 0; i < 4; i++) s->out.push_back((uint8_t)(ck >> (8 * i)));
+            for (int i = 0; i < 4; i++) s->out.push_back((uint8_t)(isz >> (8 * i)));
+        }
+        s->finished = 1;
+        s->in.clear();
+        s->in.shrink_to_fit();
+    }
+    drain(strm, s);
+    if (flush != Z_FINISH) {
+        if (strm->avail_out == 0) s->last_flush = -1;
+        return Z_OK;
+    }
+    return s->out_pos == s->out.size() ? Z_STREAM_END : Z_OK;
+}
+
 // A flush call whose event is the last of s->ev_*: its blocks and marker are
 // queued.  zlib writes the blocks first and returns need_more when the output
 // space runs out at a block (deflate.c:1685-1690 FLUSH_BLOCK); the marker
@@ -1290,9 +1393,6 @@ int deflate(z_streamp strm, int flush) {
     if (!strm->next_out || (strm->avail_in && !strm->next_in) || (s->finished && flush != Z_FINISH))
         return Z_STREAM_ERROR;
     const bool is_flush = flush != Z_NO_FLUSH && flush != Z_FINISH;
-    // level 0 with flush calls: deflate_stored's blocks follow avail_out
-    // (deflate.c:1635-1815) -- documented gap
-    if (is_flush && s->level == 0) return Z_STREAM_ERROR;
     if (strm->avail_out == 0) return Z_BUF_ERROR;
     const int old_flush = s->last_flush;
     s->last_flush = flush;
@@ -1306,6 +1406,7 @@ int deflate(z_streamp strm, int flush) {
         return Z_BUF_ERROR;
     }
     if (s->finished && strm->avail_in) return Z_BUF_ERROR;
+    if (s->level == 0) return deflate_stored_call(strm, s, flush);
     if (s->marker_due) {
         // the previous flush call cut its block but ran out of output before
         // the marker: a flush call with no input completes it with its own

@@ -1957,7 +1957,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
     }
     __syncthreads();
 
-    if (level == 0) {
+    if (level == 0 && !job.plan) {
         // deflate_stored (deflate.c:1635-1815) with a compressBound()-sized
         // output: MAX_STORED-byte stored blocks, last one final.
         int64_t done = 0;
@@ -1997,7 +1997,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
                 const uint32_t kb = g0 + (uint32_t)wave;
                 TreeLDS &T = TT[wave];
                 uint32_t *hl = HL[wave], *hd = HD[wave];
-                if (kb < nblk && !(blk[kb].flags & kBlkMarker)) {
+                if (kb < nblk && level != 0 && !(blk[kb].flags & kBlkMarker)) {
                     const BlockRec br = blk[kb];
                     // histogram (_tr_tally freq updates, deflate.h:354-372)
                     for (int i = lane; i < kLCodes; i += 64) hl[i] = 0;
@@ -2076,7 +2076,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
             // room for the largest block header (dynamic trees: < 5000 bits)
             if (s_obit - st.sbase + 6144 > kStgBits) stg_flush(st, s_obit, false);
             if (tid == 0) {
-                const int type = s_hdr[w].type;
+                const int type = level == 0 ? 0 : s_hdr[w].type;   // a level-0 plan: stored
                 const uint64_t stored_len = br.in_end - br.in_start;
                 put((uint32_t)(type << 1) + (last ? 1u : 0u), 3);
                 if (type == 0) {
@@ -2099,7 +2099,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
                 }
             }
             __syncthreads();
-            const int type = s_hdr[w].type;
+            const int type = level == 0 ? 0 : s_hdr[w].type;
             if (type == 0) {
                 // stored: raw bytes (byte aligned)
                 const int64_t len = (int64_t)(br.in_end - br.in_start);

@@ -126,6 +126,7 @@ struct DeflateJob {
     // [1] output bits at the end, [2] the window offset S at the last flush
     // (buffer-relative), [3] the last, partial output byte
     uint64_t *flush_out;
+    int plan;                // level 0 streaming: the block records were made on the host (stored blocks)
 };
 
 // ---- inflate ----
