@@ -311,3 +311,41 @@ def test_deflate_reset_copy_pending(zg, oracle):
     again = run(s, 0, [(150000, 4)])
     assert again == oracle.compress(data, 6)[1]
     assert L.deflateEnd(C.byref(s)) == 0
+
+
+def test_inflate_sync_flushed_stream_progressively(zg, oracle):
+    """An open, sync-flushed stream (what a connection carries): inflate() fed
+    up to each flush point hands out all the data before it (zlib.h,
+    Z_SYNC_FLUSH), without waiting for the end of the stream."""
+    L = zg.load()
+    L.inflateInit2_.restype = C.c_int
+    L.inflateInit2_.argtypes = [C.POINTER(ZStream), C.c_int, C.c_char_p, C.c_int]
+    L.inflate.restype = C.c_int
+    L.inflate.argtypes = [C.POINTER(ZStream), C.c_int]
+    L.inflateEnd.argtypes = [C.POINTER(ZStream)]
+    data = bytes(datagen.make("mix", 400000, 21))
+    cuts = [0, 1000, 5000, 70000, 70001, 200000, 399990, 400000]
+    for level in (0, 1, 6, 9):
+        events = [(c, 2) for c in cuts[1:]]
+        if level:
+            rc, stream = oracle.deflate_flushes(data, events, level, 1, 0, finish=False)
+            # where each flush call's output ends: the stream of its prefix
+            ends = [len(oracle.deflate_flushes(data[:c], events[:i + 1], level, 1, 0, finish=False)[1])
+                    for i, c in enumerate(cuts[1:])]
+        else:
+            rc, _, ends, stream = oracle.deflate_stored_calls(
+                data, [(b - a, 2) for a, b in zip(cuts, cuts[1:])], 1)
+        assert rc == 0
+        s = ZStream()
+        assert L.inflateInit2_(C.byref(s), 15, VERSION, C.sizeof(ZStream)) == 0
+        inbuf = C.create_string_buffer(stream, len(stream))
+        out = C.create_string_buffer(len(data) + 64)
+        s.next_out, s.avail_out = C.addressof(out), len(data) + 64
+        prev = 0
+        for c, e in zip(cuts[1:], ends):
+            s.next_in, s.avail_in = C.addressof(inbuf) + prev, e - prev
+            rc = L.inflate(C.byref(s), 2)
+            assert rc == 0, (level, c, rc)
+            assert s.total_out == c and out.raw[:c] == data[:c], (level, c, s.total_out)
+            prev = e
+        assert L.inflateEnd(C.byref(s)) == 0

@@ -1602,7 +1602,11 @@ int inflate(z_streamp strm, int flush) {
         strm->avail_in = 0;
         strm->total_in += took;
     }
-    if (!s->finished && (took == 0 || flush == Z_FINISH || s->in.size() >= 2 * s->tried)) {
+    // Decode what has arrived whenever input arrives: a stream that is still
+    // open (a sync-flushed connection, a file read in pieces) hands out every
+    // byte its input decodes to so far, as inflate() does (inflate.c:622-1221);
+    // each attempt decodes the stream from its start and gives out what is new.
+    if (!s->finished && (took || (flush == Z_FINISH && s->tried != s->in.size()))) {
         if (s->cap == 0) s->cap = std::max<size_t>(4 * s->in.size(), 1 << 16);
         for (;;) {
             s->out.resize(s->cap);
@@ -1623,7 +1627,11 @@ int inflate(z_streamp strm, int flush) {
                 s->cap *= 2;
                 continue;
             }
-            if (stop == kIInEnd) { s->tried = s->in.size(); s->out.clear(); break; }
+            if (stop == kIInEnd) {                                    // the stream goes on: its prefix so far
+                s->tried = s->in.size();
+                s->out.resize(dl);
+                break;
+            }
             s->out.resize(dl);
             s->finished = 1;
             if (stop == kIEnd) {
@@ -1649,14 +1657,14 @@ int inflate(z_streamp strm, int flush) {
         }
     }
     size_t give = 0;
-    if (s->finished) {
+    if (s->out_pos < s->out.size() || s->finished) {
         give = std::min<size_t>(strm->avail_out, s->out.size() - s->out_pos);
         std::memcpy(strm->next_out, s->out.data() + s->out_pos, give);
         s->out_pos += give;
         strm->next_out += give;
         strm->avail_out -= (uInt)give;
         strm->total_out += give;
-        if (s->out_pos == s->out.size()) return s->result;
+        if (s->finished && s->out_pos == s->out.size()) return s->result;
     }
     if (took || give) return Z_OK;
     return Z_BUF_ERROR;                                                // inflate.c:1265-1266: no progress
