@@ -337,3 +337,15 @@ def test_deflateinit2_strategy_stream(zg, oracle):
         got = out.raw[:s.total_out]
         assert L.deflateEnd(C.byref(s)) == 0
         assert got == oracle.compress(data, 6, wrap=1, strategy=strategy)[1], strategy
+
+
+def test_few_large_buffers_segmented_match(zg, oracle):
+    """A sub-batch of few large buffers runs k_match per 256 KiB segment (each
+    stages the 32 KiB before it): streams equal the oracle's at segment edges,
+    ragged sizes and every lazy level."""
+    bufs = [datagen.make("mix", (8 << 20) + 77, 61), datagen.make("text", (1 << 20) + 5, 62),
+            datagen.make("runs", 700 * 1024 + 3, 63), datagen.make("records", (5 << 18) + 4095, 64)]
+    for level in (4, 6, 9):
+        got = zg.compress_batch(bufs, level=level)
+        for b, (st, z) in zip(bufs, got):
+            assert st == 0 and z == oracle.compress(b, level)[1], (len(b), level)

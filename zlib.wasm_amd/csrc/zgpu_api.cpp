@@ -221,6 +221,7 @@ struct Ctx {
     DevBuf ws_key, ws_key2;   // k_count's walk-length keys (one byte per position)
     DevBuf ws_stg;            // k_parse_seg's symbol staging (caller's stream only)
     DevBuf ws_help;           // the a18 helpers' staging (zlib_*_simd)
+    DevBuf ws_seg;            // k_match segments of sub-batches of few large buffers
     // inflate: match records, per-stream results, checks, offsets, stop codes
     DevBuf ws_mrec, ws_irec, ws_ick, ws_imeta, ws_istop;
     hipStream_t aux = nullptr;
@@ -378,6 +379,28 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     }
     if (level >= 1 && level <= 3 && !huff && !rle && !c.ws_heads.ensure(4ull * 32768 * max_cnt))
         return ZGPU_MEM_ERROR;
+    // k_match per 256 KiB segment where a sub-batch has too few buffers to fill
+    // the GPU one workgroup per buffer (a single large zlib.h buffer, say)
+    constexpr uint64_t kSeg = 256 * 1024;
+    std::vector<uint32_t> segs;
+    std::vector<size_t> seg_at(nsub + 1, 0);
+    for (size_t sb = 0; sb < nsub; sb++) {
+        seg_at[sb] = segs.size() / 2;
+        const uint32_t a = cuts[sb], b = cuts[sb + 1];
+        uint64_t big = 0;
+        for (uint32_t i = a; i < b; i++) big = std::max(big, lens[i]);
+        if (!slow || b - a >= 512 || big <= kSeg) continue;
+        for (uint32_t i = a; i < b; i++)
+            for (uint64_t o = 0; o < lens[i]; o += kSeg) {
+                segs.push_back(i - a);
+                segs.push_back((uint32_t)o);
+            }
+    }
+    seg_at[nsub] = segs.size() / 2;
+    if (!segs.empty() && (!c.ws_seg.ensure(4 * segs.size()) ||
+                          hipMemcpyAsync(c.ws_seg.p, segs.data(), 4 * segs.size(), hipMemcpyHostToDevice, st) !=
+                              hipSuccess))
+        return ZGPU_MEM_ERROR;
     uint64_t *d_meta = c.ws_meta.as<uint64_t>();
     uint32_t *d_nblk = reinterpret_cast<uint32_t *>(d_meta + 2ull * count);
     uint32_t *d_check = d_nblk + max_cnt;
@@ -427,6 +450,11 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         job.blocks = c.ws_blk.as<BlockRec>();
         job.nblocks = d_nblk;
         job.check = d_check;
+        if (seg_at[s + 1] > seg_at[s]) {
+            job.seg = c.ws_seg.as<uint32_t>() + 2 * seg_at[s];
+            job.nseg = (uint32_t)(seg_at[s + 1] - seg_at[s]);
+            job.seg_len = (uint32_t)kSeg;
+        }
         if (fs) {
             job.fl_pos = fs->pos;
             job.fl_type = fs->type;

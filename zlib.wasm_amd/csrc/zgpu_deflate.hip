@@ -617,9 +617,16 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
     __shared__ uint16_t s_perm[kSorted ? kMT : 1];
     __shared__ int s_hist[kSortBuckets], s_base[kSortBuckets];
     const int tid = threadIdx.x;
-    const uint32_t bi = blockIdx.x;
+    // one workgroup per buffer, or -- a sub-batch of few large buffers -- per
+    // segment [s0, s1) of a buffer (job.seg: buffer, start): a position's walk
+    // needs only the 32 KiB before it, so a segment first stages the kMW/kMT
+    // tiles before s0 without walking them
+    const uint32_t bi = job.seg ? job.seg[2 * blockIdx.x] : blockIdx.x;
     const uint32_t g = job.first + bi;
     const int64_t n = (int64_t)job.src_len[g];
+    const int64_t s0 = job.seg ? (int64_t)job.seg[2 * blockIdx.x + 1] : 0;
+    const int64_t s1 = job.seg && s0 + (int64_t)job.seg_len < n ? s0 + (int64_t)job.seg_len : n;
+    const int64_t t0 = s0 > kMW ? s0 - kMW : 0;
     const uint8_t *in = job.src + job.src_off[g];
     const uint16_t *L = job.link + job.ws_off[bi];
     uint32_t *rf = job.rfull + job.ws_off[bi];
@@ -629,10 +636,10 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
     uint64_t st_lane_steps = 0, st_cmps = 0, st_walks = 0, st_wave_iters = 0;
 
     TilePre P;
-    tile_prefetch(P, 0, n, in, L, K, tid);
-    for (int64_t ts = 0; ts < n; ts += kMT) {
+    tile_prefetch(P, t0, n, in, L, K, tid);
+    for (int64_t ts = t0; ts < s1; ts += kMT) {
         const int64_t B = ts - kMW;
-        const int tile_n = (int)((n - ts) < kMT ? (n - ts) : kMT);
+        const int tile_n = ts < s0 ? 0 : (int)((n - ts) < kMT ? (n - ts) : kMT);   // 0: staging only
         tile_store(E, P, ts, tid);
         if (tid == 0) next_i = 0;
         if (kSorted && tid < kSortBuckets) s_hist[tid] = 0;
@@ -669,7 +676,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
                     s_perm[s_base[bk[u]] + rk[u]] = (uint16_t)(tid + u * kMatchThreads);
             __syncthreads();
         }
-        if (ts + kMT < n) tile_prefetch(P, ts + kMT, n, in, L, K, tid);   // lands during the walks
+        if (ts + kMT < s1) tile_prefetch(P, ts + kMT, n, in, L, K, tid);   // lands during the walks
         for (;;) {
             if (kVariant == kMatchProbeHalf && tid >= kMatchThreads / 2) break;   // probe: half the waves walk
             const int i = atomicAdd(&next_i, 1);
@@ -2224,26 +2231,27 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         break;
     case 1: {
         const int wq = (int)(job.level >= 5);
+        const dim3 mgrid(job.seg ? job.nseg : job.count);   // per segment or per buffer
         const int v = match_variant();
         if (job.nfl) {                                          // a flush job (zgpu_api.cpp deflate())
-            hipLaunchKernelGGL((k_match<kMatchDefault, true>), grid, dim3(kMatchThreads), 0, st, job, wq);
+            hipLaunchKernelGGL((k_match<kMatchDefault, true>), mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == 14) {
-            hipLaunchKernelGGL(k_match<14>, grid, dim3(kMatchThreads), 0, st, job, wq);
+            hipLaunchKernelGGL(k_match<14>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchProbeNoWalk) {
-            hipLaunchKernelGGL(k_match<kMatchProbeNoWalk>, grid, dim3(kMatchThreads), 0, st, job, wq);
+            hipLaunchKernelGGL(k_match<kMatchProbeNoWalk>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchProbeHalf) {
-            hipLaunchKernelGGL(k_match<kMatchProbeHalf>, grid, dim3(kMatchThreads), 0, st, job, wq);
+            hipLaunchKernelGGL(k_match<kMatchProbeHalf>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchProbeNoCmp) {
-            hipLaunchKernelGGL(k_match<kMatchProbeNoCmp>, grid, dim3(kMatchThreads), 0, st, job, wq);
+            hipLaunchKernelGGL(k_match<kMatchProbeNoCmp>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchProbeCmpOnly) {
-            hipLaunchKernelGGL(k_match<kMatchProbeCmpOnly>, grid, dim3(kMatchThreads), 0, st, job, wq);
+            hipLaunchKernelGGL(k_match<kMatchProbeCmpOnly>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
 
 
 
         } else if (v == kMatchStats) {
             unsigned long long z[4] = {0, 0, 0, 0}, r[4];
             (void)hipMemcpyToSymbol(HIP_SYMBOL(g_mstat), z, sizeof z);
-            hipLaunchKernelGGL(k_match<kMatchStats>, grid, dim3(kMatchThreads), 0, st, job, wq);
+            hipLaunchKernelGGL(k_match<kMatchStats>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
             (void)hipStreamSynchronize(st);
             (void)hipMemcpyFromSymbol(r, HIP_SYMBOL(g_mstat), sizeof r);
             fprintf(stderr, "k_match stats: lane_steps %llu compares %llu walks %llu wave_iters %llu "
@@ -2251,7 +2259,7 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
                     r[3] ? (double)r[0] / (64.0 * r[3]) : 0.0, r[2] ? (double)r[0] / r[2] : 0.0,
                     r[0] ? (double)r[1] / r[0] : 0.0);
         } else {
-            hipLaunchKernelGGL(k_match<kMatchDefault>, grid, dim3(kMatchThreads), 0, st, job, wq);
+            hipLaunchKernelGGL(k_match<kMatchDefault>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
         }
         break;
     }

@@ -127,6 +127,11 @@ struct DeflateJob {
     // (buffer-relative), [3] the last, partial output byte
     uint64_t *flush_out;
     int plan;                // level 0 streaming: the block records were made on the host (stored blocks)
+    // k_match over segments (a sub-batch of few large buffers): nseg pairs
+    // (buffer, start) of seg_len-byte segments, one workgroup each; null: one
+    // workgroup per buffer
+    const uint32_t *seg;
+    uint32_t nseg, seg_len;
 };
 
 // ---- inflate ----
