@@ -20,3 +20,10 @@ for mb in (1, 16, 64):
         el = time.time() - t
         print(f"single {mb} MiB L{level}: {el * 1e3:.1f} ms  {len(data) / el / 1e6:.1f} MB/s "
               f"ratio {len(data) / len(z):.2f}", flush=True)
+
+# stage breakdown of one 64 MiB L6 buffer
+data = bytes(datagen.make("mix", 64 << 20, 3))
+zgpu.stage_timing(True)
+zgpu.compress_batch([data], level=6)
+print("stages 64 MiB L6:", zgpu.stage_timing_read(), flush=True)
+zgpu.stage_timing(False)
