@@ -608,7 +608,7 @@ __device__ inline int64_t flush_limit(const DeflateJob &job, int64_t p, int64_t 
     return lo < job.nfl ? (int64_t)job.fl_pos[lo] : n;
 }
 
-template <int kVariant, bool kEv = false>
+template <int kVariant, bool kEv = false, bool kSegs = false>
 __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int want_q) {
     constexpr bool kSorted = kVariant != 14;
     constexpr int kSortBuckets = 64;
@@ -621,12 +621,12 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
     // segment [s0, s1) of a buffer (job.seg: buffer, start): a position's walk
     // needs only the 32 KiB before it, so a segment first stages the kMW/kMT
     // tiles before s0 without walking them
-    const uint32_t bi = job.seg ? job.seg[2 * blockIdx.x] : blockIdx.x;
+    const uint32_t bi = kSegs ? job.seg[2 * blockIdx.x] : blockIdx.x;
     const uint32_t g = job.first + bi;
     const int64_t n = (int64_t)job.src_len[g];
-    const int64_t s0 = job.seg ? (int64_t)job.seg[2 * blockIdx.x + 1] : 0;
-    const int64_t s1 = job.seg && s0 + (int64_t)job.seg_len < n ? s0 + (int64_t)job.seg_len : n;
-    const int64_t t0 = s0 > kMW ? s0 - kMW : 0;
+    const int64_t s0 = kSegs ? (int64_t)job.seg[2 * blockIdx.x + 1] : 0;
+    const int64_t s1 = kSegs && s0 + (int64_t)job.seg_len < n ? s0 + (int64_t)job.seg_len : n;
+    const int64_t t0 = kSegs && s0 > kMW ? s0 - kMW : 0;
     const uint8_t *in = job.src + job.src_off[g];
     const uint16_t *L = job.link + job.ws_off[bi];
     uint32_t *rf = job.rfull + job.ws_off[bi];
@@ -639,7 +639,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
     tile_prefetch(P, t0, n, in, L, K, tid);
     for (int64_t ts = t0; ts < s1; ts += kMT) {
         const int64_t B = ts - kMW;
-        const int tile_n = ts < s0 ? 0 : (int)((n - ts) < kMT ? (n - ts) : kMT);   // 0: staging only
+        const int tile_n = kSegs && ts < s0 ? 0 : (int)((n - ts) < kMT ? (n - ts) : kMT);   // 0: staging only
         tile_store(E, P, ts, tid);
         if (tid == 0) next_i = 0;
         if (kSorted && tid < kSortBuckets) s_hist[tid] = 0;
@@ -2233,8 +2233,12 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         const int wq = (int)(job.level >= 5);
         const dim3 mgrid(job.seg ? job.nseg : job.count);   // per segment or per buffer
         const int v = match_variant();
-        if (job.nfl) {                                          // a flush job (zgpu_api.cpp deflate())
+        if (job.nfl && job.seg) {                               // a flush job (zgpu_api.cpp deflate())
+            hipLaunchKernelGGL((k_match<kMatchDefault, true, true>), mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (job.nfl) {
             hipLaunchKernelGGL((k_match<kMatchDefault, true>), mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (job.seg) {                                   // few large buffers: per segment
+            hipLaunchKernelGGL((k_match<kMatchDefault, false, true>), mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == 14) {
             hipLaunchKernelGGL(k_match<14>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchProbeNoWalk) {
