@@ -349,3 +349,19 @@ def test_few_large_buffers_segmented_match(zg, oracle):
         got = zg.compress_batch(bufs, level=level)
         for b, (st, z) in zip(bufs, got):
             assert st == 0 and z == oracle.compress(b, level)[1], (len(b), level)
+
+
+def test_small_single_buffers_tile_segments(zg, oracle):
+    """A lone small buffer (C1's 64 KB compress2) walks k_match in segments as
+    short as one 4 KiB tile, each staging the <= 32 KiB before it: streams equal
+    the oracle's for one-tile, few-tile and ragged segments at every lazy level."""
+    cases = [[datagen.make("text", 64 * 1024, 71)], [datagen.make("mix", 64 * 1024 + 1, 72)],
+             [datagen.make("markup", 300 * 1024 + 9, 73)], [datagen.make("runs", 40 * 1024 - 1, 74)],
+             [datagen.make("text", 5000, 75), datagen.make("records", 150 * 1024 + 3, 76)]]
+    for bufs in cases:
+        for level in (4, 6, 9):
+            got = zg.compress_batch(bufs, level=level)
+            for b, (st, z) in zip(bufs, got):
+                assert st == 0 and z == oracle.compress(b, level)[1], (len(b), level)
+        rc, z = zg.compress2(bufs[-1], level=6)
+        assert rc == 0 and z == oracle.compress(bufs[-1], 6)[1]

@@ -379,19 +379,25 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     }
     if (level >= 1 && level <= 3 && !huff && !rle && !c.ws_heads.ensure(4ull * 32768 * max_cnt))
         return ZGPU_MEM_ERROR;
-    // k_match per 256 KiB segment where a sub-batch has too few buffers to fill
-    // the GPU one workgroup per buffer (a single large zlib.h buffer, say)
-    constexpr uint64_t kSeg = 256 * 1024;
+    // k_match per segment where a sub-batch has too few buffers to fill the GPU
+    // one workgroup per buffer (a single zlib.h buffer, say).  The segment is
+    // the sub-batch's bytes over the 256 CUs, in whole 4 KiB tiles, at most
+    // 256 KiB: a lone 64 KiB compress2 walks 16 one-tile segments side by side
+    // instead of 16 tiles in a row (each segment stages <= 32 KiB it does not walk).
+    constexpr uint64_t kSegMax = 256 * 1024, kSegTile = 4096, kSegCUs = 256;
     std::vector<uint32_t> segs;
-    std::vector<size_t> seg_at(nsub + 1, 0);
+    std::vector<size_t> seg_at(nsub + 1, 0), seg_len(nsub, kSegMax);
     for (size_t sb = 0; sb < nsub; sb++) {
         seg_at[sb] = segs.size() / 2;
         const uint32_t a = cuts[sb], b = cuts[sb + 1];
-        uint64_t big = 0;
-        for (uint32_t i = a; i < b; i++) big = std::max(big, lens[i]);
-        if (!slow || b - a >= 512 || big <= kSeg) continue;
+        uint64_t big = 0, tot = 0;
+        for (uint32_t i = a; i < b; i++) big = std::max(big, lens[i]), tot += lens[i];
+        uint64_t seg = (tot / kSegCUs + kSegTile - 1) / kSegTile * kSegTile;
+        seg = seg < kSegTile ? kSegTile : seg > kSegMax ? kSegMax : seg;
+        seg_len[sb] = seg;
+        if (!slow || b - a >= 512 || big <= seg) continue;
         for (uint32_t i = a; i < b; i++)
-            for (uint64_t o = 0; o < lens[i]; o += kSeg) {
+            for (uint64_t o = 0; o < lens[i]; o += seg) {
                 segs.push_back(i - a);
                 segs.push_back((uint32_t)o);
             }
@@ -453,7 +459,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         if (seg_at[s + 1] > seg_at[s]) {
             job.seg = c.ws_seg.as<uint32_t>() + 2 * seg_at[s];
             job.nseg = (uint32_t)(seg_at[s + 1] - seg_at[s]);
-            job.seg_len = (uint32_t)kSeg;
+            job.seg_len = (uint32_t)seg_len[s];
         }
         if (fs) {
             job.fl_pos = fs->pos;
