@@ -31,8 +31,9 @@ for kind in ("text", "mix"):
           f"host zlib 1 thread {cpu * 1e3:.3f} ms ({len(data) / cpu / 1e6:.1f} MB/s), ratio {len(data) / len(z):.2f}",
           flush=True)
 
-data = bytes(datagen.make("text", 64 * 1024, 7))
-zgpu.stage_timing(True)
-zgpu.compress2(data, level=6)
-print("stages C1 64 KiB text L6 (ms):", zgpu.stage_timing_read(), flush=True)
-zgpu.stage_timing(False)
+for kind in ("text", "mix"):
+    data = bytes(datagen.make(kind, 64 * 1024, 7))
+    zgpu.stage_timing(True)
+    zgpu.compress2(data, level=6)
+    print(f"stages C1 64 KiB {kind} L6 (ms):", zgpu.stage_timing_read(), flush=True)
+    zgpu.stage_timing(False)

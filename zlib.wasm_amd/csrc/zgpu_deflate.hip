@@ -955,7 +955,7 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
 // The lazy parse is a deterministic state machine over decision points whose
 // state is (match_length, match_start, match_available).  Whenever
 // match_length < MIN_MATCH the state is "simple" and fully described by
-// match_available.  The buffer is cut into <= kParseLanes segments of >= 1 KiB,
+// match_available.  The buffer is cut into <= kParseLanes segments of >= 512 B,
 // one lane each (several independent load chains per buffer hide latency).
 //  pass 1  lane i parses its segment from the simple state (.., avail=0) and
 //          records (2 bits per position, lane-private words in global memory)
@@ -982,7 +982,7 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
 // has more symbols than the lane has state words, is flagged
 // (nblocks = ~0) for k_parse_slow.
 // ------------------------------------------------------------------------
-constexpr int kSegMin = 1024;
+constexpr int kSegMin = 512;
 constexpr int kParseLanes = 256;                  // segments (lanes) per buffer
 constexpr uint32_t kEnd = 0xffffffffu;
 
