@@ -79,3 +79,42 @@ def test_no_oracle_linkage():
     assert "oracle" not in out and "zref" not in out
     syms = subprocess.run(["nm", "-D", LIB], capture_output=True, text=True).stdout
     assert "zo_" not in syms
+
+
+def test_oversize_buffers_refused_before_gpu_work(lib):
+    """Kernels address a buffer with 32-bit positions: buffers of 4 GiB - 64 KiB
+    or more are refused up front, never truncated into a stream that
+    covers only n mod 2^32 bytes.  The guard fires before any device access, so
+    a small real buffer passed with a huge length is never read."""
+    buf = C.create_string_buffer(64)
+    out = C.create_string_buffer(64)
+    big = (1 << 32) + 5
+    lib.compress2.restype = C.c_int
+    lib.compress2.argtypes = [C.c_void_p, C.POINTER(C.c_ulong), C.c_void_p, C.c_ulong, C.c_int]
+    dl = C.c_ulong(64)
+    assert lib.compress2(out, C.byref(dl), buf, big, 6) == -4 and dl.value == 0      # Z_MEM_ERROR
+    lib.zgpu_compress_batch.restype = C.c_int
+    src = (C.c_void_p * 1)(C.cast(buf, C.c_void_p))
+    dst = (C.c_void_p * 1)(C.cast(out, C.c_void_p))
+    sl = (C.c_size_t * 1)(big)
+    dln = (C.c_size_t * 1)(64)
+    st = (C.c_int * 1)(0)
+    assert lib.zgpu_compress_batch(src, sl, dst, dln, st, C.c_size_t(1), 6, 1) == -2  # ZGPU_STREAM_ERROR
+
+
+def test_checksums_never_abort_without_gpu(lib):
+    """crc32()/adler32() cannot report errors in zlib's API; without a usable
+    GPU they must return (0) instead of ending the host process."""
+    import subprocess
+    import sys
+    code = ("import ctypes as C, torch; L = C.CDLL(%r); L.crc32.restype = C.c_ulong; "
+            "L.crc32.argtypes = [C.c_ulong, C.c_char_p, C.c_uint]; "
+            "L.adler32.restype = C.c_ulong; L.adler32.argtypes = [C.c_ulong, C.c_char_p, C.c_uint]; "
+            "print(L.crc32(0, b'abc', 3), L.adler32(1, b'abc', 3))" % LIB)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, HIP_VISIBLE_DEVICES="-1"))
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == ["0", "0"]

@@ -82,3 +82,47 @@ def test_sharded_batch_matches_single_process(world):
     assert (tot_in, tot_out) == (want_in, want_out)
     assert [c for _, _, cs in gathered for c in cs] == want_crc
     assert abs(el - 0.1 * world) < 1e-9
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`bench.py --gpus 2` (no launcher in the environment) must start 2 ranks
+    itself and report n_gpus == 2 with the collectives' aggregate: a run that
+    ignored --gpus would print n_gpus 1 and only rank 0's bytes."""
+    import json
+    import subprocess
+    import sys
+    import zlib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    per_gpu, nbytes = 3, 20000
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--cpu-dry-run",
+                        "--buffers", str(per_gpu), "--buffer-bytes", str(nbytes), "--steps", "1",
+                        "--warmup", "0"], capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([s for s in r.stdout.splitlines() if s.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["world_size_seen"] == 2
+    assert line["config"]["collective_backend"] == "gloo"
+    from zhelpers import Oracle
+    o = Oracle()
+    for rank, pr in enumerate(line["per_rank"]):
+        ob, dg = 0, 0
+        for g in range(rank * per_gpu, (rank + 1) * per_gpu):
+            z = o.compress(datagen.mix(nbytes, g), 6)[1]
+            ob += len(z)
+            dg ^= zlib.crc32(z)
+        assert pr["out_bytes"] == ob and pr["stream_crc_xor"] == "%08x" % dg
+    want_ratio = 2 * per_gpu * nbytes / sum(p["out_bytes"] for p in line["per_rank"])
+    assert abs(line["compression_ratio"] - want_ratio) < 1e-3
+
+
+def test_bench_rejects_mismatched_world():
+    """Under a launcher, --gpus must equal WORLD_SIZE (no silent 1-GPU run)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4", "--cpu-dry-run",
+                        "--buffers", "1", "--buffer-bytes", "1000"], capture_output=True, text=True,
+                       timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stderr + r.stdout)

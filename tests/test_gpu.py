@@ -365,3 +365,144 @@ def test_small_single_buffers_tile_segments(zg, oracle):
                 assert st == 0 and z == oracle.compress(b, level)[1], (len(b), level)
         rc, z = zg.compress2(bufs[-1], level=6)
         assert rc == 0 and z == oracle.compress(bufs[-1], 6)[1]
+
+
+def test_wasm_production_entry_points(zg, oracle):
+    """The reference's production path: Zlib.compress -> zlib_compress_buffer,
+    and the zlib_crc32 / zlib_adler32 exports (src/wasm_module.c:35,66,74),
+    including their argument checks (null / zero length -> Z_STREAM_ERROR,
+    level outside 0..9 -> the default level)."""
+    L = zg.load()
+    L.zlib_compress_buffer.restype = C.c_int
+    L.zlib_compress_buffer.argtypes = [C.c_char_p, C.c_ulong, C.c_void_p, C.POINTER(C.c_ulong), C.c_int]
+    L.zlib_crc32.restype = C.c_ulong
+    L.zlib_crc32.argtypes = [C.c_ulong, C.c_char_p, C.c_uint]
+    L.zlib_adler32.restype = C.c_ulong
+    L.zlib_adler32.argtypes = [C.c_ulong, C.c_char_p, C.c_uint]
+    for i, (kind, n) in enumerate([("text", 65536), ("mix", 300000), ("runs", 1000), ("random", 70000)]):
+        data = datagen.make(kind, n, 40 + i)
+        for level, want_level in ((1, 1), (6, 6), (9, 9), (-1, 6), (12, 6)):
+            out = C.create_string_buffer(zg.compress_bound(n))
+            olen = C.c_ulong(len(out))
+            assert L.zlib_compress_buffer(data, n, out, C.byref(olen), level) == 0
+            assert out.raw[:olen.value] == oracle.compress(data, want_level)[1], (kind, level)
+        assert L.zlib_crc32(0, data, n) == oracle.crc32(data)
+        assert L.zlib_crc32(0x12345678, data, n) == oracle.crc32(data, 0x12345678)
+        assert L.zlib_adler32(1, data, n) == oracle.adler32(data)
+    out = C.create_string_buffer(64)
+    olen = C.c_ulong(64)
+    assert L.zlib_compress_buffer(None, 10, out, C.byref(olen), 6) == -2
+    assert L.zlib_compress_buffer(b"abc", 0, out, C.byref(olen), 6) == -2
+    olen = C.c_ulong(5)                                   # short output: zlib's Z_BUF_ERROR
+    assert L.zlib_compress_buffer(datagen.text(5000, 1), 5000, out, C.byref(olen), 6) == -5
+
+
+def test_concurrent_host_threads(zg, oracle):
+    """Host threads each lease their own context/stream (zlib.h:150-151): 8
+    threads running compress2 / crc32 / uncompress side by side get the same
+    results as one thread."""
+    import concurrent.futures as cf
+    datas = [datagen.make(k, 50000 + 7919 * i, 300 + i)
+             for i, k in enumerate(["text", "mix", "runs", "four"] * 6)]
+    want = [oracle.compress(d, 6)[1] for d in datas]
+
+    def work(i):
+        d = datas[i]
+        rc, z = zg.compress2(d, 6)
+        c = zg.crc32(d)
+        u = zg.uncompress2(z, len(d))
+        return rc, z, c, u
+
+    with cf.ThreadPoolExecutor(8) as ex:
+        res = list(ex.map(work, range(len(datas))))
+    for d, w, (rc, z, c, u) in zip(datas, want, res):
+        assert rc == 0 and z == w
+        assert c == oracle.crc32(d)
+        assert u[0] == 0 and u[1] == d
+
+
+def test_bench_golden_device_generated(zg):
+    """The benchmark's workloads end to end on the device: each golden case's
+    input is generated in HBM by zgpu_generate_dev (its sha256 pins the device
+    generator to the host build the fixtures came from), compressed by
+    zgpu_deflate_batch_dev at the config's level, and the stream must equal
+    the compiled reference's: C4 L6 (bench seed and indices up to 262143), C3
+    L1, and C5's 16 MiB small-vocabulary / 4-letter / runs buffers at L9 with
+    the Adler-32 trailer."""
+    import hashlib
+    import json
+    import os
+    import torch
+    here = os.path.dirname(os.path.abspath(__file__))
+    g = json.load(open(os.path.join(here, "golden", "bench_golden.json")))
+    for c in g["cases"]:
+        n = c["n"]
+        src = torch.empty(n, dtype=torch.uint8, device="cuda")
+        zg.generate_dev(src, n, 1, c["kind"], seed=c["seed"], first_index=c["index"])
+        host = src.cpu().numpy().tobytes()
+        assert hashlib.sha256(host).hexdigest() == c["input_sha256"], c["name"]
+        cap = (zg.compress_bound(n) + 15) // 16 * 16
+        dst = torch.empty(cap, dtype=torch.uint8, device="cuda")
+        z64 = lambda v: torch.tensor([v], dtype=torch.int64, device="cuda")  # noqa: E731
+        dlen, st = z64(0), torch.tensor([99], dtype=torch.int32, device="cuda")
+        zg.deflate_batch_dev(src, z64(0), z64(n), dst, z64(0), z64(cap), dlen, st, level=c["level"])
+        torch.cuda.synchronize()
+        assert int(st.item()) == 0
+        z = dst[:int(dlen.item())].cpu().numpy().tobytes()
+        assert len(z) == c["len"] and hashlib.sha256(z).hexdigest() == c["sha256"], \
+            (c["name"], c["kind"], c["index"])
+        out = torch.zeros(2, dtype=torch.int32, device="cuda")
+        zg.adler32_batch_dev(src, z64(0), z64(n), out[:1])
+        zg.crc32_batch_dev(src, z64(0), z64(n), out[1:])
+        a, cr = (int(x) & 0xffffffff for x in out.cpu().tolist())
+        assert a == c["adler32"] and cr == c["crc32"], c["name"]
+
+
+def test_literal_block_count_golden(zg):
+    """All-literal inputs of 16383*k bytes (no 3-byte string repeats): blocks
+    cut at exactly 16383 symbols (deflate.h:371), levels 1/6/9."""
+    import hashlib
+    import json
+    import os
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, "golden"))
+    from make_bench_golden import literal_input
+    g = json.load(open(os.path.join(here, "golden", "bench_golden.json")))
+    for level in (1, 6, 9):
+        bufs = [literal_input(e["n"]) for e in g["literal_blocks"]]
+        res = zg.compress_batch(bufs, level=level)
+        for e, (st, z) in zip(g["literal_blocks"], res):
+            assert st == 0 and hashlib.sha256(z).hexdigest() == e["levels"][str(level)]["sha256"], (e["k"], level)
+
+
+def test_checksum_split_few_large_buffers(zg, oracle):
+    """Few large buffers take the split checksum kernels (row ranges per wave,
+    joined per buffer): ragged lengths around the split boundaries, random
+    inits, against the oracle."""
+    import torch
+    rng = np.random.default_rng(11)
+    lens = [0, 1, 3, 4, 15, 16, 17, 4095, 4096, 4097, 65536 * 3 + 7, (1 << 20) + 1, 5 * (1 << 20) + 12345,
+            16 << 20, (16 << 20) - 1]
+    offs, pos = [], 0
+    for n in lens:
+        offs.append(pos)
+        pos += n + 1 + int(rng.integers(0, 7))
+    host = np.frombuffer(datagen.random_bytes(pos + 16, 2), dtype=np.uint8)
+    src = torch.from_numpy(host.copy()).cuda()
+    off = torch.tensor(offs, dtype=torch.int64).cuda()
+    ln = torch.tensor(lens, dtype=torch.int64).cuda()
+    ci = [int(x) for x in rng.integers(0, 1 << 32, len(lens), dtype=np.uint64)]
+    ai = [int(a) | (int(b) << 16) for a, b in zip(rng.integers(0, 65521, len(lens)), rng.integers(0, 65521, len(lens)))]
+    cin = torch.tensor(np.array(ci, dtype=np.uint32).view(np.int32)).cuda()
+    ain = torch.tensor(np.array(ai, dtype=np.uint32).view(np.int32)).cuda()
+    oc = torch.zeros(len(lens), dtype=torch.int32).cuda()
+    oa = torch.zeros(len(lens), dtype=torch.int32).cuda()
+    zg.crc32_batch_dev(src, off, ln, oc, init=cin)
+    zg.adler32_batch_dev(src, off, ln, oa, init=ain)
+    torch.cuda.synchronize()
+    gc, ga = oc.cpu().numpy().view(np.uint32), oa.cpu().numpy().view(np.uint32)
+    for i, n in enumerate(lens):
+        b = host[offs[i]:offs[i] + n].tobytes()
+        assert int(gc[i]) == oracle.crc32(b, ci[i]), n
+        assert int(ga[i]) == oracle.adler32(b, ai[i]), n

@@ -331,3 +331,32 @@ def test_oracle_stored_calls_vs_reference(oracle):
         sts, lens, whole = ref.deflate_calls(data, calls, 0, wb, 0)
         rc, osts, olens, got = oracle.deflate_stored_calls(data, calls, {15: 1, -15: 0, 31: 2}[wb])
         assert rc == 0 and osts == sts and olens == lens and got == whole, (t, n, wb)
+
+
+def test_oracle_vs_bench_golden(oracle):
+    """The benchmark's own inputs (host build of the device generator) and the
+    oracle's streams for them, against the compiled reference's fixtures:
+    C4 L6 Silesia-style buffers at bench.py's seed/indices, C3 L1, and C5's
+    three 16 MiB kinds at L9, plus the all-literal
+    16383*k block-count case."""
+    import hashlib
+    import json
+    import os
+    here = os.path.dirname(os.path.abspath(__file__))
+    g = json.load(open(os.path.join(here, "golden", "bench_golden.json")))
+    for c in g["cases"]:
+        data = oracle.generate(c["n"], 1, c["kind"], c["seed"], c["index"])[0]
+        assert hashlib.sha256(data).hexdigest() == c["input_sha256"], c["name"]
+        assert oracle.adler32(data) == c["adler32"] and oracle.crc32(data) == c["crc32"]
+        rc, z = oracle.compress(data, c["level"])
+        assert rc == 0 and len(z) == c["len"] and hashlib.sha256(z).hexdigest() == c["sha256"], \
+            (c["name"], c["kind"], c["index"])
+    import sys
+    sys.path.insert(0, os.path.join(here, "golden"))
+    from make_bench_golden import literal_input
+    for e in g["literal_blocks"]:
+        data = literal_input(e["n"])
+        assert hashlib.sha256(data).hexdigest() == e["input_sha256"]
+        for level, want in e["levels"].items():
+            rc, z = oracle.compress(data, int(level))
+            assert rc == 0 and hashlib.sha256(z).hexdigest() == want["sha256"], (e["k"], level)

@@ -58,7 +58,17 @@ class Oracle:
         L.zo_pp_links.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
         L.zo_pp_match.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_void_p,
                                   C.c_void_p, C.c_void_p]
+        L.zo_generate.restype = C.c_int
+        L.zo_generate.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_int, C.c_uint64, C.c_uint64]
         self.L = L
+
+    def generate(self, length, count, kind, seed, first_index=0):
+        """The bytes zgpu_generate_dev(kind, seed, first_index) writes (host
+        build of zgpu_gen.h): a list of `count` buffers of `length` bytes."""
+        import numpy as np
+        buf = np.zeros(length * count + 4, dtype=np.uint8)
+        assert self.L.zo_generate(buf.ctypes.data, length, count, kind, seed, first_index) == 0
+        return [buf[i * length:(i + 1) * length].tobytes() for i in range(count)]
 
     def _compress(self, fn, data, level, wrap, cap):
         data = bytes(data)

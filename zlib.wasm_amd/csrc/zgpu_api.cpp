@@ -12,6 +12,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -206,12 +208,11 @@ struct StageTimer {
 };
 
 struct Ctx {
-    std::mutex mu;
-    StageTimer timer;
-    int state = 0;            // 0 uninit, 1 ok, -1 failed
+    bool busy = false;
     int device = 0;
-    std::string info;
-    CrcTables *d_crc = nullptr;
+    hipStream_t own = nullptr;   // the stream of the host-buffer entry points
+    StageTimer timer;
+    uint64_t timer_epoch = 0;
     size_t inflight = size_t(1) << 30;
     DevBuf ws_link, ws_rf, ws_rq, ws_sym, ws_blk, ws_meta, ws_heads, ws_io, ws_io2, ws_small, ws_state;
     // second workspace slot and stream for the L4-9 pipeline (k_match of
@@ -222,60 +223,141 @@ struct Ctx {
     DevBuf ws_stg;            // k_parse_seg's symbol staging (caller's stream only)
     DevBuf ws_help;           // the a18 helpers' staging (zlib_*_simd)
     DevBuf ws_seg;            // k_match segments of sub-batches of few large buffers
+    DevBuf ws_ck;             // split checksum partials (few large buffers)
     // inflate: match records, per-stream results, checks, offsets, stop codes
     DevBuf ws_mrec, ws_irec, ws_ick, ws_imeta, ws_istop;
     hipStream_t aux = nullptr;
     hipEvent_t ev_links[2] = {nullptr, nullptr}, ev_match[2] = {nullptr, nullptr};
 };
 
-Ctx &ctx() {
-    static Ctx c;
-    return c;
+// One entry per HIP device: its static tables and a pool of contexts.  A call
+// leases a free context of the caller's current device (creating one, up to
+// kMaxCtx, when all are busy), so host threads run side by side on their own
+// streams and workspaces instead of queueing on one lock (zlib.h:150-151:
+// zlib is thread-safe).
+constexpr int kMaxDevices = 64;
+constexpr size_t kMaxCtx = 8;
+struct Device {
+    std::mutex mu;
+    std::condition_variable cv;
+    int state = 0;            // 0 uninit, 1 ok, -1 failed
+    std::string info;
+    CrcTables *d_crc = nullptr;
+    std::vector<std::unique_ptr<Ctx>> pool;
+};
+Device g_dev[kMaxDevices];
+std::atomic<size_t> g_inflight{size_t(1) << 30};
+std::atomic<bool> g_timing{false};
+std::atomic<uint64_t> g_timing_epoch{0};
+std::atomic<bool> g_nodev_said{false};
+
+int nodev(const char *why) {
+    if (!g_nodev_said.exchange(true))
+        std::fprintf(stderr, "libzgpu: %s; the GPU path cannot run (no CPU fallback)\n", why);
+    return ZGPU_ENODEV;
 }
 
-const CrcTables *g_dev_crc = nullptr;
-
-int init_locked(Ctx &c) {
-    if (c.state == 1) return ZGPU_OK;
-    if (c.state == -1) return ZGPU_ENODEV;
+int current_device(int *d) {
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
-        std::fprintf(stderr, "libzgpu: no HIP device available; the GPU path cannot run\n");
-        c.state = -1;
-        return ZGPU_ENODEV;
-    }
-    (void)hipGetDevice(&c.device);
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, c.device) != hipSuccess) { c.state = -1; return ZGPU_ENODEV; }
-    c.info = std::string("libzgpu gfx950 build; device ") + std::to_string(c.device) + ": " +
-             prop.name + " (" + prop.gcnArchName + "), " + std::to_string(prop.multiProcessorCount) +
-             " CUs";
-    CodeTables ct;
-    build_code_tables(ct);
-    static CrcTables crc;
-    build_crc_tables(crc);
-    if (launch_tables_upload(&ct, &crc) != 0) { c.state = -1; return ZGPU_ENODEV; }
-    if (hipMalloc(&c.d_crc, sizeof(CrcTables)) != hipSuccess) { c.state = -1; return ZGPU_ENODEV; }
-    if (hipMemcpy(c.d_crc, &crc, sizeof(CrcTables), hipMemcpyHostToDevice) != hipSuccess) {
-        c.state = -1;
-        return ZGPU_ENODEV;
-    }
-    g_dev_crc = c.d_crc;
-    if (const char *e = std::getenv("ZGPU_INFLIGHT_MB")) c.inflight = size_t(std::atoll(e)) << 20;
-    c.state = 1;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return nodev("no HIP device available");
+    if (hipGetDevice(d) != hipSuccess || *d < 0 || *d >= kMaxDevices) return nodev("no current HIP device");
     return ZGPU_OK;
 }
 
-int ensure_init() {
-    Ctx &c = ctx();
-    std::lock_guard<std::mutex> g(c.mu);
-    return init_locked(c);
+// first use of device d (D.mu held, d current)
+int init_device_locked(Device &D, int d) {
+    if (D.state == 1) return ZGPU_OK;
+    if (D.state == -1) return ZGPU_ENODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, d) != hipSuccess) { D.state = -1; return nodev("device query failed"); }
+    D.info = std::string("libzgpu gfx950 build; device ") + std::to_string(d) + ": " + prop.name + " (" +
+             prop.gcnArchName + "), " + std::to_string(prop.multiProcessorCount) + " CUs";
+    CodeTables ct;
+    build_code_tables(ct);
+    static CrcTables crc;
+    static std::once_flag crc_once;
+    std::call_once(crc_once, [] { build_crc_tables(crc); });
+    if (launch_tables_upload(&ct, &crc) != 0 || hipMalloc(&D.d_crc, sizeof(CrcTables)) != hipSuccess ||
+        hipMemcpy(D.d_crc, &crc, sizeof(CrcTables), hipMemcpyHostToDevice) != hipSuccess) {
+        D.state = -1;
+        return nodev("table upload failed");
+    }
+    static std::once_flag env_once;
+    std::call_once(env_once, [] {
+        if (const char *e = std::getenv("ZGPU_INFLIGHT_MB")) g_inflight = size_t(std::atoll(e)) << 20;
+    });
+    D.state = 1;
+    return ZGPU_OK;
 }
+
+// RAII lease of a context on the caller's current device; rc != 0: no context
+struct Lease {
+    Ctx *c = nullptr;
+    Device *D = nullptr;
+    int rc = ZGPU_ENODEV;
+    Lease() {
+        int d = 0;
+        if ((rc = current_device(&d))) return;
+        D = &g_dev[d];
+        std::unique_lock<std::mutex> g(D->mu);
+        if ((rc = init_device_locked(*D, d))) return;
+        for (;;) {
+            for (auto &p : D->pool)
+                if (!p->busy) { c = p.get(); break; }
+            if (c) break;
+            if (D->pool.size() < kMaxCtx) {
+                auto p = std::make_unique<Ctx>();
+                p->device = d;
+                if (hipStreamCreateWithFlags(&p->own, hipStreamNonBlocking) != hipSuccess) {
+                    rc = ZGPU_MEM_ERROR;
+                    return;
+                }
+                D->pool.push_back(std::move(p));
+                c = D->pool.back().get();
+                break;
+            }
+            D->cv.wait(g);
+        }
+        c->busy = true;
+        c->inflight = g_inflight;
+        const uint64_t ep = g_timing_epoch;
+        if (c->timer_epoch != ep) {        // zgpu_stage_timing(1) since this context last ran
+            for (int i = 0; i < kStages; i++) { c->timer.ms[i] = 0; c->timer.n[i] = 0; }
+            c->timer.pending.clear();
+            c->timer.used = 0;
+            c->timer_epoch = ep;
+        }
+        c->timer.on = g_timing;
+        rc = ZGPU_OK;
+    }
+    ~Lease() {
+        if (!c) return;
+        std::lock_guard<std::mutex> g(D->mu);
+        c->busy = false;
+        D->cv.notify_one();
+    }
+    Lease(const Lease &) = delete;
+    Lease &operator=(const Lease &) = delete;
+};
+
+int ensure_init() {
+    int d = 0;
+    if (int rc = current_device(&d)) return rc;
+    std::lock_guard<std::mutex> g(g_dev[d].mu);
+    return init_device_locked(g_dev[d], d);
+}
+
+// blocking copy on the context's stream (the stream is non-blocking, so a
+// plain hipMemcpy on the null stream would not wait for its kernels)
+inline bool copy_sync_ok(void *d, const void *src, size_t n, hipMemcpyKind k, hipStream_t st) {
+    return hipMemcpyAsync(d, src, n, k, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
+}
+#define copy_sync(d, src, n, k, st) (copy_sync_ok((d), (src), (n), (k), (st)) ? hipSuccess : hipErrorUnknown)
 
 inline int hip_ok(hipError_t e) { return e == hipSuccess ? ZGPU_OK : ZGPU_MEM_ERROR; }
 
 // ------------------------------------------------------------------------
-// deflate orchestration (caller holds ctx().mu)
+// deflate orchestration (caller holds a Lease on c)
 // ------------------------------------------------------------------------
 // The deflate(flush) calls of a streaming job (device arrays, see DeflateJob).
 struct FlushSpec {
@@ -309,6 +391,8 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     if (hipMemcpyAsync(lens.data(), src_len, 8ull * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
         return ZGPU_MEM_ERROR;
+    for (uint32_t i = 0; i < count; i++)
+        if (lens[i] >= kMaxBuffer) return ZGPU_STREAM_ERROR;   // 32-bit positions in the kernels
 
     // plan sub-batches: Σ n <= budget (a single larger buffer runs alone).  L1-3
     // keep ~6 B of workspace per in-flight byte (L4-9: ~25) and their parse is
@@ -352,6 +436,8 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     static const bool no_pipe = std::getenv("ZGPU_NO_PIPELINE") != nullptr;
     const bool piped = slow && nsub > 1 && !no_pipe;
     if (!c.ws_meta.ensure(16ull * count + 8ull * max_cnt * 2)) return ZGPU_MEM_ERROR;
+    const size_t ckb = checksum_scratch_bytes(max_cnt);     // trailer checksums of few large buffers
+    void *ck = ckb && c.ws_ck.ensure(ckb) ? c.ws_ck.p : nullptr;
     if (!c.ws_link.ensure(2 * max_pos + 64)) return ZGPU_MEM_ERROR;
     if (!c.ws_sym.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
     if (!c.ws_blk.ensure(sizeof(BlockRec) * max_blk)) return ZGPU_MEM_ERROR;
@@ -384,7 +470,8 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     // the sub-batch's bytes over the 256 CUs, in whole 4 KiB tiles, at most
     // 256 KiB: a lone 64 KiB compress2 walks 16 one-tile segments side by side
     // instead of 16 tiles in a row (each segment stages <= 32 KiB it does not walk).
-    constexpr uint64_t kSegMax = 256 * 1024, kSegTile = 4096, kSegCUs = 256;
+    constexpr uint64_t kSegMax = 256 * 1024, kSegTile = kMatchTile, kSegCUs = 256;
+    static_assert(kSegMax % kSegTile == 0, "segments are whole k_match tiles");
     std::vector<uint32_t> segs;
     std::vector<size_t> seg_at(nsub + 1, 0), seg_len(nsub, kSegMax);
     for (size_t sb = 0; sb < nsub; sb++) {
@@ -479,9 +566,9 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         const uint32_t a = cuts[s], b = cuts[s + 1];
         int rc = 0;
         if (wrap == 1)
-            rc = T.run(0, st, [&] { return launch_adler32(src, src_off + a, src_len + a, nullptr, d_check, b - a, nullptr, 0, st); });
+            rc = T.run(0, st, [&] { return launch_adler32(src, src_off + a, src_len + a, nullptr, d_check, b - a, ck, ckb, st); });
         else if (wrap == 2)
-            rc = T.run(0, st, [&] { return launch_crc32(src, src_off + a, src_len + a, nullptr, d_check, b - a, nullptr, 0, st); });
+            rc = T.run(0, st, [&] { return launch_crc32(src, src_off + a, src_len + a, nullptr, d_check, b - a, ck, ckb, st); });
         if (rc) return ZGPU_MEM_ERROR;
         if ((huff || rle) && fs) {
             if (T.run(4, st, [&] { return launch_deflate_stage(10, job, nullptr, st); })) return ZGPU_MEM_ERROR;
@@ -566,6 +653,8 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
                          size_t *dst_len, int *status, size_t count, int level, int wrap, int strategy,
                          FlushHost *fh = nullptr) {
     if (count == 0) return ZGPU_OK;
+    for (size_t i = 0; i < count; i++)
+        if (src_len[i] >= kMaxBuffer) return ZGPU_STREAM_ERROR;
     std::vector<uint64_t> so(count), sl(count), dofs(count), dcap(count);
     uint64_t in_total = 0, out_total = 0;
     for (size_t i = 0; i < count; i++) {
@@ -585,7 +674,7 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
     uint64_t *d_so = c.ws_small.as<uint64_t>();
     uint64_t *d_sl = d_so + count, *d_do = d_sl + count, *d_dc = d_do + count, *d_dl = d_dc + count;
     int32_t *d_st = reinterpret_cast<int32_t *>(d_dl + count);
-    hipStream_t st = nullptr;
+    hipStream_t st = c.own;
     static const bool poison = std::getenv("ZGPU_POISON") != nullptr;   // debug, see deflate_dev_locked
     if (poison) {
         static int round = 0;
@@ -617,24 +706,24 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
     int rc = deflate_dev_locked(c, d_in, d_so, d_sl, d_out, d_do, d_dc, d_dl, d_st, (uint32_t)count,
                                 level, wrap, strategy, st, fh ? &fs : nullptr);
     if (rc) return rc;
-    if (fh && hipMemcpy(fh->out, fs.out, 32, hipMemcpyDeviceToHost) != hipSuccess)
+    if (fh && copy_sync(fh->out, fs.out, 32, hipMemcpyDeviceToHost, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
     if (fh && fh->head_out && fh->n) {
         const uint64_t S = fh->out[2], end = fh->pos[fh->n - 1];
         fh->head_out->resize(32768);
         fh->prev_out->resize(end > S ? end - S : 0);
-        if (hipMemcpy(fh->head_out->data(), c.ws_heads.p, 4ull * 32768, hipMemcpyDeviceToHost) != hipSuccess ||
-            (end > S && hipMemcpy(fh->prev_out->data(), c.ws_link.as<uint16_t>() + S, 2 * (end - S),
-                                  hipMemcpyDeviceToHost) != hipSuccess))
+        if (copy_sync(fh->head_out->data(), c.ws_heads.p, 4ull * 32768, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            (end > S && copy_sync(fh->prev_out->data(), c.ws_link.as<uint16_t>() + S, 2 * (end - S),
+                                  hipMemcpyDeviceToHost, st) != hipSuccess))
             return ZGPU_MEM_ERROR;
     }
     std::vector<uint64_t> ol(count);
     std::vector<int32_t> os(count);
-    if (hipMemcpy(ol.data(), d_dl, 8 * count, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(os.data(), d_st, 4 * count, hipMemcpyDeviceToHost) != hipSuccess)
+    if (copy_sync(ol.data(), d_dl, 8 * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        copy_sync(os.data(), d_st, 4 * count, hipMemcpyDeviceToHost, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
     for (size_t i = 0; i < count; i++) {
-        if (ol[i] && hipMemcpy(dst[i], d_out + dofs[i], ol[i], hipMemcpyDeviceToHost) != hipSuccess)
+        if (ol[i] && copy_sync(dst[i], d_out + dofs[i], ol[i], hipMemcpyDeviceToHost, st) != hipSuccess)
             return ZGPU_MEM_ERROR;
         dst_len[i] = ol[i];
         if (status) status[i] = os[i];
@@ -643,7 +732,7 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
 }
 
 // ------------------------------------------------------------------------
-// inflate orchestration (caller holds ctx().mu).  Sub-batches keep the sum of
+// inflate orchestration (caller holds a Lease on c).  Sub-batches keep the sum of
 // output capacities within the in-flight budget; each stream gets cap/3 + 2
 // match records (a match writes >= 3 bytes, the last one may be cut short).
 // stop_out (device, optional): InflateStop per stream.
@@ -681,6 +770,8 @@ int inflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         max_rec = std::max(max_rec, acc);
         max_cnt = std::max(max_cnt, cuts[s + 1] - cuts[s]);
     }
+    const size_t ckb = checksum_scratch_bytes(max_cnt);
+    void *ck = ckb && c.ws_ck.ensure(ckb) ? c.ws_ck.p : nullptr;
     if (!c.ws_mrec.ensure(8 * max_rec + 64) || !c.ws_irec.ensure(sizeof(InflateRec) * max_cnt + 64) ||
         !c.ws_ick.ensure(8ull * max_cnt + 64) || !c.ws_imeta.ensure(8ull * count + 64))
         return ZGPU_MEM_ERROR;
@@ -704,10 +795,10 @@ int inflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         if (T.run(3, st, [&] { return launch_inflate_stage(0, job, st); })) return ZGPU_MEM_ERROR;
         if (T.run(4, st, [&] { return launch_inflate_stage(1, job, st); })) return ZGPU_MEM_ERROR;
         if ((wrap & 1) && T.run(0, st, [&] {
-                return launch_adler32(dst, dst_off + a, dst_len + a, nullptr, job.adler, b - a, nullptr, 0, st); }))
+                return launch_adler32(dst, dst_off + a, dst_len + a, nullptr, job.adler, b - a, ck, ckb, st); }))
             return ZGPU_MEM_ERROR;
         if ((wrap & 2) && T.run(0, st, [&] {
-                return launch_crc32(dst, dst_off + a, dst_len + a, nullptr, job.crc, b - a, nullptr, 0, st); }))
+                return launch_crc32(dst, dst_off + a, dst_len + a, nullptr, job.crc, b - a, ck, ckb, st); }))
             return ZGPU_MEM_ERROR;
         if (T.run(5, st, [&] { return launch_inflate_stage(2, job, st); })) return ZGPU_MEM_ERROR;
     }
@@ -742,7 +833,7 @@ int uncompress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_
     uint64_t *d_used = d_dl + count;
     int32_t *d_st = reinterpret_cast<int32_t *>(d_used + count);
     uint32_t *d_stop = c.ws_istop.as<uint32_t>();
-    hipStream_t st = nullptr;
+    hipStream_t st = c.own;
     for (size_t i = 0; i < count; i++)
         if (src_len[i] && hipMemcpyAsync(d_in + so[i], src[i], src_len[i], hipMemcpyHostToDevice, st) != hipSuccess)
             return ZGPU_MEM_ERROR;
@@ -757,13 +848,13 @@ int uncompress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_
     std::vector<uint64_t> ol(count), ou(count);
     std::vector<int32_t> os(count);
     std::vector<uint32_t> ostop(count);
-    if (hipMemcpy(ol.data(), d_dl, 8 * count, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(ou.data(), d_used, 8 * count, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(os.data(), d_st, 4 * count, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(ostop.data(), d_stop, 4 * count, hipMemcpyDeviceToHost) != hipSuccess)
+    if (copy_sync(ol.data(), d_dl, 8 * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        copy_sync(ou.data(), d_used, 8 * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        copy_sync(os.data(), d_st, 4 * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        copy_sync(ostop.data(), d_stop, 4 * count, hipMemcpyDeviceToHost, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
     for (size_t i = 0; i < count; i++) {
-        if (ol[i] && hipMemcpy(dst[i], d_out + dofs[i], ol[i], hipMemcpyDeviceToHost) != hipSuccess)
+        if (ol[i] && copy_sync(dst[i], d_out + dofs[i], ol[i], hipMemcpyDeviceToHost, st) != hipSuccess)
             return ZGPU_MEM_ERROR;
         dst_len[i] = ol[i];
         if (src_used) src_used[i] = ou[i];
@@ -809,7 +900,7 @@ int checksum_host_locked(Ctx &c, bool is_crc, const uint8_t *const *src, const s
     std::vector<uint32_t> pinit(np, is_crc ? 0u : 1u);
     for (size_t i = 0; i < count; i++)
         if (init) pinit[first[i]] = init[i];
-    hipStream_t st = nullptr;
+    hipStream_t st = c.own;
     for (size_t k = 0; k < np; k++)
         if (pieces[k].len &&
             hipMemcpyAsync(d_in + po[k], src[pieces[k].buf] + pieces[k].off, pieces[k].len,
@@ -819,11 +910,13 @@ int checksum_host_locked(Ctx &c, bool is_crc, const uint8_t *const *src, const s
         hipMemcpyAsync(d_pl, pl.data(), 8 * np, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(d_init, pinit.data(), 4 * np, hipMemcpyHostToDevice, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
-    int rc = is_crc ? launch_crc32(d_in, d_po, d_pl, d_init, d_out, (uint32_t)np, nullptr, 0, st)
-                    : launch_adler32(d_in, d_po, d_pl, d_init, d_out, (uint32_t)np, nullptr, 0, st);
+    const size_t ckb = checksum_scratch_bytes((uint32_t)np);
+    void *ck = ckb && c.ws_ck.ensure(ckb) ? c.ws_ck.p : nullptr;
+    int rc = is_crc ? launch_crc32(d_in, d_po, d_pl, d_init, d_out, (uint32_t)np, ck, ckb, st)
+                    : launch_adler32(d_in, d_po, d_pl, d_init, d_out, (uint32_t)np, ck, ckb, st);
     if (rc) return ZGPU_MEM_ERROR;
     std::vector<uint32_t> res(np);
-    if (hipMemcpy(res.data(), d_out, 4 * np, hipMemcpyDeviceToHost) != hipSuccess) return ZGPU_MEM_ERROR;
+    if (copy_sync(res.data(), d_out, 4 * np, hipMemcpyDeviceToHost, st) != hipSuccess) return ZGPU_MEM_ERROR;
     for (size_t i = 0; i < count; i++) {
         uint32_t v = res[first[i]];
         for (size_t k = first[i] + 1; k < first[i + 1]; k++)
@@ -856,7 +949,11 @@ uint64_t compress_bound64(uint64_t n) {                      // compress.c:72-75
 }  // namespace
 
 namespace zgpu {
-const CrcTables *device_crc_tables() { return g_dev_crc; }
+const CrcTables *device_crc_tables() {
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= kMaxDevices) return nullptr;
+    return g_dev[d].d_crc;
+}
 }  // namespace zgpu
 
 // ==========================================================================
@@ -867,38 +964,42 @@ extern "C" {
 int zgpu_init(void) { return ensure_init(); }
 
 const char *zgpu_info(void) {
-    Ctx &c = ctx();
-    std::lock_guard<std::mutex> g(c.mu);
-    if (init_locked(c) != ZGPU_OK) return "libzgpu: no GPU";
-    return c.info.c_str();
+    int d = 0;
+    if (current_device(&d)) return "libzgpu: no GPU";
+    Device &D = g_dev[d];
+    std::lock_guard<std::mutex> g(D.mu);
+    if (init_device_locked(D, d) != ZGPU_OK) return "libzgpu: no GPU";
+    return D.info.c_str();
 }
 
 size_t zgpu_set_inflight_bytes(size_t bytes) {
-    Ctx &c = ctx();
-    std::lock_guard<std::mutex> g(c.mu);
-    size_t old = c.inflight;
-    if (bytes >= (1u << 20)) c.inflight = bytes;
+    size_t old = g_inflight;
+    if (bytes >= (1u << 20)) g_inflight = bytes;
     return old;
 }
 
 void zgpu_stage_timing(int enable) {
-    Ctx &c = ctx();
-    std::lock_guard<std::mutex> g(c.mu);
-    c.timer.on = enable != 0;
-    if (enable) {
-        for (int i = 0; i < kStages; i++) { c.timer.ms[i] = 0; c.timer.n[i] = 0; }
-        c.timer.pending.clear();
-        c.timer.used = 0;
-    }
+    if (enable) g_timing_epoch++;
+    g_timing = enable != 0;
 }
 
+// sums over every context of every device (read after the timed work ended)
 int zgpu_stage_timing_read(double *ms, uint64_t *launches, int nstages) {
-    Ctx &c = ctx();
-    std::lock_guard<std::mutex> g(c.mu);
     int k = nstages < kStages ? nstages : kStages;
     for (int i = 0; i < k; i++) {
-        if (ms) ms[i] = c.timer.ms[i];
-        if (launches) launches[i] = c.timer.n[i];
+        if (ms) ms[i] = 0;
+        if (launches) launches[i] = 0;
+    }
+    const uint64_t ep = g_timing_epoch;
+    for (auto &D : g_dev) {
+        std::lock_guard<std::mutex> g(D.mu);
+        for (auto &p : D.pool) {
+            if (p->timer_epoch != ep) continue;
+            for (int i = 0; i < k; i++) {
+                if (ms) ms[i] += p->timer.ms[i];
+                if (launches) launches[i] += p->timer.n[i];
+            }
+        }
     }
     return k;
 }
@@ -907,10 +1008,9 @@ int zgpu_deflate_batch_dev_ex(const uint8_t *src, const uint64_t *src_off, const
                               uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
                               uint64_t *dst_len, int32_t *status, uint32_t count, int level, int wrap,
                               int strategy, void *stream) {
-    Ctx &c = ctx();
-    std::lock_guard<std::mutex> g(c.mu);
-    int rc = init_locked(c);
-    if (rc) return rc;
+    Lease L;
+    if (L.rc) return L.rc;
+    Ctx &c = *L.c;
     return deflate_dev_locked(c, src, src_off, src_len, dst, dst_off, dst_cap, dst_len, status,
                               count, level, wrap, strategy, static_cast<hipStream_t>(stream));
 }
@@ -925,26 +1025,31 @@ int zgpu_deflate_batch_dev(const uint8_t *src, const uint64_t *src_off, const ui
 
 int zgpu_crc32_batch_dev(const uint8_t *src, const uint64_t *off, const uint64_t *len,
                          const uint32_t *init, uint32_t *out, uint32_t count, void *stream) {
-    int rc = ensure_init();
-    if (rc) return rc;
-    return launch_crc32(src, off, len, init, out, count, nullptr, 0, static_cast<hipStream_t>(stream))
+    Lease L;
+    if (L.rc) return L.rc;
+    const size_t ckb = checksum_scratch_bytes(count);
+    void *ck = ckb && L.c->ws_ck.ensure(ckb) ? L.c->ws_ck.p : nullptr;
+    return launch_crc32(src, off, len, init, out, count, ck, ckb, static_cast<hipStream_t>(stream))
                ? ZGPU_MEM_ERROR : ZGPU_OK;
 }
 
 int zgpu_adler32_batch_dev(const uint8_t *src, const uint64_t *off, const uint64_t *len,
                            const uint32_t *init, uint32_t *out, uint32_t count, void *stream) {
-    int rc = ensure_init();
-    if (rc) return rc;
-    return launch_adler32(src, off, len, init, out, count, nullptr, 0, static_cast<hipStream_t>(stream))
+    Lease L;
+    if (L.rc) return L.rc;
+    const size_t ckb = checksum_scratch_bytes(count);
+    void *ck = ckb && L.c->ws_ck.ensure(ckb) ? L.c->ws_ck.p : nullptr;
+    return launch_adler32(src, off, len, init, out, count, ck, ckb, static_cast<hipStream_t>(stream))
                ? ZGPU_MEM_ERROR : ZGPU_OK;
 }
 
 int zgpu_compress_batch_ex(const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
                            size_t *dst_len, int *status, size_t count, int level, int wrap, int strategy) {
-    Ctx &c = ctx();
-    std::lock_guard<std::mutex> g(c.mu);
-    int rc = init_locked(c);
-    if (rc) return rc;
+    for (size_t i = 0; i < count; i++)          // checked before any GPU work (and testable without one)
+        if (src_len && src_len[i] >= kMaxBuffer) return ZGPU_STREAM_ERROR;
+    Lease L;
+    if (L.rc) return L.rc;
+    Ctx &c = *L.c;
     return compress_host_locked(c, src, src_len, dst, dst_len, status, count, level, wrap, strategy);
 }
 
@@ -957,10 +1062,9 @@ int zgpu_inflate_batch_dev(const uint8_t *src, const uint64_t *src_off, const ui
                            uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
                            uint64_t *dst_len, uint64_t *src_used, int32_t *status, uint32_t count,
                            int wrap, void *stream) {
-    Ctx &c = ctx();
-    std::lock_guard<std::mutex> g(c.mu);
-    int rc = init_locked(c);
-    if (rc) return rc;
+    Lease L;
+    if (L.rc) return L.rc;
+    Ctx &c = *L.c;
     return inflate_dev_locked(c, src, src_off, src_len, dst, dst_off, dst_cap, dst_len, src_used, status,
                               nullptr, count, wrap, 15, static_cast<hipStream_t>(stream));
 }
@@ -968,28 +1072,25 @@ int zgpu_inflate_batch_dev(const uint8_t *src, const uint64_t *src_off, const ui
 int zgpu_uncompress_batch(const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
                           size_t *dst_len, size_t *src_used, int *status, size_t count, int wrap) {
     if (wrap < 0 || wrap > 3) return ZGPU_STREAM_ERROR;
-    Ctx &c = ctx();
-    std::lock_guard<std::mutex> g(c.mu);
-    int rc = init_locked(c);
-    if (rc) return rc;
+    Lease L;
+    if (L.rc) return L.rc;
+    Ctx &c = *L.c;
     return uncompress_host_locked(c, src, src_len, dst, dst_len, src_used, status, nullptr, count, wrap, 15);
 }
 
 int zgpu_crc32_batch(const uint8_t *const *src, const size_t *len, const uint32_t *init,
                      uint32_t *out, size_t count) {
-    Ctx &c = ctx();
-    std::lock_guard<std::mutex> g(c.mu);
-    int rc = init_locked(c);
-    if (rc) return rc;
+    Lease L;
+    if (L.rc) return L.rc;
+    Ctx &c = *L.c;
     return checksum_host_locked(c, true, src, len, init, out, count);
 }
 
 int zgpu_adler32_batch(const uint8_t *const *src, const size_t *len, const uint32_t *init,
                        uint32_t *out, size_t count) {
-    Ctx &c = ctx();
-    std::lock_guard<std::mutex> g(c.mu);
-    int rc = init_locked(c);
-    if (rc) return rc;
+    Lease L;
+    if (L.rc) return L.rc;
+    Ctx &c = *L.c;
     return checksum_host_locked(c, false, src, len, init, out, count);
 }
 
@@ -1003,10 +1104,9 @@ int zgpu_generate_dev(uint8_t *dst, uint64_t len, uint32_t count, int kind, uint
 
 int zgpu_debug_stages(const uint8_t *src, size_t n, int level, uint16_t *link, uint32_t *rfull,
                       uint32_t *rquart) {
-    Ctx &c = ctx();
-    std::lock_guard<std::mutex> g(c.mu);
-    int rc = init_locked(c);
-    if (rc) return rc;
+    Lease L;
+    if (L.rc) return L.rc;
+    Ctx &c = *L.c;
     if (level < 4 || level > 9) return ZGPU_STREAM_ERROR;
     const size_t nn = n ? n : 1;
     if (!c.ws_io.ensure(nn + 64) || !c.ws_link.ensure(2 * nn + 64) || !c.ws_rf.ensure(4 * nn + 64) ||
@@ -1014,9 +1114,9 @@ int zgpu_debug_stages(const uint8_t *src, size_t n, int level, uint16_t *link, u
         return ZGPU_MEM_ERROR;
     uint64_t *d_meta = c.ws_small.as<uint64_t>();   // off, len, ws_off
     const uint64_t meta[3] = {0, (uint64_t)n, 0};
-    hipStream_t st = nullptr;
-    if (hipMemcpy(d_meta, meta, sizeof meta, hipMemcpyHostToDevice) != hipSuccess ||
-        (n && hipMemcpy(c.ws_io.p, src, n, hipMemcpyHostToDevice) != hipSuccess))
+    hipStream_t st = c.own;
+    if (copy_sync(d_meta, meta, sizeof meta, hipMemcpyHostToDevice, st) != hipSuccess ||
+        (n && copy_sync(c.ws_io.p, src, n, hipMemcpyHostToDevice, st) != hipSuccess))
         return ZGPU_MEM_ERROR;
     DeflateJob job{};
     job.src = c.ws_io.as<uint8_t>(); job.src_off = d_meta; job.src_len = d_meta + 1;
@@ -1027,11 +1127,11 @@ int zgpu_debug_stages(const uint8_t *src, size_t n, int level, uint16_t *link, u
     job.rquart = c.ws_rq.as<uint32_t>();
     job.key = c.ws_key.as<uint8_t>();
     if (launch_deflate_stage(0, job, nullptr, st) || launch_deflate_stage(1, job, nullptr, st) ||
-        hipDeviceSynchronize() != hipSuccess)
+        hipStreamSynchronize(st) != hipSuccess)
         return ZGPU_MEM_ERROR;
-    if (link && n && hipMemcpy(link, job.link, 2 * n, hipMemcpyDeviceToHost) != hipSuccess) return ZGPU_MEM_ERROR;
-    if (rfull && n && hipMemcpy(rfull, job.rfull, 4 * n, hipMemcpyDeviceToHost) != hipSuccess) return ZGPU_MEM_ERROR;
-    if (rquart && n && level >= 5 && hipMemcpy(rquart, job.rquart, 4 * n, hipMemcpyDeviceToHost) != hipSuccess)
+    if (link && n && copy_sync(link, job.link, 2 * n, hipMemcpyDeviceToHost, st) != hipSuccess) return ZGPU_MEM_ERROR;
+    if (rfull && n && copy_sync(rfull, job.rfull, 4 * n, hipMemcpyDeviceToHost, st) != hipSuccess) return ZGPU_MEM_ERROR;
+    if (rquart && n && level >= 5 && copy_sync(rquart, job.rquart, 4 * n, hipMemcpyDeviceToHost, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
     return ZGPU_OK;
 }
@@ -1046,6 +1146,7 @@ int compress2(Bytef *dest, uLongf *destLen, const Bytef *source, uLong sourceLen
     if (!destLen) return Z_STREAM_ERROR;
     if (level != Z_DEFAULT_COMPRESSION && (level < 0 || level > 9)) { *destLen = 0; return Z_STREAM_ERROR; }
     if (!dest || (sourceLen && !source)) { *destLen = 0; return Z_STREAM_ERROR; }
+    if ((uint64_t)sourceLen >= kMaxBuffer) { *destLen = 0; return Z_MEM_ERROR; }   // 32-bit kernel positions
     size_t cap = *destLen;
     const uint8_t *s = source;
     uint8_t *d = dest;
@@ -1067,8 +1168,14 @@ static uint32_t checksum_one(bool is_crc, uint32_t init, const Bytef *buf, size_
     uint32_t out = 0;
     int rc = is_crc ? zgpu_crc32_batch(&p, &len, &init, &out, 1) : zgpu_adler32_batch(&p, &len, &init, &out, 1);
     if (rc) {
-        std::fprintf(stderr, "libzgpu: %s failed on the GPU (rc %d)\n", is_crc ? "crc32" : "adler32", rc);
-        std::abort();       // no CPU fallback: fail loudly
+        // zlib's crc32()/adler32() have no error return and a library must not
+        // end its host process: report once on stderr and return 0 (the value
+        // of crc32(0, Z_NULL, 0)); there is no CPU fallback.
+        static std::atomic<bool> said{false};
+        if (!said.exchange(true))
+            std::fprintf(stderr, "libzgpu: %s failed on the GPU (rc %d); returning 0\n",
+                         is_crc ? "crc32" : "adler32", rc);
+        return 0;
     }
     return out;
 }
@@ -1202,10 +1309,9 @@ int deflate_part(internal_state *s, int open_end, std::vector<uint8_t> &body, ui
         fh.head_out = &s->job_head;
         fh.prev_out = &s->job_prev;
     }
-    Ctx &c = ctx();
-    std::lock_guard<std::mutex> g(c.mu);
-    int rc = init_locked(c);
-    if (!rc) rc = compress_host_locked(c, &sp, &sl, &dp, &cap, &st, 1, s->level, ZGPU_WRAP_RAW, s->strategy, &fh);
+    Lease L;
+    int rc = L.rc;
+    if (!rc) rc = compress_host_locked(*L.c, &sp, &sl, &dp, &cap, &st, 1, s->level, ZGPU_WRAP_RAW, s->strategy, &fh);
     if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
     body.resize(cap);
     for (int i = 0; i < 4; i++) out[i] = fh.out[i];
@@ -1286,6 +1392,7 @@ int deflate_stored_call(z_streamp strm, internal_state *s, int flush) {
     }
     queue_header(s);                                           // written by the first call
     if (strm->avail_in) {
+        if ((uint64_t)s->in.size() + strm->avail_in >= kMaxBuffer) return Z_MEM_ERROR;   // 32-bit kernel positions
         s->in.insert(s->in.end(), strm->next_in, strm->next_in + strm->avail_in);
         strm->total_in += strm->avail_in;
         strm->next_in += strm->avail_in;
@@ -1325,10 +1432,9 @@ int deflate_stored_call(z_streamp strm, internal_state *s, int flush) {
         fh.plan = plan.data();
         fh.nplan = (uint32_t)plan.size();
         {
-            Ctx &c = ctx();
-            std::lock_guard<std::mutex> g(c.mu);
-            int rc = init_locked(c);
-            if (!rc) rc = compress_host_locked(c, &sp, &sl, &dp, &cap, &st, 1, 0, ZGPU_WRAP_RAW, s->strategy, &fh);
+            Lease L;
+            int rc = L.rc;
+            if (!rc) rc = compress_host_locked(*L.c, &sp, &sl, &dp, &cap, &st, 1, 0, ZGPU_WRAP_RAW, s->strategy, &fh);
             if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
         }
         const size_t jb = (size_t)(s->res_bits >> 3);
@@ -1453,6 +1559,7 @@ int deflate(z_streamp strm, int flush) {
         s->ev_type.back() = Z_BLOCK;
     }
     if (strm->avail_in) {
+        if ((uint64_t)s->in.size() + strm->avail_in >= kMaxBuffer) return Z_MEM_ERROR;   // 32-bit kernel positions
         s->in.insert(s->in.end(), strm->next_in, strm->next_in + strm->avail_in);
         strm->total_in += strm->avail_in;
         strm->next_in += strm->avail_in;
@@ -1473,7 +1580,10 @@ int deflate(z_streamp strm, int flush) {
             size_t sl = s->in.size();
             int st = 0;
             int rc = zgpu_compress_batch_ex(&sp, &sl, &dp, &cap, &st, 1, s->level, s->wrap, s->strategy);
-            if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
+            if (rc || st) {
+                s->out.clear();          // nothing of a failed call may be handed out by a retry
+                return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
+            }
             s->out.resize(cap);
             strm->adler = s->wrap == 2 ? crc32_z(0, sp, sl) : (s->wrap == 1 ? adler32_z(1, sp, sl) : 0);
         } else {
@@ -1648,12 +1758,11 @@ int inflate(z_streamp strm, int flush) {
             uint8_t *dp = s->out.data();
             size_t sl = s->in.size(), dl = s->cap, used = 0;
             int st = 0, stop = 0;
-            Ctx &c = ctx();
             int rc;
             {
-                std::lock_guard<std::mutex> g(c.mu);
-                rc = init_locked(c);
-                if (!rc) rc = uncompress_host_locked(c, &sp, &sl, &dp, &dl, &used, &st, &stop, 1, s->wrap, s->wbits);
+                Lease L;
+                rc = L.rc;
+                if (!rc) rc = uncompress_host_locked(*L.c, &sp, &sl, &dp, &dl, &used, &st, &stop, 1, s->wrap, s->wbits);
             }
             if (rc) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : rc;
             if (stop == kIFull) {                                     // grow the output and decode again
@@ -1854,9 +1963,9 @@ int zlib_compress_simd_buffer(const uint8_t *src, size_t src_len, uint8_t *dest,
 void zlib_slide_hash_simd(uint16_t *hash_table, uint16_t *prev_table, uint32_t hash_size,
                           uint32_t window_size, uint16_t wsize) {    // src/zlib_simd_optimized.c:27
     if ((!hash_table && hash_size) || (!prev_table && window_size)) return;
-    Ctx &c = ctx();
-    std::lock_guard<std::mutex> g(c.mu);
-    if (init_locked(c)) return;
+    Lease L;
+    if (L.rc) return;
+    Ctx &c = *L.c;
     const size_t hb = 2ull * hash_size, pb = 2ull * window_size;
     if (!c.ws_help.ensure(hb + pb + 64)) return;
     uint16_t *dh = c.ws_help.as<uint16_t>(), *dp = dh + hash_size;
@@ -1869,9 +1978,9 @@ void zlib_slide_hash_simd(uint16_t *hash_table, uint16_t *prev_table, uint32_t h
 }
 uint32_t zlib_compare256_simd(const uint8_t *src0, const uint8_t *src1) {   // src/zlib_simd_optimized.c:74
     if (!src0 || !src1) return 0;
-    Ctx &c = ctx();
-    std::lock_guard<std::mutex> g(c.mu);
-    if (init_locked(c) || !c.ws_help.ensure(512 + 64)) return 0;
+    Lease L;
+    if (L.rc || !L.c->ws_help.ensure(512 + 64)) return 0;
+    Ctx &c = *L.c;
     uint8_t *d = c.ws_help.as<uint8_t>();
     uint32_t *dr = reinterpret_cast<uint32_t *>(d + 512), r = 0;
     if (hipMemcpy(d, src0, 256, hipMemcpyHostToDevice) != hipSuccess ||
@@ -1892,9 +2001,9 @@ uint32_t zlib_longest_match_simd(const uint8_t *window, uint32_t strstart, uint3
         prev_length < 2 || prev_length > (uint32_t)kMaxMatch ||
         (uint64_t)strstart + kMinLookahead > 2 * wsize || lookahead > 2 * wsize - strstart)
         return prev_length;
-    Ctx &c = ctx();
-    std::lock_guard<std::mutex> g(c.mu);
-    if (init_locked(c) || !c.ws_help.ensure(2 * wsize + 2 * wsize + 64)) return prev_length;
+    Lease L;
+    if (L.rc || !L.c->ws_help.ensure(2 * wsize + 2 * wsize + 64)) return prev_length;
+    Ctx &c = *L.c;
     uint8_t *dw = c.ws_help.as<uint8_t>();
     uint16_t *dp = reinterpret_cast<uint16_t *>(dw + 2 * wsize);
     uint32_t *dr = reinterpret_cast<uint32_t *>(dw + 4 * wsize), r[3] = {prev_length, 0, 0};
@@ -1911,9 +2020,9 @@ void zlib_chunkmemset_simd(uint8_t *dest, uint8_t *src, uint32_t dist,
                            uint32_t len) {                           // src/zlib_simd_optimized.c:296
     if (!dest || !src || dist == 0 || len == 0) return;
     const uint32_t sn = dist < len ? dist : len;
-    Ctx &c = ctx();
-    std::lock_guard<std::mutex> g(c.mu);
-    if (init_locked(c) || !c.ws_help.ensure((size_t)sn + len + 64)) return;
+    Lease L;
+    if (L.rc || !L.c->ws_help.ensure((size_t)sn + len + 64)) return;
+    Ctx &c = *L.c;
     uint8_t *ds = c.ws_help.as<uint8_t>(), *dd = ds + ((sn + 15) & ~15u);
     if (hipMemcpy(ds, src, sn, hipMemcpyHostToDevice) != hipSuccess ||
         launch_chunkmemset(dd, ds, dist, len, nullptr) ||

@@ -334,6 +334,228 @@ __global__ __launch_bounds__(kCkBlock) void k_adler32(const uint8_t *__restrict_
     }
 }
 
+// ------------------------------------------------------------------------
+// Few large buffers: one wave per buffer leaves the GPU idle (256 x 16 MiB is
+// 256 waves), so each buffer is cut into `parts` row ranges, one wave each
+// (k_*_part), and a per-buffer finish joins them (k_*_fin).
+//
+// Adler-32: the weights of k_adler32 are distances to the buffer's (virtual)
+// end, so the partial sums of row ranges simply add (atomics into two u64 per
+// buffer).  CRC-32: each part is a zero-init linear CRC over its rows; the
+// finish joins them by Horner, crc(A||B) = x^(8|B|) * crc(A) ^ crc(B)
+// (crc32_combine, crc32.c:1021-1026, multmodp/x2nmodp :155-187).
+// ------------------------------------------------------------------------
+__device__ inline void adler_rows(const uint8_t *buf, uint64_t L, uint64_t V, int64_t pad, uint64_t r0,
+                                  uint64_t r1, int lane, uint64_t &s1, uint64_t &s2) {
+    uint64_t row = r0;
+    for (; row + 4 <= r1; row += 4) {                 // 4 rows (64 B per lane) in flight
+        uint32_t w[4][4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) load_chunk16(buf, (int64_t)((row + q) << 10) + 16 * lane - pad, L, w[q]);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            uint32_t sx = dot4(w[q][0], 0x01010101u, 0);
+            sx = dot4(w[q][1], 0x01010101u, sx);
+            sx = dot4(w[q][2], 0x01010101u, sx);
+            sx = dot4(w[q][3], 0x01010101u, sx);
+            uint32_t sj = dot4(w[q][0], 0x03020100u, 0);
+            sj = dot4(w[q][1], 0x07060504u, sj);
+            sj = dot4(w[q][2], 0x0b0a0908u, sj);
+            sj = dot4(w[q][3], 0x0f0e0d0cu, sj);
+            const uint64_t wt = (V - ((row + q) << 10) - 16u * (uint64_t)lane) % kAdlerBase;
+            s1 += sx;
+            s2 += wt * sx + kAdlerBase - sj;
+        }
+    }
+    for (; row < r1; row++) {
+        uint32_t w[4];
+        load_chunk16(buf, (int64_t)(row << 10) + 16 * lane - pad, L, w);
+        uint32_t sx = dot4(w[0], 0x01010101u, 0);
+        sx = dot4(w[1], 0x01010101u, sx);
+        sx = dot4(w[2], 0x01010101u, sx);
+        sx = dot4(w[3], 0x01010101u, sx);
+        uint32_t sj = dot4(w[0], 0x03020100u, 0);
+        sj = dot4(w[1], 0x07060504u, sj);
+        sj = dot4(w[2], 0x0b0a0908u, sj);
+        sj = dot4(w[3], 0x0f0e0d0cu, sj);
+        const uint64_t wt = (V - (row << 10) - 16u * (uint64_t)lane) % kAdlerBase;
+        s1 += sx;
+        s2 += wt * sx + kAdlerBase - sj;
+    }
+}
+
+__global__ __launch_bounds__(kCkBlock) void k_adler32_part(const uint8_t *__restrict__ src,
+                                                           const uint64_t *__restrict__ off,
+                                                           const uint64_t *__restrict__ len,
+                                                           unsigned long long *__restrict__ acc,
+                                                           uint32_t count, uint32_t parts) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t item = (uint64_t)blockIdx.x * (kCkBlock / 64) + (threadIdx.x >> 6);
+    if (item >= (uint64_t)count * parts) return;
+    const uint32_t b = (uint32_t)(item / parts), p = (uint32_t)(item % parts);
+    const uint64_t L = len[b];
+    if (L < 16) return;
+    const uint64_t V = (L + 1023) & ~(uint64_t)1023, rows = V >> 10, per = (rows + parts - 1) / parts;
+    const uint64_t r0 = (uint64_t)p * per, r1 = r0 + per < rows ? r0 + per : rows;
+    if (r0 >= r1) return;
+    uint64_t s1 = 0, s2 = 0;
+    adler_rows(src + off[b], L, V, (int64_t)(V - L), r0, r1, lane, s1, s2);
+#pragma unroll
+    for (int l = 32; l >= 1; l >>= 1) {
+        s1 += __shfl_down(s1, l, 64);
+        s2 += __shfl_down(s2, l, 64);
+    }
+    if (lane == 0) {
+        atomicAdd(&acc[2 * b], (unsigned long long)s1);
+        atomicAdd(&acc[2 * b + 1], (unsigned long long)s2);
+    }
+}
+
+__global__ void k_adler32_fin(const uint8_t *__restrict__ src, const uint64_t *__restrict__ off,
+                              const uint64_t *__restrict__ len, const uint32_t *__restrict__ init,
+                              uint32_t *__restrict__ out, const unsigned long long *__restrict__ acc,
+                              uint32_t count) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= count) return;
+    const uint64_t L = len[b];
+    const uint32_t a0 = init ? init[b] : 1u;
+    uint64_t A0 = a0 & 0xffffu, B0 = (a0 >> 16) & 0xffffu;
+    if (L < 16) {                                      // adler32.c:71-94
+        const uint8_t *buf = src + off[b];
+        uint32_t a = (uint32_t)A0, s2 = (uint32_t)B0;
+        if (L == 1) {
+            a += buf[0];
+            if (a >= kAdlerBase) a -= kAdlerBase;
+            s2 += a;
+            if (s2 >= kAdlerBase) s2 -= kAdlerBase;
+        } else {
+            for (uint64_t i = 0; i < L; i++) { a += buf[i]; s2 += a; }
+            if (a >= kAdlerBase) a -= kAdlerBase;
+            s2 %= kAdlerBase;
+        }
+        out[b] = a | (s2 << 16);
+        return;
+    }
+    const uint64_t A = (A0 + acc[2 * b] % kAdlerBase) % kAdlerBase;
+    const uint64_t B = (B0 + (L % kAdlerBase) * A0 + acc[2 * b + 1] % kAdlerBase) % kAdlerBase;
+    out[b] = (uint32_t)A | ((uint32_t)B << 16);
+}
+
+// crc32.c:155-170 (reflected GF(2) product mod the CRC-32 polynomial)
+__device__ inline uint32_t d_multmodp(uint32_t a, uint32_t b) {
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0) break;
+        }
+        m >>= 1;
+        b = b & 1 ? (b >> 1) ^ 0xedb88320u : b >> 1;
+    }
+    return p;
+}
+// x^(8n) mod p (crc32.c:176-187 with k = 3), squaring x^(2^k) as it goes
+__device__ inline uint32_t d_x8nmodp(uint64_t n) {
+    uint32_t p = 1u << 31, sq = 1u << 30;             // x^0, x^1
+    for (int k = 0; k < 3; k++) sq = d_multmodp(sq, sq);
+    while (n) {
+        if (n & 1) p = d_multmodp(sq, p);
+        n >>= 1;
+        if (n) sq = d_multmodp(sq, sq);
+    }
+    return p;
+}
+
+constexpr uint64_t kCpRow = 64u * 64u;                 // k_crc32s<64> row: 64 lanes x 64 B
+
+__global__ __launch_bounds__(kCsBlock) void k_crc32_part(const uint8_t *__restrict__ src,
+                                                         const uint64_t *__restrict__ off,
+                                                         const uint64_t *__restrict__ len,
+                                                         const uint32_t *__restrict__ init,
+                                                         uint32_t *__restrict__ part_out, uint32_t count,
+                                                         uint32_t parts, const CrcTables *__restrict__ tab) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_t[4 * 256 << kCsCopyLog];
+    __shared__ uint32_t s_sh[kCrcSh64Tabs][8][16];
+    for (int i = threadIdx.x; i < (4 * 256 << kCsCopyLog); i += kCsBlock) s_t[i] = (&tab->s4[0][0])[i >> kCsCopyLog];
+    for (int i = threadIdx.x; i < kCrcSh64Tabs * 8 * 16; i += kCsBlock) (&s_sh[0][0][0])[i] = (&tab->sh64[0][0][0])[i];
+    __syncthreads();
+    const uint8_t *T = reinterpret_cast<const uint8_t *>(s_t);
+    const uint32_t loff = (threadIdx.x & ((1u << kCsCopyLog) - 1u)) << 2;
+    const int lane = threadIdx.x & 63;
+    const uint64_t items = (uint64_t)count * parts;
+    for (uint64_t item = (uint64_t)blockIdx.x * (kCsBlock / 64) + (threadIdx.x >> 6); item < items;
+         item += (uint64_t)gridDim.x * (kCsBlock / 64)) {
+        const uint32_t b = (uint32_t)(item / parts), p = (uint32_t)(item % parts);
+        const uint64_t L = len[b];
+        if (L < 4) continue;                           // k_crc32_fin's byte loop
+        const uint8_t *buf = src + off[b];
+        const uint64_t V = (L + kCpRow - 1) & ~(kCpRow - 1), rows = V / kCpRow, per = (rows + parts - 1) / parts;
+        const uint64_t r0 = (uint64_t)p * per, r1 = r0 + per < rows ? r0 + per : rows;
+        const int64_t pad = (int64_t)(V - L);
+        const uint32_t xv = ~(init ? init[b] : 0u);
+        uint32_t acc = 0;
+        for (uint64_t row = r0; row < r1; row++) {
+            const int64_t x = (int64_t)(row * kCpRow) + 64 * lane - pad;
+            uint32_t w[16];
+#pragma unroll
+            for (int q = 0; q < 4; q++) load_chunk16(buf, x + 16 * q, L, w + 4 * q);
+            if (x < 4 && x + 64 > 0) {                 // fold ~init into data bytes 0..3
+#pragma unroll
+                for (int j = 0; j < 64; j++) {
+                    const int64_t o = x + j;
+                    if (o >= 0 && o < 4) w[j >> 2] ^= ((xv >> (8 * o)) & 0xffu) << (8 * (j & 3));
+                }
+            }
+            acc = crc_word(acc, &s_sh[7][0][0]);       // advance over the other lanes' 63*64 bytes
+#pragma unroll
+            for (int k = 0; k < 16; k++) acc = s4_step(acc, w[k], T, loff);
+        }
+#pragma unroll
+        for (int l = 0; l < 6; l++) {
+            const uint32_t other = __shfl_down(acc, 1 << l, 64);
+            acc = crc_word(acc, &s_sh[l][0][0], other);
+        }
+        if (lane == 0) part_out[item] = acc;
+    }
+}
+
+__global__ void k_crc32_fin(const uint8_t *__restrict__ src, const uint64_t *__restrict__ off,
+                            const uint64_t *__restrict__ len, const uint32_t *__restrict__ init,
+                            uint32_t *__restrict__ out, const uint32_t *__restrict__ part_out,
+                            uint32_t count, uint32_t parts, const CrcTables *__restrict__ tab) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= count) return;
+    const uint64_t L = len[b];
+    const uint32_t c0 = init ? init[b] : 0u;
+    if (L < 4) {                                       // crc32.c byte loop (tiny input)
+        const uint8_t *buf = src + off[b];
+        uint32_t c = ~c0;
+        for (uint64_t i = 0; i < L; i++) c = (c >> 8) ^ tab->byte[(c ^ buf[i]) & 0xffu];
+        out[b] = ~c;
+        return;
+    }
+    const uint64_t V = (L + kCpRow - 1) & ~(kCpRow - 1), rows = V / kCpRow, per = (rows + parts - 1) / parts;
+    const uint32_t step = d_x8nmodp(per * kCpRow);
+    uint32_t acc = 0;
+    for (uint32_t p = 0; p < parts; p++) {
+        const uint64_t r0 = (uint64_t)p * per;
+        if (r0 >= rows) break;
+        const uint64_t r1 = r0 + per < rows ? r0 + per : rows;
+        const uint32_t sh = r1 - r0 == per ? step : d_x8nmodp((r1 - r0) * kCpRow);
+        acc = d_multmodp(sh, acc) ^ part_out[(uint64_t)b * parts + p];
+    }
+    out[b] = ~acc;
+}
+
+// parts per buffer for a split launch: enough waves to fill the chip
+static uint32_t split_parts(uint32_t count, size_t scratch, size_t per_part_bytes, size_t fixed_per_buf) {
+    if (count == 0 || count >= 4096) return 1;
+    uint32_t parts = (16384u + count - 1) / count;
+    if (parts > 1024) parts = 1024;
+    while (parts > 1 && (size_t)count * (fixed_per_buf + per_part_bytes * parts) > scratch) parts >>= 1;
+    return parts;
+}
+
 static int grid_for(uint32_t count, uint32_t per_wave = 1) {
     uint32_t waves = (count + per_wave - 1) / per_wave;
     uint32_t blocks = (waves + (kCkBlock / 64) - 1) / (kCkBlock / 64);
@@ -344,8 +566,19 @@ static int grid_for(uint32_t count, uint32_t per_wave = 1) {
 
 int launch_crc32(const uint8_t *src, const uint64_t *off, const uint64_t *len,
                  const uint32_t *init, uint32_t *out, uint32_t count,
-                 void *, size_t, hipStream_t st) {
+                 void *scratch, size_t scratch_bytes, hipStream_t st) {
     if (count == 0) return 0;
+    if (const uint32_t parts = scratch ? split_parts(count, scratch_bytes, 4, 0) : 1; parts > 1) {
+        uint32_t *po = static_cast<uint32_t *>(scratch);
+        const uint64_t items = (uint64_t)count * parts;
+        uint64_t blocks = (items + (kCsBlock / 64) - 1) / (kCsBlock / 64);
+        if (blocks > 512) blocks = 512;
+        hipLaunchKernelGGL(k_crc32_part, dim3((uint32_t)blocks), dim3(kCsBlock), 0, st, src, off, len, init, po,
+                           count, parts, device_crc_tables());
+        hipLaunchKernelGGL(k_crc32_fin, dim3((count + 63) / 64), dim3(64), 0, st, src, off, len, init, out, po,
+                           count, parts, device_crc_tables());
+        return (int)hipGetLastError();
+    }
     static const bool nibble = std::getenv("ZGPU_CRC_NIBBLE") != nullptr;   // A/B: the nibble kernel
     if (nibble) {
         // 16-lane groups once there are enough buffers to fill the chip 4x over
@@ -375,13 +608,24 @@ int launch_crc32(const uint8_t *src, const uint64_t *off, const uint64_t *len,
 
 int launch_adler32(const uint8_t *src, const uint64_t *off, const uint64_t *len,
                    const uint32_t *init, uint32_t *out, uint32_t count,
-                   void *, size_t, hipStream_t st) {
+                   void *scratch, size_t scratch_bytes, hipStream_t st) {
     if (count == 0) return 0;
+    if (const uint32_t parts = scratch ? split_parts(count, scratch_bytes, 0, 16) : 1; parts > 1) {
+        auto *acc = static_cast<unsigned long long *>(scratch);
+        if (hipMemsetAsync(acc, 0, 16ull * count, st) != hipSuccess) return (int)hipErrorInvalidValue;
+        const uint64_t items = (uint64_t)count * parts;
+        hipLaunchKernelGGL(k_adler32_part, dim3((uint32_t)((items + (kCkBlock / 64) - 1) / (kCkBlock / 64))),
+                           dim3(kCkBlock), 0, st, src, off, len, acc, count, parts);
+        hipLaunchKernelGGL(k_adler32_fin, dim3((count + 63) / 64), dim3(64), 0, st, src, off, len, init, out, acc,
+                           count);
+        return (int)hipGetLastError();
+    }
     hipLaunchKernelGGL(k_adler32, dim3(grid_for(count)), dim3(kCkBlock), 0, st, src, off, len,
                        init, out, count);
     return (int)hipGetLastError();
 }
 
-size_t checksum_scratch_bytes(uint32_t) { return 0; }
+// scratch that lets a launch of `count` buffers split them (launch_crc32/adler32)
+size_t checksum_scratch_bytes(uint32_t count) { return count >= 4096 ? 0 : 16ull * 16384 + 64ull * count; }
 
 }  // namespace zgpu

@@ -326,6 +326,7 @@ __global__ __launch_bounds__(kCntThreads) void k_count(DeflateJob job) {
 // the result after chain/4 candidates too, and stores (len<<16 | dist).
 // ------------------------------------------------------------------------
 constexpr int kMW = 32768, kMT = 4096, kMPad = 272;
+static_assert(kMT == (int)kMatchTile, "segment starts (host) must be k_match tile boundaries");
 constexpr int kME = kMW + kMT + kMPad;                     // 37136 words = 148.5 KiB
 constexpr int kMatchThreads = 1024;
 

@@ -15,6 +15,13 @@ constexpr int kMinLookahead = kMaxMatch + kMinMatch + 1;   // 262
 constexpr int kMaxDist = kWSize - kMinLookahead;            // 32506
 constexpr int kTooFar = 4096;                               // deflate.c:88-90
 constexpr int kSymLimit = 16383;                            // lit_bufsize - 1
+// k_match's tile: positions walked per LDS window load.  A segmented k_match
+// (few large buffers) must start every segment on a tile boundary, so the
+// host's segment sizes are whole multiples of it.
+constexpr uint32_t kMatchTile = 4096;
+// Buffers are addressed with 32-bit positions inside the kernels: deflate
+// refuses buffers of kMaxBuffer bytes or more (Z_STREAM_ERROR / Z_MEM_ERROR).
+constexpr uint64_t kMaxBuffer = (1ull << 32) - (1ull << 16);
 constexpr int kLCodes = 286, kDCodes = 30, kBLCodes = 19;
 constexpr int kHeapSize = 2 * kLCodes + 1;                  // 573
 constexpr int kMaxBits = 15, kMaxBLBits = 7;

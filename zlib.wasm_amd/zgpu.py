@@ -31,7 +31,7 @@ LIB_PATH = os.path.join(HERE, "libzgpu.so")
 Z_OK, Z_STREAM_END, Z_STREAM_ERROR, Z_MEM_ERROR, Z_BUF_ERROR = 0, 1, -2, -4, -5
 ZGPU_ENODEV = -100
 WRAP_RAW, WRAP_ZLIB, WRAP_GZIP = 0, 1, 2
-KIND_RANDOM, KIND_SILESIA, KIND_ENWIK, KIND_SMALLVOCAB = 0, 1, 2, 3
+KIND_RANDOM, KIND_SILESIA, KIND_ENWIK, KIND_SMALLVOCAB, KIND_FOUR, KIND_RUNS = 0, 1, 2, 3, 4, 5
 
 EXPORTED_SYMBOLS = (
     # include/zgpu.h
