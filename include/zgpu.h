@@ -93,6 +93,19 @@ int zgpu_deflate_batch_dev_ex(const uint8_t *src, const uint64_t *src_off,
                               uint64_t *dst_len, int32_t *status, uint32_t count,
                               int level, int wrap, int strategy, void *stream);
 
+/* zgpu_deflate_batch_dev with all of deflateInit2_'s parameters (zlib.h:
+ * 553-626, deflate.c:379-524): per buffer the output equals
+ * deflateInit2_(level, Z_DEFLATED, window_bits, mem_level, strategy) +
+ * deflate(Z_FINISH).  window_bits 8..15 (zlib wrapper; 8 is coded as 9),
+ * -15..-9 (raw), 25..31 (gzip); mem_level 1..9 (hash_bits = mem_level + 7,
+ * lit_bufsize = 1 << (mem_level + 6)).  Others: ZGPU_STREAM_ERROR. */
+int zgpu_deflate_batch_dev2(const uint8_t *src, const uint64_t *src_off,
+                            const uint64_t *src_len, uint8_t *dst,
+                            const uint64_t *dst_off, const uint64_t *dst_cap,
+                            uint64_t *dst_len, int32_t *status, uint32_t count,
+                            int level, int window_bits, int mem_level, int strategy,
+                            void *stream);
+
 /* crc32(init[i], buffer i) for each buffer (init == NULL: 0).  Device ptrs. */
 int zgpu_crc32_batch_dev(const uint8_t *src, const uint64_t *off, const uint64_t *len,
                          const uint32_t *init, uint32_t *out, uint32_t count,
@@ -134,6 +147,11 @@ int zgpu_compress_batch(const uint8_t *const *src, const size_t *src_len,
 int zgpu_compress_batch_ex(const uint8_t *const *src, const size_t *src_len,
                            uint8_t *const *dst, size_t *dst_len, int *status,
                            size_t count, int level, int wrap, int strategy);
+/* Host-memory form of zgpu_deflate_batch_dev2. */
+int zgpu_compress_batch2(const uint8_t *const *src, const size_t *src_len,
+                         uint8_t *const *dst, size_t *dst_len, int *status,
+                         size_t count, int level, int window_bits, int mem_level,
+                         int strategy);
 /* Host-memory form of zgpu_inflate_batch_dev: dst_len[i] in: capacity, out:
  * bytes written; src_used may be NULL.  Synchronous. */
 int zgpu_uncompress_batch(const uint8_t *const *src, const size_t *src_len,

@@ -118,3 +118,31 @@ def test_checksums_never_abort_without_gpu(lib):
         pytest.skip("a GPU is visible")
     assert r.returncode == 0, r.stderr
     assert r.stdout.split() == ["0", "0"]
+
+
+def test_deflateinit2_params_and_bound_vs_reference_golden(lib):
+    """deflateInit2_'s windowBits / memLevel validation (deflate.c:400-425) and
+    deflateBound for non-default parameters (deflate.c:842-905) against the
+    compiled reference (tests/golden/params_golden.json).  Host-only calls."""
+    import json
+    from zhelpers import ZStream
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "params_golden.json")))
+    lib.deflateInit2_.restype = C.c_int
+    lib.deflateInit2_.argtypes = [C.POINTER(ZStream), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                  C.c_char_p, C.c_int]
+    lib.deflateEnd.argtypes = [C.POINTER(ZStream)]
+    lib.deflateBound.restype = C.c_ulong
+    lib.deflateBound.argtypes = [C.POINTER(ZStream), C.c_ulong]
+    for e in g["init_rc"]:
+        s = ZStream()
+        rc = lib.deflateInit2_(C.byref(s), e["level"], 8, e["window_bits"], e["mem_level"], 0,
+                               b"1.3.1.1-motley", C.sizeof(ZStream))
+        assert rc == e["rc"], e
+        if rc == 0:
+            lib.deflateEnd(C.byref(s))
+    for e in g["bound"]:
+        s = ZStream()
+        assert lib.deflateInit2_(C.byref(s), e["level"], 8, e["window_bits"], e["mem_level"], e["strategy"],
+                                 b"1.3.1.1-motley", C.sizeof(ZStream)) == 0
+        assert lib.deflateBound(C.byref(s), e["n"]) == e["bound"], e
+        lib.deflateEnd(C.byref(s))

@@ -506,3 +506,52 @@ def test_checksum_split_few_large_buffers(zg, oracle):
         b = host[offs[i]:offs[i] + n].tobytes()
         assert int(gc[i]) == oracle.crc32(b, ci[i]), n
         assert int(ga[i]) == oracle.adler32(b, ai[i]), n
+
+
+def test_window_bits_mem_level_golden(zg, golden):
+    """deflateInit2_'s windowBits 8..15 (raw / gzip forms too) and memLevel 1..9
+    at levels 0-9 and all strategies (hash_bits, hash_shift, lit_bufsize block
+    cut, MAX_DIST, slide schedule, header): every stream equals the compiled
+    reference's (tests/golden/params_golden.json)."""
+    import hashlib
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "params_golden.json")))
+    datas = [datagen.make(k, n, s) for k, n, s in g["inputs"]]
+    for c in g["cases"]:
+        res = zg.compress_batch2(datas, level=c["level"], window_bits=c["window_bits"], mem_level=c["mem_level"],
+                                 strategy=c["strategy"])
+        for (st, z), want, (k, n, _) in zip(res, c["streams"], g["inputs"]):
+            assert st == 0 and len(z) == want["len"] and hashlib.sha256(z).hexdigest() == want["sha256"], \
+                (c["level"], c["window_bits"], c["mem_level"], c["strategy"], k, n)
+
+
+def test_deflateinit2_params_stream(zg):
+    """The z_stream API with windowBits / memLevel: deflateInit2_ + deflate(Z_FINISH)
+    equals the fixture for a sample of settings."""
+    import hashlib
+    import json
+    import os
+    from zhelpers import ZStream
+    g = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "params_golden.json")))
+    L = zg.load()
+    L.deflateInit2_.argtypes = [C.POINTER(ZStream), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                C.c_char_p, C.c_int]
+    L.deflate.argtypes = [C.POINTER(ZStream), C.c_int]
+    L.deflateEnd.argtypes = [C.POINTER(ZStream)]
+    k, n, sd = g["inputs"][1]
+    data = datagen.make(k, n, sd)
+    for c in g["cases"][::9]:
+        s = ZStream()
+        assert L.deflateInit2_(C.byref(s), c["level"], 8, c["window_bits"], c["mem_level"], c["strategy"],
+                               b"1.3.1.1-motley", C.sizeof(ZStream)) == 0
+        inb = C.create_string_buffer(data, len(data))
+        cap = len(data) * 2 + 1024
+        out = C.create_string_buffer(cap)
+        s.next_in, s.avail_in = C.addressof(inb), len(data)
+        s.next_out, s.avail_out = C.addressof(out), cap
+        assert L.deflate(C.byref(s), 4) == 1
+        z = out.raw[:cap - s.avail_out]
+        L.deflateEnd(C.byref(s))
+        want = c["streams"][1]
+        assert hashlib.sha256(z).hexdigest() == want["sha256"], (c["level"], c["window_bits"], c["mem_level"])

@@ -243,15 +243,15 @@ class Reference:
         rc = self.L.compress2(out, C.byref(n), data, len(data), level)
         return rc, out.raw[: n.value]
 
-    def deflate(self, data, level=6, wbits=15, chunk=None, strategy=0):
+    def deflate(self, data, level=6, wbits=15, chunk=None, strategy=0, mem_level=8):
         """deflateInit2 + deflate; wbits -15 raw, 15 zlib, 31 gzip.  ``chunk``
         feeds the input in pieces with Z_NO_FLUSH before Z_FINISH."""
         data = bytes(data)
         strm = ZStream()
-        rc = self.L.deflateInit2_(C.byref(strm), level, 8, wbits, 8, strategy, self.version,
+        rc = self.L.deflateInit2_(C.byref(strm), level, 8, wbits, mem_level, strategy, self.version,
                                   C.sizeof(ZStream))
         assert rc == Z_OK, rc
-        cap = compress_bound(len(data)) + 64
+        cap = len(data) + (len(data) >> 3) + (len(data) >> 6) + 64
         out = C.create_string_buffer(cap)
         inbuf = C.create_string_buffer(data, max(len(data), 1))
         base_in = C.addressof(inbuf)
@@ -272,6 +272,26 @@ class Reference:
         total = strm.total_out
         self.L.deflateEnd(C.byref(strm))
         return out.raw[:total]
+
+    def init_rc(self, level, wbits, mem_level, strategy=0):
+        """deflateInit2_'s return code (the stream is ended again if it opened)."""
+        strm = ZStream()
+        rc = self.L.deflateInit2_(C.byref(strm), level, 8, wbits, mem_level, strategy, self.version,
+                                  C.sizeof(ZStream))
+        if rc == Z_OK:
+            self.L.deflateEnd(C.byref(strm))
+        return rc
+
+    def bound(self, level, wbits, mem_level, strategy, n):
+        """deflateBound(n) of a freshly initialised stream."""
+        strm = ZStream()
+        assert self.L.deflateInit2_(C.byref(strm), level, 8, wbits, mem_level, strategy, self.version,
+                                    C.sizeof(ZStream)) == Z_OK
+        self.L.deflateBound.restype = C.c_ulong
+        self.L.deflateBound.argtypes = [C.POINTER(ZStream), C.c_ulong]
+        b = self.L.deflateBound(C.byref(strm), n)
+        self.L.deflateEnd(C.byref(strm))
+        return int(b)
 
     def deflate_calls(self, data, calls, level=6, wbits=15, strategy=0):
         """deflate() over a call sequence [(input_len, flush), ...] (the lengths

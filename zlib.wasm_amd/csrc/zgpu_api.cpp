@@ -367,7 +367,7 @@ struct FlushSpec {
     int open_end;
     uint32_t start, bit0, byte0;   // a resumed job (DeflateJob::start/bit0/byte0)
     uint64_t *out;                 // DeflateJob::flush_out
-    // levels 1..3 resumed (host arrays): k_parse_fast's head[32768], rebased to
+    // levels 1..3 resumed (host arrays): k_parse_fast's head[hash_size], rebased to
     // the job's buffer, and the prev links of its positions [0, prev_n)
     const uint32_t *head_in;
     const uint16_t *prev_in;
@@ -378,13 +378,39 @@ struct FlushSpec {
     uint32_t nplan;
 };
 
+// deflateInit2_'s windowBits / memLevel rules (deflate.c:400-425): negative
+// windowBits raw deflate, 16 + windowBits gzip, 8 made 9 (zlib wrapper only)
+int parse_window(int windowBits, int memLevel, int *wrap, int *wbits) {
+    int w = 1;
+    if (windowBits < 0) {
+        w = 0;
+        if (windowBits < -15) return ZGPU_STREAM_ERROR;
+        windowBits = -windowBits;
+    } else if (windowBits > 15) {
+        w = 2;
+        windowBits -= 16;
+    }
+    if (memLevel < 1 || memLevel > 9 || windowBits < 8 || windowBits > 15 || (windowBits == 8 && w != 1))
+        return ZGPU_STREAM_ERROR;
+    *wrap = w;
+    *wbits = windowBits == 8 ? 9 : windowBits;
+    return ZGPU_OK;
+}
+
+// wbits 9..15 (deflateInit2_'s windowBits with 8 already made 9), mem_level
+// 1..9 (hash_bits = mem_level + 7, lit_bufsize = 1 << (mem_level + 6))
 int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
                        uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
                        uint64_t *dst_len, int32_t *status, uint32_t count, int level, int wrap,
-                       int strategy, hipStream_t st, const FlushSpec *fs = nullptr) {
+                       int strategy, hipStream_t st, const FlushSpec *fs = nullptr, int wbits = 15,
+                       int mem_level = 8) {
     if (level == -1) level = 6;
-    if (level < 0 || level > 9 || wrap < 0 || wrap > 2 || strategy < 0 || strategy > 4)
+    if (level < 0 || level > 9 || wrap < 0 || wrap > 2 || strategy < 0 || strategy > 4 || wbits < 9 ||
+        wbits > 15 || mem_level < 1 || mem_level > 9)
         return ZGPU_STREAM_ERROR;
+    const int hbits = mem_level + 7;
+    const WinP wp = win_params(wbits, hbits);
+    const uint64_t hsize = 1ull << hbits;
     if (fs && (count != 1 || (level == 0) != (fs->plan != nullptr))) return ZGPU_STREAM_ERROR;
     if (count == 0) return ZGPU_OK;
     std::vector<uint64_t> lens(count);
@@ -422,7 +448,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             // literal at index n (a run of literals up to the end), which must
             // not land in the next buffer's region
             pos += (lens[i] + 64) & ~63ull;
-            blk += lens[i] / kSymLimit + 2 + (fs ? 2ull * fs->n + fs->nplan : 0);   // a flush: a block and a marker
+            blk += lens[i] / wp.sym_limit + 2 + (fs ? 2ull * fs->n + fs->nplan : 0);   // a flush: a block and a marker
         }
         max_pos = std::max(max_pos, pos);
         max_blk = std::max(max_blk, blk);
@@ -463,7 +489,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
                 return ZGPU_MEM_ERROR;
         }
     }
-    if (level >= 1 && level <= 3 && !huff && !rle && !c.ws_heads.ensure(4ull * 32768 * max_cnt))
+    if (level >= 1 && level <= 3 && !huff && !rle && !c.ws_heads.ensure(4ull * hsize * max_cnt))
         return ZGPU_MEM_ERROR;
     // k_match per segment where a sub-batch has too few buffers to fill the GPU
     // one workgroup per buffer (a single zlib.h buffer, say).  The segment is
@@ -515,8 +541,8 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
          hipMemcpyAsync(d_nblk, &fs->nplan, 4, hipMemcpyHostToDevice, st) != hipSuccess))
         return ZGPU_MEM_ERROR;
     if (fs && fs->head_in) {
-        if (!c.ws_heads.ensure(4ull * 32768) ||
-            hipMemcpyAsync(c.ws_heads.p, fs->head_in, 4ull * 32768, hipMemcpyHostToDevice, st) != hipSuccess ||
+        if (!c.ws_heads.ensure(4ull * hsize) ||
+            hipMemcpyAsync(c.ws_heads.p, fs->head_in, 4ull * hsize, hipMemcpyHostToDevice, st) != hipSuccess ||
             (fs->prev_n && hipMemcpyAsync(c.ws_link.p, fs->prev_in, 2ull * fs->prev_n, hipMemcpyHostToDevice, st) !=
                                hipSuccess))
             return ZGPU_MEM_ERROR;
@@ -531,6 +557,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         job.dst = dst; job.dst_off = dst_off; job.dst_cap = dst_cap;
         job.dst_len = dst_len; job.status = status;
         job.first = a; job.count = b - a; job.level = level; job.wrap = wrap; job.strategy = strategy;
+        job.wbits = wbits; job.hbits = hbits;
         job.ws_off = d_meta + a;
         job.blk_off = d_meta + count + a;
         job.link = (slot ? c.ws_link2 : c.ws_link).as<uint16_t>();
@@ -651,7 +678,7 @@ struct FlushHost {
 
 int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
                          size_t *dst_len, int *status, size_t count, int level, int wrap, int strategy,
-                         FlushHost *fh = nullptr) {
+                         FlushHost *fh = nullptr, int wbits = 15, int mem_level = 8) {
     if (count == 0) return ZGPU_OK;
     for (size_t i = 0; i < count; i++)
         if (src_len[i] >= kMaxBuffer) return ZGPU_STREAM_ERROR;
@@ -704,15 +731,16 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
                        fh->head_in, fh->prev_in, fh->prev_n, fh->plan, fh->nplan};
     }
     int rc = deflate_dev_locked(c, d_in, d_so, d_sl, d_out, d_do, d_dc, d_dl, d_st, (uint32_t)count,
-                                level, wrap, strategy, st, fh ? &fs : nullptr);
+                                level, wrap, strategy, st, fh ? &fs : nullptr, wbits, mem_level);
     if (rc) return rc;
     if (fh && copy_sync(fh->out, fs.out, 32, hipMemcpyDeviceToHost, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
     if (fh && fh->head_out && fh->n) {
         const uint64_t S = fh->out[2], end = fh->pos[fh->n - 1];
-        fh->head_out->resize(32768);
+        const size_t hsize = size_t(1) << (mem_level + 7);
+        fh->head_out->resize(hsize);
         fh->prev_out->resize(end > S ? end - S : 0);
-        if (copy_sync(fh->head_out->data(), c.ws_heads.p, 4ull * 32768, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        if (copy_sync(fh->head_out->data(), c.ws_heads.p, 4ull * hsize, hipMemcpyDeviceToHost, st) != hipSuccess ||
             (end > S && copy_sync(fh->prev_out->data(), c.ws_link.as<uint16_t>() + S, 2 * (end - S),
                                   hipMemcpyDeviceToHost, st) != hipSuccess))
             return ZGPU_MEM_ERROR;
@@ -1015,6 +1043,18 @@ int zgpu_deflate_batch_dev_ex(const uint8_t *src, const uint64_t *src_off, const
                               count, level, wrap, strategy, static_cast<hipStream_t>(stream));
 }
 
+int zgpu_deflate_batch_dev2(const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
+                            uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
+                            uint64_t *dst_len, int32_t *status, uint32_t count, int level, int window_bits,
+                            int mem_level, int strategy, void *stream) {
+    int wrap = 0, wbits = 0;
+    if (parse_window(window_bits, mem_level, &wrap, &wbits)) return ZGPU_STREAM_ERROR;
+    Lease L;
+    if (L.rc) return L.rc;
+    return deflate_dev_locked(*L.c, src, src_off, src_len, dst, dst_off, dst_cap, dst_len, status, count, level,
+                              wrap, strategy, static_cast<hipStream_t>(stream), nullptr, wbits, mem_level);
+}
+
 int zgpu_deflate_batch_dev(const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
                            uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
                            uint64_t *dst_len, int32_t *status, uint32_t count, int level, int wrap,
@@ -1051,6 +1091,19 @@ int zgpu_compress_batch_ex(const uint8_t *const *src, const size_t *src_len, uin
     if (L.rc) return L.rc;
     Ctx &c = *L.c;
     return compress_host_locked(c, src, src_len, dst, dst_len, status, count, level, wrap, strategy);
+}
+
+int zgpu_compress_batch2(const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
+                         size_t *dst_len, int *status, size_t count, int level, int window_bits, int mem_level,
+                         int strategy) {
+    int wrap = 0, wbits = 0;
+    if (parse_window(window_bits, mem_level, &wrap, &wbits)) return ZGPU_STREAM_ERROR;
+    for (size_t i = 0; i < count; i++)
+        if (src_len && src_len[i] >= kMaxBuffer) return ZGPU_STREAM_ERROR;
+    Lease L;
+    if (L.rc) return L.rc;
+    return compress_host_locked(*L.c, src, src_len, dst, dst_len, status, count, level, wrap, strategy, nullptr,
+                                wbits, mem_level);
 }
 
 int zgpu_compress_batch(const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
@@ -1241,7 +1294,8 @@ struct internal_state {
     std::vector<uint16_t> fast_prev, job_prev;
     // inflate streams
     int inflating = 0;
-    int wbits = 15;
+    int wbits = 15;         // deflate: w_bits (9..15); inflate: inflateInit2_'s windowBits
+    int mem_level = 8;      // deflate: memLevel (hash_bits = memLevel + 7)
     size_t tried = 0;       // gathered input at the last decode attempt that ran out of input
     size_t cap = 0;         // output capacity of the next attempt
     int result = Z_OK;      // once decoded: Z_STREAM_END, Z_DATA_ERROR or Z_NEED_DICT
@@ -1254,17 +1308,16 @@ int deflateInit2_(z_streamp strm, int level, int method, int windowBits, int mem
     if (!strm) return Z_STREAM_ERROR;
     strm->msg = nullptr;
     if (level == Z_DEFAULT_COMPRESSION) level = 6;
-    int wrap;
-    if (windowBits == 15) wrap = 1;
-    else if (windowBits == -15) wrap = 0;
-    else if (windowBits == 31) wrap = 2;
-    else return Z_STREAM_ERROR;
-    if (method != Z_DEFLATED || memLevel != 8 || strategy < 0 || strategy > Z_FIXED || level < 0 || level > 9)
-        return Z_STREAM_ERROR;
+    int wrap = 1, wbits = 15;
+    if (parse_window(windowBits, memLevel, &wrap, &wbits) || method != Z_DEFLATED || strategy < 0 ||
+        strategy > Z_FIXED || level < 0 || level > 9)
+        return Z_STREAM_ERROR;                          // deflate.c:400-425
     internal_state *s = new (std::nothrow) internal_state();
     if (!s) return Z_MEM_ERROR;
     s->level = level;
     s->wrap = wrap;
+    s->wbits = wbits;
+    s->mem_level = memLevel;
     s->strategy = strategy;
     s->out_pos = 0;
     s->finished = 0;
@@ -1300,8 +1353,9 @@ int deflate_part(internal_state *s, int open_end, std::vector<uint8_t> &body, ui
     std::vector<uint32_t> head_in;
     if (s->level >= 1 && s->level <= 3 && s->strategy != Z_HUFFMAN_ONLY && s->strategy != Z_RLE) {
         if (s->res_pos > base) {                               // rebase the saved chains to this buffer
-            head_in.resize(32768);
-            for (size_t i = 0; i < 32768; i++) head_in[i] = s->fast_head[i] > base ? s->fast_head[i] - (uint32_t)base : 0;
+            head_in.resize(s->fast_head.size());
+            for (size_t i = 0; i < head_in.size(); i++)
+                head_in[i] = s->fast_head[i] > base ? s->fast_head[i] - (uint32_t)base : 0;
             fh.head_in = head_in.data();
             fh.prev_in = s->fast_prev.data();
             fh.prev_n = s->fast_prev.size();
@@ -1311,7 +1365,8 @@ int deflate_part(internal_state *s, int open_end, std::vector<uint8_t> &body, ui
     }
     Lease L;
     int rc = L.rc;
-    if (!rc) rc = compress_host_locked(*L.c, &sp, &sl, &dp, &cap, &st, 1, s->level, ZGPU_WRAP_RAW, s->strategy, &fh);
+    if (!rc) rc = compress_host_locked(*L.c, &sp, &sl, &dp, &cap, &st, 1, s->level, ZGPU_WRAP_RAW, s->strategy, &fh,
+                                       s->wbits, s->mem_level);
     if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
     body.resize(cap);
     for (int i = 0; i < 4; i++) out[i] = fh.out[i];
@@ -1349,7 +1404,7 @@ void queue_header(internal_state *s) {                          // deflate.c:100
     if (s->header_done) return;
     s->header_done = true;
     if (s->wrap == 1) {
-        uint32_t header = (8u + ((15u - 8u) << 4)) << 8;
+        uint32_t header = (8u + ((uint32_t)(s->wbits - 8) << 4)) << 8;
         const uint32_t flags = (s->strategy >= 2 || s->level < 2) ? 0u : s->level < 6 ? 1u : s->level == 6 ? 2u : 3u;
         header |= flags << 6;
         header += 31 - (header % 31);
@@ -1434,7 +1489,8 @@ int deflate_stored_call(z_streamp strm, internal_state *s, int flush) {
         {
             Lease L;
             int rc = L.rc;
-            if (!rc) rc = compress_host_locked(*L.c, &sp, &sl, &dp, &cap, &st, 1, 0, ZGPU_WRAP_RAW, s->strategy, &fh);
+            if (!rc) rc = compress_host_locked(*L.c, &sp, &sl, &dp, &cap, &st, 1, 0, ZGPU_WRAP_RAW, s->strategy, &fh,
+                                               s->wbits, s->mem_level);
             if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
         }
         const size_t jb = (size_t)(s->res_bits >> 3);
@@ -1506,8 +1562,8 @@ int emit_flush(z_streamp strm, internal_state *s, int flush) {
         // the next job resumes here; the input before the window offset is not needed again
         if (!s->job_head.empty()) {                            // levels 1..3: keep the chains
             const uint32_t base = (uint32_t)s->res_S;
-            s->fast_head.resize(32768);
-            for (size_t i = 0; i < 32768; i++) s->fast_head[i] = s->job_head[i] ? s->job_head[i] + base : 0;
+            s->fast_head.resize(s->job_head.size());
+            for (size_t i = 0; i < s->job_head.size(); i++) s->fast_head[i] = s->job_head[i] ? s->job_head[i] + base : 0;
             s->fast_prev.swap(s->job_prev);
             s->job_head.clear();
         }
@@ -1579,7 +1635,13 @@ int deflate(z_streamp strm, int flush) {
             uint8_t *dp = s->out.data();
             size_t sl = s->in.size();
             int st = 0;
-            int rc = zgpu_compress_batch_ex(&sp, &sl, &dp, &cap, &st, 1, s->level, s->wrap, s->strategy);
+            int rc;
+            {
+                Lease L;
+                rc = L.rc;
+                if (!rc) rc = compress_host_locked(*L.c, &sp, &sl, &dp, &cap, &st, 1, s->level, s->wrap, s->strategy,
+                                                   nullptr, s->wbits, s->mem_level);
+            }
             if (rc || st) {
                 s->out.clear();          // nothing of a failed call may be handed out by a retry
                 return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
@@ -1618,11 +1680,13 @@ int deflate(z_streamp strm, int flush) {
 int deflateReset(z_streamp strm) {                              // deflate.c:560-620
     if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
-    const int level = s->level, wrap = s->wrap, strategy = s->strategy;
+    const int level = s->level, wrap = s->wrap, strategy = s->strategy, wbits = s->wbits, mem = s->mem_level;
     *s = internal_state();
     s->level = level;
     s->wrap = wrap;
     s->strategy = strategy;
+    s->wbits = wbits;
+    s->mem_level = mem;
     s->out_pos = 0;
     s->finished = 0;
     s->check = wrap == 2 ? 0 : 1;
@@ -1664,8 +1728,11 @@ uLong deflateBound(z_streamp strm, uLong sourceLen) {          // deflate.c:842-
     const uLong fixedlen = sourceLen + (sourceLen >> 3) + (sourceLen >> 8) + (sourceLen >> 9) + 4;
     const uLong storelen = sourceLen + (sourceLen >> 5) + (sourceLen >> 7) + (sourceLen >> 11) + 7;
     if (!strm || !strm->state) return (fixedlen > storelen ? fixedlen : storelen) + 18;
-    const int w = strm->state->wrap;
+    const internal_state *s = strm->state;
+    const int w = s->wrap;
     const uLong wraplen = w == 0 ? 0 : w == 1 ? 6 : 18;
+    if (s->wbits != 15 || s->mem_level + 7 != 8 + 7)   // not the default parameters: a conservative bound
+        return (s->wbits <= s->mem_level + 7 && s->level ? fixedlen : storelen) + wraplen;
     return sourceLen + (sourceLen >> 12) + (sourceLen >> 14) + (sourceLen >> 25) + 13 - 6 + wraplen;
 }
 

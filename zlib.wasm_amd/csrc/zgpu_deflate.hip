@@ -38,6 +38,12 @@ constexpr uint32_t kParseFallback = 0xffffffffu;
 __device__ inline uint32_t hash3(uint32_t b0, uint32_t b1, uint32_t b2) {
     return ((b0 & 31u) << 10) ^ (b1 << 5) ^ b2;        // UPDATE_HASH x3, hash_shift 5
 }
+// UPDATE_HASH x3 for any memLevel: ((b0 << 2s) ^ (b1 << s) ^ b2) & mask; with
+// 3s >= hash_bits the rolling hash depends on these three bytes only
+__device__ inline uint32_t hashp(uint32_t b0, uint32_t b1, uint32_t b2, const WinP &w) {
+    return ((b0 << (2 * w.shift)) ^ (b1 << w.shift) ^ b2) & w.mask;
+}
+__device__ inline WinP job_win(const DeflateJob &job) { return win_params(job.wbits, job.hbits); }
 
 // unaligned 4-byte read from an LDS byte array (two aligned dwords + alignbyte)
 __device__ inline uint32_t lds32u(const uint8_t *base, int off) {
@@ -205,10 +211,14 @@ __device__ __attribute__((always_inline)) inline void links_radix_pass(const uin
     __syncthreads();
 }
 
+// kH head entries (1 << hash_bits, <= 32768 in the default layout; 65536 for
+// memLevel 9 with kC = 2048-position chunks so head[] fits in LDS)
+template <int kC, int kH>
 __global__ __launch_bounds__(kLThreads) void k_links(DeflateJob job) {
-    __shared__ uint16_t head[32768];
-    __shared__ uint32_t ka[kLC], kb[kLC];
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kLC + 16];
+    static_assert(kC <= kLC && (kC & (kC - 1)) == 0, "chunk");
+    __shared__ uint16_t head[kH];
+    __shared__ uint32_t ka[kC], kb[kC];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kC + 16];
     __shared__ uint16_t wcnt[kLWaves][256];
     __shared__ int wsum[kLWaves];
     const int tid = threadIdx.x;
@@ -217,23 +227,24 @@ __global__ __launch_bounds__(kLThreads) void k_links(DeflateJob job) {
     const int64_t n = (int64_t)job.src_len[g];
     const uint8_t *in = job.src + job.src_off[g];
     uint16_t *out = job.link + job.ws_off[bi];
+    const WinP wp = job_win(job);
 
-    for (int i = tid; i < 32768; i += kLThreads) head[i] = 32768;   // "position -32768"
-    for (int64_t c0 = 0; c0 < n; c0 += kLC) {
+    for (int i = tid; i < kH; i += kLThreads) head[i] = 32768;   // "position -32768"
+    for (int64_t c0 = 0; c0 < n; c0 += kC) {
         __syncthreads();
         if ((c0 & 32767) == 0 && c0 > 0) {                   // slide sweep (slide_hash analogue)
             const uint32_t now = (uint32_t)c0;
-            for (int i = tid; i < 32768; i += kLThreads) {
+            for (int i = tid; i < kH; i += kLThreads) {
                 const uint32_t age = (now - head[i]) & 0xffffu;
                 if (age == 0 || age >= 32768u) head[i] = (uint16_t)((now - 32768u) & 0xffffu);
             }
         }
-        stage_bytes<kLThreads, (kLC + 16) / 16 / kLThreads + 1>(stage, in, c0, kLC + 16, n, tid);
+        stage_bytes<kLThreads, (kC + 16) / 16 / kLThreads + 1>(stage, in, c0, kC + 16, n, tid);
         __syncthreads();
-        const int cnt = (int)((n - c0) < kLC ? (n - c0) : kLC);          // positions in the chunk
-        const int m = (int)((n - 2 - c0) < kLC ? ((n - 2 - c0) > 0 ? n - 2 - c0 : 0) : kLC);   // p <= n-3
+        const int cnt = (int)((n - c0) < kC ? (n - c0) : kC);            // positions in the chunk
+        const int m = (int)((n - 2 - c0) < kC ? ((n - 2 - c0) > 0 ? n - 2 - c0 : 0) : kC);   // p <= n-3
         for (int e = tid; e < m; e += kLThreads)
-            ka[e] = hash3(stage[e], stage[e + 1], stage[e + 2]) << 13 | (uint32_t)e;
+            ka[e] = hashp(stage[e], stage[e + 1], stage[e + 2], wp) << 13 | (uint32_t)e;
         links_radix_pass(ka, kb, m, 13, wcnt, wsum, tid);
         links_radix_pass(kb, ka, m, 21, wcnt, wsum, tid);
         // sorted: ka[i] = hash << 13 | e, hashes ascending, e ascending within a hash
@@ -508,18 +519,19 @@ __device__ __attribute__((always_inline)) inline bool mw14_loop(MW3 &w, uint32_t
 template <int kUnroll, bool kBatch, int kProbe = 0>
 __device__ __attribute__((always_inline)) inline void mw14_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
                                                                 const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
-                                                                int want_q, uint32_t *st_steps = nullptr,
+                                                                int want_q, int64_t max_dist,
+                                                                uint32_t *st_steps = nullptr,
                                                                 uint32_t *st_cmp = nullptr) {
     const int s = (int)(p - B);
     const uint32_t e0 = E[s];
     const uint32_t d0 = e0 & 0xffffu;
-    if (d0 > (uint32_t)kMaxDist) {
+    if (d0 > (uint32_t)max_dist) {                 // deflate.c:1955: strstart - hash_head <= MAX_DIST
         rf[p] = 0;
         if (want_q) rq[p] = 0;
         return;
     }
     MW3 w;
-    const int64_t labs = p > kMaxDist ? p - kMaxDist : 0;
+    const int64_t labs = p > max_dist ? p - max_dist : 0;
     w.limit4 = (int)(labs - B) * 4;
     const int64_t rem = n - p;
     w.nice = rem < cfg.nice ? (int)rem : cfg.nice;
@@ -634,6 +646,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
     uint32_t *rq = job.rquart + job.ws_off[bi];
     const uint8_t *K = kSorted ? job.key + job.ws_off[bi] : nullptr;
     const LevelCfg cfg = c_ct.cfg[job.level];
+    const int64_t max_dist = job_win(job).max_dist;
     uint64_t st_lane_steps = 0, st_cmps = 0, st_walks = 0, st_wave_iters = 0;
 
     TilePre P;
@@ -688,7 +701,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
             const int64_t nl = kEv ? flush_limit(job, p, n) : n;
             if (kVariant == kMatchStats) {
                 uint32_t steps = 0, cmps = 0;
-                mw14_walk<2, false>(E, p, B, nl, cfg, rf, rq, want_q, &steps, &cmps);
+                mw14_walk<2, false>(E, p, B, nl, cfg, rf, rq, want_q, max_dist, &steps, &cmps);
                 uint32_t mx = steps;
 #pragma unroll
                 for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
@@ -697,9 +710,9 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
                 st_walks += steps ? 1u : 0u;
                 if ((tid & 63) == __builtin_ctzll(__ballot(1))) st_wave_iters += mx;
             } else if (kVariant == kMatchProbeNoCmp) {
-                mw14_walk<2, false, 1>(E, p, B, nl, cfg, rf, rq, want_q);
+                mw14_walk<2, false, 1>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
             } else if (kVariant == kMatchProbeCmpOnly) {
-                mw14_walk<2, false, 2>(E, p, B, nl, cfg, rf, rq, want_q);
+                mw14_walk<2, false, 2>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
 
 
 
@@ -707,7 +720,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
                 rf[p] = 0;                                  // probe: staging, sort and stores only
                 if (want_q) rq[p] = 0;
             } else {
-                mw14_walk<2, false>(E, p, B, nl, cfg, rf, rq, want_q);
+                mw14_walk<2, false>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
             }
         }
         __syncthreads();
@@ -728,12 +741,15 @@ struct ParseOut {
     BlockRec *blk;
     uint32_t nsym, blk_nsym, blk_sym_start, nblk;
     int64_t block_start, S, E;
+    int64_t wsize, max_dist;      // w_size, MAX_DIST (deflate.c:440-444)
+    uint32_t sym_limit;           // lit_bufsize - 1 (deflate.c:455, deflate.h:371)
     bool lead;               // the lane that stores (the state itself is wave-uniform)
 
+    __device__ inline void win(const WinP &w) { wsize = w.wsize; max_dist = w.max_dist; sym_limit = w.sym_limit; }
     __device__ inline bool tally(uint32_t v) {          // _tr_tally_*: returns bflush
         if (lead) sym[nsym] = v;
         nsym++;
-        return ++blk_nsym == (uint32_t)kSymLimit;
+        return ++blk_nsym == sym_limit;
     }
     __device__ inline void flush(int64_t strstart, bool last) {   // FLUSH_BLOCK_ONLY
         BlockRec r;
@@ -763,8 +779,8 @@ struct ParseOut {
     // fill_window (deflate.c:251-368), bookkeeping only; n = the end of the
     // input deflate() has been given so far
     __device__ inline void fill(int64_t p, int64_t n) {
-        if (p - S >= (int64_t)(kWSize + kMaxDist)) S += kWSize;
-        if (E < n) { int64_t e = S + 2 * kWSize; E = e < n ? e : n; }
+        if (p - S >= wsize + max_dist) S += wsize;
+        if (E < n) { int64_t e = S + 2 * wsize; E = e < n ? e : n; }
     }
 };
 
@@ -785,6 +801,7 @@ struct ParseU {                     // wave-uniform parse output state
     BlockRec *blk;
     uint32_t nsym, blk_nsym, blk_sym_start, nblk;
     uint32_t block_start, S, E;
+    uint32_t wsize, max_dist, sym_limit;     // w_size, MAX_DIST, lit_bufsize - 1
     __device__ inline void flush(uint32_t strstart, bool last, int lane) {   // FLUSH_BLOCK_ONLY
         if (lane == 0) {
             BlockRec r;
@@ -804,7 +821,7 @@ struct ParseU {                     // wave-uniform parse output state
     __device__ inline bool tally1(uint32_t v, int lane) {                   // _tr_tally_*
         if (lane == 0) sym[nsym] = v;
         nsym++;
-        return ++blk_nsym == (uint32_t)kSymLimit;
+        return ++blk_nsym == sym_limit;
     }
     __device__ inline void marker(uint32_t strstart, uint32_t kind, int lane) {   // see ParseOut::marker
         if (lane == 0) {
@@ -819,8 +836,8 @@ struct ParseU {                     // wave-uniform parse output state
         nblk++;
     }
     __device__ inline void fill(uint32_t p, uint32_t n) {                   // fill_window bookkeeping
-        if (p - S >= (uint32_t)(kWSize + kMaxDist)) S += kWSize;
-        if (E < n) { uint32_t e = S + 2 * kWSize; E = e < n ? e : n; }
+        if (p - S >= wsize + max_dist) S += wsize;
+        if (E < n) { uint32_t e = S + 2 * wsize; E = e < n ? e : n; }
     }
 };
 
@@ -845,6 +862,10 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
     po.sym = job.sym + job.ws_off[bi];
     po.blk = job.blocks + job.blk_off[bi];
     po.nsym = po.blk_nsym = po.blk_sym_start = po.nblk = 0;
+    {
+        const WinP wp = job_win(job);
+        po.wsize = (uint32_t)wp.wsize; po.max_dist = (uint32_t)wp.max_dist; po.sym_limit = wp.sym_limit;
+    }
     // a resumed flush job starts at its last flush: window read up to there
     // (E), nothing pending, a new block (deflate.c state after :2030-2042)
     uint32_t p = job.start, match_start = 0, match_length = kMinMatch - 1;
@@ -896,13 +917,13 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
                     uint32_t a = avail ? p - 1 : p;
                     const uint32_t b = p + k - 1;
                     while (a < b) {
-                        const uint32_t room = kSymLimit - po.blk_nsym;
+                        const uint32_t room = po.sym_limit - po.blk_nsym;
                         const uint32_t take = (b - a) < room ? (b - a) : room;
                         if ((uint32_t)lane < take) po.sym[po.nsym + lane] = s_in[a + lane - t0 + 16];
                         po.nsym += take;
                         po.blk_nsym += take;
                         a += take;
-                        if (po.blk_nsym == (uint32_t)kSymLimit) po.flush(a, false, lane);
+                        if (po.blk_nsym == po.sym_limit) po.flush(a, false, lane);
                     }
                     avail = true;
                     p += k;
@@ -1070,14 +1091,14 @@ __device__ __attribute__((always_inline)) inline int slow_step(SlowLane &L, uint
 // p at which the k-th window slide (k >= 1) becomes due: fill_window is called
 // when lookahead < MIN_LOOKAHEAD and slides when strstart >= WSIZE+MAX_DIST
 // (deflate.c:277); with all input present the window end is min(n, S + 64K).
-__device__ inline int64_t slide_threshold(uint32_t k, uint32_t n, int64_t refill = kMinLookahead - 1) {
+__device__ inline int64_t slide_threshold(uint32_t k, uint32_t n, int64_t refill, const WinP &w) {
     // fill_window runs at a decision point p with lookahead E - p <= refill
     // (261 for deflate_slow/fast, 258 for deflate_rle, 0 for deflate_huff) and
     // slides when p - S >= WSIZE + MAX_DIST (deflate.c:277); all input is
-    // present, so the window end is E = min(n, S + 64K).
-    const int64_t S = (int64_t)kWSize * (k - 1);
-    const int64_t E = (int64_t)n > S + 2 * kWSize ? S + 2 * kWSize : (int64_t)n;
-    const int64_t a = E - refill, b = S + kWSize + kMaxDist;
+    // present, so the window end is E = min(n, S + 2 WSIZE).
+    const int64_t S = w.wsize * (k - 1);
+    const int64_t E = (int64_t)n > S + 2 * w.wsize ? S + 2 * w.wsize : (int64_t)n;
+    const int64_t a = E - refill, b = S + w.wsize + w.max_dist;
     return a > b ? a : b;
 }
 
@@ -1107,6 +1128,8 @@ struct SymBuf {
 };
 
 __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
+    const WinP wp = job_win(job);
+    const uint32_t symlim = wp.sym_limit;
     __shared__ uint32_t s_y[kParseLanes], s_sig[kParseLanes];
     __shared__ uint32_t s_wsum[kParseLanes / 64];
     __shared__ int s_fail;
@@ -1253,7 +1276,7 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
         total += t;
     }
     const uint32_t base = woff + incl - cnt;
-    const uint32_t ncut = total / kSymLimit - ((s_final && total % kSymLimit == 0) ? 1u : 0u);
+    const uint32_t ncut = total / symlim - ((s_final && total % symlim == 0) ? 1u : 0u);
     // the symbols of lane i tile the input from y(i-1) - sig(i-1) (its first
     // symbol may be the literal pending at y(i-1))
     const uint32_t pos0 = start - start_av;
@@ -1283,8 +1306,8 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
             if (have) {
                 const uint32_t gi = jb + idx;
                 sym[gi] = v;
-                if ((gi + 1) % (uint32_t)kSymLimit == 0 && (gi + 1) / (uint32_t)kSymLimit <= ncut) {
-                    const uint32_t b = (gi + 1) / (uint32_t)kSymLimit - 1;
+                if ((gi + 1) % symlim == 0 && (gi + 1) / symlim <= ncut) {
+                    const uint32_t b = (gi + 1) / symlim - 1;
                     blk[b].in_end = (uint64_t)(sp + len);
                     blk[b].pad = sp + 1;                        // decision point of the flush
                 }
@@ -1296,7 +1319,7 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
 
     // ---- block records (all cut fields read before any record is written)
     uint32_t nthr = 0;
-    while (slide_threshold(nthr + 1, n) <= (int64_t)n) nthr++;
+    while (slide_threshold(nthr + 1, n, kMinLookahead - 1, wp) <= (int64_t)n) nthr++;
     constexpr int kRecs = 8;
     BlockRec r[kRecs];
     for (uint32_t b0 = 0; b0 <= ncut; b0 += kParseLanes * kRecs) {
@@ -1309,12 +1332,12 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
             const uint64_t pd = last ? n : blk[b].pad;
             const uint64_t in_start = b == 0 ? 0 : blk[b - 1].in_end;
             uint32_t slides = 0;
-            while (slides < nthr && slide_threshold(slides + 1, n) <= (int64_t)pd) slides++;
-            r[u].sym_start = b * kSymLimit;
-            r[u].nsym = last ? total - b * kSymLimit : (uint32_t)kSymLimit;
+            while (slides < nthr && slide_threshold(slides + 1, n, kMinLookahead - 1, wp) <= (int64_t)pd) slides++;
+            r[u].sym_start = b * symlim;
+            r[u].nsym = last ? total - b * symlim : symlim;
             r[u].in_start = in_start;
             r[u].in_end = in_end;
-            r[u].flags = (last ? 1u : 0u) | (in_start >= (uint64_t)kWSize * slides ? 2u : 0u);
+            r[u].flags = (last ? 1u : 0u) | (in_start >= (uint64_t)wp.wsize * slides ? 2u : 0u);
             r[u].pad = 0;
         }
         __syncthreads();
@@ -1337,23 +1360,24 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
 // flushed at n.  cut_end/cut_pd: per cut, the end and decision point.
 // ------------------------------------------------------------------------
 __device__ void cut_blocks(BlockRec *blk, uint32_t n, uint32_t total, const uint32_t *cut_end,
-                           const uint32_t *cut_pd, int64_t refill, int tid, int nthreads) {
-    const uint32_t ncut = total / kSymLimit;
+                           const uint32_t *cut_pd, int64_t refill, int tid, int nthreads, const WinP &wp) {
+    const uint32_t symlim = wp.sym_limit;
+    const uint32_t ncut = total / symlim;
     uint32_t nthr = 0;
-    while (slide_threshold(nthr + 1, n, refill) <= (int64_t)n) nthr++;
+    while (slide_threshold(nthr + 1, n, refill, wp) <= (int64_t)n) nthr++;
     for (uint32_t b = tid; b <= ncut; b += nthreads) {
         const bool last = b == ncut;
         const uint64_t in_end = last ? n : cut_end[b];
         const uint64_t pd = last ? n : cut_pd[b];
         const uint64_t in_start = b == 0 ? 0 : cut_end[b - 1];
         uint32_t slides = 0;
-        while (slides < nthr && slide_threshold(slides + 1, n, refill) <= (int64_t)pd) slides++;
+        while (slides < nthr && slide_threshold(slides + 1, n, refill, wp) <= (int64_t)pd) slides++;
         BlockRec r;
-        r.sym_start = b * kSymLimit;
-        r.nsym = last ? total - b * kSymLimit : (uint32_t)kSymLimit;
+        r.sym_start = b * symlim;
+        r.nsym = last ? total - b * symlim : symlim;
         r.in_start = in_start;
         r.in_end = in_end;
-        r.flags = (last ? 1u : 0u) | (in_start >= (uint64_t)kWSize * slides ? 2u : 0u);
+        r.flags = (last ? 1u : 0u) | (in_start >= (uint64_t)wp.wsize * slides ? 2u : 0u);
         r.pad = 0;
         blk[b] = r;
     }
@@ -1370,18 +1394,20 @@ __global__ __launch_bounds__(kHuffThreads) void k_parse_huff(DeflateJob job) {
     const uint8_t *in = job.src + job.src_off[g];
     uint32_t *sym = job.sym + job.ws_off[bi];
     BlockRec *blk = job.blocks + job.blk_off[bi];
+    const WinP wp = job_win(job);
+    const uint32_t symlim = wp.sym_limit;
     for (uint32_t i = tid; i < n; i += kHuffThreads) sym[i] = in[i];
     // cut ends / decision points live in the rfull workspace (unused here)
     uint32_t *cut_end = job.rfull + job.ws_off[bi];
-    uint32_t *cut_pd = cut_end + (n / kSymLimit + 1);
-    const uint32_t ncut = n / kSymLimit;
+    uint32_t *cut_pd = cut_end + (n / symlim + 1);
+    const uint32_t ncut = n / symlim;
     for (uint32_t b = tid; b < ncut; b += kHuffThreads) {
-        cut_end[b] = (b + 1) * kSymLimit;
-        cut_pd[b] = (b + 1) * kSymLimit - 1;
+        cut_end[b] = (b + 1) * symlim;
+        cut_pd[b] = (b + 1) * symlim - 1;
     }
     __threadfence_block();
     __syncthreads();
-    cut_blocks(blk, n, n, cut_end, cut_pd, 0, tid, kHuffThreads);
+    cut_blocks(blk, n, n, cut_end, cut_pd, 0, tid, kHuffThreads, wp);
     if (tid == 0) job.nblocks[bi] = ncut + 1;
 }
 
@@ -1397,8 +1423,10 @@ __global__ __launch_bounds__(64) void k_parse_rle(DeflateJob job) {
     const uint8_t *in = job.src + job.src_off[g];
     uint32_t *sym = job.sym + job.ws_off[bi];
     BlockRec *blk = job.blocks + job.blk_off[bi];
+    const WinP wp = job_win(job);
+    const uint32_t symlim = wp.sym_limit;
     uint32_t *cut_end = job.rfull + job.ws_off[bi];
-    uint32_t *cut_pd = cut_end + (n / kSymLimit + 1);
+    uint32_t *cut_pd = cut_end + (n / symlim + 1);
     __shared__ uint32_t s_total;
     if (lane == 0) {
         BCache cb;
@@ -1418,9 +1446,9 @@ __global__ __launch_bounds__(64) void k_parse_rle(DeflateJob job) {
             if (len >= (uint32_t)kMinMatch) { v = (1u << 8) | (len - kMinMatch); sl = len; }
             else { v = bget(in, p, cb); sl = 1; }
             sym[cnt] = v;
-            if ((cnt + 1) % (uint32_t)kSymLimit == 0) {
-                cut_end[cnt / kSymLimit] = p + sl;
-                cut_pd[cnt / kSymLimit] = p;
+            if ((cnt + 1) % symlim == 0) {
+                cut_end[cnt / symlim] = p + sl;
+                cut_pd[cnt / symlim] = p;
             }
             cnt++;
             p += sl;
@@ -1430,8 +1458,8 @@ __global__ __launch_bounds__(64) void k_parse_rle(DeflateJob job) {
     __threadfence_block();
     __syncthreads();
     const uint32_t total = s_total;
-    cut_blocks(blk, n, total, cut_end, cut_pd, kMaxMatch, lane, 64);
-    if (lane == 0) job.nblocks[bi] = total / kSymLimit + 1;
+    cut_blocks(blk, n, total, cut_end, cut_pd, kMaxMatch, lane, 64, wp);
+    if (lane == 0) job.nblocks[bi] = total / symlim + 1;
 }
 
 // ------------------------------------------------------------------------
@@ -1452,6 +1480,7 @@ __global__ __launch_bounds__(64) void k_parse_ev(DeflateJob job) {
     po.sym = job.sym + job.ws_off[bi];
     po.blk = job.blocks + job.blk_off[bi];
     po.nsym = po.blk_nsym = po.blk_sym_start = po.nblk = 0;
+    po.win(job_win(job));
     po.lead = true;
     int64_t p = job.start;                      // a resumed job: see k_parse_slow
     po.block_start = p; po.S = 0; po.E = p;
@@ -1517,12 +1546,14 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     const int64_t n = (int64_t)job.src_len[g];
     const uint8_t *in = job.src + job.src_off[g];
     uint16_t *prev = job.link + job.ws_off[bi];
-    uint32_t *head = heads + (size_t)bi * 32768;
+    const WinP wp = job_win(job);
+    const uint32_t hsize = wp.mask + 1;                  // hash_size = 1 << hash_bits
+    uint32_t *head = heads + (size_t)bi * hsize;
     const LevelCfg cfg = c_ct.cfg[job.level];
     // a resumed flush job (start > 0) finds head[] and prev[] as the last job
     // left them, rebased to its buffer (zgpu_api.cpp deflate_part)
     if (!kEv || job.start == 0)
-        for (int i = lane; i < 32768; i += 64) head[i] = 0;
+        for (int i = lane; i < (int)hsize; i += 64) head[i] = 0;
     __threadfence_block();
     __syncthreads();
 
@@ -1530,6 +1561,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     po.sym = job.sym + job.ws_off[bi];
     po.blk = job.blocks + job.blk_off[bi];
     po.nsym = po.blk_nsym = po.blk_sym_start = po.nblk = 0;
+    po.win(job_win(job));
     const int64_t start = kEv ? (int64_t)job.start : 0;
     po.block_start = start; po.S = 0; po.E = start;
     po.lead = lead;
@@ -1551,7 +1583,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         const int o = (int)(x - wb);
         return (uint32_t)__builtin_amdgcn_readlane((int)(o < 64 ? w0 : w1), o & 63);
     };
-    auto whash = [&](int64_t q) -> uint32_t { return hash3(wbyte(q), wbyte(q + 1), wbyte(q + 2)); };
+    auto whash = [&](int64_t q) -> uint32_t { return hashp(wbyte(q), wbyte(q + 1), wbyte(q + 2), wp); };
     auto insert = [&](int64_t q) -> int64_t {           // INSERT_STRING
         const uint32_t h = whash(q);
         const int64_t hh = ufl(head[h]);
@@ -1623,12 +1655,12 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         int64_t lookahead = po.E - p;
         int64_t hh = 0;
         if (lookahead >= kMinMatch) hh = insert(p);
-        if (hh > po.S && p - hh <= kMaxDist) {
+        if (hh > po.S && p - hh <= wp.max_dist) {
             // longest_match (deflate.c:1356-1497), prev_length == 2: the first
             // candidate with the longest prefix wins, stop at nice, chain, limit
             uint32_t chain = cfg.chain;
             const int nice = lookahead < cfg.nice ? (int)lookahead : cfg.nice;
-            const int64_t limit = (p - po.S) > kMaxDist ? p - kMaxDist : po.S;
+            const int64_t limit = (p - po.S) > wp.max_dist ? p - wp.max_dist : po.S;
             const int64_t rem = n - p;
             const int maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
             int best = kMinMatch - 1;
@@ -1950,7 +1982,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
         s_obit = job.bit0;                      // a resumed flush job: the partial byte's bits
         stg[0] = job.byte0;
         if (job.wrap == 1) {                    // zlib header (deflate.c:1004-1037)
-            uint32_t header = (8u + ((15u - 8u) << 4)) << 8;
+            uint32_t header = (8u + ((uint32_t)(job.wbits - 8) << 4)) << 8;
             uint32_t flags = (job.strategy >= 2 || level < 2) ? 0u : level < 6 ? 1u : level == 6 ? 2u : 3u;
             header |= flags << 6;
             header += 31 - (header % 31);
@@ -2227,7 +2259,8 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     const dim3 grid(job.count);
     switch (stage) {
     case 0:
-        hipLaunchKernelGGL(k_links, grid, dim3(kLThreads), 0, st, job);
+        if (job.hbits > 15) hipLaunchKernelGGL((k_links<2048, 65536>), grid, dim3(kLThreads), 0, st, job);
+        else hipLaunchKernelGGL((k_links<kLC, 32768>), grid, dim3(kLThreads), 0, st, job);
         if (match_variant() != 14) hipLaunchKernelGGL(k_count, grid, dim3(kCntThreads), 0, st, job);
         break;
     case 1: {

@@ -139,7 +139,27 @@ struct DeflateJob {
     // workgroup per buffer
     const uint32_t *seg;
     uint32_t nseg, seg_len;
+    // deflateInit2_'s windowBits (9..15; 8 is stored as 9, deflate.c:395) and
+    // memLevel + 7 = hash_bits (8..16): w_size = 1 << wbits, MAX_DIST = w_size
+    // - 262, hash_shift = (hash_bits + 2) / 3, lit_bufsize = 1 << (memLevel + 6)
+    // and the block cut at lit_bufsize - 1 symbols (deflate.c:440-455)
+    int wbits, hbits;
 };
+
+// the per-job window/hash parameters (deflate.c:440-455)
+struct WinP {
+    int64_t wsize, max_dist;
+    uint32_t shift, mask, sym_limit;
+};
+__host__ __device__ inline WinP win_params(int wbits, int hbits) {
+    WinP w;
+    w.wsize = (int64_t)1 << wbits;
+    w.max_dist = w.wsize - kMinLookahead;
+    w.shift = (uint32_t)(hbits + kMinMatch - 1) / kMinMatch;
+    w.mask = (1u << hbits) - 1u;
+    w.sym_limit = (1u << (hbits - 7 + 6)) - 1u;
+    return w;
+}
 
 // ---- inflate ----
 // where k_inflate_decode stopped (zo_inflate_run's codes)

@@ -40,6 +40,7 @@ EXPORTED_SYMBOLS = (
     "zgpu_crc32_batch_dev", "zgpu_adler32_batch_dev", "zgpu_compress_batch",
     "zgpu_crc32_batch", "zgpu_adler32_batch", "zgpu_generate_dev", "zgpu_stage_timing",
     "zgpu_stage_timing_read", "zgpu_inflate_batch_dev", "zgpu_uncompress_batch",
+    "zgpu_deflate_batch_dev2", "zgpu_compress_batch2",
     # include/zgpu_zlib.h
     "zlibVersion", "compress", "compress2", "compressBound", "deflateInit_",
     "deflateInit2_", "deflate", "deflateEnd", "deflateBound", "deflateReset", "deflateCopy", "deflatePending", "crc32", "crc32_z",
@@ -102,6 +103,10 @@ def load(path=LIB_PATH):
     L.zgpu_compress_batch.argtypes = [P, P, P, P, P, C.c_size_t, I32, I32]
     L.zgpu_compress_batch_ex.restype = I32
     L.zgpu_compress_batch_ex.argtypes = [P, P, P, P, P, C.c_size_t, I32, I32, I32]
+    L.zgpu_compress_batch2.restype = I32
+    L.zgpu_compress_batch2.argtypes = [P, P, P, P, P, C.c_size_t, I32, I32, I32, I32]
+    L.zgpu_deflate_batch_dev2.restype = I32
+    L.zgpu_deflate_batch_dev2.argtypes = [P, P, P, P, P, P, P, P, U32, I32, I32, I32, I32, P]
     for f in ("zgpu_crc32_batch", "zgpu_adler32_batch"):
         getattr(L, f).restype = I32
         getattr(L, f).argtypes = [P, P, P, P, C.c_size_t]
@@ -176,6 +181,26 @@ def compress_batch(bufs, level=6, wrap=WRAP_ZLIB, caps=None, strategy=0):
     rc = L.zgpu_compress_batch_ex(src, lens, dst, dlen, st, n, level, wrap, strategy)
     if rc:
         raise ZlibCompressionError(f"zgpu_compress_batch failed: {rc}")
+    del keep
+    return [(st[i], outs[i].raw[: dlen[i]]) for i in range(n)]
+
+
+def compress_batch2(bufs, level=6, window_bits=15, mem_level=8, strategy=0, caps=None):
+    """compress_batch with deflateInit2_'s windowBits (8..15 zlib, -15..-9 raw,
+    25..31 gzip) and memLevel (1..9); returns [(status, bytes)]."""
+    L = load()
+    n = len(bufs)
+    src, keep = _ptr_array(bufs)
+    lens = (C.c_size_t * n)(*[len(b) for b in bufs])
+    if caps is None:                                 # deflateBound's conservative bound + wrapper
+        caps = [conservative_bound(len(b)) + 18 for b in bufs]
+    outs = [C.create_string_buffer(max(c, 1)) for c in caps]
+    dst = (C.c_void_p * n)(*[C.addressof(o) for o in outs])
+    dlen = (C.c_size_t * n)(*caps)
+    st = (C.c_int * n)()
+    rc = L.zgpu_compress_batch2(src, lens, dst, dlen, st, n, level, window_bits, mem_level, strategy)
+    if rc:
+        raise ZlibCompressionError(f"zgpu_compress_batch2 failed: {rc}")
     del keep
     return [(st[i], outs[i].raw[: dlen[i]]) for i in range(n)]
 
