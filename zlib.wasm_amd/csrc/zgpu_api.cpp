@@ -1174,6 +1174,7 @@ int zgpu_debug_stages(const uint8_t *src, size_t n, int level, uint16_t *link, u
     DeflateJob job{};
     job.src = c.ws_io.as<uint8_t>(); job.src_off = d_meta; job.src_len = d_meta + 1;
     job.first = 0; job.count = 1; job.level = level; job.wrap = 1;
+    job.wbits = 15; job.hbits = 15;                   // deflateInit_ defaults (deflate.c:444)
     job.ws_off = d_meta + 2;
     job.link = c.ws_link.as<uint16_t>();
     job.rfull = c.ws_rf.as<uint32_t>();
