@@ -1,14 +1,12 @@
-#!/bin/bash
-# A/B of k_match variants on one L6 sub-batch (4096 x 1 MiB Silesia-style),
-# no pipeline so per-stage times are clean.  Usage: tools/ab_match.sh V1 V2 ...
+# A/B of k_match variants (ZGPU_MATCH_VARIANT): parity tests, walk statistics, bench
 set -o pipefail
-mkdir -p gpurun_out
-for v in "$@"; do
-  ZGPU_MATCH_VARIANT=$v ZGPU_NO_PIPELINE=1 timeout -k 10 240 python bench.py --buffers 4096 --steps 2 --warmup 1 \
-      --no-cpu --no-inflate --verify 4 --crc-buffers 1024 ${AB_ARGS} > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err || exit $?
-  python - "$v" <<'PY'
-import json, sys
-d = json.load(open(f"gpurun_out/ab_{sys.argv[1]}.json"))
-print("variant", sys.argv[1], "MB/s", d["value"], "stages", d["stage_ms_per_step"])
-PY
+V=${1:-40}
+export ZGPU_MATCH_VARIANT=$V
+timeout -k 10 400 python -u -m pytest tests/test_gpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/v${V}_tests.log 2>&1
+echo "tests rc=$?" >> gpurun_out/v${V}_tests.log
+for S in 41 21; do
+  ZGPU_MATCH_VARIANT=$S timeout -k 10 200 python bench.py --steps 1 --warmup 0 --buffers 4096 --no-cpu --no-inflate --crc-buffers 4096 --adler-buffers 0 --verify 2 > gpurun_out/v${S}_stats.json 2> gpurun_out/v${S}_stats.err
+done
+for W in $V 19; do
+  ZGPU_MATCH_VARIANT=$W timeout -k 10 200 python bench.py --steps 2 --warmup 1 --buffers 8192 --no-cpu --no-inflate --crc-buffers 4096 --adler-buffers 0 > gpurun_out/v${W}_bench.json 2> gpurun_out/v${W}_bench.err
 done

@@ -1,21 +1,9 @@
-#!/bin/bash
-# LDS-side PMC counters of k_match for the given variants (one 512 x 1 MiB L6
-# sub-batch, no pipeline).  Usage: tools/pmc_match.sh V1 V2 ...
-set -e
-mkdir -p gpurun_out/pmcm
+# SQ counters of k_match for two variants (rocprofv3 --pmc, one pass per counter set)
+set -o pipefail
 export TMPDIR=/tmp
-for v in "$@"; do
-  ZGPU_MATCH_VARIANT=$v ZGPU_NO_PIPELINE=1 timeout -s KILL 120 rocprofv3 --pmc ${PMC:-SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE} \
-     --kernel-include-regex k_match --output-format csv -d gpurun_out/pmcm/v$v -o run -- \
-     python3 bench.py --steps 1 --warmup 0 --buffers 512 --no-cpu --no-inflate --verify 1 --crc-buffers 1024 > gpurun_out/pmcm/v$v.json 2> gpurun_out/pmcm/v$v.err
-  python3 - "$v" <<'PY'
-import csv, glob, sys, collections
-v = sys.argv[1]
-f = glob.glob(f"gpurun_out/pmcm/v{v}/**/*counter_collection.csv", recursive=True)[0]
-d = collections.defaultdict(float)
-for r in csv.DictReader(open(f)):
-    if "k_match" in r["Kernel_Name"]:
-        d[r["Counter_Name"]] += float(r["Counter_Value"])
-print("variant", v, {k: f"{x:.4g}" for k, x in sorted(d.items())})
-PY
+mkdir -p gpurun_out/pmc
+for V in "$@"; do
+  export ZGPU_MATCH_VARIANT=$V
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU --output-format csv -d gpurun_out/pmc/v${V}a -o run -- python3 bench.py --steps 1 --warmup 0 --buffers 512 --no-cpu --no-inflate --verify 1 --crc-buffers 4096 --adler-buffers 0 > gpurun_out/pmc/v${V}a.json 2> gpurun_out/pmc/v${V}a.err || exit 1
+  timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc/v${V}b -o run -- python3 bench.py --steps 1 --warmup 0 --buffers 512 --no-cpu --no-inflate --verify 1 --crc-buffers 4096 --adler-buffers 0 > gpurun_out/pmc/v${V}b.json 2> gpurun_out/pmc/v${V}b.err || exit 1
 done

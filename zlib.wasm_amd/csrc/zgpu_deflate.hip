@@ -559,10 +559,231 @@ __device__ __attribute__((always_inline)) inline void mw14_walk(const uint32_t *
     if (st_steps) { *st_steps = w.count; *st_cmp = w.ncmp; }
 }
 
+// ------------------------------------------------------------------------
+// The deferred-compare walk (default).  In mw14_walk a lane whose candidate
+// passes the quick reject compares at once, and the other 63 lanes of its wave
+// wait: 3.4 % of the steps compare, yet 86 % of a wave's steps run the compare
+// code.  Here the compare is taken out of the step:
+//   1. the first kD0 candidates of every walk are compared by the whole wave
+//      together (all lanes start their walks at the same time), so the walk
+//      goes on with the best the chain's head gives -- that is where most
+//      improvements happen;
+//   2. the step tests the quick reject against that (stale) best and, on a
+//      pass, pushes the candidate into a kDQ-deep per-lane queue; a stale best
+//      is never larger than the true one, so the queue holds every candidate
+//      the exact walk would compare (and some it would reject);
+//   3. when some lane's queue is full, at the chain/4 budget snapshot and at
+//      the end, the wave empties the queues together, oldest first, applying
+//      longest_match's rule (a strictly longer match wins, stop at nice) with
+//      the true running best: the result equals longest_match's
+//      (deflate.c:1417-1497) for every position.  A lane that reaches nice in a
+//      flush drops its later entries and steps.
+// A CPU model of the C4 mix at L6: 2.1 queued candidates per walk, a full
+// queue (kDQ 4) on 0.3 % of lane steps.
+// ------------------------------------------------------------------------
+constexpr int kD0 = 2;      // leading candidates compared by the whole wave
+__device__ inline uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+constexpr int kDQ = 4;      // deferred-compare queue depth
+
+// bytes i..i+3 from the packed words: one byte permute (v_perm_b32) of the
+// high halves of E[i] and E[i+2]
+__device__ __attribute__((always_inline)) inline uint32_t get4p(const uint32_t *E, int i) {
+    return __builtin_amdgcn_perm(E[i + 2], E[i], 0x07060302u);
+}
+
+// lowest set bit of x, or 0xffffffff for x == 0 (v_ffbl_b32's own result)
+__device__ __attribute__((always_inline)) inline uint32_t ffbl(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
+// index of the first differing byte of two 16-byte strings given as four
+// xor words, 16 if none.  ffbl(x_j) | 32 j is 32 j + ctz(x_j), or stays
+// 0xffffffff when x_j == 0, so one min over the four needs no branch.
+__device__ __attribute__((always_inline)) inline int diff16(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+    const uint32_t b = min(min(ffbl(x0), ffbl(x1) | 32u), min(ffbl(x2) | 64u, ffbl(x3) | 96u));
+    return (int)(min(b, 128u) >> 3);
+}
+
+// LCP of the scan at s and the candidate at m, capped at maxcmp: 16 bytes per
+// LDS round trip (all reads of a round issued before any test).
+__device__ __attribute__((always_inline)) inline int lcp16(const uint32_t *E, int m, int s, const Scan16 &S,
+                                                           int maxcmp) {
+    int k = diff16(get4p(E, m) ^ S.s0, get4p(E, m + 4) ^ S.s1, get4p(E, m + 8) ^ S.s2, get4p(E, m + 12) ^ S.s3);
+    if (k >= 16) {
+        while (k < maxcmp) {
+            const int r = diff16(get4p(E, m + k) ^ get4p(E, s + k), get4p(E, m + k + 4) ^ get4p(E, s + k + 4),
+                                 get4p(E, m + k + 8) ^ get4p(E, s + k + 8), get4p(E, m + k + 12) ^ get4p(E, s + k + 12));
+            k += r;
+            if (r < 16) break;
+        }
+    }
+    return k < maxcmp ? k : maxcmp;
+}
+
+// The walk state between flushes.  Candidate m (byte address m4 = 4 m) has
+// its two words em (link, bytes m, m+1) and eb (bytes m+best-1, m+best)
+// loaded; the queue holds byte addresses, newest in q0.
+struct DWS {
+    int m4, limit4, be4, occ;
+    int q0, q1, q2, q3;
+    uint32_t em, eb, scan01, scanE;
+};
+
+// Steps every lane of the wave until the uniform budget count `end` is
+// reached, some lane's queue is full or no lane has a candidate left.  A lane
+// whose chain ended stays in the loop: its candidate address is then <= the
+// limit and only falls further (links are >= 0), so it queues nothing more.
+// The loop has one exit, taken by the whole wave, and every update is a
+// select.  `count` is wave-uniform (all lanes start their walks together and
+// step together).
+__device__ __attribute__((always_inline)) inline void dw_steps(DWS &w, const char *Eb, uint32_t &count, uint32_t end) {
+    for (;;) {
+        const bool valid = w.m4 > w.limit4;
+        const int m4n = w.m4 + (int)(w.em & 0xffffu) * -4;
+        const int a = m4n > 0 ? m4n : 0;
+        const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + a);
+        const uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
+        const bool pass = valid & ((w.em >> 16) == w.scan01) & ((w.eb >> 16) == w.scanE);
+        w.q3 = pass ? w.q2 : w.q3;
+        w.q2 = pass ? w.q1 : w.q2;
+        w.q1 = pass ? w.q0 : w.q1;
+        w.q0 = pass ? w.m4 : w.q0;
+        w.occ += pass ? 1 : 0;
+        w.m4 = m4n;
+        w.em = emn;
+        w.eb = ebn;
+        count++;
+        const uint64_t walkers = __ballot(m4n > w.limit4), full = __ballot(w.occ == kDQ);
+        if (count >= end || walkers == 0 || full != 0) break;
+    }
+}
+
+__device__ inline uint32_t match_rec(int best, int s4, int bpos4) {
+    return best >= kMinMatch ? (((uint32_t)best << 16) | (uint32_t)((s4 - bpos4) >> 2)) : 0u;
+}
+
+// One position's longest_match with deferred compares.  Every lane of the
+// wave that took a position calls this together (the flushes are wave-wide
+// decisions taken with ballots).
+__device__ unsigned long long g_dstat[4];   // deferred-walk statistics (variant 41)
+
+template <bool kStats = false, int kHead = kD0>
+__device__ __attribute__((always_inline)) inline void dw_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
+                                                              const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
+                                                              int want_q, int64_t max_dist) {
+    const int s = (int)(p - B);
+    const uint32_t e0 = E[s];
+    const uint32_t d0 = e0 & 0xffffu;
+    if (d0 > (uint32_t)max_dist) {                 // deflate.c:1955: strstart - hash_head <= MAX_DIST
+        rf[p] = 0;
+        if (want_q) rq[p] = 0;
+        return;
+    }
+    const int64_t labs = p > max_dist ? p - max_dist : 0;
+    const int limit4 = (int)(labs - B) * 4;
+    const int64_t rem = n - p;
+    const int nice = rem < cfg.nice ? (int)rem : cfg.nice;
+    const int maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
+    const uint32_t chain = (uint32_t)cfg.chain;
+    const uint32_t qc = want_q ? chain >> 2 : chain;
+    const int s4 = s * 4;
+    const Scan16 S{get4(E, s), get4(E, s + 4), get4(E, s + 8), get4(E, s + 12)};
+    int best = kMinMatch - 1, bpos4 = 0;
+    int m4 = (s - (int)d0) * 4;
+    uint32_t count = 0;
+    bool walking = true;
+    // 1. the chain's first kD0 candidates, compared by the whole wave at once
+#pragma unroll
+    for (int k = 0; k < kHead; k++) {
+        if (walking) {
+            const int m = m4 >> 2;
+            const uint32_t em = E[m];
+            const int len = lcp16(E, m, s, S, maxcmp);
+            if (len > best) { best = len; bpos4 = m4; }
+            count++;
+            const int m4n = m4 - (int)((em & 0xffffu) << 2);
+            if (best >= nice || m4n <= limit4 || count >= chain) walking = false;
+            m4 = m4n;
+        }
+    }
+    bool need_q = want_q != 0;
+    if (!walking) {                                  // the walk ended within its head
+        const uint32_t r = match_rec(best, s4, bpos4);
+        if (need_q) rq[p] = r;
+        rf[p] = r;
+        return;
+    }
+    // 2./3. walk with the stale best, queue the passes, flush wave-wide
+    const char *Eb = reinterpret_cast<const char *>(E);
+    DWS w;
+    w.m4 = m4;
+    w.limit4 = limit4;
+    w.be4 = (best - 1) * 4;
+    w.occ = 0;
+    w.q0 = w.q1 = w.q2 = w.q3 = 0;
+    w.scan01 = e0 >> 16;
+    w.scanE = E[s + best - 1] >> 16;
+    w.em = *reinterpret_cast<const uint32_t *>(Eb + m4);
+    w.eb = *reinterpret_cast<const uint32_t *>(Eb + m4 + w.be4);
+    static_assert(kDQ == 4, "queue registers q0..q3");
+    count = ufl(count);                 // every lane still walking took kD0 steps
+    for (;;) {
+        // walk to the next uniform stop: the chain/4 snapshot, the budget, a full queue
+        const uint32_t end = count < qc ? qc : chain;
+        const uint32_t c0 = count;
+        dw_steps(w, Eb, count, end);
+        if (kStats) {
+            int mo = 0;
+#pragma unroll
+            for (int j = 1; j <= kDQ; j++) mo = __ballot(w.occ >= j) != 0 ? j : mo;
+            if (__builtin_ctzll(__ballot(1)) == (threadIdx.x & 63)) {
+                atomicAdd(&g_dstat[0], (unsigned long long)(count - c0));  // wave iterations
+                atomicAdd(&g_dstat[1], 1ull);                              // flushes
+                atomicAdd(&g_dstat[2], (unsigned long long)mo);            // flush rounds
+            }
+        }
+        walking = w.m4 > limit4 && count < chain;
+        // flush, oldest first: entry j (< occ) is the (occ - j)-th oldest
+        const int best0 = best;
+#pragma unroll
+        for (int j = kDQ - 1; j >= 0; j--) {
+            if (__ballot(j < w.occ) != 0) {
+                if (j < w.occ) {
+                    const int mj = j == 3 ? w.q3 : j == 2 ? w.q2 : j == 1 ? w.q1 : w.q0;
+                    const int len = lcp16(E, mj >> 2, s, S, maxcmp);
+                    if (len > best) {
+                        best = len;
+                        bpos4 = mj;
+                        if (len >= nice) { walking = false; w.occ = 0; }   // drop the later entries
+                    }
+                }
+            }
+        }
+        w.occ = 0;
+        if (need_q && (count >= qc || !walking)) {     // deflate.c:1390-1392 (chain >>= 2)
+            rq[p] = match_rec(best, s4, bpos4);
+            need_q = false;
+        }
+        if (!walking) break;
+        if (best != best0) {                           // the quick reject now tests the new best
+            w.be4 = (best - 1) * 4;
+            w.scanE = E[s + best - 1] >> 16;
+            w.eb = *reinterpret_cast<const uint32_t *>(Eb + (w.m4 > 0 ? w.m4 : 0) + w.be4);
+        }
+    }
+    rf[p] = match_rec(best, s4, bpos4);
+}
+
 __device__ unsigned long long g_mstat[4];   // kMatchStats statistics
 
 // k_match variants (ZGPU_MATCH_VARIANT, for A/B runs):
-//   19 (default)  positions of a tile walked in k_count's key order, longest
+//   40 (default)  19 with deferred compares (dw_walk): 495 -> 412 ms per 4 GiB
+//                 C4 sub-batch at L6 (the C4 shard 7.7 -> 9.1 GB/s)
+//   41            40 plus statistics (wave iterations, flushes, flush rounds)
+//   42            40 with three wave-wide head compares (no faster)
+//   19            positions of a tile walked in k_count's key order, longest
 //                 walks first: the 64 walks a wave runs side by side have
 //                 similar lengths (SIMT utilisation 63 % -> 90 % at L6,
 //                 20 % -> 93 % at L9, measured with kMatchStats)
@@ -584,10 +805,12 @@ __device__ unsigned long long g_mstat[4];   // kMatchStats statistics
 //                 sort and stores: 33 ms of 351 per 4 GiB at L6); 35 half the
 //                 waves walk (1.6x slower at L6, 1.8x at L9: the walks are
 //                 latency-bound at the 16 waves the LDS window allows)
-constexpr int kMatchDefault = 19, kMatchStats = 21, kMatchProbeNoWalk = 33, kMatchProbeHalf = 35,
+constexpr int kMatchDefer = 40, kMatchDeferStats = 41, kMatchDefer3 = 42;
+constexpr int kMatchWalk = 19;
+constexpr int kMatchDefault = kMatchDefer;
+constexpr int kMatchStats = 21, kMatchProbeNoWalk = 33, kMatchProbeHalf = 35,
               kMatchProbeNoCmp = 37, kMatchProbeCmpOnly = 38;
 
-__device__ inline uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
 // The deflate(flush) calls of a flush job (DeflateJob::fl_pos/fl_type): the
 // parse runs as if the input ended at the next flush position (deflate() has
@@ -716,6 +939,13 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
 
 
 
+            } else if (kVariant == kMatchDefer) {
+                dw_walk(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+            } else if (kVariant == kMatchDefer3) {
+                dw_walk<false, 3>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+            } else if (kVariant == kMatchDeferStats) {
+                dw_walk<true>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+                if (__builtin_ctzll(__ballot(1)) == (threadIdx.x & 63)) atomicAdd(&g_dstat[3], 1ull);   // wave walks
             } else if (kVariant == kMatchProbeNoWalk) {
                 rf[p] = 0;                                  // probe: staging, sort and stores only
                 if (want_q) rq[p] = 0;
@@ -2249,8 +2479,8 @@ static int match_variant() {
     static const int v = [] {
         const char *e = getenv("ZGPU_MATCH_VARIANT");
         const int x = e ? atoi(e) : kMatchDefault;
-        return (x == 14 || x == kMatchStats || x == kMatchProbeNoWalk || x == kMatchProbeHalf ||
-                x == kMatchProbeNoCmp || x == kMatchProbeCmpOnly) ? x : kMatchDefault;
+        return (x == 14 || x == kMatchWalk || x == kMatchStats || x == kMatchProbeNoWalk || x == kMatchProbeHalf ||
+                x == kMatchProbeNoCmp || x == kMatchProbeCmpOnly || x == kMatchDefer || x == kMatchDeferStats || x == kMatchDefer3) ? x : kMatchDefault;
     }();
     return v;
 }
@@ -2275,6 +2505,20 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
             hipLaunchKernelGGL((k_match<kMatchDefault, false, true>), mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == 14) {
             hipLaunchKernelGGL(k_match<14>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchWalk) {
+            hipLaunchKernelGGL(k_match<kMatchWalk>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchDefer3) {
+            hipLaunchKernelGGL(k_match<kMatchDefer3>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchDeferStats) {
+            unsigned long long z[4] = {0, 0, 0, 0}, r[4];
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dstat), z, sizeof z);
+            hipLaunchKernelGGL(k_match<kMatchDeferStats>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+            (void)hipStreamSynchronize(st);
+            (void)hipMemcpyFromSymbol(r, HIP_SYMBOL(g_dstat), sizeof r);
+            fprintf(stderr, "k_match defer stats: wave_iters %llu flushes %llu flush_rounds %llu wave_walks %llu "
+                    "iters/flush %.2f rounds/flush %.2f flushes/wave-walk %.2f\n", r[0], r[1], r[2], r[3],
+                    r[1] ? (double)r[0] / r[1] : 0.0, r[1] ? (double)r[2] / r[1] : 0.0,
+                    r[3] ? (double)r[1] / r[3] : 0.0);
         } else if (v == kMatchProbeNoWalk) {
             hipLaunchKernelGGL(k_match<kMatchProbeNoWalk>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchProbeHalf) {
