@@ -660,6 +660,56 @@ __device__ __attribute__((always_inline)) inline void dw_steps(DWS &w, const cha
     }
 }
 
+// dw_steps with the full-queue flush inside the loop: when some lane's queue
+// is full, every lane compares its oldest entry (one wave round, a uniform
+// branch) and the walk goes on, with no exit from the loop.  A lane that
+// reaches nice there stops queueing (limit4 = INT_MAX) and drops its entries.
+// Returns at the budget count `end` or when no lane has a candidate left.
+struct DWB {                      // the running best of dw_steps_in
+    int best, bpos4, s, maxcmp, nice;
+};
+
+__device__ __attribute__((always_inline)) inline void dw_steps_in(DWS &w, DWB &b, const uint32_t *E, const Scan16 &S,
+                                                                  uint32_t &count, uint32_t end) {
+    const char *Eb = reinterpret_cast<const char *>(E);
+    for (;;) {
+        const bool valid = w.m4 > w.limit4;
+        const int m4n = w.m4 + (int)(w.em & 0xffffu) * -4;
+        const int a = m4n > 0 ? m4n : 0;
+        const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + a);
+        uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
+        const bool pass = valid & ((w.em >> 16) == w.scan01) & ((w.eb >> 16) == w.scanE);
+        w.q3 = pass ? w.q2 : w.q3;
+        w.q2 = pass ? w.q1 : w.q2;
+        w.q1 = pass ? w.q0 : w.q1;
+        w.q0 = pass ? w.m4 : w.q0;
+        w.occ += pass ? 1 : 0;
+        w.m4 = m4n;
+        w.em = emn;
+        count++;
+        if (__ballot(w.occ == kDQ) != 0) {
+            if (w.occ > 0) {
+                const int mj = w.occ == 4 ? w.q3 : w.occ == 3 ? w.q2 : w.occ == 2 ? w.q1 : w.q0;
+                const int len = lcp16(E, mj >> 2, b.s, S, b.maxcmp);
+                w.occ--;
+                if (len > b.best) {
+                    b.best = len;
+                    b.bpos4 = mj;
+                    if (len >= b.nice) {
+                        w.limit4 = 0x7fffffff;   // walk over: nothing more is queued
+                        w.occ = 0;
+                    }
+                    w.be4 = (len - 1) * 4;
+                    w.scanE = E[b.s + len - 1] >> 16;
+                    ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
+                }
+            }
+        }
+        w.eb = ebn;
+        if (count >= end || __ballot(m4n > w.limit4) == 0) break;
+    }
+}
+
 __device__ inline uint32_t match_rec(int best, int s4, int bpos4) {
     return best >= kMinMatch ? (((uint32_t)best << 16) | (uint32_t)((s4 - bpos4) >> 2)) : 0u;
 }
@@ -669,7 +719,8 @@ __device__ inline uint32_t match_rec(int best, int s4, int bpos4) {
 // decisions taken with ballots).
 __device__ unsigned long long g_dstat[4];   // deferred-walk statistics (variant 41)
 
-template <bool kStats = false, int kHead = kD0>
+template <bool kStats = false, int kHead = kD0, bool kPartial = false, bool kNoFlush = false, bool kRecheck = false,
+          bool kBatchFlush = false>
 __device__ __attribute__((always_inline)) inline void dw_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
                                                               const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
                                                               int want_q, int64_t max_dist) {
@@ -733,7 +784,19 @@ __device__ __attribute__((always_inline)) inline void dw_walk(const uint32_t *E,
         // walk to the next uniform stop: the chain/4 snapshot, the budget, a full queue
         const uint32_t end = count < qc ? qc : chain;
         const uint32_t c0 = count;
-        dw_steps(w, Eb, count, end);
+        int best0 = best;
+        if (kPartial) {
+            DWB b{best, bpos4, s, maxcmp, nice};
+            dw_steps_in(w, b, E, S, count, end);
+            best = b.best;
+            bpos4 = b.bpos4;
+            walking = w.m4 > w.limit4 && count < chain;
+            if (best >= nice) walking = false;
+        } else {
+            dw_steps(w, Eb, count, end);
+            walking = w.m4 > limit4 && count < chain;
+        }
+        const bool partial = false;
         if (kStats) {
             int mo = 0;
 #pragma unroll
@@ -741,33 +804,88 @@ __device__ __attribute__((always_inline)) inline void dw_walk(const uint32_t *E,
             if (__builtin_ctzll(__ballot(1)) == (threadIdx.x & 63)) {
                 atomicAdd(&g_dstat[0], (unsigned long long)(count - c0));  // wave iterations
                 atomicAdd(&g_dstat[1], 1ull);                              // flushes
-                atomicAdd(&g_dstat[2], (unsigned long long)mo);            // flush rounds
+                atomicAdd(&g_dstat[2], (unsigned long long)(partial ? (mo > 0) : mo));   // rounds
             }
         }
-        walking = w.m4 > limit4 && count < chain;
-        // flush, oldest first: entry j (< occ) is the (occ - j)-th oldest
-        const int best0 = best;
+        if (partial) {
+            if (w.occ > 0) {
+                const int mj = w.occ == 4 ? w.q3 : w.occ == 3 ? w.q2 : w.occ == 2 ? w.q1 : w.q0;
+                const int len = lcp16(E, mj >> 2, s, S, maxcmp);
+                w.occ--;
+                if (len > best) {
+                    best = len;
+                    bpos4 = mj;
+                    if (len >= nice) { walking = false; w.occ = 0; }
+                }
+            }
+        } else if (kBatchFlush) {
+            // every entry, oldest first (entry j < occ is the (occ - j)-th
+            // oldest); the first 16 bytes of all kDQ entries are read in one
+            // LDS round trip, entries matching all 16 continue one by one
+            if (__ballot(w.occ > 0) != 0) {
+                const int qm[kDQ] = {w.q0 >> 2, w.q1 >> 2, w.q2 >> 2, w.q3 >> 2};
+                int k16[kDQ];
 #pragma unroll
-        for (int j = kDQ - 1; j >= 0; j--) {
-            if (__ballot(j < w.occ) != 0) {
-                if (j < w.occ) {
-                    const int mj = j == 3 ? w.q3 : j == 2 ? w.q2 : j == 1 ? w.q1 : w.q0;
-                    const int len = lcp16(E, mj >> 2, s, S, maxcmp);
-                    if (len > best) {
+                for (int j = 0; j < kDQ; j++) {
+                    const int m = j < w.occ ? qm[j] : s;   // an empty slot compares the scan with itself
+                    k16[j] = diff16(get4p(E, m) ^ S.s0, get4p(E, m + 4) ^ S.s1, get4p(E, m + 8) ^ S.s2,
+                                    get4p(E, m + 12) ^ S.s3);
+                }
+#pragma unroll
+                for (int j = kDQ - 1; j >= 0; j--) {
+                    int len = k16[j];
+                    if (__ballot(j < w.occ && len >= 16 && maxcmp > 16) != 0) {
+                        if (j < w.occ && len >= 16) {
+                            const int m = qm[j];
+                            while (len < maxcmp) {
+                                const int r = diff16(get4p(E, m + len) ^ get4p(E, s + len),
+                                                     get4p(E, m + len + 4) ^ get4p(E, s + len + 4),
+                                                     get4p(E, m + len + 8) ^ get4p(E, s + len + 8),
+                                                     get4p(E, m + len + 12) ^ get4p(E, s + len + 12));
+                                len += r;
+                                if (r < 16) break;
+                            }
+                        }
+                    }
+                    len = len < maxcmp ? len : maxcmp;
+                    if (j < w.occ && len > best) {
                         best = len;
-                        bpos4 = mj;
+                        bpos4 = qm[j] * 4;
                         if (len >= nice) { walking = false; w.occ = 0; }   // drop the later entries
                     }
                 }
             }
+            w.occ = 0;
+        } else {
+            // every entry, oldest first: entry j (< occ) is the (occ - j)-th oldest
+            uint32_t scanE = w.scanE;                   // scan bytes best-1, best
+#pragma unroll
+            for (int j = kDQ - 1; j >= 0; j--) {
+                const int mj = j == 3 ? w.q3 : j == 2 ? w.q2 : j == 1 ? w.q1 : w.q0;
+                // the entry was queued against an older best: test it again
+                // against the current one (one read) before comparing
+                const bool cand = j < w.occ && (!kRecheck || (E[(mj >> 2) + best - 1] >> 16) == scanE);
+                if (!kNoFlush && __ballot(cand) != 0) {
+                    if (cand) {
+                        const int len = lcp16(E, mj >> 2, s, S, maxcmp);
+                        if (len > best) {
+                            best = len;
+                            bpos4 = mj;
+                            if (len >= nice) { walking = false; w.occ = 0; }   // drop the later entries
+                            if (kRecheck) scanE = E[s + len - 1] >> 16;
+                        }
+                    }
+                }
+            }
+            w.occ = 0;
         }
-        w.occ = 0;
-        if (need_q && (count >= qc || !walking)) {     // deflate.c:1390-1392 (chain >>= 2)
+        const bool fin = !walking && w.occ == 0;
+        if (need_q && (count >= qc || fin)) {          // deflate.c:1390-1392 (chain >>= 2)
             rq[p] = match_rec(best, s4, bpos4);
             need_q = false;
         }
-        if (!walking) break;
-        if (best != best0) {                           // the quick reject now tests the new best
+        if (fin) break;
+        if (best != best0 && walking) {                // the quick reject now tests the new best
             w.be4 = (best - 1) * 4;
             w.scanE = E[s + best - 1] >> 16;
             w.eb = *reinterpret_cast<const uint32_t *>(Eb + (w.m4 > 0 ? w.m4 : 0) + w.be4);
@@ -783,6 +901,14 @@ __device__ unsigned long long g_mstat[4];   // kMatchStats statistics
 //                 C4 sub-batch at L6 (the C4 shard 7.7 -> 9.1 GB/s)
 //   41            40 plus statistics (wave iterations, flushes, flush rounds)
 //   42            40 with three wave-wide head compares (no faster)
+//   43            40 with a full queue's flush inside the step loop, one round
+//                 of each lane's oldest entry (flush rounds -32 %): 432 vs 417 ms
+//   45            timing probe (wrong results): 40 without flush compares:
+//                 270 of 417 ms (the old walk without compares, 37: 226)
+//   46            40 re-testing each queued entry against the current best
+//                 before its compare (one more read): 436 vs 417 ms
+//   47            40 reading the first 16 bytes of all four entries in one
+//                 round trip: 448 vs 419 ms
 //   19            positions of a tile walked in k_count's key order, longest
 //                 walks first: the 64 walks a wave runs side by side have
 //                 similar lengths (SIMT utilisation 63 % -> 90 % at L6,
@@ -805,7 +931,8 @@ __device__ unsigned long long g_mstat[4];   // kMatchStats statistics
 //                 sort and stores: 33 ms of 351 per 4 GiB at L6); 35 half the
 //                 waves walk (1.6x slower at L6, 1.8x at L9: the walks are
 //                 latency-bound at the 16 waves the LDS window allows)
-constexpr int kMatchDefer = 40, kMatchDeferStats = 41, kMatchDefer3 = 42;
+constexpr int kMatchDefer = 40, kMatchDeferStats = 41, kMatchDefer3 = 42, kMatchDeferP = 43, kMatchDeferPStats = 44,
+              kMatchProbeNoFlush = 45, kMatchDeferR = 46, kMatchDeferB = 47;
 constexpr int kMatchWalk = 19;
 constexpr int kMatchDefault = kMatchDefer;
 constexpr int kMatchStats = 21, kMatchProbeNoWalk = 33, kMatchProbeHalf = 35,
@@ -943,6 +1070,17 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
                 dw_walk(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
             } else if (kVariant == kMatchDefer3) {
                 dw_walk<false, 3>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+            } else if (kVariant == kMatchDeferB) {
+                dw_walk<false, kD0, false, false, false, true>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+            } else if (kVariant == kMatchDeferR) {
+                dw_walk<false, kD0, false, false, true>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+            } else if (kVariant == kMatchProbeNoFlush) {
+                dw_walk<false, kD0, false, true>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+            } else if (kVariant == kMatchDeferP) {
+                dw_walk<false, kD0, true>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+            } else if (kVariant == kMatchDeferPStats) {
+                dw_walk<true, kD0, true>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+                if (__builtin_ctzll(__ballot(1)) == (threadIdx.x & 63)) atomicAdd(&g_dstat[3], 1ull);
             } else if (kVariant == kMatchDeferStats) {
                 dw_walk<true>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
                 if (__builtin_ctzll(__ballot(1)) == (threadIdx.x & 63)) atomicAdd(&g_dstat[3], 1ull);   // wave walks
@@ -2480,7 +2618,9 @@ static int match_variant() {
         const char *e = getenv("ZGPU_MATCH_VARIANT");
         const int x = e ? atoi(e) : kMatchDefault;
         return (x == 14 || x == kMatchWalk || x == kMatchStats || x == kMatchProbeNoWalk || x == kMatchProbeHalf ||
-                x == kMatchProbeNoCmp || x == kMatchProbeCmpOnly || x == kMatchDefer || x == kMatchDeferStats || x == kMatchDefer3) ? x : kMatchDefault;
+                x == kMatchProbeNoCmp || x == kMatchProbeCmpOnly || x == kMatchDefer || x == kMatchDeferStats || x == kMatchDefer3 || x == kMatchDeferP ||
+                x == kMatchDeferPStats || x == kMatchProbeNoFlush || x == kMatchDeferR ||
+                x == kMatchDeferB) ? x : kMatchDefault;
     }();
     return v;
 }
@@ -2507,12 +2647,23 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
             hipLaunchKernelGGL(k_match<14>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchWalk) {
             hipLaunchKernelGGL(k_match<kMatchWalk>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchDeferB) {
+            hipLaunchKernelGGL(k_match<kMatchDeferB>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchDeferR) {
+            hipLaunchKernelGGL(k_match<kMatchDeferR>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchProbeNoFlush) {
+            hipLaunchKernelGGL(k_match<kMatchProbeNoFlush>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchDeferP) {
+            hipLaunchKernelGGL(k_match<kMatchDeferP>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchDefer3) {
             hipLaunchKernelGGL(k_match<kMatchDefer3>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchDeferStats) {
+        } else if (v == kMatchDeferStats || v == kMatchDeferPStats) {
             unsigned long long z[4] = {0, 0, 0, 0}, r[4];
             (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dstat), z, sizeof z);
-            hipLaunchKernelGGL(k_match<kMatchDeferStats>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+            if (v == kMatchDeferStats)
+                hipLaunchKernelGGL(k_match<kMatchDeferStats>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+            else
+                hipLaunchKernelGGL(k_match<kMatchDeferPStats>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
             (void)hipStreamSynchronize(st);
             (void)hipMemcpyFromSymbol(r, HIP_SYMBOL(g_dstat), sizeof r);
             fprintf(stderr, "k_match defer stats: wave_iters %llu flushes %llu flush_rounds %llu wave_walks %llu "
