@@ -12,6 +12,7 @@ import pytest
 
 import datagen
 import inflate_cases as ic
+from zhelpers import ZStream
 
 pytestmark = pytest.mark.gpu
 
@@ -205,3 +206,62 @@ def test_inflate_device_api(zg, oracle):
     for i, b in enumerate(bufs):
         assert int(status[i]) == 0 and int(dst_len[i]) == len(b) and int(used[i]) == len(zs[i])
         assert host[doff[i]: doff[i] + len(b)] == b
+
+
+def _stream_inflate(L, z, chunk, outsz, wbits):
+    s = ZStream()
+    assert L.inflateInit2_(C.byref(s), wbits, b"1.3.1.1-motley", C.sizeof(ZStream)) == 0
+    inbuf = C.create_string_buffer(bytes(z), len(z))
+    outbuf = C.create_string_buffer(outsz)
+    got, pos, rc, calls = bytearray(), 0, 0, 0
+    while True:
+        if s.avail_in == 0 and pos < len(z):
+            take = min(chunk, len(z) - pos)
+            s.next_in, s.avail_in = C.addressof(inbuf) + pos, take
+            pos += take
+        s.next_out, s.avail_out = C.addressof(outbuf), outsz
+        rc = L.inflate(C.byref(s), 0)
+        calls += 1
+        got += outbuf.raw[: outsz - s.avail_out]
+        if rc != 0 or (pos == len(z) and s.avail_in == 0 and s.avail_out == outsz):
+            break
+    tin, tout = s.total_in, s.total_out
+    L.inflateEnd(C.byref(s))
+    return rc, bytes(got), tin, tout, calls
+
+
+@pytest.mark.gpu
+def test_inflate_stream_resumes_linear(zg, oracle):
+    """A zpipe-style loop feeding a multi-MiB stream 4 KiB at a time: each call
+    resumes at the last complete block (the window carried), so the ~1500
+    calls cost linear work; output, totals and Z_STREAM_END as zlib's."""
+    L = zg.load()
+    L.inflateInit2_.restype = C.c_int
+    L.inflateInit2_.argtypes = [C.POINTER(ZStream), C.c_int, C.c_char_p, C.c_int]
+    L.inflate.restype = C.c_int
+    L.inflate.argtypes = [C.POINTER(ZStream), C.c_int]
+    L.inflateEnd.argtypes = [C.POINTER(ZStream)]
+    data = datagen.make("mix", 6 << 20, 11)
+    for level, wrap, wbits in ((6, 1, 15), (1, 2, 31), (9, 0, -15), (0, 1, 15)):
+        z = oracle.compress(data, level, wrap=wrap)[1]
+        rc, got, tin, tout, calls = _stream_inflate(L, z + b"tail", 4096, 65536, wbits)
+        assert rc == 1 and got == data, (level, wrap, rc, len(got))
+        assert tin == len(z) and tout == len(data) and calls > len(z) // 4096
+
+
+@pytest.mark.gpu
+def test_inflate_stream_resume_bad_trailer(zg, oracle):
+    """Streaming, resumed decode: a damaged Adler-32 / CRC-32 / ISIZE trailer
+    is Z_DATA_ERROR after all the data, as inflate.c:1183-1221."""
+    L = zg.load()
+    L.inflateInit2_.restype = C.c_int
+    L.inflateInit2_.argtypes = [C.POINTER(ZStream), C.c_int, C.c_char_p, C.c_int]
+    L.inflate.restype = C.c_int
+    L.inflate.argtypes = [C.POINTER(ZStream), C.c_int]
+    L.inflateEnd.argtypes = [C.POINTER(ZStream)]
+    data = datagen.make("text", 1 << 20, 5)
+    for wrap, wbits, k in ((1, 15, -1), (2, 31, -5), (2, 31, -1)):
+        z = bytearray(oracle.compress(data, 6, wrap=wrap)[1])
+        z[k] ^= 0x01
+        rc, got, _, _, _ = _stream_inflate(L, z, 8192, 1 << 20, wbits)
+        assert rc == -3 and got == data, (wrap, k, rc)

@@ -765,10 +765,16 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
 // match records (a match writes >= 3 bytes, the last one may be cut short).
 // stop_out (device, optional): InflateStop per stream.
 // ------------------------------------------------------------------------
+struct InflateResumeDev {          // InflateJob's resume arrays (device, per stream)
+    const uint64_t *res_bit;
+    const uint32_t *res_hist;
+    uint64_t *blk_out;
+};
+
 int inflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
                        uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap, uint64_t *dst_len,
                        uint64_t *src_used, int32_t *status, uint32_t *stop_out, uint32_t count, int wrap,
-                       int wbits, hipStream_t st) {
+                       int wbits, hipStream_t st, const InflateResumeDev *rs = nullptr) {
     if (wrap < 0 || wrap > 3) return ZGPU_STREAM_ERROR;
     if (count == 0) return ZGPU_OK;
     std::vector<uint64_t> lens(count), caps(count);
@@ -820,6 +826,11 @@ int inflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         job.adler = c.ws_ick.as<uint32_t>();
         job.crc = job.adler + max_cnt;
         job.crc_byte = device_crc_tables()->byte;
+        if (rs) {
+            job.res_bit = rs->res_bit;
+            job.res_hist = rs->res_hist;
+            job.blk_out = rs->blk_out;
+        }
         if (T.run(3, st, [&] { return launch_inflate_stage(0, job, st); })) return ZGPU_MEM_ERROR;
         if (T.run(4, st, [&] { return launch_inflate_stage(1, job, st); })) return ZGPU_MEM_ERROR;
         if ((wrap & 1) && T.run(0, st, [&] {
@@ -889,6 +900,62 @@ int uncompress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_
         if (status) status[i] = os[i];
         if (stop) stop[i] = (int)ostop[i];
     }
+    return ZGPU_OK;
+}
+
+// One attempt of the streaming inflate(): the stream's input `in` (n bytes)
+// decoded from its start (resume == false: header, blocks, trailer) or, raw,
+// from the block header at bit start_bit with the window `hist` already in
+// front of the output.  out receives hist + the new output (at most cap bytes
+// in all); t the stop reason, the bytes used and the last block boundary.
+struct InflateTry {
+    uint32_t stop;
+    int status;
+    uint64_t put, used, blk_bit, blk_put;
+};
+
+int inflate_try_locked(Ctx &c, const uint8_t *in, size_t n, bool resume, uint64_t start_bit, const uint8_t *hist,
+                       size_t hist_len, size_t cap, int wrap, int wbits, std::vector<uint8_t> &out, InflateTry &t) {
+    if (!c.ws_io.ensure(n + 64) || !c.ws_io2.ensure(cap + 64) || !c.ws_small.ensure(8 * 16 + 64) ||
+        !c.ws_istop.ensure(64))
+        return ZGPU_MEM_ERROR;
+    uint8_t *d_in = c.ws_io.as<uint8_t>(), *d_out = c.ws_io2.as<uint8_t>();
+    uint64_t *m = c.ws_small.as<uint64_t>();          // so sl do dc dl used | st | rbit hist | blk[2]
+    int32_t *d_st = reinterpret_cast<int32_t *>(m + 6);
+    uint64_t *d_rbit = m + 7;
+    uint32_t *d_hist = reinterpret_cast<uint32_t *>(m + 8);
+    uint64_t *d_blk = m + 9;
+    uint32_t *d_stop = c.ws_istop.as<uint32_t>();
+    hipStream_t st = c.own;
+    const uint64_t meta[4] = {0, (uint64_t)n, 0, (uint64_t)cap};
+    const uint64_t rbit = start_bit;
+    const uint32_t hl = (uint32_t)hist_len;
+    if ((n && hipMemcpyAsync(d_in, in, n, hipMemcpyHostToDevice, st) != hipSuccess) ||
+        (hist_len && hipMemcpyAsync(d_out, hist, hist_len, hipMemcpyHostToDevice, st) != hipSuccess) ||
+        hipMemcpyAsync(m, meta, sizeof meta, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_rbit, &rbit, 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_hist, &hl, 4, hipMemcpyHostToDevice, st) != hipSuccess)
+        return ZGPU_MEM_ERROR;
+    const InflateResumeDev rs{resume ? d_rbit : nullptr, resume ? d_hist : nullptr, d_blk};
+    int rc = inflate_dev_locked(c, d_in, m, m + 1, d_out, m + 2, m + 3, m + 4, m + 5, d_st, d_stop, 1,
+                                resume ? 0 : wrap, wbits, st, &rs);
+    if (rc) return rc;
+    uint64_t res[2], blk[2];
+    int32_t status = 0;
+    uint32_t stop = 0;
+    if (copy_sync(res, m + 4, 16, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        copy_sync(blk, d_blk, 16, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        copy_sync(&status, d_st, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        copy_sync(&stop, d_stop, 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+        return ZGPU_MEM_ERROR;
+    out.resize(res[0]);
+    if (res[0] && copy_sync(out.data(), d_out, res[0], hipMemcpyDeviceToHost, st) != hipSuccess) return ZGPU_MEM_ERROR;
+    t.stop = stop;
+    t.status = status;
+    t.put = res[0];
+    t.used = res[1];
+    t.blk_bit = blk[0];
+    t.blk_put = blk[1];
     return ZGPU_OK;
 }
 
@@ -1297,9 +1364,20 @@ struct internal_state {
     int inflating = 0;
     int wbits = 15;         // deflate: w_bits (9..15); inflate: inflateInit2_'s windowBits
     int mem_level = 8;      // deflate: memLevel (hash_bits = memLevel + 7)
-    size_t tried = 0;       // gathered input at the last decode attempt that ran out of input
-    size_t cap = 0;         // output capacity of the next attempt
+    size_t tried = 0;       // input end (absolute) at the last decode attempt that ran out of input
+    size_t cap = 0;         // output capacity of the next attempt (beyond the window)
     int result = Z_OK;      // once decoded: Z_STREAM_END, Z_DATA_ERROR or Z_NEED_DICT
+    // inflate resume point: once a block of the stream is complete, every later
+    // attempt decodes raw from the last block boundary (res_bit, absolute
+    // input bit; res_put, absolute output byte) with the 32 KiB of output
+    // before it (hist) as the window, so a stream fed in pieces costs linear
+    // work.  in_base: absolute input offset of in[0]; ideliv: output bytes
+    // handed out; out holds the decoded bytes not handed out yet.
+    int imode = 0;          // 0: decode from the stream start, 1: resume
+    int igz = 0;            // the stream has a gzip header (CRC-32 + ISIZE trailer)
+    uint64_t res_bit = 0, res_put = 0, ideliv = 0;
+    uint32_t icheck = 0;    // Adler-32 / CRC-32 of the output before res_put
+    std::vector<uint8_t> hist;
 };
 
 int deflateInit2_(z_streamp strm, int level, int method, int windowBits, int memLevel, int strategy,
@@ -1794,13 +1872,151 @@ int inflateInit_(z_streamp strm, const char *version, int stream_size) {
 int inflateReset(z_streamp strm) {
     if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
-    s->in.clear(); s->out.clear();
+    s->in.clear(); s->out.clear(); s->hist.clear();
     s->out_pos = 0; s->finished = 0; s->tried = 0; s->cap = 0; s->result = Z_OK;
+    s->in_base = 0; s->imode = 0; s->igz = 0; s->res_bit = s->res_put = s->ideliv = 0; s->icheck = 0;
     strm->total_in = strm->total_out = 0;
     strm->msg = nullptr;
     strm->adler = s->wrap & 1;
     return Z_OK;
 }
+
+namespace {
+// One decode attempt of the streaming inflate() over the input gathered so
+// far: from the stream start until a block is complete, then from the last
+// block boundary.  Sets s->out (bytes not handed out yet), s->finished and
+// s->result; `took` input bytes of this call may be handed back past the end.
+int inflate_attempt(z_streamp strm, internal_state *s, size_t took) {
+    const uint64_t in_end = s->in_base + s->in.size();
+    if (s->cap == 0) s->cap = std::max<size_t>(4 * s->in.size(), 1 << 16);
+    const bool is_check = s->wrap != 0;
+    auto check_of = [&](uint32_t init, const uint8_t *p, size_t n) -> uint32_t {
+        return s->igz ? (uint32_t)crc32_z(init, p, n) : (uint32_t)adler32_z(init, p, n);
+    };
+    for (;;) {
+        const bool resume = s->imode == 1;
+        const size_t hl = resume ? s->hist.size() : 0;
+        std::vector<uint8_t> o;
+        InflateTry t{};
+        int rc;
+        {
+            Lease L;
+            rc = L.rc;
+            if (!rc) rc = inflate_try_locked(*L.c, s->in.data(), s->in.size(), resume,
+                                             resume ? s->res_bit - 8ull * s->in_base : 0, s->hist.data(), hl,
+                                             hl + s->cap, s->wrap, s->wbits, o, t);
+        }
+        if (rc) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : rc;
+        if (t.stop == kIFull) {                                  // grow the output and decode again
+            if (s->cap >= (size_t(1) << 31)) return Z_MEM_ERROR;
+            s->cap *= 2;
+            continue;
+        }
+        const uint64_t obase = resume ? s->res_put - hl : 0;     // absolute output byte of o[0]
+        auto append_new = [&](uint64_t upto) {                   // decoded bytes beyond those kept
+            const uint64_t have = s->ideliv + (s->out.size() - s->out_pos);
+            if (s->out_pos) {
+                s->out.erase(s->out.begin(), s->out.begin() + (std::ptrdiff_t)s->out_pos);
+                s->out_pos = 0;
+            }
+            if (upto > have) s->out.insert(s->out.end(), o.begin() + (std::ptrdiff_t)(have - obase),
+                                           o.begin() + (std::ptrdiff_t)(upto - obase));
+        };
+        const uint64_t put_abs = obase + t.put;
+        if (!resume && t.stop != kIInEnd) {                      // the whole stream in one attempt
+            append_new(put_abs);
+            s->finished = 1;
+            if (t.stop == kIEnd) {
+                s->result = Z_STREAM_END;
+                const size_t extra = in_end - t.used;            // give back input past the stream end
+                const size_t back = std::min<size_t>(extra, took);
+                strm->next_in -= back;
+                strm->avail_in += (uInt)back;
+                strm->total_in = t.used;
+                if (s->wrap) strm->adler = s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b
+                                               ? crc32_z(0, o.data(), o.size())
+                                               : adler32_z(1, o.data(), o.size());
+            } else if (t.stop == kIDict) {
+                s->result = Z_NEED_DICT;
+                strm->adler = ((uLong)s->in[2] << 24) | ((uLong)s->in[3] << 16) | ((uLong)s->in[4] << 8) | s->in[5];
+            } else {
+                s->result = Z_DATA_ERROR;
+                strm->msg = const_cast<char *>("invalid or corrupt deflate stream");
+            }
+            s->in.clear();
+            s->in.shrink_to_fit();
+            return Z_OK;
+        }
+        if (resume && t.stop == kIData) {
+            append_new(put_abs);
+            s->finished = 1;
+            s->result = Z_DATA_ERROR;
+            strm->msg = const_cast<char *>("invalid or corrupt deflate stream");
+            s->in.clear();
+            s->in.shrink_to_fit();
+            return Z_OK;
+        }
+        if (resume && t.stop == kIEnd) {                         // the final block: check the trailer
+            const uint64_t tpos = s->in_base + t.used;
+            const uint64_t need = !s->wrap ? 0 : s->igz ? 8 : 4;
+            if (in_end >= tpos + need) {
+                append_new(put_abs);
+                s->finished = 1;
+                s->result = Z_STREAM_END;
+                uint32_t ck = s->icheck;
+                if (is_check) ck = check_of(ck, o.data() + (s->res_put - obase), (size_t)(put_abs - s->res_put));
+                const uint8_t *tr = s->in.data() + (tpos - s->in_base);
+                bool ok = true;
+                if (s->wrap && !s->igz) {
+                    ok = ((uint32_t)tr[0] << 24 | (uint32_t)tr[1] << 16 | (uint32_t)tr[2] << 8 | tr[3]) == ck;
+                    if (!ok) strm->msg = const_cast<char *>("incorrect data check");
+                } else if (s->igz) {
+                    const uint32_t c = tr[0] | (uint32_t)tr[1] << 8 | (uint32_t)tr[2] << 16 | (uint32_t)tr[3] << 24;
+                    const uint32_t z = tr[4] | (uint32_t)tr[5] << 8 | (uint32_t)tr[6] << 16 | (uint32_t)tr[7] << 24;
+                    ok = c == ck && z == (uint32_t)put_abs;
+                    if (!ok) strm->msg = const_cast<char *>(c != ck ? "incorrect data check" : "incorrect length check");
+                }
+                if (ok) {
+                    const uint64_t used = tpos + need;
+                    const size_t back = std::min<size_t>(in_end - used, took);
+                    strm->next_in -= back;
+                    strm->avail_in += (uInt)back;
+                    strm->total_in = used;
+                    if (s->wrap) strm->adler = ck;
+                } else {
+                    s->result = Z_DATA_ERROR;
+                }
+                s->in.clear();
+                s->in.shrink_to_fit();
+                return Z_OK;
+            }
+            // the trailer is not all here: wait at the last block boundary
+        }
+        // the stream goes on: hand out its prefix, move the resume point
+        append_new(put_abs);
+        s->tried = in_end;
+        uint64_t bb = t.blk_bit, bp = t.blk_put;
+        if (resume) { bb += 8ull * s->in_base; bp += obase; }
+        if (bb && bb > s->res_bit) {
+            if (!resume) {
+                s->igz = (s->wrap & 2) && s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b;
+                s->icheck = s->igz ? 0u : 1u;
+            }
+            if (is_check) s->icheck = check_of(s->icheck, o.data() + (s->res_put - obase), (size_t)(bp - s->res_put));
+            const uint64_t h0 = bp > 32768 ? bp - 32768 : 0;      // the window before the new point
+            std::vector<uint8_t> h(o.begin() + (std::ptrdiff_t)(h0 - obase), o.begin() + (std::ptrdiff_t)(bp - obase));
+            s->hist.swap(h);
+            s->res_bit = bb;
+            s->res_put = bp;
+            s->imode = 1;
+            const uint64_t drop = (bb >> 3) - s->in_base;        // input before the boundary's byte
+            s->in.erase(s->in.begin(), s->in.begin() + (std::ptrdiff_t)drop);
+            s->in_base += drop;
+        }
+        return Z_OK;
+    }
+}
+}  // namespace
 
 int inflate(z_streamp strm, int flush) {
     if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
@@ -1816,62 +2032,17 @@ int inflate(z_streamp strm, int flush) {
     }
     // Decode what has arrived whenever input arrives: a stream that is still
     // open (a sync-flushed connection, a file read in pieces) hands out every
-    // byte its input decodes to so far, as inflate() does (inflate.c:622-1221);
-    // each attempt decodes the stream from its start and gives out what is new.
-    if (!s->finished && (took || (flush == Z_FINISH && s->tried != s->in.size()))) {
-        if (s->cap == 0) s->cap = std::max<size_t>(4 * s->in.size(), 1 << 16);
-        for (;;) {
-            s->out.resize(s->cap);
-            const uint8_t *sp = s->in.data();
-            uint8_t *dp = s->out.data();
-            size_t sl = s->in.size(), dl = s->cap, used = 0;
-            int st = 0, stop = 0;
-            int rc;
-            {
-                Lease L;
-                rc = L.rc;
-                if (!rc) rc = uncompress_host_locked(*L.c, &sp, &sl, &dp, &dl, &used, &st, &stop, 1, s->wrap, s->wbits);
-            }
-            if (rc) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : rc;
-            if (stop == kIFull) {                                     // grow the output and decode again
-                if (s->cap >= (size_t(1) << 31)) return Z_MEM_ERROR;
-                s->cap *= 2;
-                continue;
-            }
-            if (stop == kIInEnd) {                                    // the stream goes on: its prefix so far
-                s->tried = s->in.size();
-                s->out.resize(dl);
-                break;
-            }
-            s->out.resize(dl);
-            s->finished = 1;
-            if (stop == kIEnd) {
-                s->result = Z_STREAM_END;
-                const size_t extra = s->in.size() - used;             // give back input past the stream end
-                const size_t back = std::min(extra, took);
-                strm->next_in -= back;
-                strm->avail_in += (uInt)back;
-                strm->total_in = used;
-                if (s->wrap) strm->adler = s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b
-                                               ? crc32_z(0, s->out.data(), s->out.size())
-                                               : adler32_z(1, s->out.data(), s->out.size());
-            } else if (stop == kIDict) {
-                s->result = Z_NEED_DICT;
-                strm->adler = ((uLong)s->in[2] << 24) | ((uLong)s->in[3] << 16) | ((uLong)s->in[4] << 8) | s->in[5];
-            } else {
-                s->result = Z_DATA_ERROR;
-                strm->msg = const_cast<char *>("invalid or corrupt deflate stream");
-            }
-            s->in.clear();
-            s->in.shrink_to_fit();
-            break;
-        }
-    }
+    // byte its input decodes to so far, as inflate() does (inflate.c:622-1221).
+    // Each attempt resumes at the last complete block (inflate_attempt).
+    const uint64_t in_end = s->in_base + s->in.size();
+    if (!s->finished && (took || (flush == Z_FINISH && s->tried != in_end)))
+        if (int rc = inflate_attempt(strm, s, took)) return rc;
     size_t give = 0;
     if (s->out_pos < s->out.size() || s->finished) {
         give = std::min<size_t>(strm->avail_out, s->out.size() - s->out_pos);
         std::memcpy(strm->next_out, s->out.data() + s->out_pos, give);
         s->out_pos += give;
+        s->ideliv += give;
         strm->next_out += give;
         strm->avail_out -= (uInt)give;
         strm->total_out += give;

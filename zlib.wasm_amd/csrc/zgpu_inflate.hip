@@ -223,13 +223,23 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
 
     Rd r;
     r.hold = 0; r.bits = 0; r.ipos = 0; r.rbase = 0;
-    ring_stage(S, r, in, n, 0, lane);
+    const uint64_t rb = job.res_bit ? job.res_bit[g] : 0;       // resume: the block header's bit
+    ring_stage(S, r, in, n, (uint32_t)(rb >> 3) & ~3u, lane);
 
-    uint32_t put = 0, ob = 0, nm = 0, pbyte = 0;
+    uint32_t put = job.res_hist ? job.res_hist[g] : 0, ob = put, nm = 0, pbyte = 0;
     uint32_t stop = kIEnd;
     uint64_t used = 0, used_bad = 0;
     uint32_t chk_kind = 0, chk_want = 0, isize = 0;
     bool gz = false;
+    uint64_t blk_bit = 0;                            // the last block boundary reached
+    uint32_t blk_put = 0;
+    if (job.res_bit) {
+        seek(r, (uint32_t)(rb >> 3));
+        refill(S, r, in, n, lane);
+        dropb(r, (uint32_t)(rb & 7));
+        blk_bit = rb;
+        blk_put = put;
+    }
 
     auto ceil_used = [&]() -> uint64_t { return (bitpos(r) + 7) >> 3; };
     auto flush_obuf = [&](uint32_t upto) {          // output bytes [ob, upto), upto <= ob + kOBuf
@@ -245,7 +255,7 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
     };
 
     // ---------------- HEAD (inflate.c:622-669) / gzip header (:629-807) ----------------
-    if (wrap) {
+    if (wrap && !job.res_bit) {
         refill(S, r, in, n, lane);
         if (bitpos(r) + 16 > inbits) { stop = kIInEnd; used = n; goto done; }
         const uint32_t h16 = (uint32_t)r.hold & 0xffffu;
@@ -449,6 +459,8 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
             }
         }
         if (last) break;
+        blk_bit = bitpos(r);                         // a block boundary: resumable here
+        blk_put = put;
     }
 
     // ---------------- CHECK, LENGTH (inflate.c:1183-1221) ----------------
@@ -498,6 +510,10 @@ done:
         rc.pbyte = pbyte;
         job.rec[bi] = rc;
         job.dst_len[g] = probe ? 0 : put;            // the checksum kernels read this
+        if (job.blk_out) {
+            job.blk_out[2 * (uint64_t)g] = blk_bit;
+            job.blk_out[2 * (uint64_t)g + 1] = blk_put;
+        }
     }
 }
 

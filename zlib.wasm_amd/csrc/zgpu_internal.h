@@ -196,6 +196,15 @@ struct InflateJob {
     InflateRec *rec;         // [count]
     uint32_t *adler, *crc;   // [count] checks of the produced output
     const uint32_t *crc_byte;   // CRC-32 byte table (device)
+    // resuming a stream at a block boundary (the streaming inflate()), all
+    // optional: res_bit[g] = bit position of a block header in the stream's
+    // input (the job is then raw: no header, no trailer); res_hist[g] = bytes
+    // of earlier output already at dst (<= 32 KiB, the window), decoding
+    // appends after them; blk_out[2g], [2g+1] = bit position and output
+    // position of the last block boundary the decode reached (0, 0: none)
+    const uint64_t *res_bit;
+    const uint32_t *res_hist;
+    uint64_t *blk_out;
 };
 int launch_inflate_stage(int stage, const InflateJob &job, hipStream_t st);
 
