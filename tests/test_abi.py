@@ -146,3 +146,57 @@ def test_deflateinit2_params_and_bound_vs_reference_golden(lib):
                                  b"1.3.1.1-motley", C.sizeof(ZStream)) == 0
         assert lib.deflateBound(C.byref(s), e["n"]) == e["bound"], e
         lib.deflateEnd(C.byref(s))
+
+
+def test_zalloc_zfree_honoured(lib):
+    """deflateInit2_ / inflateInit2_ allocate the stream state through the
+    caller's zalloc and give it back through zfree (deflate.c:393-406,
+    inflate.c:208-221); a zalloc that fails is Z_MEM_ERROR; with none given the
+    defaults are stored in the stream (zutil.c:286-294).  No GPU work."""
+    from zhelpers import ZStream
+    ALLOC = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_uint, C.c_uint)
+    FREE = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p)
+    libc = C.CDLL(None)
+    libc.calloc.restype = C.c_void_p
+    libc.calloc.argtypes = [C.c_size_t, C.c_size_t]
+    libc.free.argtypes = [C.c_void_p]
+    live, calls = {}, []
+
+    def za(opaque, items, size):
+        calls.append(("a", opaque, items * size))
+        p = libc.calloc(items, size)
+        live[p] = items * size
+        return p
+
+    def zf(opaque, p):
+        calls.append(("f", opaque, p))
+        del live[p]
+        libc.free(p)
+
+    za_c, zf_c = ALLOC(za), FREE(zf)
+    null_c = ALLOC(lambda o, i, s: None)
+    lib.deflateInit2_.restype = C.c_int
+    lib.deflateInit2_.argtypes = [C.POINTER(ZStream), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                  C.c_char_p, C.c_int]
+    lib.deflateEnd.argtypes = [C.POINTER(ZStream)]
+    lib.inflateInit2_.restype = C.c_int
+    lib.inflateInit2_.argtypes = [C.POINTER(ZStream), C.c_int, C.c_char_p, C.c_int]
+    lib.inflateEnd.argtypes = [C.POINTER(ZStream)]
+    for init, end in ((lambda s: lib.deflateInit2_(C.byref(s), 6, 8, 15, 8, 0, b"1.3.1.1-motley", C.sizeof(ZStream)),
+                       lib.deflateEnd),
+                      (lambda s: lib.inflateInit2_(C.byref(s), 15, b"1.3.1.1-motley", C.sizeof(ZStream)),
+                       lib.inflateEnd)):
+        s = ZStream()
+        s.zalloc = C.cast(za_c, C.c_void_p).value
+        s.zfree = C.cast(zf_c, C.c_void_p).value
+        s.opaque = 1234
+        calls.clear()
+        assert init(s) == 0 and s.state in live and calls and calls[0][1] == 1234
+        assert end(C.byref(s)) == 0 and not live and calls[-1][0] == "f"
+        s = ZStream()
+        s.zalloc = C.cast(null_c, C.c_void_p).value
+        s.zfree = C.cast(zf_c, C.c_void_p).value
+        assert init(s) == -4 and not s.state            # Z_MEM_ERROR
+        s = ZStream()
+        assert init(s) == 0 and s.zalloc and s.zfree    # the defaults are stored
+        assert end(C.byref(s)) == 0

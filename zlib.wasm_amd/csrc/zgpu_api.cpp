@@ -1263,7 +1263,7 @@ const char *zlibVersion(void) { return ZGPU_ZLIB_VERSION; }
 
 uLong compressBound(uLong sourceLen) { return (uLong)compress_bound64(sourceLen); }
 
-int compress2(Bytef *dest, uLongf *destLen, const Bytef *source, uLong sourceLen, int level) {
+static int compress2_body(Bytef *dest, uLongf *destLen, const Bytef *source, uLong sourceLen, int level) {
     if (!destLen) return Z_STREAM_ERROR;
     if (level != Z_DEFAULT_COMPRESSION && (level < 0 || level > 9)) { *destLen = 0; return Z_STREAM_ERROR; }
     if (!dest || (sourceLen && !source)) { *destLen = 0; return Z_STREAM_ERROR; }
@@ -1326,11 +1326,49 @@ uLong adler32_combine64(uLong adler1, uLong adler2, int64_t len2) {
 }
 uLong adler32_combine(uLong adler1, uLong adler2, long len2) { return adler32_combine64(adler1, adler2, len2); }
 
+// The stream state and its buffers are allocated through the caller's
+// zalloc / zfree, as deflateInit2_ / inflateInit2_ do (deflate.c:393-406,
+// zutil.c:286-294): ZAlloc is a std allocator over them (malloc / free when
+// the stream gives none).  An allocation that fails throws std::bad_alloc,
+// which every entry point turns into Z_MEM_ERROR.
+extern "C++" {
+template <class T> struct ZAlloc {
+    using value_type = T;
+    alloc_func za = nullptr;
+    free_func zf = nullptr;
+    voidpf op = nullptr;
+    ZAlloc() = default;
+    ZAlloc(alloc_func a, free_func f, voidpf o) : za(a), zf(f), op(o) {}
+    template <class U> ZAlloc(const ZAlloc<U> &o) : za(o.za), zf(o.zf), op(o.op) {}
+    T *allocate(size_t n) {
+        if (n == 0) n = 1;
+        if (n > 0xffffffffull / sizeof(T)) throw std::bad_alloc();
+        void *p = za ? za(op, (uInt)n, (uInt)sizeof(T)) : std::malloc(n * sizeof(T));
+        if (!p) throw std::bad_alloc();
+        return static_cast<T *>(p);
+    }
+    void deallocate(T *p, size_t) {
+        if (zf) zf(op, p);
+        else std::free(p);
+    }
+    template <class U> bool operator==(const ZAlloc<U> &o) const { return za == o.za && zf == o.zf && op == o.op; }
+    template <class U> bool operator!=(const ZAlloc<U> &o) const { return !(*this == o); }
+};
+template <class T> using zvec = std::vector<T, ZAlloc<T>>;
+}  // extern "C++"
+
+// the defaults deflateInit2_ / inflateInit2_ store in the stream (zutil.c:286-294)
+voidpf zgpu_zcalloc(voidpf, uInt items, uInt size) { return std::calloc(items, size); }
+void zgpu_zcfree(voidpf, voidpf ptr) { std::free(ptr); }
+
 // z_stream deflate: gather input, compress on the GPU at a flush call or at
 // Z_FINISH, drain.
 struct internal_state {
+    ZAlloc<uint8_t> al;
+    explicit internal_state(const ZAlloc<uint8_t> &a = {})
+        : al(a), in(a), out(a), ev_pos(a), ev_type(a), fast_head(a), fast_prev(a), hist(a) {}
     int level, wrap, strategy;
-    std::vector<uint8_t> in, out;   // deflate: the input since the last Z_FULL_FLUSH; output queue
+    zvec<uint8_t> in, out;          // deflate: the input since the last Z_FULL_FLUSH; output queue
     size_t out_pos;
     int finished;     // 0 gathering, 1 compressed / decoded
     // deflate(flush) calls (Z_PARTIAL_FLUSH, Z_SYNC_FLUSH, Z_FULL_FLUSH, Z_BLOCK):
@@ -1340,8 +1378,8 @@ struct internal_state {
     int last_flush = -2;            // deflate.c: s->last_flush (deflateReset)
     bool flushed = false;           // a flush call was acted on
     bool header_done = false;
-    std::vector<uint64_t> ev_pos;   // the current part's flush calls (part-relative)
-    std::vector<uint32_t> ev_type;
+    zvec<uint64_t> ev_pos;          // the current part's flush calls (part-relative)
+    zvec<uint32_t> ev_type;
     size_t part_out = 0;            // bytes of the current part already queued
     bool marker_due = false;        // the last flush call ran out of output before its marker
     size_t in_base = 0;             // part position of in[0] (input behind the resume point is dropped)
@@ -1358,8 +1396,10 @@ struct internal_state {
     uint32_t res_byte = 0;
     // levels 1..3: k_parse_fast's hash chains at the resume point (head[] as
     // part positions, prev links of [res_S, res_pos)) and as the last job left them
-    std::vector<uint32_t> fast_head, job_head;
-    std::vector<uint16_t> fast_prev, job_prev;
+    zvec<uint32_t> fast_head;
+    zvec<uint16_t> fast_prev;
+    std::vector<uint32_t> job_head;   // what the last job left (scratch of one call)
+    std::vector<uint16_t> job_prev;
     // inflate streams
     int inflating = 0;
     int wbits = 15;         // deflate: w_bits (9..15); inflate: inflateInit2_'s windowBits
@@ -1377,8 +1417,29 @@ struct internal_state {
     int igz = 0;            // the stream has a gzip header (CRC-32 + ISIZE trailer)
     uint64_t res_bit = 0, res_put = 0, ideliv = 0;
     uint32_t icheck = 0;    // Adler-32 / CRC-32 of the output before res_put
-    std::vector<uint8_t> hist;
+    zvec<uint8_t> hist;
 };
+
+namespace {
+// a state in the stream's memory (ZALLOC, deflate.c:406); nullptr when it fails
+internal_state *new_state(z_streamp strm, const internal_state *copy = nullptr) {
+    if (!strm->zalloc) { strm->zalloc = zgpu_zcalloc; strm->opaque = nullptr; }   // deflate.c:393-401
+    if (!strm->zfree) strm->zfree = zgpu_zcfree;
+    void *mem = strm->zalloc(strm->opaque, 1, (uInt)sizeof(internal_state));
+    if (!mem) return nullptr;
+    try {
+        return copy ? new (mem) internal_state(*copy)
+                    : new (mem) internal_state(ZAlloc<uint8_t>(strm->zalloc, strm->zfree, strm->opaque));
+    } catch (const std::bad_alloc &) {
+        strm->zfree(strm->opaque, mem);
+        return nullptr;
+    }
+}
+void free_state(z_streamp strm, internal_state *s) {
+    s->~internal_state();
+    strm->zfree(strm->opaque, s);
+}
+}  // namespace
 
 int deflateInit2_(z_streamp strm, int level, int method, int windowBits, int memLevel, int strategy,
                   const char *version, int stream_size) {
@@ -1391,7 +1452,7 @@ int deflateInit2_(z_streamp strm, int level, int method, int windowBits, int mem
     if (parse_window(windowBits, memLevel, &wrap, &wbits) || method != Z_DEFLATED || strategy < 0 ||
         strategy > Z_FIXED || level < 0 || level > 9)
         return Z_STREAM_ERROR;                          // deflate.c:400-425
-    internal_state *s = new (std::nothrow) internal_state();
+    internal_state *s = new_state(strm);
     if (!s) return Z_MEM_ERROR;
     s->level = level;
     s->wrap = wrap;
@@ -1643,7 +1704,8 @@ int emit_flush(z_streamp strm, internal_state *s, int flush) {
             const uint32_t base = (uint32_t)s->res_S;
             s->fast_head.resize(s->job_head.size());
             for (size_t i = 0; i < s->job_head.size(); i++) s->fast_head[i] = s->job_head[i] ? s->job_head[i] + base : 0;
-            s->fast_prev.swap(s->job_prev);
+            s->fast_prev.assign(s->job_prev.begin(), s->job_prev.end());
+            s->job_prev.clear();
             s->job_head.clear();
         }
         s->res_S += (size_t)o[2];
@@ -1662,7 +1724,7 @@ int emit_flush(z_streamp strm, internal_state *s, int flush) {
 }
 }  // namespace
 
-int deflate(z_streamp strm, int flush) {
+static int deflate_body(z_streamp strm, int flush) {
     if (!strm || !strm->state || strm->state->inflating || flush < 0 || flush > Z_BLOCK) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
     if (!strm->next_out || (strm->avail_in && !strm->next_in) || (s->finished && flush != Z_FINISH))
@@ -1760,7 +1822,7 @@ int deflateReset(z_streamp strm) {                              // deflate.c:560
     if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
     const int level = s->level, wrap = s->wrap, strategy = s->strategy, wbits = s->wbits, mem = s->mem_level;
-    *s = internal_state();
+    *s = internal_state(s->al);
     s->level = level;
     s->wrap = wrap;
     s->strategy = strategy;
@@ -1778,9 +1840,9 @@ int deflateReset(z_streamp strm) {                              // deflate.c:560
 
 int deflateCopy(z_streamp dest, z_streamp source) {             // deflate.c:1270-1311
     if (!dest || !source || !source->state || source->state->inflating) return Z_STREAM_ERROR;
-    internal_state *s = new (std::nothrow) internal_state(*source->state);
-    if (!s) return Z_MEM_ERROR;
     *dest = *source;
+    internal_state *s = new_state(dest, source->state);
+    if (!s) return Z_MEM_ERROR;
     dest->state = s;
     return Z_OK;
 }
@@ -1798,7 +1860,7 @@ int deflatePending(z_streamp strm, unsigned *pending, int *bits) {
 
 int deflateEnd(z_streamp strm) {
     if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
-    delete strm->state;
+    free_state(strm, strm->state);
     strm->state = nullptr;
     return Z_OK;
 }
@@ -1817,7 +1879,7 @@ uLong deflateBound(z_streamp strm, uLong sourceLen) {          // deflate.c:842-
 
 // ------------------------------- inflate -------------------------------
 
-int uncompress2(Bytef *dest, uLongf *destLen, const Bytef *source, uLong *sourceLen) {   // uncompr.c:24-80
+static int uncompress2_body(Bytef *dest, uLongf *destLen, const Bytef *source, uLong *sourceLen) {
     if (!destLen || !sourceLen || (*sourceLen && !source) || (*destLen && !dest)) return Z_STREAM_ERROR;
     const uint8_t *s = source;
     uint8_t *d = dest;
@@ -1851,7 +1913,7 @@ int inflateInit2_(z_streamp strm, int windowBits, const char *version, int strea
         if (windowBits < 48) windowBits &= 15;
     }
     if (windowBits && (windowBits < 8 || windowBits > 15)) return Z_STREAM_ERROR;
-    internal_state *s = new (std::nothrow) internal_state();
+    internal_state *s = new_state(strm);
     if (!s) return Z_MEM_ERROR;
     s->inflating = 1;
     s->wrap = wrap;
@@ -2004,8 +2066,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took) {
             }
             if (is_check) s->icheck = check_of(s->icheck, o.data() + (s->res_put - obase), (size_t)(bp - s->res_put));
             const uint64_t h0 = bp > 32768 ? bp - 32768 : 0;      // the window before the new point
-            std::vector<uint8_t> h(o.begin() + (std::ptrdiff_t)(h0 - obase), o.begin() + (std::ptrdiff_t)(bp - obase));
-            s->hist.swap(h);
+            s->hist.assign(o.begin() + (std::ptrdiff_t)(h0 - obase), o.begin() + (std::ptrdiff_t)(bp - obase));
             s->res_bit = bb;
             s->res_put = bp;
             s->imode = 1;
@@ -2018,7 +2079,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took) {
 }
 }  // namespace
 
-int inflate(z_streamp strm, int flush) {
+static int inflate_body(z_streamp strm, int flush) {
     if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
     if (!strm->next_out || (strm->avail_in && !strm->next_in)) return Z_STREAM_ERROR;   // inflate.c:610-612
@@ -2054,9 +2115,39 @@ int inflate(z_streamp strm, int flush) {
 
 int inflateEnd(z_streamp strm) {
     if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
-    delete strm->state;
+    free_state(strm, strm->state);
     strm->state = nullptr;
     return Z_OK;
+}
+
+// the entry points that allocate: an allocation failure is Z_MEM_ERROR
+int deflate(z_streamp strm, int flush) {
+    try {
+        return deflate_body(strm, flush);
+    } catch (const std::bad_alloc &) {
+        return Z_MEM_ERROR;
+    }
+}
+int inflate(z_streamp strm, int flush) {
+    try {
+        return inflate_body(strm, flush);
+    } catch (const std::bad_alloc &) {
+        return Z_MEM_ERROR;
+    }
+}
+int compress2(Bytef *dest, uLongf *destLen, const Bytef *source, uLong sourceLen, int level) {
+    try {
+        return compress2_body(dest, destLen, source, sourceLen, level);
+    } catch (const std::bad_alloc &) {
+        return Z_MEM_ERROR;
+    }
+}
+int uncompress2(Bytef *dest, uLongf *destLen, const Bytef *source, uLong *sourceLen) {
+    try {
+        return uncompress2_body(dest, destLen, source, sourceLen);
+    } catch (const std::bad_alloc &) {
+        return Z_MEM_ERROR;
+    }
 }
 
 // ----------------------- reference WASM front-end -----------------------
