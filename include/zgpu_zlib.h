@@ -8,26 +8,31 @@
  *
  * uncompress()/uncompress2() return what the reference returns for every input
  * (valid, corrupt, truncated, short output), with the same output and the same
- * consumed length.  inflate() gathers input across calls and decodes on the
- * GPU once the gathered input holds a whole stream (checked when the input has
- * doubled since the last attempt, when a call brings no new input, and at
- * Z_FINISH); the output is then drained through next_out/avail_out.  The bytes
- * and the final return code equal the reference's; output arrives once per
- * stream instead of progressively.  inflateSetDictionary is not provided: a
- * stream that needs a preset dictionary returns Z_NEED_DICT.
+ * consumed length.  inflate() decodes whenever input arrives and hands out
+ * every byte decoded so far; each attempt resumes at the last complete block
+ * with the 32 KiB window carried (linear in the stream), and the trailer is
+ * checked as inflate.c does.  inflateSetDictionary() answers Z_NEED_DICT
+ * (zlib streams) or presets a raw stream's window before its first input.
  *
- * deflate() semantics: deflateInit2_ accepts windowBits 15 / -15 / 31 (zlib /
- * raw / gzip wrappers), memLevel 8 and every strategy (Z_DEFAULT_STRATEGY,
- * Z_FILTERED, Z_HUFFMAN_ONLY, Z_RLE, Z_FIXED; deflate.c:1190-1193,1964,
- * 2051-2152, trees.c:1035) — compress2() and the reference's compressSIMD
- * path use the default (compress.c:36, src/zlib_simd_optimized.c:365).  Input is gathered across
- * Z_NO_FLUSH calls and compressed on the GPU at the next flush call or at
- * Z_FINISH; the stream is then drained through next_out/avail_out across as
- * many calls as needed.  Z_PARTIAL_FLUSH, Z_SYNC_FLUSH, Z_FULL_FLUSH and
- * Z_BLOCK act as in deflate.c:763-1265 (markers, full-flush reset, refused
- * repeats with Z_BUF_ERROR); each flush call hands out the stream up to its
- * marker (level 0: deflate_stored's blocks, handed out by every call).  Other
- * parameters return Z_STREAM_ERROR.
+ * deflate() semantics: deflateInit2_ accepts windowBits 8..15 (zlib), -8..-15
+ * (raw), 24..31 (gzip), memLevel 1..9 and every strategy (Z_DEFAULT_STRATEGY,
+ * Z_FILTERED, Z_HUFFMAN_ONLY, Z_RLE, Z_FIXED); the stream is allocated through
+ * zalloc/zfree.  Input is gathered across Z_NO_FLUSH calls and compressed on
+ * the GPU at the next flush call or at Z_FINISH (levels 1..9: Z_NO_FLUSH
+ * calls hand out nothing; the final stream is the reference's); Z_PARTIAL_FLUSH,
+ * Z_SYNC_FLUSH, Z_FULL_FLUSH and Z_BLOCK act as in deflate.c (markers,
+ * full-flush reset, refused repeats with Z_BUF_ERROR), each flush call handing
+ * out the stream up to its marker (level 0: deflate_stored's blocks, handed
+ * out by every call).  deflateSetDictionary, deflateSetHeader, deflatePrime,
+ * deflateTune and deflateParams give the reference's stream where the change
+ * takes effect at a point this library's model knows exactly: before the first
+ * deflate() call, or right after a flush with no input pending (deflateParams
+ * flushes with Z_BLOCK itself when the level's function or the strategy
+ * changes, as deflate.c does).  A change the model cannot place -- tuning a
+ * stream with unflushed input, switching to or from level 0, Z_HUFFMAN_ONLY or
+ * Z_RLE, or between deflate_fast and deflate_slow levels after data, a
+ * dictionary at level 0 -- returns Z_STREAM_ERROR with strm->msg set, never a
+ * different stream.
  */
 #ifndef ZGPU_ZLIB_H
 #define ZGPU_ZLIB_H
@@ -103,6 +108,34 @@ uLong deflateBound(z_streamp strm, uLong sourceLen);                    /* zlib.
 int deflateReset(z_streamp strm);                                       /* zlib.h:621 */
 int deflateCopy(z_streamp dest, z_streamp source);                      /* zlib.h:603 */
 int deflatePending(z_streamp strm, unsigned *pending, int *bits);       /* zlib.h:746 */
+
+/* gzip header (zlib.h gz_header) for deflateSetHeader */
+typedef struct gz_header_s {
+    int text;
+    uLong time;
+    int xflags;
+    int os;
+    Bytef *extra;
+    uInt extra_len;
+    uInt extra_max;
+    Bytef *name;
+    uInt name_max;
+    Bytef *comment;
+    uInt comm_max;
+    int hcrc;
+    int done;
+} gz_header;
+typedef gz_header *gz_headerp;
+
+int deflateSetDictionary(z_streamp strm, const Bytef *dictionary,
+                         uInt dictLength);                              /* zlib.h deflateSetDictionary; deflate.c */
+int deflateParams(z_streamp strm, int level, int strategy);            /* zlib.h deflateParams; deflate.c */
+int deflateTune(z_streamp strm, int good_length, int max_lazy,
+                int nice_length, int max_chain);                        /* zlib.h deflateTune; deflate.c */
+int deflatePrime(z_streamp strm, int bits, int value);                 /* zlib.h deflatePrime; deflate.c */
+int deflateSetHeader(z_streamp strm, gz_headerp head);                 /* zlib.h deflateSetHeader; deflate.c */
+int inflateSetDictionary(z_streamp strm, const Bytef *dictionary,
+                         uInt dictLength);                              /* zlib.h inflateSetDictionary; inflate.c */
 int compress(Bytef *dest, uLongf *destLen, const Bytef *source,
              uLong sourceLen);                                          /* zlib.h:1251 */
 int compress2(Bytef *dest, uLongf *destLen, const Bytef *source,

@@ -1,0 +1,149 @@
+"""Regenerate tests/golden/zstream_golden.json from the COMPILED REFERENCE.
+
+Build container only (oracle/_ref/libzref.so, `make -C oracle ref`):
+
+    python tests/golden/make_zstream_golden.py
+
+Scripted z_stream sessions over the reference's deflateSetDictionary,
+deflateTune, deflateParams, deflatePrime and deflateSetHeader (deflate.c),
+run by tests/zhelpers.run_zsession: each fixture records the session (ops with
+data given as tests/datagen.py specs), the reference's return code of every op
+and the stream's length and sha256.  Only sessions whose changes fall where
+libzgpu.so's model is exact (zgpu_zlib.h) are included; tests/test_gpu_zstream.py
+replays them on the GPU library.
+"""
+import hashlib
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+import datagen  # noqa: E402
+from zhelpers import Reference, run_zsession  # noqa: E402
+
+
+def spec_bytes(x):
+    if x[0] == "gen":
+        d = datagen.make(x[1], x[2], x[3])
+        return d[x[4]: x[5]] if len(x) > 4 else d
+    return bytes.fromhex(x[1])
+
+
+def materialize(ops):
+    out = []
+    for op in ops:
+        if op[0] in ("dict",):
+            out.append((op[0], spec_bytes(op[1])))
+        elif op[0] == "deflate":
+            out.append(("deflate", spec_bytes(op[1]), op[2]))
+        elif op[0] == "header":
+            f = dict(op[1])
+            for k in ("extra", "name", "comment"):
+                if k in f:
+                    f[k] = bytes.fromhex(f[k])
+            out.append(("header", f))
+        else:
+            out.append(tuple(op))
+    return out
+
+
+def sessions():
+    S = []
+    text = ["gen", "text", 150000, 21]
+    mix = ["gen", "mix", 200000, 22]
+    d_small = ["gen", "text", 300, 31]
+    d_mid = ["gen", "text", 9000, 32]
+    d_win = ["gen", "mix", 32768, 33]
+    d_big = ["gen", "text", 50000, 34]
+    # deflateSetDictionary before the first deflate(): zlib and raw wrappers,
+    # fast and slow levels, strategies, dictionary sizes up to beyond the window
+    for level in (1, 3, 4, 6, 9):
+        for wb in (15, -15, 11):
+            for d in (d_small, d_mid, d_win):
+                S.append({"name": f"dict-L{level}-w{wb}-{d[2]}", "ops": [
+                    ["init", level, wb, 8, 0], ["dict", d], ["deflate", text, 4]]})
+    for strategy in (1, 2, 3, 4):
+        S.append({"name": f"dict-L6-s{strategy}", "ops": [
+            ["init", 6, 15, 8, strategy], ["dict", d_mid], ["deflate", mix, 4]]})
+    S.append({"name": "dict-big-raw", "ops": [["init", 6, -15, 8, 0], ["dict", d_big], ["deflate", text, 4]]})
+    S.append({"name": "dict-two", "ops": [["init", 6, 15, 8, 0], ["dict", d_small], ["dict", d_mid],
+                                          ["deflate", text, 4]]})
+    S.append({"name": "dict-flushes", "ops": [["init", 6, 15, 8, 0], ["dict", d_mid],
+                                              ["deflate", ["gen", "text", 150000, 21, 0, 70000], 2],
+                                              ["deflate", ["gen", "text", 150000, 21, 70000, 150000], 4]]})
+    S.append({"name": "dict-L2-flushes", "ops": [["init", 2, 15, 8, 0], ["dict", d_mid],
+                                                 ["deflate", ["gen", "mix", 200000, 22, 0, 90000], 1],
+                                                 ["deflate", ["gen", "mix", 200000, 22, 90000, 200000], 4]]})
+    S.append({"name": "dict-gzip-refused", "ops": [["init", 6, 31, 8, 0], ["dict", d_mid], ["deflate", text, 4]]})
+    S.append({"name": "dict-after-deflate-refused", "ops": [["init", 6, 15, 8, 0],
+                                                            ["deflate", ["gen", "text", 1000, 3], 0],
+                                                            ["dict", d_mid], ["deflate", text, 4]]})
+    # deflateTune before data and after a flush
+    for level, t in ((6, (4, 4, 8, 4)), (6, (8, 16, 258, 0)), (6, (1, 300, 258, 100)), (9, (32, 258, 258, 8192)),
+                     (4, (2, 10, 20, 5)), (2, (2, 6, 12, 16)), (1, (8, 3, 300, 2)), (6, (0, 0, 0, 1)),
+                     (5, (300, 8, 40, 64))):
+        S.append({"name": f"tune-L{level}-{'-'.join(map(str, t))}", "ops": [
+            ["init", level, 15, 8, 0], ["tune"] + list(t), ["deflate", mix, 4]]})
+    S.append({"name": "tune-after-flush", "ops": [
+        ["init", 6, 15, 8, 0], ["deflate", ["gen", "mix", 200000, 22, 0, 100000], 2],
+        ["tune", 4, 6, 32, 16], ["deflate", ["gen", "mix", 200000, 22, 100000, 200000], 4]]})
+    # deflateParams: before data, after a flush, strategy switches with their own Z_BLOCK
+    for a, b in ((6, 1), (1, 9), (6, 0), (0, 6), (9, 4)):
+        S.append({"name": f"params-start-{a}-{b}", "ops": [
+            ["init", a, 15, 8, 0], ["params", b, 0], ["deflate", text, 4]]})
+    S.append({"name": "params-after-flush-6-9", "ops": [
+        ["init", 6, 15, 8, 0], ["deflate", ["gen", "mix", 200000, 22, 0, 100000], 3],
+        ["params", 9, 0], ["deflate", ["gen", "mix", 200000, 22, 100000, 200000], 4]]})
+    S.append({"name": "params-after-flush-2-1", "ops": [
+        ["init", 2, 15, 8, 0], ["deflate", ["gen", "text", 150000, 21, 0, 60000], 2],
+        ["params", 1, 0], ["deflate", ["gen", "text", 150000, 21, 60000, 150000], 4]]})
+    S.append({"name": "params-strategy-block", "ops": [
+        ["init", 6, 15, 8, 0], ["deflate", ["gen", "mix", 200000, 22, 0, 120000], 0],
+        ["params", 6, 1], ["deflate", ["gen", "mix", 200000, 22, 120000, 200000], 4]]})
+    S.append({"name": "params-fixed-block", "ops": [
+        ["init", 4, -15, 8, 0], ["deflate", ["gen", "text", 150000, 21, 0, 50000], 0],
+        ["params", 5, 4], ["deflate", ["gen", "text", 150000, 21, 50000, 150000], 4]]})
+    # deflatePrime
+    for wb in (-15, 15):
+        for bits, val in ((1, 1), (3, 5), (8, 0xa5), (11, 0x5a5), (16, 0xbeef), (0, 0)):
+            S.append({"name": f"prime-w{wb}-{bits}", "ops": [
+                ["init", 6, wb, 8, 0], ["prime", bits, val], ["deflate", text, 4]]})
+    S.append({"name": "prime-twice-L1", "ops": [["init", 1, -15, 8, 0], ["prime", 5, 19], ["prime", 7, 100],
+                                                ["deflate", mix, 4]]})
+    S.append({"name": "prime-L0", "ops": [["init", 0, -15, 8, 0], ["prime", 6, 33], ["deflate", text, 4]]})
+    S.append({"name": "prime-after-partial", "ops": [
+        ["init", 6, -15, 8, 0], ["deflate", ["gen", "text", 150000, 21, 0, 40000], 1],
+        ["prime", 5, 9], ["deflate", ["gen", "text", 150000, 21, 40000, 150000], 4]]})
+    S.append({"name": "prime-bad", "ops": [["init", 6, -15, 8, 0], ["prime", 17, 1], ["prime", -1, 1],
+                                           ["deflate", text, 4]]})
+    # deflateSetHeader
+    hdrs = [{"text": 1, "time": 1234567890, "os": 3},
+            {"time": 7, "os": 11, "name": b"file.txt".hex(), "comment": b"a comment".hex()},
+            {"text": 0, "time": 99, "os": 255, "extra": bytes(range(40)).hex(), "hcrc": 1},
+            {"text": 1, "time": 0xffffffff, "os": 0, "extra": b"AB\x03\x00xyz".hex(), "name": b"n".hex(),
+             "comment": b"".hex(), "hcrc": 1}]
+    for i, h in enumerate(hdrs):
+        for level in (1, 6, 9):
+            S.append({"name": f"header-{i}-L{level}", "ops": [
+                ["init", level, 31, 8, 0], ["header", h], ["deflate", text, 4]]})
+    S.append({"name": "header-on-zlib-refused", "ops": [["init", 6, 15, 8, 0], ["header", hdrs[0]],
+                                                        ["deflate", text, 4]]})
+    return S
+
+
+def main():
+    ref = Reference()
+    out = {"reference": ref.version.decode(), "sessions": []}
+    for sess in sessions():
+        rcs, z = run_zsession(ref.L, materialize(sess["ops"]))
+        out["sessions"].append({"name": sess["name"], "ops": sess["ops"], "rcs": rcs, "len": len(z),
+                                "sha256": hashlib.sha256(z).hexdigest()})
+    path = os.path.join(HERE, "zstream_golden.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=0, sort_keys=True)
+    print(f"wrote {path}: {len(out['sessions'])} sessions")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,65 @@
+"""GPU parity of the z_stream controls (deflateSetDictionary, deflateTune,
+deflateParams, deflatePrime, deflateSetHeader, inflateSetDictionary): scripted
+sessions replayed on libzgpu.so against the compiled reference's return codes
+and streams, frozen in tests/golden/zstream_golden.json by
+tests/golden/make_zstream_golden.py."""
+import hashlib
+import json
+import os
+import sys
+
+import pytest
+
+import datagen
+from zhelpers import run_isession, run_zsession
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+from make_zstream_golden import materialize  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def zs_golden():
+    with open(os.path.join(HERE, "golden", "zstream_golden.json")) as f:
+        return json.load(f)
+
+
+def _rc_equal(op, got, want):
+    if op[0] == "dict":                     # (rc, strm->adler); the adler only where the call succeeded
+        return got[0] == want[0] and (want[0] != 0 or got[1] == want[1])
+    return got == want
+
+
+def test_zstream_sessions_vs_reference(zg, zs_golden):
+    L = zg.load()
+    bad = []
+    for sess in zs_golden["sessions"]:
+        rcs, z = run_zsession(L, materialize(sess["ops"]))
+        ok = len(rcs) == len(sess["rcs"]) and all(
+            _rc_equal(op, tuple(g) if isinstance(g, tuple) else g, tuple(w) if op[0] == "dict" else w)
+            for op, g, w in zip(sess["ops"], rcs, sess["rcs"]))
+        if not ok or len(z) != sess["len"] or hashlib.sha256(z).hexdigest() != sess["sha256"]:
+            bad.append((sess["name"], rcs, sess["rcs"], len(z), sess["len"]))
+    assert not bad, bad[:5]
+
+
+def test_inflate_with_dictionary(zg):
+    """A zlib stream with FDICT: Z_NEED_DICT with the header consumed and
+    strm->adler = DICTID, a wrong dictionary is Z_DATA_ERROR, the right one
+    decodes; a raw stream takes its dictionary before the first input."""
+    L = zg.load()
+    data = datagen.make("text", 200000, 40)
+    dic = datagen.make("text", 20000, 41)
+    for level, wb in ((6, 15), (1, 15), (9, 12)):
+        _, z = run_zsession(L, [("init", level, wb, 8, 0), ("dict", dic), ("deflate", data, 4)])
+        for chunk in (1 << 30, 4096):
+            rcs, out = run_isession(L, z, wb, dic, chunk)
+            assert out == data and rcs[-1] == 1, (level, wb, chunk, rcs[:4])
+            assert rcs[1][0] == "need" and rcs[1][2] == 6
+        rcs, out = run_isession(L, z, wb, dic[:-1] + b"?")
+        assert rcs[-1] == -3 and out == b""
+    _, z = run_zsession(L, [("init", 6, -15, 8, 0), ("dict", dic), ("deflate", data, 4)])
+    rcs, out = run_isession(L, z, -15, dic, 3000)
+    assert out == data and rcs[-1] == 1

@@ -343,3 +343,128 @@ def flush_events(calls):
 
 def reference_available():
     return os.path.exists(REF_SO)
+
+
+class GzHeader(C.Structure):
+    """gz_header as zlib.h declares it (deflateSetHeader)."""
+    _fields_ = [("text", C.c_int), ("time", C.c_ulong), ("xflags", C.c_int), ("os", C.c_int),
+                ("extra", C.c_void_p), ("extra_len", C.c_uint), ("extra_max", C.c_uint),
+                ("name", C.c_void_p), ("name_max", C.c_uint), ("comment", C.c_void_p),
+                ("comm_max", C.c_uint), ("hcrc", C.c_int), ("done", C.c_int)]
+
+
+def _bind_zstream(L):
+    P = C.POINTER(ZStream)
+    for name, res, args in (
+            ("deflateInit2_", C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_int]),
+            ("deflate", C.c_int, [P, C.c_int]), ("deflateEnd", C.c_int, [P]),
+            ("deflateSetDictionary", C.c_int, [P, C.c_void_p, C.c_uint]),
+            ("deflateParams", C.c_int, [P, C.c_int, C.c_int]),
+            ("deflateTune", C.c_int, [P, C.c_int, C.c_int, C.c_int, C.c_int]),
+            ("deflatePrime", C.c_int, [P, C.c_int, C.c_int]),
+            ("deflateSetHeader", C.c_int, [P, C.POINTER(GzHeader)]),
+            ("inflateInit2_", C.c_int, [P, C.c_int, C.c_char_p, C.c_int]),
+            ("inflate", C.c_int, [P, C.c_int]), ("inflateEnd", C.c_int, [P]),
+            ("inflateSetDictionary", C.c_int, [P, C.c_void_p, C.c_uint])):
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+
+
+def run_zsession(L, ops, version=b"1.3.1.1-motley"):
+    """Run a scripted z_stream deflate session on library L (the reference or
+    libzgpu.so) and return (return codes / adler values per op, stream bytes).
+    ops: ("init", level, windowBits, memLevel, strategy), ("dict", bytes),
+    ("tune", good, lazy, nice, chain), ("params", level, strategy),
+    ("prime", bits, value), ("header", dict of gz_header fields),
+    ("deflate", bytes, flush).  Output space is always ample."""
+    _bind_zstream(L)
+    s = ZStream()
+    out, rcs, keep = bytearray(), [], []
+    obuf_n = 1 << 16
+
+    def with_out(call, extra=0):
+        n = obuf_n + extra
+        ob = C.create_string_buffer(n)
+        s.next_out, s.avail_out = C.addressof(ob), n
+        rc = call()
+        out.extend(ob.raw[: n - s.avail_out])
+        return rc
+
+    for op in ops:
+        k = op[0]
+        if k == "init":
+            rcs.append(L.deflateInit2_(C.byref(s), op[1], 8, op[2], op[3], op[4], version, C.sizeof(ZStream)))
+        elif k == "dict":
+            b = C.create_string_buffer(op[1], len(op[1]))
+            rcs.append((L.deflateSetDictionary(C.byref(s), b, len(op[1])), s.adler))
+        elif k == "tune":
+            rcs.append(L.deflateTune(C.byref(s), *op[1:]))
+        elif k == "params":
+            rcs.append(with_out(lambda: L.deflateParams(C.byref(s), op[1], op[2]), 1 << 20))
+        elif k == "prime":
+            rcs.append(L.deflatePrime(C.byref(s), op[1], op[2]))
+        elif k == "header":
+            h = GzHeader()
+            f = op[1]
+            h.text, h.time, h.os, h.hcrc = f.get("text", 0), f.get("time", 0), f.get("os", 3), f.get("hcrc", 0)
+            for fld in ("extra", "name", "comment"):
+                if fld in f:
+                    buf = C.create_string_buffer(f[fld], len(f[fld]) + (0 if fld == "extra" else 1))
+                    keep.append(buf)
+                    setattr(h, fld, C.addressof(buf))
+            if "extra" in f:
+                h.extra_len = len(f["extra"])
+            keep.append(h)
+            rcs.append(L.deflateSetHeader(C.byref(s), C.byref(h)))
+        elif k == "deflate":
+            data, flush = op[1], op[2]
+            ib = C.create_string_buffer(data, len(data))
+            keep.append(ib)
+            s.next_in, s.avail_in = C.addressof(ib), len(data)
+            seq = []
+            for _ in range(1000):
+                rc = with_out(lambda: L.deflate(C.byref(s), flush), len(data) + len(data) // 2)
+                seq.append(rc)
+                if rc < 0 or rc == 1 or (s.avail_in == 0 and s.avail_out != 0):
+                    break
+            rcs.append(seq)
+        else:
+            raise ValueError(k)
+    L.deflateEnd(C.byref(s))
+    return rcs, bytes(out)
+
+
+def run_isession(L, z, wbits=15, dictionary=None, chunk=1 << 30, version=b"1.3.1.1-motley"):
+    """Inflate z on library L through the z_stream API, answering Z_NEED_DICT
+    with `dictionary` (or setting it up front for raw streams, wbits < 0);
+    returns (return codes, output)."""
+    _bind_zstream(L)
+    s = ZStream()
+    rcs = [L.inflateInit2_(C.byref(s), wbits, version, C.sizeof(ZStream))]
+    if dictionary is not None and wbits < 0:
+        rcs.append(L.inflateSetDictionary(C.byref(s), dictionary, len(dictionary)))
+    ib = C.create_string_buffer(bytes(z), len(z))
+    ob = C.create_string_buffer(1 << 20)
+    out, pos = bytearray(), 0
+    for _ in range(100000):
+        if s.avail_in == 0 and pos < len(z):
+            take = min(chunk, len(z) - pos)
+            s.next_in, s.avail_in = C.addressof(ib) + pos, take
+            pos += take
+        s.next_out, s.avail_out = C.addressof(ob), 1 << 20
+        rc = L.inflate(C.byref(s), 0)
+        out.extend(ob.raw[: (1 << 20) - s.avail_out])
+        if rc == 2:                                      # Z_NEED_DICT
+            rcs.append(("need", s.adler, s.total_in))
+            d = dictionary if dictionary is not None else b""
+            r = L.inflateSetDictionary(C.byref(s), d, len(d))
+            rcs.append(r)
+            if r != 0:
+                break
+            continue
+        if rc != 0 or (pos == len(z) and s.avail_in == 0 and s.avail_out != 0):
+            rcs.append(rc)
+            break
+    L.inflateEnd(C.byref(s))
+    return rcs, bytes(out)

@@ -59,6 +59,12 @@ uint32_t x2nmodp(int64_t n, unsigned k) {                     // crc32.c:176-187
     return p;
 }
 
+// configuration_table (deflate.c:112-125): good, lazy, nice, chain
+const LevelCfg kLevelCfg[10] = {{0, 0, 0, 0},      {4, 4, 8, 4},       {4, 5, 16, 8},
+                                {4, 6, 32, 32},    {4, 4, 16, 16},    {8, 16, 32, 32},
+                                {8, 16, 128, 128}, {8, 32, 128, 256}, {32, 128, 258, 1024},
+                                {32, 258, 258, 4096}};
+
 unsigned bitrev(unsigned code, int len) {
     unsigned r = 0;
     while (len-- > 0) { r = (r << 1) | (code & 1u); code >>= 1; }
@@ -103,11 +109,7 @@ void build_code_tables(CodeTables &t) {
     for (int n = 0; n < 288; n++) t.stat_lcode[n] = (uint16_t)bitrev(next[t.stat_llen[n]]++, t.stat_llen[n]);
     for (int n = 0; n < 30; n++) t.stat_dcode[n] = (uint16_t)bitrev((unsigned)n, 5);
     for (int n = 0; n < 30; n++) t.stat_dlen[n] = 5;
-    static const LevelCfg cfg[10] = {{0, 0, 0, 0},      {4, 4, 8, 4},       {4, 5, 16, 8},
-                                     {4, 6, 32, 32},    {4, 4, 16, 16},    {8, 16, 32, 32},
-                                     {8, 16, 128, 128}, {8, 32, 128, 256}, {32, 128, 258, 1024},
-                                     {32, 258, 258, 4096}};
-    std::memcpy(t.cfg, cfg, sizeof cfg);
+    std::memcpy(t.cfg, kLevelCfg, sizeof kLevelCfg);
 }
 
 void build_crc_tables(CrcTables &t) {
@@ -376,6 +378,8 @@ struct FlushSpec {
     // way deflate_stored cuts them (see deflate_stored_call)
     const BlockRec *plan;
     uint32_t nplan;
+    int dict;                      // DeflateJob::dict / pre_ins (a preset dictionary)
+    uint32_t pre_ins;
 };
 
 // deflateInit2_'s windowBits / memLevel rules (deflate.c:400-425): negative
@@ -403,7 +407,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
                        uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
                        uint64_t *dst_len, int32_t *status, uint32_t count, int level, int wrap,
                        int strategy, hipStream_t st, const FlushSpec *fs = nullptr, int wbits = 15,
-                       int mem_level = 8) {
+                       int mem_level = 8, const LevelCfg *tune = nullptr) {
     if (level == -1) level = 6;
     if (level < 0 || level > 9 || wrap < 0 || wrap > 2 || strategy < 0 || strategy > 4 || wbits < 9 ||
         wbits > 15 || mem_level < 1 || mem_level > 9)
@@ -558,6 +562,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         job.dst_len = dst_len; job.status = status;
         job.first = a; job.count = b - a; job.level = level; job.wrap = wrap; job.strategy = strategy;
         job.wbits = wbits; job.hbits = hbits;
+        job.cfg = tune ? *tune : kLevelCfg[level];
         job.ws_off = d_meta + a;
         job.blk_off = d_meta + count + a;
         job.link = (slot ? c.ws_link2 : c.ws_link).as<uint16_t>();
@@ -585,6 +590,8 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.byte0 = fs->byte0;
             job.flush_out = fs->out;
             job.plan = fs->plan != nullptr;
+            job.dict = fs->dict;
+            job.pre_ins = fs->pre_ins;
         }
         return job;
     };
@@ -674,11 +681,14 @@ struct FlushHost {
     std::vector<uint16_t> *prev_out = nullptr;
     const BlockRec *plan = nullptr;    // level 0: see FlushSpec
     uint32_t nplan = 0;
+    int dict = 0;                      // see FlushSpec
+    uint32_t pre_ins = 0;
 };
 
 int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
                          size_t *dst_len, int *status, size_t count, int level, int wrap, int strategy,
-                         FlushHost *fh = nullptr, int wbits = 15, int mem_level = 8) {
+                         FlushHost *fh = nullptr, int wbits = 15, int mem_level = 8,
+                         const LevelCfg *tune = nullptr) {
     if (count == 0) return ZGPU_OK;
     for (size_t i = 0; i < count; i++)
         if (src_len[i] >= kMaxBuffer) return ZGPU_STREAM_ERROR;
@@ -728,10 +738,10 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
         uint64_t *d_mb = d_fp + fh->n + (fh->n + 1) / 2;
         if (hipMemsetAsync(d_mb, 0, 32, st) != hipSuccess) return ZGPU_MEM_ERROR;
         fs = FlushSpec{d_fp, d_ft, fh->n, fh->open_end, fh->start, fh->bit0, fh->byte0, d_mb,
-                       fh->head_in, fh->prev_in, fh->prev_n, fh->plan, fh->nplan};
+                       fh->head_in, fh->prev_in, fh->prev_n, fh->plan, fh->nplan, fh->dict, fh->pre_ins};
     }
     int rc = deflate_dev_locked(c, d_in, d_so, d_sl, d_out, d_do, d_dc, d_dl, d_st, (uint32_t)count,
-                                level, wrap, strategy, st, fh ? &fs : nullptr, wbits, mem_level);
+                                level, wrap, strategy, st, fh ? &fs : nullptr, wbits, mem_level, tune);
     if (rc) return rc;
     if (fh && copy_sync(fh->out, fs.out, 32, hipMemcpyDeviceToHost, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
@@ -1242,6 +1252,7 @@ int zgpu_debug_stages(const uint8_t *src, size_t n, int level, uint16_t *link, u
     job.src = c.ws_io.as<uint8_t>(); job.src_off = d_meta; job.src_len = d_meta + 1;
     job.first = 0; job.count = 1; job.level = level; job.wrap = 1;
     job.wbits = 15; job.hbits = 15;                   // deflateInit_ defaults (deflate.c:444)
+    job.cfg = kLevelCfg[level];
     job.ws_off = d_meta + 2;
     job.link = c.ws_link.as<uint16_t>();
     job.rfull = c.ws_rf.as<uint32_t>();
@@ -1418,6 +1429,14 @@ struct internal_state {
     uint64_t res_bit = 0, res_put = 0, ideliv = 0;
     uint32_t icheck = 0;    // Adler-32 / CRC-32 of the output before res_put
     zvec<uint8_t> hist;
+    // deflateTune (deflate.c:805-820): the jobs' good/lazy/nice/chain
+    bool tuned = false;
+    LevelCfg tune{};
+    const gz_header *gzhead = nullptr;   // deflateSetHeader: written by the first deflate() call
+    bool dict_set = false;               // deflateSetDictionary: the zlib header's FDICT + DICTID
+    uint32_t dict_id = 0;
+    bool need_dict = false;              // inflate: Z_NEED_DICT answered, waiting for the dictionary
+    uint32_t want_dict = 0;              // its DICTID
 };
 
 namespace {
@@ -1491,8 +1510,16 @@ int deflate_part(internal_state *s, int open_end, std::vector<uint8_t> &body, ui
     FlushHost fh{pos.data(), s->ev_type.data() + s->res_ev, (uint32_t)nev, open_end, (uint32_t)(s->res_pos - base),
                  (uint32_t)(s->res_bits & 7), s->res_byte & ((1u << (s->res_bits & 7)) - 1u), {0, 0, 0, 0}};
     std::vector<uint32_t> head_in;
+    if (s->level >= 1 && s->level <= 3 && s->strategy != Z_HUFFMAN_ONLY && s->strategy != Z_RLE &&
+        s->res_pos > base && s->fast_head.empty()) {
+        // the part starts with a preset dictionary: its strings are inserted
+        // first, all but the last two (deflateSetDictionary, deflate.c)
+        const uint32_t d = (uint32_t)(s->res_pos - base);
+        fh.dict = 1;
+        fh.pre_ins = d >= kMinMatch ? d - (kMinMatch - 1) : 0;
+    }
     if (s->level >= 1 && s->level <= 3 && s->strategy != Z_HUFFMAN_ONLY && s->strategy != Z_RLE) {
-        if (s->res_pos > base) {                               // rebase the saved chains to this buffer
+        if (s->res_pos > base && !fh.dict) {                   // rebase the saved chains to this buffer
             head_in.resize(s->fast_head.size());
             for (size_t i = 0; i < head_in.size(); i++)
                 head_in[i] = s->fast_head[i] > base ? s->fast_head[i] - (uint32_t)base : 0;
@@ -1506,7 +1533,7 @@ int deflate_part(internal_state *s, int open_end, std::vector<uint8_t> &body, ui
     Lease L;
     int rc = L.rc;
     if (!rc) rc = compress_host_locked(*L.c, &sp, &sl, &dp, &cap, &st, 1, s->level, ZGPU_WRAP_RAW, s->strategy, &fh,
-                                       s->wbits, s->mem_level);
+                                       s->wbits, s->mem_level, s->tuned ? &s->tune : nullptr);
     if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
     body.resize(cap);
     for (int i = 0; i < 4; i++) out[i] = fh.out[i];
@@ -1547,14 +1574,51 @@ void queue_header(internal_state *s) {                          // deflate.c:100
         uint32_t header = (8u + ((uint32_t)(s->wbits - 8) << 4)) << 8;
         const uint32_t flags = (s->strategy >= 2 || s->level < 2) ? 0u : s->level < 6 ? 1u : s->level == 6 ? 2u : 3u;
         header |= flags << 6;
+        if (s->dict_set) header |= 0x20;                        // PRESET_DICT
         header += 31 - (header % 31);
         s->out.push_back((uint8_t)(header >> 8));
         s->out.push_back((uint8_t)header);
+        if (s->dict_set)                                        // DICTID, most significant byte first
+            for (int i = 3; i >= 0; i--) s->out.push_back((uint8_t)(s->dict_id >> (8 * i)));
     } else if (s->wrap == 2) {
         const uint8_t xfl = s->level == 9 ? 2 : (s->strategy >= 2 || s->level < 2) ? 4 : 0;
-        const uint8_t g[10] = {31, 139, 8, 0, 0, 0, 0, 0, xfl, 3};
-        s->out.insert(s->out.end(), g, g + 10);
+        const gz_header *h = s->gzhead;
+        if (!h) {
+            const uint8_t g[10] = {31, 139, 8, 0, 0, 0, 0, 0, xfl, 3};   // OS_CODE 3 (Unix)
+            s->out.insert(s->out.end(), g, g + 10);
+            return;
+        }
+        // deflateSetHeader's fields (deflate.c GZIP_STATE .. HCRC_STATE)
+        std::vector<uint8_t> g = {31, 139, 8,
+                                  (uint8_t)((h->text ? 1 : 0) + (h->hcrc ? 2 : 0) + (h->extra ? 4 : 0) +
+                                            (h->name ? 8 : 0) + (h->comment ? 16 : 0)),
+                                  (uint8_t)(h->time & 0xff), (uint8_t)((h->time >> 8) & 0xff),
+                                  (uint8_t)((h->time >> 16) & 0xff), (uint8_t)((h->time >> 24) & 0xff), xfl,
+                                  (uint8_t)(h->os & 0xff)};
+        if (h->extra) {
+            g.push_back((uint8_t)(h->extra_len & 0xff));
+            g.push_back((uint8_t)((h->extra_len >> 8) & 0xff));
+            g.insert(g.end(), h->extra, h->extra + (h->extra_len & 0xffff));
+        }
+        if (h->name)
+            for (const Bytef *p = h->name;; p++) { g.push_back(*p); if (!*p) break; }
+        if (h->comment)
+            for (const Bytef *p = h->comment;; p++) { g.push_back(*p); if (!*p) break; }
+        if (h->hcrc) {                                          // the header's CRC-32, low 16 bits
+            const uint32_t c = (uint32_t)crc32_z(0, g.data(), g.size());
+            g.push_back((uint8_t)(c & 0xff));
+            g.push_back((uint8_t)((c >> 8) & 0xff));
+        }
+        s->out.insert(s->out.end(), g.begin(), g.end());
     }
+}
+
+// input given to deflate() since the last point where the whole stream is
+// known (the start, or a flush that compressed everything)
+bool pending_input(const internal_state *s) {
+    if (s->last_flush == -2 || s->finished) return false;
+    if (s->level == 0) return !s->in.empty();
+    return s->in_base + s->in.size() > s->res_pos || s->marker_due;
 }
 
 void drain(z_streamp strm, internal_state *s) {
@@ -1781,7 +1845,7 @@ static int deflate_body(z_streamp strm, int flush) {
                 Lease L;
                 rc = L.rc;
                 if (!rc) rc = compress_host_locked(*L.c, &sp, &sl, &dp, &cap, &st, 1, s->level, s->wrap, s->strategy,
-                                                   nullptr, s->wbits, s->mem_level);
+                                                   nullptr, s->wbits, s->mem_level, s->tuned ? &s->tune : nullptr);
             }
             if (rc || st) {
                 s->out.clear();          // nothing of a failed call may be handed out by a retry
@@ -1822,7 +1886,9 @@ int deflateReset(z_streamp strm) {                              // deflate.c:560
     if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
     const int level = s->level, wrap = s->wrap, strategy = s->strategy, wbits = s->wbits, mem = s->mem_level;
+    const gz_header *gzhead = s->gzhead;                       // deflateResetKeep keeps it
     *s = internal_state(s->al);
+    s->gzhead = gzhead;
     s->level = level;
     s->wrap = wrap;
     s->strategy = strategy;
@@ -1855,6 +1921,136 @@ int deflatePending(z_streamp strm, unsigned *pending, int *bits) {
     internal_state *s = strm->state;
     if (pending) *pending = (unsigned)(s->out.size() - s->out_pos);
     if (bits) *bits = s->finished ? 0 : (int)(s->res_bits & 7);
+    return Z_OK;
+}
+
+namespace {
+int unsupported(z_streamp strm, const char *why) {
+    strm->msg = const_cast<char *>(why);
+    return Z_STREAM_ERROR;
+}
+int deflate_fn(int level) { return level == 0 ? 0 : level <= 3 ? 1 : 2; }   // stored, fast, slow
+}  // namespace
+
+// deflateSetDictionary (deflate.c): the dictionary (its last w_size bytes)
+// becomes the window the first part is compressed against: the part's buffer
+// starts with it and the parse at its end; a zlib stream's header carries
+// FDICT and its Adler-32.  Before the first deflate() call only (the zlib
+// wrapper's own rule; raw streams mid-stream are not modelled), not at level 0.
+int deflateSetDictionary(z_streamp strm, const Bytef *dictionary, uInt dictLength) {
+    if (!strm || !strm->state || strm->state->inflating || !dictionary) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    if (s->wrap == 2 || (s->wrap == 1 && s->last_flush != -2)) return Z_STREAM_ERROR;
+    if (s->last_flush != -2) return unsupported(strm, "deflateSetDictionary: only before the first deflate()");
+    if (s->level == 0) return unsupported(strm, "deflateSetDictionary: level 0 not supported");
+    try {
+        if (s->wrap == 1) strm->adler = adler32_z(strm->adler, dictionary, dictLength);
+        const size_t wsize = size_t(1) << s->wbits;
+        if (dictLength == 0) return Z_OK;
+        if (dictLength >= wsize) {                 // the tail replaces the history
+            if (s->wrap == 1 && !s->in.empty())
+                return unsupported(strm, "deflateSetDictionary: a second dictionary beyond the window size");
+            s->in.assign(dictionary + (dictLength - wsize), dictionary + dictLength);
+        } else {
+            if (s->in.size() + dictLength > wsize)
+                return unsupported(strm, "deflateSetDictionary: dictionaries beyond the window size");
+            s->in.insert(s->in.end(), dictionary, dictionary + dictLength);
+        }
+        s->in_base = 0;
+        s->res_S = 0;
+        s->res_pos = s->ck_pos = s->in.size();
+        s->res_ev = 0;
+        s->flushed = true;                 // the part path (bit and parse offsets)
+        s->dict_set = s->wrap == 1;
+        s->dict_id = (uint32_t)strm->adler;
+        return Z_OK;
+    } catch (const std::bad_alloc &) {
+        return Z_MEM_ERROR;
+    }
+}
+
+// deflateTune (deflate.c): good_length, max_lazy, nice_length, max_chain for
+// the jobs from here on (unsigned as deflate_state holds them; a chain of 0
+// never runs out in longest_match's unsigned count).  Exact where no input is
+// pending (see zgpu_zlib.h).
+int deflateTune(z_streamp strm, int good_length, int max_lazy, int nice_length, int max_chain) {
+    if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    if (pending_input(s)) return unsupported(strm, "deflateTune: input pending since the last flush");
+    s->tune = LevelCfg{(uint32_t)good_length, (uint32_t)max_lazy,
+                       nice_length < 0 ? 0xffffffffu : (uint32_t)nice_length,
+                       max_chain == 0 ? 0xffffffffu : (uint32_t)max_chain};
+    s->tuned = true;
+    return Z_OK;
+}
+
+// deflateParams (deflate.c): flushes with Z_BLOCK when the level's function
+// or the strategy changes and deflate() has run, then switches.
+int deflateParams(z_streamp strm, int level, int strategy) {
+    if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    if (level == Z_DEFAULT_COMPRESSION) level = 6;
+    if (level < 0 || level > 9 || strategy < 0 || strategy > Z_FIXED) return Z_STREAM_ERROR;
+    const bool started = s->last_flush != -2;
+    if (started && !s->finished) {
+        const bool own_fn = strategy == Z_HUFFMAN_ONLY || strategy == Z_RLE ||
+                            s->strategy == Z_HUFFMAN_ONLY || s->strategy == Z_RLE;
+        if (deflate_fn(level) != deflate_fn(s->level) || (strategy != s->strategy && own_fn))
+            return unsupported(strm, "deflateParams: this switch after data is not modelled");
+    }
+    if ((strategy != s->strategy || deflate_fn(level) != deflate_fn(s->level)) && started) {
+        const int err = deflate(strm, Z_BLOCK);
+        if (err == Z_STREAM_ERROR) return err;
+        if (strm->avail_in || pending_input(s)) return Z_BUF_ERROR;
+    } else if (s->level != level && pending_input(s)) {
+        return unsupported(strm, "deflateParams: input pending since the last flush");
+    }
+    if (s->level != level) {
+        s->level = level;
+        s->tuned = false;                  // configuration_table's row again
+    }
+    s->strategy = strategy;
+    return Z_OK;
+}
+
+// deflatePrime (deflate.c): bits in front of what deflate() writes next.
+// Whole bytes are queued at once (pending, ahead of a header not written
+// yet), the rest starts the part's first byte.
+int deflatePrime(z_streamp strm, int bits, int value) {
+    if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    if (bits < 0 || bits > 16) return Z_BUF_ERROR;
+    if (s->finished || pending_input(s)) return unsupported(strm, "deflatePrime: input pending since the last flush");
+    try {
+        uint32_t nb = (uint32_t)(s->res_bits & 7);
+        uint64_t acc = (s->res_byte & ((1u << nb) - 1u)) | ((uint64_t)((uint32_t)value & ((1u << bits) - 1u)) << nb);
+        nb += (uint32_t)bits;
+        uint64_t whole = 0;
+        while (nb >= 8) {
+            s->out.push_back((uint8_t)acc);
+            acc >>= 8;
+            nb -= 8;
+            whole++;
+        }
+        if (s->header_done) {              // part bytes
+            s->part_out += whole;
+            s->res_bits = ((s->res_bits >> 3) + whole) * 8 + nb;
+        } else {                           // ahead of the header: the part starts at the partial byte
+            s->res_bits = nb;
+        }
+        s->res_byte = (uint32_t)acc & 0xffu;
+        s->flushed = true;
+        return Z_OK;
+    } catch (const std::bad_alloc &) {
+        return Z_MEM_ERROR;
+    }
+}
+
+// deflateSetHeader (deflate.c): the gzip header the first deflate() call writes
+int deflateSetHeader(z_streamp strm, gz_headerp head) {
+    if (!strm || !strm->state || strm->state->inflating || strm->state->wrap != 2) return Z_STREAM_ERROR;
+    strm->state->gzhead = head;
+    if (head) strm->state->flushed = true;   // the header is written on the host (queue_header)
     return Z_OK;
 }
 
@@ -1937,6 +2133,7 @@ int inflateReset(z_streamp strm) {
     s->in.clear(); s->out.clear(); s->hist.clear();
     s->out_pos = 0; s->finished = 0; s->tried = 0; s->cap = 0; s->result = Z_OK;
     s->in_base = 0; s->imode = 0; s->igz = 0; s->res_bit = s->res_put = s->ideliv = 0; s->icheck = 0;
+    s->need_dict = false; s->want_dict = 0;
     strm->total_in = strm->total_out = 0;
     strm->msg = nullptr;
     strm->adler = s->wrap & 1;
@@ -1985,6 +2182,20 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took) {
                                            o.begin() + (std::ptrdiff_t)(upto - obase));
         };
         const uint64_t put_abs = obase + t.put;
+        if (!resume && t.stop == kIDict) {
+            // a zlib header with FDICT: Z_NEED_DICT with the header (2 bytes +
+            // DICTID) consumed and the rest handed back (inflate.c DICTID/DICT);
+            // inflateSetDictionary resumes after it
+            const size_t keep = 6, back = std::min<size_t>(s->in.size() - keep, took);
+            strm->next_in -= back;
+            strm->avail_in += (uInt)back;
+            strm->total_in -= back;
+            s->in.resize(s->in.size() - back);
+            s->need_dict = true;
+            s->want_dict = ((uint32_t)s->in[2] << 24) | ((uint32_t)s->in[3] << 16) | ((uint32_t)s->in[4] << 8) | s->in[5];
+            strm->adler = s->want_dict;
+            return Z_OK;
+        }
         if (!resume && t.stop != kIInEnd) {                      // the whole stream in one attempt
             append_new(put_abs);
             s->finished = 1;
@@ -1998,9 +2209,6 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took) {
                 if (s->wrap) strm->adler = s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b
                                                ? crc32_z(0, o.data(), o.size())
                                                : adler32_z(1, o.data(), o.size());
-            } else if (t.stop == kIDict) {
-                s->result = Z_NEED_DICT;
-                strm->adler = ((uLong)s->in[2] << 24) | ((uLong)s->in[3] << 16) | ((uLong)s->in[4] << 8) | s->in[5];
             } else {
                 s->result = Z_DATA_ERROR;
                 strm->msg = const_cast<char *>("invalid or corrupt deflate stream");
@@ -2084,6 +2292,7 @@ static int inflate_body(z_streamp strm, int flush) {
     internal_state *s = strm->state;
     if (!strm->next_out || (strm->avail_in && !strm->next_in)) return Z_STREAM_ERROR;   // inflate.c:610-612
     if (flush == Z_BLOCK || flush == 6 /* Z_TREES */) return Z_STREAM_ERROR;           // documented gap
+    if (s->need_dict) return Z_NEED_DICT;                      // inflate.c DICT: until the dictionary is set
     const size_t took = s->finished ? 0 : strm->avail_in;
     if (took) {
         s->in.insert(s->in.end(), strm->next_in, strm->next_in + took);
@@ -2096,8 +2305,10 @@ static int inflate_body(z_streamp strm, int flush) {
     // byte its input decodes to so far, as inflate() does (inflate.c:622-1221).
     // Each attempt resumes at the last complete block (inflate_attempt).
     const uint64_t in_end = s->in_base + s->in.size();
-    if (!s->finished && (took || (flush == Z_FINISH && s->tried != in_end)))
+    if (!s->finished && (took || (flush == Z_FINISH && s->tried != in_end))) {
         if (int rc = inflate_attempt(strm, s, took)) return rc;
+        if (s->need_dict) return Z_NEED_DICT;
+    }
     size_t give = 0;
     if (s->out_pos < s->out.size() || s->finished) {
         give = std::min<size_t>(strm->avail_out, s->out.size() - s->out_pos);
@@ -2111,6 +2322,39 @@ static int inflate_body(z_streamp strm, int flush) {
     }
     if (took || give) return Z_OK;
     return Z_BUF_ERROR;                                                // inflate.c:1265-1266: no progress
+}
+
+// inflateSetDictionary (inflate.c): a zlib stream that answered Z_NEED_DICT
+// goes on with the dictionary as its window (its Adler-32 must equal the
+// header's DICTID, else Z_DATA_ERROR); a raw stream takes it as the window
+// before its first input.  The decode resumes after the 6 header bytes with the
+// window's last 1 << CINFO+8 bytes in front of the output (inflate_attempt).
+int inflateSetDictionary(z_streamp strm, const Bytef *dictionary, uInt dictLength) {
+    if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    if (s->wrap != 0 && !s->need_dict) return Z_STREAM_ERROR;
+    if (dictLength && !dictionary) return Z_STREAM_ERROR;
+    try {
+        if (s->need_dict) {
+            if ((uint32_t)adler32_z(1, dictionary, dictLength) != s->want_dict) return Z_DATA_ERROR;
+        } else if (!s->in.empty() || s->ideliv || s->imode) {
+            strm->msg = const_cast<char *>("inflateSetDictionary: raw streams before their first input only");
+            return Z_STREAM_ERROR;
+        }
+        const int wb = s->need_dict ? (s->in[0] >> 4) + 8 : (s->wbits ? s->wbits : 15);
+        const size_t wsize = size_t(1) << wb, keep = std::min<size_t>(dictLength, wsize);
+        s->hist.assign(dictionary + (dictLength - keep), dictionary + dictLength);
+        s->res_bit = s->need_dict ? 48 : 0;                    // after CMF, FLG and DICTID
+        s->res_put = s->ideliv = s->hist.size();               // the window counts as handed out
+        s->icheck = 1;
+        s->igz = 0;
+        s->imode = 1;
+        s->need_dict = false;
+        s->tried = 0;
+        return Z_OK;
+    } catch (const std::bad_alloc &) {
+        return Z_MEM_ERROR;
+    }
 }
 
 int inflateEnd(z_streamp strm) {

@@ -301,7 +301,7 @@ __global__ __launch_bounds__(kCntThreads) void k_count(DeflateJob job) {
     const int64_t n = (int64_t)job.src_len[g];
     const uint8_t *in = job.src + job.src_off[g];
     uint8_t *key = job.key + job.ws_off[bi];
-    const uint32_t chain = c_ct.cfg[job.level].chain;
+    const uint32_t chain = job.cfg.chain;
     for (int i = tid; i < 16384; i += kCntThreads) cnt[i] = 0;
     for (int64_t t0 = 0; t0 < n; t0 += kCntStage) {
         __syncthreads();
@@ -745,6 +745,7 @@ __device__ __attribute__((always_inline)) inline void dw_walk(const uint32_t *E,
     int m4 = (s - (int)d0) * 4;
     uint32_t count = 0;
     bool walking = true;
+    bool need_q = want_q != 0;
     // 1. the chain's first kD0 candidates, compared by the whole wave at once
 #pragma unroll
     for (int k = 0; k < kHead; k++) {
@@ -756,10 +757,13 @@ __device__ __attribute__((always_inline)) inline void dw_walk(const uint32_t *E,
             count++;
             const int m4n = m4 - (int)((em & 0xffffu) << 2);
             if (best >= nice || m4n <= limit4 || count >= chain) walking = false;
+            if (need_q && count == qc && walking) {      // a tuned chain/4 inside the head
+                rq[p] = match_rec(best, s4, bpos4);
+                need_q = false;
+            }
             m4 = m4n;
         }
     }
-    bool need_q = want_q != 0;
     if (!walking) {                                  // the walk ended within its head
         const uint32_t r = match_rec(best, s4, bpos4);
         if (need_q) rq[p] = r;
@@ -995,7 +999,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
     uint32_t *rf = job.rfull + job.ws_off[bi];
     uint32_t *rq = job.rquart + job.ws_off[bi];
     const uint8_t *K = kSorted ? job.key + job.ws_off[bi] : nullptr;
-    const LevelCfg cfg = c_ct.cfg[job.level];
+    const LevelCfg cfg = job.cfg;
     const int64_t max_dist = job_win(job).max_dist;
     uint64_t st_lane_steps = 0, st_cmps = 0, st_walks = 0, st_wave_iters = 0;
 
@@ -1220,7 +1224,7 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
     const uint8_t *in = job.src + job.src_off[g];
     const uint32_t *rf = job.rfull + job.ws_off[bi];
     const uint32_t *rq = job.rquart + job.ws_off[bi];
-    const LevelCfg cfg = c_ct.cfg[job.level];
+    const LevelCfg cfg = job.cfg;
     const bool use_q = cfg.good < cfg.lazy;
     const bool filtered = job.strategy == 1;
     const uint32_t lazy = cfg.lazy, good = cfg.good;
@@ -1514,7 +1518,7 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
     uint32_t *stg = job.stage + job.ws_off[bi];
     uint32_t *sst = job.pstate + (job.ws_off[bi] >> 4);      // 2 bits per position
     BlockRec *blk = job.blocks + job.blk_off[bi];
-    const LevelCfg cfg = c_ct.cfg[job.level];
+    const LevelCfg cfg = job.cfg;
     const bool use_q = cfg.good < cfg.lazy;
     const bool filtered = job.strategy == 1;
 
@@ -1917,10 +1921,10 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     const WinP wp = job_win(job);
     const uint32_t hsize = wp.mask + 1;                  // hash_size = 1 << hash_bits
     uint32_t *head = heads + (size_t)bi * hsize;
-    const LevelCfg cfg = c_ct.cfg[job.level];
+    const LevelCfg cfg = job.cfg;
     // a resumed flush job (start > 0) finds head[] and prev[] as the last job
     // left them, rebased to its buffer (zgpu_api.cpp deflate_part)
-    if (!kEv || job.start == 0)
+    if (!kEv || job.start == 0 || job.dict)
         for (int i = lane; i < (int)hsize; i += 64) head[i] = 0;
     __threadfence_block();
     __syncthreads();
@@ -1982,6 +1986,11 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         return maxcmp;
     };
 
+    if (kEv && job.dict)                                  // a preset dictionary's strings
+        for (int64_t q = 0; q < (int64_t)job.pre_ins; q++) {
+            wsee(q);
+            insert(q);
+        }
     int64_t p = start, match_start = 0;
     uint32_t match_length = kMinMatch - 1;
     FlushEv fe = flush_ev(job);
@@ -2026,8 +2035,10 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         if (hh > po.S && p - hh <= wp.max_dist) {
             // longest_match (deflate.c:1356-1497), prev_length == 2: the first
             // candidate with the longest prefix wins, stop at nice, chain, limit
-            uint32_t chain = cfg.chain;
-            const int nice = lookahead < cfg.nice ? (int)lookahead : cfg.nice;
+            // prev_length stays MIN_MATCH-1 under deflate_fast: the budget is
+            // quartered only for a deflateTune good_length <= 2 (deflate.c:1390)
+            uint32_t chain = cfg.good <= kMinMatch - 1 ? cfg.chain >> 2 : cfg.chain;
+            const int nice = lookahead < (int64_t)cfg.nice ? (int)lookahead : (int)cfg.nice;
             const int64_t limit = (p - po.S) > wp.max_dist ? p - wp.max_dist : po.S;
             const int64_t rem = n - p;
             const int maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
@@ -2634,7 +2645,7 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         if (match_variant() != 14) hipLaunchKernelGGL(k_count, grid, dim3(kCntThreads), 0, st, job);
         break;
     case 1: {
-        const int wq = (int)(job.level >= 5);
+        const int wq = (int)(job.cfg.good < job.cfg.lazy);   // the parse reads rquart (prev_length >= good)
         const dim3 mgrid(job.seg ? job.nseg : job.count);   // per segment or per buffer
         const int v = match_variant();
         if (job.nfl && job.seg) {                               // a flush job (zgpu_api.cpp deflate())

@@ -28,7 +28,10 @@ constexpr int kMaxBits = 15, kMaxBLBits = 7;
 constexpr int kEndBlock = 256;
 
 // configuration_table (deflate.c:112-125)
-struct LevelCfg { uint16_t good, lazy, nice, chain; };
+// configuration_table (deflate.c:112-125) or deflateTune's values
+// (deflate.c:805-820); chain 0xffffffff: no budget (deflateTune's 0, which
+// longest_match's unsigned count never reaches again)
+struct LevelCfg { uint32_t good, lazy, nice, chain; };
 
 // Static code tables (RFC 1951 §3.2.5-3.2.6), derived on the host at init the
 // way tr_static_init (trees.c:303-396) derives them, copied to __constant__.
@@ -144,6 +147,15 @@ struct DeflateJob {
     // - 262, hash_shift = (hash_bits + 2) / 3, lit_bufsize = 1 << (memLevel + 6)
     // and the block cut at lit_bufsize - 1 symbols (deflate.c:440-455)
     int wbits, hbits;
+    // good_match, max_lazy_match, nice_match, max_chain_length of the job
+    // (the level's configuration_table row, or deflateTune's)
+    LevelCfg cfg;
+    // deflateSetDictionary (levels 1..3): the buffer starts with the
+    // dictionary, the parse at `start`; the hash chains start empty and
+    // positions [0, pre_ins) are inserted first (deflate.c deflateSetDictionary
+    // inserts all but the last two, which wait as s->insert)
+    int dict;
+    uint32_t pre_ins;
 };
 
 // the per-job window/hash parameters (deflate.c:440-455)
