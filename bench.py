@@ -399,11 +399,14 @@ def cpu_baselines(a, sample, want, level):
 
 # ------------------------------------------------------------------ reporting
 
-def pmc_traffic(kernel, tag):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+def pmc_traffic(kernels, tag):
+    """HBM bytes per launch of a leg from the committed rocprofv3 PMC passes
     (profiles/*_pmc_fetch_*.csv, *_pmc_write_*.csv; FETCH_SIZE doubled per the
     gfx950 streaming-read correction, units KiB).  Only for profiles taken on
-    this launch's shape (the file name carries the shape tag)."""
+    this launch's shape (the file name carries the shape tag).  `kernels`: the
+    name prefixes of the kernels one launch of the leg runs; for each, only the
+    dispatches with its largest grid (the leg's own launches, not the small
+    verification or trailer launches of the same kernel) are averaged."""
     import csv
     import glob
     fetch = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_fetch_*{tag}*.csv")))
@@ -412,9 +415,16 @@ def pmc_traffic(kernel, tag):
         return None, None
 
     def per_launch(path, counter):
-        vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-                if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]]
-        return sum(vals) / len(vals) * 1024.0 if vals else None
+        total = 0.0
+        rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
+        for k in kernels:
+            mine = [r for r in rows if r["Kernel_Name"].split("(")[0].replace("void ", "").startswith("zgpu::" + k)]
+            if not mine:
+                return None
+            g = max(int(r["Grid_Size"]) for r in mine)
+            vals = [float(r["Counter_Value"]) for r in mine if int(r["Grid_Size"]) == g]
+            total += sum(vals) / len(vals) * 1024.0
+        return total
 
     f = per_launch(fetch[-1], "FETCH_SIZE")
     w = per_launch(write[-1], "WRITE_SIZE")
@@ -435,7 +445,10 @@ def checksum_report(a, c, D, which, tag):
     alg = (c["n"] + 4) * c["B"]
     gbs = alg / (c["kernel_ms"] / 1e3) / 1e9
     kern = "k_crc32" if which == "crc32" else "k_adler32"
-    traffic, src = pmc_traffic(kern, tag)
+    # the kernels one launch runs: 16 lanes per buffer for C2's 1 M buffers;
+    # pieces + combine for the C5 leg's few large buffers (zgpu_checksum.hip)
+    parts = ["k_crc32s<16>"] if which == "crc32" else ["k_adler32_part", "k_adler32_fin"]
+    traffic, src = pmc_traffic(parts, tag)
     return {"value": round(tot / el / 1e9, 2), "unit": "GB/s",
             "roofline": {"bound": "hbm", "kernel": kern, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
@@ -512,7 +525,7 @@ def main(argv=None):
             alg_per_launch = per_step_alg / launches_per_step
             m_avg_ms = mms / max(1, mcount)
             achieved = alg_per_launch / (m_avg_ms / 1e3) / 1e9 if m_avg_ms > 0 else 0.0
-            m_traffic, m_src = pmc_traffic("k_match", f"L{a.level}_{launches_tag(a)}")
+            m_traffic, m_src = pmc_traffic(["k_match<"], f"L{a.level}_{launches_tag(a)}")
             roof = {"bound": "hbm", "kernel": "k_match",
                     "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 6),
