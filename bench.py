@@ -357,36 +357,47 @@ def _timed_threads(fn, sample, threads, seconds):
     return total / (time.perf_counter() - t0) / 1e6, total
 
 
+def progress(msg):
+    """A progress line on stderr (a long CPU or verification phase stays visibly alive)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_baselines(a, sample, want, level):
-    """Oracle port and system zlib on 1 thread and on all CPUs of the affinity
-    set (SURVEY §8(d) / BASELINE.md §3)."""
+    """Oracle port and system zlib on 1 thread and on all CPUs this process may
+    use: the affinity set, capped at the cgroup CPU quota when there is one
+    (more threads than the quota's CPUs share the same CPU time and only
+    stretch the run); SURVEY §8(d) / BASELINE.md §3."""
     import zlib
     from zhelpers import Oracle
     o = Oracle()
     host = host_info()
-    allt = a.cpu_threads or host["affinity_cpus"]
-    secs = a.cpu_seconds
-    port1, _ = _timed_threads(lambda b: o.compress(b, level), sample, 1, secs / 2)
-    portn, portn_b = _timed_threads(lambda b: o.compress(b, level), sample, allt, secs)
     quota = None
     try:
         q, per = host["cgroup_cpu_max"].split()
         quota = None if q == "max" else round(int(q) / int(per), 2)
     except (AttributeError, ValueError):
         pass
+    allt = a.cpu_threads or host["affinity_cpus"]
+    if not a.cpu_threads and quota:
+        allt = max(1, min(allt, int(quota + 0.999)))
+    secs = a.cpu_seconds
+    progress(f"cpu baseline: oracle port, 1 thread then {allt}")
+    port1, _ = _timed_threads(lambda b: o.compress(b, level), sample, 1, secs / 2)
+    portn, portn_b = _timed_threads(lambda b: o.compress(b, level), sample, allt, secs)
     cpu = {"value": round(portn, 2), "unit": "MB/s", "cores": allt, "kind": "port",
            "cpu_quota_cpus": quota,
            "per_core_1thread": round(port1, 2),
            "sample": f"{len(sample)} distinct {a.buffer_bytes} B {a.kind} buffers of this batch, "
                      f"compressed repeatedly at level {level} by oracle/liboracle.so: ~{secs / 2:.0f} s on "
                      f"1 thread, ~{secs:.0f} s ({portn_b / 1e6:.0f} MB) on {allt} threads "
-                     f"(every CPU of this process's affinity set)",
+                     f"(the CPUs this process may use: affinity set, cgroup quota)",
            "host": host}
     ok = all(zlib.compress(b, level) == z for b, z in zip(sample, want))
     if not ok:
         cpu["system_zlib"] = {"value": None, "version": zlib.ZLIB_RUNTIME_VERSION,
                               "note": "system zlib output differs from the reference stream; not timed"}
         return cpu
+    progress(f"cpu baseline: system zlib, 1 thread then {allt}")
     sys1, _ = _timed_threads(lambda b: zlib.compress(b, level), sample, 1, secs / 2)
     sysn, sysn_b = _timed_threads(lambda b: zlib.compress(b, level), sample, allt, secs)
     cpu["system_zlib"] = {
@@ -468,8 +479,11 @@ def main(argv=None):
     else:
         assert zgpu.load().zgpu_init() == 0, "libzgpu: GPU init failed"
         zgpu.set_inflight_bytes(a.inflight_mb << 20)
+        progress("deflate leg")
         d = deflate_leg(a, D)
+        progress("inflate leg")
         inf = None if a.no_inflate else inflate_leg(a, D, d)
+        progress("checksum legs")
         c = checksum_leg(a, D, "crc32")
         ad = checksum_leg(a, D, "adler32") if a.adler_buffers > 0 else None
 
@@ -490,6 +504,7 @@ def main(argv=None):
         idx = sorted(set(int(i) for i in torch.linspace(0, a.buffers - 1, a.verify).tolist())) \
             if a.verify > 0 else []
         for i in idx:
+            progress(f"verifying buffer {i} against the oracle")
             raw = d["src"][i * n:(i + 1) * n].cpu().numpy().tobytes()
             z = d["dst"][i * d["cap"]: i * d["cap"] + int(h_dlen[i])].cpu().numpy().tobytes()
             assert z == o.compress(raw, a.level)[1], f"buffer {i}: GPU stream != oracle"
