@@ -1,0 +1,45 @@
+"""deflate() driven through small output buffers and Z_NO_FLUSH input in
+pieces, on the GPU, against tests/golden/stream_golden.json: sessions run
+through the compiled reference (tests/golden/make_stream_golden.py,
+tests/zhelpers.run_dsession) -- zpipe.c-style loops and free call sequences
+at levels 1..9, every strategy, zlib/raw/gzip wrappers, windowBits and
+memLevel settings.  Every call's return code, the input it left unconsumed
+(avail_in) and the bytes it wrote must be the reference's (deflate.c:763-1265:
+need_more after a block when avail_out runs out, FLUSH_BLOCK), and so must the
+stream."""
+import hashlib
+import json
+import os
+
+import pytest
+
+import datagen
+from zhelpers import run_dsession
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def stream_golden():
+    with open(os.path.join(HERE, "golden", "stream_golden.json")) as f:
+        return json.load(f)["cases"]
+
+
+def test_stream_sessions_vs_reference(zg, stream_golden):
+    L = zg.load()
+    bad = []
+    for c in stream_golden:
+        if c["level"] == 0:
+            continue
+        print("case", c["kind"], c["n"], c["seed"], c["level"], flush=True)
+        data = datagen.make(c["kind"], c["n"], c["seed"])
+        plan = [tuple(p) for p in c["plan"]]
+        recs, whole = run_dsession(L, data, plan, c["level"], c["wbits"], c["mem"], c["strategy"])
+        recs = [list(r) for r in recs]
+        tag = (c["kind"], c["n"], c["level"], c["strategy"], c["wbits"], c["mem"])
+        if recs != c["recs"] or hashlib.sha256(whole).hexdigest() != c["sha256"]:
+            k = next((i for i, (a, b) in enumerate(zip(recs, c["recs"])) if a != b), min(len(recs), len(c["recs"])))
+            bad.append((tag, k, recs[k:k + 2], c["recs"][k:k + 2], len(recs), len(c["recs"])))
+    assert not bad, bad[:4]

@@ -468,3 +468,41 @@ def run_isession(L, z, wbits=15, dictionary=None, chunk=1 << 30, version=b"1.3.1
             break
     L.inflateEnd(C.byref(s))
     return rcs, bytes(out)
+
+
+def run_dsession(L, data, plan, level=6, wbits=15, mem=8, strategy=0, version=b"1.3.1.1-motley",
+                 max_calls=20000):
+    """deflate() over `data` on library L the way a caller with a fixed-size
+    output buffer drives it, recording what every call does.
+
+    plan: [(new_input, flush, avail_out, loop), ...].  Each entry offers
+    `new_input` more bytes (unconsumed input stays offered: next_in / avail_in
+    continue where the library left them) and calls deflate(flush) with
+    `avail_out` bytes of output space; with loop set it calls again (no new
+    input) while the call used up all of avail_out, as zpipe.c does.
+    Returns (records, stream): one (return code, avail_in after, bytes
+    written) per call."""
+    _bind_zstream(L)
+    s = ZStream()
+    rc = L.deflateInit2_(C.byref(s), level, 8, wbits, mem, strategy, version, C.sizeof(ZStream))
+    assert rc == 0, rc
+    ib = C.create_string_buffer(bytes(data), max(len(data), 1))
+    base = C.addressof(ib)
+    out, recs, offered = bytearray(), [], 0
+    ob = C.create_string_buffer(1 << 20)
+    for new, flush, avail, loop in plan:
+        offered = min(len(data), offered + new)
+        while True:
+            s.next_in = base + s.total_in
+            s.avail_in = offered - s.total_in
+            s.next_out, s.avail_out = C.addressof(ob), avail
+            r = L.deflate(C.byref(s), flush)
+            got = avail - s.avail_out
+            out.extend(ob.raw[:got])
+            recs.append((r, s.avail_in, got))
+            if len(recs) >= max_calls or not loop or r not in (0, -5) or s.avail_out != 0 or r == 1:
+                break
+        if len(recs) >= max_calls:
+            break
+    L.deflateEnd(C.byref(s))
+    return recs, bytes(out)

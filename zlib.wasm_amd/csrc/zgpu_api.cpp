@@ -24,6 +24,24 @@
 #include "../../include/zgpu_wasm.h"
 #include "../../include/zgpu_debug.h"
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
+// debug (ZGPU_SEGV_TRACE): a host backtrace of the library on SIGSEGV
+namespace {
+void segv_backtrace(int sig) {
+    void *a[64];
+    const int n = backtrace(a, 64);
+    backtrace_symbols_fd(a, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+__attribute__((constructor)) void install_segv_backtrace() {
+    if (std::getenv("ZGPU_SEGV_TRACE")) signal(SIGSEGV, segv_backtrace);
+}
+}  // namespace
+
 using namespace zgpu;
 
 namespace {
@@ -226,6 +244,7 @@ struct Ctx {
     DevBuf ws_help;           // the a18 helpers' staging (zlib_*_simd)
     DevBuf ws_seg;            // k_match segments of sub-batches of few large buffers
     DevBuf ws_ck;             // split checksum partials (few large buffers)
+    DevBuf ws_srec, ws_snap;  // a streaming job's block records and head[] snapshot
     // inflate: match records, per-stream results, checks, offsets, stop codes
     DevBuf ws_mrec, ws_irec, ws_ick, ws_imeta, ws_istop;
     hipStream_t aux = nullptr;
@@ -380,6 +399,15 @@ struct FlushSpec {
     uint32_t nplan;
     int dict;                      // DeflateJob::dict / pre_ins (a preset dictionary)
     uint32_t pre_ins;
+    // Z_NO_FLUSH stops (DeflateJob::mlim .. snap, fl_aux, device arrays)
+    const uint64_t *mlim;
+    uint32_t nmlim;
+    uint64_t *srec;
+    uint32_t *ev_blk;
+    uint32_t e0;
+    int cut;
+    uint32_t *snap;
+    const uint64_t *aux;
 };
 
 // deflateInit2_'s windowBits / memLevel rules (deflate.c:400-425): negative
@@ -592,6 +620,14 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.plan = fs->plan != nullptr;
             job.dict = fs->dict;
             job.pre_ins = fs->pre_ins;
+            job.mlim = fs->mlim;
+            job.nmlim = fs->nmlim;
+            job.srec = fs->srec;
+            job.ev_blk = fs->ev_blk;
+            job.e0 = fs->e0;
+            job.cut = fs->cut;
+            job.snap = fs->snap;
+            job.fl_aux = fs->aux;
         }
         return job;
     };
@@ -683,8 +719,23 @@ struct FlushHost {
     uint32_t nplan = 0;
     int dict = 0;                      // see FlushSpec
     uint32_t pre_ins = 0;
+    // Z_NO_FLUSH stops (events of kind 0): in, a job resumed at a block cut;
+    // out, the records (DeflateJob::srec), the records before each event, and
+    // for levels 1..3 head[] at the last cut with that record's index and the
+    // prev links of [its S, its end)
+    uint32_t e0 = 0;
+    int cut = 0;
+    const uint64_t *aux = nullptr;     // DeflateJob::fl_aux (pause events), n entries
+    std::vector<uint64_t> *rec_out = nullptr;
+    std::vector<uint32_t> *evb_out = nullptr;
+    std::vector<uint32_t> *snap_head = nullptr;
+    std::vector<uint16_t> *snap_prev = nullptr;
+    uint32_t snap_rec = 0xffffffffu;
 };
 
+// debug trace of the streaming deflate() engine (ZGPU_STREAM_TRACE)
+#define ZTRACE(...) do { static const bool on_ = std::getenv("ZGPU_STREAM_TRACE") != nullptr; \
+    if (on_) { std::fprintf(stderr, __VA_ARGS__); std::fflush(stderr); } } while (0)
 int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
                          size_t *dst_len, int *status, size_t count, int level, int wrap, int strategy,
                          FlushHost *fh = nullptr, int wbits = 15, int mem_level = 8,
@@ -702,7 +753,7 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
         dcap[i] = dst_len[i];
         out_total += (dst_len[i] + 15) & ~15ull;
     }
-    const size_t ev_bytes = fh ? 16ull * fh->n + 64 : 0;
+    const size_t ev_bytes = fh ? 32ull * fh->n + 160 : 0;
     const size_t meta_bytes = 8 * 4 * count + 16 * count + ev_bytes;
     if (!c.ws_io.ensure(in_total + 64) || !c.ws_io2.ensure(out_total + 64) ||
         !c.ws_small.ensure(meta_bytes + 64))
@@ -737,14 +788,70 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
             return ZGPU_MEM_ERROR;
         uint64_t *d_mb = d_fp + fh->n + (fh->n + 1) / 2;
         if (hipMemsetAsync(d_mb, 0, 32, st) != hipSuccess) return ZGPU_MEM_ERROR;
+        // k_match's clamps: the flush events only (not the Z_NO_FLUSH stops)
+        std::vector<uint64_t> ml;
+        for (uint32_t i = 0; i < fh->n; i++)
+            if (fh->type[i] != 0 && fh->type[i] != kEvPause) ml.push_back(fh->pos[i]);
+        uint64_t *d_ml = d_mb + 4;
+        uint64_t *d_aux = d_ml + fh->n;
+        uint32_t *d_evb = reinterpret_cast<uint32_t *>(d_aux + fh->n);
+        if (!ml.empty() && hipMemcpyAsync(d_ml, ml.data(), 8 * ml.size(), hipMemcpyHostToDevice, st) != hipSuccess)
+            return ZGPU_MEM_ERROR;
+        if (fh->n && hipMemsetAsync(d_evb, 0xff, 4ull * fh->n, st) != hipSuccess) return ZGPU_MEM_ERROR;
+        if (fh->aux && fh->n && hipMemcpyAsync(d_aux, fh->aux, 8ull * fh->n, hipMemcpyHostToDevice, st) != hipSuccess)
+            return ZGPU_MEM_ERROR;
         fs = FlushSpec{d_fp, d_ft, fh->n, fh->open_end, fh->start, fh->bit0, fh->byte0, d_mb,
-                       fh->head_in, fh->prev_in, fh->prev_n, fh->plan, fh->nplan, fh->dict, fh->pre_ins};
+                       fh->head_in, fh->prev_in, fh->prev_n, fh->plan, fh->nplan, fh->dict, fh->pre_ins,
+                       d_ml, (uint32_t)ml.size(), nullptr, d_evb, fh->e0, fh->cut, nullptr,
+                       fh->aux ? d_aux : nullptr};
+        if (fh->rec_out) {
+            const size_t sym_limit = (size_t(1) << (mem_level + 6)) - 1;         // lit_bufsize - 1
+            const size_t nrec = src_len[0] / sym_limit + 4 + 2ull * fh->n + fh->nplan;
+            if (!c.ws_srec.ensure(32 * nrec)) return ZGPU_MEM_ERROR;
+            fs.srec = c.ws_srec.as<uint64_t>();
+        }
+        if (fh->snap_head) {
+            const size_t hsize = size_t(1) << (mem_level + 7);
+            if (!c.ws_snap.ensure(4 * (hsize + 1)) ||
+                hipMemsetAsync(c.ws_snap.p, 0xff, 4 * (hsize + 1), st) != hipSuccess)
+                return ZGPU_MEM_ERROR;
+            fs.snap = c.ws_snap.as<uint32_t>();
+        }
     }
+    if (fh) ZTRACE("chl: launch n %u open %d\n", fh->n, fh->open_end);
     int rc = deflate_dev_locked(c, d_in, d_so, d_sl, d_out, d_do, d_dc, d_dl, d_st, (uint32_t)count,
                                 level, wrap, strategy, st, fh ? &fs : nullptr, wbits, mem_level, tune);
+    if (fh) ZTRACE("chl: ran rc %d\n", rc);
     if (rc) return rc;
     if (fh && copy_sync(fh->out, fs.out, 32, hipMemcpyDeviceToHost, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
+    if (fh && fh->rec_out) {
+        uint32_t nb = 0;
+        if (copy_sync(&nb, c.ws_meta.as<uint64_t>() + 2, 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+            return ZGPU_MEM_ERROR;
+        ZTRACE("chl: nb %u\n", nb);
+        fh->rec_out->resize(4ull * nb);
+        fh->evb_out->resize(fh->n);
+        if ((nb && copy_sync(fh->rec_out->data(), fs.srec, 32ull * nb, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+            (fh->n && copy_sync(fh->evb_out->data(), fs.ev_blk, 4ull * fh->n, hipMemcpyDeviceToHost, st) != hipSuccess))
+            return ZGPU_MEM_ERROR;
+        fh->snap_rec = 0xffffffffu;
+        if (fh->snap_head) {
+            const size_t hsize = size_t(1) << (mem_level + 7);
+            uint32_t k = 0xffffffffu;
+            if (copy_sync(&k, fs.snap + hsize, 4, hipMemcpyDeviceToHost, st) != hipSuccess) return ZGPU_MEM_ERROR;
+            if (k < nb) {
+                const uint64_t S = (*fh->rec_out)[4ull * k + 2] >> 32, x = (*fh->rec_out)[4ull * k + 2] & 0xffffffffu;
+                fh->snap_head->resize(hsize);
+                fh->snap_prev->resize(x > S ? x - S : 0);
+                if (copy_sync(fh->snap_head->data(), fs.snap, 4ull * hsize, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                    (x > S && copy_sync(fh->snap_prev->data(), c.ws_link.as<uint16_t>() + S, 2 * (x - S),
+                                        hipMemcpyDeviceToHost, st) != hipSuccess))
+                    return ZGPU_MEM_ERROR;
+                fh->snap_rec = k;
+            }
+        }
+    }
     if (fh && fh->head_out && fh->n) {
         const uint64_t S = fh->out[2], end = fh->pos[fh->n - 1];
         const size_t hsize = size_t(1) << (mem_level + 7);
@@ -1374,10 +1481,21 @@ void zgpu_zcfree(voidpf, voidpf ptr) { std::free(ptr); }
 
 // z_stream deflate: gather input, compress on the GPU at a flush call or at
 // Z_FINISH, drain.
+// one step of a streaming deflate job's timeline (see deflate_part)
+struct StreamItem {
+    uint64_t end_bit;        // part output bit after it
+    uint64_t in_end, S, E;   // part positions: where it ends, the window offset, fill_window's end of input read
+    uint32_t ev;             // a stop's or marker's event index (internal_state::ev_*), else ~0u
+    uint32_t rec;            // the job's record index (blocks, markers)
+    uint8_t kind, pbyte, res;
+};
+enum : uint8_t { kItStop = 0, kItBlock = 1, kItMarker = 2, kItFinal = 3 };
+
 struct internal_state {
     ZAlloc<uint8_t> al;
     explicit internal_state(const ZAlloc<uint8_t> &a = {})
-        : al(a), in(a), out(a), ev_pos(a), ev_type(a), fast_head(a), fast_prev(a), hist(a) {}
+        : al(a), in(a), out(a), ev_pos(a), ev_type(a), ev_aux(a), fast_head(a), fast_prev(a), hist(a), body(a),
+          items(ZAlloc<StreamItem>(a)), evb(ZAlloc<uint32_t>(a)) {}
     int level, wrap, strategy;
     zvec<uint8_t> in, out;          // deflate: the input since the last Z_FULL_FLUSH; output queue
     size_t out_pos;
@@ -1391,8 +1509,8 @@ struct internal_state {
     bool header_done = false;
     zvec<uint64_t> ev_pos;          // the current part's flush calls (part-relative)
     zvec<uint32_t> ev_type;
+    zvec<uint64_t> ev_aux;          // kEvPause events: the end of the block the call stopped after
     size_t part_out = 0;            // bytes of the current part already queued
-    bool marker_due = false;        // the last flush call ran out of output before its marker
     size_t in_base = 0;             // part position of in[0] (input behind the resume point is dropped)
     uint32_t check = 0;             // adler32 / crc32 of the stream's input before ck_pos
     size_t ck_pos = 0;              // part position the running check has reached
@@ -1409,8 +1527,6 @@ struct internal_state {
     // part positions, prev links of [res_S, res_pos)) and as the last job left them
     zvec<uint32_t> fast_head;
     zvec<uint16_t> fast_prev;
-    std::vector<uint32_t> job_head;   // what the last job left (scratch of one call)
-    std::vector<uint16_t> job_prev;
     // inflate streams
     int inflating = 0;
     int wbits = 15;         // deflate: w_bits (9..15); inflate: inflateInit2_'s windowBits
@@ -1432,6 +1548,31 @@ struct internal_state {
     // deflateTune (deflate.c:805-820): the jobs' good/lazy/nice/chain
     bool tuned = false;
     LevelCfg tune{};
+    // the timeline of the last streaming job (deflate_part): its output bytes
+    // from part byte body_at on, its items, the next one to hand out (t) and
+    // the one the resume point stands at (res_item, -1: before the first)
+    zvec<uint8_t> body;
+    size_t body_at = 0;
+    std::vector<StreamItem, ZAlloc<StreamItem>> items;
+    size_t t = 0;
+    long res_item = -1;
+    zvec<uint32_t> evb;                  // per event from job_ev on: the job's records before it
+    size_t job_ev = 0;                   // the last job's first event
+    bool trailer_due = false;            // Z_FINISH: the last block is out, the trailer not yet queued
+    bool stale = true;                   // events changed since the last job
+    bool job_closed = false;             // the last job ran to Z_FINISH
+    bool tentative = false;              // the last event is a stop its call did not reach
+    size_t rd = 0;                       // part position the reference's fill_window has read up to
+    size_t rd_seen = 0;                  // ... as next_in / total_in show it
+    size_t ev_done = 0;                  // events whose call got to them (stop reached, marker handed out)
+    size_t flush_done = 0;               // part position of the last flush handed out
+    uint64_t proc_bits = 0;              // part output bit after the last item handed out
+    uint64_t res_E = 0;                  // the resume point's E (fill_window's end of input read)
+    int res_cut = 0;                     // the resume point is a block cut (not a flush)
+    size_t job_base = 0;                 // res_S of the last job (snapshots are relative to it)
+    uint32_t snap_rec = 0xffffffffu;     // levels 1..3: the record whose head[] the last job kept
+    std::vector<uint32_t> snap_head;
+    std::vector<uint16_t> snap_prev;
     const gz_header *gzhead = nullptr;   // deflateSetHeader: written by the first deflate() call
     bool dict_set = false;               // deflateSetDictionary: the zlib header's FDICT + DICTID
     uint32_t dict_id = 0;
@@ -1493,32 +1634,61 @@ int deflateInit_(z_streamp strm, int level, const char *version, int stream_size
 }
 
 namespace {
-// deflate(flush) calls: the current part from its resume point up to the end
-// of the input given so far, compressed with the flush calls since then as a
-// raw stream; open_end: it stops after the last flush (complete bytes only).
-// body[0] is the part's output byte res_bits / 8; out as FlushHost::out.
-int deflate_part(internal_state *s, int open_end, std::vector<uint8_t> &body, uint64_t *out) {
+// ---------------------------------------------------------------------------
+// Streaming deflate() at levels 1..9.  Every call that offers input or asks
+// for a flush records an event: the end of the input it offers and its flush
+// kind (0: Z_NO_FLUSH).  A job compresses the current part (the input since
+// the last Z_FULL_FLUSH) from its resume point, with every event since, as
+// one raw stream on the GPU: the parse stands still at each Z_NO_FLUSH call's
+// need_more point and acts on each flush there, as deflate_slow /
+// deflate_fast / deflate_rle / deflate_huff do.  It returns a timeline: its
+// blocks and markers with the output bit after each and the input
+// fill_window had read when each was flushed, and its stops.  deflate() hands
+// out what the reference's call hands out -- every block flushed before the
+// call's own stop, marker or final block -- and pauses after a block when
+// avail_out is used up (FLUSH_BLOCK's need_more, deflate.c:1685-1690), having
+// consumed only the input read by then.  A later job resumes at the last
+// block cut handed out whose state a new job starts in (the lazy parse's
+// simple state; for levels 1..3 with head[] as it stood there).
+// ---------------------------------------------------------------------------
+int deflate_part(internal_state *s, bool closed) {
+    // a pause at the block the resume point stands at is behind it already
+    while (s->res_ev < s->ev_pos.size() && s->ev_type[s->res_ev] == kEvPause && s->ev_aux[s->res_ev] <= s->res_pos)
+        s->res_ev++;
     const size_t base = s->res_S, nev = s->ev_pos.size() - s->res_ev;
-    std::vector<uint64_t> pos(nev + 1);
-    for (size_t i = 0; i < nev; i++) pos[i] = s->ev_pos[s->res_ev + i] - base;
+    std::vector<uint64_t> pos(nev + 1), aux(nev + 1, 0);
+    for (size_t i = 0; i < nev; i++) {
+        pos[i] = s->ev_pos[s->res_ev + i] - base;
+        if (s->ev_type[s->res_ev + i] == kEvPause) aux[i] = s->ev_aux[s->res_ev + i] - base;
+    }
     const uint8_t *sp = s->in.data() + (base - s->in_base);
     size_t sl = s->in_base + s->in.size() - base;
-    size_t cap = (size_t)compress_bound64(sl) + 64 + 16ull * nev;
-    body.resize(cap);
-    uint8_t *dp = body.data();
+    // any windowBits / memLevel: blocks may be fixed-code where stored would
+    // not fit the window (up to 9 bits a literal), plus headers and markers
+    size_t cap = sl + (sl >> 2) + 1024 + 16ull * nev;
+    s->body.resize(cap);
+    uint8_t *dp = s->body.data();
     int st = 0;
-    FlushHost fh{pos.data(), s->ev_type.data() + s->res_ev, (uint32_t)nev, open_end, (uint32_t)(s->res_pos - base),
-                 (uint32_t)(s->res_bits & 7), s->res_byte & ((1u << (s->res_bits & 7)) - 1u), {0, 0, 0, 0}};
+    FlushHost fh{pos.data(), s->ev_type.data() + s->res_ev, (uint32_t)nev, closed ? 0 : 1,
+                 (uint32_t)(s->res_pos - base), (uint32_t)(s->res_bits & 7),
+                 s->res_byte & ((1u << (s->res_bits & 7)) - 1u), {0, 0, 0, 0}};
+    fh.e0 = s->res_E > base ? (uint32_t)(s->res_E - base) : 0;
+    fh.cut = s->res_cut;
+    fh.aux = aux.data();
+    std::vector<uint64_t> rec;
+    std::vector<uint32_t> evb;
+    fh.rec_out = &rec;
+    fh.evb_out = &evb;
     std::vector<uint32_t> head_in;
-    if (s->level >= 1 && s->level <= 3 && s->strategy != Z_HUFFMAN_ONLY && s->strategy != Z_RLE &&
-        s->res_pos > base && s->fast_head.empty()) {
+    const bool fast = s->level >= 1 && s->level <= 3 && s->strategy != Z_HUFFMAN_ONLY && s->strategy != Z_RLE;
+    if (fast && s->res_pos > base && s->fast_head.empty()) {
         // the part starts with a preset dictionary: its strings are inserted
         // first, all but the last two (deflateSetDictionary, deflate.c)
         const uint32_t d = (uint32_t)(s->res_pos - base);
         fh.dict = 1;
         fh.pre_ins = d >= kMinMatch ? d - (kMinMatch - 1) : 0;
     }
-    if (s->level >= 1 && s->level <= 3 && s->strategy != Z_HUFFMAN_ONLY && s->strategy != Z_RLE) {
+    if (fast) {
         if (s->res_pos > base && !fh.dict) {                   // rebase the saved chains to this buffer
             head_in.resize(s->fast_head.size());
             for (size_t i = 0; i < head_in.size(); i++)
@@ -1527,22 +1697,99 @@ int deflate_part(internal_state *s, int open_end, std::vector<uint8_t> &body, ui
             fh.prev_in = s->fast_prev.data();
             fh.prev_n = s->fast_prev.size();
         }
-        fh.head_out = &s->job_head;
-        fh.prev_out = &s->job_prev;
+        fh.snap_head = &s->snap_head;
+        fh.snap_prev = &s->snap_prev;
     }
-    Lease L;
-    int rc = L.rc;
-    if (!rc) rc = compress_host_locked(*L.c, &sp, &sl, &dp, &cap, &st, 1, s->level, ZGPU_WRAP_RAW, s->strategy, &fh,
-                                       s->wbits, s->mem_level, s->tuned ? &s->tune : nullptr);
-    if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
-    body.resize(cap);
-    for (int i = 0; i < 4; i++) out[i] = fh.out[i];
+    ZTRACE("part: base %zu nev %zu sl %zu cap %zu start %u bit0 %u e0 %u cut %d fast %d\n", base, nev, sl, cap,
+           fh.start, fh.bit0, fh.e0, fh.cut, (int)fast);
+    {
+        Lease L;
+        int rc = L.rc;
+        if (!rc) rc = compress_host_locked(*L.c, &sp, &sl, &dp, &cap, &st, 1, s->level, ZGPU_WRAP_RAW, s->strategy,
+                                           &fh, s->wbits, s->mem_level, s->tuned ? &s->tune : nullptr);
+        ZTRACE("part: rc %d st %d out %zu recs %zu evb %zu snap %u\n", rc, st, cap, rec.size() / 4, evb.size(),
+               fh.snap_rec);
+        if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
+    }
+    s->body.resize(cap);
+    s->body_at = (size_t)(s->res_bits >> 3);
+    s->job_base = base;
+    s->snap_rec = fast ? fh.snap_rec : 0xffffffffu;
+    // the timeline: records in order, each stop before the first record
+    // flushed after it, each flush event's marker as its record
+    const uint32_t nb = (uint32_t)(rec.size() / 4);
+    const uint64_t bit0 = (uint64_t)s->body_at << 3;
+    {
+        // what the device reported must describe this job's input and output
+        uint64_t lb = s->res_bits & 7, le = 0;
+        bool ok = evb.size() == nev;
+        for (uint32_t j = 0; ok && j < nb; j++) {
+            const uint64_t eb = rec[4ull * j], x = rec[4ull * j + 2] & 0xffffffffu, S = rec[4ull * j + 2] >> 32,
+                           E = rec[4ull * j + 3] & 0xffffffffu;
+            ok = eb >= lb && eb <= 8ull * cap + 7 && x >= le && x <= sl && S <= x && E >= x && E <= sl;
+            if (!ok) ZTRACE("part: bad record %u: bit %lu (last %lu, cap %zu) end %lu (last %lu) S %lu E %lu sl %zu\n",
+                            j, (unsigned long)eb, (unsigned long)lb, cap, (unsigned long)x, (unsigned long)le,
+                            (unsigned long)S, (unsigned long)E, sl);
+            lb = eb;
+            le = x;
+        }
+        for (size_t i = 0; ok && i < nev; i++) ok = evb[i] <= nb || evb[i] == 0xffffffffu;
+        if (!ok) {
+            ZTRACE("part: bad job (nb %u nev %zu evb %zu)\n", nb, nev, evb.size());
+            return Z_STREAM_ERROR;
+        }
+    }
+    s->items.clear();
+    uint64_t last_bit = s->res_bits;
+    size_t e = 0;
+    for (uint32_t j = 0;; j++) {
+        while (e < nev && evb[e] == j && (s->ev_type[s->res_ev + e] == 0 || s->ev_type[s->res_ev + e] == kEvPause)) {
+            if (s->ev_type[s->res_ev + e] == kEvPause) {        // no item: the next fill reads further
+                e++;
+                continue;
+            }
+            StreamItem it{};
+            it.kind = kItStop;
+            it.end_bit = last_bit;
+            it.in_end = it.E = s->ev_pos[s->res_ev + e];
+            it.ev = (uint32_t)(s->res_ev + e);
+            it.rec = ~0u;
+            s->items.push_back(it);
+            e++;
+        }
+        if (j == nb) break;
+        StreamItem it{};
+        it.end_bit = bit0 + rec[4ull * j];
+        it.pbyte = (uint8_t)rec[4ull * j + 1];
+        it.in_end = base + (rec[4ull * j + 2] & 0xffffffffu);
+        it.S = base + (rec[4ull * j + 2] >> 32);
+        it.E = base + (rec[4ull * j + 3] & 0xffffffffu);
+        it.res = (uint8_t)(rec[4ull * j + 3] >> 63);
+        it.rec = j;
+        it.ev = ~0u;
+        if (e < nev && evb[e] == j) {
+            it.kind = kItMarker;
+            it.ev = (uint32_t)(s->res_ev + e);
+            e++;
+        } else {
+            it.kind = closed && j + 1 == nb ? kItFinal : kItBlock;
+        }
+        s->items.push_back(it);
+        last_bit = it.end_bit;
+    }
+    ZTRACE("part: items %zu\n", s->items.size());
+    s->evb.assign(evb.begin(), evb.end());
+    s->job_ev = s->res_ev;
+    s->job_closed = closed;
+    s->stale = false;
+    // the items before the resume point were handed out by earlier calls
+    s->t -= (size_t)(s->res_item + 1);
+    s->res_item = -1;
     return Z_OK;
 }
 
-// the running Adler-32 / CRC-32 up to the end of the input given so far
-void advance_check(internal_state *s) {
-    const size_t end = s->in_base + s->in.size();
+// the running Adler-32 / CRC-32 up to part position `end`
+void advance_check(internal_state *s, size_t end) {
     if (!s->wrap || s->ck_pos >= end) return;
     const uint8_t *p = s->in.data() + (s->ck_pos - s->in_base);
     const size_t n = end - s->ck_pos;
@@ -1557,14 +1804,65 @@ void close_part(internal_state *s) {
     s->ck_pos = 0;
     s->ev_pos.clear();
     s->ev_type.clear();
+    s->ev_aux.clear();
+    s->evb.clear();
+    s->job_ev = 0;
+    s->trailer_due = false;
     s->part_out = 0;
     s->res_S = s->res_pos = s->res_ev = 0;
     s->res_bits = 0;
     s->res_byte = 0;
+    s->res_E = 0;
+    s->res_cut = 0;
     s->fast_head.clear();
     s->fast_prev.clear();
-    s->job_head.clear();
-    s->job_prev.clear();
+    s->items.clear();
+    s->t = 0;
+    s->res_item = -1;
+    s->stale = true;
+    s->tentative = false;
+    s->rd = s->rd_seen = 0;
+    s->ev_done = 0;
+    s->flush_done = 0;
+    s->proc_bits = 0;
+    s->body.clear();
+    s->body_at = 0;
+}
+
+// after a call: the latest item handed out that a new job can start at
+void choose_resume(internal_state *s) {
+    const bool fast = s->level >= 1 && s->level <= 3 && s->strategy != Z_HUFFMAN_ONLY && s->strategy != Z_RLE;
+    for (long r = (long)s->t - 1; r > s->res_item; r--) {
+        const StreamItem &it = s->items[(size_t)r];
+        if (it.kind == kItStop || it.kind == kItFinal || !it.res) continue;
+        if (fast && it.rec != s->snap_rec) continue;
+        s->res_S = it.S;
+        s->res_pos = it.in_end;
+        s->res_bits = it.end_bit;
+        s->res_byte = it.pbyte;
+        s->res_E = it.E;
+        s->res_cut = it.kind == kItBlock;
+        // the events after it: a stop or marker comes after record `rec` when
+        // its record index is above it; a pause applies after the record before
+        // its index, so one at this record is behind the resume point already
+        s->res_ev = s->ev_pos.size();
+        for (size_t k = s->job_ev; k < s->ev_pos.size() && k - s->job_ev < s->evb.size(); k++) {
+            const uint32_t b = s->evb[k - s->job_ev];
+            if (b > it.rec + (s->ev_type[k] == kEvPause ? 1u : 0u)) { s->res_ev = k; break; }
+        }
+        if (fast) {
+            const uint32_t b = (uint32_t)s->job_base;
+            s->fast_head.resize(s->snap_head.size());
+            for (size_t i = 0; i < s->snap_head.size(); i++) s->fast_head[i] = s->snap_head[i] ? s->snap_head[i] + b : 0;
+            s->fast_prev.assign(s->snap_prev.begin(), s->snap_prev.end());
+        }
+        if (s->res_S > s->in_base) {                 // the input before the window is not needed again
+            s->in.erase(s->in.begin(), s->in.begin() + (std::ptrdiff_t)(s->res_S - s->in_base));
+            s->in_base = s->res_S;
+        }
+        s->res_item = r;
+        return;
+    }
 }
 
 void queue_header(internal_state *s) {                          // deflate.c:1002-1073
@@ -1618,7 +1916,7 @@ void queue_header(internal_state *s) {                          // deflate.c:100
 bool pending_input(const internal_state *s) {
     if (s->last_flush == -2 || s->finished) return false;
     if (s->level == 0) return !s->in.empty();
-    return s->in_base + s->in.size() > s->res_pos || s->marker_due;
+    return s->in_base + s->in.size() > s->flush_done || s->ev_done < s->ev_type.size() || s->t < s->items.size();
 }
 
 void drain(z_streamp strm, internal_state *s) {
@@ -1657,7 +1955,7 @@ int deflate_stored_call(z_streamp strm, internal_state *s, int flush) {
         strm->next_in += strm->avail_in;
         strm->avail_in = 0;
     }
-    advance_check(s);
+    advance_check(s, s->in_base + s->in.size());
     std::vector<BlockRec> plan;
     size_t off = 0, total = s->in.size();
     bool last = false;
@@ -1729,71 +2027,113 @@ int deflate_stored_call(z_streamp strm, internal_state *s, int flush) {
     return s->out_pos == s->out.size() ? Z_STREAM_END : Z_OK;
 }
 
-// A flush call whose event is the last of s->ev_*: its blocks and marker are
-// queued.  zlib writes the blocks first and returns need_more when the output
-// space runs out at a block (deflate.c:1685-1690 FLUSH_BLOCK); the marker
-// follows only in a call that got past the last block (the zlib.h contract
-// repeats the flush call while avail_out == 0) -- and a call that ends with
-// avail_out == 0 after the marker makes the next one append another
-// (zlib.h: "avail_out is greater than six to avoid repeated flush markers").
-int emit_flush(z_streamp strm, internal_state *s, int flush) {
-    std::vector<uint8_t> body;
-    uint64_t o[4];
-    if (int rc = deflate_part(s, 1, body, o)) return rc;
-    queue_header(s);
-    const size_t jb = (size_t)(s->res_bits >> 3);             // part byte of body[0]
-    const uint64_t queued = strm->total_out + (s->out.size() - s->out_pos);
-    const uint64_t cap = strm->total_out + strm->avail_out;
-    const size_t q_last = jb + (size_t)(o[0] >> 3);           // complete bytes before the marker
-    auto queue = [&](size_t to) {                              // part bytes [part_out, to)
-        s->out.insert(s->out.end(), body.begin() + (std::ptrdiff_t)(s->part_out - jb),
-                      body.begin() + (std::ptrdiff_t)(to - jb));
-        s->part_out = to;
-    };
-    if (q_last > s->part_out && queued - s->part_out + q_last >= cap) {
-        queue(q_last);
-        s->marker_due = true;
-        drain(strm, s);
-        s->last_flush = -1;
-        return Z_OK;
-    }
-    queue(jb + body.size());
-    advance_check(s);
-    if (s->wrap) strm->adler = s->check;
-    if (flush == Z_FULL_FLUSH) {
-        close_part(s);
+// part output bytes [part_out, to) of the last job into the output queue
+void queue_to(internal_state *s, size_t to) {
+    if (to <= s->part_out) return;
+    s->out.insert(s->out.end(), s->body.begin() + (std::ptrdiff_t)(s->part_out - s->body_at),
+                  s->body.begin() + (std::ptrdiff_t)(to - s->body_at));
+    s->part_out = to;
+}
+
+// the input the reference has read by now (s->rd) out of next_in / avail_in
+void sync_input(z_streamp strm, internal_state *s) {
+    if (s->rd <= s->rd_seen) return;
+    const size_t d = s->rd - s->rd_seen;
+    strm->next_in += d;
+    strm->avail_in -= (uInt)d;
+    strm->total_in += d;
+    s->rd_seen = s->rd;
+}
+
+void queue_trailer(z_streamp strm, internal_state *s) {        // deflate.c:1236-1262
+    if (!s->wrap) return;
+    advance_check(s, s->in_base + s->in.size());
+    const uint32_t ck = s->check;
+    strm->adler = ck;
+    if (s->wrap == 1) {
+        for (int i = 3; i >= 0; i--) s->out.push_back((uint8_t)(ck >> (8 * i)));
     } else {
-        // the next job resumes here; the input before the window offset is not needed again
-        if (!s->job_head.empty()) {                            // levels 1..3: keep the chains
-            const uint32_t base = (uint32_t)s->res_S;
-            s->fast_head.resize(s->job_head.size());
-            for (size_t i = 0; i < s->job_head.size(); i++) s->fast_head[i] = s->job_head[i] ? s->job_head[i] + base : 0;
-            s->fast_prev.assign(s->job_prev.begin(), s->job_prev.end());
-            s->job_prev.clear();
-            s->job_head.clear();
+        const uint32_t isz = (uint32_t)strm->total_in;
+        for (int i = 0; i < 4; i++) s->out.push_back((uint8_t)(ck >> (8 * i)));
+        for (int i = 0; i < 4; i++) s->out.push_back((uint8_t)(isz >> (8 * i)));
+    }
+}
+
+// Hands out the timeline from s->t on, as the reference's call does, until
+// the call's own event `own` (its stop or its marker; ~0u: Z_FINISH, the
+// final block) or until avail_out is used up after a block.  *full: a
+// Z_FULL_FLUSH marker was handed out (the part ends).
+int run_items(z_streamp strm, internal_state *s, uint32_t own, bool *full) {
+    while (s->t < s->items.size()) {
+        const StreamItem it = s->items[s->t];
+        s->t++;
+        if (it.kind == kItStop) {                 // need_more (deflate.c:1941-1944)
+            s->rd = it.E;
+            if (it.ev == own) {
+                s->ev_done = own + 1;
+                s->tentative = false;
+                return Z_OK;
+            }
+            continue;
         }
-        s->res_S += (size_t)o[2];
-        s->res_pos = s->ev_pos.back();
-        s->res_ev = s->ev_pos.size();
-        s->res_bits = ((uint64_t)jb << 3) + o[1];
-        s->res_byte = (uint32_t)o[3];
-        if (s->res_S > s->in_base) {
-            s->in.erase(s->in.begin(), s->in.begin() + (std::ptrdiff_t)(s->res_S - s->in_base));
-            s->in_base = s->res_S;
+        if (it.E > s->rd) s->rd = it.E;
+        s->proc_bits = it.end_bit;
+        if (it.kind == kItFinal) {                // FLUSH_BLOCK(s, 1), then the trailer
+            queue_to(s, s->body_at + s->body.size());
+            s->rd = s->in_base + s->in.size();
+            sync_input(strm, s);
+            s->finished = 1;
+            drain(strm, s);
+            if (strm->avail_out == 0) {           // finish_started: the trailer comes with a later call
+                s->trailer_due = true;
+                s->last_flush = -1;
+                return Z_OK;
+            }
+            queue_trailer(strm, s);               // finish_done (deflate.c:1236-1262)
+            drain(strm, s);
+            return s->out_pos == s->out.size() ? Z_STREAM_END : Z_OK;
+        }
+        queue_to(s, (size_t)(it.end_bit >> 3));
+        drain(strm, s);
+        if (it.kind == kItMarker) {               // block_done: the flush's marker (deflate.c:1211-1233)
+            s->rd = it.in_end;
+            if (it.ev != own) continue;           // an earlier flush left without bits (Z_BLOCK)
+            s->ev_done = own + 1;
+            s->flush_done = it.in_end;
+            *full = s->ev_type[own] == Z_FULL_FLUSH;
+            if (strm->avail_out == 0) s->last_flush = -1;
+            return Z_OK;
+        }
+        if (strm->avail_out == 0) {               // FLUSH_BLOCK's need_more (deflate.c:1685-1690)
+            s->last_flush = -1;
+            if (own != ~0u && s->ev_type[own] == 0) s->tentative = true;
+            return Z_OK;
         }
     }
-    drain(strm, s);
-    if (strm->avail_out == 0) s->last_flush = -1;
     return Z_OK;
 }
 }  // namespace
+
+static void stream_trace(const char *where, z_streamp strm, const internal_state *s, int flush) {
+    static const bool on = std::getenv("ZGPU_STREAM_TRACE") != nullptr;   // debug
+    if (!on) return;
+    std::fprintf(stderr, "[%s] flush %d in %u out %u total_in %lu rd %zu seen %zu C %zu in_base %zu ev %zu done %zu "
+                 "items %zu t %zu res_item %ld res_S %zu res_pos %zu part_out %zu body_at %zu body %zu q %zu/%zu\n",
+                 where, flush, strm->avail_in, strm->avail_out, (unsigned long)strm->total_in, s->rd, s->rd_seen,
+                 s->in_base + s->in.size(), s->in_base, s->ev_pos.size(), s->ev_done, s->items.size(), s->t,
+                 s->res_item, s->res_S, s->res_pos, s->part_out, s->body_at, s->body.size(), s->out_pos, s->out.size());
+}
 
 static int deflate_body(z_streamp strm, int flush) {
     if (!strm || !strm->state || strm->state->inflating || flush < 0 || flush > Z_BLOCK) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
     if (!strm->next_out || (strm->avail_in && !strm->next_in) || (s->finished && flush != Z_FINISH))
         return Z_STREAM_ERROR;
-    const bool is_flush = flush != Z_NO_FLUSH && flush != Z_FINISH;
+    if (s->job_closed && flush != Z_FINISH) {
+        // zlib.h: after Z_FINISH, deflate() is called with Z_FINISH until Z_STREAM_END
+        strm->msg = const_cast<char *>("deflate: Z_FINISH is pending, call with Z_FINISH until Z_STREAM_END");
+        return Z_STREAM_ERROR;
+    }
     if (strm->avail_out == 0) return Z_BUF_ERROR;
     const int old_flush = s->last_flush;
     s->last_flush = flush;
@@ -1808,78 +2148,157 @@ static int deflate_body(z_streamp strm, int flush) {
     }
     if (s->finished && strm->avail_in) return Z_BUF_ERROR;
     if (s->level == 0) return deflate_stored_call(strm, s, flush);
-    if (s->marker_due) {
-        // the previous flush call cut its block but ran out of output before
-        // the marker: a flush call with no input completes it with its own
-        // kind; anything else leaves the cut without a marker (Z_BLOCK's)
-        s->marker_due = false;
-        if (!strm->avail_in && is_flush) {
-            s->ev_type.back() = (uint32_t)flush;
-            return emit_flush(strm, s, flush);
+    if (s->finished) {                                          // FINISH_STATE
+        if (s->trailer_due) {
+            s->trailer_due = false;
+            queue_trailer(strm, s);
+            drain(strm, s);
+            return s->out_pos == s->out.size() ? Z_STREAM_END : Z_OK;
         }
-        s->ev_type.back() = Z_BLOCK;
+        return Z_STREAM_END;
     }
-    if (strm->avail_in) {
-        if ((uint64_t)s->in.size() + strm->avail_in >= kMaxBuffer) return Z_MEM_ERROR;   // 32-bit kernel positions
-        s->in.insert(s->in.end(), strm->next_in, strm->next_in + strm->avail_in);
-        strm->total_in += strm->avail_in;
-        strm->next_in += strm->avail_in;
-        strm->avail_in = 0;
+    const size_t C = s->in_base + s->in.size();                // part position of the input copied so far
+    const size_t P = s->rd + strm->avail_in;                   // the input this call offers ends here
+    if (P > C && (uint64_t)(P - s->in_base) >= kMaxBuffer) return Z_MEM_ERROR;   // 32-bit kernel positions
+
+    // the first call asks for Z_FINISH with everything: one batch job, when
+    // its output fits (otherwise the timeline below pauses like zlib)
+    if (flush == Z_FINISH && !s->header_done && !s->flushed && C == 0) {
+        size_t cap = (size_t)strm->avail_in + (strm->avail_in >> 2) + 1024;   // any windowBits / memLevel
+        std::vector<uint8_t> tmp(cap);
+        const uint8_t *sp = strm->next_in;
+        uint8_t *dp = tmp.data();
+        size_t sl = strm->avail_in;
+        int st = 0;
+        int rc;
+        {
+            Lease L;
+            rc = L.rc;
+            if (!rc) rc = compress_host_locked(*L.c, &sp, &sl, &dp, &cap, &st, 1, s->level, s->wrap, s->strategy,
+                                               nullptr, s->wbits, s->mem_level, s->tuned ? &s->tune : nullptr);
+        }
+        if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
+        if (cap <= strm->avail_out) {
+            std::memcpy(strm->next_out, tmp.data(), cap);
+            strm->next_out += cap;
+            strm->avail_out -= (uInt)cap;
+            strm->total_out += cap;
+            strm->adler = s->wrap == 2 ? crc32_z(0, sp, sl) : (s->wrap == 1 ? adler32_z(1, sp, sl) : strm->adler);
+            strm->next_in += sl;
+            strm->total_in += sl;
+            strm->avail_in = 0;
+            s->header_done = true;
+            s->finished = 1;
+            return Z_STREAM_END;
+        }
     }
-    if (is_flush) {
-        s->flushed = true;
-        s->ev_pos.push_back(s->in_base + s->in.size());
-        s->ev_type.push_back((uint32_t)flush);
-        return emit_flush(strm, s, flush);
+    if (!s->header_done) {                                      // deflate.c:1002-1073
+        queue_header(s);
+        drain(strm, s);
+        if (s->out_pos < s->out.size()) {
+            s->last_flush = -1;
+            return Z_OK;
+        }
     }
-    if (flush == Z_FINISH && !s->finished) {
-        if (!s->flushed) {
-            size_t cap = (size_t)compress_bound64(s->in.size()) + 32;
-            s->out.resize(cap);
-            const uint8_t *sp = s->in.data();
-            uint8_t *dp = s->out.data();
-            size_t sl = s->in.size();
-            int st = 0;
-            int rc;
-            {
-                Lease L;
-                rc = L.rc;
-                if (!rc) rc = compress_host_locked(*L.c, &sp, &sl, &dp, &cap, &st, 1, s->level, s->wrap, s->strategy,
-                                                   nullptr, s->wbits, s->mem_level, s->tuned ? &s->tune : nullptr);
+    s->flushed = true;
+    if (P > C) {                                                // copy what is new
+        s->in.insert(s->in.end(), strm->next_in + (C - s->rd), strm->next_in + (P - s->rd));
+    } else if (P < C) {                                         // offered less than before: drop the rest
+        s->in.resize(P - s->in_base);
+        s->stale = true;
+    }
+
+    // the call's event
+    uint32_t own = ~0u;
+    if (s->ev_done < s->ev_type.size()) {                       // the last call did not get to its event
+        const size_t le = s->ev_type.size() - 1;
+        if (s->ev_type[le] == 0) {                              // a stop it paused before
+            if (P != s->ev_pos[le]) {
+                // more input: the reference goes on from the paused block
+                // reading up to the new end, the stop never comes
+                if (s->t == 0 || s->items[s->t - 1].kind != kItBlock) return Z_STREAM_ERROR;   // not paused
+                s->ev_type[le] = kEvPause;
+                s->ev_aux[le] = s->items[s->t - 1].in_end;
+                s->ev_done = le + 1;
+                s->stale = true;
+            } else if (flush == Z_NO_FLUSH) {
+                own = (uint32_t)le;
             }
-            if (rc || st) {
-                s->out.clear();          // nothing of a failed call may be handed out by a retry
-                return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
+        } else {                                                // a flush whose marker is still due
+            const bool at_marker = s->t < s->items.size() && s->items[s->t].kind == kItMarker &&
+                                   s->items[s->t].ev == (uint32_t)le;
+            if (P == s->ev_pos[le] && flush != Z_NO_FLUSH && flush != Z_FINISH) {
+                // the repeated flush call: its own kind of marker (deflate.c:1211-1233)
+                s->ev_type[le] = (uint32_t)flush;
+                own = (uint32_t)le;
+            } else if (at_marker) {
+                s->ev_type[le] = Z_BLOCK;                       // the cut stays, no marker bits
+                s->ev_done = le + 1;
+            } else if (P != s->ev_pos[le] || flush == Z_NO_FLUSH) {
+                // more input, or no flush: the reference goes on from the
+                // paused block reading up to the new end, no marker (zlib.h asks
+                // for the same flush until it completes; k_match keeps no clamp)
+                if (s->t == 0 || s->items[s->t - 1].kind != kItBlock) return Z_STREAM_ERROR;   // not paused
+                s->ev_type[le] = kEvPause;
+                s->ev_aux[le] = s->items[s->t - 1].in_end;
+                s->ev_done = le + 1;
+            } else {                                            // Z_FINISH's drain takes over
+                s->ev_pos.pop_back();
+                s->ev_type.pop_back();
+                s->ev_aux.pop_back();
             }
-            s->out.resize(cap);
-            strm->adler = s->wrap == 2 ? crc32_z(0, sp, sl) : (s->wrap == 1 ? adler32_z(1, sp, sl) : 0);
+            s->stale = true;
+        }
+    }
+    if (own == ~0u && flush != Z_FINISH) {
+        const size_t last = s->ev_pos.empty() ? s->res_pos : (size_t)s->ev_pos.back();   // a pause's: its call's end
+        if (flush != Z_NO_FLUSH || P > last) {
+            s->ev_pos.push_back(P);
+            s->ev_type.push_back((uint32_t)flush);
+            s->ev_aux.push_back(0);
+            own = (uint32_t)(s->ev_pos.size() - 1);
+            s->stale = true;
+        }
+    }
+    int rc = Z_OK;
+    bool full = false;
+    stream_trace("event", strm, s, flush);
+    if (own != ~0u || flush == Z_FINISH) {
+        // a Z_NO_FLUSH call that cannot complete a block before its stop (a
+        // block holds lit_bufsize - 1 symbols, each covering >= 1 input byte
+        // below P) hands out nothing: no job
+        bool skip = false;
+        if (flush == Z_NO_FLUSH && s->t == s->items.size() && !s->job_closed) {
+            size_t x0 = s->res_pos;
+            for (size_t k = s->t; k-- > 0;)
+                if (s->items[k].kind != kItStop) { x0 = (size_t)s->items[k].in_end; break; }
+            const size_t sym_limit = ((size_t)1 << (s->mem_level + 6)) - 1;
+            skip = P < x0 + sym_limit;
+        }
+        if (skip) {
+            s->rd = P;
+            s->ev_done = own + 1;
+            s->tentative = false;
         } else {
-            std::vector<uint8_t> body;
-            uint64_t o[4];
-            if (int rc = deflate_part(s, 0, body, o)) return rc;
-            queue_header(s);
-            const size_t jb = (size_t)(s->res_bits >> 3);
-            s->out.insert(s->out.end(), body.begin() + (std::ptrdiff_t)(s->part_out - jb), body.end());
-            if (s->wrap) {
-                advance_check(s);
-                const uint32_t ck = s->check;
-                strm->adler = ck;
-                if (s->wrap == 1) {
-                    for (int i = 3; i >= 0; i--) s->out.push_back((uint8_t)(ck >> (8 * i)));
-                } else {
-                    const uint32_t isz = (uint32_t)strm->total_in;
-                    for (int i = 0; i < 4; i++) s->out.push_back((uint8_t)(ck >> (8 * i)));
-                    for (int i = 0; i < 4; i++) s->out.push_back((uint8_t)(isz >> (8 * i)));
-                }
+            if (s->stale || (flush == Z_FINISH && !s->job_closed)) {
+                if (int e = deflate_part(s, flush == Z_FINISH)) return e;
             }
+            stream_trace("job", strm, s, flush);
+            rc = run_items(strm, s, own, &full);
         }
-        s->finished = 1;
-        s->in.clear();
-        s->in.shrink_to_fit();
     }
-    drain(strm, s);
-    if (flush != Z_FINISH) return Z_OK;
-    return s->out_pos == s->out.size() ? Z_STREAM_END : Z_OK;
+    stream_trace("ran", strm, s, flush);
+    sync_input(strm, s);
+    if (!s->finished) {
+        advance_check(s, s->rd);
+        if (s->wrap) strm->adler = s->check;
+    }
+    if (full) {
+        close_part(s);
+    } else if (!s->finished) {
+        choose_resume(s);
+    }
+    return rc;
 }
 
 int deflateReset(z_streamp strm) {                              // deflate.c:560-620
@@ -1920,7 +2339,7 @@ int deflatePending(z_streamp strm, unsigned *pending, int *bits) {
     if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
     if (pending) *pending = (unsigned)(s->out.size() - s->out_pos);
-    if (bits) *bits = s->finished ? 0 : (int)(s->res_bits & 7);
+    if (bits) *bits = s->finished ? 0 : (int)((s->level == 0 ? s->res_bits : s->proc_bits) & 7);
     return Z_OK;
 }
 
@@ -1959,6 +2378,7 @@ int deflateSetDictionary(z_streamp strm, const Bytef *dictionary, uInt dictLengt
         s->in_base = 0;
         s->res_S = 0;
         s->res_pos = s->ck_pos = s->in.size();
+        s->rd = s->rd_seen = s->flush_done = s->in.size();
         s->res_ev = 0;
         s->flushed = true;                 // the part path (bit and parse offsets)
         s->dict_set = s->wrap == 1;
@@ -2039,6 +2459,7 @@ int deflatePrime(z_streamp strm, int bits, int value) {
             s->res_bits = nb;
         }
         s->res_byte = (uint32_t)acc & 0xffu;
+        s->proc_bits = s->res_bits;
         s->flushed = true;
         return Z_OK;
     } catch (const std::bad_alloc &) {

@@ -951,8 +951,18 @@ constexpr int kMatchStats = 21, kMatchProbeNoWalk = 33, kMatchProbeHalf = 35,
 struct FlushEv {
     const uint64_t *pos;
     const uint32_t *type;
+    const uint64_t *aux;
     uint32_t n, i;
-    __device__ inline bool at(int64_t p) const { return i < n && (int64_t)ufl64(pos[i]) == p; }
+    // a flush call's input ends at p
+    __device__ inline bool at(int64_t p) const {
+        return i < n && kind() != 0 && kind() != kEvPause && (int64_t)ufl64(pos[i]) == p;
+    }
+    // the end of a Z_NO_FLUSH call's input, reached: all of it read (E == lim)
+    __device__ inline bool stop_at(int64_t e, int64_t lim) const { return i < n && kind() == 0 && e == lim; }
+    // the block just flushed ends where a call stopped on a full output buffer
+    __device__ inline bool pause_at(int64_t x) const {
+        return i < n && kind() == kEvPause && (int64_t)ufl64(aux[i]) == x;
+    }
     __device__ inline uint32_t kind() const { return (uint32_t)__builtin_amdgcn_readfirstlane((int)type[i]); }
     __device__ inline int64_t limit(int64_t end) const { return i < n ? (int64_t)ufl64(pos[i]) : end; }
     __device__ static inline uint64_t ufl64(uint64_t v) {
@@ -961,18 +971,20 @@ struct FlushEv {
         return ((uint64_t)hi << 32) | lo;
     }
 };
-__device__ inline FlushEv flush_ev(const DeflateJob &job) { return FlushEv{job.fl_pos, job.fl_type, job.nfl, 0}; }
+__device__ inline FlushEv flush_ev(const DeflateJob &job) { return FlushEv{job.fl_pos, job.fl_type, job.fl_aux, job.nfl, 0}; }
 
 // first flush position > p: the end of the input deflate() has seen when the
-// parse decides at p (longest_match's nice / lookahead clamp), else n
+// parse decides at p (longest_match's nice / lookahead clamp), else n.  The
+// ends of Z_NO_FLUSH calls do not count: the parse decides no position within
+// MIN_LOOKAHEAD of one before the next call's input is there (DeflateJob::mlim).
 __device__ inline int64_t flush_limit(const DeflateJob &job, int64_t p, int64_t n) {
-    uint32_t lo = 0, hi = job.nfl;
+    uint32_t lo = 0, hi = job.nmlim;
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
-        if ((int64_t)job.fl_pos[mid] > p) hi = mid;
+        if ((int64_t)job.mlim[mid] > p) hi = mid;
         else lo = mid + 1;
     }
-    return lo < job.nfl ? (int64_t)job.fl_pos[lo] : n;
+    return lo < job.nmlim ? (int64_t)job.mlim[lo] : n;
 }
 
 template <int kVariant, bool kEv = false, bool kSegs = false>
@@ -1116,6 +1128,14 @@ struct ParseOut {
     int64_t wsize, max_dist;      // w_size, MAX_DIST (deflate.c:440-444)
     uint32_t sym_limit;           // lit_bufsize - 1 (deflate.c:455, deflate.h:371)
     bool lead;               // the lane that stores (the state itself is wave-uniform)
+    uint64_t *srec = nullptr;     // a streaming job's records (DeflateJob::srec)
+
+    __device__ inline void rec(int64_t strstart, bool res) {      // srec[4 nblk + 2, + 3]
+        if (lead && srec) {
+            srec[4ull * nblk + 2] = ((uint64_t)S << 32) | (uint64_t)strstart;
+            srec[4ull * nblk + 3] = (uint64_t)E | (res ? 1ull << 63 : 0ull);
+        }
+    }
 
     __device__ inline void win(const WinP &w) { wsize = w.wsize; max_dist = w.max_dist; sym_limit = w.sym_limit; }
     __device__ inline bool tally(uint32_t v) {          // _tr_tally_*: returns bflush
@@ -1132,6 +1152,7 @@ struct ParseOut {
         r.flags = (last ? 1u : 0u) | (block_start >= S ? 2u : 0u);
         r.pad = 0;
         if (lead) blk[nblk] = r;
+        rec(strstart, true);
         nblk++;
         block_start = strstart;
         blk_sym_start = nsym;
@@ -1146,6 +1167,7 @@ struct ParseOut {
         r.flags = kBlkMarker | (kind << 4);
         r.pad = 0;
         if (lead) blk[nblk] = r;
+        rec(strstart, true);
         nblk++;
     }
     // fill_window (deflate.c:251-368), bookkeeping only; n = the end of the
@@ -1174,7 +1196,17 @@ struct ParseU {                     // wave-uniform parse output state
     uint32_t nsym, blk_nsym, blk_sym_start, nblk;
     uint32_t block_start, S, E;
     uint32_t wsize, max_dist, sym_limit;     // w_size, MAX_DIST, lit_bufsize - 1
-    __device__ inline void flush(uint32_t strstart, bool last, int lane) {   // FLUSH_BLOCK_ONLY
+    uint64_t *srec;                          // a streaming job's records (DeflateJob::srec)
+    __device__ inline void rec(uint32_t strstart, bool res, int lane) {
+        if (lane == 0 && srec) {
+            srec[4ull * nblk + 2] = ((uint64_t)S << 32) | strstart;
+            srec[4ull * nblk + 3] = (uint64_t)E | (res ? 1ull << 63 : 0ull);
+        }
+    }
+    // FLUSH_BLOCK_ONLY; res: the lazy state after it is the simple one
+    // (nothing pending, or a pending literal whose own match is < MIN_MATCH)
+    __device__ inline void flush(uint32_t strstart, bool last, int lane, bool res = true) {
+        rec(strstart, res, lane);
         if (lane == 0) {
             BlockRec r;
             r.sym_start = blk_sym_start;
@@ -1205,6 +1237,7 @@ struct ParseU {                     // wave-uniform parse output state
             r.pad = 0;
             blk[nblk] = r;
         }
+        rec(strstart, true, lane);
         nblk++;
     }
     __device__ inline void fill(uint32_t p, uint32_t n) {                   // fill_window bookkeeping
@@ -1239,9 +1272,12 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
         po.wsize = (uint32_t)wp.wsize; po.max_dist = (uint32_t)wp.max_dist; po.sym_limit = wp.sym_limit;
     }
     // a resumed flush job starts at its last flush: window read up to there
-    // (E), nothing pending, a new block (deflate.c state after :2030-2042)
+    // (E), nothing pending, a new block (deflate.c state after :2030-2042); one
+    // resumed at a block cut has read up to e0 and nothing pending either
+    // (ParseU::flush's res)
     uint32_t p = job.start, match_start = 0, match_length = kMinMatch - 1;
-    po.block_start = p; po.S = 0; po.E = p;
+    po.block_start = p; po.S = 0; po.E = job.e0 > p ? job.e0 : p;
+    po.srec = job.srec;
     bool avail = false, done = false;
     FlushEv fe = flush_ev(job);
     uint32_t lim = (uint32_t)fe.limit(n);      // input deflate() has been given
@@ -1255,8 +1291,19 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
         const bool tile_to_end = (uint64_t)t0 + kPT >= n;
         for (;;) {
             if (!tile_to_end && p + 64 > t0 + kPT) break;         // reload, keep 64 lookahead
+            if (p > po.E) { done = true; break; }                 // guard: never parse past the input read
             if (po.E - p < (uint32_t)kMinLookahead) {
                 po.fill(p, lim);
+                // a Z_NO_FLUSH call's input is used up: need_more (deflate.c:1941-1944);
+                // the next call's fill_window goes on from here
+                while (fe.stop_at(po.E, lim) && po.E - p < (uint32_t)kMinLookahead) {
+                    if (lane == 0 && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+                    fe.i++;
+                    if (fe.i == fe.n && job.open_end) { done = true; break; }
+                    lim = (uint32_t)fe.limit(n);
+                    po.fill(p, lim);
+                }
+                if (done) break;
                 if (po.E == p) {
                     if (fe.at(p)) {
                         // a deflate(flush) call ends here (deflate.c:2030-2042): the
@@ -1266,6 +1313,7 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
                         avail = false;
                         match_length = kMinMatch - 1;
                         if (po.blk_nsym) po.flush(p, false, lane);
+                        if (lane == 0 && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
                         po.marker(p, fe.kind(), lane);
                         if (lane == 0 && job.flush_out) job.flush_out[2] = po.S;
                         fe.i++;
@@ -1295,7 +1343,14 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
                         po.nsym += take;
                         po.blk_nsym += take;
                         a += take;
-                        if (po.blk_nsym == po.sym_limit) po.flush(a, false, lane);
+                        if (po.blk_nsym == po.sym_limit) {
+                            po.flush(a, false, lane);
+                            if (fe.pause_at(a)) {
+                                if (lane == 0 && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+                                fe.i++;
+                                lim = (uint32_t)fe.limit(n);
+                            }
+                        }
                     }
                     avail = true;
                     p += k;
@@ -1321,10 +1376,26 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
                 p += prev_length - 1;
                 avail = false;
                 match_length = kMinMatch - 1;
-                if (bflush) po.flush(p, false, lane);
+                if (bflush) {
+                    po.flush(p, false, lane);
+                    if (fe.pause_at(p)) {
+                        if (lane == 0 && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+                        fe.i++;
+                        lim = (uint32_t)fe.limit(n);
+                    }
+                }
             } else if (avail) {
                 const uint32_t lit = ufl(s_in[p - 1 - t0 + 16]);
-                if (po.tally1(lit, lane)) po.flush(p, false, lane);
+                // a new job starting at p would find the same state only when
+                // nothing longer than MIN_MATCH - 1 was pending here
+                if (po.tally1(lit, lane)) {
+                    po.flush(p, false, lane, prev_length < kMinMatch);
+                    if (fe.pause_at(p)) {
+                        if (lane == 0 && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+                        fe.i++;
+                        lim = (uint32_t)fe.limit(n);
+                    }
+                }
                 p++;
             } else {
                 avail = true;
@@ -1855,15 +1926,28 @@ __global__ __launch_bounds__(64) void k_parse_ev(DeflateJob job) {
     po.win(job_win(job));
     po.lead = true;
     int64_t p = job.start;                      // a resumed job: see k_parse_slow
-    po.block_start = p; po.S = 0; po.E = p;
+    po.block_start = p; po.S = 0; po.E = (int64_t)job.e0 > p ? (int64_t)job.e0 : p;
+    po.srec = job.srec;
     FlushEv fe = flush_ev(job);
     int64_t lim = fe.limit(n);
+    bool done = false;
     for (;;) {
+        if (p > po.E) break;                                      // guard: never parse past the input read
         if (rle ? po.E - p <= kMaxMatch : po.E == p) {
             po.fill(p, lim);
+            // a Z_NO_FLUSH call's input is used up: need_more (deflate.c:2065-2068, :2129-2134)
+            while (fe.stop_at(po.E, lim) && (rle ? po.E - p <= kMaxMatch : po.E == p)) {
+                if (job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+                fe.i++;
+                if (fe.i == fe.n && job.open_end) { done = true; break; }
+                lim = fe.limit(n);
+                po.fill(p, lim);
+            }
+            if (done) break;
             if (po.E == p) {
                 if (fe.at(p)) {
                     if (po.blk_nsym) po.flush(p, false);
+                    if (job.ev_blk) job.ev_blk[fe.i] = po.nblk;
                     po.marker(p, fe.kind());
                     if (job.flush_out) job.flush_out[2] = (uint64_t)po.S;
                     fe.i++;
@@ -1891,7 +1975,14 @@ __global__ __launch_bounds__(64) void k_parse_ev(DeflateJob job) {
             bflush = po.tally(in[p]);
             p++;
         }
-        if (bflush) po.flush(p, false);
+        if (bflush) {
+            po.flush(p, false);
+            if (fe.pause_at(p)) {
+                if (job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+                fe.i++;
+                lim = fe.limit(n);
+            }
+        }
     }
     if (!job.open_end) po.flush(p, true);
     job.nblocks[bi] = po.nblk;
@@ -1935,8 +2026,9 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     po.nsym = po.blk_nsym = po.blk_sym_start = po.nblk = 0;
     po.win(job_win(job));
     const int64_t start = kEv ? (int64_t)job.start : 0;
-    po.block_start = start; po.S = 0; po.E = start;
+    po.block_start = start; po.S = 0; po.E = kEv && (int64_t)job.e0 > start ? (int64_t)job.e0 : start;
     po.lead = lead;
+    if (kEv) po.srec = job.srec;
 
     // input window in registers: lane j holds in[wb + j] (w0) and in[wb + 64 + j]
     // (w1); it is moved forward 64 bytes at a time, so hashing and the scan side
@@ -1996,30 +2088,54 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     FlushEv fe = flush_ev(job);
     int64_t lim = kEv ? fe.limit(n) : n;       // input deflate() has been given
     // s->insert: strings a flush left unhashed (a resumed job starts right
-    // after a flush at its window offset + start)
-    int64_t pend = p < kMinMatch - 1 ? p : kMinMatch - 1;
-    for (;;) {
-        if (po.E - p < kMinLookahead) {
-            const bool reads = kEv && po.E < lim;
-            po.fill(p, lim);
-            // fill_window hashes the strings the last flush left unhashed once
-            // new input is read (deflate.c:318-335)
-            if (reads && pend && po.E - p + pend >= kMinMatch) {
-                int64_t str = p - pend;
-                while (pend) {
-                    wsee(str);
-                    insert(str);
-                    str++;
-                    pend--;
-                    if (po.E - p + pend < kMinMatch) break;
-                }
+    // after a flush at its window offset + start; none at a block cut)
+    int64_t pend = (kEv && job.cut) ? 0 : p < kMinMatch - 1 ? p : kMinMatch - 1;
+    // a streaming job keeps head[] as it stands at its last cut (the block or
+    // marker record snap[hsize]): a later job resumes there
+    auto snapshot = [&]() {
+        if (!kEv || !job.snap) return;
+        __threadfence_block();
+        for (uint32_t i = (uint32_t)lane; i < hsize; i += 64) job.snap[i] = head[i];
+        if (lead) job.snap[hsize] = po.nblk - 1;
+    };
+    auto fill = [&]() {
+        const bool reads = kEv && po.E < lim;
+        po.fill(p, lim);
+        // fill_window hashes the strings the last flush left unhashed once
+        // new input is read (deflate.c:318-335)
+        if (reads && pend && po.E - p + pend >= kMinMatch) {
+            int64_t str = p - pend;
+            while (pend) {
+                wsee(str);
+                insert(str);
+                str++;
+                pend--;
+                if (po.E - p + pend < kMinMatch) break;
             }
+        }
+    };
+    for (;;) {
+        if (p > po.E) break;                                      // guard: never parse past the input read
+        if (po.E - p < kMinLookahead) {
+            fill();
+            // a Z_NO_FLUSH call's input is used up: need_more (deflate.c:1841-1844)
+            bool done = false;
+            while (kEv && fe.stop_at(po.E, lim) && po.E - p < kMinLookahead) {
+                if (lead && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+                fe.i++;
+                if (fe.i == fe.n && job.open_end) { done = true; break; }
+                lim = fe.limit(n);
+                fill();
+            }
+            if (done) break;
             if (po.E == p) {
                 if (kEv && fe.at(p)) {
                     // a deflate(flush) call ends here (deflate.c:1903-1914, :1211-1233)
                     pend = p - po.S < kMinMatch - 1 ? p - po.S : kMinMatch - 1;
                     if (po.blk_nsym) po.flush(p, false);
+                    if (lead && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
                     po.marker(p, fe.kind());
+                    snapshot();
                     if (lead && job.flush_out) job.flush_out[2] = (uint64_t)po.S;
                     fe.i++;
                     lim = fe.limit(n);
@@ -2096,7 +2212,15 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
             bflush = po.tally(wbyte(p));
             p++;
         }
-        if (bflush) po.flush(p, false);
+        if (bflush) {
+            po.flush(p, false);
+            snapshot();
+            if (kEv && fe.pause_at(p)) {
+                if (lead && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+                fe.i++;
+                lim = fe.limit(n);
+            }
+        }
     }
     if (!kEv || !job.open_end) po.flush(p, true);
     if (lead) job.nblocks[bi] = po.nblk;
@@ -2356,6 +2480,14 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
         stg_or(stg, s_obit - st.sbase, v);
         s_obit += nb;
     };
+    // a streaming job's record k (tid 0): the output bit after it and the
+    // partial byte there (still in the staging window)
+    auto stream_rec = [&](uint32_t k) {
+        if (!job.srec) return;
+        const int64_t r = s_obit - st.sbase;
+        job.srec[4ull * k] = (uint64_t)s_obit;
+        job.srec[4ull * k + 1] = (stg[r >> 5] >> (((r >> 3) & 3) * 8)) & ((1u << (r & 7)) - 1u);
+    };
 
     if (tid == 0) {
         s_obit = job.bit0;                      // a resumed flush job: the partial byte's bits
@@ -2488,6 +2620,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
                         put(0, 16);
                         put(0xffffu, 16);
                     }
+                    stream_rec(k);
                 }
                 __syncthreads();
                 continue;
@@ -2588,6 +2721,10 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
             }
             if (last && tid == 0) s_obit = (s_obit + 7) & ~7ll;   // bi_windup
             __syncthreads();
+            if (job.srec) {                      // a streaming job: where this block ends
+                if (tid == 0) stream_rec(k);
+                __syncthreads();
+            }
           }
         }
     }
@@ -2711,7 +2848,7 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     case 5: hipLaunchKernelGGL(k_parse_seg, grid, dim3(kParseLanes), 0, st, job); break;
     case 6: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 1); break;
     case 3:
-        if (job.nfl || job.start) hipLaunchKernelGGL(k_parse_fast<true>, grid, dim3(64), 0, st, job, heads);
+        if (job.nfl || job.start || job.srec) hipLaunchKernelGGL(k_parse_fast<true>, grid, dim3(64), 0, st, job, heads);
         else hipLaunchKernelGGL(k_parse_fast<false>, grid, dim3(64), 0, st, job, heads);
         break;
     case 4: hipLaunchKernelGGL(k_encode, grid, dim3(kEncThreads), 0, st, job); break;

@@ -90,6 +90,7 @@ constexpr uint32_t kBlkStored = 2u;   // stored-eligible (block_start still in t
 // Z_PARTIAL_FLUSH 1 (_tr_align), Z_SYNC_FLUSH 2 / Z_FULL_FLUSH 3 (an empty
 // stored block), Z_BLOCK 5 (nothing).
 constexpr uint32_t kBlkMarker = 8u;
+constexpr uint32_t kEvPause = 8u;      // DeflateJob::fl_aux
 __host__ __device__ constexpr uint32_t blk_marker_kind(uint32_t flags) { return (flags >> 4) & 7u; }
 
 // Per-buffer workspace layout for one deflate sub-batch (device arrays).
@@ -156,6 +157,31 @@ struct DeflateJob {
     // inserts all but the last two, which wait as s->insert)
     int dict;
     uint32_t pre_ins;
+    // Z_NO_FLUSH calls of a streaming job: an event of kind 0 is the end of
+    // such a call's input.  The parse stops there once the lookahead is below
+    // MIN_LOOKAHEAD (deflate_slow, deflate_fast), at most MAX_MATCH
+    // (deflate_rle) or 0 (deflate_huff) with that input used up -- need_more
+    // (deflate.c:1941-1944, :1841-1844, :2065-2068, :2129-2134) -- and goes on
+    // with the next call's input.  Only events of other kinds clamp k_match
+    // (mlim: their positions), since a position decided before a need_more
+    // return has MIN_LOOKAHEAD bytes after it.
+    const uint64_t *mlim;
+    uint32_t nmlim;
+    // an event of kind kEvPause: the call before stopped on a full output
+    // buffer right after the block that ends at fl_aux[i], and the next call
+    // offered more input: from there on fill_window reads up to the next
+    // event's end instead of stopping at this one's (fl_pos[i])
+    const uint64_t *fl_aux;
+    // per block / marker record j of a streaming job (or null): srec[4j] the
+    // output bit after it and srec[4j + 1] the partial byte there (k_encode),
+    // srec[4j + 2] = S << 32 | in_end and srec[4j + 3] = E | resumable << 63 as
+    // the parse flushed it (window offset, fill_window's end of input read,
+    // whether the lazy state there is the simple one a new job starts in)
+    uint64_t *srec;
+    uint32_t *ev_blk;        // per event: the records before it when it was acted on
+    uint32_t e0;             // a job resumed at a block cut: E there (0: the start, nothing read ahead)
+    int cut;                 // resumed at a block cut, not after a flush (no s->insert strings)
+    uint32_t *snap;          // levels 1..3: head[] at the last cut; snap[hash_size] = its record
 };
 
 // the per-job window/hash parameters (deflate.c:440-455)
