@@ -14,25 +14,31 @@
  * checked as inflate.c does.  inflateSetDictionary() answers Z_NEED_DICT
  * (zlib streams) or presets a raw stream's window before its first input.
  *
- * deflate() semantics: deflateInit2_ accepts windowBits 8..15 (zlib), -8..-15
- * (raw), 24..31 (gzip), memLevel 1..9 and every strategy (Z_DEFAULT_STRATEGY,
+ * deflate() semantics: deflateInit2_ accepts windowBits 8..15 (zlib), -9..-15
+ * (raw), 25..31 (gzip), memLevel 1..9 and every strategy (Z_DEFAULT_STRATEGY,
  * Z_FILTERED, Z_HUFFMAN_ONLY, Z_RLE, Z_FIXED); the stream is allocated through
- * zalloc/zfree.  Input is gathered across Z_NO_FLUSH calls and compressed on
- * the GPU at the next flush call or at Z_FINISH (levels 1..9: Z_NO_FLUSH
- * calls hand out nothing; the final stream is the reference's); Z_PARTIAL_FLUSH,
- * Z_SYNC_FLUSH, Z_FULL_FLUSH and Z_BLOCK act as in deflate.c (markers,
- * full-flush reset, refused repeats with Z_BUF_ERROR), each flush call handing
- * out the stream up to its marker (level 0: deflate_stored's blocks, handed
- * out by every call).  deflateSetDictionary, deflateSetHeader, deflatePrime,
- * deflateTune and deflateParams give the reference's stream where the change
- * takes effect at a point this library's model knows exactly: before the first
- * deflate() call, or right after a flush with no input pending (deflateParams
- * flushes with Z_BLOCK itself when the level's function or the strategy
- * changes, as deflate.c does).  A change the model cannot place -- tuning a
- * stream with unflushed input, switching to or from level 0, Z_HUFFMAN_ONLY or
- * Z_RLE, or between deflate_fast and deflate_slow levels after data, a
- * dictionary at level 0 -- returns Z_STREAM_ERROR with strm->msg set, never a
- * different stream.
+ * zalloc/zfree.  Every call does what the reference's call does, levels 1..9:
+ * the header on the first call, the blocks completed before a Z_NO_FLUSH call's
+ * need_more point, a flush call's blocks and marker (Z_PARTIAL_FLUSH,
+ * Z_SYNC_FLUSH, Z_FULL_FLUSH, Z_BLOCK; refused repeats with Z_BUF_ERROR), the
+ * last block and trailer at Z_FINISH -- and it stops after a block when
+ * avail_out is used up, consuming only the input the reference had read by
+ * then (avail_in / total_in).  The parse runs on the GPU, one job per call that
+ * can complete a block, resumed at the last block cut handed out.  Level 0:
+ * deflate_stored's blocks as its first loop cuts them (a small avail_out that
+ * makes the reference cut shorter blocks is not modelled).  After Z_FINISH the
+ * caller continues with Z_FINISH until Z_STREAM_END (zlib.h); a flush call
+ * that ran out of output space is repeated with the same flush (zlib.h) --
+ * given more input instead, the stream stays valid but may differ.
+ * deflateSetDictionary, deflateSetHeader, deflatePrime, deflateTune and
+ * deflateParams give the reference's stream where the change takes effect at a
+ * point this library's model knows exactly: before the first deflate() call, or
+ * right after a flush with no input pending (deflateParams flushes with Z_BLOCK
+ * itself when the level's function or the strategy changes, as deflate.c does).
+ * A change the model cannot place -- tuning a stream with unflushed input,
+ * switching to or from level 0, Z_HUFFMAN_ONLY or Z_RLE, or between
+ * deflate_fast and deflate_slow levels after data, a dictionary at level 0 --
+ * returns Z_STREAM_ERROR with strm->msg set, never a different stream.
  */
 #ifndef ZGPU_ZLIB_H
 #define ZGPU_ZLIB_H

@@ -2333,8 +2333,7 @@ int deflateCopy(z_streamp dest, z_streamp source) {             // deflate.c:127
 }
 
 // Bytes generated and not yet handed out; bits: those of a partial last byte
-// after a Z_PARTIAL_FLUSH / Z_BLOCK (deflate.c:739-747).  Output of Z_NO_FLUSH
-// calls is deferred here, so it is not counted until a flush or Z_FINISH.
+// after the last block or marker handed out (deflate.c:739-747).
 int deflatePending(z_streamp strm, unsigned *pending, int *bits) {
     if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
