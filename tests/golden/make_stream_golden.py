@@ -52,11 +52,11 @@ def main():
     rng = np.random.default_rng(77)
     cases = []
     kinds = ["text", "mix", "runs", "random", "four", "records", "markup"]
-    for t in range(120):
+    for t in range(140):
         kind = kinds[t % 7]
         n = int(rng.choice([0, 5, 3000, 70000, 200000, 600000]))
         seed = 900 + t
-        level = [1, 2, 3, 4, 5, 6, 7, 8, 9][t % 9]
+        level = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9][t % 10]
         strategy = int(rng.choice([0, 0, 0, 0, 1, 2, 3, 4]))
         wbits = int(rng.choice([15, 15, -15, 31, 12, -9]))
         mem = int(rng.choice([8, 8, 8, 1, 5, 9]))

@@ -2,7 +2,7 @@
 pieces, on the GPU, against tests/golden/stream_golden.json: sessions run
 through the compiled reference (tests/golden/make_stream_golden.py,
 tests/zhelpers.run_dsession) -- zpipe.c-style loops and free call sequences
-at levels 1..9, every strategy, zlib/raw/gzip wrappers, windowBits and
+at levels 0..9, every strategy, zlib/raw/gzip wrappers, windowBits and
 memLevel settings.  Every call's return code, the input it left unconsumed
 (avail_in) and the bytes it wrote must be the reference's (deflate.c:763-1265:
 need_more after a block when avail_out runs out, FLUSH_BLOCK), and so must the
@@ -31,9 +31,6 @@ def test_stream_sessions_vs_reference(zg, stream_golden):
     L = zg.load()
     bad = []
     for c in stream_golden:
-        if c["level"] == 0:
-            continue
-        print("case", c["kind"], c["n"], c["seed"], c["level"], flush=True)
         data = datagen.make(c["kind"], c["n"], c["seed"])
         plan = [tuple(p) for p in c["plan"]]
         recs, whole = run_dsession(L, data, plan, c["level"], c["wbits"], c["mem"], c["strategy"])

@@ -1569,6 +1569,7 @@ struct internal_state {
     uint64_t proc_bits = 0;              // part output bit after the last item handed out
     uint64_t res_E = 0;                  // the resume point's E (fill_window's end of input read)
     int res_cut = 0;                     // the resume point is a block cut (not a flush)
+    int64_t st_strstart = 0, st_block_start = 0;   // level 0: deflate_stored's window offsets
     size_t job_base = 0;                 // res_S of the last job (snapshots are relative to it)
     uint32_t snap_rec = 0xffffffffu;     // levels 1..3: the record whose head[] the last job kept
     std::vector<uint32_t> snap_head;
@@ -1934,55 +1935,116 @@ void drain(z_streamp strm, internal_state *s) {
 
 inline int flush_rank(int f) { return f * 2 - (f > 4 ? 9 : 0); }   // deflate.c: RANK
 
-// Level 0: one deflate() call of deflate_stored (deflate.c:1635-1815) with an
-// output buffer that takes the call's output.  Its first loop sends stored
-// blocks of up to MAX_STORED bytes straight from the window and the input: a
-// Z_NO_FLUSH call while at least min_block (w_size = 32768) bytes are there,
-// any other call all of them (the last one final at Z_FINISH); the rest waits
-// in the window.  The block cuts are made here, the blocks and deflate()'s
-// markers are written by k_encode on the GPU.  zlib cuts smaller blocks when
-// the output space is smaller -- the one way a level-0 stream can differ.
+// Level 0: one deflate() call of deflate_stored (deflate.c:1635-1815), its
+// block cuts made here exactly as the reference makes them -- its first loop
+// sends stored blocks straight to next_out while the output space holds a
+// whole worthy (min_block) or flushed block, the rest of the input fills the
+// window, and a worthy or flushed block goes through the pending buffer --
+// with the window offsets (strstart, block_start), the pending buffer size and
+// the output space it sees.  The blocks and deflate()'s markers are written by
+// k_encode on the GPU from a host-made block list (DeflateJob::plan).  s->in
+// holds the window's unsent bytes [block_start, strstart).
 int deflate_stored_call(z_streamp strm, internal_state *s, int flush) {
-    if (s->finished) {
-        drain(strm, s);
-        return flush == Z_FINISH && s->out_pos == s->out.size() ? Z_STREAM_END : Z_OK;
-    }
-    queue_header(s);                                           // written by the first call
-    if (strm->avail_in) {
-        if ((uint64_t)s->in.size() + strm->avail_in >= kMaxBuffer) return Z_MEM_ERROR;   // 32-bit kernel positions
-        s->in.insert(s->in.end(), strm->next_in, strm->next_in + strm->avail_in);
-        strm->total_in += strm->avail_in;
-        strm->next_in += strm->avail_in;
-        strm->avail_in = 0;
-    }
-    advance_check(s, s->in_base + s->in.size());
+    // deflate.c:1192: deflate_stored runs when there is input or a flush
+    if (strm->avail_in == 0 && flush == Z_NO_FLUSH) return Z_OK;
+    const uint64_t w_size = 1ull << s->wbits, window_size = 2 * w_size;
+    const uint64_t pbs = 1ull << (s->mem_level + 8);          // pending_buf_size = lit_bufsize * 4
+    constexpr uint64_t kMaxStored = 65535;
+    int64_t &strstart = s->st_strstart, &block_start = s->st_block_start;
+    uint64_t aout = strm->avail_out;                            // the output space as the reference sees it
+    uint32_t bits = (uint32_t)(s->res_bits & 7);                // bi_valid
     std::vector<BlockRec> plan;
-    size_t off = 0, total = s->in.size();
-    bool last = false;
-    for (;;) {                                                 // deflate.c:1652-1725
-        const size_t len = std::min<size_t>(total, 65535);
-        if (len < 32768 && ((len == 0 && flush != Z_FINISH) || flush == Z_NO_FLUSH)) break;
-        last = flush == Z_FINISH && len == total;
+    std::vector<uint8_t> buf(s->in.begin(), s->in.end());      // the job's input: unsent window bytes, then reads
+    uint64_t bpos = 0;                                          // buf position of the next byte to send
+    auto read = [&](uint64_t n) {                               // read_buf (deflate.c:218-239)
+        if (!n) return;
+        buf.insert(buf.end(), strm->next_in, strm->next_in + n);
+        if (s->wrap == 1) s->check = (uint32_t)adler32_z(s->check, strm->next_in, n);
+        else if (s->wrap == 2) s->check = (uint32_t)crc32_z(s->check, strm->next_in, n);
+        strm->next_in += n;
+        strm->avail_in -= (uInt)n;
+        strm->total_in += n;
+    };
+    auto block = [&](uint64_t len, bool last) {                 // _tr_stored_block + flush_pending
         BlockRec r{};
-        r.in_start = off;
-        r.in_end = off + len;
+        r.in_start = bpos;
+        r.in_end = bpos + len;
         r.flags = last ? kBlkLast : 0u;
         plan.push_back(r);
-        off += len;
-        total -= len;
-        if (last) break;
+        const uint64_t bytes = (bits + 3 + 7) / 8 + 4 + len;
+        aout -= std::min(aout, bytes);
+        bits = 0;
+        bpos += len;
+    };
+    uint64_t min_block = std::min(pbs - 5, w_size);
+    const uint64_t used0 = strm->avail_in;
+    bool last = false;
+    do {                                                        // deflate.c:1652-1725
+        uint64_t len = kMaxStored;
+        uint64_t have = (bits + 42) >> 3;
+        if (aout < have) break;
+        have = aout - have;
+        const uint64_t left = (uint64_t)(strstart - block_start);
+        if (len > left + strm->avail_in) len = left + strm->avail_in;
+        if (len > have) len = have;
+        if (len < min_block && ((len == 0 && flush != Z_FINISH) || flush == Z_NO_FLUSH || len != left + strm->avail_in))
+            break;
+        last = flush == Z_FINISH && len == left + strm->avail_in;
+        const uint64_t from_win = std::min(left, len);
+        block_start += (int64_t)from_win;
+        read(len - from_win);                                   // straight from next_in
+        block(len, last);
+    } while (!last);
+    const uint64_t used = used0 - strm->avail_in;
+    if (used) {                                                 // deflate.c:1733-1760
+        if (used >= w_size) {
+            strstart = (int64_t)w_size;
+        } else {
+            if (window_size - (uint64_t)strstart <= used) strstart -= (int64_t)w_size;
+            strstart += (int64_t)used;
+        }
+        block_start = strstart;
     }
-    if (!last && flush != Z_NO_FLUSH && flush != Z_FINISH && total == 0) {   // block_done: :1211-1233
+    int bstate;                                                 // 0 need_more, 1 block_done, 2 finish_started, 3 finish_done
+    if (last) {
+        bstate = 3;
+    } else if (flush != Z_NO_FLUSH && flush != Z_FINISH && strm->avail_in == 0 && strstart == block_start) {
+        bstate = 1;
+    } else {
+        uint64_t have = window_size - (uint64_t)strstart;       // fill the window (deflate.c:1770-1790)
+        if (strm->avail_in > have && block_start >= (int64_t)w_size) {
+            block_start -= (int64_t)w_size;
+            strstart -= (int64_t)w_size;
+            have += w_size;
+        }
+        if (have > strm->avail_in) have = strm->avail_in;
+        read(have);
+        strstart += (int64_t)have;
+        have = (bits + 42) >> 3;                                // a block through pending (deflate.c:1792-1813)
+        have = std::min(pbs - have, kMaxStored);
+        min_block = std::min(have, w_size);
+        const uint64_t left = (uint64_t)(strstart - block_start);
+        if (left >= min_block ||
+            ((left || flush == Z_FINISH) && flush != Z_NO_FLUSH && strm->avail_in == 0 && left <= have)) {
+            const uint64_t len = std::min(left, have);
+            last = flush == Z_FINISH && strm->avail_in == 0 && len == left;
+            block(len, last);
+            block_start += (int64_t)len;
+        }
+        bstate = last ? 2 : 0;
+    }
+    if (bstate == 1) {                                          // deflate.c:1211-1233: the flush's marker
         BlockRec r{};
-        r.in_start = r.in_end = off;
+        r.in_start = r.in_end = bpos;
         r.flags = kBlkMarker | ((uint32_t)flush << 4);
         plan.push_back(r);
+        if (flush == Z_FULL_FLUSH) strstart = block_start = 0;
     }
     if (!plan.empty()) {
-        std::vector<uint8_t> body((size_t)compress_bound64(off) + 64 + 8 * plan.size());
-        const uint8_t *sp = s->in.data();
+        std::vector<uint8_t> body((size_t)compress_bound64(bpos) + 64 + 8 * plan.size());
+        const uint8_t *sp = buf.data();
         uint8_t *dp = body.data();
-        size_t sl = off, cap = body.size();
+        size_t sl = bpos, cap = body.size();
         int st = 0;
         FlushHost fh{nullptr, nullptr, 0, 1, 0, (uint32_t)(s->res_bits & 7),
                      s->res_byte & ((1u << (s->res_bits & 7)) - 1u), {0, 0, 0, 0}};
@@ -2001,30 +2063,32 @@ int deflate_stored_call(z_streamp strm, internal_state *s, int flush) {
         s->part_out = jb + cap;
         s->res_bits = ((uint64_t)jb << 3) + fh.out[1];
         s->res_byte = (uint32_t)fh.out[3];
-        s->in.erase(s->in.begin(), s->in.begin() + (std::ptrdiff_t)off);
-        s->in_base += off;
-        s->ck_pos = std::max(s->ck_pos, s->in_base);
     }
+    s->in.assign(buf.begin() + (std::ptrdiff_t)bpos, buf.end());   // the window's unsent bytes
     if (s->wrap) strm->adler = s->check;
-    if (last) {                                                // the trailer (deflate.c:1236-1262)
-        const uint32_t ck = s->check;
-        if (s->wrap == 1) {
-            for (int i = 3; i >= 0; i--) s->out.push_back((uint8_t)(ck >> (8 * i)));
-        } else if (s->wrap == 2) {
-            const uint32_t isz = (uint32_t)strm->total_in;
-            for (int i = 0; i < 4; i++) s->out.push_back((uint8_t)(ck >> (8 * i)));
-            for (int i = 0; i < 4; i++) s->out.push_back((uint8_t)(isz >> (8 * i)));
-        }
-        s->finished = 1;
-        s->in.clear();
-        s->in.shrink_to_fit();
-    }
     drain(strm, s);
-    if (flush != Z_FINISH) {
-        if (strm->avail_out == 0) s->last_flush = -1;
-        return Z_OK;
+    if (bstate == 1 && flush == Z_FULL_FLUSH) s->part_out = 0, s->res_bits = 0;   // a new part: byte aligned
+    if (bstate == 3) {                                          // finish_done: the trailer now
+        s->finished = 1;
+        if (s->wrap) {
+            const uint32_t ck = s->check;
+            if (s->wrap == 1) {
+                for (int i = 3; i >= 0; i--) s->out.push_back((uint8_t)(ck >> (8 * i)));
+            } else {
+                const uint32_t isz = (uint32_t)strm->total_in;
+                for (int i = 0; i < 4; i++) s->out.push_back((uint8_t)(ck >> (8 * i)));
+                for (int i = 0; i < 4; i++) s->out.push_back((uint8_t)(isz >> (8 * i)));
+            }
+        }
+        drain(strm, s);
+        return s->out_pos == s->out.size() ? Z_STREAM_END : Z_OK;
     }
-    return s->out_pos == s->out.size() ? Z_STREAM_END : Z_OK;
+    if (bstate == 2) {                                          // finish_started: the trailer with a later call
+        s->finished = 1;
+        s->trailer_due = true;
+    }
+    if (strm->avail_out == 0) s->last_flush = -1;
+    return Z_OK;
 }
 
 // part output bytes [part_out, to) of the last job into the output queue
@@ -2147,7 +2211,6 @@ static int deflate_body(z_streamp strm, int flush) {
         return Z_BUF_ERROR;
     }
     if (s->finished && strm->avail_in) return Z_BUF_ERROR;
-    if (s->level == 0) return deflate_stored_call(strm, s, flush);
     if (s->finished) {                                          // FINISH_STATE
         if (s->trailer_due) {
             s->trailer_due = false;
@@ -2163,7 +2226,7 @@ static int deflate_body(z_streamp strm, int flush) {
 
     // the first call asks for Z_FINISH with everything: one batch job, when
     // its output fits (otherwise the timeline below pauses like zlib)
-    if (flush == Z_FINISH && !s->header_done && !s->flushed && C == 0) {
+    if (flush == Z_FINISH && !s->header_done && !s->flushed && C == 0 && s->level != 0) {
         size_t cap = (size_t)strm->avail_in + (strm->avail_in >> 2) + 1024;   // any windowBits / memLevel
         std::vector<uint8_t> tmp(cap);
         const uint8_t *sp = strm->next_in;
@@ -2200,6 +2263,7 @@ static int deflate_body(z_streamp strm, int flush) {
             return Z_OK;
         }
     }
+    if (s->level == 0) return deflate_stored_call(strm, s, flush);
     s->flushed = true;
     if (P > C) {                                                // copy what is new
         s->in.insert(s->in.end(), strm->next_in + (C - s->rd), strm->next_in + (P - s->rd));
