@@ -404,6 +404,18 @@ __device__ __attribute__((always_inline)) inline void tile_prefetch(TilePre &P, 
 
 // Tile load from the prefetched registers: slide the window down by kMT words
 // (later tiles), then write words kMW.. of the new tile and its pad.
+// kIdx: the low half of a word is the LDS word index of the predecessor (0:
+// none, or older than the window -- index 0 is always beyond a walk's limit),
+// so a chain step needs no subtraction; sliding lowers every index by kMT,
+// saturating at 0 (one packed 16-bit subtract per word).
+// Otherwise the low half is the distance to it (0xffff: none, nil_link).
+__device__ __attribute__((always_inline)) inline uint32_t slide_idx(uint32_t w) {
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const us2 v = __builtin_bit_cast(us2, w);
+    const us2 d = {(unsigned short)kMT, (unsigned short)0};
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(v, d));
+}
+template <bool kIdx = false>
 __device__ __attribute__((always_inline)) inline void tile_store(uint32_t *E, const TilePre &P, int64_t ts,
                                                                  int tid) {
     if (ts == 0) {
@@ -412,15 +424,26 @@ __device__ __attribute__((always_inline)) inline void tile_store(uint32_t *E, co
         // kMW/4 uint4 chunks, thread t moves chunks t (mod kMatchThreads) in
         // increasing order: no chunk is overwritten before it is read
         uint4 *dE = reinterpret_cast<uint4 *>(E);
-        for (int c = tid; c < kMW / 4; c += kMatchThreads) dE[c] = dE[c + kMT / 4];
+        for (int c = tid; c < kMW / 4; c += kMatchThreads) {
+            uint4 v = dE[c + kMT / 4];
+            if (kIdx) v = make_uint4(slide_idx(v.x), slide_idx(v.y), slide_idx(v.z), slide_idx(v.w));
+            dE[c] = v;
+        }
         __syncthreads();
     }
     const int w0 = kMW + 4 * tid;
     uint4 v;
-    v.x = P.b[0] << 16 | nil_link(P.lk[0]);
-    v.y = P.b[1] << 16 | nil_link(P.lk[1]);
-    v.z = P.b[2] << 16 | nil_link(P.lk[2]);
-    v.w = P.b[3] << 16 | nil_link(P.lk[3]);
+    if (kIdx) {
+        v.x = P.b[0] << 16 | (P.lk[0] ? (uint32_t)(w0 + 0) - P.lk[0] : 0u);
+        v.y = P.b[1] << 16 | (P.lk[1] ? (uint32_t)(w0 + 1) - P.lk[1] : 0u);
+        v.z = P.b[2] << 16 | (P.lk[2] ? (uint32_t)(w0 + 2) - P.lk[2] : 0u);
+        v.w = P.b[3] << 16 | (P.lk[3] ? (uint32_t)(w0 + 3) - P.lk[3] : 0u);
+    } else {
+        v.x = P.b[0] << 16 | nil_link(P.lk[0]);
+        v.y = P.b[1] << 16 | nil_link(P.lk[1]);
+        v.z = P.b[2] << 16 | nil_link(P.lk[2]);
+        v.w = P.b[3] << 16 | nil_link(P.lk[3]);
+    }
     *reinterpret_cast<uint4 *>(E + w0) = v;
     if (tid < kMPad / 4)
         *reinterpret_cast<uint4 *>(E + kMW + kMT + 4 * tid) =
@@ -638,11 +661,12 @@ struct DWS {
 // The loop has one exit, taken by the whole wave, and every update is a
 // select.  `count` is wave-uniform (all lanes start their walks together and
 // step together).
+template <bool kIdx = false>
 __device__ __attribute__((always_inline)) inline void dw_steps(DWS &w, const char *Eb, uint32_t &count, uint32_t end) {
     for (;;) {
         const bool valid = w.m4 > w.limit4;
-        const int m4n = w.m4 + (int)(w.em & 0xffffu) * -4;
-        const int a = m4n > 0 ? m4n : 0;
+        const int m4n = kIdx ? (int)((w.em << 2) & 0x3fffcu) : w.m4 + (int)(w.em & 0xffffu) * -4;
+        const int a = kIdx ? m4n : (m4n > 0 ? m4n : 0);
         const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + a);
         const uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
         const bool pass = valid & ((w.em >> 16) == w.scan01) & ((w.eb >> 16) == w.scanE);
@@ -720,13 +744,14 @@ __device__ inline uint32_t match_rec(int best, int s4, int bpos4) {
 __device__ unsigned long long g_dstat[4];   // deferred-walk statistics (variant 41)
 
 template <bool kStats = false, int kHead = kD0, bool kPartial = false, bool kNoFlush = false, bool kRecheck = false,
-          bool kBatchFlush = false>
+          bool kBatchFlush = false, bool kIdx = false>
 __device__ __attribute__((always_inline)) inline void dw_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
                                                               const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
                                                               int want_q, int64_t max_dist) {
     const int s = (int)(p - B);
     const uint32_t e0 = E[s];
-    const uint32_t d0 = e0 & 0xffffu;
+    // the distance to the chain's head (kIdx: from its window index; index 0, none)
+    const uint32_t d0 = kIdx ? ((e0 & 0xffffu) ? (uint32_t)s - (e0 & 0xffffu) : 0xffffu) : e0 & 0xffffu;
     if (d0 > (uint32_t)max_dist) {                 // deflate.c:1955: strstart - hash_head <= MAX_DIST
         rf[p] = 0;
         if (want_q) rq[p] = 0;
@@ -755,7 +780,7 @@ __device__ __attribute__((always_inline)) inline void dw_walk(const uint32_t *E,
             const int len = lcp16(E, m, s, S, maxcmp);
             if (len > best) { best = len; bpos4 = m4; }
             count++;
-            const int m4n = m4 - (int)((em & 0xffffu) << 2);
+            const int m4n = kIdx ? (int)((em & 0xffffu) << 2) : m4 - (int)((em & 0xffffu) << 2);
             if (best >= nice || m4n <= limit4 || count >= chain) walking = false;
             if (need_q && count == qc && walking) {      // a tuned chain/4 inside the head
                 rq[p] = match_rec(best, s4, bpos4);
@@ -797,7 +822,7 @@ __device__ __attribute__((always_inline)) inline void dw_walk(const uint32_t *E,
             walking = w.m4 > w.limit4 && count < chain;
             if (best >= nice) walking = false;
         } else {
-            dw_steps(w, Eb, count, end);
+            dw_steps<kIdx>(w, Eb, count, end);
             walking = w.m4 > limit4 && count < chain;
         }
         const bool partial = false;
@@ -898,10 +923,144 @@ __device__ __attribute__((always_inline)) inline void dw_walk(const uint32_t *E,
     rf[p] = match_rec(best, s4, bpos4);
 }
 
+
+// dw_walk (kIdx) with a kQ-deep queue: flushes come when some lane holds kQ
+// passes, so a deeper queue means fewer, fuller flush rounds
+template <int kQ>
+struct DWQ {
+    int m4, limit4, be4, occ;
+    int q[kQ];
+    uint32_t em, eb, scan01, scanE;
+};
+template <int kQ>
+__device__ __attribute__((always_inline)) inline void dwq_steps(DWQ<kQ> &w, const char *Eb, uint32_t &count,
+                                                                uint32_t end) {
+    for (;;) {
+        const bool valid = w.m4 > w.limit4;
+        const int m4n = (int)((w.em << 2) & 0x3fffcu);
+        const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + m4n);
+        const uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + m4n + w.be4);
+        const bool pass = valid & ((w.em >> 16) == w.scan01) & ((w.eb >> 16) == w.scanE);
+#pragma unroll
+        for (int j = kQ - 1; j > 0; j--) w.q[j] = pass ? w.q[j - 1] : w.q[j];
+        w.q[0] = pass ? w.m4 : w.q[0];
+        w.occ += pass ? 1 : 0;
+        w.m4 = m4n;
+        w.em = emn;
+        w.eb = ebn;
+        count++;
+        const uint64_t walkers = __ballot(m4n > w.limit4), full = __ballot(w.occ == kQ);
+        if (count >= end || walkers == 0 || full != 0) break;
+    }
+}
+
+template <int kQ>
+__device__ __attribute__((always_inline)) inline void dwq_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
+                                                               const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
+                                                               int want_q, int64_t max_dist) {
+    const int s = (int)(p - B);
+    const uint32_t e0 = E[s];
+    const uint32_t d0 = (e0 & 0xffffu) ? (uint32_t)s - (e0 & 0xffffu) : 0xffffu;
+    if (d0 > (uint32_t)max_dist) {                 // deflate.c:1955: strstart - hash_head <= MAX_DIST
+        rf[p] = 0;
+        if (want_q) rq[p] = 0;
+        return;
+    }
+    const int64_t labs = p > max_dist ? p - max_dist : 0;
+    const int limit4 = (int)(labs - B) * 4;
+    const int64_t rem = n - p;
+    const int nice = rem < cfg.nice ? (int)rem : cfg.nice;
+    const int maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
+    const uint32_t chain = (uint32_t)cfg.chain;
+    const uint32_t qc = want_q ? chain >> 2 : chain;
+    const int s4 = s * 4;
+    const Scan16 S{get4(E, s), get4(E, s + 4), get4(E, s + 8), get4(E, s + 12)};
+    int best = kMinMatch - 1, bpos4 = 0;
+    int m4 = (int)(e0 & 0xffffu) * 4;
+    uint32_t count = 0;
+    bool walking = true;
+    bool need_q = want_q != 0;
+#pragma unroll
+    for (int k = 0; k < kD0; k++) {                 // the chain's head, compared by the whole wave
+        if (walking) {
+            const int m = m4 >> 2;
+            const uint32_t em = E[m];
+            const int len = lcp16(E, m, s, S, maxcmp);
+            if (len > best) { best = len; bpos4 = m4; }
+            count++;
+            const int m4n = (int)((em & 0xffffu) << 2);
+            if (best >= nice || m4n <= limit4 || count >= chain) walking = false;
+            if (need_q && count == qc && walking) {
+                rq[p] = match_rec(best, s4, bpos4);
+                need_q = false;
+            }
+            m4 = m4n;
+        }
+    }
+    if (!walking) {
+        const uint32_t r = match_rec(best, s4, bpos4);
+        if (need_q) rq[p] = r;
+        rf[p] = r;
+        return;
+    }
+    const char *Eb = reinterpret_cast<const char *>(E);
+    DWQ<kQ> w;
+    w.m4 = m4;
+    w.limit4 = limit4;
+    w.be4 = (best - 1) * 4;
+    w.occ = 0;
+#pragma unroll
+    for (int j = 0; j < kQ; j++) w.q[j] = 0;
+    w.scan01 = e0 >> 16;
+    w.scanE = E[s + best - 1] >> 16;
+    w.em = *reinterpret_cast<const uint32_t *>(Eb + m4);
+    w.eb = *reinterpret_cast<const uint32_t *>(Eb + m4 + w.be4);
+    count = ufl(count);
+    for (;;) {
+        const uint32_t end = count < qc ? qc : chain;
+        const int best0 = best;
+        dwq_steps<kQ>(w, Eb, count, end);
+        walking = w.m4 > limit4 && count < chain;
+        // every entry, oldest first: entry j (< occ) is the (occ - j)-th oldest
+#pragma unroll
+        for (int j = kQ - 1; j >= 0; j--) {
+            const bool cand = j < w.occ;
+            if (__ballot(cand) != 0) {
+                if (cand) {
+                    const int len = lcp16(E, w.q[j] >> 2, s, S, maxcmp);
+                    if (len > best) {
+                        best = len;
+                        bpos4 = w.q[j];
+                        if (len >= nice) { walking = false; w.occ = 0; }   // drop the later entries
+                    }
+                }
+            }
+        }
+        w.occ = 0;
+        const bool fin = !walking;
+        if (need_q && (count >= qc || fin)) {          // deflate.c:1390-1392 (chain >>= 2)
+            rq[p] = match_rec(best, s4, bpos4);
+            need_q = false;
+        }
+        if (fin) break;
+        if (best != best0) {                           // the quick reject now tests the new best
+            w.be4 = (best - 1) * 4;
+            w.scanE = E[s + best - 1] >> 16;
+            w.eb = *reinterpret_cast<const uint32_t *>(Eb + w.m4 + w.be4);
+        }
+    }
+    rf[p] = match_rec(best, s4, bpos4);
+}
+
 __device__ unsigned long long g_mstat[4];   // kMatchStats statistics
 
 // k_match variants (ZGPU_MATCH_VARIANT, for A/B runs):
-//   40 (default)  19 with deferred compares (dw_walk): 495 -> 412 ms per 4 GiB
+//   49 (default)  48 with a 6-deep queue (dwq_walk): 411 -> 401 ms
+//   48            40 with links stored as the predecessor's LDS word index (a
+//                 chain step needs no subtraction; the slide lowers every index
+//                 with one saturating packed subtract): 418 -> 411 ms
+//   50, 51        48 with an 8-deep (407 ms) or 3-deep (407 ms) queue
+//   40            19 with deferred compares (dw_walk): 495 -> 412 ms per 4 GiB
 //                 C4 sub-batch at L6 (the C4 shard 7.7 -> 9.1 GB/s)
 //   41            40 plus statistics (wave iterations, flushes, flush rounds)
 //   42            40 with three wave-wide head compares (no faster)
@@ -936,9 +1095,10 @@ __device__ unsigned long long g_mstat[4];   // kMatchStats statistics
 //                 waves walk (1.6x slower at L6, 1.8x at L9: the walks are
 //                 latency-bound at the 16 waves the LDS window allows)
 constexpr int kMatchDefer = 40, kMatchDeferStats = 41, kMatchDefer3 = 42, kMatchDeferP = 43, kMatchDeferPStats = 44,
-              kMatchProbeNoFlush = 45, kMatchDeferR = 46, kMatchDeferB = 47;
+              kMatchProbeNoFlush = 45, kMatchDeferR = 46, kMatchDeferB = 47, kMatchDeferIdx = 48,
+              kMatchQ6 = 49, kMatchQ8 = 50, kMatchQ3 = 51;
 constexpr int kMatchWalk = 19;
-constexpr int kMatchDefault = kMatchDefer;
+constexpr int kMatchDefault = kMatchQ6;
 constexpr int kMatchStats = 21, kMatchProbeNoWalk = 33, kMatchProbeHalf = 35,
               kMatchProbeNoCmp = 37, kMatchProbeCmpOnly = 38;
 
@@ -1020,7 +1180,8 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
     for (int64_t ts = t0; ts < s1; ts += kMT) {
         const int64_t B = ts - kMW;
         const int tile_n = kSegs && ts < s0 ? 0 : (int)((n - ts) < kMT ? (n - ts) : kMT);   // 0: staging only
-        tile_store(E, P, ts, tid);
+        tile_store<kVariant == kMatchDeferIdx || kVariant == kMatchQ6 || kVariant == kMatchQ8 || kVariant == kMatchQ3>(
+            E, P, ts, tid);
         if (tid == 0) next_i = 0;
         if (kSorted && tid < kSortBuckets) s_hist[tid] = 0;
         __syncthreads();
@@ -1084,6 +1245,14 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
 
             } else if (kVariant == kMatchDefer) {
                 dw_walk(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+            } else if (kVariant == kMatchQ6) {
+                dwq_walk<6>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+            } else if (kVariant == kMatchQ8) {
+                dwq_walk<8>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+            } else if (kVariant == kMatchQ3) {
+                dwq_walk<3>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+            } else if (kVariant == kMatchDeferIdx) {
+                dw_walk<false, kD0, false, false, false, false, true>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
             } else if (kVariant == kMatchDefer3) {
                 dw_walk<false, 3>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
             } else if (kVariant == kMatchDeferB) {
@@ -2768,7 +2937,8 @@ static int match_variant() {
         return (x == 14 || x == kMatchWalk || x == kMatchStats || x == kMatchProbeNoWalk || x == kMatchProbeHalf ||
                 x == kMatchProbeNoCmp || x == kMatchProbeCmpOnly || x == kMatchDefer || x == kMatchDeferStats || x == kMatchDefer3 || x == kMatchDeferP ||
                 x == kMatchDeferPStats || x == kMatchProbeNoFlush || x == kMatchDeferR ||
-                x == kMatchDeferB) ? x : kMatchDefault;
+                x == kMatchDeferB || x == kMatchDeferIdx || x == kMatchQ6 || x == kMatchQ8 || x == kMatchQ3)
+                   ? x : kMatchDefault;
     }();
     return v;
 }
@@ -2797,6 +2967,14 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
             hipLaunchKernelGGL(k_match<kMatchWalk>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchDeferB) {
             hipLaunchKernelGGL(k_match<kMatchDeferB>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchDeferIdx) {
+            hipLaunchKernelGGL(k_match<kMatchDeferIdx>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchQ6) {
+            hipLaunchKernelGGL(k_match<kMatchQ6>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchQ8) {
+            hipLaunchKernelGGL(k_match<kMatchQ8>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchQ3) {
+            hipLaunchKernelGGL(k_match<kMatchQ3>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchDeferR) {
             hipLaunchKernelGGL(k_match<kMatchDeferR>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchProbeNoFlush) {
