@@ -129,6 +129,14 @@ def sessions():
                 ["init", level, 31, 8, 0], ["header", h], ["deflate", text, 4]]})
     S.append({"name": "header-on-zlib-refused", "ops": [["init", 6, 15, 8, 0], ["header", hdrs[0]],
                                                         ["deflate", text, 4]]})
+    # deflateTune's max_lazy is deflate_fast's max_insert_length: long matches
+    # inserted position by position at levels 1..3
+    runs = ["gen", "runs", 120000, 41]
+    for level in (1, 2, 3):
+        for lazy in (40, 100, 258):
+            for data in (text, runs):
+                S.append({"name": f"tune-fast-insert-L{level}-{lazy}-{data[1]}", "ops": [
+                    ["init", level, 15, 8, 0], ["tune", 4, lazy, 258, 64], ["deflate", data, 4]]})
     return S
 
 

@@ -2347,10 +2347,11 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         if (match_length >= kMinMatch) {
             bflush = po.tally(((uint32_t)(p - match_start) << 8) | (match_length - kMinMatch));
             lookahead -= match_length;
-            if (match_length <= cfg.lazy && lookahead >= kMinMatch) {
-                // positions p+1 .. p+len-1 (at most 5), one lane each: the head
-                // loads go out together; a position whose hash a lower lane
-                // also inserts takes that lane's position (zlib inserts in order)
+            if (match_length <= cfg.lazy && lookahead >= kMinMatch && match_length <= 48) {
+                // positions p+1 .. p+len-1 (at most 5 unless deflateTune), one
+                // lane each: the head loads go out together; a position whose
+                // hash a lower lane also inserts takes that lane's position (zlib
+                // inserts in order)
                 const uint32_t cntk = match_length - 1;
                 const bool mine = (uint32_t)lane < cntk;
                 const int64_t q = p + 1 + lane;
@@ -2373,6 +2374,12 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
                     const int64_t dd = q - hq;
                     prev[q] = (hq != 0 && dd <= 32767) ? (uint16_t)dd : 0;
                     if (last) head[h] = (uint32_t)q;
+                }
+            } else if (match_length <= cfg.lazy && lookahead >= kMinMatch) {
+                // deflateTune's longer max_insert_length: one insert at a time
+                for (uint32_t k = 1; k < match_length; k++) {
+                    wsee(p + k);
+                    insert(p + k);
                 }
             }
             p += match_length;
