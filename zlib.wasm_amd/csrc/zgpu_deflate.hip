@@ -1052,6 +1052,194 @@ __device__ __attribute__((always_inline)) inline void dwq_walk(const uint32_t *E
     rf[p] = match_rec(best, s4, bpos4);
 }
 
+// dwq_walk for two positions per lane: the two chains step in the same loop
+// iteration, so each lane keeps two independent LDS round trips in flight
+// (the walks are latency-bound at the 16 waves the LDS window allows).  A
+// walk that ends first idles (its limit rises out of reach) until the other
+// one is done.  `live` false: no position (the tile's odd last one).
+template <int kQ>
+struct DWP {
+    int64_t p;
+    int s, s4, limit4, nice, maxcmp, best, bpos4, best0;
+    bool walking, need_q, live;
+    Scan16 S;
+    DWQ<kQ> w;
+};
+
+template <int kQ>
+__device__ __attribute__((always_inline)) inline void dwp_init(DWP<kQ> &x, const uint32_t *E, int64_t p, bool live,
+                                                               int64_t B, int64_t n, const LevelCfg &cfg, uint32_t *rf,
+                                                               uint32_t *rq, int want_q, int64_t max_dist) {
+    x.p = p;
+    x.s = live ? (int)(p - B) : 0;
+    x.s4 = x.s * 4;
+    const uint32_t e0 = E[x.s];
+    const uint32_t d0 = (e0 & 0xffffu) ? (uint32_t)x.s - (e0 & 0xffffu) : 0xffffu;
+    x.live = live;
+    if (live && d0 > (uint32_t)max_dist) {          // deflate.c:1955: strstart - hash_head <= MAX_DIST
+        rf[p] = 0;
+        if (want_q) rq[p] = 0;
+        x.live = false;
+    }
+    const int64_t labs = p > max_dist ? p - max_dist : 0;
+    x.limit4 = (int)(labs - B) * 4;
+    const int64_t rem = n - p;
+    x.nice = rem < cfg.nice ? (int)rem : cfg.nice;
+    x.maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
+    x.S = Scan16{get4(E, x.s), get4(E, x.s + 4), get4(E, x.s + 8), get4(E, x.s + 12)};
+    x.best = kMinMatch - 1;
+    x.bpos4 = 0;
+    x.walking = x.live;
+    x.need_q = x.live && want_q != 0;
+    x.w.m4 = (int)(e0 & 0xffffu) * 4;
+    x.w.scan01 = e0 >> 16;
+}
+
+// one head compare of a pair walk (count is the shared step count before it)
+template <int kQ>
+__device__ __attribute__((always_inline)) inline void dwp_head(DWP<kQ> &x, const uint32_t *E, uint32_t count,
+                                                               uint32_t chain, uint32_t qc, uint32_t *rq) {
+    if (x.walking) {
+        const int m = x.w.m4 >> 2;
+        const uint32_t em = E[m];
+        const int len = lcp16(E, m, x.s, x.S, x.maxcmp);
+        if (len > x.best) { x.best = len; x.bpos4 = x.w.m4; }
+        const int m4n = (int)((em & 0xffffu) << 2);
+        if (x.best >= x.nice || m4n <= x.limit4 || count + 1 >= chain) x.walking = false;
+        if (x.need_q && count + 1 == qc && x.walking) {
+            rq[x.p] = match_rec(x.best, x.s4, x.bpos4);
+            x.need_q = false;
+        }
+        x.w.m4 = m4n;
+    }
+}
+
+// a pair walk that is done writes its results and stops queueing
+template <int kQ>
+__device__ __attribute__((always_inline)) inline void dwp_finish(DWP<kQ> &x, uint32_t *rf, uint32_t *rq) {
+    const uint32_t r = match_rec(x.best, x.s4, x.bpos4);
+    if (x.need_q) rq[x.p] = r;
+    rf[x.p] = r;
+    x.need_q = false;
+    x.live = false;
+    x.walking = false;
+    x.w.limit4 = 0x7fffffff;
+    x.w.occ = 0;
+}
+
+template <int kQ>
+__device__ __attribute__((always_inline)) inline void dwp_arm(DWP<kQ> &x, const uint32_t *E) {
+    const char *Eb = reinterpret_cast<const char *>(E);
+    if (!x.walking) x.w.m4 = 0;                     // idle: reads word 0, queues nothing
+    x.w.limit4 = x.walking ? x.limit4 : 0x7fffffff;
+    x.w.be4 = (x.best - 1) * 4;
+    x.w.occ = 0;
+#pragma unroll
+    for (int j = 0; j < kQ; j++) x.w.q[j] = 0;
+    x.w.scanE = E[x.s + x.best - 1] >> 16;
+    x.w.em = *reinterpret_cast<const uint32_t *>(Eb + x.w.m4);
+    x.w.eb = *reinterpret_cast<const uint32_t *>(Eb + x.w.m4 + x.w.be4);
+}
+
+template <int kQ>
+__device__ __attribute__((always_inline)) inline bool dwq_step1(DWQ<kQ> &w, const char *Eb) {
+    const bool valid = w.m4 > w.limit4;
+    const int m4n = (int)((w.em << 2) & 0x3fffcu);
+    const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + m4n);
+    const uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + m4n + w.be4);
+    const bool pass = valid & ((w.em >> 16) == w.scan01) & ((w.eb >> 16) == w.scanE);
+#pragma unroll
+    for (int j = kQ - 1; j > 0; j--) w.q[j] = pass ? w.q[j - 1] : w.q[j];
+    w.q[0] = pass ? w.m4 : w.q[0];
+    w.occ += pass ? 1 : 0;
+    w.m4 = m4n;
+    w.em = emn;
+    w.eb = ebn;
+    return m4n > w.limit4;
+}
+
+template <int kQ>
+__device__ __attribute__((always_inline)) inline void dwp_flush_one(DWP<kQ> &x, const uint32_t *E, int j) {
+    if (j < x.w.occ) {
+        const int len = lcp16(E, x.w.q[j] >> 2, x.s, x.S, x.maxcmp);
+        if (len > x.best) {
+            x.best = len;
+            x.bpos4 = x.w.q[j];
+            if (len >= x.nice) { x.walking = false; x.w.occ = 0; }   // drop the later entries
+        }
+    }
+}
+
+template <int kQ>
+__device__ __attribute__((always_inline)) inline void dwp_after(DWP<kQ> &x, const uint32_t *E, uint32_t count,
+                                                                uint32_t qc, uint32_t *rf, uint32_t *rq) {
+    if (!x.live) return;
+    const bool fin = !x.walking;
+    if (x.need_q && (count >= qc || fin)) {         // deflate.c:1390-1392 (chain >>= 2)
+        rq[x.p] = match_rec(x.best, x.s4, x.bpos4);
+        x.need_q = false;
+    }
+    if (fin) {
+        dwp_finish(x, rf, rq);
+    } else if (x.best != x.best0) {                  // the quick reject now tests the new best
+        const char *Eb = reinterpret_cast<const char *>(E);
+        x.w.be4 = (x.best - 1) * 4;
+        x.w.scanE = E[x.s + x.best - 1] >> 16;
+        x.w.eb = *reinterpret_cast<const uint32_t *>(Eb + x.w.m4 + x.w.be4);
+    }
+}
+
+template <int kQ>
+__device__ __attribute__((always_inline)) inline void dwp_walk(const uint32_t *E, int64_t pa, int64_t na, int64_t pb,
+                                                               int64_t nb, bool live_b, int64_t B, const LevelCfg &cfg,
+                                                               uint32_t *rf, uint32_t *rq, int want_q, int64_t max_dist) {
+    const uint32_t chain = (uint32_t)cfg.chain;
+    const uint32_t qc = want_q ? chain >> 2 : chain;
+    DWP<kQ> a, b;
+    dwp_init(a, E, pa, true, B, na, cfg, rf, rq, want_q, max_dist);
+    dwp_init(b, E, pb, live_b, B, nb, cfg, rf, rq, want_q, max_dist);
+    uint32_t count = 0;
+#pragma unroll
+    for (int k = 0; k < kD0; k++) {                 // the chains' heads, compared by the whole wave
+        dwp_head(a, E, count, chain, qc, rq);
+        dwp_head(b, E, count, chain, qc, rq);
+        count++;
+    }
+    if (a.live && !a.walking) dwp_finish(a, rf, rq);
+    if (b.live && !b.walking) dwp_finish(b, rf, rq);
+    if (!a.live && !b.live) return;
+    dwp_arm(a, E);
+    dwp_arm(b, E);
+    const char *Eb = reinterpret_cast<const char *>(E);
+    for (;;) {
+        const uint32_t end = count < qc ? qc : chain;
+        a.best0 = a.best;
+        b.best0 = b.best;
+        for (;;) {
+            const bool wa = dwq_step1(a.w, Eb);
+            const bool wb = dwq_step1(b.w, Eb);
+            count++;
+            const uint64_t walkers = __ballot(wa | wb), full = __ballot((a.w.occ == kQ) | (b.w.occ == kQ));
+            if (count >= end || walkers == 0 || full != 0) break;
+        }
+        a.walking = a.walking && a.w.m4 > a.w.limit4 && count < chain;
+        b.walking = b.walking && b.w.m4 > b.w.limit4 && count < chain;
+        // every entry, oldest first: entry j (< occ) is the (occ - j)-th oldest
+#pragma unroll
+        for (int j = kQ - 1; j >= 0; j--) {
+            if (__ballot((j < a.w.occ) | (j < b.w.occ)) != 0) {
+                dwp_flush_one(a, E, j);
+                dwp_flush_one(b, E, j);
+            }
+        }
+        a.w.occ = 0;
+        b.w.occ = 0;
+        dwp_after(a, E, count, qc, rf, rq);
+        dwp_after(b, E, count, qc, rf, rq);
+        if (!a.live && !b.live) break;
+    }
+}
+
 __device__ unsigned long long g_mstat[4];   // kMatchStats statistics
 
 // k_match variants (ZGPU_MATCH_VARIANT, for A/B runs):
@@ -1060,6 +1248,9 @@ __device__ unsigned long long g_mstat[4];   // kMatchStats statistics
 //                 chain step needs no subtraction; the slide lowers every index
 //                 with one saturating packed subtract): 418 -> 411 ms
 //   50, 51        48 with an 8-deep (407 ms) or 3-deep (407 ms) queue
+//   52            49 with two positions per lane stepping in one loop (two
+//                 LDS round trips in flight per lane): 463 vs 403 ms -- the
+//                 doubled step and flush work costs more than the overlap wins
 //   40            19 with deferred compares (dw_walk): 495 -> 412 ms per 4 GiB
 //                 C4 sub-batch at L6 (the C4 shard 7.7 -> 9.1 GB/s)
 //   41            40 plus statistics (wave iterations, flushes, flush rounds)
@@ -1096,7 +1287,7 @@ __device__ unsigned long long g_mstat[4];   // kMatchStats statistics
 //                 latency-bound at the 16 waves the LDS window allows)
 constexpr int kMatchDefer = 40, kMatchDeferStats = 41, kMatchDefer3 = 42, kMatchDeferP = 43, kMatchDeferPStats = 44,
               kMatchProbeNoFlush = 45, kMatchDeferR = 46, kMatchDeferB = 47, kMatchDeferIdx = 48,
-              kMatchQ6 = 49, kMatchQ8 = 50, kMatchQ3 = 51;
+              kMatchQ6 = 49, kMatchQ8 = 50, kMatchQ3 = 51, kMatchPair = 52;
 constexpr int kMatchWalk = 19;
 constexpr int kMatchDefault = kMatchQ6;
 constexpr int kMatchStats = 21, kMatchProbeNoWalk = 33, kMatchProbeHalf = 35,
@@ -1180,7 +1371,8 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
     for (int64_t ts = t0; ts < s1; ts += kMT) {
         const int64_t B = ts - kMW;
         const int tile_n = kSegs && ts < s0 ? 0 : (int)((n - ts) < kMT ? (n - ts) : kMT);   // 0: staging only
-        tile_store<kVariant == kMatchDeferIdx || kVariant == kMatchQ6 || kVariant == kMatchQ8 || kVariant == kMatchQ3>(
+        tile_store<kVariant == kMatchDeferIdx || kVariant == kMatchQ6 || kVariant == kMatchQ8 || kVariant == kMatchQ3 ||
+                   kVariant == kMatchPair>(
             E, P, ts, tid);
         if (tid == 0) next_i = 0;
         if (kSorted && tid < kSortBuckets) s_hist[tid] = 0;
@@ -1220,6 +1412,17 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
         if (ts + kMT < s1) tile_prefetch(P, ts + kMT, n, in, L, K, tid);   // lands during the walks
         for (;;) {
             if (kVariant == kMatchProbeHalf && tid >= kMatchThreads / 2) break;   // probe: half the waves walk
+            if (kVariant == kMatchPair) {              // two adjacent positions of the key order per lane
+                const int i = atomicAdd(&next_i, 2);
+                if (i >= tile_n) break;
+                const bool live_b = i + 1 < tile_n;
+                const int64_t pa = ts + (int)s_perm[i];
+                const int64_t pb = live_b ? ts + (int)s_perm[i + 1] : pa;
+                const int64_t na = kEv ? flush_limit(job, pa, n) : n;
+                const int64_t nb = kEv ? flush_limit(job, pb, n) : n;
+                dwp_walk<6>(E, pa, na, pb, nb, live_b, B, cfg, rf, rq, want_q, max_dist);
+                continue;
+            }
             const int i = atomicAdd(&next_i, 1);
             if (i >= tile_n) break;
             const int64_t p = ts + (kSorted ? (int)s_perm[i] : i);
@@ -2944,7 +3147,8 @@ static int match_variant() {
         return (x == 14 || x == kMatchWalk || x == kMatchStats || x == kMatchProbeNoWalk || x == kMatchProbeHalf ||
                 x == kMatchProbeNoCmp || x == kMatchProbeCmpOnly || x == kMatchDefer || x == kMatchDeferStats || x == kMatchDefer3 || x == kMatchDeferP ||
                 x == kMatchDeferPStats || x == kMatchProbeNoFlush || x == kMatchDeferR ||
-                x == kMatchDeferB || x == kMatchDeferIdx || x == kMatchQ6 || x == kMatchQ8 || x == kMatchQ3)
+                x == kMatchDeferB || x == kMatchDeferIdx || x == kMatchQ6 || x == kMatchQ8 || x == kMatchQ3 ||
+                x == kMatchPair)
                    ? x : kMatchDefault;
     }();
     return v;
@@ -2982,6 +3186,8 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
             hipLaunchKernelGGL(k_match<kMatchQ8>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchQ3) {
             hipLaunchKernelGGL(k_match<kMatchQ3>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchPair) {
+            hipLaunchKernelGGL(k_match<kMatchPair>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchDeferR) {
             hipLaunchKernelGGL(k_match<kMatchDeferR>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchProbeNoFlush) {
