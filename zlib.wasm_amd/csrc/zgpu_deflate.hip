@@ -2371,9 +2371,21 @@ __global__ __launch_bounds__(64) void k_parse_ev(DeflateJob job) {
 // link loaded in the same round trip.
 // ------------------------------------------------------------------------
 // kEv: a flush job (events, a resumed start, late hashing); batch jobs run
-// the <false> instance, whose loop carries none of that
-template <bool kEv>
+// the <false> instance, whose loop carries none of that.
+// kHC (ZGPU_FAST_VARIANT): 0 every INSERT_STRING loads head[] from memory (the
+// round-1/2 walk); 1 head cache (below); 2 head cache plus the first chain
+// candidate's link and 4 bytes prefetched for all 64 positions of a block;
+// 3 (default) 2 with deferred stores: a block's prev[] entries and head[]
+// updates are kept in lanes and written when the next block is set up, the
+// symbols 64 at a time (measured: no faster than 0);
+// 4 (default) the round-1/2 walk with one memory round trip per candidate: the
+// link and the candidate's 64 bytes are loaded together (the link used to be
+// made uniform before the bytes were requested, two round trips), the bytes
+// with a clamped index instead of a bounds branch, and the scan side of the
+// compare fetched once per position instead of once per candidate.
+template <bool kEv, int kHC>
 __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *heads) {
+    constexpr bool kCache = kHC >= 1 && kHC <= 3, kPre = kHC == 2 || kHC == 3, kDefer = kHC == 3;
     const int lane = threadIdx.x;
     const bool lead = lane == 0;
     const uint32_t bi = blockIdx.x;
@@ -2420,9 +2432,79 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         return (uint32_t)__builtin_amdgcn_readlane((int)(o < 64 ? w0 : w1), o & 63);
     };
     auto whash = [&](int64_t q) -> uint32_t { return hashp(wbyte(q), wbyte(q + 1), wbyte(q + 2), wp); };
+    // Head cache (kCache).  Block [cb, cb + 64) of positions: lane j holds
+    // ch = hash(cb + j) and cv = head[ch] as it stood when the block was set
+    // up; bit j of cins is set once cb + j has been inserted.  zlib inserts in
+    // position order (deflate.c:1849-1897), so a block set up at its first
+    // cached insertion has seen every earlier one in cv, and INSERT_STRING of
+    // q = cb + j finds head[hash] as the newest inserted block position below
+    // q with q's hash (one ballot), else cv[j]: no memory round trip.  Every
+    // insertion still stores head[] and prev[], so memory stays current for
+    // the next block's setup and for the chain walks.
+    int64_t cb = INT64_MIN / 2;
+    uint32_t ch = 0, cv = 0, pv = 0, cw = 0;
+    uint64_t cins = 0;
+    int64_t hit_j = -1;                                  // block lane of the last insert's cv hit
+    uint32_t pbuf = 0;                                   // kHC 3: prev[cb + lane], not yet stored
+    // kHC 3: store the block's insertions: every prev[] entry, and head[h]
+    // from the newest inserted lane with hash h (a lane is dropped when a
+    // higher inserted lane has its hash; plain stores, as a direct insert makes)
+    auto flush_block = [&]() {
+        if (kDefer && cins) {
+            const bool ins = (cins >> lane) & 1ull;
+            bool newest = ins;
+            for (uint64_t r = cins & (cins - 1); r; r &= r - 1) {   // inserted lanes above the lowest
+                const int k = __builtin_ctzll(r);
+                newest = newest && !(lane < k && ch == (uint32_t)__builtin_amdgcn_readlane((int)ch, k));
+            }
+            if (ins) prev[cb + lane] = (uint16_t)pbuf;
+            if (newest) head[ch] = (uint32_t)(cb + lane);
+        }
+        cins = 0;
+    };
+    auto setup = [&]() {                                 // block at the window base (wsee just ran)
+        flush_block();
+        const int l1 = (lane + 1) & 63, l2 = (lane + 2) & 63;
+        const uint32_t a1 = (uint32_t)__shfl((int)w0, l1, 64), b1 = (uint32_t)__shfl((int)w1, l1, 64);
+        const uint32_t a2 = (uint32_t)__shfl((int)w0, l2, 64), b2 = (uint32_t)__shfl((int)w1, l2, 64);
+        ch = hashp(w0, lane + 1 < 64 ? a1 : b1, lane + 2 < 64 ? a2 : b2, wp);
+        cb = wb;
+        cins = 0;
+        cv = head[ch];
+        if (kPre) {                                  // the first candidate's link and bytes 0..3
+            const int64_t c = cv;
+            pv = c ? (uint32_t)prev[c] : 0u;
+            cw = c ? (uint32_t)in[c] | (uint32_t)in[c + 1] << 8 | (uint32_t)in[c + 2] << 16 |
+                     (uint32_t)in[c + 3] << 24 : 0u;
+        }
+    };
     auto insert = [&](int64_t q) -> int64_t {           // INSERT_STRING
-        const uint32_t h = whash(q);
-        const int64_t hh = ufl(head[h]);
+        int64_t hh;
+        uint32_t h;
+        hit_j = -1;
+        if (kCache && (q - cb >= 64 || q < cb) && wb == (q & ~(int64_t)63)) setup();
+        if (kCache && q >= cb && q - cb < 64) {
+            const int j = (int)(q - cb);
+            h = (uint32_t)__builtin_amdgcn_readlane((int)ch, j);
+            const uint64_t m = __ballot(lane < j && ((cins >> lane) & 1ull) && ch == h);
+            if (m) {
+                hh = cb + 63 - __builtin_clzll(m);
+            } else {
+                hh = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)cv, j);
+                hit_j = j;
+            }
+            cins |= 1ull << j;
+            if (kDefer) {
+                const int64_t d = q - hh;
+                const uint32_t pvq = (hh != 0 && d <= 32767) ? (uint32_t)d : 0u;
+                pbuf = lane == j ? pvq : pbuf;
+                return hh;
+            }
+        } else {
+            if (kDefer) { flush_block(); cb = INT64_MIN / 2; }   // memory current before a direct insert
+            h = whash(q);
+            hh = ufl(head[h]);
+        }
         const int64_t d = q - hh;
         if (lead) {
             prev[q] = (hh != 0 && d <= 32767) ? (uint16_t)d : 0;
@@ -2449,7 +2531,29 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         }
         return maxcmp;
     };
+    auto common_from = [&](int64_t a, int64_t pp, int maxcmp, int k0) -> int {   // bytes k0.. from memory
+        for (; k0 < maxcmp; k0 += 64) {
+            const int k = k0 + lane;
+            const int kc = k < maxcmp ? k : maxcmp - 1;
+            const bool diff = k < maxcmp && in[a + kc] != in[pp + kc];
+            const uint64_t m = __ballot(diff);
+            if (m) return k0 + __builtin_ctzll(m);
+        }
+        return maxcmp;
+    };
 
+    // _tr_tally; kHC 3 keeps symbol nsym in lane nsym % 64 and stores 64 at once
+    uint32_t sbuf = 0;
+    auto tally = [&](uint32_t v) -> bool {
+        if (kDefer) {
+            const uint32_t k = po.nsym & 63u;
+            sbuf = (uint32_t)lane == k ? v : sbuf;
+            if (k == 63u) po.sym[(po.nsym & ~63u) + lane] = sbuf;
+            po.nsym++;
+            return ++po.blk_nsym == po.sym_limit;
+        }
+        return po.tally(v);
+    };
     if (kEv && job.dict)                                  // a preset dictionary's strings
         for (int64_t q = 0; q < (int64_t)job.pre_ins; q++) {
             wsee(q);
@@ -2466,6 +2570,8 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     // marker record snap[hsize]): a later job resumes there
     auto snapshot = [&]() {
         if (!kEv || !job.snap) return;
+        flush_block();
+        cb = INT64_MIN / 2;
         __threadfence_block();
         for (uint32_t i = (uint32_t)lane; i < hsize; i += 64) job.snap[i] = head[i];
         if (lead) job.snap[hsize] = po.nblk - 1;
@@ -2532,9 +2638,44 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
             const int maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
             int best = kMinMatch - 1;
             int64_t cur = hh;
+            // kHC 2: the first candidate is cv[j] (no newer block position had
+            // the hash), its link and first 4 bytes are in registers
+            int64_t pre = kPre ? hit_j : -1;
+            uint32_t sb = 0;
+            const int lc = lane < maxcmp ? lane : maxcmp - 1;
+            if (kHC == 4) {                              // scan bytes p + lane, from the register window
+                const int o = (int)(p - wb) + lane;
+                const uint32_t x0 = (uint32_t)__shfl((int)w0, o & 63, 64), x1 = (uint32_t)__shfl((int)w1, o & 63, 64);
+                sb = o < 64 ? x0 : x1;
+            }
             for (;;) {
-                const uint32_t d = ufl(prev[cur]);
-                const int k = common(cur, p, maxcmp);
+                uint32_t d;
+                int k;
+                if (kHC == 4) {
+                    // link and candidate bytes in one round trip; cur + lc < n
+                    // since cur < p and maxcmp <= n - p
+                    const uint32_t dv = prev[cur];
+                    const uint32_t cbyte = in[cur + lc];
+                    const uint64_t m = __ballot(lane < maxcmp && cbyte != sb);
+                    k = m ? (int)__builtin_ctzll(m) : common_from(cur, p, maxcmp, 64);
+                    d = ufl(dv);
+                } else if (kPre && pre >= 0) {
+                    const int j = (int)pre;
+                    pre = -1;
+                    d = (uint32_t)__builtin_amdgcn_readlane((int)pv, j);
+                    const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)cw, j) ^
+                                       (wbyte(p) | wbyte(p + 1) << 8 | wbyte(p + 2) << 16 | wbyte(p + 3) << 24);
+                    const int q4 = x ? (int)(__builtin_ctz(x) >> 3) : 4;
+                    k = q4 < kMinMatch ? q4 : common(cur, p, maxcmp);   // a quick reject needs no round trip
+                } else {
+                    if (kDefer && cur >= cb && cur - cb < 64 && ((cins >> (cur - cb)) & 1ull))
+                        // a link not stored yet (a block position inserted before
+                        // the block's setup is in memory)
+                        d = (uint32_t)__builtin_amdgcn_readlane((int)pbuf, (int)(cur - cb));
+                    else
+                        d = ufl(prev[cur]);
+                    k = common(cur, p, maxcmp);
+                }
                 if (k > best) {
                     match_start = cur;
                     best = k;
@@ -2548,7 +2689,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         }
         bool bflush;
         if (match_length >= kMinMatch) {
-            bflush = po.tally(((uint32_t)(p - match_start) << 8) | (match_length - kMinMatch));
+            bflush = tally(((uint32_t)(p - match_start) << 8) | (match_length - kMinMatch));
             lookahead -= match_length;
             if (match_length <= cfg.lazy && lookahead >= kMinMatch && match_length <= 48) {
                 // positions p+1 .. p+len-1 (at most 5 unless deflateTune), one
@@ -2556,27 +2697,38 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
                 // hash a lower lane also inserts takes that lane's position (zlib
                 // inserts in order)
                 const uint32_t cntk = match_length - 1;
-                const bool mine = (uint32_t)lane < cntk;
-                const int64_t q = p + 1 + lane;
-                uint32_t h = 0xffffffffu;
-                for (uint32_t k = 0; k < cntk; k++) {
-                    const uint32_t hk = whash(p + 1 + k);
-                    if ((uint32_t)lane == k) h = hk;
-                }
-                const int64_t hh0 = mine ? (int64_t)head[h] : 0;
-                int64_t hq = hh0;
-                bool last = mine;
-                for (uint32_t k = 0; k < cntk; k++) {
-                    const uint32_t hk = (uint32_t)__shfl((int)h, (int)k, 64);
-                    if (mine && hk == h) {
-                        if (k < (uint32_t)lane) hq = p + 1 + k;        // a lower lane's position
-                        if (k > (uint32_t)lane) last = false;          // a higher lane writes head
+                if (kCache && p >= cb && p + (int64_t)cntk - cb < 64) {
+                    // all in the cached block: one at a time, no memory round trip
+                    for (uint32_t k = 1; k <= cntk; k++) insert(p + k);
+                } else {
+                    if (kDefer) { flush_block(); cb = INT64_MIN / 2; }   // memory current first
+                    const bool mine = (uint32_t)lane < cntk;
+                    const int64_t q = p + 1 + lane;
+                    uint32_t h = 0xffffffffu;
+                    for (uint32_t k = 0; k < cntk; k++) {
+                        const uint32_t hk = whash(p + 1 + k);
+                        if ((uint32_t)lane == k) h = hk;
                     }
-                }
-                if (mine) {
-                    const int64_t dd = q - hq;
-                    prev[q] = (hq != 0 && dd <= 32767) ? (uint16_t)dd : 0;
-                    if (last) head[h] = (uint32_t)q;
+                    const int64_t hh0 = mine ? (int64_t)head[h] : 0;
+                    int64_t hq = hh0;
+                    bool last = mine;
+                    for (uint32_t k = 0; k < cntk; k++) {
+                        const uint32_t hk = (uint32_t)__shfl((int)h, (int)k, 64);
+                        if (mine && hk == h) {
+                            if (k < (uint32_t)lane) hq = p + 1 + k;        // a lower lane's position
+                            if (k > (uint32_t)lane) last = false;          // a higher lane writes head
+                        }
+                    }
+                    if (mine) {
+                        const int64_t dd = q - hq;
+                        prev[q] = (hq != 0 && dd <= 32767) ? (uint16_t)dd : 0;
+                        if (last) head[h] = (uint32_t)q;
+                    }
+                    if (kCache)                        // the cached block's inserted positions
+                        for (uint32_t k = 1; k <= cntk; k++) {
+                            const int64_t qk = p + k;
+                            if (qk >= cb && qk - cb < 64) cins |= 1ull << (qk - cb);
+                        }
                 }
             } else if (match_length <= cfg.lazy && lookahead >= kMinMatch) {
                 // deflateTune's longer max_insert_length: one insert at a time
@@ -2588,7 +2740,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
             p += match_length;
             match_length = 0;
         } else {
-            bflush = po.tally(wbyte(p));
+            bflush = tally(wbyte(p));
             p++;
         }
         if (bflush) {
@@ -2601,6 +2753,8 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
             }
         }
     }
+    flush_block();
+    if (kDefer && (po.nsym & 63u) && (uint32_t)lane < (po.nsym & 63u)) po.sym[(po.nsym & ~63u) + lane] = sbuf;
     if (!kEv || !job.open_end) po.flush(p, true);
     if (lead) job.nblocks[bi] = po.nblk;
 }
@@ -3238,10 +3392,31 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     case 2: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 0); break;
     case 5: hipLaunchKernelGGL(k_parse_seg, grid, dim3(kParseLanes), 0, st, job); break;
     case 6: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 1); break;
-    case 3:
-        if (job.nfl || job.start || job.srec) hipLaunchKernelGGL(k_parse_fast<true>, grid, dim3(64), 0, st, job, heads);
-        else hipLaunchKernelGGL(k_parse_fast<false>, grid, dim3(64), 0, st, job, heads);
+    case 3: {
+        static const int fv = [] {                   // k_parse_fast variant (A/B runs), default 4
+            const char *e = getenv("ZGPU_FAST_VARIANT");
+            const int v = e ? atoi(e) : 4;
+            return v >= 0 && v <= 4 ? v : 4;
+        }();
+        const bool ev = job.nfl || job.start || job.srec;
+        if (fv == 0) {
+            if (ev) hipLaunchKernelGGL((k_parse_fast<true, 0>), grid, dim3(64), 0, st, job, heads);
+            else hipLaunchKernelGGL((k_parse_fast<false, 0>), grid, dim3(64), 0, st, job, heads);
+        } else if (fv == 1) {
+            if (ev) hipLaunchKernelGGL((k_parse_fast<true, 1>), grid, dim3(64), 0, st, job, heads);
+            else hipLaunchKernelGGL((k_parse_fast<false, 1>), grid, dim3(64), 0, st, job, heads);
+        } else if (fv == 2) {
+            if (ev) hipLaunchKernelGGL((k_parse_fast<true, 2>), grid, dim3(64), 0, st, job, heads);
+            else hipLaunchKernelGGL((k_parse_fast<false, 2>), grid, dim3(64), 0, st, job, heads);
+        } else if (fv == 3) {
+            if (ev) hipLaunchKernelGGL((k_parse_fast<true, 3>), grid, dim3(64), 0, st, job, heads);
+            else hipLaunchKernelGGL((k_parse_fast<false, 3>), grid, dim3(64), 0, st, job, heads);
+        } else {
+            if (ev) hipLaunchKernelGGL((k_parse_fast<true, 4>), grid, dim3(64), 0, st, job, heads);
+            else hipLaunchKernelGGL((k_parse_fast<false, 4>), grid, dim3(64), 0, st, job, heads);
+        }
         break;
+    }
     case 4: hipLaunchKernelGGL(k_encode, grid, dim3(kEncThreads), 0, st, job); break;
     case 7: hipLaunchKernelGGL(k_parse_huff, grid, dim3(kHuffThreads), 0, st, job); break;
     case 8: hipLaunchKernelGGL(k_parse_rle, grid, dim3(64), 0, st, job); break;
