@@ -602,6 +602,9 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         job.pstate = slow ? (slot ? c.ws_state2 : c.ws_state).as<uint32_t>() : nullptr;
         job.blocks = c.ws_blk.as<BlockRec>();
         job.nblocks = d_nblk;
+        job.pos31 = 1;
+        for (uint32_t i = a; i < b; i++)
+            if (lens[i] >= (1ull << 31) - (1ull << 16)) job.pos31 = 0;
         job.check = d_check;
         if (seg_at[s + 1] > seg_at[s]) {
             job.seg = c.ws_seg.as<uint32_t>() + 2 * seg_at[s];

@@ -1492,17 +1492,18 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
 // ------------------------------------------------------------------------
 // block bookkeeping shared by both parses (lane 0 only)
 // ------------------------------------------------------------------------
-struct ParseOut {
+template <typename P>
+struct ParseOutT {
     uint32_t *sym;
     BlockRec *blk;
     uint32_t nsym, blk_nsym, blk_sym_start, nblk;
-    int64_t block_start, S, E;
-    int64_t wsize, max_dist;      // w_size, MAX_DIST (deflate.c:440-444)
+    P block_start, S, E;
+    P wsize, max_dist;      // w_size, MAX_DIST (deflate.c:440-444)
     uint32_t sym_limit;           // lit_bufsize - 1 (deflate.c:455, deflate.h:371)
     bool lead;               // the lane that stores (the state itself is wave-uniform)
     uint64_t *srec = nullptr;     // a streaming job's records (DeflateJob::srec)
 
-    __device__ inline void rec(int64_t strstart, bool res) {      // srec[4 nblk + 2, + 3]
+    __device__ inline void rec(P strstart, bool res) {      // srec[4 nblk + 2, + 3]
         if (lead && srec) {
             srec[4ull * nblk + 2] = ((uint64_t)S << 32) | (uint64_t)strstart;
             srec[4ull * nblk + 3] = (uint64_t)E | (res ? 1ull << 63 : 0ull);
@@ -1515,7 +1516,7 @@ struct ParseOut {
         nsym++;
         return ++blk_nsym == sym_limit;
     }
-    __device__ inline void flush(int64_t strstart, bool last) {   // FLUSH_BLOCK_ONLY
+    __device__ inline void flush(P strstart, bool last) {   // FLUSH_BLOCK_ONLY
         BlockRec r;
         r.sym_start = blk_sym_start;
         r.nsym = blk_nsym;
@@ -1531,7 +1532,7 @@ struct ParseOut {
         blk_nsym = 0;
     }
     // the bits a deflate(flush) call appends after its blocks (kBlkMarker)
-    __device__ inline void marker(int64_t strstart, uint32_t kind) {
+    __device__ inline void marker(P strstart, uint32_t kind) {
         BlockRec r;
         r.sym_start = blk_sym_start;
         r.nsym = 0;
@@ -1544,11 +1545,12 @@ struct ParseOut {
     }
     // fill_window (deflate.c:251-368), bookkeeping only; n = the end of the
     // input deflate() has been given so far
-    __device__ inline void fill(int64_t p, int64_t n) {
+    __device__ inline void fill(P p, P n) {
         if (p - S >= wsize + max_dist) S += wsize;
-        if (E < n) { int64_t e = S + 2 * wsize; E = e < n ? e : n; }
+        if (E < n) { P e = S + 2 * wsize; E = e < n ? e : n; }
     }
 };
+using ParseOut = ParseOutT<int64_t>;
 
 
 // ------------------------------------------------------------------------
@@ -2372,25 +2374,24 @@ __global__ __launch_bounds__(64) void k_parse_ev(DeflateJob job) {
 // ------------------------------------------------------------------------
 // kEv: a flush job (events, a resumed start, late hashing); batch jobs run
 // the <false> instance, whose loop carries none of that.
-// kHC (ZGPU_FAST_VARIANT): 0 every INSERT_STRING loads head[] from memory (the
-// round-1/2 walk); 1 head cache (below); 2 head cache plus the first chain
-// candidate's link and 4 bytes prefetched for all 64 positions of a block;
-// 3 (default) 2 with deferred stores: a block's prev[] entries and head[]
-// updates are kept in lanes and written when the next block is set up, the
-// symbols 64 at a time (measured: no faster than 0);
-// 4 (default) the round-1/2 walk with one memory round trip per candidate: the
-// link and the candidate's 64 bytes are loaded together (the link used to be
-// made uniform before the bytes were requested, two round trips), the bytes
-// with a clamped index instead of a bounds branch, and the scan side of the
-// compare fetched once per position instead of once per candidate.
-template <bool kEv, int kHC>
+// kOne (the default; ZGPU_FAST_VARIANT=0 runs the round-2 walk for A/B): one
+// memory round trip per chain candidate.  The link and the candidate's 64
+// bytes are loaded together (the round-2 walk made the link uniform before it
+// requested the bytes: two round trips), the bytes through a clamped index
+// instead of a bounds branch, and the scan side of the compare is taken from
+// the register window once per position instead of once per candidate.
+// P: the position type.  A batch whose buffers are all under 2^31 bytes
+// (DeflateJob::pos31) runs on int32_t: the parse is one wave-uniform program
+// whose state lives in SGPRs, and 64-bit positions doubled its scalar
+// arithmetic (add/addc pairs, 64-bit compares) -- at 28 waves per CU sharing
+// one scalar unit, scalar issue is what bounds it.
+template <bool kEv, bool kOne, typename P>
 __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *heads) {
-    constexpr bool kCache = kHC >= 1 && kHC <= 3, kPre = kHC == 2 || kHC == 3, kDefer = kHC == 3;
     const int lane = threadIdx.x;
     const bool lead = lane == 0;
     const uint32_t bi = blockIdx.x;
     const uint32_t g = job.first + bi;
-    const int64_t n = (int64_t)job.src_len[g];
+    const P n = (P)job.src_len[g];
     const uint8_t *in = job.src + job.src_off[g];
     uint16_t *prev = job.link + job.ws_off[bi];
     const WinP wp = job_win(job);
@@ -2404,108 +2405,38 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     __threadfence_block();
     __syncthreads();
 
-    ParseOut po;
+    ParseOutT<P> po;
     po.sym = job.sym + job.ws_off[bi];
     po.blk = job.blocks + job.blk_off[bi];
     po.nsym = po.blk_nsym = po.blk_sym_start = po.nblk = 0;
     po.win(job_win(job));
-    const int64_t start = kEv ? (int64_t)job.start : 0;
-    po.block_start = start; po.S = 0; po.E = kEv && (int64_t)job.e0 > start ? (int64_t)job.e0 : start;
+    const P start = kEv ? (P)job.start : 0;
+    po.block_start = start; po.S = 0; po.E = kEv && (P)job.e0 > start ? (P)job.e0 : start;
     po.lead = lead;
     if (kEv) po.srec = job.srec;
 
     // input window in registers: lane j holds in[wb + j] (w0) and in[wb + 64 + j]
     // (w1); it is moved forward 64 bytes at a time, so hashing and the scan side
     // of a compare need no memory round trip
-    int64_t wb = -128;
+    P wb = -128;
     uint32_t w0 = 0, w1 = 0;
-    auto ld = [&](int64_t x) -> uint32_t { return x < n ? (uint32_t)in[x] : 0u; };
-    auto wsee = [&](int64_t x) {                        // make [x, x + 66) resident
+    auto ld = [&](P x) -> uint32_t { return x < n ? (uint32_t)in[x] : 0u; };
+    auto wsee = [&](P x) {                        // make [x, x + 66) resident
         if (x >= wb && x + 66 <= wb + 128) return;
-        const int64_t nb = x & ~(int64_t)63;
+        const P nb = x & ~(P)63;
         if (nb == wb + 64) { w0 = w1; w1 = ld(nb + 64 + lane); }
         else { w0 = ld(nb + lane); w1 = ld(nb + 64 + lane); }
         wb = nb;
     };
-    auto wbyte = [&](int64_t x) -> uint32_t {           // uniform x in the window
+    auto wbyte = [&](P x) -> uint32_t {           // uniform x in the window
         const int o = (int)(x - wb);
         return (uint32_t)__builtin_amdgcn_readlane((int)(o < 64 ? w0 : w1), o & 63);
     };
-    auto whash = [&](int64_t q) -> uint32_t { return hashp(wbyte(q), wbyte(q + 1), wbyte(q + 2), wp); };
-    // Head cache (kCache).  Block [cb, cb + 64) of positions: lane j holds
-    // ch = hash(cb + j) and cv = head[ch] as it stood when the block was set
-    // up; bit j of cins is set once cb + j has been inserted.  zlib inserts in
-    // position order (deflate.c:1849-1897), so a block set up at its first
-    // cached insertion has seen every earlier one in cv, and INSERT_STRING of
-    // q = cb + j finds head[hash] as the newest inserted block position below
-    // q with q's hash (one ballot), else cv[j]: no memory round trip.  Every
-    // insertion still stores head[] and prev[], so memory stays current for
-    // the next block's setup and for the chain walks.
-    int64_t cb = INT64_MIN / 2;
-    uint32_t ch = 0, cv = 0, pv = 0, cw = 0;
-    uint64_t cins = 0;
-    int64_t hit_j = -1;                                  // block lane of the last insert's cv hit
-    uint32_t pbuf = 0;                                   // kHC 3: prev[cb + lane], not yet stored
-    // kHC 3: store the block's insertions: every prev[] entry, and head[h]
-    // from the newest inserted lane with hash h (a lane is dropped when a
-    // higher inserted lane has its hash; plain stores, as a direct insert makes)
-    auto flush_block = [&]() {
-        if (kDefer && cins) {
-            const bool ins = (cins >> lane) & 1ull;
-            bool newest = ins;
-            for (uint64_t r = cins & (cins - 1); r; r &= r - 1) {   // inserted lanes above the lowest
-                const int k = __builtin_ctzll(r);
-                newest = newest && !(lane < k && ch == (uint32_t)__builtin_amdgcn_readlane((int)ch, k));
-            }
-            if (ins) prev[cb + lane] = (uint16_t)pbuf;
-            if (newest) head[ch] = (uint32_t)(cb + lane);
-        }
-        cins = 0;
-    };
-    auto setup = [&]() {                                 // block at the window base (wsee just ran)
-        flush_block();
-        const int l1 = (lane + 1) & 63, l2 = (lane + 2) & 63;
-        const uint32_t a1 = (uint32_t)__shfl((int)w0, l1, 64), b1 = (uint32_t)__shfl((int)w1, l1, 64);
-        const uint32_t a2 = (uint32_t)__shfl((int)w0, l2, 64), b2 = (uint32_t)__shfl((int)w1, l2, 64);
-        ch = hashp(w0, lane + 1 < 64 ? a1 : b1, lane + 2 < 64 ? a2 : b2, wp);
-        cb = wb;
-        cins = 0;
-        cv = head[ch];
-        if (kPre) {                                  // the first candidate's link and bytes 0..3
-            const int64_t c = cv;
-            pv = c ? (uint32_t)prev[c] : 0u;
-            cw = c ? (uint32_t)in[c] | (uint32_t)in[c + 1] << 8 | (uint32_t)in[c + 2] << 16 |
-                     (uint32_t)in[c + 3] << 24 : 0u;
-        }
-    };
-    auto insert = [&](int64_t q) -> int64_t {           // INSERT_STRING
-        int64_t hh;
-        uint32_t h;
-        hit_j = -1;
-        if (kCache && (q - cb >= 64 || q < cb) && wb == (q & ~(int64_t)63)) setup();
-        if (kCache && q >= cb && q - cb < 64) {
-            const int j = (int)(q - cb);
-            h = (uint32_t)__builtin_amdgcn_readlane((int)ch, j);
-            const uint64_t m = __ballot(lane < j && ((cins >> lane) & 1ull) && ch == h);
-            if (m) {
-                hh = cb + 63 - __builtin_clzll(m);
-            } else {
-                hh = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)cv, j);
-                hit_j = j;
-            }
-            cins |= 1ull << j;
-            if (kDefer) {
-                const int64_t d = q - hh;
-                const uint32_t pvq = (hh != 0 && d <= 32767) ? (uint32_t)d : 0u;
-                pbuf = lane == j ? pvq : pbuf;
-                return hh;
-            }
-        } else {
-            if (kDefer) { flush_block(); cb = INT64_MIN / 2; }   // memory current before a direct insert
-            h = whash(q);
-            hh = ufl(head[h]);
-        }
-        const int64_t d = q - hh;
+    auto whash = [&](P q) -> uint32_t { return hashp(wbyte(q), wbyte(q + 1), wbyte(q + 2), wp); };
+    auto insert = [&](P q) -> P {           // INSERT_STRING
+        const uint32_t h = whash(q);
+        const P hh = ufl(head[h]);
+        const P d = q - hh;
         if (lead) {
             prev[q] = (hh != 0 && d <= 32767) ? (uint16_t)d : 0;
             head[h] = (uint32_t)q;
@@ -2514,7 +2445,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     };
     // common prefix of in[a..] and in[p..], capped at maxcmp (a < p); the scan
     // side of the first 64 bytes comes from the register window
-    auto common = [&](int64_t a, int64_t pp, int maxcmp) -> int {
+    auto common = [&](P a, P pp, int maxcmp) -> int {
         const int o = (int)(pp - wb) + lane;            // < 128 + 63
         const uint32_t x0 = (uint32_t)__shfl((int)w0, o & 63, 64), x1 = (uint32_t)__shfl((int)w1, o & 63, 64);
         const uint32_t sb = o < 64 ? x0 : x1;           // wsee(pp): pp - wb <= 62
@@ -2531,47 +2462,32 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         }
         return maxcmp;
     };
-    auto common_from = [&](int64_t a, int64_t pp, int maxcmp, int k0) -> int {   // bytes k0.. from memory
+    auto common_from = [&](P a, P pp, int maxcmp, int k0) -> int {   // bytes k0.. from memory
         for (; k0 < maxcmp; k0 += 64) {
-            const int k = k0 + lane;
-            const int kc = k < maxcmp ? k : maxcmp - 1;
-            const bool diff = k < maxcmp && in[a + kc] != in[pp + kc];
-            const uint64_t m = __ballot(diff);
+            const int kk = k0 + lane;
+            const int kc = kk < maxcmp ? kk : maxcmp - 1;
+            const uint64_t m = __ballot(kk < maxcmp && in[a + kc] != in[pp + kc]);
             if (m) return k0 + __builtin_ctzll(m);
         }
         return maxcmp;
     };
 
-    // _tr_tally; kHC 3 keeps symbol nsym in lane nsym % 64 and stores 64 at once
-    uint32_t sbuf = 0;
-    auto tally = [&](uint32_t v) -> bool {
-        if (kDefer) {
-            const uint32_t k = po.nsym & 63u;
-            sbuf = (uint32_t)lane == k ? v : sbuf;
-            if (k == 63u) po.sym[(po.nsym & ~63u) + lane] = sbuf;
-            po.nsym++;
-            return ++po.blk_nsym == po.sym_limit;
-        }
-        return po.tally(v);
-    };
     if (kEv && job.dict)                                  // a preset dictionary's strings
-        for (int64_t q = 0; q < (int64_t)job.pre_ins; q++) {
+        for (P q = 0; q < (P)job.pre_ins; q++) {
             wsee(q);
             insert(q);
         }
-    int64_t p = start, match_start = 0;
+    P p = start, match_start = 0;
     uint32_t match_length = kMinMatch - 1;
     FlushEv fe = flush_ev(job);
-    int64_t lim = kEv ? fe.limit(n) : n;       // input deflate() has been given
+    P lim = kEv ? (P)fe.limit(n) : n;   // input deflate() has been given
     // s->insert: strings a flush left unhashed (a resumed job starts right
     // after a flush at its window offset + start; none at a block cut)
-    int64_t pend = (kEv && job.cut) ? 0 : p < kMinMatch - 1 ? p : kMinMatch - 1;
+    P pend = (kEv && job.cut) ? 0 : p < kMinMatch - 1 ? p : kMinMatch - 1;
     // a streaming job keeps head[] as it stands at its last cut (the block or
     // marker record snap[hsize]): a later job resumes there
     auto snapshot = [&]() {
         if (!kEv || !job.snap) return;
-        flush_block();
-        cb = INT64_MIN / 2;
         __threadfence_block();
         for (uint32_t i = (uint32_t)lane; i < hsize; i += 64) job.snap[i] = head[i];
         if (lead) job.snap[hsize] = po.nblk - 1;
@@ -2582,7 +2498,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         // fill_window hashes the strings the last flush left unhashed once
         // new input is read (deflate.c:318-335)
         if (reads && pend && po.E - p + pend >= kMinMatch) {
-            int64_t str = p - pend;
+            P str = p - pend;
             while (pend) {
                 wsee(str);
                 insert(str);
@@ -2602,7 +2518,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
                 if (lead && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
                 fe.i++;
                 if (fe.i == fe.n && job.open_end) { done = true; break; }
-                lim = fe.limit(n);
+                lim = (P)fe.limit(n);
                 fill();
             }
             if (done) break;
@@ -2616,15 +2532,15 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
                     snapshot();
                     if (lead && job.flush_out) job.flush_out[2] = (uint64_t)po.S;
                     fe.i++;
-                    lim = fe.limit(n);
+                    lim = (P)fe.limit(n);
                     continue;
                 }
                 break;
             }
         }
         wsee(p);
-        int64_t lookahead = po.E - p;
-        int64_t hh = 0;
+        P lookahead = po.E - p;
+        P hh = 0;
         if (lookahead >= kMinMatch) hh = insert(p);
         if (hh > po.S && p - hh <= wp.max_dist) {
             // longest_match (deflate.c:1356-1497), prev_length == 2: the first
@@ -2632,18 +2548,15 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
             // prev_length stays MIN_MATCH-1 under deflate_fast: the budget is
             // quartered only for a deflateTune good_length <= 2 (deflate.c:1390)
             uint32_t chain = cfg.good <= kMinMatch - 1 ? cfg.chain >> 2 : cfg.chain;
-            const int nice = lookahead < (int64_t)cfg.nice ? (int)lookahead : (int)cfg.nice;
-            const int64_t limit = (p - po.S) > wp.max_dist ? p - wp.max_dist : po.S;
-            const int64_t rem = n - p;
+            const int nice = lookahead < (P)cfg.nice ? (int)lookahead : (int)cfg.nice;
+            const P limit = (p - po.S) > wp.max_dist ? p - wp.max_dist : po.S;
+            const P rem = n - p;
             const int maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
             int best = kMinMatch - 1;
-            int64_t cur = hh;
-            // kHC 2: the first candidate is cv[j] (no newer block position had
-            // the hash), its link and first 4 bytes are in registers
-            int64_t pre = kPre ? hit_j : -1;
+            P cur = hh;
             uint32_t sb = 0;
             const int lc = lane < maxcmp ? lane : maxcmp - 1;
-            if (kHC == 4) {                              // scan bytes p + lane, from the register window
+            if (kOne) {                                  // scan bytes p + lane, from the register window
                 const int o = (int)(p - wb) + lane;
                 const uint32_t x0 = (uint32_t)__shfl((int)w0, o & 63, 64), x1 = (uint32_t)__shfl((int)w1, o & 63, 64);
                 sb = o < 64 ? x0 : x1;
@@ -2651,7 +2564,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
             for (;;) {
                 uint32_t d;
                 int k;
-                if (kHC == 4) {
+                if (kOne) {
                     // link and candidate bytes in one round trip; cur + lc < n
                     // since cur < p and maxcmp <= n - p
                     const uint32_t dv = prev[cur];
@@ -2659,21 +2572,8 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
                     const uint64_t m = __ballot(lane < maxcmp && cbyte != sb);
                     k = m ? (int)__builtin_ctzll(m) : common_from(cur, p, maxcmp, 64);
                     d = ufl(dv);
-                } else if (kPre && pre >= 0) {
-                    const int j = (int)pre;
-                    pre = -1;
-                    d = (uint32_t)__builtin_amdgcn_readlane((int)pv, j);
-                    const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)cw, j) ^
-                                       (wbyte(p) | wbyte(p + 1) << 8 | wbyte(p + 2) << 16 | wbyte(p + 3) << 24);
-                    const int q4 = x ? (int)(__builtin_ctz(x) >> 3) : 4;
-                    k = q4 < kMinMatch ? q4 : common(cur, p, maxcmp);   // a quick reject needs no round trip
                 } else {
-                    if (kDefer && cur >= cb && cur - cb < 64 && ((cins >> (cur - cb)) & 1ull))
-                        // a link not stored yet (a block position inserted before
-                        // the block's setup is in memory)
-                        d = (uint32_t)__builtin_amdgcn_readlane((int)pbuf, (int)(cur - cb));
-                    else
-                        d = ufl(prev[cur]);
+                    d = ufl(prev[cur]);
                     k = common(cur, p, maxcmp);
                 }
                 if (k > best) {
@@ -2685,11 +2585,11 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
                 cur -= d;
                 if (cur <= limit || --chain == 0) break;
             }
-            match_length = (int64_t)best <= lookahead ? (uint32_t)best : (uint32_t)lookahead;
+            match_length = (P)best <= lookahead ? (uint32_t)best : (uint32_t)lookahead;
         }
         bool bflush;
         if (match_length >= kMinMatch) {
-            bflush = tally(((uint32_t)(p - match_start) << 8) | (match_length - kMinMatch));
+            bflush = po.tally(((uint32_t)(p - match_start) << 8) | (match_length - kMinMatch));
             lookahead -= match_length;
             if (match_length <= cfg.lazy && lookahead >= kMinMatch && match_length <= 48) {
                 // positions p+1 .. p+len-1 (at most 5 unless deflateTune), one
@@ -2697,38 +2597,27 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
                 // hash a lower lane also inserts takes that lane's position (zlib
                 // inserts in order)
                 const uint32_t cntk = match_length - 1;
-                if (kCache && p >= cb && p + (int64_t)cntk - cb < 64) {
-                    // all in the cached block: one at a time, no memory round trip
-                    for (uint32_t k = 1; k <= cntk; k++) insert(p + k);
-                } else {
-                    if (kDefer) { flush_block(); cb = INT64_MIN / 2; }   // memory current first
-                    const bool mine = (uint32_t)lane < cntk;
-                    const int64_t q = p + 1 + lane;
-                    uint32_t h = 0xffffffffu;
-                    for (uint32_t k = 0; k < cntk; k++) {
-                        const uint32_t hk = whash(p + 1 + k);
-                        if ((uint32_t)lane == k) h = hk;
+                const bool mine = (uint32_t)lane < cntk;
+                const P q = p + 1 + lane;
+                uint32_t h = 0xffffffffu;
+                for (uint32_t k = 0; k < cntk; k++) {
+                    const uint32_t hk = whash(p + 1 + k);
+                    if ((uint32_t)lane == k) h = hk;
+                }
+                const P hh0 = mine ? (P)head[h] : 0;
+                P hq = hh0;
+                bool last = mine;
+                for (uint32_t k = 0; k < cntk; k++) {
+                    const uint32_t hk = (uint32_t)__shfl((int)h, (int)k, 64);
+                    if (mine && hk == h) {
+                        if (k < (uint32_t)lane) hq = p + 1 + k;        // a lower lane's position
+                        if (k > (uint32_t)lane) last = false;          // a higher lane writes head
                     }
-                    const int64_t hh0 = mine ? (int64_t)head[h] : 0;
-                    int64_t hq = hh0;
-                    bool last = mine;
-                    for (uint32_t k = 0; k < cntk; k++) {
-                        const uint32_t hk = (uint32_t)__shfl((int)h, (int)k, 64);
-                        if (mine && hk == h) {
-                            if (k < (uint32_t)lane) hq = p + 1 + k;        // a lower lane's position
-                            if (k > (uint32_t)lane) last = false;          // a higher lane writes head
-                        }
-                    }
-                    if (mine) {
-                        const int64_t dd = q - hq;
-                        prev[q] = (hq != 0 && dd <= 32767) ? (uint16_t)dd : 0;
-                        if (last) head[h] = (uint32_t)q;
-                    }
-                    if (kCache)                        // the cached block's inserted positions
-                        for (uint32_t k = 1; k <= cntk; k++) {
-                            const int64_t qk = p + k;
-                            if (qk >= cb && qk - cb < 64) cins |= 1ull << (qk - cb);
-                        }
+                }
+                if (mine) {
+                    const P dd = q - hq;
+                    prev[q] = (hq != 0 && dd <= 32767) ? (uint16_t)dd : 0;
+                    if (last) head[h] = (uint32_t)q;
                 }
             } else if (match_length <= cfg.lazy && lookahead >= kMinMatch) {
                 // deflateTune's longer max_insert_length: one insert at a time
@@ -2740,7 +2629,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
             p += match_length;
             match_length = 0;
         } else {
-            bflush = tally(wbyte(p));
+            bflush = po.tally(wbyte(p));
             p++;
         }
         if (bflush) {
@@ -2749,12 +2638,10 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
             if (kEv && fe.pause_at(p)) {
                 if (lead && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
                 fe.i++;
-                lim = fe.limit(n);
+                lim = (P)fe.limit(n);
             }
         }
     }
-    flush_block();
-    if (kDefer && (po.nsym & 63u) && (uint32_t)lane < (po.nsym & 63u)) po.sym[(po.nsym & ~63u) + lane] = sbuf;
     if (!kEv || !job.open_end) po.flush(p, true);
     if (lead) job.nblocks[bi] = po.nblk;
 }
@@ -3393,27 +3280,19 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     case 5: hipLaunchKernelGGL(k_parse_seg, grid, dim3(kParseLanes), 0, st, job); break;
     case 6: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 1); break;
     case 3: {
-        static const int fv = [] {                   // k_parse_fast variant (A/B runs), default 4
-            const char *e = getenv("ZGPU_FAST_VARIANT");
-            const int v = e ? atoi(e) : 4;
-            return v >= 0 && v <= 4 ? v : 4;
-        }();
+        // ZGPU_FAST_VARIANT (A/B runs): 0 the round-2 walk, 4 64-bit positions
+        static const int fv = [] { const char *e = getenv("ZGPU_FAST_VARIANT"); return e ? atoi(e) : -1; }();
+        const bool old_walk = fv == 0;
         const bool ev = job.nfl || job.start || job.srec;
-        if (fv == 0) {
-            if (ev) hipLaunchKernelGGL((k_parse_fast<true, 0>), grid, dim3(64), 0, st, job, heads);
-            else hipLaunchKernelGGL((k_parse_fast<false, 0>), grid, dim3(64), 0, st, job, heads);
-        } else if (fv == 1) {
-            if (ev) hipLaunchKernelGGL((k_parse_fast<true, 1>), grid, dim3(64), 0, st, job, heads);
-            else hipLaunchKernelGGL((k_parse_fast<false, 1>), grid, dim3(64), 0, st, job, heads);
-        } else if (fv == 2) {
-            if (ev) hipLaunchKernelGGL((k_parse_fast<true, 2>), grid, dim3(64), 0, st, job, heads);
-            else hipLaunchKernelGGL((k_parse_fast<false, 2>), grid, dim3(64), 0, st, job, heads);
-        } else if (fv == 3) {
-            if (ev) hipLaunchKernelGGL((k_parse_fast<true, 3>), grid, dim3(64), 0, st, job, heads);
-            else hipLaunchKernelGGL((k_parse_fast<false, 3>), grid, dim3(64), 0, st, job, heads);
+        if (ev) {
+            if (old_walk) hipLaunchKernelGGL((k_parse_fast<true, false, int64_t>), grid, dim3(64), 0, st, job, heads);
+            else hipLaunchKernelGGL((k_parse_fast<true, true, int64_t>), grid, dim3(64), 0, st, job, heads);
+        } else if (old_walk) {
+            hipLaunchKernelGGL((k_parse_fast<false, false, int64_t>), grid, dim3(64), 0, st, job, heads);
+        } else if (job.pos31 && fv != 4) {
+            hipLaunchKernelGGL((k_parse_fast<false, true, int32_t>), grid, dim3(64), 0, st, job, heads);
         } else {
-            if (ev) hipLaunchKernelGGL((k_parse_fast<true, 4>), grid, dim3(64), 0, st, job, heads);
-            else hipLaunchKernelGGL((k_parse_fast<false, 4>), grid, dim3(64), 0, st, job, heads);
+            hipLaunchKernelGGL((k_parse_fast<false, true, int64_t>), grid, dim3(64), 0, st, job, heads);
         }
         break;
     }

@@ -143,6 +143,9 @@ struct DeflateJob {
     // workgroup per buffer
     const uint32_t *seg;
     uint32_t nseg, seg_len;
+    // every buffer of the sub-batch is under 2^31 bytes: k_parse_fast runs on
+    // 32-bit positions
+    int pos31;
     // deflateInit2_'s windowBits (9..15; 8 is stored as 9, deflate.c:395) and
     // memLevel + 7 = hash_bits (8..16): w_size = 1 << wbits, MAX_DIST = w_size
     // - 262, hash_shift = (hash_bits + 2) / 3, lit_bufsize = 1 << (memLevel + 6)
