@@ -446,7 +446,9 @@ def pmc_traffic(kernels, tag):
 
 def launches_tag(a):
     """Shape of one deflate launch (sub-batch): buffers x bytes."""
-    per = max(1, min(a.buffers, (a.inflight_mb << 20) // a.buffer_bytes))
+    # levels 1-3 keep 4x the in-flight budget (zgpu_api.cpp deflate_dev_locked)
+    mult = 4 if 1 <= a.level <= 3 else 1
+    per = max(1, min(a.buffers, mult * (a.inflight_mb << 20) // a.buffer_bytes))
     return f"{per}x{a.buffer_bytes}"
 
 
@@ -531,25 +533,33 @@ def main(argv=None):
         ratio = in_total / a.steps / max(1.0, out_total)
         st = d["stages"]
         roof = None
-        if "match" in st:
-            # dominant kernel: k_match ("match"); algorithmic bytes per launch =
-            # Σ (n + out_len) over the buffers one launch processes
-            mms, mcount = st["match"]
+        # dominant kernel: k_match ("match") at L4-9, k_parse_fast ("parse_greedy")
+        # at L1-3; algorithmic bytes per launch = Σ (n + out_len) over the
+        # buffers one launch processes
+        dom = None
+        if st.get("match", (0, 0))[1] > 0:
+            dom = ("match", "k_match<", "k_match",
+                   "not HBM: dependent LDS round trips of the chain walks and instruction issue (DESIGN.md 4.3)")
+        elif st.get("parse_greedy", (0, 0))[1] > 0:
+            dom = ("parse_greedy", "k_parse_fast<", "k_parse_fast",
+                   "not HBM: one wave-uniform sequential parse per buffer (deflate_fast), bound by scalar "
+                   "instruction issue on the CU's one scalar unit (DESIGN.md 4.5)")
+        if dom is not None:
+            mms, mcount = st[dom[0]]
             per_step_alg = d["in_bytes"] + d["out_bytes"]
             launches_per_step = max(1, mcount // max(1, a.steps))
             alg_per_launch = per_step_alg / launches_per_step
             m_avg_ms = mms / max(1, mcount)
             achieved = alg_per_launch / (m_avg_ms / 1e3) / 1e9 if m_avg_ms > 0 else 0.0
-            m_traffic, m_src = pmc_traffic(["k_match<"], f"L{a.level}_{launches_tag(a)}")
-            roof = {"bound": "hbm", "kernel": "k_match",
+            m_traffic, m_src = pmc_traffic([dom[1]], f"L{a.level}_{launches_tag(a)}")
+            roof = {"bound": "hbm", "kernel": dom[2],
                     "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 6),
                     "traffic": None if m_traffic is None else int(m_traffic),
                     "traffic_source": m_src,
                     "alg_bytes_per_launch": int(alg_per_launch),
                     "avg_launch_ms": round(m_avg_ms, 3),
-                    "limiter": "not HBM: dependent LDS round trips of the chain walks and instruction "
-                               "issue (DESIGN.md 4.3)"}
+                    "limiter": dom[3]}
         cpu = None
         if not a.no_cpu and sample and D.world == 1:
             cpu = cpu_baselines(a, sample, want, a.level)

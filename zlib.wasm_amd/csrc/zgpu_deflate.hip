@@ -2406,13 +2406,14 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     __syncthreads();
 
     ParseOutT<P> po;
+    const P max_dist = (P)wp.max_dist;
     po.sym = job.sym + job.ws_off[bi];
     po.blk = job.blocks + job.blk_off[bi];
     po.nsym = po.blk_nsym = po.blk_sym_start = po.nblk = 0;
     po.win(job_win(job));
     const P start = kEv ? (P)job.start : 0;
     po.block_start = start; po.S = 0; po.E = kEv && (P)job.e0 > start ? (P)job.e0 : start;
-    po.lead = lead;
+    po.lead = kOne || lead;                              // kOne: all lanes store the symbols
     if (kEv) po.srec = job.srec;
 
     // input window in registers: lane j holds in[wb + j] (w0) and in[wb + 64 + j]
@@ -2420,7 +2421,12 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     // of a compare need no memory round trip
     P wb = -128;
     uint32_t w0 = 0, w1 = 0;
-    auto ld = [&](P x) -> uint32_t { return x < n ? (uint32_t)in[x] : 0u; };
+    // in[x], 0 past the end: a clamped load and a select (kOne), no exec-mask branch
+    auto ld = [&](P x) -> uint32_t {
+        if (!kOne) return x < n ? (uint32_t)in[x] : 0u;
+        const uint32_t v = in[x < n ? x : n - 1];
+        return x < n ? v : 0u;
+    };
     auto wsee = [&](P x) {                        // make [x, x + 66) resident
         if (x >= wb && x + 66 <= wb + 128) return;
         const P nb = x & ~(P)63;
@@ -2437,7 +2443,9 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         const uint32_t h = whash(q);
         const P hh = ufl(head[h]);
         const P d = q - hh;
-        if (lead) {
+        // kOne: every lane stores the same (uniform) value, which keeps the
+        // scalar exec-mask save/restore of a lane-0 store off the parse's path
+        if (kOne || lead) {
             prev[q] = (hh != 0 && d <= 32767) ? (uint16_t)d : 0;
             head[h] = (uint32_t)q;
         }
@@ -2542,14 +2550,14 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         P lookahead = po.E - p;
         P hh = 0;
         if (lookahead >= kMinMatch) hh = insert(p);
-        if (hh > po.S && p - hh <= wp.max_dist) {
+        if (hh > po.S && p - hh <= max_dist) {
             // longest_match (deflate.c:1356-1497), prev_length == 2: the first
             // candidate with the longest prefix wins, stop at nice, chain, limit
             // prev_length stays MIN_MATCH-1 under deflate_fast: the budget is
             // quartered only for a deflateTune good_length <= 2 (deflate.c:1390)
             uint32_t chain = cfg.good <= kMinMatch - 1 ? cfg.chain >> 2 : cfg.chain;
             const int nice = lookahead < (P)cfg.nice ? (int)lookahead : (int)cfg.nice;
-            const P limit = (p - po.S) > wp.max_dist ? p - wp.max_dist : po.S;
+            const P limit = (p - po.S) > max_dist ? p - max_dist : po.S;
             const P rem = n - p;
             const int maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
             int best = kMinMatch - 1;
