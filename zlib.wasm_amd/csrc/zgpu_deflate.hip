@@ -1492,6 +1492,12 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
 // ------------------------------------------------------------------------
 // block bookkeeping shared by both parses (lane 0 only)
 // ------------------------------------------------------------------------
+// a uniform value as a VGPR operand (the compiler then treats it as divergent):
+// k_parse_fast forms its addresses on the vector side, off the scalar unit
+__device__ inline uint32_t vg(uint32_t x) {        // identity DPP move (quad_perm 0,1,2,3)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xE4, 0xF, 0xF, false);
+}
+
 template <typename P>
 struct ParseOutT {
     uint32_t *sym;
@@ -1501,6 +1507,7 @@ struct ParseOutT {
     P wsize, max_dist;      // w_size, MAX_DIST (deflate.c:440-444)
     uint32_t sym_limit;           // lit_bufsize - 1 (deflate.c:455, deflate.h:371)
     bool lead;               // the lane that stores (the state itself is wave-uniform)
+    bool vaddr = false;      // symbol stores through a VGPR index (vg)
     uint64_t *srec = nullptr;     // a streaming job's records (DeflateJob::srec)
 
     __device__ inline void rec(P strstart, bool res) {      // srec[4 nblk + 2, + 3]
@@ -1512,7 +1519,8 @@ struct ParseOutT {
 
     __device__ inline void win(const WinP &w) { wsize = w.wsize; max_dist = w.max_dist; sym_limit = w.sym_limit; }
     __device__ inline bool tally(uint32_t v) {          // _tr_tally_*: returns bflush
-        if (lead) sym[nsym] = v;
+        if (vaddr) sym[vg(nsym)] = v;
+        else if (lead) sym[nsym] = v;
         nsym++;
         return ++blk_nsym == sym_limit;
     }
@@ -2414,6 +2422,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     const P start = kEv ? (P)job.start : 0;
     po.block_start = start; po.S = 0; po.E = kEv && (P)job.e0 > start ? (P)job.e0 : start;
     po.lead = kOne || lead;                              // kOne: all lanes store the symbols
+    po.vaddr = kOne;
     if (kEv) po.srec = job.srec;
 
     // input window in registers: lane j holds in[wb + j] (w0) and in[wb + 64 + j]
@@ -2424,7 +2433,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     // in[x], 0 past the end: a clamped load and a select (kOne), no exec-mask branch
     auto ld = [&](P x) -> uint32_t {
         if (!kOne) return x < n ? (uint32_t)in[x] : 0u;
-        const uint32_t v = in[x < n ? x : n - 1];
+        const uint32_t v = in[(uint32_t)(x < n ? x : n - 1)];
         return x < n ? v : 0u;
     };
     auto wsee = [&](P x) {                        // make [x, x + 66) resident
@@ -2441,13 +2450,18 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     auto whash = [&](P q) -> uint32_t { return hashp(wbyte(q), wbyte(q + 1), wbyte(q + 2), wp); };
     auto insert = [&](P q) -> P {           // INSERT_STRING
         const uint32_t h = whash(q);
-        const P hh = ufl(head[h]);
+        const P hh = ufl(head[kOne ? vg(h) : h]);
         const P d = q - hh;
         // kOne: every lane stores the same (uniform) value, which keeps the
         // scalar exec-mask save/restore of a lane-0 store off the parse's path
         if (kOne || lead) {
-            prev[q] = (hh != 0 && d <= 32767) ? (uint16_t)d : 0;
-            head[h] = (uint32_t)q;
+            if (kOne) {                                  // addresses in VGPRs (vg)
+                prev[vg((uint32_t)q)] = (hh != 0 && d <= 32767) ? (uint16_t)d : 0;
+                head[vg(h)] = (uint32_t)q;
+            } else {
+                prev[q] = (hh != 0 && d <= 32767) ? (uint16_t)d : 0;
+                head[h] = (uint32_t)q;
+            }
         }
         return hh;
     };
@@ -2474,7 +2488,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         for (; k0 < maxcmp; k0 += 64) {
             const int kk = k0 + lane;
             const int kc = kk < maxcmp ? kk : maxcmp - 1;
-            const uint64_t m = __ballot(kk < maxcmp && in[a + kc] != in[pp + kc]);
+            const uint64_t m = __ballot(kk < maxcmp && in[(uint32_t)(a + kc)] != in[(uint32_t)(pp + kc)]);
             if (m) return k0 + __builtin_ctzll(m);
         }
         return maxcmp;
@@ -2575,8 +2589,9 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
                 if (kOne) {
                     // link and candidate bytes in one round trip; cur + lc < n
                     // since cur < p and maxcmp <= n - p
-                    const uint32_t dv = prev[cur];
-                    const uint32_t cbyte = in[cur + lc];
+                    const uint32_t dv = prev[vg((uint32_t)cur)];
+                    const uint32_t cbyte = in[(uint32_t)(cur + lc)];
+                    __builtin_amdgcn_sched_barrier(0);       // both loads issued before either is used
                     const uint64_t m = __ballot(lane < maxcmp && cbyte != sb);
                     k = m ? (int)__builtin_ctzll(m) : common_from(cur, p, maxcmp, 64);
                     d = ufl(dv);
