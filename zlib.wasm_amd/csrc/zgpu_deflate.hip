@@ -932,9 +932,54 @@ struct DWQ {
     int q[kQ];
     uint32_t em, eb, scan01, scanE;
 };
-template <int kQ>
+// kU > 1: kU steps per exit test (the loop's ballots and budget compare are
+// scalar work every wave of the CU shares one scalar unit for).  A lane whose
+// walk has ended keeps stepping harmlessly (links only go back, so it stays
+// past its limit and queues nothing); the queue test fires kU - 1 entries
+// early so that kU steps cannot overflow it, and single steps are taken when
+// fewer than kU are left of the budget, so the stops are those of kU 1.
+// kV: the quick-reject test as one integer (the two byte-pair differences and
+// the limit test's sign bit or-ed together, one compare), instead of three
+// compares whose lane masks are and-ed on the scalar unit.
+template <int kQ, int kU = 1, bool kV = false>
 __device__ __attribute__((always_inline)) inline void dwq_steps(DWQ<kQ> &w, const char *Eb, uint32_t &count,
                                                                 uint32_t end) {
+    if (kU > 1) {
+        auto step = [&]() {
+            const int m4n = (int)((w.em << 2) & 0x3fffcu);
+            const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + m4n);
+            const uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + m4n + w.be4);
+            bool pass;
+            if (kV) {
+                // m4 > limit4 <=> m4 - limit4 - 1 >= 0 (both within +-2^18)
+                const uint32_t x = ((w.em >> 16) ^ w.scan01) | ((w.eb >> 16) ^ w.scanE) |
+                                   ((uint32_t)(w.m4 - w.limit4 - 1) >> 31);
+                pass = x == 0;
+            } else {
+                pass = (w.m4 > w.limit4) & ((w.em >> 16) == w.scan01) & ((w.eb >> 16) == w.scanE);
+            }
+#pragma unroll
+            for (int j = kQ - 1; j > 0; j--) w.q[j] = pass ? w.q[j - 1] : w.q[j];
+            w.q[0] = pass ? w.m4 : w.q[0];
+            w.occ += pass ? 1 : 0;
+            w.m4 = m4n;
+            w.em = emn;
+            w.eb = ebn;
+        };
+        for (;;) {
+            if (end - count >= (uint32_t)kU) {
+#pragma unroll
+                for (int u = 0; u < kU; u++) step();
+                count += kU;
+            } else {
+                step();
+                count += 1;
+            }
+            const uint64_t walkers = __ballot(w.m4 > w.limit4), full = __ballot(w.occ >= kQ - (kU - 1));
+            if (count >= end || walkers == 0 || full != 0) break;
+        }
+        return;
+    }
     for (;;) {
         const bool valid = w.m4 > w.limit4;
         const int m4n = (int)((w.em << 2) & 0x3fffcu);
@@ -954,7 +999,7 @@ __device__ __attribute__((always_inline)) inline void dwq_steps(DWQ<kQ> &w, cons
     }
 }
 
-template <int kQ>
+template <int kQ, int kU = 1, bool kV = false>
 __device__ __attribute__((always_inline)) inline void dwq_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
                                                                const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
                                                                int want_q, int64_t max_dist) {
@@ -1019,7 +1064,7 @@ __device__ __attribute__((always_inline)) inline void dwq_walk(const uint32_t *E
     for (;;) {
         const uint32_t end = count < qc ? qc : chain;
         const int best0 = best;
-        dwq_steps<kQ>(w, Eb, count, end);
+        dwq_steps<kQ, kU, kV>(w, Eb, count, end);
         walking = w.m4 > limit4 && count < chain;
         // every entry, oldest first: entry j (< occ) is the (occ - j)-th oldest
 #pragma unroll
@@ -1243,7 +1288,17 @@ __device__ __attribute__((always_inline)) inline void dwp_walk(const uint32_t *E
 __device__ unsigned long long g_mstat[4];   // kMatchStats statistics
 
 // k_match variants (ZGPU_MATCH_VARIANT, for A/B runs):
-//   49 (default)  48 with a 6-deep queue (dwq_walk): 411 -> 401 ms
+//   55 (default)  49 with three steps per exit test (dwq_steps kU 3: the
+//                 loop's two ballots and budget compare are scalar work that
+//                 the CU's 16 walking waves share one scalar unit for):
+//                 402 -> 375 ms per 4 GiB L6 sub-batch (interleaved A/B, 2x)
+//   53, 57, 58    two steps (397 ms), four with an 8-deep queue (377), four
+//                 with a 6-deep queue flushed at 3 (386)
+//   56            three steps, 7-deep queue (380)
+//   59            55 with the quick reject as one integer or-ed from the byte
+//                 differences and the limit's sign bit (fewer scalar mask ands,
+//                 more vector instructions): 382 vs 375 ms
+//   49            48 with a 6-deep queue (dwq_walk): 411 -> 401 ms
 //   48            40 with links stored as the predecessor's LDS word index (a
 //                 chain step needs no subtraction; the slide lowers every index
 //                 with one saturating packed subtract): 418 -> 411 ms
@@ -1287,9 +1342,10 @@ __device__ unsigned long long g_mstat[4];   // kMatchStats statistics
 //                 latency-bound at the 16 waves the LDS window allows)
 constexpr int kMatchDefer = 40, kMatchDeferStats = 41, kMatchDefer3 = 42, kMatchDeferP = 43, kMatchDeferPStats = 44,
               kMatchProbeNoFlush = 45, kMatchDeferR = 46, kMatchDeferB = 47, kMatchDeferIdx = 48,
-              kMatchQ6 = 49, kMatchQ8 = 50, kMatchQ3 = 51, kMatchPair = 52;
+              kMatchQ6 = 49, kMatchQ8 = 50, kMatchQ3 = 51, kMatchPair = 52, kMatchQ6U2 = 53, kMatchQ7U2 = 54,
+              kMatchQ6U3 = 55, kMatchQ7U3 = 56, kMatchQ8U4 = 57, kMatchQ6U4 = 58, kMatchQ6U3V = 59;
 constexpr int kMatchWalk = 19;
-constexpr int kMatchDefault = kMatchQ6;
+constexpr int kMatchDefault = kMatchQ6U3;
 constexpr int kMatchStats = 21, kMatchProbeNoWalk = 33, kMatchProbeHalf = 35,
               kMatchProbeNoCmp = 37, kMatchProbeCmpOnly = 38;
 
@@ -1372,7 +1428,9 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
         const int64_t B = ts - kMW;
         const int tile_n = kSegs && ts < s0 ? 0 : (int)((n - ts) < kMT ? (n - ts) : kMT);   // 0: staging only
         tile_store<kVariant == kMatchDeferIdx || kVariant == kMatchQ6 || kVariant == kMatchQ8 || kVariant == kMatchQ3 ||
-                   kVariant == kMatchPair>(
+                   kVariant == kMatchPair || kVariant == kMatchQ6U2 || kVariant == kMatchQ7U2 || kVariant == kMatchQ6U3 ||
+                   kVariant == kMatchQ7U3 || kVariant == kMatchQ8U4 || kVariant == kMatchQ6U4 ||
+                   kVariant == kMatchQ6U3V>(
             E, P, ts, tid);
         if (tid == 0) next_i = 0;
         if (kSorted && tid < kSortBuckets) s_hist[tid] = 0;
@@ -1452,6 +1510,20 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
                 dwq_walk<6>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
             } else if (kVariant == kMatchQ8) {
                 dwq_walk<8>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+            } else if (kVariant == kMatchQ6U2) {
+                dwq_walk<6, 2>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+            } else if (kVariant == kMatchQ7U2) {
+                dwq_walk<7, 2>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+            } else if (kVariant == kMatchQ6U3) {
+                dwq_walk<6, 3>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+            } else if (kVariant == kMatchQ7U3) {
+                dwq_walk<7, 3>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+            } else if (kVariant == kMatchQ8U4) {
+                dwq_walk<8, 4>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+            } else if (kVariant == kMatchQ6U4) {
+                dwq_walk<6, 4>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+            } else if (kVariant == kMatchQ6U3V) {
+                dwq_walk<6, 3, true>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
             } else if (kVariant == kMatchQ3) {
                 dwq_walk<3>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
             } else if (kVariant == kMatchDeferIdx) {
@@ -3212,7 +3284,8 @@ static int match_variant() {
                 x == kMatchProbeNoCmp || x == kMatchProbeCmpOnly || x == kMatchDefer || x == kMatchDeferStats || x == kMatchDefer3 || x == kMatchDeferP ||
                 x == kMatchDeferPStats || x == kMatchProbeNoFlush || x == kMatchDeferR ||
                 x == kMatchDeferB || x == kMatchDeferIdx || x == kMatchQ6 || x == kMatchQ8 || x == kMatchQ3 ||
-                x == kMatchPair)
+                x == kMatchPair || x == kMatchQ6U2 || x == kMatchQ7U2 ||
+                x == kMatchQ6U3 || x == kMatchQ7U3 || x == kMatchQ8U4 || x == kMatchQ6U4 || x == kMatchQ6U3V)
                    ? x : kMatchDefault;
     }();
     return v;
@@ -3248,6 +3321,20 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
             hipLaunchKernelGGL(k_match<kMatchQ6>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchQ8) {
             hipLaunchKernelGGL(k_match<kMatchQ8>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchQ6U2) {
+            hipLaunchKernelGGL(k_match<kMatchQ6U2>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchQ7U2) {
+            hipLaunchKernelGGL(k_match<kMatchQ7U2>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchQ6U3) {
+            hipLaunchKernelGGL(k_match<kMatchQ6U3>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchQ7U3) {
+            hipLaunchKernelGGL(k_match<kMatchQ7U3>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchQ8U4) {
+            hipLaunchKernelGGL(k_match<kMatchQ8U4>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchQ6U4) {
+            hipLaunchKernelGGL(k_match<kMatchQ6U4>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        } else if (v == kMatchQ6U3V) {
+            hipLaunchKernelGGL(k_match<kMatchQ6U3V>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchQ3) {
             hipLaunchKernelGGL(k_match<kMatchQ3>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
         } else if (v == kMatchPair) {
