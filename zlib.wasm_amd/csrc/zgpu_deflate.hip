@@ -2560,7 +2560,8 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         for (; k0 < maxcmp; k0 += 64) {
             const int kk = k0 + lane;
             const int kc = kk < maxcmp ? kk : maxcmp - 1;
-            const uint64_t m = __ballot(kk < maxcmp && in[(uint32_t)(a + kc)] != in[(uint32_t)(pp + kc)]);
+            const uint32_t x = in[(uint32_t)(a + kc)], y = in[(uint32_t)(pp + kc)];   // unconditional loads
+            const uint64_t m = __ballot((kk < maxcmp) & (x != y));
             if (m) return k0 + __builtin_ctzll(m);
         }
         return maxcmp;
