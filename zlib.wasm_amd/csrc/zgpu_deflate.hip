@@ -2508,18 +2508,35 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         const uint32_t v = in[(uint32_t)(x < n ? x : n - 1)];
         return x < n ? v : 0u;
     };
+    // kOne: lane j also holds hv = the hash of position wb + j (its bytes are
+    // all in the window), made when the window moves, so INSERT_STRING's hash
+    // is one readlane instead of three byte reads and the hash arithmetic on
+    // the scalar unit
+    uint32_t hv = 0;
     auto wsee = [&](P x) {                        // make [x, x + 66) resident
         if (x >= wb && x + 66 <= wb + 128) return;
         const P nb = x & ~(P)63;
         if (nb == wb + 64) { w0 = w1; w1 = ld(nb + 64 + lane); }
         else { w0 = ld(nb + lane); w1 = ld(nb + 64 + lane); }
         wb = nb;
+        if (kOne) {
+            const int l1 = (lane + 1) & 63, l2 = (lane + 2) & 63;
+            const uint32_t a1 = (uint32_t)__shfl((int)w0, l1, 64), c1 = (uint32_t)__shfl((int)w1, l1, 64);
+            const uint32_t a2 = (uint32_t)__shfl((int)w0, l2, 64), c2 = (uint32_t)__shfl((int)w1, l2, 64);
+            hv = hashp(w0, lane < 63 ? a1 : c1, lane < 62 ? a2 : c2, wp);
+        }
     };
     auto wbyte = [&](P x) -> uint32_t {           // uniform x in the window
         const int o = (int)(x - wb);
         return (uint32_t)__builtin_amdgcn_readlane((int)(o < 64 ? w0 : w1), o & 63);
     };
-    auto whash = [&](P q) -> uint32_t { return hashp(wbyte(q), wbyte(q + 1), wbyte(q + 2), wp); };
+    auto whash = [&](P q) -> uint32_t {
+        if (kOne) {
+            const int o = (int)(q - wb);
+            if (o < 64) return (uint32_t)__builtin_amdgcn_readlane((int)hv, o);
+        }
+        return hashp(wbyte(q), wbyte(q + 1), wbyte(q + 2), wp);
+    };
     auto insert = [&](P q) -> P {           // INSERT_STRING
         const uint32_t h = whash(q);
         const P hh = ufl(head[kOne ? vg(h) : h]);
