@@ -2713,15 +2713,23 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
                 const bool mine = (uint32_t)lane < cntk;
                 const P q = p + 1 + lane;
                 uint32_t h = 0xffffffffu;
-                for (uint32_t k = 0; k < cntk; k++) {
-                    const uint32_t hk = whash(p + 1 + k);
-                    if ((uint32_t)lane == k) h = hk;
+                const int ob = (int)(p + 1 - wb);            // window offset of p + 1
+                if (kOne && ob + (int)cntk <= 64) {
+                    // lane k < cntk: the hash of p + 1 + k, from the window's hashes
+                    const uint32_t hx = (uint32_t)__shfl((int)hv, (ob + lane) & 63, 64);
+                    h = mine ? hx : 0xffffffffu;
+                } else {
+                    for (uint32_t k = 0; k < cntk; k++) {
+                        const uint32_t hk = whash(p + 1 + k);
+                        if ((uint32_t)lane == k) h = hk;
+                    }
                 }
                 const P hh0 = mine ? (P)head[h] : 0;
                 P hq = hh0;
                 bool last = mine;
                 for (uint32_t k = 0; k < cntk; k++) {
-                    const uint32_t hk = (uint32_t)__shfl((int)h, (int)k, 64);
+                    const uint32_t hk = kOne ? (uint32_t)__builtin_amdgcn_readlane((int)h, (int)k)
+                                             : (uint32_t)__shfl((int)h, (int)k, 64);
                     if (mine && hk == h) {
                         if (k < (uint32_t)lane) hq = p + 1 + k;        // a lower lane's position
                         if (k > (uint32_t)lane) last = false;          // a higher lane writes head
