@@ -556,3 +556,27 @@ def test_deflateinit2_params_stream(zg):
         L.deflateEnd(C.byref(s))
         want = c["streams"][1]
         assert hashlib.sha256(z).hexdigest() == want["sha256"], (c["level"], c["window_bits"], c["mem_level"])
+
+
+def test_huffman_length_overflow(zg, oracle):
+    """Literal counts on a Fibonacci ladder (a 19-leaf tree 18 deep): gen_bitlen's
+    overflow repair (trees.c:446-484) in the literal tree, and skewed code-length
+    counts for the bit-length tree (max 7).  k_encode's wave-wide tree build
+    (w_build) against the oracle, Z_HUFFMAN_ONLY and level 6/9 parses, one and
+    several blocks."""
+    fib = [1, 1]
+    while len(fib) < 19:
+        fib.append(fib[-1] + fib[-2])
+    rng = np.random.default_rng(11)
+    bufs = []
+    for seed in range(6):
+        syms = rng.permutation(256)[:19]
+        parts = []
+        for rep in range(1 + seed % 3):                  # 1..3 blocks of symbols
+            a = np.repeat(syms, fib)
+            parts.append(a[rng.permutation(len(a))])
+        bufs.append(np.concatenate(parts).astype(np.uint8).tobytes())
+    for level, strategy in ((6, 2), (1, 2), (6, 0), (9, 0)):
+        res = zg.compress_batch(bufs, level=level, strategy=strategy)
+        for b, (st, z) in zip(bufs, res):
+            assert st == 0 and z == oracle.compress(b, level, strategy=strategy)[1], (len(b), level, strategy)

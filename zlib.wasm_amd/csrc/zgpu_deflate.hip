@@ -2774,6 +2774,7 @@ constexpr int kEncThreads = 256;
 constexpr int kStgWords = 2048;                 // 8 KiB output staging window
 constexpr int kEncGroup = kEncThreads / 64;     // blocks whose trees are built at once (one per wave)
 constexpr int kStgBits = kStgWords * 32;
+constexpr int kWNodeSlots = (kHeapSize + 63) / 64;   // w_build: tree nodes per lane (9)
 
 struct TreeLDS {
     // leaves: freq/code; all nodes: dad/len (internal-node freqs live in heap keys)
@@ -2785,6 +2786,7 @@ struct TreeLDS {
     uint8_t blen[2 * kBLCodes + 2];
     uint32_t heap[kHeapSize + 1];        // packed keys, see hkey()
     uint16_t bl_count[kMaxBits + 1];
+    uint32_t pj[2][kWNodeSlots * 64];    // w_build: pointer-jumping exchange (dad | depth << 16)
 };
 
 struct TreeRef {
@@ -2914,6 +2916,251 @@ __device__ void t_build(TreeRef &t, TreeLDS &h, int elems, const uint8_t *slen, 
     t_gen_codes(t, h.bl_count);
 }
 
+// ---- w_build: build_tree + gen_bitlen + gen_codes (trees.c:540-706, 589-625) by a whole wave ----
+// The heap lives in five VGPRs across the wave's lanes: heap[j] is lane j & 63 of register j >> 6
+// (heap_len <= 286 < 320). A heap access is a readlane/writelane with a wave-uniform index instead of
+// a dependent LDS round trip of one lane, and the sequence of heap operations -- hence every tie
+// pqdownheap breaks -- is trees.c's. The node depths of gen_bitlen come from pointer jumping over the
+// dad links, bl_count and the codes of gen_codes from per-length ballots.
+struct RHeap { uint32_t r[5]; };
+
+__device__ __attribute__((always_inline)) inline uint32_t rl(uint32_t v, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+__device__ __attribute__((always_inline)) inline uint32_t wl(uint32_t v, uint32_t l, uint32_t old) {
+    return (threadIdx.x & 63u) == l ? v : old;      // v_cmp + v_cndmask (no writelane builtin here)
+}
+template <int D>   // j on heap level D (2^D <= j < 2^(D+1))
+__device__ __attribute__((always_inline)) inline uint32_t rget(const RHeap &H, uint32_t j) {
+    if constexpr (D <= 5) return rl(H.r[0], j);
+    else if constexpr (D == 6) return rl(H.r[1], j & 63u);
+    else if constexpr (D == 7) return (j & 64u) ? rl(H.r[3], j & 63u) : rl(H.r[2], j & 63u);
+    else return rl(H.r[4], j & 63u);
+}
+template <int D>
+__device__ __attribute__((always_inline)) inline void rset(RHeap &H, uint32_t j, uint32_t v) {
+    if constexpr (D <= 5) H.r[0] = wl(v, j, H.r[0]);
+    else if constexpr (D == 6) H.r[1] = wl(v, j & 63u, H.r[1]);
+    else if constexpr (D == 7) {
+        if (j & 64u) H.r[3] = wl(v, j & 63u, H.r[3]);
+        else H.r[2] = wl(v, j & 63u, H.r[2]);
+    } else H.r[4] = wl(v, j & 63u, H.r[4]);
+}
+__device__ __attribute__((always_inline)) inline uint32_t rget_any(const RHeap &H, uint32_t j) {
+    switch (j >> 6) {
+    case 0: return rl(H.r[0], j);
+    case 1: return rl(H.r[1], j & 63u);
+    case 2: return rl(H.r[2], j & 63u);
+    case 3: return rl(H.r[3], j & 63u);
+    default: return rl(H.r[4], j & 63u);
+    }
+}
+// pqdownheap (trees.c:509-527) of key v entering at node k of level D
+template <int D>
+__device__ __attribute__((always_inline)) inline void r_down(RHeap &H, int heap_len, uint32_t k, uint32_t v) {
+    if constexpr (D < 8) {
+        uint32_t j = k << 1;
+        if ((int)j <= heap_len) {
+            uint32_t hj = rget<D + 1>(H, j);
+            if ((int)j < heap_len) {
+                const uint32_t hj1 = rget<D + 1>(H, j + 1);
+                if (hle(hj1, hj)) { j++; hj = hj1; }
+            }
+            if (!hle(v, hj)) {
+                rset<D>(H, k, hj);
+                r_down<D + 1>(H, heap_len, j, v);
+                return;
+            }
+        }
+    }
+    rset<D>(H, k, v);
+}
+__device__ inline void r_down_any(RHeap &H, int heap_len, uint32_t k) {   // build_tree's heapify
+    const uint32_t v = rget_any(H, k);
+    switch (31 - __builtin_clz(k)) {
+    case 0: r_down<0>(H, heap_len, k, v); break;
+    case 1: r_down<1>(H, heap_len, k, v); break;
+    case 2: r_down<2>(H, heap_len, k, v); break;
+    case 3: r_down<3>(H, heap_len, k, v); break;
+    case 4: r_down<4>(H, heap_len, k, v); break;
+    case 5: r_down<5>(H, heap_len, k, v); break;
+    case 6: r_down<6>(H, heap_len, k, v); break;
+    default: r_down<7>(H, heap_len, k, v); break;       // k <= heap_len / 2 < 256
+    }
+}
+
+// Called by all 64 lanes of a wave with wave-uniform arguments; opt_len/static_len stay uniform.
+__device__ __attribute__((always_inline)) inline void w_build(TreeRef &t, TreeLDS &h, int elems, const uint8_t *slen, const uint8_t *extra,
+                        int xbase, int max_length, int64_t &opt_len, int64_t &static_len) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint32_t *hs = h.heap;
+    int max_code = -1, heap_len = 0;
+    for (int c = 0; c < elems; c += 64) {              // the leaves, in symbol order
+        const int n = c + (int)lane;
+        const uint32_t f = n < elems ? t.freq[n] : 0u;
+        const uint64_t m = __ballot(f != 0);
+        if (f != 0) hs[heap_len + 1 + __popcll(m & below)] = hkey(f, 0, (uint32_t)n);
+        else if (n < elems) t.len[n] = 0;
+        if (m) max_code = c + 63 - __clzll(m);
+        heap_len += __popcll(m);
+    }
+    while (heap_len < 2) {                             // trees.c:560-569
+        const int node = max_code < 2 ? ++max_code : 0;
+        heap_len++;
+        if (lane == 0) { hs[heap_len] = hkey(1, 0, (uint32_t)node); t.freq[node] = 1; }
+        opt_len--;
+        if (slen) static_len -= slen[node];
+    }
+    t.max_code = max_code;
+    __builtin_amdgcn_wave_barrier();
+    RHeap H;
+#pragma unroll
+    for (int r = 0; r < 5; r++) {
+        const int j = r * 64 + (int)lane;
+        H.r[r] = (j >= 1 && j <= heap_len) ? hs[j] : 0u;
+    }
+    for (int k = heap_len / 2; k >= 1; k--) r_down_any(H, heap_len, (uint32_t)k);
+    int heap_max = kHeapSize;
+    uint32_t node = (uint32_t)elems;
+    do {                                               // trees.c:583-604
+        const uint32_t kn = rl(H.r[0], 1);
+        const uint32_t last = rget_any(H, (uint32_t)heap_len);
+        heap_len--;
+        r_down<0>(H, heap_len, 1, last);
+        const uint32_t km = rl(H.r[0], 1);
+        heap_max -= 2;
+        if (lane == 0) {
+            hs[heap_max + 1] = kn;
+            hs[heap_max] = km;
+            t.dad[kn & 1023u] = (uint16_t)node;
+            t.dad[km & 1023u] = (uint16_t)node;
+        }
+        const uint32_t f = (kn >> 16) + (km >> 16);
+        const uint32_t dn = (kn >> 10) & 63u, dm = (km >> 10) & 63u;
+        r_down<0>(H, heap_len, 1, hkey(f, (dn >= dm ? dn : dm) + 1, node));
+        node++;
+    } while (heap_len >= 2);
+    heap_max--;
+    const uint32_t rootn = rl(H.r[0], 1) & 1023u;
+    if (lane == 0) hs[heap_max] = rl(H.r[0], 1);
+    __builtin_amdgcn_wave_barrier();
+
+    // gen_bitlen (trees.c:406-485): depth of every node by pointer jumping; len = min(depth, max_length),
+    // overflow = nodes deeper than max_length (a clamped parent pushes its children past it too)
+    uint32_t nid[kWNodeSlots], P[kWNodeSlots], Dp[kWNodeSlots], fq[kWNodeSlots];
+#pragma unroll
+    for (int i = 0; i < kWNodeSlots; i++) {
+        const int hh = heap_max + (int)lane + 64 * i;
+        const bool valid = hh < kHeapSize;
+        const uint32_t key = valid ? hs[hh] : hkey(0, 0, rootn);
+        nid[i] = key & 1023u;
+        fq[i] = key >> 16;
+        P[i] = nid[i] == rootn ? rootn : t.dad[nid[i]];
+        Dp[i] = nid[i] == rootn ? 0u : 1u;
+        if (valid) h.pj[0][nid[i]] = P[i] | (Dp[i] << 16);
+    }
+    for (int r = 0; r < 9; r++) {                      // 2^9 > the deepest tree (285)
+        bool open = false;
+#pragma unroll
+        for (int i = 0; i < kWNodeSlots; i++) open |= P[i] != rootn;
+        if (!__any(open)) break;
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t *src = h.pj[r & 1];
+        uint32_t *dst = h.pj[(r + 1) & 1];
+        uint32_t w[kWNodeSlots];
+#pragma unroll
+        for (int i = 0; i < kWNodeSlots; i++) w[i] = src[P[i]];
+#pragma unroll
+        for (int i = 0; i < kWNodeSlots; i++) {
+            Dp[i] += w[i] >> 16;
+            P[i] = w[i] & 0xffffu;
+            if (heap_max + (int)lane + 64 * i < kHeapSize) dst[nid[i]] = P[i] | (Dp[i] << 16);
+        }
+    }
+    int overflow = 0;
+    int64_t ol = 0, sl = 0;
+    uint32_t bc[kMaxBits + 1];
+#pragma unroll
+    for (int b = 0; b <= kMaxBits; b++) bc[b] = 0;
+#pragma unroll
+    for (int i = 0; i < kWNodeSlots; i++) {
+        const bool valid = heap_max + (int)lane + 64 * i < kHeapSize;
+        const int bits = (int)Dp[i] > max_length ? max_length : (int)Dp[i];
+        const bool leaf = valid && (int)nid[i] <= max_code;
+        if (valid) {
+            overflow += (int)Dp[i] > max_length;
+            t.len[nid[i]] = (uint8_t)bits;
+        }
+        if (leaf) {
+            const int n = (int)nid[i];
+            const int xb = n >= xbase ? extra[n - xbase] : 0;
+            ol += (int64_t)fq[i] * (bits + xb);
+            if (slen) sl += (int64_t)fq[i] * (slen[n] + xb);
+        }
+#pragma unroll
+        for (int b = 1; b <= kMaxBits; b++) bc[b] += (uint32_t)__popcll(__ballot(leaf && bits == b));
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        overflow += __shfl_xor(overflow, o, 64);
+        ol += __shfl_xor(ol, o, 64);
+        sl += __shfl_xor(sl, o, 64);
+    }
+    opt_len += ol;
+    static_len += sl;
+    if (overflow != 0) {                               // trees.c:446-484, one lane
+        int64_t dl = 0;
+        if (lane == 0) {
+            for (int b = 0; b <= kMaxBits; b++) h.bl_count[b] = (uint16_t)bc[b];
+            do {
+                int bits = max_length - 1;
+                while (h.bl_count[bits] == 0) bits--;
+                h.bl_count[bits]--;
+                h.bl_count[bits + 1] += 2;
+                h.bl_count[max_length]--;
+                overflow -= 2;
+            } while (overflow > 0);
+            int hh = kHeapSize;
+            for (int bits = max_length; bits != 0; bits--) {
+                int n = h.bl_count[bits];
+                while (n != 0) {
+                    const int m = (int)(hs[--hh] & 1023u);
+                    if (m > max_code) continue;
+                    if (t.len[m] != bits) {
+                        dl += ((int64_t)bits - t.len[m]) * t.freq[m];
+                        t.len[m] = (uint8_t)bits;
+                    }
+                    n--;
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        opt_len += __shfl(dl, 0, 64);
+#pragma unroll
+        for (int b = 0; b <= kMaxBits; b++) bc[b] = h.bl_count[b];
+    }
+    // gen_codes (trees.c:589-625): a length's codes go to its symbols in symbol order
+    uint32_t next[kMaxBits + 1];
+    uint32_t c = 0;
+#pragma unroll
+    for (int b = 1; b <= kMaxBits; b++) { c = (c + bc[b - 1]) << 1; next[b] = c; }
+    __builtin_amdgcn_wave_barrier();
+    for (int c0 = 0; c0 <= max_code; c0 += 64) {
+        const int n = c0 + (int)lane;
+        const int len = n <= max_code ? t.len[n] : 0;
+        uint32_t code = 0;
+#pragma unroll
+        for (int b = 1; b <= kMaxBits; b++) {
+            const uint64_t m = __ballot(len == b);
+            if (len == b) code = next[b] + (uint32_t)__popcll(m & below);
+            next[b] += (uint32_t)__popcll(m);
+        }
+        if (len) t.code[n] = (uint16_t)(__brev(code) >> (32 - len));
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 // code-length RLE walk of scan_tree/send_tree (trees.c:712-794)
 template <typename Sink>
 __device__ void t_rle(const uint8_t *len, int max_code, Sink sink) {
@@ -2962,7 +3209,7 @@ __device__ inline void stg_or(uint32_t *stg, int64_t rel, uint64_t v) {  // v < 
 }
 
 // write completed words below bit `upto` to global, keep the partial word
-__device__ void stg_flush(Stage &st, int64_t upto, bool final_flush) {
+__device__ __attribute__((always_inline)) inline void stg_flush(Stage &st, int64_t upto, bool final_flush) {
     const int tid = threadIdx.x;
     const int64_t rel = upto - st.sbase;
     const int full = (int)(rel >> 5);
@@ -2992,6 +3239,7 @@ __device__ void stg_flush(Stage &st, int64_t upto, bool final_flush) {
     }
 }
 
+template <bool kWaveTrees>
 __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
     __shared__ uint32_t stg[kStgWords];
     __shared__ TreeLDS TT[kEncGroup];
@@ -3110,17 +3358,28 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
                     if (lane < kDCodes) T.dfreq[lane] = (uint16_t)hd[lane];
                     if (lane < kBLCodes) T.bfreq[lane] = 0;
                     __builtin_amdgcn_wave_barrier();
-                    if (lane == 0) {
-                        int64_t opt_len = 0, static_len = 0;
-                        TreeRef lt{T.lfreq, T.ldad, T.lcode, T.llen, 0};
-                        TreeRef dt{T.dfreq, T.ddad, T.dcode, T.dlen, 0};
-                        TreeRef bt{T.bfreq, T.bdad, T.bcode, T.blen, 0};
+                    int64_t opt_len = 0, static_len = 0;
+                    TreeRef lt{T.lfreq, T.ldad, T.lcode, T.llen, 0};
+                    TreeRef dt{T.dfreq, T.ddad, T.dcode, T.dlen, 0};
+                    TreeRef bt{T.bfreq, T.bdad, T.bcode, T.blen, 0};
+                    auto cnt = [&](int s, int, int) { T.bfreq[s]++; };
+                    if constexpr (kWaveTrees) {         // the whole wave builds (w_build)
+                        w_build(lt, T, kLCodes, c_ct.stat_llen, c_ct.xlbits, 257, kMaxBits, opt_len, static_len);
+                        w_build(dt, T, kDCodes, c_ct.stat_dlen, c_ct.xdbits, 0, kMaxBits, opt_len, static_len);
+                        if (lane == 0) {
+                            t_rle(T.llen, lt.max_code, cnt);
+                            t_rle(T.dlen, dt.max_code, cnt);
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                        w_build(bt, T, kBLCodes, nullptr, c_ct.xblbits, 0, kMaxBLBits, opt_len, static_len);
+                    } else if (lane == 0) {             // one lane builds (t_build)
                         t_build(lt, T, kLCodes, c_ct.stat_llen, c_ct.xlbits, 257, kMaxBits, opt_len, static_len);
                         t_build(dt, T, kDCodes, c_ct.stat_dlen, c_ct.xdbits, 0, kMaxBits, opt_len, static_len);
-                        auto cnt = [&](int s, int, int) { T.bfreq[s]++; };
                         t_rle(T.llen, lt.max_code, cnt);
                         t_rle(T.dlen, dt.max_code, cnt);
                         t_build(bt, T, kBLCodes, nullptr, c_ct.xblbits, 0, kMaxBLBits, opt_len, static_len);
+                    }
+                    if (lane == 0) {
                         int max_blindex;
                         for (max_blindex = kBLCodes - 1; max_blindex >= 3; max_blindex--)
                             if (T.blen[c_ct.bl_order[max_blindex]] != 0) break;
@@ -3432,7 +3691,13 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         }
         break;
     }
-    case 4: hipLaunchKernelGGL(k_encode, grid, dim3(kEncThreads), 0, st, job); break;
+    case 4: {
+        // ZGPU_ENCODE_VARIANT=1: the one-lane tree build (t_build) instead of w_build
+        static const int ev = [] { const char *e = getenv("ZGPU_ENCODE_VARIANT"); return e ? atoi(e) : 0; }();
+        if (ev == 1) hipLaunchKernelGGL(k_encode<false>, grid, dim3(kEncThreads), 0, st, job);
+        else hipLaunchKernelGGL(k_encode<true>, grid, dim3(kEncThreads), 0, st, job);
+        break;
+    }
     case 7: hipLaunchKernelGGL(k_parse_huff, grid, dim3(kHuffThreads), 0, st, job); break;
     case 8: hipLaunchKernelGGL(k_parse_rle, grid, dim3(64), 0, st, job); break;
     case 9: hipLaunchKernelGGL(k_count, grid, dim3(kCntThreads), 0, st, job); break;
