@@ -2775,6 +2775,7 @@ constexpr int kStgWords = 2048;                 // 8 KiB output staging window
 constexpr int kEncGroup = kEncThreads / 64;     // blocks whose trees are built at once (one per wave)
 constexpr int kStgBits = kStgWords * 32;
 constexpr int kWNodeSlots = (kHeapSize + 63) / 64;   // w_build: tree nodes per lane (9)
+constexpr unsigned kEncWaveBuildMax = 1024;          // w_build below this many buffers per launch
 
 struct TreeLDS {
     // leaves: freq/code; all nodes: dad/len (internal-node freqs live in heap keys)
@@ -2786,7 +2787,7 @@ struct TreeLDS {
     uint8_t blen[2 * kBLCodes + 2];
     uint32_t heap[kHeapSize + 1];        // packed keys, see hkey()
     uint16_t bl_count[kMaxBits + 1];
-    uint32_t pj[2][kWNodeSlots * 64];    // w_build: pointer-jumping exchange (dad | depth << 16)
+    uint32_t pj[kWNodeSlots * 64];       // w_build: pointer-jumping exchange (dad | depth << 16)
 };
 
 struct TreeRef {
@@ -3048,34 +3049,32 @@ __device__ __attribute__((always_inline)) inline void w_build(TreeRef &t, TreeLD
 
     // gen_bitlen (trees.c:406-485): depth of every node by pointer jumping; len = min(depth, max_length),
     // overflow = nodes deeper than max_length (a clamped parent pushes its children past it too)
-    uint32_t nid[kWNodeSlots], P[kWNodeSlots], Dp[kWNodeSlots], fq[kWNodeSlots];
+    uint32_t key[kWNodeSlots], pd[kWNodeSlots];        // heap key; dad | depth << 16
 #pragma unroll
     for (int i = 0; i < kWNodeSlots; i++) {
         const int hh = heap_max + (int)lane + 64 * i;
         const bool valid = hh < kHeapSize;
-        const uint32_t key = valid ? hs[hh] : hkey(0, 0, rootn);
-        nid[i] = key & 1023u;
-        fq[i] = key >> 16;
-        P[i] = nid[i] == rootn ? rootn : t.dad[nid[i]];
-        Dp[i] = nid[i] == rootn ? 0u : 1u;
-        if (valid) h.pj[0][nid[i]] = P[i] | (Dp[i] << 16);
+        key[i] = valid ? hs[hh] : hkey(0, 0, rootn);
+        const uint32_t n = key[i] & 1023u;
+        pd[i] = n == rootn ? rootn : (t.dad[n] | (1u << 16));
+        if (valid) h.pj[n] = pd[i];
     }
     for (int r = 0; r < 9; r++) {                      // 2^9 > the deepest tree (285)
         bool open = false;
 #pragma unroll
-        for (int i = 0; i < kWNodeSlots; i++) open |= P[i] != rootn;
+        for (int i = 0; i < kWNodeSlots; i++) open |= (pd[i] & 0xffffu) != rootn;
         if (!__any(open)) break;
+        // in place: the wave's reads of a round are all issued before its writes, and LDS keeps one
+        // wave's instructions in order
         __builtin_amdgcn_wave_barrier();
-        const uint32_t *src = h.pj[r & 1];
-        uint32_t *dst = h.pj[(r + 1) & 1];
         uint32_t w[kWNodeSlots];
 #pragma unroll
-        for (int i = 0; i < kWNodeSlots; i++) w[i] = src[P[i]];
+        for (int i = 0; i < kWNodeSlots; i++) w[i] = h.pj[pd[i] & 0xffffu];
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int i = 0; i < kWNodeSlots; i++) {
-            Dp[i] += w[i] >> 16;
-            P[i] = w[i] & 0xffffu;
-            if (heap_max + (int)lane + 64 * i < kHeapSize) dst[nid[i]] = P[i] | (Dp[i] << 16);
+            pd[i] = (w[i] & 0xffffu) | (((pd[i] >> 16) + (w[i] >> 16)) << 16);
+            if (heap_max + (int)lane + 64 * i < kHeapSize) h.pj[key[i] & 1023u] = pd[i];
         }
     }
     int overflow = 0;
@@ -3086,17 +3085,17 @@ __device__ __attribute__((always_inline)) inline void w_build(TreeRef &t, TreeLD
 #pragma unroll
     for (int i = 0; i < kWNodeSlots; i++) {
         const bool valid = heap_max + (int)lane + 64 * i < kHeapSize;
-        const int bits = (int)Dp[i] > max_length ? max_length : (int)Dp[i];
-        const bool leaf = valid && (int)nid[i] <= max_code;
+        const int dep = (int)(pd[i] >> 16), n = (int)(key[i] & 1023u);
+        const int bits = dep > max_length ? max_length : dep;
+        const bool leaf = valid && n <= max_code;
         if (valid) {
-            overflow += (int)Dp[i] > max_length;
-            t.len[nid[i]] = (uint8_t)bits;
+            overflow += dep > max_length;
+            t.len[n] = (uint8_t)bits;
         }
         if (leaf) {
-            const int n = (int)nid[i];
             const int xb = n >= xbase ? extra[n - xbase] : 0;
-            ol += (int64_t)fq[i] * (bits + xb);
-            if (slen) sl += (int64_t)fq[i] * (slen[n] + xb);
+            ol += (int64_t)(key[i] >> 16) * (bits + xb);
+            if (slen) sl += (int64_t)(key[i] >> 16) * (slen[n] + xb);
         }
 #pragma unroll
         for (int b = 1; b <= kMaxBits; b++) bc[b] += (uint32_t)__popcll(__ballot(leaf && bits == b));
@@ -3692,9 +3691,12 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         break;
     }
     case 4: {
-        // ZGPU_ENCODE_VARIANT=1: the one-lane tree build (t_build) instead of w_build
+        // Tree build: the whole wave (w_build) for launches of few buffers, where one block's build is the
+        // kernel's latency; one lane (t_build) for large batches, where the other resident waves hide it
+        // and t_build's fewer registers and instructions win. ZGPU_ENCODE_VARIANT=1 / 2 forces lane / wave.
         static const int ev = [] { const char *e = getenv("ZGPU_ENCODE_VARIANT"); return e ? atoi(e) : 0; }();
-        if (ev == 1) hipLaunchKernelGGL(k_encode<false>, grid, dim3(kEncThreads), 0, st, job);
+        const bool lane_build = ev == 1 || (ev != 2 && grid.x >= kEncWaveBuildMax);
+        if (lane_build) hipLaunchKernelGGL(k_encode<false>, grid, dim3(kEncThreads), 0, st, job);
         else hipLaunchKernelGGL(k_encode<true>, grid, dim3(kEncThreads), 0, st, job);
         break;
     }
