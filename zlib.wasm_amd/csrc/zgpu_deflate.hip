@@ -2802,7 +2802,8 @@ struct TreeRef {
 __device__ inline uint32_t hkey(uint32_t freq, uint32_t depth, uint32_t node) {
     return (freq << 16) | (depth << 10) | node;
 }
-__device__ inline bool hle(uint32_t a, uint32_t b) { return (a >> 10) <= (b >> 10); }
+// (a >> 10) <= (b >> 10)  <=>  a < ((b >> 10) + 1) << 10  <=>  a <= (b | 1023): one OR, no shifts
+__device__ inline bool hle(uint32_t a, uint32_t b) { return a <= (b | 1023u); }
 
 __device__ void t_downheap(uint32_t *heap, int heap_len, int k) {        // pqdownheap
     const uint32_t v = heap[k];
