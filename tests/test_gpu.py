@@ -562,8 +562,9 @@ def test_huffman_length_overflow(zg, oracle):
     """Literal counts on a Fibonacci ladder (a 19-leaf tree 18 deep): gen_bitlen's
     overflow repair (trees.c:446-484) in the literal tree, and skewed code-length
     counts for the bit-length tree (max 7).  k_encode's wave-wide tree build
-    (w_build) against the oracle, Z_HUFFMAN_ONLY and level 6/9 parses, one and
-    several blocks."""
+    (w_build, launches under 1024 buffers) and its one-lane build (t_build, a
+    1026-buffer launch) against the oracle, Z_HUFFMAN_ONLY and level 1/6/9
+    parses, one and several blocks."""
     fib = [1, 1]
     while len(fib) < 19:
         fib.append(fib[-1] + fib[-2])
@@ -580,3 +581,10 @@ def test_huffman_length_overflow(zg, oracle):
         res = zg.compress_batch(bufs, level=level, strategy=strategy)
         for b, (st, z) in zip(bufs, res):
             assert st == 0 and z == oracle.compress(b, level, strategy=strategy)[1], (len(b), level, strategy)
+    # >= 1024 buffers in one launch: k_encode's one-lane build (t_build), same inputs
+    many = bufs * 171
+    for level, strategy in ((6, 2), (6, 0)):
+        want = [oracle.compress(b, level, strategy=strategy)[1] for b in bufs]
+        res = zg.compress_batch(many, level=level, strategy=strategy)
+        for i, (st, z) in enumerate(res):
+            assert st == 0 and z == want[i % len(bufs)], (i, level, strategy)
