@@ -14,13 +14,15 @@ buffers, 1/2/4/8 GPU".
   §8(d): n + out_len per deflate buffer, n + 4 per checksum buffer.
 * adler32 leg (C5 shape: 16 MiB small-vocabulary buffers, 4 GiB per launch)
   reported as "adler32" with its own roofline.
-* cpu_baseline (rank 0, N=1 only): the oracle port (oracle/liboracle.so, our C
-  restatement of the reference deflate.c/trees.c) timed on a bounded sample of
-  the same buffers, on 1 thread and on every CPU this process may run on
-  (os.sched_getaffinity); kind "port" (the compiled reference never leaves the
-  build container); plus host system zlib on the same sample
-  (`system_zlib`), checked byte-identical first.  `host` records nproc, the
-  affinity set, the cgroup CPU quota and the CPU model.
+* cpu_baseline (rank 0, N=1 only): the host's system zlib (the
+  upstream zlib the reference vendors; its streams are checked byte-identical to
+  ours, i.e. to the reference's, on the sample first) timed from C
+  (oracle/libzbase.so, no Python in the loop) on a bounded sample of >= 64
+  distinct buffers of the same batch, on 1 thread and on every CPU this process
+  may use (the affinity set capped at the cgroup quota); `port` gives the oracle
+  port (oracle/liboracle.so) on the same sample for comparison.  The crc32 and
+  adler32 legs carry their own system-zlib baselines.  `host` records nproc,
+  the affinity set, the cgroup CPU quota and the CPU model.
 * roofline.traffic: HBM bytes per launch from the committed rocprofv3 PMC
   passes of the same launch shape (profiles/), FETCH_SIZE x2 + WRITE_SIZE.
 * After timing, a sample of outputs is checked bit-exact against the oracle and
@@ -86,12 +88,13 @@ def parse(argv=None):
     ap.add_argument("--crc-bytes", type=int, default=4096)
     ap.add_argument("--adler-buffers", type=int, default=256, help="C5-shaped Adler-32 leg (0: skip)")
     ap.add_argument("--adler-bytes", type=int, default=16 << 20)
-    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="per CPU measurement")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="per CPU measurement")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the all-core CPU run (0: every CPU in the affinity set)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-inflate", action="store_true", help="skip the inflate round-trip leg")
-    ap.add_argument("--verify", type=int, default=8, help="outputs checked vs oracle")
+    ap.add_argument("--verify", type=int, default=64,
+                    help="outputs checked bit-exact vs the oracle (at most 64 MiB of them); also the CPU sample")
     ap.add_argument("--inflight-mb", type=int, default=4096,
                     help="input bytes per deflate sub-batch (workspace ~15 B per byte)")
     ap.add_argument("--cpu-dry-run", action="store_true",
@@ -362,14 +365,24 @@ def progress(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def cpu_baselines(a, sample, want, level):
-    """Oracle port and system zlib on 1 thread and on all CPUs this process may
-    use: the affinity set, capped at the cgroup CPU quota when there is one
-    (more threads than the quota's CPUs share the same CPU time and only
-    stretch the run); SURVEY §8(d) / BASELINE.md §3."""
-    import zlib
-    from zhelpers import Oracle
-    o = Oracle()
+def _zbase():
+    """oracle/libzbase.so: system zlib timed from C threads (bench infrastructure)."""
+    import ctypes as C
+    lib = C.CDLL(os.path.join(ROOT, "oracle", "libzbase.so"))
+    lib.zb_compress_rate.restype = C.c_double
+    lib.zb_compress_rate.argtypes = [C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_int, C.c_int, C.c_int,
+                                     C.c_double, C.POINTER(C.c_uint64)]
+    for f in (lib.zb_crc32_rate, lib.zb_adler32_rate):
+        f.restype = C.c_double
+        f.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_int, C.c_double, C.POINTER(C.c_uint64)]
+    lib.zb_zlib_version.restype = C.c_char_p
+    return lib
+
+
+def cpu_threads(a):
+    """(threads, host info, quota): every CPU this process may use -- the affinity
+    set, capped at the cgroup CPU quota when there is one (more threads than the
+    quota's CPUs share the same CPU time and only stretch the run)."""
     host = host_info()
     quota = None
     try:
@@ -380,35 +393,92 @@ def cpu_baselines(a, sample, want, level):
     allt = a.cpu_threads or host["affinity_cpus"]
     if not a.cpu_threads and quota:
         allt = max(1, min(allt, int(quota + 0.999)))
+    return allt, host, quota
+
+
+def cpu_baselines(a, sample, want, level):
+    """System zlib and the oracle port on 1 thread and on all
+    CPUs this process may use; SURVEY §8(d) / BASELINE.md §3."""
+    import ctypes as C
+    import zlib
+    from zhelpers import Oracle
+    o = Oracle()
+    allt, host, quota = cpu_threads(a)
     secs = a.cpu_seconds
+    zb = _zbase()
+    ver = zb.zb_zlib_version().decode()
+    bufs = [C.create_string_buffer(b, len(b)) for b in sample]
+    ptrs = (C.c_void_p * len(bufs))(*[C.cast(b, C.c_void_p) for b in bufs])
+    lens = (C.c_size_t * len(bufs))(*[len(b) for b in sample])
+    done = C.c_uint64(0)
+    ident = all(zlib.compress(b, level) == z for b, z in zip(sample, want))
+    mb = sum(len(b) for b in sample) / 1e6
+    progress(f"cpu baseline: system zlib {ver}, 1 thread then {allt} ({len(sample)} buffers, {mb:.0f} MB)")
+    sys1 = zb.zb_compress_rate(ptrs, lens, len(bufs), level, 1, secs / 2, C.byref(done))
+    sysn = zb.zb_compress_rate(ptrs, lens, len(bufs), level, allt, secs, C.byref(done))
+    sysn_b = done.value
     progress(f"cpu baseline: oracle port, 1 thread then {allt}")
-    port1, _ = _timed_threads(lambda b: o.compress(b, level), sample, 1, secs / 2)
-    portn, portn_b = _timed_threads(lambda b: o.compress(b, level), sample, allt, secs)
-    cpu = {"value": round(portn, 2), "unit": "MB/s", "cores": allt, "kind": "port",
-           "cpu_quota_cpus": quota,
-           "per_core_1thread": round(port1, 2),
-           "sample": f"{len(sample)} distinct {a.buffer_bytes} B {a.kind} buffers of this batch, "
-                     f"compressed repeatedly at level {level} by oracle/liboracle.so: ~{secs / 2:.0f} s on "
-                     f"1 thread, ~{secs:.0f} s ({portn_b / 1e6:.0f} MB) on {allt} threads "
-                     f"(the CPUs this process may use: affinity set, cgroup quota)",
-           "host": host}
-    ok = all(zlib.compress(b, level) == z for b, z in zip(sample, want))
-    if not ok:
-        cpu["system_zlib"] = {"value": None, "version": zlib.ZLIB_RUNTIME_VERSION,
-                              "note": "system zlib output differs from the reference stream; not timed"}
-        return cpu
-    progress(f"cpu baseline: system zlib, 1 thread then {allt}")
-    sys1, _ = _timed_threads(lambda b: zlib.compress(b, level), sample, 1, secs / 2)
-    sysn, sysn_b = _timed_threads(lambda b: zlib.compress(b, level), sample, allt, secs)
-    cpu["system_zlib"] = {
-        "value": round(sysn, 2), "unit": "MB/s", "cores": allt, "per_core_1thread": round(sys1, 2),
-        "all_host_cpus_linear_estimate": round(sys1 * host["nproc"], 1),
-        "version": zlib.ZLIB_RUNTIME_VERSION, "bit_identical_on_sample": True,
-        "sample": f"same {len(sample)} buffers; {sysn_b / 1e6:.0f} MB on {allt} threads"}
-    return cpu
+    port1, _ = _timed_threads(lambda b: o.compress(b, level), sample, 1, secs / 4)
+    portn, portn_b = _timed_threads(lambda b: o.compress(b, level), sample, allt, secs / 2)
+    return {"value": round(sysn, 2), "unit": "MB/s", "cores": allt,
+            "kind": "reference",
+            "kind_note": f"system zlib {ver} compress2() (upstream zlib: the deflate.c/trees.c the reference "
+                         f"vendors as zlib 1.3.1.1-motley; BASELINE.md §3.1), "
+                         + ("byte-identical to this run's GPU streams on every sample buffer"
+                            if ident else "NOT byte-identical on the sample"),
+            "bit_identical_on_sample": ident,
+            "cpu_quota_cpus": quota,
+            "per_core_1thread": round(sys1, 2),
+            "all_host_cpus_linear_estimate": round(sys1 * host["nproc"], 1),
+            "sample": f"{len(sample)} distinct {a.buffer_bytes} B {a.kind} buffers of this batch "
+                      f"(evenly strided indices, the ones verified bit-exact), compressed repeatedly at level "
+                      f"{level} from C threads: ~{secs / 2:.0f} s on 1 thread, ~{secs:.0f} s "
+                      f"({sysn_b / 1e6:.0f} MB) on {allt} threads (the CPUs this process may use: affinity "
+                      f"set capped at the cgroup quota)",
+            "port": {"value": round(portn, 2), "per_core_1thread": round(port1, 2), "cores": allt,
+                     "note": f"oracle/liboracle.so (our C restatement of deflate.c/trees.c) on the same sample, "
+                             f"{portn_b / 1e6:.0f} MB"},
+            "host": host}
+
+
+def checksum_cpu_baseline(a, which, c):
+    """System zlib crc32()/adler32() over the leg's own buffers (the first 64 MiB
+    of them, in the leg's buffer size) on 1 thread and on all CPUs this process
+    may use."""
+    import ctypes as C
+    allt, _, _ = cpu_threads(a)
+    nb = max(1, min(c["B"], (64 << 20) // c["n"]))
+    host = c["src"][:nb * c["n"]].cpu().numpy()
+    buf = C.create_string_buffer(host.tobytes(), nb * c["n"])
+    zb = _zbase()
+    fn = zb.zb_crc32_rate if which == "crc32" else zb.zb_adler32_rate
+    done = C.c_uint64(0)
+    secs = max(1.0, a.cpu_seconds / 4)
+    one = fn(buf, nb * c["n"], c["n"], 1, secs / 2, C.byref(done))
+    alln = fn(buf, nb * c["n"], c["n"], allt, secs, C.byref(done))
+    out = {"value": round(alln / 1e3, 3), "unit": "GB/s", "cores": allt, "kind": "reference",
+           "kind_note": f"system zlib {zb.zb_zlib_version().decode()} {which}()",
+           "per_core_1thread": round(one / 1e3, 3),
+           "sample": f"{nb} x {c['n']} B buffers of this leg, one {which}() call per buffer, repeatedly: "
+                     f"~{secs / 2:.1f} s on 1 thread, ~{secs:.1f} s ({done.value / 1e9:.1f} GB) on {allt} threads"}
+    if which == "crc32":
+        out["reference_braided_crc32_per_core_container"] = {
+            "value": 2.26, "unit": "GB/s",
+            "note": "the reference's zlib 1.3.1.1 braided crc32 measured in the build container (BASELINE.md §2); "
+                    "system zlib 1.2.11's crc32 is about 2x slower"}
+    return out
 
 
 # ------------------------------------------------------------------ reporting
+
+def shipped_kernels():
+    """Kernel instances compiled into the current libzgpu.so ("k_match<false, false>", ...),
+    from the host-side launch stubs."""
+    import re
+    out = subprocess.run(["nm", "-C", os.path.join(ROOT, "zlib.wasm_amd", "libzgpu.so")],
+                         capture_output=True, text=True).stdout
+    return set(m.group(1) for m in re.finditer(r"__device_stub__(k_[A-Za-z0-9_]+(?:<[^>]*>)?)\(", out))
+
 
 def pmc_traffic(kernels, tag):
     """HBM bytes per launch of a leg from the committed rocprofv3 PMC passes
@@ -417,23 +487,33 @@ def pmc_traffic(kernels, tag):
     this launch's shape (the file name carries the shape tag).  `kernels`: the
     name prefixes of the kernels one launch of the leg runs; for each, only the
     dispatches with its largest grid (the leg's own launches, not the small
-    verification or trailer launches of the same kernel) are averaged."""
+    verification or trailer launches of the same kernel) are averaged.  A
+    profile of a kernel instance the current library does not ship (a renamed
+    template, an old A/B variant) is refused: the figure must be of the timed
+    kernel."""
     import csv
     import glob
     fetch = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_fetch_*{tag}*.csv")))
     write = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_write_*{tag}*.csv")))
     if not fetch or not write:
         return None, None
+    shipped = shipped_kernels()
+
+    def name(r):
+        return r["Kernel_Name"].split("(")[0].replace("void ", "").replace("zgpu::", "")
 
     def per_launch(path, counter):
         total = 0.0
         rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
         for k in kernels:
-            mine = [r for r in rows if r["Kernel_Name"].split("(")[0].replace("void ", "").startswith("zgpu::" + k)]
+            mine = [r for r in rows if name(r).startswith(k)]
             if not mine:
                 return None
             g = max(int(r["Grid_Size"]) for r in mine)
-            vals = [float(r["Counter_Value"]) for r in mine if int(r["Grid_Size"]) == g]
+            top = [r for r in mine if int(r["Grid_Size"]) == g]
+            if any(name(r) not in shipped for r in top):
+                return None
+            vals = [float(r["Counter_Value"]) for r in top]
             total += sum(vals) / len(vals) * 1024.0
         return total
 
@@ -452,7 +532,7 @@ def launches_tag(a):
     return f"{per}x{a.buffer_bytes}"
 
 
-def checksum_report(a, c, D, which, tag):
+def checksum_report(a, c, D, which, tag, cpu=None):
     el, = D.max(c["elapsed"])
     tot, = D.sum(float(c["bytes"]) * a.steps)
     alg = (c["n"] + 4) * c["B"]
@@ -466,7 +546,8 @@ def checksum_report(a, c, D, which, tag):
             "roofline": {"bound": "hbm", "kernel": kern, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                          "traffic": None if traffic is None else int(traffic), "traffic_source": src,
-                         "alg_bytes_per_launch": alg, "avg_launch_ms": round(c["kernel_ms"], 4)}}
+                         "alg_bytes_per_launch": alg, "avg_launch_ms": round(c["kernel_ms"], 4)},
+            "cpu_baseline": cpu}
 
 
 def main(argv=None):
@@ -503,7 +584,8 @@ def main(argv=None):
     n = a.buffer_bytes
     if not a.cpu_dry_run:
         h_dlen = d["dlen"].cpu().numpy()
-        idx = sorted(set(int(i) for i in torch.linspace(0, a.buffers - 1, a.verify).tolist())) \
+        nver = min(a.verify, max(1, (64 << 20) // n))
+        idx = sorted(set(int(i) for i in torch.linspace(0, a.buffers - 1, nver).tolist())) \
             if a.verify > 0 else []
         for i in idx:
             progress(f"verifying buffer {i} against the oracle")
@@ -525,8 +607,11 @@ def main(argv=None):
     if inf is not None:
         inf_el, = D.max(inf["elapsed"])
         inf_total, = D.sum(float(inf["out_bytes"]) * a.steps)
-    crc = None if c is None else checksum_report(a, c, D, "crc32", f"C2_{a.crc_buffers}x{a.crc_bytes}")
-    adl = None if ad is None else checksum_report(a, ad, D, "adler32", f"A5_{a.adler_buffers}x{a.adler_bytes}")
+    cpu_on = not a.no_cpu and not a.cpu_dry_run and D.world == 1 and D.rank == 0
+    crc = None if c is None else checksum_report(a, c, D, "crc32", f"C2_{a.crc_buffers}x{a.crc_bytes}",
+                                                 checksum_cpu_baseline(a, "crc32", c) if cpu_on else None)
+    adl = None if ad is None else checksum_report(a, ad, D, "adler32", f"A5_{a.adler_buffers}x{a.adler_bytes}",
+                                                  checksum_cpu_baseline(a, "adler32", ad) if cpu_on else None)
 
     if D.rank == 0:
         mbps = in_total / el / 1e6
@@ -563,6 +648,10 @@ def main(argv=None):
         cpu = None
         if not a.no_cpu and sample and D.world == 1:
             cpu = cpu_baselines(a, sample, want, a.level)
+            cpu["gpu_over_cpu"] = {"vs_value": round(mbps / cpu["value"], 2),
+                                   "vs_one_core": round(mbps / cpu["per_core_1thread"], 1),
+                                   "vs_all_host_cpus_linear_estimate":
+                                       round(mbps / cpu["all_host_cpus_linear_estimate"], 3)}
         line = {
             "metric": METRIC,
             "value": round(mbps, 1),

@@ -81,6 +81,23 @@ def test_no_oracle_linkage():
     assert "zo_" not in syms
 
 
+def test_no_probe_or_variant_kernels_shipped():
+    """The product library carries one k_match instance per job kind (batch /
+    flush job x per buffer / per segment) and no timing probes, statistics
+    builds or A/B walk variants; no environment variable selects a different
+    match finder or parse (VERDICT r2 #7)."""
+    import subprocess
+    syms = subprocess.run(["nm", "-C", LIB], capture_output=True, text=True).stdout
+    inst = set(re.findall(r"__device_stub__k_match<([^>]*)>", syms))
+    assert inst == {"false, false", "false, true", "true, false", "true, true"}, inst
+    fast = set(re.findall(r"__device_stub__k_parse_fast<([^>]*)>", syms))
+    assert all(", true, " in f for f in fast), fast            # only the one-round-trip walk
+    assert not re.search(r"g_[dm]stat|mw14|dw_walk|dwp_walk", syms)
+    blob = open(LIB, "rb").read()
+    for env in (b"ZGPU_MATCH_VARIANT", b"ZGPU_FAST_VARIANT"):
+        assert env not in blob, env
+
+
 def test_oversize_buffers_refused_before_gpu_work(lib):
     """Kernels address a buffer with 32-bit positions: buffers of 4 GiB - 64 KiB
     or more are refused up front (ADVICE r1), never truncated into a stream that

@@ -1528,7 +1528,7 @@ struct internal_state {
     uint32_t res_byte = 0;
     // levels 1..3: k_parse_fast's hash chains at the resume point (head[] as
     // part positions, prev links of [res_S, res_pos)) and as the last job left them
-    zvec<uint32_t> fast_head;
+    zvec<uint64_t> fast_head;       // level 1-3 head[] at the resume point: 64-bit part positions
     zvec<uint16_t> fast_prev;
     // inflate streams
     int inflating = 0;
@@ -1696,7 +1696,7 @@ int deflate_part(internal_state *s, bool closed) {
         if (s->res_pos > base && !fh.dict) {                   // rebase the saved chains to this buffer
             head_in.resize(s->fast_head.size());
             for (size_t i = 0; i < head_in.size(); i++)
-                head_in[i] = s->fast_head[i] > base ? s->fast_head[i] - (uint32_t)base : 0;
+                head_in[i] = s->fast_head[i] > base ? (uint32_t)(s->fast_head[i] - base) : 0;
             fh.head_in = head_in.data();
             fh.prev_in = s->fast_prev.data();
             fh.prev_n = s->fast_prev.size();
@@ -1855,9 +1855,12 @@ void choose_resume(internal_state *s) {
             if (b > it.rec + (s->ev_type[k] == kEvPause ? 1u : 0u)) { s->res_ev = k; break; }
         }
         if (fast) {
-            const uint32_t b = (uint32_t)s->job_base;
+            // job-relative heads -> part positions in 64 bits: a part may run past 4 GiB
+            // (in_base moves with every resume), a job never does (its input is < kMaxBuffer)
+            const uint64_t b = s->job_base;
             s->fast_head.resize(s->snap_head.size());
-            for (size_t i = 0; i < s->snap_head.size(); i++) s->fast_head[i] = s->snap_head[i] ? s->snap_head[i] + b : 0;
+            for (size_t i = 0; i < s->snap_head.size(); i++)
+                s->fast_head[i] = s->snap_head[i] ? (uint64_t)s->snap_head[i] + b : 0;
             s->fast_prev.assign(s->snap_prev.begin(), s->snap_prev.end());
         }
         if (s->res_S > s->in_base) {                 // the input before the window is not needed again
@@ -2548,13 +2551,40 @@ int deflateEnd(z_streamp strm) {
     return Z_OK;
 }
 
+// deflate_state's strstart != 0 (deflateBound's DICTID allowance): a preset
+// dictionary or a flush put positions behind the parse, or the parse has
+// decided a position -- which a Z_NO_FLUSH call does once the lookahead it
+// leaves (below MIN_LOOKAHEAD, at most MAX_MATCH for Z_RLE, 0 for
+// Z_HUFFMAN_ONLY) is less than what it has read.  A Z_FULL_FLUSH resets it
+// (deflate.c:1225-1229), as it resets the part.
+static bool strstart_nonzero(const internal_state *s) {
+    if (s->level == 0) return s->st_strstart != 0;
+    if (s->flush_done > 0) return true;
+    const size_t need = s->strategy == Z_HUFFMAN_ONLY ? 1 : s->strategy == Z_RLE ? kMaxMatch + 1 : kMinLookahead;
+    return s->rd >= need;
+}
+
 uLong deflateBound(z_streamp strm, uLong sourceLen) {          // deflate.c:842-905
     const uLong fixedlen = sourceLen + (sourceLen >> 3) + (sourceLen >> 8) + (sourceLen >> 9) + 4;
     const uLong storelen = sourceLen + (sourceLen >> 5) + (sourceLen >> 7) + (sourceLen >> 11) + 7;
-    if (!strm || !strm->state) return (fixedlen > storelen ? fixedlen : storelen) + 18;
+    if (!strm || !strm->state || strm->state->inflating) return (fixedlen > storelen ? fixedlen : storelen) + 18;
     const internal_state *s = strm->state;
-    const int w = s->wrap;
-    const uLong wraplen = w == 0 ? 0 : w == 1 ? 6 : 18;
+    // deflate() negates wrap once the trailer is written: then the default row (6)
+    const int w = s->finished && s->wrap ? -1 : s->wrap;
+    uLong wraplen = 6;
+    if (w == 0) {
+        wraplen = 0;
+    } else if (w == 1) {
+        wraplen = 6 + (strstart_nonzero(s) ? 4 : 0);
+    } else if (w == 2) {
+        wraplen = 18;
+        if (const gz_header *h = s->gzhead) {                      // the caller's header, read now
+            if (h->extra) wraplen += 2 + h->extra_len;
+            if (const Bytef *str = h->name) do wraplen++; while (*str++);
+            if (const Bytef *str = h->comment) do wraplen++; while (*str++);
+            if (h->hcrc) wraplen += 2;
+        }
+    }
     if (s->wbits != 15 || s->mem_level + 7 != 8 + 7)   // not the default parameters: a conservative bound
         return (s->wbits <= s->mem_level + 7 && s->level ? fixedlen : storelen) + wraplen;
     return sourceLen + (sourceLen >> 12) + (sourceLen >> 14) + (sourceLen >> 25) + 13 - 6 + wraplen;

@@ -450,143 +450,18 @@ __device__ __attribute__((always_inline)) inline void tile_store(uint32_t *E, co
             make_uint4(P.pb[0] << 16, P.pb[1] << 16, P.pb[2] << 16, P.pb[3] << 16);
 }
 
-// One position's longest_match walk (deflate.c:1356-1497) over the packed
-// window: byte addresses (4 x window index), no chain-end test (nil_link), the
-// chain/4 snapshot between two loops (no per-step snapshot test), the next
-// candidate's two words loaded before the current one is tested, and both
-// quick-reject pairs tested as one predicate so both loads precede the single
-// branch.  A nice-length stop is folded into the limit test (limit4 = INT_MAX).
-struct MW3 {
-    int s4, m4, be4, best, bpos4, limit4, nice, maxcmp;
-    uint32_t count, scan01, scanE;
-    uint32_t ncmp;            // compares (statistics build only)
-};
-
 // The compare: the first 16 scan bytes are held in registers (loaded once per
 // walk); a hit reads the candidate word by word (most compares end in the
 // first 4-8 bytes) and longer matches continue 16 bytes (both sides) per LDS
 // round trip.
 struct Scan16 { uint32_t s0, s1, s2, s3; };
 
-// first mismatching byte of a 4-byte xor word at byte offset `at`, or 99 if none
-__device__ __attribute__((always_inline)) inline int mism(uint32_t x, int at) {
-    return x ? at + (int)(__builtin_ctz(x) >> 3) : 99;
-}
-
-template <bool kBatch>
-__device__ __attribute__((always_inline)) inline int cmp16(const uint32_t *E, int m, int s, const Scan16 &S,
-                                                           int maxcmp) {
-    if (kBatch) {
-        // all four candidate words loaded before anything is tested
-        const uint32_t x0 = get4(E, m) ^ S.s0, x1 = get4(E, m + 4) ^ S.s1;
-        const uint32_t x2 = get4(E, m + 8) ^ S.s2, x3 = get4(E, m + 12) ^ S.s3;
-        const int k16 = min(min(mism(x0, 0), mism(x1, 4)), min(mism(x2, 8), mism(x3, 12)));
-        if (k16 < 16 || maxcmp <= 16) return k16 < 16 ? k16 : 16;
-    } else {
-        // word by word: most compares end in the first 4-8 bytes
-        uint32_t x = get4(E, m) ^ S.s0;
-        if (x) return __builtin_ctz(x) >> 3;
-        if ((x = get4(E, m + 4) ^ S.s1)) return 4 + (__builtin_ctz(x) >> 3);
-        if ((x = get4(E, m + 8) ^ S.s2)) return 8 + (__builtin_ctz(x) >> 3);
-        if ((x = get4(E, m + 12) ^ S.s3)) return 12 + (__builtin_ctz(x) >> 3);
-    }
-    int k = 16;
-    while (k < maxcmp) {
-        const uint32_t y0 = get4(E, m + k) ^ get4(E, s + k);
-        const uint32_t y1 = get4(E, m + k + 4) ^ get4(E, s + k + 4);
-        const uint32_t y2 = get4(E, m + k + 8) ^ get4(E, s + k + 8);
-        const uint32_t y3 = get4(E, m + k + 12) ^ get4(E, s + k + 12);
-        const int r = min(min(mism(y0, 0), mism(y1, 4)), min(mism(y2, 8), mism(y3, 12)));
-        if (r < 16) return k + r;
-        k += 16;
-    }
-    return k;
-}
-
-template <int kUnroll, bool kBatch, int kProbe = 0>
-__device__ __attribute__((always_inline)) inline bool mw14_loop(MW3 &w, uint32_t &em, uint32_t &eb,
-                                                                const Scan16 &S, const uint32_t *E, uint32_t end) {
-    const char *Eb = reinterpret_cast<const char *>(E);
-#pragma unroll kUnroll
-    for (;;) {
-        const int m4n = w.m4 - (int)((em & 0xffffu) << 2);
-        const int a = m4n > 0 ? m4n : 0;
-        const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + a);
-        uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
-        const uint32_t miss = ((em >> 16) ^ w.scan01) | ((eb >> 16) ^ w.scanE);
-        if (kProbe != 1 && __builtin_expect(miss == 0, 0)) {
-            w.ncmp++;
-            const int m = w.m4 >> 2, s = w.s4 >> 2;
-            const int k = cmp16<kBatch>(E, m, s, S, w.maxcmp);
-            const int len = k < w.maxcmp ? k : w.maxcmp;
-            if (kProbe == 2) {
-                w.ncmp += (uint32_t)len;             // probe 38: compare, keep nothing
-            } else if (len > w.best) {
-                w.best = len;
-                w.bpos4 = w.m4;
-                if (len >= w.nice) w.limit4 = 0x7fffffff;
-                w.be4 = (len - 1) * 4;
-                w.scanE = E[s + len - 1] >> 16;
-                ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
-            }
-        }
-        w.count++;
-        w.m4 = m4n;
-        em = emn;
-        eb = ebn;
-        if (m4n <= w.limit4) return true;
-        if (w.count >= end) return false;
-    }
-}
-
-template <int kUnroll, bool kBatch, int kProbe = 0>
-__device__ __attribute__((always_inline)) inline void mw14_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
-                                                                const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
-                                                                int want_q, int64_t max_dist,
-                                                                uint32_t *st_steps = nullptr,
-                                                                uint32_t *st_cmp = nullptr) {
-    const int s = (int)(p - B);
-    const uint32_t e0 = E[s];
-    const uint32_t d0 = e0 & 0xffffu;
-    if (d0 > (uint32_t)max_dist) {                 // deflate.c:1955: strstart - hash_head <= MAX_DIST
-        rf[p] = 0;
-        if (want_q) rq[p] = 0;
-        return;
-    }
-    MW3 w;
-    const int64_t labs = p > max_dist ? p - max_dist : 0;
-    w.limit4 = (int)(labs - B) * 4;
-    const int64_t rem = n - p;
-    w.nice = rem < cfg.nice ? (int)rem : cfg.nice;
-    w.maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
-    w.s4 = s * 4;
-    w.m4 = (s - (int)d0) * 4;
-    w.best = kMinMatch - 1;
-    w.bpos4 = 0;
-    w.be4 = (kMinMatch - 2) * 4;
-    w.scan01 = e0 >> 16;
-    w.scanE = E[s + 1] >> 16;
-    w.count = 0;
-    w.ncmp = 0;
-    Scan16 S{get4(E, s), get4(E, s + 4), get4(E, s + 8), get4(E, s + 12)};
-    uint32_t em = E[s - (int)d0];
-    uint32_t eb = E[s - (int)d0 + 1];
-    const uint32_t qc = want_q ? (uint32_t)(cfg.chain >> 2) : (uint32_t)cfg.chain;
-    const bool done = mw14_loop<kUnroll, kBatch, kProbe>(w, em, eb, S, E, qc);
-    if (want_q) {
-        rq[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
-        if (!done) mw14_loop<kUnroll, kBatch, kProbe>(w, em, eb, S, E, (uint32_t)cfg.chain);
-    }
-    rf[p] = w.best >= kMinMatch ? (((uint32_t)w.best << 16) | (uint32_t)((w.s4 - w.bpos4) >> 2)) : 0u;
-    if (kProbe) rf[p] = (w.count ^ (uint32_t)w.m4 ^ w.ncmp) == 0x7fffffffu ? 1u : 0u;   // probe: keep the walk live
-    if (st_steps) { *st_steps = w.count; *st_cmp = w.ncmp; }
-}
 
 // ------------------------------------------------------------------------
-// The deferred-compare walk (default).  In mw14_walk a lane whose candidate
-// passes the quick reject compares at once, and the other 63 lanes of its wave
-// wait: 3.4 % of the steps compare, yet 86 % of a wave's steps run the compare
-// code.  Here the compare is taken out of the step:
+// The deferred-compare walk.  A lane whose candidate passes the quick reject
+// would compare at once while the other 63 lanes of its wave wait (3.4 % of
+// the steps compare, yet 86 % of a wave's steps would run the compare code).
+// The compare is therefore taken out of the step:
 //   1. the first kD0 candidates of every walk are compared by the whole wave
 //      together (all lanes start their walks at the same time), so the walk
 //      goes on with the best the chain's head gives -- that is where most
@@ -595,18 +470,20 @@ __device__ __attribute__((always_inline)) inline void mw14_walk(const uint32_t *
 //      pass, pushes the candidate into a kDQ-deep per-lane queue; a stale best
 //      is never larger than the true one, so the queue holds every candidate
 //      the exact walk would compare (and some it would reject);
-//   3. when some lane's queue is full, at the chain/4 budget snapshot and at
-//      the end, the wave empties the queues together, oldest first, applying
-//      longest_match's rule (a strictly longer match wins, stop at nice) with
-//      the true running best: the result equals longest_match's
-//      (deflate.c:1417-1497) for every position.  A lane that reaches nice in a
-//      flush drops its later entries and steps.
-// A CPU model of the C4 mix at L6: 2.1 queued candidates per walk, a full
-// queue (kDQ 4) on 0.3 % of lane steps.
+//   3. when some lane's queue is (nearly) full, at the chain/4 budget snapshot
+//      and at the end, the wave empties the queues together, oldest first,
+//      applying longest_match's rule (a strictly longer match wins, stop at
+//      nice) with the true running best: the result equals longest_match's
+//      (deflate.c:1417-1497) for every position.  A lane that reaches nice in
+//      a flush drops its later entries and steps.
+// The measured alternatives (queue depths 3..8, 1..4 steps per exit test, a
+// one-integer quick reject, two walks per lane, flushes inside the step loop,
+// ...) are recorded in DESIGN.md 4.3; only the fastest ships.
 // ------------------------------------------------------------------------
 constexpr int kD0 = 2;      // leading candidates compared by the whole wave
+constexpr int kDQ = 6;      // deferred-compare queue depth
+constexpr int kDU = 3;      // chain steps per exit test
 __device__ inline uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-constexpr int kDQ = 4;      // deferred-compare queue depth
 
 // bytes i..i+3 from the packed words: one byte permute (v_perm_b32) of the
 // high halves of E[i] and E[i+2]
@@ -644,362 +521,60 @@ __device__ __attribute__((always_inline)) inline int lcp16(const uint32_t *E, in
     }
     return k < maxcmp ? k : maxcmp;
 }
-
-// The walk state between flushes.  Candidate m (byte address m4 = 4 m) has
-// its two words em (link, bytes m, m+1) and eb (bytes m+best-1, m+best)
-// loaded; the queue holds byte addresses, newest in q0.
-struct DWS {
-    int m4, limit4, be4, occ;
-    int q0, q1, q2, q3;
-    uint32_t em, eb, scan01, scanE;
-};
-
-// Steps every lane of the wave until the uniform budget count `end` is
-// reached, some lane's queue is full or no lane has a candidate left.  A lane
-// whose chain ended stays in the loop: its candidate address is then <= the
-// limit and only falls further (links are >= 0), so it queues nothing more.
-// The loop has one exit, taken by the whole wave, and every update is a
-// select.  `count` is wave-uniform (all lanes start their walks together and
-// step together).
-template <bool kIdx = false>
-__device__ __attribute__((always_inline)) inline void dw_steps(DWS &w, const char *Eb, uint32_t &count, uint32_t end) {
-    for (;;) {
-        const bool valid = w.m4 > w.limit4;
-        const int m4n = kIdx ? (int)((w.em << 2) & 0x3fffcu) : w.m4 + (int)(w.em & 0xffffu) * -4;
-        const int a = kIdx ? m4n : (m4n > 0 ? m4n : 0);
-        const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + a);
-        const uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
-        const bool pass = valid & ((w.em >> 16) == w.scan01) & ((w.eb >> 16) == w.scanE);
-        w.q3 = pass ? w.q2 : w.q3;
-        w.q2 = pass ? w.q1 : w.q2;
-        w.q1 = pass ? w.q0 : w.q1;
-        w.q0 = pass ? w.m4 : w.q0;
-        w.occ += pass ? 1 : 0;
-        w.m4 = m4n;
-        w.em = emn;
-        w.eb = ebn;
-        count++;
-        const uint64_t walkers = __ballot(m4n > w.limit4), full = __ballot(w.occ == kDQ);
-        if (count >= end || walkers == 0 || full != 0) break;
-    }
-}
-
-// dw_steps with the full-queue flush inside the loop: when some lane's queue
-// is full, every lane compares its oldest entry (one wave round, a uniform
-// branch) and the walk goes on, with no exit from the loop.  A lane that
-// reaches nice there stops queueing (limit4 = INT_MAX) and drops its entries.
-// Returns at the budget count `end` or when no lane has a candidate left.
-struct DWB {                      // the running best of dw_steps_in
-    int best, bpos4, s, maxcmp, nice;
-};
-
-__device__ __attribute__((always_inline)) inline void dw_steps_in(DWS &w, DWB &b, const uint32_t *E, const Scan16 &S,
-                                                                  uint32_t &count, uint32_t end) {
-    const char *Eb = reinterpret_cast<const char *>(E);
-    for (;;) {
-        const bool valid = w.m4 > w.limit4;
-        const int m4n = w.m4 + (int)(w.em & 0xffffu) * -4;
-        const int a = m4n > 0 ? m4n : 0;
-        const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + a);
-        uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
-        const bool pass = valid & ((w.em >> 16) == w.scan01) & ((w.eb >> 16) == w.scanE);
-        w.q3 = pass ? w.q2 : w.q3;
-        w.q2 = pass ? w.q1 : w.q2;
-        w.q1 = pass ? w.q0 : w.q1;
-        w.q0 = pass ? w.m4 : w.q0;
-        w.occ += pass ? 1 : 0;
-        w.m4 = m4n;
-        w.em = emn;
-        count++;
-        if (__ballot(w.occ == kDQ) != 0) {
-            if (w.occ > 0) {
-                const int mj = w.occ == 4 ? w.q3 : w.occ == 3 ? w.q2 : w.occ == 2 ? w.q1 : w.q0;
-                const int len = lcp16(E, mj >> 2, b.s, S, b.maxcmp);
-                w.occ--;
-                if (len > b.best) {
-                    b.best = len;
-                    b.bpos4 = mj;
-                    if (len >= b.nice) {
-                        w.limit4 = 0x7fffffff;   // walk over: nothing more is queued
-                        w.occ = 0;
-                    }
-                    w.be4 = (len - 1) * 4;
-                    w.scanE = E[b.s + len - 1] >> 16;
-                    ebn = *reinterpret_cast<const uint32_t *>(Eb + a + w.be4);
-                }
-            }
-        }
-        w.eb = ebn;
-        if (count >= end || __ballot(m4n > w.limit4) == 0) break;
-    }
-}
-
 __device__ inline uint32_t match_rec(int best, int s4, int bpos4) {
     return best >= kMinMatch ? (((uint32_t)best << 16) | (uint32_t)((s4 - bpos4) >> 2)) : 0u;
 }
 
-// One position's longest_match with deferred compares.  Every lane of the
-// wave that took a position calls this together (the flushes are wave-wide
-// decisions taken with ballots).
-__device__ unsigned long long g_dstat[4];   // deferred-walk statistics (variant 41)
 
-template <bool kStats = false, int kHead = kD0, bool kPartial = false, bool kNoFlush = false, bool kRecheck = false,
-          bool kBatchFlush = false, bool kIdx = false>
-__device__ __attribute__((always_inline)) inline void dw_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
-                                                              const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
-                                                              int want_q, int64_t max_dist) {
-    const int s = (int)(p - B);
-    const uint32_t e0 = E[s];
-    // the distance to the chain's head (kIdx: from its window index; index 0, none)
-    const uint32_t d0 = kIdx ? ((e0 & 0xffffu) ? (uint32_t)s - (e0 & 0xffffu) : 0xffffu) : e0 & 0xffffu;
-    if (d0 > (uint32_t)max_dist) {                 // deflate.c:1955: strstart - hash_head <= MAX_DIST
-        rf[p] = 0;
-        if (want_q) rq[p] = 0;
-        return;
-    }
-    const int64_t labs = p > max_dist ? p - max_dist : 0;
-    const int limit4 = (int)(labs - B) * 4;
-    const int64_t rem = n - p;
-    const int nice = rem < cfg.nice ? (int)rem : cfg.nice;
-    const int maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
-    const uint32_t chain = (uint32_t)cfg.chain;
-    const uint32_t qc = want_q ? chain >> 2 : chain;
-    const int s4 = s * 4;
-    const Scan16 S{get4(E, s), get4(E, s + 4), get4(E, s + 8), get4(E, s + 12)};
-    int best = kMinMatch - 1, bpos4 = 0;
-    int m4 = (s - (int)d0) * 4;
-    uint32_t count = 0;
-    bool walking = true;
-    bool need_q = want_q != 0;
-    // 1. the chain's first kD0 candidates, compared by the whole wave at once
-#pragma unroll
-    for (int k = 0; k < kHead; k++) {
-        if (walking) {
-            const int m = m4 >> 2;
-            const uint32_t em = E[m];
-            const int len = lcp16(E, m, s, S, maxcmp);
-            if (len > best) { best = len; bpos4 = m4; }
-            count++;
-            const int m4n = kIdx ? (int)((em & 0xffffu) << 2) : m4 - (int)((em & 0xffffu) << 2);
-            if (best >= nice || m4n <= limit4 || count >= chain) walking = false;
-            if (need_q && count == qc && walking) {      // a tuned chain/4 inside the head
-                rq[p] = match_rec(best, s4, bpos4);
-                need_q = false;
-            }
-            m4 = m4n;
-        }
-    }
-    if (!walking) {                                  // the walk ended within its head
-        const uint32_t r = match_rec(best, s4, bpos4);
-        if (need_q) rq[p] = r;
-        rf[p] = r;
-        return;
-    }
-    // 2./3. walk with the stale best, queue the passes, flush wave-wide
-    const char *Eb = reinterpret_cast<const char *>(E);
-    DWS w;
-    w.m4 = m4;
-    w.limit4 = limit4;
-    w.be4 = (best - 1) * 4;
-    w.occ = 0;
-    w.q0 = w.q1 = w.q2 = w.q3 = 0;
-    w.scan01 = e0 >> 16;
-    w.scanE = E[s + best - 1] >> 16;
-    w.em = *reinterpret_cast<const uint32_t *>(Eb + m4);
-    w.eb = *reinterpret_cast<const uint32_t *>(Eb + m4 + w.be4);
-    static_assert(kDQ == 4, "queue registers q0..q3");
-    count = ufl(count);                 // every lane still walking took kD0 steps
-    for (;;) {
-        // walk to the next uniform stop: the chain/4 snapshot, the budget, a full queue
-        const uint32_t end = count < qc ? qc : chain;
-        const uint32_t c0 = count;
-        int best0 = best;
-        if (kPartial) {
-            DWB b{best, bpos4, s, maxcmp, nice};
-            dw_steps_in(w, b, E, S, count, end);
-            best = b.best;
-            bpos4 = b.bpos4;
-            walking = w.m4 > w.limit4 && count < chain;
-            if (best >= nice) walking = false;
-        } else {
-            dw_steps<kIdx>(w, Eb, count, end);
-            walking = w.m4 > limit4 && count < chain;
-        }
-        const bool partial = false;
-        if (kStats) {
-            int mo = 0;
-#pragma unroll
-            for (int j = 1; j <= kDQ; j++) mo = __ballot(w.occ >= j) != 0 ? j : mo;
-            if (__builtin_ctzll(__ballot(1)) == (threadIdx.x & 63)) {
-                atomicAdd(&g_dstat[0], (unsigned long long)(count - c0));  // wave iterations
-                atomicAdd(&g_dstat[1], 1ull);                              // flushes
-                atomicAdd(&g_dstat[2], (unsigned long long)(partial ? (mo > 0) : mo));   // rounds
-            }
-        }
-        if (partial) {
-            if (w.occ > 0) {
-                const int mj = w.occ == 4 ? w.q3 : w.occ == 3 ? w.q2 : w.occ == 2 ? w.q1 : w.q0;
-                const int len = lcp16(E, mj >> 2, s, S, maxcmp);
-                w.occ--;
-                if (len > best) {
-                    best = len;
-                    bpos4 = mj;
-                    if (len >= nice) { walking = false; w.occ = 0; }
-                }
-            }
-        } else if (kBatchFlush) {
-            // every entry, oldest first (entry j < occ is the (occ - j)-th
-            // oldest); the first 16 bytes of all kDQ entries are read in one
-            // LDS round trip, entries matching all 16 continue one by one
-            if (__ballot(w.occ > 0) != 0) {
-                const int qm[kDQ] = {w.q0 >> 2, w.q1 >> 2, w.q2 >> 2, w.q3 >> 2};
-                int k16[kDQ];
-#pragma unroll
-                for (int j = 0; j < kDQ; j++) {
-                    const int m = j < w.occ ? qm[j] : s;   // an empty slot compares the scan with itself
-                    k16[j] = diff16(get4p(E, m) ^ S.s0, get4p(E, m + 4) ^ S.s1, get4p(E, m + 8) ^ S.s2,
-                                    get4p(E, m + 12) ^ S.s3);
-                }
-#pragma unroll
-                for (int j = kDQ - 1; j >= 0; j--) {
-                    int len = k16[j];
-                    if (__ballot(j < w.occ && len >= 16 && maxcmp > 16) != 0) {
-                        if (j < w.occ && len >= 16) {
-                            const int m = qm[j];
-                            while (len < maxcmp) {
-                                const int r = diff16(get4p(E, m + len) ^ get4p(E, s + len),
-                                                     get4p(E, m + len + 4) ^ get4p(E, s + len + 4),
-                                                     get4p(E, m + len + 8) ^ get4p(E, s + len + 8),
-                                                     get4p(E, m + len + 12) ^ get4p(E, s + len + 12));
-                                len += r;
-                                if (r < 16) break;
-                            }
-                        }
-                    }
-                    len = len < maxcmp ? len : maxcmp;
-                    if (j < w.occ && len > best) {
-                        best = len;
-                        bpos4 = qm[j] * 4;
-                        if (len >= nice) { walking = false; w.occ = 0; }   // drop the later entries
-                    }
-                }
-            }
-            w.occ = 0;
-        } else {
-            // every entry, oldest first: entry j (< occ) is the (occ - j)-th oldest
-            uint32_t scanE = w.scanE;                   // scan bytes best-1, best
-#pragma unroll
-            for (int j = kDQ - 1; j >= 0; j--) {
-                const int mj = j == 3 ? w.q3 : j == 2 ? w.q2 : j == 1 ? w.q1 : w.q0;
-                // the entry was queued against an older best: test it again
-                // against the current one (one read) before comparing
-                const bool cand = j < w.occ && (!kRecheck || (E[(mj >> 2) + best - 1] >> 16) == scanE);
-                if (!kNoFlush && __ballot(cand) != 0) {
-                    if (cand) {
-                        const int len = lcp16(E, mj >> 2, s, S, maxcmp);
-                        if (len > best) {
-                            best = len;
-                            bpos4 = mj;
-                            if (len >= nice) { walking = false; w.occ = 0; }   // drop the later entries
-                            if (kRecheck) scanE = E[s + len - 1] >> 16;
-                        }
-                    }
-                }
-            }
-            w.occ = 0;
-        }
-        const bool fin = !walking && w.occ == 0;
-        if (need_q && (count >= qc || fin)) {          // deflate.c:1390-1392 (chain >>= 2)
-            rq[p] = match_rec(best, s4, bpos4);
-            need_q = false;
-        }
-        if (fin) break;
-        if (best != best0 && walking) {                // the quick reject now tests the new best
-            w.be4 = (best - 1) * 4;
-            w.scanE = E[s + best - 1] >> 16;
-            w.eb = *reinterpret_cast<const uint32_t *>(Eb + (w.m4 > 0 ? w.m4 : 0) + w.be4);
-        }
-    }
-    rf[p] = match_rec(best, s4, bpos4);
-}
-
-
-// dw_walk (kIdx) with a kQ-deep queue: flushes come when some lane holds kQ
-// passes, so a deeper queue means fewer, fuller flush rounds
-template <int kQ>
+// The walk state between flushes: candidate m (byte address m4 = 4 m) has its
+// two words em (link index, bytes m, m+1) and eb (bytes m+best-1, m+best)
+// loaded; the queue holds byte addresses, newest in q[0].
 struct DWQ {
     int m4, limit4, be4, occ;
-    int q[kQ];
+    int q[kDQ];
     uint32_t em, eb, scan01, scanE;
 };
-// kU > 1: kU steps per exit test (the loop's ballots and budget compare are
-// scalar work every wave of the CU shares one scalar unit for).  A lane whose
-// walk has ended keeps stepping harmlessly (links only go back, so it stays
-// past its limit and queues nothing); the queue test fires kU - 1 entries
-// early so that kU steps cannot overflow it, and single steps are taken when
-// fewer than kU are left of the budget, so the stops are those of kU 1.
-// kV: the quick-reject test as one integer (the two byte-pair differences and
-// the limit test's sign bit or-ed together, one compare), instead of three
-// compares whose lane masks are and-ed on the scalar unit.
-template <int kQ, int kU = 1, bool kV = false>
-__device__ __attribute__((always_inline)) inline void dwq_steps(DWQ<kQ> &w, const char *Eb, uint32_t &count,
+// Steps every lane of the wave until the uniform budget count `end` is
+// reached, some lane's queue is nearly full or no lane has a candidate left.
+// kDU steps per exit test: the loop's ballots and budget compare are scalar
+// work every wave of the CU shares one scalar unit for.  A lane whose walk has
+// ended keeps stepping harmlessly (links only go back, so it stays past its
+// limit and queues nothing); the queue test fires kDU - 1 entries early so
+// that kDU steps cannot overflow it, and single steps are taken when fewer
+// than kDU are left of the budget, so the stops are those of one step per
+// test.  `count` is wave-uniform (all lanes start their walks together).
+__device__ __attribute__((always_inline)) inline void dwq_steps(DWQ &w, const char *Eb, uint32_t &count,
                                                                 uint32_t end) {
-    if (kU > 1) {
-        auto step = [&]() {
-            const int m4n = (int)((w.em << 2) & 0x3fffcu);
-            const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + m4n);
-            const uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + m4n + w.be4);
-            bool pass;
-            if (kV) {
-                // m4 > limit4 <=> m4 - limit4 - 1 >= 0 (both within +-2^18)
-                const uint32_t x = ((w.em >> 16) ^ w.scan01) | ((w.eb >> 16) ^ w.scanE) |
-                                   ((uint32_t)(w.m4 - w.limit4 - 1) >> 31);
-                pass = x == 0;
-            } else {
-                pass = (w.m4 > w.limit4) & ((w.em >> 16) == w.scan01) & ((w.eb >> 16) == w.scanE);
-            }
-#pragma unroll
-            for (int j = kQ - 1; j > 0; j--) w.q[j] = pass ? w.q[j - 1] : w.q[j];
-            w.q[0] = pass ? w.m4 : w.q[0];
-            w.occ += pass ? 1 : 0;
-            w.m4 = m4n;
-            w.em = emn;
-            w.eb = ebn;
-        };
-        for (;;) {
-            if (end - count >= (uint32_t)kU) {
-#pragma unroll
-                for (int u = 0; u < kU; u++) step();
-                count += kU;
-            } else {
-                step();
-                count += 1;
-            }
-            const uint64_t walkers = __ballot(w.m4 > w.limit4), full = __ballot(w.occ >= kQ - (kU - 1));
-            if (count >= end || walkers == 0 || full != 0) break;
-        }
-        return;
-    }
-    for (;;) {
-        const bool valid = w.m4 > w.limit4;
+    auto step = [&]() {
         const int m4n = (int)((w.em << 2) & 0x3fffcu);
         const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + m4n);
         const uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + m4n + w.be4);
-        const bool pass = valid & ((w.em >> 16) == w.scan01) & ((w.eb >> 16) == w.scanE);
+        const bool pass = (w.m4 > w.limit4) & ((w.em >> 16) == w.scan01) & ((w.eb >> 16) == w.scanE);
 #pragma unroll
-        for (int j = kQ - 1; j > 0; j--) w.q[j] = pass ? w.q[j - 1] : w.q[j];
+        for (int j = kDQ - 1; j > 0; j--) w.q[j] = pass ? w.q[j - 1] : w.q[j];
         w.q[0] = pass ? w.m4 : w.q[0];
         w.occ += pass ? 1 : 0;
         w.m4 = m4n;
         w.em = emn;
         w.eb = ebn;
-        count++;
-        const uint64_t walkers = __ballot(m4n > w.limit4), full = __ballot(w.occ == kQ);
+    };
+    for (;;) {
+        if (end - count >= (uint32_t)kDU) {
+#pragma unroll
+            for (int u = 0; u < kDU; u++) step();
+            count += kDU;
+        } else {
+            step();
+            count += 1;
+        }
+        const uint64_t walkers = __ballot(w.m4 > w.limit4), full = __ballot(w.occ >= kDQ - (kDU - 1));
         if (count >= end || walkers == 0 || full != 0) break;
     }
 }
 
-template <int kQ, int kU = 1, bool kV = false>
+// One position's longest_match with deferred compares.  Every lane of the
+// wave that took a position calls this together (the flushes are wave-wide
+// decisions taken with ballots).
 __device__ __attribute__((always_inline)) inline void dwq_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
                                                                const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
                                                                int want_q, int64_t max_dist) {
@@ -1049,13 +624,13 @@ __device__ __attribute__((always_inline)) inline void dwq_walk(const uint32_t *E
         return;
     }
     const char *Eb = reinterpret_cast<const char *>(E);
-    DWQ<kQ> w;
+    DWQ w;
     w.m4 = m4;
     w.limit4 = limit4;
     w.be4 = (best - 1) * 4;
     w.occ = 0;
 #pragma unroll
-    for (int j = 0; j < kQ; j++) w.q[j] = 0;
+    for (int j = 0; j < kDQ; j++) w.q[j] = 0;
     w.scan01 = e0 >> 16;
     w.scanE = E[s + best - 1] >> 16;
     w.em = *reinterpret_cast<const uint32_t *>(Eb + m4);
@@ -1064,11 +639,11 @@ __device__ __attribute__((always_inline)) inline void dwq_walk(const uint32_t *E
     for (;;) {
         const uint32_t end = count < qc ? qc : chain;
         const int best0 = best;
-        dwq_steps<kQ, kU, kV>(w, Eb, count, end);
+        dwq_steps(w, Eb, count, end);
         walking = w.m4 > limit4 && count < chain;
         // every entry, oldest first: entry j (< occ) is the (occ - j)-th oldest
 #pragma unroll
-        for (int j = kQ - 1; j >= 0; j--) {
+        for (int j = kDQ - 1; j >= 0; j--) {
             const bool cand = j < w.occ;
             if (__ballot(cand) != 0) {
                 if (cand) {
@@ -1096,258 +671,6 @@ __device__ __attribute__((always_inline)) inline void dwq_walk(const uint32_t *E
     }
     rf[p] = match_rec(best, s4, bpos4);
 }
-
-// dwq_walk for two positions per lane: the two chains step in the same loop
-// iteration, so each lane keeps two independent LDS round trips in flight
-// (the walks are latency-bound at the 16 waves the LDS window allows).  A
-// walk that ends first idles (its limit rises out of reach) until the other
-// one is done.  `live` false: no position (the tile's odd last one).
-template <int kQ>
-struct DWP {
-    int64_t p;
-    int s, s4, limit4, nice, maxcmp, best, bpos4, best0;
-    bool walking, need_q, live;
-    Scan16 S;
-    DWQ<kQ> w;
-};
-
-template <int kQ>
-__device__ __attribute__((always_inline)) inline void dwp_init(DWP<kQ> &x, const uint32_t *E, int64_t p, bool live,
-                                                               int64_t B, int64_t n, const LevelCfg &cfg, uint32_t *rf,
-                                                               uint32_t *rq, int want_q, int64_t max_dist) {
-    x.p = p;
-    x.s = live ? (int)(p - B) : 0;
-    x.s4 = x.s * 4;
-    const uint32_t e0 = E[x.s];
-    const uint32_t d0 = (e0 & 0xffffu) ? (uint32_t)x.s - (e0 & 0xffffu) : 0xffffu;
-    x.live = live;
-    if (live && d0 > (uint32_t)max_dist) {          // deflate.c:1955: strstart - hash_head <= MAX_DIST
-        rf[p] = 0;
-        if (want_q) rq[p] = 0;
-        x.live = false;
-    }
-    const int64_t labs = p > max_dist ? p - max_dist : 0;
-    x.limit4 = (int)(labs - B) * 4;
-    const int64_t rem = n - p;
-    x.nice = rem < cfg.nice ? (int)rem : cfg.nice;
-    x.maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
-    x.S = Scan16{get4(E, x.s), get4(E, x.s + 4), get4(E, x.s + 8), get4(E, x.s + 12)};
-    x.best = kMinMatch - 1;
-    x.bpos4 = 0;
-    x.walking = x.live;
-    x.need_q = x.live && want_q != 0;
-    x.w.m4 = (int)(e0 & 0xffffu) * 4;
-    x.w.scan01 = e0 >> 16;
-}
-
-// one head compare of a pair walk (count is the shared step count before it)
-template <int kQ>
-__device__ __attribute__((always_inline)) inline void dwp_head(DWP<kQ> &x, const uint32_t *E, uint32_t count,
-                                                               uint32_t chain, uint32_t qc, uint32_t *rq) {
-    if (x.walking) {
-        const int m = x.w.m4 >> 2;
-        const uint32_t em = E[m];
-        const int len = lcp16(E, m, x.s, x.S, x.maxcmp);
-        if (len > x.best) { x.best = len; x.bpos4 = x.w.m4; }
-        const int m4n = (int)((em & 0xffffu) << 2);
-        if (x.best >= x.nice || m4n <= x.limit4 || count + 1 >= chain) x.walking = false;
-        if (x.need_q && count + 1 == qc && x.walking) {
-            rq[x.p] = match_rec(x.best, x.s4, x.bpos4);
-            x.need_q = false;
-        }
-        x.w.m4 = m4n;
-    }
-}
-
-// a pair walk that is done writes its results and stops queueing
-template <int kQ>
-__device__ __attribute__((always_inline)) inline void dwp_finish(DWP<kQ> &x, uint32_t *rf, uint32_t *rq) {
-    const uint32_t r = match_rec(x.best, x.s4, x.bpos4);
-    if (x.need_q) rq[x.p] = r;
-    rf[x.p] = r;
-    x.need_q = false;
-    x.live = false;
-    x.walking = false;
-    x.w.limit4 = 0x7fffffff;
-    x.w.occ = 0;
-}
-
-template <int kQ>
-__device__ __attribute__((always_inline)) inline void dwp_arm(DWP<kQ> &x, const uint32_t *E) {
-    const char *Eb = reinterpret_cast<const char *>(E);
-    if (!x.walking) x.w.m4 = 0;                     // idle: reads word 0, queues nothing
-    x.w.limit4 = x.walking ? x.limit4 : 0x7fffffff;
-    x.w.be4 = (x.best - 1) * 4;
-    x.w.occ = 0;
-#pragma unroll
-    for (int j = 0; j < kQ; j++) x.w.q[j] = 0;
-    x.w.scanE = E[x.s + x.best - 1] >> 16;
-    x.w.em = *reinterpret_cast<const uint32_t *>(Eb + x.w.m4);
-    x.w.eb = *reinterpret_cast<const uint32_t *>(Eb + x.w.m4 + x.w.be4);
-}
-
-template <int kQ>
-__device__ __attribute__((always_inline)) inline bool dwq_step1(DWQ<kQ> &w, const char *Eb) {
-    const bool valid = w.m4 > w.limit4;
-    const int m4n = (int)((w.em << 2) & 0x3fffcu);
-    const uint32_t emn = *reinterpret_cast<const uint32_t *>(Eb + m4n);
-    const uint32_t ebn = *reinterpret_cast<const uint32_t *>(Eb + m4n + w.be4);
-    const bool pass = valid & ((w.em >> 16) == w.scan01) & ((w.eb >> 16) == w.scanE);
-#pragma unroll
-    for (int j = kQ - 1; j > 0; j--) w.q[j] = pass ? w.q[j - 1] : w.q[j];
-    w.q[0] = pass ? w.m4 : w.q[0];
-    w.occ += pass ? 1 : 0;
-    w.m4 = m4n;
-    w.em = emn;
-    w.eb = ebn;
-    return m4n > w.limit4;
-}
-
-template <int kQ>
-__device__ __attribute__((always_inline)) inline void dwp_flush_one(DWP<kQ> &x, const uint32_t *E, int j) {
-    if (j < x.w.occ) {
-        const int len = lcp16(E, x.w.q[j] >> 2, x.s, x.S, x.maxcmp);
-        if (len > x.best) {
-            x.best = len;
-            x.bpos4 = x.w.q[j];
-            if (len >= x.nice) { x.walking = false; x.w.occ = 0; }   // drop the later entries
-        }
-    }
-}
-
-template <int kQ>
-__device__ __attribute__((always_inline)) inline void dwp_after(DWP<kQ> &x, const uint32_t *E, uint32_t count,
-                                                                uint32_t qc, uint32_t *rf, uint32_t *rq) {
-    if (!x.live) return;
-    const bool fin = !x.walking;
-    if (x.need_q && (count >= qc || fin)) {         // deflate.c:1390-1392 (chain >>= 2)
-        rq[x.p] = match_rec(x.best, x.s4, x.bpos4);
-        x.need_q = false;
-    }
-    if (fin) {
-        dwp_finish(x, rf, rq);
-    } else if (x.best != x.best0) {                  // the quick reject now tests the new best
-        const char *Eb = reinterpret_cast<const char *>(E);
-        x.w.be4 = (x.best - 1) * 4;
-        x.w.scanE = E[x.s + x.best - 1] >> 16;
-        x.w.eb = *reinterpret_cast<const uint32_t *>(Eb + x.w.m4 + x.w.be4);
-    }
-}
-
-template <int kQ>
-__device__ __attribute__((always_inline)) inline void dwp_walk(const uint32_t *E, int64_t pa, int64_t na, int64_t pb,
-                                                               int64_t nb, bool live_b, int64_t B, const LevelCfg &cfg,
-                                                               uint32_t *rf, uint32_t *rq, int want_q, int64_t max_dist) {
-    const uint32_t chain = (uint32_t)cfg.chain;
-    const uint32_t qc = want_q ? chain >> 2 : chain;
-    DWP<kQ> a, b;
-    dwp_init(a, E, pa, true, B, na, cfg, rf, rq, want_q, max_dist);
-    dwp_init(b, E, pb, live_b, B, nb, cfg, rf, rq, want_q, max_dist);
-    uint32_t count = 0;
-#pragma unroll
-    for (int k = 0; k < kD0; k++) {                 // the chains' heads, compared by the whole wave
-        dwp_head(a, E, count, chain, qc, rq);
-        dwp_head(b, E, count, chain, qc, rq);
-        count++;
-    }
-    if (a.live && !a.walking) dwp_finish(a, rf, rq);
-    if (b.live && !b.walking) dwp_finish(b, rf, rq);
-    if (!a.live && !b.live) return;
-    dwp_arm(a, E);
-    dwp_arm(b, E);
-    const char *Eb = reinterpret_cast<const char *>(E);
-    for (;;) {
-        const uint32_t end = count < qc ? qc : chain;
-        a.best0 = a.best;
-        b.best0 = b.best;
-        for (;;) {
-            const bool wa = dwq_step1(a.w, Eb);
-            const bool wb = dwq_step1(b.w, Eb);
-            count++;
-            const uint64_t walkers = __ballot(wa | wb), full = __ballot((a.w.occ == kQ) | (b.w.occ == kQ));
-            if (count >= end || walkers == 0 || full != 0) break;
-        }
-        a.walking = a.walking && a.w.m4 > a.w.limit4 && count < chain;
-        b.walking = b.walking && b.w.m4 > b.w.limit4 && count < chain;
-        // every entry, oldest first: entry j (< occ) is the (occ - j)-th oldest
-#pragma unroll
-        for (int j = kQ - 1; j >= 0; j--) {
-            if (__ballot((j < a.w.occ) | (j < b.w.occ)) != 0) {
-                dwp_flush_one(a, E, j);
-                dwp_flush_one(b, E, j);
-            }
-        }
-        a.w.occ = 0;
-        b.w.occ = 0;
-        dwp_after(a, E, count, qc, rf, rq);
-        dwp_after(b, E, count, qc, rf, rq);
-        if (!a.live && !b.live) break;
-    }
-}
-
-__device__ unsigned long long g_mstat[4];   // kMatchStats statistics
-
-// k_match variants (ZGPU_MATCH_VARIANT, for A/B runs):
-//   55 (default)  49 with three steps per exit test (dwq_steps kU 3: the
-//                 loop's two ballots and budget compare are scalar work that
-//                 the CU's 16 walking waves share one scalar unit for):
-//                 402 -> 375 ms per 4 GiB L6 sub-batch (interleaved A/B, 2x)
-//   53, 57, 58    two steps (397 ms), four with an 8-deep queue (377), four
-//                 with a 6-deep queue flushed at 3 (386)
-//   56            three steps, 7-deep queue (380)
-//   59            55 with the quick reject as one integer or-ed from the byte
-//                 differences and the limit's sign bit (fewer scalar mask ands,
-//                 more vector instructions): 382 vs 375 ms
-//   49            48 with a 6-deep queue (dwq_walk): 411 -> 401 ms
-//   48            40 with links stored as the predecessor's LDS word index (a
-//                 chain step needs no subtraction; the slide lowers every index
-//                 with one saturating packed subtract): 418 -> 411 ms
-//   50, 51        48 with an 8-deep (407 ms) or 3-deep (407 ms) queue
-//   52            49 with two positions per lane stepping in one loop (two
-//                 LDS round trips in flight per lane): 463 vs 403 ms -- the
-//                 doubled step and flush work costs more than the overlap wins
-//   40            19 with deferred compares (dw_walk): 495 -> 412 ms per 4 GiB
-//                 C4 sub-batch at L6 (the C4 shard 7.7 -> 9.1 GB/s)
-//   41            40 plus statistics (wave iterations, flushes, flush rounds)
-//   42            40 with three wave-wide head compares (no faster)
-//   43            40 with a full queue's flush inside the step loop, one round
-//                 of each lane's oldest entry (flush rounds -32 %): 432 vs 417 ms
-//   45            timing probe (wrong results): 40 without flush compares:
-//                 270 of 417 ms (the old walk without compares, 37: 226)
-//   46            40 re-testing each queued entry against the current best
-//                 before its compare (one more read): 436 vs 417 ms
-//   47            40 reading the first 16 bytes of all four entries in one
-//                 round trip: 448 vs 419 ms
-//   19            positions of a tile walked in k_count's key order, longest
-//                 walks first: the 64 walks a wave runs side by side have
-//                 similar lengths (SIMT utilisation 63 % -> 90 % at L6,
-//                 20 % -> 93 % at L9, measured with kMatchStats)
-//   14            positions in index order (no keys)
-//   21            19 plus statistics (lane steps, compares, walks, wave
-//                 iterations) printed after each launch
-//   38            timing probe (wrong results): 37 plus every compare done
-//                 and its length discarded (best, nice and the quick-reject
-//                 offset stay as in 37, so nearly every same-hash candidate
-//                 passes the quick reject): 1624 ms -- with most lanes
-//                 comparing together a compare costs ~1/3 of what a lone
-//                 lane's compare costs its wave
-//   37            timing probe (wrong results): walks without compares (every
-//                 quick-reject pass ignored, so no walk stops at nice): 127 ms
-//                 of 355 per 4 GiB at L6 -- the compares, 3.4 % of the steps,
-//                 hold their waves for the rest (in most steps some lane of 64
-//                 compares)
-//   33, 35        timing probes (wrong results): 33 no walks (tile staging,
-//                 sort and stores: 33 ms of 351 per 4 GiB at L6); 35 half the
-//                 waves walk (1.6x slower at L6, 1.8x at L9: the walks are
-//                 latency-bound at the 16 waves the LDS window allows)
-constexpr int kMatchDefer = 40, kMatchDeferStats = 41, kMatchDefer3 = 42, kMatchDeferP = 43, kMatchDeferPStats = 44,
-              kMatchProbeNoFlush = 45, kMatchDeferR = 46, kMatchDeferB = 47, kMatchDeferIdx = 48,
-              kMatchQ6 = 49, kMatchQ8 = 50, kMatchQ3 = 51, kMatchPair = 52, kMatchQ6U2 = 53, kMatchQ7U2 = 54,
-              kMatchQ6U3 = 55, kMatchQ7U3 = 56, kMatchQ8U4 = 57, kMatchQ6U4 = 58, kMatchQ6U3V = 59;
-constexpr int kMatchWalk = 19;
-constexpr int kMatchDefault = kMatchQ6U3;
-constexpr int kMatchStats = 21, kMatchProbeNoWalk = 33, kMatchProbeHalf = 35,
-              kMatchProbeNoCmp = 37, kMatchProbeCmpOnly = 38;
 
 
 // The deflate(flush) calls of a flush job (DeflateJob::fl_pos/fl_type): the
@@ -1394,13 +717,12 @@ __device__ inline int64_t flush_limit(const DeflateJob &job, int64_t p, int64_t 
     return lo < job.nmlim ? (int64_t)job.mlim[lo] : n;
 }
 
-template <int kVariant, bool kEv = false, bool kSegs = false>
+template <bool kEv = false, bool kSegs = false>
 __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int want_q) {
-    constexpr bool kSorted = kVariant != 14;
     constexpr int kSortBuckets = 64;
     __shared__ __attribute__((aligned(16))) uint32_t E[kME];
     __shared__ int next_i;
-    __shared__ uint16_t s_perm[kSorted ? kMT : 1];
+    __shared__ uint16_t s_perm[kMT];
     __shared__ int s_hist[kSortBuckets], s_base[kSortBuckets];
     const int tid = threadIdx.x;
     // one workgroup per buffer, or -- a sub-batch of few large buffers -- per
@@ -1417,147 +739,62 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
     const uint16_t *L = job.link + job.ws_off[bi];
     uint32_t *rf = job.rfull + job.ws_off[bi];
     uint32_t *rq = job.rquart + job.ws_off[bi];
-    const uint8_t *K = kSorted ? job.key + job.ws_off[bi] : nullptr;
+    const uint8_t *K = job.key + job.ws_off[bi];
     const LevelCfg cfg = job.cfg;
     const int64_t max_dist = job_win(job).max_dist;
-    uint64_t st_lane_steps = 0, st_cmps = 0, st_walks = 0, st_wave_iters = 0;
 
     TilePre P;
     tile_prefetch(P, t0, n, in, L, K, tid);
     for (int64_t ts = t0; ts < s1; ts += kMT) {
         const int64_t B = ts - kMW;
         const int tile_n = kSegs && ts < s0 ? 0 : (int)((n - ts) < kMT ? (n - ts) : kMT);   // 0: staging only
-        tile_store<kVariant == kMatchDeferIdx || kVariant == kMatchQ6 || kVariant == kMatchQ8 || kVariant == kMatchQ3 ||
-                   kVariant == kMatchPair || kVariant == kMatchQ6U2 || kVariant == kMatchQ7U2 || kVariant == kMatchQ6U3 ||
-                   kVariant == kMatchQ7U3 || kVariant == kMatchQ8U4 || kVariant == kMatchQ6U4 ||
-                   kVariant == kMatchQ6U3V>(
-            E, P, ts, tid);
+        tile_store<true>(E, P, ts, tid);
         if (tid == 0) next_i = 0;
-        if (kSorted && tid < kSortBuckets) s_hist[tid] = 0;
+        if (tid < kSortBuckets) s_hist[tid] = 0;
         __syncthreads();
-        if (kSorted) {
-            // counting sort of the tile's positions by key (64 buckets), longest
-            // first.  Thread t takes positions t + 1024u, so within a bucket the
-            // ranks come out nearly in position order and a wave's lanes get
-            // nearby positions (nearby candidates, fewer LDS bank conflicts).
-            int bk[4], rk[4];
+        // counting sort of the tile's positions by key (64 buckets), longest
+        // first: the 64 walks a wave runs side by side then have similar
+        // lengths (SIMT utilisation 63 % -> 90 % at L6, 20 % -> 93 % at L9).
+        // Thread t takes positions t + 1024u, so within a bucket the ranks come
+        // out nearly in position order and a wave's lanes get nearby positions
+        // (nearby candidates, fewer LDS bank conflicts).
+        int bk[4], rk[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int i = tid + u * kMatchThreads;
-                bk[u] = kSortBuckets - 1 - (i < tile_n ? (int)(P.key[u] >> 2) : 0);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-                rk[u] = tid + u * kMatchThreads < tile_n ? atomicAdd(&s_hist[bk[u]], 1) : 0;
-            __syncthreads();
-            if (tid < 64) {                              // exclusive scan of the bucket sizes
-                const int v = s_hist[tid];
-                int incl = v;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const int t = __shfl_up(incl, o, 64);
-                    if (tid >= o) incl += t;
-                }
-                s_base[tid] = incl - v;
-            }
-            __syncthreads();
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-                if (tid + u * kMatchThreads < tile_n)
-                    s_perm[s_base[bk[u]] + rk[u]] = (uint16_t)(tid + u * kMatchThreads);
-            __syncthreads();
+        for (int u = 0; u < 4; u++) {
+            const int i = tid + u * kMatchThreads;
+            bk[u] = kSortBuckets - 1 - (i < tile_n ? (int)(P.key[u] >> 2) : 0);
         }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            rk[u] = tid + u * kMatchThreads < tile_n ? atomicAdd(&s_hist[bk[u]], 1) : 0;
+        __syncthreads();
+        if (tid < 64) {                              // exclusive scan of the bucket sizes
+            const int v = s_hist[tid];
+            int incl = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(incl, o, 64);
+                if (tid >= o) incl += t;
+            }
+            s_base[tid] = incl - v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (tid + u * kMatchThreads < tile_n)
+                s_perm[s_base[bk[u]] + rk[u]] = (uint16_t)(tid + u * kMatchThreads);
+        __syncthreads();
         if (ts + kMT < s1) tile_prefetch(P, ts + kMT, n, in, L, K, tid);   // lands during the walks
         for (;;) {
-            if (kVariant == kMatchProbeHalf && tid >= kMatchThreads / 2) break;   // probe: half the waves walk
-            if (kVariant == kMatchPair) {              // two adjacent positions of the key order per lane
-                const int i = atomicAdd(&next_i, 2);
-                if (i >= tile_n) break;
-                const bool live_b = i + 1 < tile_n;
-                const int64_t pa = ts + (int)s_perm[i];
-                const int64_t pb = live_b ? ts + (int)s_perm[i + 1] : pa;
-                const int64_t na = kEv ? flush_limit(job, pa, n) : n;
-                const int64_t nb = kEv ? flush_limit(job, pb, n) : n;
-                dwp_walk<6>(E, pa, na, pb, nb, live_b, B, cfg, rf, rq, want_q, max_dist);
-                continue;
-            }
             const int i = atomicAdd(&next_i, 1);
             if (i >= tile_n) break;
-            const int64_t p = ts + (kSorted ? (int)s_perm[i] : i);
+            const int64_t p = ts + (int)s_perm[i];
             // a flush job's search at p sees the input up to the next flush
             // position only (nice and the compare length are clamped to it)
             const int64_t nl = kEv ? flush_limit(job, p, n) : n;
-            if (kVariant == kMatchStats) {
-                uint32_t steps = 0, cmps = 0;
-                mw14_walk<2, false>(E, p, B, nl, cfg, rf, rq, want_q, max_dist, &steps, &cmps);
-                uint32_t mx = steps;
-#pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
-                st_lane_steps += steps;
-                st_cmps += cmps;
-                st_walks += steps ? 1u : 0u;
-                if ((tid & 63) == __builtin_ctzll(__ballot(1))) st_wave_iters += mx;
-            } else if (kVariant == kMatchProbeNoCmp) {
-                mw14_walk<2, false, 1>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            } else if (kVariant == kMatchProbeCmpOnly) {
-                mw14_walk<2, false, 2>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-
-
-
-            } else if (kVariant == kMatchDefer) {
-                dw_walk(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            } else if (kVariant == kMatchQ6) {
-                dwq_walk<6>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            } else if (kVariant == kMatchQ8) {
-                dwq_walk<8>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            } else if (kVariant == kMatchQ6U2) {
-                dwq_walk<6, 2>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            } else if (kVariant == kMatchQ7U2) {
-                dwq_walk<7, 2>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            } else if (kVariant == kMatchQ6U3) {
-                dwq_walk<6, 3>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            } else if (kVariant == kMatchQ7U3) {
-                dwq_walk<7, 3>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            } else if (kVariant == kMatchQ8U4) {
-                dwq_walk<8, 4>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            } else if (kVariant == kMatchQ6U4) {
-                dwq_walk<6, 4>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            } else if (kVariant == kMatchQ6U3V) {
-                dwq_walk<6, 3, true>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            } else if (kVariant == kMatchQ3) {
-                dwq_walk<3>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            } else if (kVariant == kMatchDeferIdx) {
-                dw_walk<false, kD0, false, false, false, false, true>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            } else if (kVariant == kMatchDefer3) {
-                dw_walk<false, 3>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            } else if (kVariant == kMatchDeferB) {
-                dw_walk<false, kD0, false, false, false, true>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            } else if (kVariant == kMatchDeferR) {
-                dw_walk<false, kD0, false, false, true>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            } else if (kVariant == kMatchProbeNoFlush) {
-                dw_walk<false, kD0, false, true>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            } else if (kVariant == kMatchDeferP) {
-                dw_walk<false, kD0, true>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            } else if (kVariant == kMatchDeferPStats) {
-                dw_walk<true, kD0, true>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-                if (__builtin_ctzll(__ballot(1)) == (threadIdx.x & 63)) atomicAdd(&g_dstat[3], 1ull);
-            } else if (kVariant == kMatchDeferStats) {
-                dw_walk<true>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-                if (__builtin_ctzll(__ballot(1)) == (threadIdx.x & 63)) atomicAdd(&g_dstat[3], 1ull);   // wave walks
-            } else if (kVariant == kMatchProbeNoWalk) {
-                rf[p] = 0;                                  // probe: staging, sort and stores only
-                if (want_q) rq[p] = 0;
-            } else {
-                mw14_walk<2, false>(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
-            }
+            dwq_walk(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
         }
         __syncthreads();
-    }
-    if (kVariant == kMatchStats) {
-        atomicAdd(&g_mstat[0], (unsigned long long)st_lane_steps);
-        atomicAdd(&g_mstat[1], (unsigned long long)st_cmps);
-        atomicAdd(&g_mstat[2], (unsigned long long)st_walks);
-        atomicAdd(&g_mstat[3], (unsigned long long)st_wave_iters);
     }
 }
 
@@ -2454,7 +1691,7 @@ __global__ __launch_bounds__(64) void k_parse_ev(DeflateJob job) {
 // ------------------------------------------------------------------------
 // kEv: a flush job (events, a resumed start, late hashing); batch jobs run
 // the <false> instance, whose loop carries none of that.
-// kOne (the default; ZGPU_FAST_VARIANT=0 runs the round-2 walk for A/B): one
+// kOne (the only instance built; kOne false is the round-2 walk): one
 // memory round trip per chain candidate.  The link and the candidate's 64
 // bytes are loaded together (the round-2 walk made the link uniform before it
 // requested the bytes: two round trips), the bytes through a clamped index
@@ -3561,134 +2798,35 @@ int launch_tables_upload(const CodeTables *ct, const CrcTables *) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(c_ct), ct, sizeof(CodeTables));
 }
 
-static int match_variant() {
-    static const int v = [] {
-        const char *e = getenv("ZGPU_MATCH_VARIANT");
-        const int x = e ? atoi(e) : kMatchDefault;
-        return (x == 14 || x == kMatchWalk || x == kMatchStats || x == kMatchProbeNoWalk || x == kMatchProbeHalf ||
-                x == kMatchProbeNoCmp || x == kMatchProbeCmpOnly || x == kMatchDefer || x == kMatchDeferStats || x == kMatchDefer3 || x == kMatchDeferP ||
-                x == kMatchDeferPStats || x == kMatchProbeNoFlush || x == kMatchDeferR ||
-                x == kMatchDeferB || x == kMatchDeferIdx || x == kMatchQ6 || x == kMatchQ8 || x == kMatchQ3 ||
-                x == kMatchPair || x == kMatchQ6U2 || x == kMatchQ7U2 ||
-                x == kMatchQ6U3 || x == kMatchQ7U3 || x == kMatchQ8U4 || x == kMatchQ6U4 || x == kMatchQ6U3V)
-                   ? x : kMatchDefault;
-    }();
-    return v;
-}
-
 int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipStream_t st) {
     const dim3 grid(job.count);
     switch (stage) {
     case 0:
         if (job.hbits > 15) hipLaunchKernelGGL((k_links<2048, 65536>), grid, dim3(kLThreads), 0, st, job);
         else hipLaunchKernelGGL((k_links<kLC, 32768>), grid, dim3(kLThreads), 0, st, job);
-        if (match_variant() != 14) hipLaunchKernelGGL(k_count, grid, dim3(kCntThreads), 0, st, job);
+        hipLaunchKernelGGL(k_count, grid, dim3(kCntThreads), 0, st, job);
         break;
     case 1: {
         const int wq = (int)(job.cfg.good < job.cfg.lazy);   // the parse reads rquart (prev_length >= good)
         const dim3 mgrid(job.seg ? job.nseg : job.count);   // per segment or per buffer
-        const int v = match_variant();
-        if (job.nfl && job.seg) {                               // a flush job (zgpu_api.cpp deflate())
-            hipLaunchKernelGGL((k_match<kMatchDefault, true, true>), mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (job.nfl) {
-            hipLaunchKernelGGL((k_match<kMatchDefault, true>), mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (job.seg) {                                   // few large buffers: per segment
-            hipLaunchKernelGGL((k_match<kMatchDefault, false, true>), mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == 14) {
-            hipLaunchKernelGGL(k_match<14>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchWalk) {
-            hipLaunchKernelGGL(k_match<kMatchWalk>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchDeferB) {
-            hipLaunchKernelGGL(k_match<kMatchDeferB>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchDeferIdx) {
-            hipLaunchKernelGGL(k_match<kMatchDeferIdx>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchQ6) {
-            hipLaunchKernelGGL(k_match<kMatchQ6>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchQ8) {
-            hipLaunchKernelGGL(k_match<kMatchQ8>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchQ6U2) {
-            hipLaunchKernelGGL(k_match<kMatchQ6U2>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchQ7U2) {
-            hipLaunchKernelGGL(k_match<kMatchQ7U2>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchQ6U3) {
-            hipLaunchKernelGGL(k_match<kMatchQ6U3>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchQ7U3) {
-            hipLaunchKernelGGL(k_match<kMatchQ7U3>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchQ8U4) {
-            hipLaunchKernelGGL(k_match<kMatchQ8U4>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchQ6U4) {
-            hipLaunchKernelGGL(k_match<kMatchQ6U4>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchQ6U3V) {
-            hipLaunchKernelGGL(k_match<kMatchQ6U3V>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchQ3) {
-            hipLaunchKernelGGL(k_match<kMatchQ3>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchPair) {
-            hipLaunchKernelGGL(k_match<kMatchPair>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchDeferR) {
-            hipLaunchKernelGGL(k_match<kMatchDeferR>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchProbeNoFlush) {
-            hipLaunchKernelGGL(k_match<kMatchProbeNoFlush>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchDeferP) {
-            hipLaunchKernelGGL(k_match<kMatchDeferP>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchDefer3) {
-            hipLaunchKernelGGL(k_match<kMatchDefer3>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchDeferStats || v == kMatchDeferPStats) {
-            unsigned long long z[4] = {0, 0, 0, 0}, r[4];
-            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dstat), z, sizeof z);
-            if (v == kMatchDeferStats)
-                hipLaunchKernelGGL(k_match<kMatchDeferStats>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-            else
-                hipLaunchKernelGGL(k_match<kMatchDeferPStats>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-            (void)hipStreamSynchronize(st);
-            (void)hipMemcpyFromSymbol(r, HIP_SYMBOL(g_dstat), sizeof r);
-            fprintf(stderr, "k_match defer stats: wave_iters %llu flushes %llu flush_rounds %llu wave_walks %llu "
-                    "iters/flush %.2f rounds/flush %.2f flushes/wave-walk %.2f\n", r[0], r[1], r[2], r[3],
-                    r[1] ? (double)r[0] / r[1] : 0.0, r[1] ? (double)r[2] / r[1] : 0.0,
-                    r[3] ? (double)r[1] / r[3] : 0.0);
-        } else if (v == kMatchProbeNoWalk) {
-            hipLaunchKernelGGL(k_match<kMatchProbeNoWalk>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchProbeHalf) {
-            hipLaunchKernelGGL(k_match<kMatchProbeHalf>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchProbeNoCmp) {
-            hipLaunchKernelGGL(k_match<kMatchProbeNoCmp>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        } else if (v == kMatchProbeCmpOnly) {
-            hipLaunchKernelGGL(k_match<kMatchProbeCmpOnly>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-
-
-
-        } else if (v == kMatchStats) {
-            unsigned long long z[4] = {0, 0, 0, 0}, r[4];
-            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_mstat), z, sizeof z);
-            hipLaunchKernelGGL(k_match<kMatchStats>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-            (void)hipStreamSynchronize(st);
-            (void)hipMemcpyFromSymbol(r, HIP_SYMBOL(g_mstat), sizeof r);
-            fprintf(stderr, "k_match stats: lane_steps %llu compares %llu walks %llu wave_iters %llu "
-                    "simt %.3f steps/walk %.2f cmp/step %.4f\n", r[0], r[1], r[2], r[3],
-                    r[3] ? (double)r[0] / (64.0 * r[3]) : 0.0, r[2] ? (double)r[0] / r[2] : 0.0,
-                    r[0] ? (double)r[1] / r[0] : 0.0);
-        } else {
-            hipLaunchKernelGGL(k_match<kMatchDefault>, mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        }
+        if (job.nfl && job.seg)                                 // a flush job (zgpu_api.cpp deflate())
+            hipLaunchKernelGGL((k_match<true, true>), mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        else if (job.nfl)
+            hipLaunchKernelGGL((k_match<true, false>), mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        else if (job.seg)                                       // few large buffers: per segment
+            hipLaunchKernelGGL((k_match<false, true>), mgrid, dim3(kMatchThreads), 0, st, job, wq);
+        else
+            hipLaunchKernelGGL((k_match<false, false>), mgrid, dim3(kMatchThreads), 0, st, job, wq);
         break;
     }
     case 2: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 0); break;
     case 5: hipLaunchKernelGGL(k_parse_seg, grid, dim3(kParseLanes), 0, st, job); break;
     case 6: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 1); break;
     case 3: {
-        // ZGPU_FAST_VARIANT (A/B runs): 0 the round-2 walk, 4 64-bit positions
-        static const int fv = [] { const char *e = getenv("ZGPU_FAST_VARIANT"); return e ? atoi(e) : -1; }();
-        const bool old_walk = fv == 0;
         const bool ev = job.nfl || job.start || job.srec;
-        if (ev) {
-            if (old_walk) hipLaunchKernelGGL((k_parse_fast<true, false, int64_t>), grid, dim3(64), 0, st, job, heads);
-            else hipLaunchKernelGGL((k_parse_fast<true, true, int64_t>), grid, dim3(64), 0, st, job, heads);
-        } else if (old_walk) {
-            hipLaunchKernelGGL((k_parse_fast<false, false, int64_t>), grid, dim3(64), 0, st, job, heads);
-        } else if (job.pos31 && fv != 4) {
-            hipLaunchKernelGGL((k_parse_fast<false, true, int32_t>), grid, dim3(64), 0, st, job, heads);
-        } else {
-            hipLaunchKernelGGL((k_parse_fast<false, true, int64_t>), grid, dim3(64), 0, st, job, heads);
-        }
+        if (ev) hipLaunchKernelGGL((k_parse_fast<true, true, int64_t>), grid, dim3(64), 0, st, job, heads);
+        else if (job.pos31) hipLaunchKernelGGL((k_parse_fast<false, true, int32_t>), grid, dim3(64), 0, st, job, heads);
+        else hipLaunchKernelGGL((k_parse_fast<false, true, int64_t>), grid, dim3(64), 0, st, job, heads);
         break;
     }
     case 4: {
