@@ -588,3 +588,52 @@ def test_huffman_length_overflow(zg, oracle):
         res = zg.compress_batch(many, level=level, strategy=strategy)
         for i, (st, z) in enumerate(res):
             assert st == 0 and z == want[i % len(bufs)], (i, level, strategy)
+
+
+def test_bench_scale_subbatch_golden(zg):
+    """Bench-scale parity: a whole sub-batch of the benchmark's
+    shape -- 4096 x 1 MiB at L6 in one 4 GiB in-flight sub-batch (lane-built
+    trees, the two-slot pipeline's slot 0), and 4096 x 1 MiB enwik-style at L1
+    -- through zgpu_deflate_batch_dev; a strided sample of the streams equals
+    the compiled reference's (tests/golden/batch_golden.json), every status is
+    Z_OK and every stream inflates back to its input on the device."""
+    import json
+    import os
+    import torch
+    here = os.path.dirname(os.path.abspath(__file__))
+    g = json.load(open(os.path.join(here, "golden", "batch_golden.json")))
+    old = zg.set_inflight_bytes(4 << 30)
+    try:
+        for b in g["batches"]:
+            n, B = b["n"], b["buffers"]
+            cap = (zg.compress_bound(n) + 15) // 16 * 16
+            src = torch.empty(n * B, dtype=torch.uint8, device="cuda")
+            zg.generate_dev(src, n, B, b["kind"], seed=b["seed"], first_index=0)
+            off = torch.arange(B, dtype=torch.int64, device="cuda") * n
+            ln = torch.full((B,), n, dtype=torch.int64, device="cuda")
+            dst = torch.empty(cap * B, dtype=torch.uint8, device="cuda")
+            doff = torch.arange(B, dtype=torch.int64, device="cuda") * cap
+            dcap = torch.full((B,), cap, dtype=torch.int64, device="cuda")
+            dlen = torch.zeros(B, dtype=torch.int64, device="cuda")
+            st = torch.full((B,), 99, dtype=torch.int32, device="cuda")
+            zg.deflate_batch_dev(src, off, ln, dst, doff, dcap, dlen, st, level=b["level"])
+            torch.cuda.synchronize()
+            assert int((st != 0).sum().item()) == 0, b["name"]
+            lens = dlen.cpu().tolist()
+            for c in b["cases"]:
+                i = c["index"]
+                raw = src[i * n:(i + 1) * n].cpu().numpy().tobytes()
+                assert hashlib.sha256(raw).hexdigest() == c["input_sha256"], (b["name"], i)
+                z = dst[i * cap:i * cap + lens[i]].cpu().numpy().tobytes()
+                assert len(z) == c["len"] and hashlib.sha256(z).hexdigest() == c["sha256"], (b["name"], i)
+            out = torch.empty(n * B, dtype=torch.uint8, device="cuda")
+            olen = torch.zeros(B, dtype=torch.int64, device="cuda")
+            ost = torch.full((B,), 99, dtype=torch.int32, device="cuda")
+            zg.inflate_batch_dev(dst, doff, dlen, out, off, ln, olen, ost)
+            torch.cuda.synchronize()
+            assert int((ost != 0).sum().item()) == 0 and bool((olen == n).all().item())
+            assert torch.equal(out, src), b["name"]
+            del src, dst, out
+            torch.cuda.empty_cache()
+    finally:
+        zg.set_inflight_bytes(old)
