@@ -137,6 +137,74 @@ def sessions():
             for data in (text, runs):
                 S.append({"name": f"tune-fast-insert-L{level}-{lazy}-{data[1]}", "ops": [
                     ["init", level, 15, 8, 0], ["tune", 4, lazy, 258, 64], ["deflate", data, 4]]})
+    S += sessions_r3()
+    return S
+
+
+def sessions_r3():
+    """Round 3: z_stream controls with input pending and deflateBound after the
+    state changes (deflate.c:760-905)."""
+    S = []
+    text = ["gen", "text", 150000, 21]
+    mix = ["gen", "mix", 200000, 22]
+
+    def part(d, a, b):
+        return d[:4] + [a, b]
+    # a level change within the function while the last Z_NO_FLUSH call's
+    # input waits in the window: the decisions from where the parse stands
+    # read the new row
+    for a, b in ((6, 9), (9, 4), (4, 6), (5, 8), (7, 6), (6, 5), (1, 3), (3, 1), (2, 1)):
+        for cut in (100, 5000, 77777):
+            d = mix if a >= 4 else text
+            S.append({"name": f"params-pending-{a}-{b}-{cut}", "ops": [
+                ["init", a, 15, 8, 0], ["deflate", part(d, 0, cut), 0], ["params", b, 0],
+                ["deflate", part(d, cut, d[2]), 4]]})
+    for level, t in ((6, (4, 4, 16, 16)), (6, (32, 128, 258, 1024)), (9, (8, 16, 128, 128)),
+                     (4, (2, 6, 40, 8)), (1, (4, 20, 32, 32)), (2, (2, 4, 8, 4)), (8, (8, 8, 8, 0))):
+        S.append({"name": f"tune-pending-L{level}-{'-'.join(map(str, t))}", "ops": [
+            ["init", level, 15, 8, 0], ["deflate", part(mix, 0, 64000), 0], ["tune"] + list(t),
+            ["deflate", part(mix, 64000, 200000), 4]]})
+    # several changes, flushes in between, raw and gzip wrappers
+    for wb, lv in ((15, 6), (-15, 4), (31, 9), (15, 2)):
+        S.append({"name": f"params-many-w{wb}-L{lv}", "ops": [
+            ["init", lv, wb, 8, 0], ["deflate", part(mix, 0, 30000), 0],
+            ["params", 9 if lv >= 4 else 1, 0], ["deflate", part(mix, 30000, 61000), 0],
+            ["tune", 8, 16, 64, 32], ["deflate", part(mix, 61000, 90000), 2],
+            ["params", 5 if lv >= 4 else 3, 0], ["deflate", part(mix, 90000, 120000), 0],
+            ["params", 6 if lv >= 4 else 2, 0], ["deflate", part(mix, 120000, 200000), 4]]})
+    # a change while the last call stopped on a full output buffer (the parse
+    # stands at the end of the last block it handed out)
+    for lv, nb in ((6, 9), (9, 5), (2, 3), (1, 2)):
+        for out in (2000, 20000):
+            S.append({"name": f"params-paused-{lv}-{nb}-{out}", "ops": [
+                ["init", lv, 15, 8, 0], ["deflate", part(mix, 0, 150000), 0, out], ["params", nb, 0],
+                ["deflate", part(mix, 150000, 200000), 4, out]]})
+        S.append({"name": f"tune-paused-{lv}", "ops": [
+            ["init", lv, 15, 8, 0], ["deflate", part(mix, 0, 150000), 0, 3000], ["tune", 4, 8, 16, 8],
+            ["deflate", part(mix, 150000, 200000), 4, 3000]]})
+    # deflateBound after the state changes (deflate.c:842-905: the DICTID once
+    # strstart != 0, the gzip header's fields)
+    S.append({"name": "bound-states-zlib", "ops": [
+        ["init", 6, 15, 8, 0], ["bound", 100000], ["deflate", part(text, 0, 100), 0], ["bound", 100000],
+        ["deflate", part(text, 100, 5000), 0], ["bound", 100000], ["deflate", part(text, 5000, 9000), 2],
+        ["bound", 100000], ["deflate", part(text, 9000, 12000), 3], ["bound", 100000],
+        ["deflate", part(text, 12000, 150000), 4], ["bound", 100000]]})
+    S.append({"name": "bound-dict", "ops": [
+        ["init", 6, 15, 8, 0], ["bound", 5000], ["dict", ["gen", "text", 300, 31]], ["bound", 5000],
+        ["deflate", text, 4]]})
+    S.append({"name": "bound-dict-raw-w12", "ops": [
+        ["init", 9, -12, 8, 0], ["dict", ["gen", "text", 9000, 32]], ["bound", 5000], ["deflate", text, 4]]})
+    hdr = {"text": 1, "time": 7, "os": 11, "name": b"file.txt".hex(), "comment": b"a comment".hex(),
+           "extra": bytes(range(40)).hex(), "hcrc": 1}
+    S.append({"name": "bound-gzip-header", "ops": [
+        ["init", 6, 31, 8, 0], ["bound", 77777], ["header", hdr], ["bound", 77777], ["deflate", text, 4],
+        ["bound", 77777]]})
+    S.append({"name": "bound-gzip-header-w10", "ops": [
+        ["init", 3, 26, 5, 0], ["header", hdr], ["bound", 77777], ["deflate", text, 4]]})
+    for lv, st in ((0, 0), (1, 2), (4, 3)):
+        S.append({"name": f"bound-L{lv}-s{st}", "ops": [
+            ["init", lv, 15, 8, st], ["deflate", part(text, 0, 200), 0], ["bound", 1000],
+            ["deflate", part(text, 200, 300), 0], ["bound", 1000], ["deflate", part(text, 300, 150000), 4]]})
     return S
 
 

@@ -217,3 +217,32 @@ def test_zalloc_zfree_honoured(lib):
         s = ZStream()
         assert init(s) == 0 and s.zalloc and s.zfree    # the defaults are stored
         assert end(C.byref(s)) == 0
+
+
+def test_deflate_bound_states_vs_reference_golden(lib):
+    """deflateBound on the host side of the golden z_stream sessions: the
+    prefix of every session up to its first deflate() call (init, dictionary,
+    gzip header, bound) must give the compiled reference's values -- the DICTID
+    allowance once a dictionary is set, the gzip header's extra / name /
+    comment / HCRC bytes (deflate.c:842-905).  The rest runs on the GPU
+    (tests/test_gpu_zstream.py)."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from make_zstream_golden import materialize
+    from zhelpers import run_zsession
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "zstream_golden.json")))
+    checked = 0
+    for sess in g["sessions"]:
+        ops = sess["ops"]
+        k = next((i for i, op in enumerate(ops) if op[0] not in ("init", "dict", "header", "bound", "tune")), len(ops))
+        if not any(op[0] == "bound" for op in ops[:k]):
+            continue
+        rcs, _ = run_zsession(lib, materialize(ops[:k]))
+        for op, got, want in zip(ops[:k], rcs, sess["rcs"][:k]):
+            if op[0] == "dict":
+                assert got[0] == want[0], sess["name"]
+            else:
+                assert got == want, (sess["name"], op, got, want)
+        checked += 1
+    assert checked >= 4

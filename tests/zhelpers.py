@@ -365,7 +365,8 @@ def _bind_zstream(L):
             ("deflateSetHeader", C.c_int, [P, C.POINTER(GzHeader)]),
             ("inflateInit2_", C.c_int, [P, C.c_int, C.c_char_p, C.c_int]),
             ("inflate", C.c_int, [P, C.c_int]), ("inflateEnd", C.c_int, [P]),
-            ("inflateSetDictionary", C.c_int, [P, C.c_void_p, C.c_uint])):
+            ("inflateSetDictionary", C.c_int, [P, C.c_void_p, C.c_uint]),
+            ("deflateBound", C.c_ulong, [P, C.c_ulong])):
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
@@ -377,7 +378,10 @@ def run_zsession(L, ops, version=b"1.3.1.1-motley"):
     ops: ("init", level, windowBits, memLevel, strategy), ("dict", bytes),
     ("tune", good, lazy, nice, chain), ("params", level, strategy),
     ("prime", bits, value), ("header", dict of gz_header fields),
-    ("deflate", bytes, flush).  Output space is always ample."""
+    ("deflate", bytes, flush[, out]), ("bound", sourceLen).  Output space is
+    ample unless a deflate op gives `out`: then every call gets `out` bytes and
+    the op repeats the call until the input is taken and the call ends with
+    space left (or Z_STREAM_END), as zpipe.c's loop does."""
     _bind_zstream(L)
     s = ZStream()
     out, rcs, keep = bytearray(), [], []
@@ -423,12 +427,25 @@ def run_zsession(L, ops, version=b"1.3.1.1-motley"):
             keep.append(ib)
             s.next_in, s.avail_in = C.addressof(ib), len(data)
             seq = []
+            if len(op) > 3:                      # small output buffers: one call per `out` bytes
+                ob = C.create_string_buffer(op[3])
+                for _ in range(200000):
+                    s.next_out, s.avail_out = C.addressof(ob), op[3]
+                    rc = L.deflate(C.byref(s), flush)
+                    out.extend(ob.raw[: op[3] - s.avail_out])
+                    seq.append(rc)
+                    if rc < 0 or rc == 1 or (s.avail_in == 0 and s.avail_out != 0):
+                        break
+                rcs.append(seq)
+                continue
             for _ in range(1000):
                 rc = with_out(lambda: L.deflate(C.byref(s), flush), len(data) + len(data) // 2)
                 seq.append(rc)
                 if rc < 0 or rc == 1 or (s.avail_in == 0 and s.avail_out != 0):
                     break
             rcs.append(seq)
+        elif k == "bound":
+            rcs.append(int(L.deflateBound(C.byref(s), op[1])))
         else:
             raise ValueError(k)
     L.deflateEnd(C.byref(s))

@@ -408,6 +408,11 @@ struct FlushSpec {
     int cut;
     uint32_t *snap;
     const uint64_t *aux;
+    // configuration changes (DeflateJob::cfg_pos / cfg_tab / ncfg / cfg_q, device arrays)
+    const uint64_t *cfg_pos = nullptr;
+    const LevelCfg *cfg_tab = nullptr;
+    uint32_t ncfg = 0;
+    int cfg_q = 0;
 };
 
 // deflateInit2_'s windowBits / memLevel rules (deflate.c:400-425): negative
@@ -631,6 +636,10 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.cut = fs->cut;
             job.snap = fs->snap;
             job.fl_aux = fs->aux;
+            job.cfg_pos = fs->cfg_pos;
+            job.cfg_tab = fs->cfg_tab;
+            job.ncfg = fs->ncfg;
+            job.cfg_q = fs->cfg_q;
         }
         return job;
     };
@@ -734,6 +743,10 @@ struct FlushHost {
     std::vector<uint32_t> *snap_head = nullptr;
     std::vector<uint16_t> *snap_prev = nullptr;
     uint32_t snap_rec = 0xffffffffu;
+    // configuration changes (host arrays, see DeflateJob::cfg_pos)
+    const uint64_t *cfg_pos = nullptr;
+    const LevelCfg *cfg_tab = nullptr;
+    uint32_t ncfg = 0;
 };
 
 // debug trace of the streaming deflate() engine (ZGPU_STREAM_TRACE)
@@ -756,7 +769,7 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
         dcap[i] = dst_len[i];
         out_total += (dst_len[i] + 15) & ~15ull;
     }
-    const size_t ev_bytes = fh ? 32ull * fh->n + 160 : 0;
+    const size_t ev_bytes = fh ? 32ull * fh->n + 160 + (8 + sizeof(LevelCfg)) * fh->ncfg + 16 : 0;
     const size_t meta_bytes = 8 * 4 * count + 16 * count + ev_bytes;
     if (!c.ws_io.ensure(in_total + 64) || !c.ws_io2.ensure(out_total + 64) ||
         !c.ws_small.ensure(meta_bytes + 64))
@@ -807,6 +820,18 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
                        fh->head_in, fh->prev_in, fh->prev_n, fh->plan, fh->nplan, fh->dict, fh->pre_ins,
                        d_ml, (uint32_t)ml.size(), nullptr, d_evb, fh->e0, fh->cut, nullptr,
                        fh->aux ? d_aux : nullptr};
+        if (fh->ncfg) {                                  // configuration changes after the events
+            uint64_t *d_cp = reinterpret_cast<uint64_t *>(d_evb + fh->n + (fh->n & 1));
+            LevelCfg *d_ct = reinterpret_cast<LevelCfg *>(d_cp + fh->ncfg);
+            if (hipMemcpyAsync(d_cp, fh->cfg_pos, 8ull * fh->ncfg, hipMemcpyHostToDevice, st) != hipSuccess ||
+                hipMemcpyAsync(d_ct, fh->cfg_tab, sizeof(LevelCfg) * fh->ncfg, hipMemcpyHostToDevice, st) !=
+                    hipSuccess)
+                return ZGPU_MEM_ERROR;
+            fs.cfg_pos = d_cp;
+            fs.cfg_tab = d_ct;
+            fs.ncfg = fh->ncfg;
+            for (uint32_t k = 0; k < fh->ncfg; k++) fs.cfg_q |= (int)(fh->cfg_tab[k].good < fh->cfg_tab[k].lazy);
+        }
         if (fh->rec_out) {
             const size_t sym_limit = (size_t(1) << (mem_level + 6)) - 1;         // lit_bufsize - 1
             const size_t nrec = src_len[0] / sym_limit + 4 + 2ull * fh->n + fh->nplan;
@@ -1498,7 +1523,7 @@ struct internal_state {
     ZAlloc<uint8_t> al;
     explicit internal_state(const ZAlloc<uint8_t> &a = {})
         : al(a), in(a), out(a), ev_pos(a), ev_type(a), ev_aux(a), fast_head(a), fast_prev(a), hist(a), body(a),
-          items(ZAlloc<StreamItem>(a)), evb(ZAlloc<uint32_t>(a)) {}
+          items(ZAlloc<StreamItem>(a)), evb(ZAlloc<uint32_t>(a)), cfg_pos(a), cfg_row(ZAlloc<LevelCfg>(a)) {}
     int level, wrap, strategy;
     zvec<uint8_t> in, out;          // deflate: the input since the last Z_FULL_FLUSH; output queue
     size_t out_pos;
@@ -1582,6 +1607,13 @@ struct internal_state {
     uint32_t dict_id = 0;
     bool need_dict = false;              // inflate: Z_NEED_DICT answered, waiting for the dictionary
     uint32_t want_dict = 0;              // its DICTID
+    // configuration rows changed with input pending (deflateParams within the
+    // same function, deflateTune; deflate.c:760-820): row cfg_row[k] governs
+    // the current part's decision points from part position cfg_pos[k] on,
+    // cfg0 the ones before cfg_pos[0]
+    zvec<uint64_t> cfg_pos;
+    std::vector<LevelCfg, ZAlloc<LevelCfg>> cfg_row;
+    LevelCfg cfg0{};
 };
 
 namespace {
@@ -1683,6 +1715,24 @@ int deflate_part(internal_state *s, bool closed) {
     std::vector<uint32_t> evb;
     fh.rec_out = &rec;
     fh.evb_out = &evb;
+    // the configuration row at the resume point, and the changes after it
+    LevelCfg job_cfg = s->tuned ? s->tune : kLevelCfg[s->level];
+    std::vector<uint64_t> cpos;
+    std::vector<LevelCfg> crow;
+    if (!s->cfg_pos.empty()) {
+        job_cfg = s->cfg0;
+        for (size_t k = 0; k < s->cfg_pos.size(); k++) {
+            if (s->cfg_pos[k] <= s->res_pos) {
+                job_cfg = s->cfg_row[k];
+            } else {
+                cpos.push_back(s->cfg_pos[k] - base);
+                crow.push_back(s->cfg_row[k]);
+            }
+        }
+        fh.cfg_pos = cpos.data();
+        fh.cfg_tab = crow.data();
+        fh.ncfg = (uint32_t)cpos.size();
+    }
     std::vector<uint32_t> head_in;
     const bool fast = s->level >= 1 && s->level <= 3 && s->strategy != Z_HUFFMAN_ONLY && s->strategy != Z_RLE;
     if (fast && s->res_pos > base && s->fast_head.empty()) {
@@ -1710,7 +1760,7 @@ int deflate_part(internal_state *s, bool closed) {
         Lease L;
         int rc = L.rc;
         if (!rc) rc = compress_host_locked(*L.c, &sp, &sl, &dp, &cap, &st, 1, s->level, ZGPU_WRAP_RAW, s->strategy,
-                                           &fh, s->wbits, s->mem_level, s->tuned ? &s->tune : nullptr);
+                                           &fh, s->wbits, s->mem_level, &job_cfg);
         ZTRACE("part: rc %d st %d out %zu recs %zu evb %zu snap %u\n", rc, st, cap, rec.size() / 4, evb.size(),
                fh.snap_rec);
         if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
@@ -1831,6 +1881,8 @@ void close_part(internal_state *s) {
     s->proc_bits = 0;
     s->body.clear();
     s->body_at = 0;
+    s->cfg_pos.clear();                 // the current row goes on (s->level, s->tune)
+    s->cfg_row.clear();
 }
 
 // after a call: the latest item handed out that a new job can start at
@@ -1867,6 +1919,10 @@ void choose_resume(internal_state *s) {
             s->in.erase(s->in.begin(), s->in.begin() + (std::ptrdiff_t)(s->res_S - s->in_base));
             s->in_base = s->res_S;
         }
+        size_t k = 0;                                 // rows behind the resume point: the job's first row
+        while (k < s->cfg_pos.size() && s->cfg_pos[k] <= s->res_pos) s->cfg0 = s->cfg_row[k++];
+        s->cfg_pos.erase(s->cfg_pos.begin(), s->cfg_pos.begin() + (std::ptrdiff_t)k);
+        s->cfg_row.erase(s->cfg_row.begin(), s->cfg_row.begin() + (std::ptrdiff_t)k);
         s->res_item = r;
         return;
     }
@@ -2458,23 +2514,59 @@ int deflateSetDictionary(z_streamp strm, const Bytef *dictionary, uInt dictLengt
     }
 }
 
-// deflateTune (deflate.c): good_length, max_lazy, nice_length, max_chain for
-// the jobs from here on (unsigned as deflate_state holds them; a chain of 0
-// never runs out in longest_match's unsigned count).  Exact where no input is
-// pending (see zgpu_zlib.h).
+// The decision point the parse stands at between two deflate() calls (part
+// position): after a call that stopped on a full output buffer, the end of the
+// last block it handed out (the reference's strstart there); after need_more,
+// the first point with less than MIN_LOOKAHEAD of the input read ahead of it
+// (deflate_slow / deflate_fast decide no position closer to the end of the
+// input without a flush, deflate.c:1841-1844, :1941-1944), or the last flush.
+size_t parse_point(const internal_state *s) {
+    if (s->ev_done < s->ev_type.size() && s->t > 0 && s->items[s->t - 1].kind == kItBlock)
+        return (size_t)s->items[s->t - 1].in_end;
+    const size_t x = s->rd > (size_t)(kMinLookahead - 1) ? s->rd - (kMinLookahead - 1) : 0;
+    return std::max(x, s->flush_done);
+}
+
+// A configuration row changed with input pending (deflate.c:760-820 rewrite
+// max_lazy_match, good_match, nice_match, max_chain_length in the state): the
+// decisions from the point the parse stands at on read the new row.  A later
+// job carries it as a change at that part position (DeflateJob::cfg_pos).
+// Z_HUFFMAN_ONLY / Z_RLE read no row.
+void cfg_change(internal_state *s, const LevelCfg &before) {
+    if (!pending_input(s) || s->level == 0 || s->strategy == Z_HUFFMAN_ONLY || s->strategy == Z_RLE) return;
+    const LevelCfg now = s->tuned ? s->tune : kLevelCfg[s->level];
+    const size_t x = parse_point(s);
+    if (s->cfg_pos.empty()) s->cfg0 = before;
+    if (!s->cfg_pos.empty() && s->cfg_pos.back() >= x) {   // a second change at the same point
+        s->cfg_row.back() = now;
+        return;
+    }
+    s->cfg_pos.push_back(x);
+    s->cfg_row.push_back(now);
+}
+
+// deflateTune (deflate.c:805-820): good_length, max_lazy, nice_length,
+// max_chain for the decisions from here on (unsigned as deflate_state holds
+// them; a chain of 0 never runs out in longest_match's unsigned count).
 int deflateTune(z_streamp strm, int good_length, int max_lazy, int nice_length, int max_chain) {
     if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
-    if (pending_input(s)) return unsupported(strm, "deflateTune: input pending since the last flush");
-    s->tune = LevelCfg{(uint32_t)good_length, (uint32_t)max_lazy,
-                       nice_length < 0 ? 0xffffffffu : (uint32_t)nice_length,
-                       max_chain == 0 ? 0xffffffffu : (uint32_t)max_chain};
-    s->tuned = true;
-    return Z_OK;
+    try {
+        const LevelCfg before = s->tuned ? s->tune : kLevelCfg[s->level];
+        s->tune = LevelCfg{(uint32_t)good_length, (uint32_t)max_lazy,
+                           nice_length < 0 ? 0xffffffffu : (uint32_t)nice_length,
+                           max_chain == 0 ? 0xffffffffu : (uint32_t)max_chain};
+        s->tuned = true;
+        cfg_change(s, before);
+        return Z_OK;
+    } catch (const std::bad_alloc &) {
+        return Z_MEM_ERROR;
+    }
 }
 
-// deflateParams (deflate.c): flushes with Z_BLOCK when the level's function
-// or the strategy changes and deflate() has run, then switches.
+// deflateParams (deflate.c:760-803): flushes with Z_BLOCK when the level's
+// function or the strategy changes and deflate() has run, then switches; a
+// level change within the same function takes effect at the next decision.
 int deflateParams(z_streamp strm, int level, int strategy) {
     if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
@@ -2491,15 +2583,19 @@ int deflateParams(z_streamp strm, int level, int strategy) {
         const int err = deflate(strm, Z_BLOCK);
         if (err == Z_STREAM_ERROR) return err;
         if (strm->avail_in || pending_input(s)) return Z_BUF_ERROR;
-    } else if (s->level != level && pending_input(s)) {
-        return unsupported(strm, "deflateParams: input pending since the last flush");
     }
-    if (s->level != level) {
-        s->level = level;
-        s->tuned = false;                  // configuration_table's row again
+    try {
+        if (s->level != level) {
+            const LevelCfg before = s->tuned ? s->tune : kLevelCfg[s->level];
+            s->level = level;
+            s->tuned = false;                  // configuration_table's row again
+            cfg_change(s, before);
+        }
+        s->strategy = strategy;
+        return Z_OK;
+    } catch (const std::bad_alloc &) {
+        return Z_MEM_ERROR;
     }
-    s->strategy = strategy;
-    return Z_OK;
 }
 
 // deflatePrime (deflate.c): bits in front of what deflate() writes next.

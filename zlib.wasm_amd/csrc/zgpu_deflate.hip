@@ -717,6 +717,15 @@ __device__ inline int64_t flush_limit(const DeflateJob &job, int64_t p, int64_t 
     return lo < job.nmlim ? (int64_t)job.mlim[lo] : n;
 }
 
+// configuration rows in force at decision point p: the number of changes at
+// or before p (DeflateJob::cfg_pos), 0 for none
+__device__ inline uint32_t cfg_count(const DeflateJob &job, int64_t p) {
+    uint32_t k = 0;
+    while (k < job.ncfg && (int64_t)job.cfg_pos[k] <= p) k++;
+    return k;
+}
+__device__ inline LevelCfg cfg_row(const DeflateJob &job, uint32_t k) { return k ? job.cfg_tab[k - 1] : job.cfg; }
+
 template <bool kEv = false, bool kSegs = false>
 __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int want_q) {
     constexpr int kSortBuckets = 64;
@@ -785,14 +794,30 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
                 s_perm[s_base[bk[u]] + rk[u]] = (uint16_t)(tid + u * kMatchThreads);
         __syncthreads();
         if (ts + kMT < s1) tile_prefetch(P, ts + kMT, n, in, L, K, tid);   // lands during the walks
-        for (;;) {
-            const int i = atomicAdd(&next_i, 1);
-            if (i >= tile_n) break;
-            const int64_t p = ts + (int)s_perm[i];
-            // a flush job's search at p sees the input up to the next flush
-            // position only (nice and the compare length are clamped to it)
-            const int64_t nl = kEv ? flush_limit(job, p, n) : n;
-            dwq_walk(E, p, B, nl, cfg, rf, rq, want_q, max_dist);
+        // a streaming job whose configuration changes inside this tile walks it
+        // once per row, each pass taking the positions of its row: the budget
+        // count of a wave's walks stays uniform
+        const uint32_t k0 = kEv && tile_n ? cfg_count(job, ts) : 0;
+        const uint32_t k1 = kEv && tile_n ? cfg_count(job, ts + tile_n - 1) : 0;
+        for (uint32_t k = k0; k <= k1; k++) {
+            const LevelCfg c = kEv ? cfg_row(job, k) : cfg;
+            const int64_t lo = k ? (int64_t)job.cfg_pos[k - 1] : -1;
+            const int64_t hi = kEv && k < job.ncfg ? (int64_t)job.cfg_pos[k] : INT64_MAX;
+            if (k > k0) {
+                __syncthreads();
+                if (tid == 0) next_i = 0;
+                __syncthreads();
+            }
+            for (;;) {
+                const int i = atomicAdd(&next_i, 1);
+                if (i >= tile_n) break;
+                const int64_t p = ts + (int)s_perm[i];
+                if (kEv && (p < lo || p >= hi)) continue;
+                // a flush job's search at p sees the input up to the next flush
+                // position only (nice and the compare length are clamped to it)
+                const int64_t nl = kEv ? flush_limit(job, p, n) : n;
+                dwq_walk(E, p, B, nl, c, rf, rq, want_q, max_dist);
+            }
         }
         __syncthreads();
     }
@@ -949,9 +974,12 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
     const uint32_t *rf = job.rfull + job.ws_off[bi];
     const uint32_t *rq = job.rquart + job.ws_off[bi];
     const LevelCfg cfg = job.cfg;
-    const bool use_q = cfg.good < cfg.lazy;
+    bool use_q = cfg.good < cfg.lazy;
+    bool stage_q = use_q;                         // any row of the job reads rquart
+    for (uint32_t k = 0; k < job.ncfg; k++) stage_q |= job.cfg_tab[k].good < job.cfg_tab[k].lazy;
     const bool filtered = job.strategy == 1;
-    const uint32_t lazy = cfg.lazy, good = cfg.good;
+    uint32_t lazy = cfg.lazy, good = cfg.good;
+    uint32_t ci = 0;                              // configuration changes acted on
     if (only_flagged && job.nblocks[bi] != kParseFallback) return;
 
     ParseU po;
@@ -976,7 +1004,7 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
     uint32_t t0 = p & ~15u;
     while (!done) {
         stage_words<64, kPT / 4 / 64>(s_rf, rf, t0, kPT, n, lane);
-        if (use_q) stage_words<64, kPT / 4 / 64>(s_rq, rq, t0, kPT, n, lane);
+        if (stage_q) stage_words<64, kPT / 4 / 64>(s_rq, rq, t0, kPT, n, lane);
         stage_bytes<64, (kPT + 16) / 16 / 64 + 1>(s_in, in, (int64_t)t0 - 16, kPT + 16, n, lane);
         __syncthreads();
         const bool tile_to_end = (uint64_t)t0 + kPT >= n;
@@ -1049,6 +1077,12 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
                 }
             }
             // ---- one deflate_slow step (deflate.c:1946-2027) ----
+            while (ci < job.ncfg && p >= (uint32_t)job.cfg_pos[ci]) {   // deflateParams / deflateTune
+                lazy = job.cfg_tab[ci].lazy;
+                good = job.cfg_tab[ci].good;
+                use_q = good < lazy;
+                ci++;
+            }
             const uint32_t prev_length = match_length, prev_match = match_start;
             match_length = kMinMatch - 1;
             if (lookahead >= kMinMatch && prev_length < lazy) {
@@ -1714,7 +1748,8 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     const WinP wp = job_win(job);
     const uint32_t hsize = wp.mask + 1;                  // hash_size = 1 << hash_bits
     uint32_t *head = heads + (size_t)bi * hsize;
-    const LevelCfg cfg = job.cfg;
+    LevelCfg cfg = job.cfg;
+    uint32_t ci = 0;                                     // configuration changes acted on
     // a resumed flush job (start > 0) finds head[] and prev[] as the last job
     // left them, rebased to its buffer (zgpu_api.cpp deflate_part)
     if (!kEv || job.start == 0 || job.dict)
@@ -1888,6 +1923,8 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
             }
         }
         wsee(p);
+        if (kEv)                                         // deflateParams / deflateTune
+            while (ci < job.ncfg && p >= (P)job.cfg_pos[ci]) cfg = job.cfg_tab[ci++];
         P lookahead = po.E - p;
         P hh = 0;
         if (lookahead >= kMinMatch) hh = insert(p);
@@ -2807,11 +2844,12 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         hipLaunchKernelGGL(k_count, grid, dim3(kCntThreads), 0, st, job);
         break;
     case 1: {
-        const int wq = (int)(job.cfg.good < job.cfg.lazy);   // the parse reads rquart (prev_length >= good)
+        const int wq = (int)(job.cfg.good < job.cfg.lazy) | job.cfg_q;   // the parse reads rquart (prev_length >= good)
         const dim3 mgrid(job.seg ? job.nseg : job.count);   // per segment or per buffer
-        if (job.nfl && job.seg)                                 // a flush job (zgpu_api.cpp deflate())
+        const bool ev = job.nfl || job.ncfg;                // a streaming job (zgpu_api.cpp deflate())
+        if (ev && job.seg)
             hipLaunchKernelGGL((k_match<true, true>), mgrid, dim3(kMatchThreads), 0, st, job, wq);
-        else if (job.nfl)
+        else if (ev)
             hipLaunchKernelGGL((k_match<true, false>), mgrid, dim3(kMatchThreads), 0, st, job, wq);
         else if (job.seg)                                       // few large buffers: per segment
             hipLaunchKernelGGL((k_match<false, true>), mgrid, dim3(kMatchThreads), 0, st, job, wq);

@@ -185,6 +185,16 @@ struct DeflateJob {
     uint32_t e0;             // a job resumed at a block cut: E there (0: the start, nothing read ahead)
     int cut;                 // resumed at a block cut, not after a flush (no s->insert strings)
     uint32_t *snap;          // levels 1..3: head[] at the last cut; snap[hash_size] = its record
+    // configuration changes of a streaming job (deflateParams within the same
+    // function, deflateTune, with input pending: deflate.c:760-820): cfg_tab[k]
+    // applies to the decision points at or after cfg_pos[k] (ascending,
+    // buffer-relative); before cfg_pos[0], `cfg`.  Each decision reads its
+    // row when it is made (deflate_slow / deflate_fast / longest_match read
+    // max_lazy, good, nice and chain from the state each time).
+    const uint64_t *cfg_pos;
+    const LevelCfg *cfg_tab;
+    uint32_t ncfg;
+    int cfg_q;               // some row of cfg_tab has good < lazy: k_match computes rquart
 };
 
 // the per-job window/hash parameters (deflate.c:440-455)
