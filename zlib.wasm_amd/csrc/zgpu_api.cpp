@@ -2653,8 +2653,10 @@ int deflateEnd(z_streamp strm) {
 // leaves (below MIN_LOOKAHEAD, at most MAX_MATCH for Z_RLE, 0 for
 // Z_HUFFMAN_ONLY) is less than what it has read.  A Z_FULL_FLUSH resets it
 // (deflate.c:1225-1229), as it resets the part.
-static bool strstart_nonzero(const internal_state *s) {
+static bool strstart_nonzero(const z_stream *strm, const internal_state *s) {
     if (s->level == 0) return s->st_strstart != 0;
+    if (s->finished)                       // the part since the last Z_FULL_FLUSH, or the one-call stream
+        return s->flushed ? s->in_base + s->in.size() > 0 : strm->total_in > 0;
     if (s->flush_done > 0) return true;
     const size_t need = s->strategy == Z_HUFFMAN_ONLY ? 1 : s->strategy == Z_RLE ? kMaxMatch + 1 : kMinLookahead;
     return s->rd >= need;
@@ -2665,13 +2667,14 @@ uLong deflateBound(z_streamp strm, uLong sourceLen) {          // deflate.c:842-
     const uLong storelen = sourceLen + (sourceLen >> 5) + (sourceLen >> 7) + (sourceLen >> 11) + 7;
     if (!strm || !strm->state || strm->state->inflating) return (fixedlen > storelen ? fixedlen : storelen) + 18;
     const internal_state *s = strm->state;
-    // deflate() negates wrap once the trailer is written: then the default row (6)
-    const int w = s->finished && s->wrap ? -1 : s->wrap;
+    // the wrapper's row also after Z_STREAM_END (the reference's bound does not
+    // change once the trailer is written: tests/golden/zstream_golden.json)
+    const int w = s->wrap;
     uLong wraplen = 6;
     if (w == 0) {
         wraplen = 0;
     } else if (w == 1) {
-        wraplen = 6 + (strstart_nonzero(s) ? 4 : 0);
+        wraplen = 6 + (strstart_nonzero(strm, s) ? 4 : 0);
     } else if (w == 2) {
         wraplen = 18;
         if (const gz_header *h = s->gzhead) {                      // the caller's header, read now
