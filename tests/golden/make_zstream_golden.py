@@ -205,6 +205,48 @@ def sessions_r3():
         S.append({"name": f"bound-L{lv}-s{st}", "ops": [
             ["init", lv, 15, 8, st], ["deflate", part(text, 0, 200), 0], ["bound", 1000],
             ["deflate", part(text, 200, 300), 0], ["bound", 1000], ["deflate", part(text, 300, 150000), 4]]})
+    # deflateParams switching the level's function after data (deflate.c:777-803):
+    # the Z_BLOCK flush, then the new function over the same window -- deflate_fast
+    # inserts selectively, deflate_slow everything, deflate_stored nothing until
+    # fill_window hashes its s->insert strings; gzsetparams' pattern
+    # (gzwrite.c:587: a Z_BLOCK flush of the pending input, then deflateParams)
+    chains = [(6, 1), (1, 6), (6, 0), (0, 6), (1, 0), (0, 1), (3, 9), (9, 2), (2, 4)]
+    for a, b in chains:
+        for wb in (15, -15):
+            S.append({"name": f"switch-{a}-{b}-w{wb}", "ops": [
+                ["init", a, wb, 8, 0], ["deflate", part(mix, 0, 70000), 0], ["params", b, 0],
+                ["deflate", part(mix, 70000, 200000), 4]]})
+    for seq in ((1, 0, 1), (6, 0, 6), (1, 6, 1), (6, 1, 6), (9, 2, 0, 7), (0, 3, 0, 5), (2, 0, 8, 1)):
+        ops = [["init", seq[0], 15, 8, 0]]
+        step = 200000 // len(seq)
+        for i, lv in enumerate(seq):
+            if i:
+                ops.append(["params", lv, 0])
+            ops.append(["deflate", part(mix, i * step, (i + 1) * step if i + 1 < len(seq) else 200000),
+                        4 if i + 1 == len(seq) else 0])
+        S.append({"name": "switch-seq-" + "-".join(map(str, seq)), "ops": ops})
+    for a, b in ((6, 1), (1, 6), (0, 6), (6, 0), (2, 0)):
+        S.append({"name": f"gzsetparams-{a}-{b}", "ops": [
+            ["init", a, 31, 8, 0], ["deflate", part(text, 0, 40000), 0], ["deflate", part(text, 40000, 41000), 5],
+            ["params", b, 0], ["deflate", part(text, 41000, 150000), 4]]})
+        S.append({"name": f"switch-small-out-{a}-{b}", "ops": [
+            ["init", a, 15, 8, 0], ["deflate", part(mix, 0, 90000), 0, 3000], ["params", b, 0],
+            ["deflate", part(mix, 90000, 200000), 4, 3000]]})
+    for a, b, wb, ml in ((6, 1, 10, 5), (1, 6, 12, 9), (0, 2, 9, 1), (3, 0, 11, 7)):
+        S.append({"name": f"switch-{a}-{b}-w{wb}-m{ml}", "ops": [
+            ["init", a, wb, ml, 0], ["deflate", part(mix, 0, 50000), 0], ["params", b, 0],
+            ["deflate", part(mix, 50000, 130000), 2], ["params", a, 0], ["deflate", part(mix, 130000, 200000), 4]]})
+    # small stretches between switches (the window mixes functions)
+    S.append({"name": "switch-short-stretches", "ops": [
+        ["init", 1, 15, 8, 0], ["deflate", part(text, 0, 20000), 0], ["params", 0, 0],
+        ["deflate", part(text, 20000, 20100), 0], ["params", 6, 0], ["deflate", part(text, 20100, 21000), 0],
+        ["params", 2, 0], ["deflate", part(text, 21000, 21500), 0], ["params", 7, 0],
+        ["deflate", part(text, 21500, 150000), 4]]})
+    # strategy changes within deflate_slow / deflate_fast
+    for a, sa, sb in ((6, 0, 1), (6, 1, 4), (4, 4, 0), (2, 0, 1), (1, 4, 0)):
+        S.append({"name": f"strategy-{a}-{sa}-{sb}", "ops": [
+            ["init", a, 15, 8, sa], ["deflate", part(mix, 0, 80000), 0], ["params", a, sb],
+            ["deflate", part(mix, 80000, 200000), 4]]})
     return S
 
 

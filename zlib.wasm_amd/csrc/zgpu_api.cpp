@@ -413,6 +413,9 @@ struct FlushSpec {
     const LevelCfg *cfg_tab = nullptr;
     uint32_t ncfg = 0;
     int cfg_q = 0;
+    // a window parsed partly by deflate_fast (DeflateJob::lk_n, pre_from, keep_head)
+    uint32_t lk_n = 0, pre_from = 0;
+    int keep_head = 0;
 };
 
 // deflateInit2_'s windowBits / memLevel rules (deflate.c:400-425): negative
@@ -640,6 +643,12 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.cfg_tab = fs->cfg_tab;
             job.ncfg = fs->ncfg;
             job.cfg_q = fs->cfg_q;
+            job.pre_from = fs->pre_from;
+            job.keep_head = fs->keep_head;
+            if (slow && fs->head_in) {                  // k_links resumes deflate_fast's chains
+                job.lk_n = fs->lk_n;
+                job.lk_head = c.ws_heads.as<uint32_t>();
+            }
         }
         return job;
     };
@@ -747,6 +756,9 @@ struct FlushHost {
     const uint64_t *cfg_pos = nullptr;
     const LevelCfg *cfg_tab = nullptr;
     uint32_t ncfg = 0;
+    // a window parsed partly by deflate_fast: see FlushSpec
+    uint32_t lk_n = 0, pre_from = 0;
+    int keep_head = 0;
 };
 
 // debug trace of the streaming deflate() engine (ZGPU_STREAM_TRACE)
@@ -832,6 +844,9 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
             fs.ncfg = fh->ncfg;
             for (uint32_t k = 0; k < fh->ncfg; k++) fs.cfg_q |= (int)(fh->cfg_tab[k].good < fh->cfg_tab[k].lazy);
         }
+        fs.lk_n = fh->lk_n;
+        fs.pre_from = fh->pre_from;
+        fs.keep_head = fh->keep_head;
         if (fh->rec_out) {
             const size_t sym_limit = (size_t(1) << (mem_level + 6)) - 1;         // lit_bufsize - 1
             const size_t nrec = src_len[0] / sym_limit + 4 + 2ull * fh->n + fh->nplan;
@@ -1522,7 +1537,7 @@ enum : uint8_t { kItStop = 0, kItBlock = 1, kItMarker = 2, kItFinal = 3 };
 struct internal_state {
     ZAlloc<uint8_t> al;
     explicit internal_state(const ZAlloc<uint8_t> &a = {})
-        : al(a), in(a), out(a), ev_pos(a), ev_type(a), ev_aux(a), fast_head(a), fast_prev(a), hist(a), body(a),
+        : al(a), in(a), out(a), ev_pos(a), ev_type(a), ev_aux(a), fast_head(a), fast_prev(a), l0_hist(a), hist(a), body(a),
           items(ZAlloc<StreamItem>(a)), evb(ZAlloc<uint32_t>(a)), cfg_pos(a), cfg_row(ZAlloc<LevelCfg>(a)) {}
     int level, wrap, strategy;
     zvec<uint8_t> in, out;          // deflate: the input since the last Z_FULL_FLUSH; output queue
@@ -1554,7 +1569,14 @@ struct internal_state {
     // levels 1..3: k_parse_fast's hash chains at the resume point (head[] as
     // part positions, prev links of [res_S, res_pos)) and as the last job left them
     zvec<uint64_t> fast_head;       // level 1-3 head[] at the resume point: 64-bit part positions
-    zvec<uint16_t> fast_prev;
+    zvec<uint16_t> fast_prev;       // the prev links of part positions [fast_S, fast_at)
+    uint64_t fast_at = 0, fast_S = 0;   // the snapshot's part position and its window offset
+    uint32_t fast_pend = 0;             // strings a flush left unhashed there (s->insert)
+    // level 0 (deflate_stored_call): the window's bytes (the last st_strstart
+    // input bytes) and the part position of the input consumed, for a
+    // deflateParams switch to a level that searches the window
+    zvec<uint8_t> l0_hist;
+    uint64_t l0_pos = 0;
     // inflate streams
     int inflating = 0;
     int wbits = 15;         // deflate: w_bits (9..15); inflate: inflateInit2_'s windowBits
@@ -1733,24 +1755,41 @@ int deflate_part(internal_state *s, bool closed) {
         fh.cfg_tab = crow.data();
         fh.ncfg = (uint32_t)cpos.size();
     }
+    // The hash chains the job starts from.  deflate_fast inserts selectively
+    // (deflate.c:1873-1897): where it parsed, its chains come from the snapshot
+    // of its last resume point (fast_head / fast_prev at part position fast_at,
+    // fast_pend strings still to be hashed there).  Everything after that -- or
+    // everything, with no deflate_fast region in reach -- was inserted string by
+    // string (deflate_slow, a dictionary, a stored stretch's s->insert strings
+    // that fill_window hashes, deflate.c:318-335), the last two of a flush late.
     std::vector<uint32_t> head_in;
     const bool fast = s->level >= 1 && s->level <= 3 && s->strategy != Z_HUFFMAN_ONLY && s->strategy != Z_RLE;
-    if (fast && s->res_pos > base && s->fast_head.empty()) {
-        // the part starts with a preset dictionary: its strings are inserted
-        // first, all but the last two (deflateSetDictionary, deflate.c)
+    const bool slow = s->level >= 4 && s->strategy != Z_HUFFMAN_ONLY && s->strategy != Z_RLE;
+    const uint64_t wsize = 1ull << s->wbits;
+    const bool have_fast = !s->fast_head.empty() && s->fast_S <= base && base <= s->fast_at &&
+                           s->fast_at + wsize > s->res_pos;
+    if ((fast || slow) && have_fast && s->res_pos > base) {     // rebase the saved chains to this buffer
+        head_in.resize(s->fast_head.size());
+        for (size_t i = 0; i < head_in.size(); i++)
+            head_in[i] = s->fast_head[i] > base ? (uint32_t)(s->fast_head[i] - base) : 0;
+        fh.head_in = head_in.data();
+        fh.prev_in = s->fast_prev.data() + (base - s->fast_S);
+        fh.prev_n = (size_t)(s->fast_at - base);
+    }
+    const uint32_t snap_end = have_fast ? (uint32_t)(s->fast_at - s->fast_pend - base) : 0;
+    if (fast && s->res_pos > base && !(have_fast && s->fast_at == s->res_pos)) {
+        // the window's strings are inserted first, all but the last two (a preset
+        // dictionary, deflateSetDictionary; or a window another function parsed):
+        // from the snapshot's end on, or all of them with no snapshot
         const uint32_t d = (uint32_t)(s->res_pos - base);
         fh.dict = 1;
+        fh.keep_head = have_fast ? 1 : 0;
+        fh.pre_from = snap_end;
         fh.pre_ins = d >= kMinMatch ? d - (kMinMatch - 1) : 0;
+        if (fh.pre_ins < fh.pre_from) fh.pre_ins = fh.pre_from;
     }
+    if (slow && have_fast && snap_end > 0) fh.lk_n = snap_end;   // k_links: deflate_fast's links below snap_end
     if (fast) {
-        if (s->res_pos > base && !fh.dict) {                   // rebase the saved chains to this buffer
-            head_in.resize(s->fast_head.size());
-            for (size_t i = 0; i < head_in.size(); i++)
-                head_in[i] = s->fast_head[i] > base ? (uint32_t)(s->fast_head[i] - base) : 0;
-            fh.head_in = head_in.data();
-            fh.prev_in = s->fast_prev.data();
-            fh.prev_n = s->fast_prev.size();
-        }
         fh.snap_head = &s->snap_head;
         fh.snap_prev = &s->snap_prev;
     }
@@ -1914,6 +1953,9 @@ void choose_resume(internal_state *s) {
             for (size_t i = 0; i < s->snap_head.size(); i++)
                 s->fast_head[i] = s->snap_head[i] ? (uint64_t)s->snap_head[i] + b : 0;
             s->fast_prev.assign(s->snap_prev.begin(), s->snap_prev.end());
+            s->fast_at = s->res_pos;
+            s->fast_S = s->res_S;
+            s->fast_pend = it.kind == kItBlock ? 0u : (uint32_t)std::min<uint64_t>(s->res_pos - s->res_S, kMinMatch - 1);
         }
         if (s->res_S > s->in_base) {                 // the input before the window is not needed again
             s->in.erase(s->in.begin(), s->in.begin() + (std::ptrdiff_t)(s->res_S - s->in_base));
@@ -2040,6 +2082,7 @@ int deflate_stored_call(z_streamp strm, internal_state *s, int flush) {
     };
     uint64_t min_block = std::min(pbs - 5, w_size);
     const uint64_t used0 = strm->avail_in;
+    const Bytef *const in0 = strm->next_in;                     // this call's reads start here
     bool last = false;
     do {                                                        // deflate.c:1652-1725
         uint64_t len = kMaxStored;
@@ -2127,6 +2170,17 @@ int deflate_stored_call(z_streamp strm, internal_state *s, int flush) {
         s->res_byte = (uint32_t)fh.out[3];
     }
     s->in.assign(buf.begin() + (std::ptrdiff_t)bpos, buf.end());   // the window's unsent bytes
+    {   // the window: the last strstart bytes read (deflate.c:1733-1790 keep them contiguous)
+        const uint64_t rd = used0 - strm->avail_in, keep = (uint64_t)strstart;
+        if (rd >= keep) {
+            s->l0_hist.assign(in0 + (rd - keep), in0 + rd);
+        } else {
+            s->l0_hist.insert(s->l0_hist.end(), in0, in0 + rd);
+            if (s->l0_hist.size() > keep) s->l0_hist.erase(s->l0_hist.begin(), s->l0_hist.end() - (std::ptrdiff_t)keep);
+        }
+        s->l0_pos += rd;
+        if (bstate == 1 && flush == Z_FULL_FLUSH) s->l0_hist.clear(), s->l0_pos = 0;   // a new part
+    }
     if (s->wrap) strm->adler = s->check;
     drain(strm, s);
     if (bstate == 1 && flush == Z_FULL_FLUSH) s->part_out = 0, s->res_bits = 0;   // a new part: byte aligned
@@ -2564,6 +2618,47 @@ int deflateTune(z_streamp strm, int good_length, int max_lazy, int nice_length, 
     }
 }
 
+// Level 0 <-> a searching level after deflateParams' Z_BLOCK flush (everything
+// given so far is out).  deflate_stored keeps the window (its last strstart
+// bytes) and s->insert (deflate.c:1733-1760); the function after it hashes
+// those strings in fill_window (deflate.c:318-335) and searches the window, so
+// the part goes on with the window as its history.  The other way, deflate_stored
+// starts with strstart = block_start at the window position of the flush.
+void enter_stored(internal_state *s) {
+    const size_t X = s->in_base + s->in.size();                 // == s->rd after the flush
+    s->st_strstart = s->st_block_start = (int64_t)(X - s->res_S);
+    s->l0_hist.assign(s->in.begin() + (std::ptrdiff_t)(s->res_S - s->in_base), s->in.end());
+    s->l0_pos = X;
+    s->in.clear();                                              // the window's unsent bytes: none
+}
+
+void leave_stored(internal_state *s) {
+    const size_t X = (size_t)s->l0_pos, S = X - s->l0_hist.size();
+    s->in.assign(s->l0_hist.begin(), s->l0_hist.end());
+    s->in_base = s->res_S = S;
+    s->res_pos = s->rd = s->rd_seen = s->flush_done = s->ck_pos = X;
+    s->res_E = X;
+    s->res_cut = 0;                                             // s->insert strings wait for the next fill
+    s->res_ev = 0;
+    s->ev_pos.clear();
+    s->ev_type.clear();
+    s->ev_aux.clear();
+    s->evb.clear();
+    s->job_ev = 0;
+    s->ev_done = 0;
+    s->items.clear();
+    s->t = 0;
+    s->res_item = -1;
+    s->stale = true;
+    s->tentative = false;
+    s->job_closed = false;
+    s->proc_bits = s->res_bits;
+    s->body.clear();
+    s->body_at = 0;
+    s->cfg_pos.clear();
+    s->cfg_row.clear();
+}
+
 // deflateParams (deflate.c:760-803): flushes with Z_BLOCK when the level's
 // function or the strategy changes and deflate() has run, then switches; a
 // level change within the same function takes effect at the next decision.
@@ -2576,8 +2671,8 @@ int deflateParams(z_streamp strm, int level, int strategy) {
     if (started && !s->finished) {
         const bool own_fn = strategy == Z_HUFFMAN_ONLY || strategy == Z_RLE ||
                             s->strategy == Z_HUFFMAN_ONLY || s->strategy == Z_RLE;
-        if (deflate_fn(level) != deflate_fn(s->level) || (strategy != s->strategy && own_fn))
-            return unsupported(strm, "deflateParams: this switch after data is not modelled");
+        if (strategy != s->strategy && own_fn && level != 0 && s->level != 0)
+            return unsupported(strm, "deflateParams: a switch to or from Z_HUFFMAN_ONLY / Z_RLE after data is not modelled");
     }
     if ((strategy != s->strategy || deflate_fn(level) != deflate_fn(s->level)) && started) {
         const int err = deflate(strm, Z_BLOCK);
@@ -2585,6 +2680,10 @@ int deflateParams(z_streamp strm, int level, int strategy) {
         if (strm->avail_in || pending_input(s)) return Z_BUF_ERROR;
     }
     try {
+        if (started && !s->finished && (level == 0) != (s->level == 0)) {
+            if (level == 0) enter_stored(s);
+            else leave_stored(s);
+        }
         if (s->level != level) {
             const LevelCfg before = s->tuned ? s->tune : kLevelCfg[s->level];
             s->level = level;

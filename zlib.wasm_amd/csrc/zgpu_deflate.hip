@@ -230,8 +230,17 @@ __global__ __launch_bounds__(kLThreads) void k_links(DeflateJob job) {
     const WinP wp = job_win(job);
 
     for (int i = tid; i < kH; i += kLThreads) head[i] = 32768;   // "position -32768"
+    const int64_t lk_n = job.lk_head ? (int64_t)job.lk_n : 0;
     for (int64_t c0 = 0; c0 < n; c0 += kC) {
         __syncthreads();
+        if (c0 + kC <= lk_n) continue;                       // links as uploaded (deflate_fast's chains)
+        if (c0 <= lk_n && job.lk_head) {                     // the chains at lk_n: head[] of the uploaded state
+            for (int i = tid; i < kH; i += kLThreads) {
+                const int64_t q = (int64_t)job.lk_head[i];
+                head[i] = (uint16_t)(q != 0 && c0 - q < 32768 ? q & 0xffff : (c0 - 32768) & 0xffff);
+            }
+            __syncthreads();
+        }
         if ((c0 & 32767) == 0 && c0 > 0) {                   // slide sweep (slide_hash analogue)
             const uint32_t now = (uint32_t)c0;
             for (int i = tid; i < kH; i += kLThreads) {
@@ -243,12 +252,16 @@ __global__ __launch_bounds__(kLThreads) void k_links(DeflateJob job) {
         __syncthreads();
         const int cnt = (int)((n - c0) < kC ? (n - c0) : kC);            // positions in the chunk
         const int m = (int)((n - 2 - c0) < kC ? ((n - 2 - c0) > 0 ? n - 2 - c0 : 0) : kC);   // p <= n-3
-        for (int e = tid; e < m; e += kLThreads)
-            ka[e] = hashp(stage[e], stage[e + 1], stage[e + 2], wp) << 13 | (uint32_t)e;
-        links_radix_pass(ka, kb, m, 13, wcnt, wsum, tid);
-        links_radix_pass(kb, ka, m, 21, wcnt, wsum, tid);
+        // positions below lk_n keep their uploaded links and are not inserted
+        // again: only the chunk's positions from e0 on are keyed and sorted
+        const int e0 = lk_n > c0 ? (int)(lk_n - c0) : 0;
+        const int ms = m > e0 ? m - e0 : 0;
+        for (int e = e0 + tid; e < m; e += kLThreads)
+            ka[e - e0] = hashp(stage[e], stage[e + 1], stage[e + 2], wp) << 13 | (uint32_t)e;
+        links_radix_pass(ka, kb, ms, 13, wcnt, wsum, tid);
+        links_radix_pass(kb, ka, ms, 21, wcnt, wsum, tid);
         // sorted: ka[i] = hash << 13 | e, hashes ascending, e ascending within a hash
-        for (int i = tid; i < m; i += kLThreads) {
+        for (int i = tid; i < ms; i += kLThreads) {
             const uint32_t key = ka[i];
             const uint32_t h = key >> 13, e = key & (kLC - 1);
             const uint32_t p = (uint32_t)c0 + e;
@@ -258,12 +271,12 @@ __global__ __launch_bounds__(kLThreads) void k_links(DeflateJob job) {
             kb[e] = (d != 0 && d <= 32767u && d != p) ? d : 0u;               // position 0 is NIL
         }
         __syncthreads();
-        for (int i = tid; i < m; i += kLThreads) {
+        for (int i = tid; i < ms; i += kLThreads) {
             const uint32_t key = ka[i];
-            if (i == m - 1 || (ka[i + 1] >> 13) != (key >> 13))
+            if (i == ms - 1 || (ka[i + 1] >> 13) != (key >> 13))
                 head[key >> 13] = (uint16_t)(((uint32_t)c0 + (key & (kLC - 1))) & 0xffffu);
         }
-        for (int e = tid; e < cnt; e += kLThreads) out[c0 + e] = e < m ? (uint16_t)kb[e] : (uint16_t)0;
+        for (int e = tid + e0; e < cnt; e += kLThreads) out[c0 + e] = e < m ? (uint16_t)kb[e] : (uint16_t)0;
     }
 }
 
@@ -1752,7 +1765,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     uint32_t ci = 0;                                     // configuration changes acted on
     // a resumed flush job (start > 0) finds head[] and prev[] as the last job
     // left them, rebased to its buffer (zgpu_api.cpp deflate_part)
-    if (!kEv || job.start == 0 || job.dict)
+    if (!kEv || job.start == 0 || (job.dict && !job.keep_head))
         for (int i = lane; i < (int)hsize; i += 64) head[i] = 0;
     __threadfence_block();
     __syncthreads();
@@ -1856,8 +1869,8 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         return maxcmp;
     };
 
-    if (kEv && job.dict)                                  // a preset dictionary's strings
-        for (P q = 0; q < (P)job.pre_ins; q++) {
+    if (kEv && job.dict)                                  // a preset dictionary's strings, or a window
+        for (P q = (P)job.pre_from; q < (P)job.pre_ins; q++) {   // parsed by a function that inserts all
             wsee(q);
             insert(q);
         }

@@ -195,6 +195,18 @@ struct DeflateJob {
     const LevelCfg *cfg_tab;
     uint32_t ncfg;
     int cfg_q;               // some row of cfg_tab has good < lazy: k_match computes rquart
+    // a streaming job whose window was (partly) parsed by deflate_fast, which
+    // inserts selectively (deflate.c:1873-1897), while this job's function
+    // inserts every position (deflateParams switched it after a Z_BLOCK flush):
+    //  k_links: positions [0, lk_n) keep the links already in `link` (the
+    //           deflate_fast chains, uploaded), the chunk holding lk_n starts
+    //           from lk_head[hash] (buffer positions, 0 none) instead of empty;
+    //  k_parse_fast (keep_head): head[] and prev[] as uploaded, then positions
+    //           [pre_from, pre_ins) inserted in order before the parse starts
+    uint32_t lk_n;
+    const uint32_t *lk_head;
+    uint32_t pre_from;
+    int keep_head;
 };
 
 // the per-job window/hash parameters (deflate.c:440-455)
