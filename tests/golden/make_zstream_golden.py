@@ -242,6 +242,36 @@ def sessions_r3():
         ["deflate", part(text, 20000, 20100), 0], ["params", 6, 0], ["deflate", part(text, 20100, 21000), 0],
         ["params", 2, 0], ["deflate", part(text, 21000, 21500), 0], ["params", 7, 0],
         ["deflate", part(text, 21500, 150000), 4]]})
+    # deflateSetDictionary on a raw stream after a flush (lookahead 0), at level 0
+    # (deflate_stored keeps no lookahead: any time, unsent window bytes dropped),
+    # and a zlib stream's dictionary at level 0 (deflate.c:550-613)
+    d_small = ["gen", "text", 300, 31]
+    d_mid = ["gen", "text", 9000, 32]
+    d_big = ["gen", "text", 50000, 34]
+    for lv in (1, 2, 6, 9):
+        for d in (d_small, d_mid, d_big):
+            S.append({"name": f"dict-raw-after-flush-L{lv}-{d[2]}", "ops": [
+                ["init", lv, -15, 8, 0], ["deflate", part(text, 0, 60000), 2], ["dict", d],
+                ["deflate", part(text, 60000, 150000), 4]]})
+    S.append({"name": "dict-raw-after-noflush-refused", "ops": [
+        ["init", 6, -15, 8, 0], ["deflate", part(text, 0, 60000), 0], ["dict", d_mid],
+        ["deflate", part(text, 60000, 150000), 4]]})
+    S.append({"name": "dict-raw-twice-flushes", "ops": [
+        ["init", 4, -15, 8, 0], ["dict", d_mid], ["deflate", part(mix, 0, 50000), 3], ["dict", d_small],
+        ["deflate", part(mix, 50000, 120000), 5], ["dict", d_big], ["deflate", part(mix, 120000, 200000), 4]]})
+    for wb in (15, -15, -10):
+        for d in (d_small, d_big):
+            S.append({"name": f"dict-L0-w{wb}-{d[2]}", "ops": [
+                ["init", 0, wb, 8, 0], ["dict", d], ["deflate", text, 4]]})
+    S.append({"name": "dict-L0-raw-midstream", "ops": [
+        ["init", 0, -15, 8, 0], ["deflate", part(text, 0, 70000), 0, 5000], ["dict", d_mid],
+        ["deflate", part(text, 70000, 150000), 4, 5000]]})
+    S.append({"name": "dict-L0-then-L6", "ops": [
+        ["init", 0, -15, 8, 0], ["deflate", part(text, 0, 30000), 2], ["dict", d_mid], ["params", 6, 0],
+        ["deflate", part(text, 30000, 150000), 4]]})
+    S.append({"name": "dict-L1-then-L0-dict-L1", "ops": [
+        ["init", 1, -15, 8, 0], ["deflate", part(text, 0, 30000), 0], ["params", 0, 0], ["dict", d_small],
+        ["deflate", part(text, 30000, 40000), 5], ["params", 1, 0], ["deflate", part(text, 40000, 150000), 4]]})
     # strategy changes within deflate_slow / deflate_fast
     for a, sa, sb in ((6, 0, 1), (6, 1, 4), (4, 4, 0), (2, 0, 1), (1, 4, 0)):
         S.append({"name": f"strategy-{a}-{sa}-{sb}", "ops": [

@@ -2530,38 +2530,84 @@ int unsupported(z_streamp strm, const char *why) {
 int deflate_fn(int level) { return level == 0 ? 0 : level <= 3 ? 1 : 2; }   // stored, fast, slow
 }  // namespace
 
-// deflateSetDictionary (deflate.c): the dictionary (its last w_size bytes)
-// becomes the window the first part is compressed against: the part's buffer
-// starts with it and the parse at its end; a zlib stream's header carries
-// FDICT and its Adler-32.  Before the first deflate() call only (the zlib
-// wrapper's own rule; raw streams mid-stream are not modelled), not at level 0.
+// deflateSetDictionary (deflate.c:550-613).  Accepted on a zlib stream
+// before its first deflate() call and on a raw stream whenever the window holds
+// no unprocessed input (lookahead == 0: before any data, after a flush, and at
+// level 0, which keeps no lookahead).  The dictionary (its last w_size bytes; a
+// raw stream's longer dictionary replaces the history, strings and all) goes
+// into the window as if it were input that is never sent: every string of it is
+// hashed but the last two, which wait as s->insert, and block_start moves past
+// it (so a level-0 stream's unsent window bytes are dropped, as the reference's
+// are).  Here the part's input gets the bytes and the resume point moves to
+// their end; at level 0 deflate_stored's window offsets move as fill_window
+// moves them.  A zlib stream's header then carries FDICT and the DICTID.
 int deflateSetDictionary(z_streamp strm, const Bytef *dictionary, uInt dictLength) {
     if (!strm || !strm->state || strm->state->inflating || !dictionary) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
     if (s->wrap == 2 || (s->wrap == 1 && s->last_flush != -2)) return Z_STREAM_ERROR;
-    if (s->last_flush != -2) return unsupported(strm, "deflateSetDictionary: only before the first deflate()");
-    if (s->level == 0) return unsupported(strm, "deflateSetDictionary: level 0 not supported");
+    if (s->level != 0 && pending_input(s)) return Z_STREAM_ERROR;        // s->lookahead != 0
+    if (s->finished) return unsupported(strm, "deflateSetDictionary: the stream has ended");
     try {
         if (s->wrap == 1) strm->adler = adler32_z(strm->adler, dictionary, dictLength);
-        const size_t wsize = size_t(1) << s->wbits;
-        if (dictLength == 0) return Z_OK;
-        if (dictLength >= wsize) {                 // the tail replaces the history
-            if (s->wrap == 1 && !s->in.empty())
-                return unsupported(strm, "deflateSetDictionary: a second dictionary beyond the window size");
-            s->in.assign(dictionary + (dictLength - wsize), dictionary + dictLength);
-        } else {
-            if (s->in.size() + dictLength > wsize)
-                return unsupported(strm, "deflateSetDictionary: dictionaries beyond the window size");
-            s->in.insert(s->in.end(), dictionary, dictionary + dictLength);
+        const uint64_t wsize = uint64_t(1) << s->wbits;
+        bool reset = false;
+        if (dictLength >= wsize) {                      // the tail replaces the history
+            reset = s->wrap == 0;                       // a zlib stream's window is empty anyway
+            dictionary += dictLength - wsize;
+            dictLength = (uInt)wsize;
         }
-        s->in_base = 0;
-        s->res_S = 0;
-        s->res_pos = s->ck_pos = s->in.size();
-        s->rd = s->rd_seen = s->flush_done = s->in.size();
-        s->res_ev = 0;
-        s->flushed = true;                 // the part path (bit and parse offsets)
-        s->dict_set = s->wrap == 1;
-        s->dict_id = (uint32_t)strm->adler;
+        if (s->wrap == 1 && dictLength) {               // strstart != 0: FDICT + DICTID (deflate.c:1027-1036)
+            s->dict_set = true;
+            s->dict_id = (uint32_t)strm->adler;
+        }
+        if (s->level == 0) {
+            // deflate_stored's window: fill_window's reads and slides as the
+            // reference's deflateSetDictionary drives them (deflate.c:582-605)
+            int64_t ss = reset ? 0 : s->st_strstart, bs = reset ? 0 : s->st_block_start;
+            const int64_t W = (int64_t)wsize, maxd = W - kMinLookahead;
+            uint64_t look = 0, avail = dictLength;
+            auto fill = [&] {
+                do {
+                    if (ss >= W + maxd) { ss -= W; bs -= W; }
+                    const uint64_t more = (uint64_t)(2 * W - (int64_t)look - ss), take = std::min(avail, more);
+                    avail -= take;
+                    look += take;
+                } while (look < (uint64_t)kMinLookahead && avail != 0);
+            };
+            fill();
+            while (look >= (uint64_t)kMinMatch) {
+                ss += (int64_t)look - (kMinMatch - 1);
+                look = kMinMatch - 1;
+                fill();
+            }
+            ss += (int64_t)look;
+            s->st_strstart = s->st_block_start = ss;
+            (void)bs;
+            if (reset) s->l0_hist.clear();
+            s->l0_hist.insert(s->l0_hist.end(), dictionary, dictionary + dictLength);
+            if (s->l0_hist.size() > (uint64_t)ss)
+                s->l0_hist.erase(s->l0_hist.begin(), s->l0_hist.end() - (std::ptrdiff_t)ss);
+            s->l0_pos += dictLength;
+            s->in.clear();                              // block_start = strstart: unsent bytes dropped
+            return Z_OK;
+        }
+        if (dictLength == 0) return Z_OK;
+        const size_t X = s->in_base + s->in.size();     // the part position everything is processed to
+        if (reset) {                                    // CLEAR_HASH, strstart = block_start = 0
+            s->in.clear();
+            s->in_base = s->res_S = X;
+        }
+        s->in.insert(s->in.end(), dictionary, dictionary + dictLength);
+        s->res_pos = s->rd = s->rd_seen = s->flush_done = s->ck_pos = X + dictLength;
+        s->res_E = X + dictLength;
+        s->res_cut = 0;                                 // the last two strings wait as s->insert
+        s->res_ev = s->ev_pos.size();
+        s->ev_done = s->ev_type.size();
+        s->items.clear();
+        s->t = 0;
+        s->res_item = -1;
+        s->stale = true;
+        s->flushed = true;                              // the part path (bit and parse offsets)
         return Z_OK;
     } catch (const std::bad_alloc &) {
         return Z_MEM_ERROR;
