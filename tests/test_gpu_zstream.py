@@ -42,6 +42,8 @@ def test_zstream_sessions_vs_reference(zg, zs_golden):
             for op, g, w in zip(sess["ops"], rcs, sess["rcs"]))
         if not ok or len(z) != sess["len"] or hashlib.sha256(z).hexdigest() != sess["sha256"]:
             bad.append((sess["name"], rcs, sess["rcs"], len(z), sess["len"]))
+    if bad:
+        print("BAD SESSIONS:", [b[0] for b in bad])
     assert not bad, ([b[0] for b in bad], bad[:3])
 
 

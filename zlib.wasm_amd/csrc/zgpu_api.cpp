@@ -416,6 +416,7 @@ struct FlushSpec {
     // a window parsed partly by deflate_fast (DeflateJob::lk_n, pre_from, keep_head)
     uint32_t lk_n = 0, pre_from = 0;
     int keep_head = 0;
+    int zp0 = kMinMatch - 1, zm0 = kMinMatch - 1;   // DeflateJob::zp0 / zm0
 };
 
 // deflateInit2_'s windowBits / memLevel rules (deflate.c:400-425): negative
@@ -439,6 +440,14 @@ int parse_window(int windowBits, int memLevel, int *wrap, int *wbits) {
 
 // wbits 9..15 (deflateInit2_'s windowBits with 8 already made 9), mem_level
 // 1..9 (hash_bits = mem_level + 7, lit_bufsize = 1 << (mem_level + 6))
+// a failed device step of a deflate launch (ZGPU_STREAM_TRACE names its line)
+static int zfail(int line) {
+    static const bool on = std::getenv("ZGPU_STREAM_TRACE") != nullptr;
+    if (on) std::fprintf(stderr, "deflate_dev_locked: failed at zgpu_api.cpp:%d (%s)\n", line,
+                         hipGetErrorString(hipGetLastError()));
+    return ZGPU_MEM_ERROR;
+}
+
 int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
                        uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
                        uint64_t *dst_len, int32_t *status, uint32_t count, int level, int wrap,
@@ -456,7 +465,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     std::vector<uint64_t> lens(count);
     if (hipMemcpyAsync(lens.data(), src_len, 8ull * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
-        return ZGPU_MEM_ERROR;
+        return zfail(__LINE__);
     for (uint32_t i = 0; i < count; i++)
         if (lens[i] >= kMaxBuffer) return ZGPU_STREAM_ERROR;   // 32-bit positions in the kernels
 
@@ -501,36 +510,36 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     const size_t nsub = cuts.size() - 1;
     static const bool no_pipe = std::getenv("ZGPU_NO_PIPELINE") != nullptr;
     const bool piped = slow && nsub > 1 && !no_pipe;
-    if (!c.ws_meta.ensure(16ull * count + 8ull * max_cnt * 2)) return ZGPU_MEM_ERROR;
+    if (!c.ws_meta.ensure(16ull * count + 8ull * max_cnt * 2)) return zfail(__LINE__);
     const size_t ckb = checksum_scratch_bytes(max_cnt);     // trailer checksums of few large buffers
     void *ck = ckb && c.ws_ck.ensure(ckb) ? c.ws_ck.p : nullptr;
-    if (!c.ws_link.ensure(2 * max_pos + 64)) return ZGPU_MEM_ERROR;
-    if (!c.ws_sym.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
-    if (!c.ws_blk.ensure(sizeof(BlockRec) * max_blk)) return ZGPU_MEM_ERROR;
-    if ((slow || huff || rle) && !c.ws_rf.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
+    if (!c.ws_link.ensure(2 * max_pos + 64)) return zfail(__LINE__);
+    if (!c.ws_sym.ensure(4 * max_pos + 64)) return zfail(__LINE__);
+    if (!c.ws_blk.ensure(sizeof(BlockRec) * max_blk)) return zfail(__LINE__);
+    if ((slow || huff || rle) && !c.ws_rf.ensure(4 * max_pos + 64)) return zfail(__LINE__);
     // rquart: quarter-budget results (L5-9) and the lazy parse's symbol-start staging (L4-9)
-    if (slow && !c.ws_rq.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
-    if (slow && !c.ws_state.ensure(max_pos / 4 + 64)) return ZGPU_MEM_ERROR;
-    if (slow && !c.ws_key.ensure(max_pos + 64)) return ZGPU_MEM_ERROR;
-    if (slow && !c.ws_stg.ensure(4 * max_pos + 64)) return ZGPU_MEM_ERROR;
+    if (slow && !c.ws_rq.ensure(4 * max_pos + 64)) return zfail(__LINE__);
+    if (slow && !c.ws_state.ensure(max_pos / 4 + 64)) return zfail(__LINE__);
+    if (slow && !c.ws_key.ensure(max_pos + 64)) return zfail(__LINE__);
+    if (slow && !c.ws_stg.ensure(4 * max_pos + 64)) return zfail(__LINE__);
     if (piped) {
-        if (!c.ws_key2.ensure(max_pos + 64)) return ZGPU_MEM_ERROR;
+        if (!c.ws_key2.ensure(max_pos + 64)) return zfail(__LINE__);
         if (!c.ws_link2.ensure(2 * max_pos + 64) || !c.ws_rf2.ensure(4 * max_pos + 64) ||
             !c.ws_rq2.ensure(4 * max_pos + 64) || !c.ws_state2.ensure(max_pos / 4 + 64))
-            return ZGPU_MEM_ERROR;
+            return zfail(__LINE__);
         if (!c.aux && hipStreamCreateWithFlags(&c.aux, hipStreamNonBlocking) != hipSuccess) {
             c.aux = nullptr;
-            return ZGPU_MEM_ERROR;
+            return zfail(__LINE__);
         }
         for (int k = 0; k < 2; k++) {
             if (!c.ev_links[k] && hipEventCreateWithFlags(&c.ev_links[k], hipEventDisableTiming) != hipSuccess)
-                return ZGPU_MEM_ERROR;
+                return zfail(__LINE__);
             if (!c.ev_match[k] && hipEventCreateWithFlags(&c.ev_match[k], hipEventDisableTiming) != hipSuccess)
-                return ZGPU_MEM_ERROR;
+                return zfail(__LINE__);
         }
     }
     if (level >= 1 && level <= 3 && !huff && !rle && !c.ws_heads.ensure(4ull * hsize * max_cnt))
-        return ZGPU_MEM_ERROR;
+        return zfail(__LINE__);
     // k_match per segment where a sub-batch has too few buffers to fill the GPU
     // one workgroup per buffer (a single zlib.h buffer, say).  The segment is
     // the sub-batch's bytes over the 256 CUs, in whole 4 KiB tiles, at most
@@ -559,12 +568,12 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     if (!segs.empty() && (!c.ws_seg.ensure(4 * segs.size()) ||
                           hipMemcpyAsync(c.ws_seg.p, segs.data(), 4 * segs.size(), hipMemcpyHostToDevice, st) !=
                               hipSuccess))
-        return ZGPU_MEM_ERROR;
+        return zfail(__LINE__);
     uint64_t *d_meta = c.ws_meta.as<uint64_t>();
     uint32_t *d_nblk = reinterpret_cast<uint32_t *>(d_meta + 2ull * count);
     uint32_t *d_check = d_nblk + max_cnt;
     if (hipMemcpyAsync(d_meta, meta.data(), 16ull * count, hipMemcpyHostToDevice, st) != hipSuccess)
-        return ZGPU_MEM_ERROR;
+        return zfail(__LINE__);
     // ZGPU_POISON (debug): fill every workspace with a per-call byte pattern so
     // a kernel that reads a word it did not write shows up as a mismatch
     static const bool poison = std::getenv("ZGPU_POISON") != nullptr;
@@ -573,19 +582,19 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         const int v = 0x5a ^ (round++ * 0x3b);
         for (DevBuf *b : {&c.ws_link, &c.ws_sym, &c.ws_stg, &c.ws_blk, &c.ws_rf, &c.ws_rq, &c.ws_state, &c.ws_heads,
                           &c.ws_link2, &c.ws_rf2, &c.ws_rq2, &c.ws_state2})
-            if (b->p && hipMemsetAsync(b->p, v & 0xff, b->cap, st) != hipSuccess) return ZGPU_MEM_ERROR;
-        if (hipMemsetAsync(d_nblk, v & 0xff, 8ull * max_cnt, st) != hipSuccess) return ZGPU_MEM_ERROR;
+            if (b->p && hipMemsetAsync(b->p, v & 0xff, b->cap, st) != hipSuccess) return zfail(__LINE__);
+        if (hipMemsetAsync(d_nblk, v & 0xff, 8ull * max_cnt, st) != hipSuccess) return zfail(__LINE__);
     }
     if (fs && fs->plan &&
         (hipMemcpyAsync(c.ws_blk.p, fs->plan, sizeof(BlockRec) * fs->nplan, hipMemcpyHostToDevice, st) != hipSuccess ||
          hipMemcpyAsync(d_nblk, &fs->nplan, 4, hipMemcpyHostToDevice, st) != hipSuccess))
-        return ZGPU_MEM_ERROR;
+        return zfail(__LINE__);
     if (fs && fs->head_in) {
         if (!c.ws_heads.ensure(4ull * hsize) ||
             hipMemcpyAsync(c.ws_heads.p, fs->head_in, 4ull * hsize, hipMemcpyHostToDevice, st) != hipSuccess ||
             (fs->prev_n && hipMemcpyAsync(c.ws_link.p, fs->prev_in, 2ull * fs->prev_n, hipMemcpyHostToDevice, st) !=
                                hipSuccess))
-            return ZGPU_MEM_ERROR;
+            return zfail(__LINE__);
     }
 
     StageTimer &T = c.timer;
@@ -645,6 +654,8 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.cfg_q = fs->cfg_q;
             job.pre_from = fs->pre_from;
             job.keep_head = fs->keep_head;
+            job.zp0 = fs->zp0;
+            job.zm0 = fs->zm0;
             if (slow && fs->head_in) {                  // k_links resumes deflate_fast's chains
                 job.lk_n = fs->lk_n;
                 job.lk_head = c.ws_heads.as<uint32_t>();
@@ -660,25 +671,25 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             rc = T.run(0, st, [&] { return launch_adler32(src, src_off + a, src_len + a, nullptr, d_check, b - a, ck, ckb, st); });
         else if (wrap == 2)
             rc = T.run(0, st, [&] { return launch_crc32(src, src_off + a, src_len + a, nullptr, d_check, b - a, ck, ckb, st); });
-        if (rc) return ZGPU_MEM_ERROR;
+        if (rc) return zfail(__LINE__);
         if ((huff || rle) && fs) {
-            if (T.run(4, st, [&] { return launch_deflate_stage(10, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+            if (T.run(4, st, [&] { return launch_deflate_stage(10, job, nullptr, st); })) return zfail(__LINE__);
         } else if (huff) {
-            if (T.run(4, st, [&] { return launch_deflate_stage(7, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+            if (T.run(4, st, [&] { return launch_deflate_stage(7, job, nullptr, st); })) return zfail(__LINE__);
         } else if (rle) {
-            if (T.run(4, st, [&] { return launch_deflate_stage(8, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+            if (T.run(4, st, [&] { return launch_deflate_stage(8, job, nullptr, st); })) return zfail(__LINE__);
         } else if (level >= 4 && fs) {
             // flush jobs: the sequential lazy parse (the segmented one assumes
             // the input is all there)
-            if (T.run(3, st, [&] { return launch_deflate_stage(2, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+            if (T.run(3, st, [&] { return launch_deflate_stage(2, job, nullptr, st); })) return zfail(__LINE__);
         } else if (level >= 4) {
-            if (T.run(3, st, [&] { return launch_deflate_stage(5, job, nullptr, st); })) return ZGPU_MEM_ERROR;
-            if (T.run(3, st, [&] { return launch_deflate_stage(6, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+            if (T.run(3, st, [&] { return launch_deflate_stage(5, job, nullptr, st); })) return zfail(__LINE__);
+            if (T.run(3, st, [&] { return launch_deflate_stage(6, job, nullptr, st); })) return zfail(__LINE__);
         } else if (level >= 1) {
             uint32_t *heads = c.ws_heads.as<uint32_t>();
-            if (T.run(4, st, [&] { return launch_deflate_stage(3, job, heads, st); })) return ZGPU_MEM_ERROR;
+            if (T.run(4, st, [&] { return launch_deflate_stage(3, job, heads, st); })) return zfail(__LINE__);
         }
-        if (T.run(5, st, [&] { return launch_deflate_stage(4, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+        if (T.run(5, st, [&] { return launch_deflate_stage(4, job, nullptr, st); })) return zfail(__LINE__);
         return ZGPU_OK;
     };
 
@@ -686,8 +697,8 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         for (size_t s = 0; s < nsub; s++) {
             const DeflateJob job = make_job(s);
             if (slow) {
-                if (T.run(1, st, [&] { return launch_deflate_stage(0, job, nullptr, st); })) return ZGPU_MEM_ERROR;
-                if (T.run(2, st, [&] { return launch_deflate_stage(1, job, nullptr, st); })) return ZGPU_MEM_ERROR;
+                if (T.run(1, st, [&] { return launch_deflate_stage(0, job, nullptr, st); })) return zfail(__LINE__);
+                if (T.run(2, st, [&] { return launch_deflate_stage(1, job, nullptr, st); })) return zfail(__LINE__);
             }
             if (int rc = tail(s, job)) return rc;
         }
@@ -700,21 +711,24 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         hipStream_t ax = c.aux;
         auto links = [&](size_t s) -> int {
             const DeflateJob job = make_job(s);
-            if (T.run(1, st, [&] { return launch_deflate_stage(0, job, nullptr, st); })) return ZGPU_MEM_ERROR;
-            if (hipEventRecord(c.ev_links[s & 1], st) != hipSuccess) return ZGPU_MEM_ERROR;
-            if (hipStreamWaitEvent(ax, c.ev_links[s & 1], 0) != hipSuccess) return ZGPU_MEM_ERROR;
-            if (T.run(2, ax, [&] { return launch_deflate_stage(1, job, nullptr, ax); })) return ZGPU_MEM_ERROR;
-            if (hipEventRecord(c.ev_match[s & 1], ax) != hipSuccess) return ZGPU_MEM_ERROR;
+            if (T.run(1, st, [&] { return launch_deflate_stage(0, job, nullptr, st); })) return zfail(__LINE__);
+            if (hipEventRecord(c.ev_links[s & 1], st) != hipSuccess) return zfail(__LINE__);
+            if (hipStreamWaitEvent(ax, c.ev_links[s & 1], 0) != hipSuccess) return zfail(__LINE__);
+            if (T.run(2, ax, [&] { return launch_deflate_stage(1, job, nullptr, ax); })) return zfail(__LINE__);
+            if (hipEventRecord(c.ev_match[s & 1], ax) != hipSuccess) return zfail(__LINE__);
             return ZGPU_OK;
         };
         if (int rc = links(0)) return rc;
         for (size_t s = 0; s < nsub; s++) {
             if (s + 1 < nsub) if (int rc = links(s + 1)) return rc;
-            if (hipStreamWaitEvent(st, c.ev_match[s & 1], 0) != hipSuccess) return ZGPU_MEM_ERROR;
+            if (hipStreamWaitEvent(st, c.ev_match[s & 1], 0) != hipSuccess) return zfail(__LINE__);
             if (int rc = tail(s, make_job(s))) return rc;
         }
     }
-    int rc = hip_ok(hipStreamSynchronize(st));
+    const hipError_t se = hipStreamSynchronize(st);
+    int rc = hip_ok(se);
+    if (rc) { static const bool on = std::getenv("ZGPU_STREAM_TRACE") != nullptr;
+              if (on) std::fprintf(stderr, "deflate_dev_locked: sync %s\n", hipGetErrorString(se)); }
     if (piped && rc == ZGPU_OK) rc = hip_ok(hipStreamSynchronize(c.aux));
     c.timer.collect();
     return rc;
@@ -728,7 +742,7 @@ struct FlushHost {
     uint32_t n;
     int open_end;
     uint32_t start, bit0, byte0;   // in: a resumed job (see DeflateJob)
-    uint64_t out[4];               // out: DeflateJob::flush_out
+    uint64_t out[8];               // out: DeflateJob::flush_out
     // levels 1..3 (see FlushSpec): the chains the job starts from, and where
     // it leaves them: head[32768] and the prev links of [S, last flush), S = out[2]
     const uint32_t *head_in = nullptr;
@@ -759,6 +773,7 @@ struct FlushHost {
     // a window parsed partly by deflate_fast: see FlushSpec
     uint32_t lk_n = 0, pre_from = 0;
     int keep_head = 0;
+    int zp0 = kMinMatch - 1, zm0 = kMinMatch - 1;   // DeflateJob::zp0 / zm0
 };
 
 // debug trace of the streaming deflate() engine (ZGPU_STREAM_TRACE)
@@ -781,7 +796,7 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
         dcap[i] = dst_len[i];
         out_total += (dst_len[i] + 15) & ~15ull;
     }
-    const size_t ev_bytes = fh ? 32ull * fh->n + 160 + (8 + sizeof(LevelCfg)) * fh->ncfg + 16 : 0;
+    const size_t ev_bytes = fh ? 32ull * fh->n + 192 + (8 + sizeof(LevelCfg)) * fh->ncfg + 16 : 0;
     const size_t meta_bytes = 8 * 4 * count + 16 * count + ev_bytes;
     if (!c.ws_io.ensure(in_total + 64) || !c.ws_io2.ensure(out_total + 64) ||
         !c.ws_small.ensure(meta_bytes + 64))
@@ -815,12 +830,12 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
                       hipMemcpyAsync(d_ft, fh->type, 4ull * fh->n, hipMemcpyHostToDevice, st) != hipSuccess))
             return ZGPU_MEM_ERROR;
         uint64_t *d_mb = d_fp + fh->n + (fh->n + 1) / 2;
-        if (hipMemsetAsync(d_mb, 0, 32, st) != hipSuccess) return ZGPU_MEM_ERROR;
+        if (hipMemsetAsync(d_mb, 0, 64, st) != hipSuccess) return ZGPU_MEM_ERROR;
         // k_match's clamps: the flush events only (not the Z_NO_FLUSH stops)
         std::vector<uint64_t> ml;
         for (uint32_t i = 0; i < fh->n; i++)
             if (fh->type[i] != 0 && fh->type[i] != kEvPause) ml.push_back(fh->pos[i]);
-        uint64_t *d_ml = d_mb + 4;
+        uint64_t *d_ml = d_mb + 8;
         uint64_t *d_aux = d_ml + fh->n;
         uint32_t *d_evb = reinterpret_cast<uint32_t *>(d_aux + fh->n);
         if (!ml.empty() && hipMemcpyAsync(d_ml, ml.data(), 8 * ml.size(), hipMemcpyHostToDevice, st) != hipSuccess)
@@ -847,6 +862,8 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
         fs.lk_n = fh->lk_n;
         fs.pre_from = fh->pre_from;
         fs.keep_head = fh->keep_head;
+        fs.zp0 = fh->zp0;
+        fs.zm0 = fh->zm0;
         if (fh->rec_out) {
             const size_t sym_limit = (size_t(1) << (mem_level + 6)) - 1;         // lit_bufsize - 1
             const size_t nrec = src_len[0] / sym_limit + 4 + 2ull * fh->n + fh->nplan;
@@ -866,7 +883,7 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
                                 level, wrap, strategy, st, fh ? &fs : nullptr, wbits, mem_level, tune);
     if (fh) ZTRACE("chl: ran rc %d\n", rc);
     if (rc) return rc;
-    if (fh && copy_sync(fh->out, fs.out, 32, hipMemcpyDeviceToHost, st) != hipSuccess)
+    if (fh && copy_sync(fh->out, fs.out, 64, hipMemcpyDeviceToHost, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
     if (fh && fh->rec_out) {
         uint32_t nb = 0;
@@ -1636,6 +1653,12 @@ struct internal_state {
     zvec<uint64_t> cfg_pos;
     std::vector<LevelCfg, ZAlloc<LevelCfg>> cfg_row;
     LevelCfg cfg0{};
+    // deflate_state's prev_length / match_length across a function switch
+    // (DeflateJob::zp0 / zm0): as the last job left them (exit_*), and as they
+    // stand at the last switch (zl_*, part position zl_pos; ~0: none in this part)
+    uint32_t exit_p = kMinMatch - 1, exit_m = kMinMatch - 1;
+    uint32_t zl_p = kMinMatch - 1, zl_m = kMinMatch - 1;
+    uint64_t zl_pos = ~0ull;
 };
 
 namespace {
@@ -1789,6 +1812,10 @@ int deflate_part(internal_state *s, bool closed) {
         if (fh.pre_ins < fh.pre_from) fh.pre_ins = fh.pre_from;
     }
     if (slow && have_fast && snap_end > 0) fh.lk_n = snap_end;   // k_links: deflate_fast's links below snap_end
+    // prev_length / match_length: the state a function switch left at its flush, else the clean one
+    const bool at_switch = s->res_pos == s->zl_pos;
+    fh.zp0 = fast ? (int)s->zl_p : (at_switch ? (int)s->zl_p : kMinMatch - 1);
+    fh.zm0 = at_switch ? (int)s->zl_m : kMinMatch - 1;
     if (fast) {
         fh.snap_head = &s->snap_head;
         fh.snap_prev = &s->snap_prev;
@@ -1807,6 +1834,8 @@ int deflate_part(internal_state *s, bool closed) {
     s->body.resize(cap);
     s->body_at = (size_t)(s->res_bits >> 3);
     s->job_base = base;
+    s->exit_p = (uint32_t)(fh.out[4] & 0xffffu);     // the parse's state after the job's last event
+    s->exit_m = (uint32_t)((fh.out[4] >> 16) & 0xffffu);
     s->snap_rec = fast ? fh.snap_rec : 0xffffffffu;
     // the timeline: records in order, each stop before the first record
     // flushed after it, each flush event's marker as its record
@@ -1922,6 +1951,7 @@ void close_part(internal_state *s) {
     s->body_at = 0;
     s->cfg_pos.clear();                 // the current row goes on (s->level, s->tune)
     s->cfg_row.clear();
+    s->zl_pos = ~0ull;                  // prev_length (zl_p) goes on: deflate_fast never resets it
 }
 
 // after a call: the latest item handed out that a new job can start at
@@ -2295,7 +2325,7 @@ int run_items(z_streamp strm, internal_state *s, uint32_t own, bool *full) {
 }  // namespace
 
 static void stream_trace(const char *where, z_streamp strm, const internal_state *s, int flush) {
-    static const bool on = std::getenv("ZGPU_STREAM_TRACE") != nullptr;   // debug
+    static const bool on = std::getenv("ZGPU_STREAM_TRACE") != nullptr;
     if (!on) return;
     std::fprintf(stderr, "[%s] flush %d in %u out %u total_in %lu rd %zu seen %zu C %zu in_base %zu ev %zu done %zu "
                  "items %zu t %zu res_item %ld res_S %zu res_pos %zu part_out %zu body_at %zu body %zu q %zu/%zu\n",
@@ -2556,6 +2586,8 @@ int deflateSetDictionary(z_streamp strm, const Bytef *dictionary, uInt dictLengt
             dictionary += dictLength - wsize;
             dictLength = (uInt)wsize;
         }
+        s->zl_p = s->zl_m = kMinMatch - 1;               // match_length = prev_length = MIN_MATCH-1
+        s->zl_pos = ~0ull;
         if (s->wrap == 1 && dictLength) {               // strstart != 0: FDICT + DICTID (deflate.c:1027-1036)
             s->dict_set = true;
             s->dict_id = (uint32_t)strm->adler;
@@ -2703,6 +2735,7 @@ void leave_stored(internal_state *s) {
     s->body_at = 0;
     s->cfg_pos.clear();
     s->cfg_row.clear();
+    s->zl_pos = X;                                              // deflate_stored kept prev/match_length
 }
 
 // deflateParams (deflate.c:760-803): flushes with Z_BLOCK when the level's
@@ -2726,6 +2759,14 @@ int deflateParams(z_streamp strm, int level, int strategy) {
         if (strm->avail_in || pending_input(s)) return Z_BUF_ERROR;
     }
     try {
+        if (started && !s->finished && deflate_fn(level) != deflate_fn(s->level)) {
+            // the parse state the next function inherits (deflate_slow rewrites
+            // prev_length at every decision, deflate_fast only match_length,
+            // deflate_stored neither)
+            if (s->level >= 4 && s->strategy != Z_HUFFMAN_ONLY && s->strategy != Z_RLE) s->zl_p = s->exit_p;
+            if (s->level != 0) s->zl_m = s->exit_m;
+            s->zl_pos = s->level != 0 ? s->res_pos : s->zl_pos;
+        }
         if (started && !s->finished && (level == 0) != (s->level == 0)) {
             if (level == 0) enter_stored(s);
             else leave_stored(s);

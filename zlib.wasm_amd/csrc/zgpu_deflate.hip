@@ -235,13 +235,15 @@ __global__ __launch_bounds__(kLThreads) void k_links(DeflateJob job) {
         __syncthreads();
         if (c0 + kC <= lk_n) continue;                       // links as uploaded (deflate_fast's chains)
         if (c0 <= lk_n && job.lk_head) {                     // the chains at lk_n: head[] of the uploaded state
+            // (entries may lie inside this chunk, below lk_n: no sweep here, the
+            // age test is this one)
+            const int hn = (int)wp.mask + 1;                 // hash_size entries were uploaded
             for (int i = tid; i < kH; i += kLThreads) {
-                const int64_t q = (int64_t)job.lk_head[i];
+                const int64_t q = i < hn ? (int64_t)job.lk_head[i] : 0;
                 head[i] = (uint16_t)(q != 0 && c0 - q < 32768 ? q & 0xffff : (c0 - 32768) & 0xffff);
             }
             __syncthreads();
-        }
-        if ((c0 & 32767) == 0 && c0 > 0) {                   // slide sweep (slide_hash analogue)
+        } else if ((c0 & 32767) == 0 && c0 > 0) {            // slide sweep (slide_hash analogue)
             const uint32_t now = (uint32_t)c0;
             for (int i = tid; i < kH; i += kLThreads) {
                 const uint32_t age = (now - head[i]) & 0xffffu;
@@ -447,10 +449,13 @@ __device__ __attribute__((always_inline)) inline void tile_store(uint32_t *E, co
     const int w0 = kMW + 4 * tid;
     uint4 v;
     if (kIdx) {
-        v.x = P.b[0] << 16 | (P.lk[0] ? (uint32_t)(w0 + 0) - P.lk[0] : 0u);
-        v.y = P.b[1] << 16 | (P.lk[1] ? (uint32_t)(w0 + 1) - P.lk[1] : 0u);
-        v.z = P.b[2] << 16 | (P.lk[2] ? (uint32_t)(w0 + 2) - P.lk[2] : 0u);
-        v.w = P.b[3] << 16 | (P.lk[3] ? (uint32_t)(w0 + 3) - P.lk[3] : 0u);
+        // masked to the low half: a position no chain reaches may carry any
+        // link (a deflate_fast window's uninserted positions keep stale prev[]
+        // entries), which must not spill into its bytes
+        v.x = P.b[0] << 16 | (P.lk[0] ? ((uint32_t)(w0 + 0) - P.lk[0]) & 0xffffu : 0u);
+        v.y = P.b[1] << 16 | (P.lk[1] ? ((uint32_t)(w0 + 1) - P.lk[1]) & 0xffffu : 0u);
+        v.z = P.b[2] << 16 | (P.lk[2] ? ((uint32_t)(w0 + 2) - P.lk[2]) & 0xffffu : 0u);
+        v.w = P.b[3] << 16 | (P.lk[3] ? ((uint32_t)(w0 + 3) - P.lk[3]) & 0xffffu : 0u);
     } else {
         v.x = P.b[0] << 16 | nil_link(P.lk[0]);
         v.y = P.b[1] << 16 | nil_link(P.lk[1]);
@@ -975,6 +980,51 @@ struct ParseU {                     // wave-uniform parse output state
     }
 };
 
+// longest_match (deflate.c:1356-1497) from best_len 0, over the buffer and its
+// links in global memory, wave-uniform: deflate_slow's searches right after a
+// function switch that left match_length 0 (DeflateJob::zm0).  With best_len 0
+// the quick reject compares match[-1] with scan[-1] (scan_end1) until a
+// candidate is taken; from then on it is the usual walk.  Returns the length
+// (0: nothing taken) clamped to the lookahead, *ms the match start; *searched
+// false when there is no valid chain head (deflate.c:1955).
+__device__ uint32_t walk_best0(const uint8_t *in, const uint16_t *lk, uint32_t p, uint32_t n, uint32_t lookahead,
+                               uint32_t S, uint32_t max_dist, const LevelCfg &cfg, uint32_t *ms, bool *searched,
+                               int lane) {
+    const uint32_t d0 = lk[p];
+    *searched = d0 != 0 && d0 <= max_dist;
+    if (!*searched) return kMinMatch - 1;
+    uint32_t chain = cfg.good == 0 ? cfg.chain >> 2 : cfg.chain;   // prev_length (0) >= good_match
+    const uint32_t nice = lookahead < cfg.nice ? lookahead : cfg.nice;
+    const uint32_t limit = p - S > max_dist ? p - max_dist : S;
+    const uint32_t maxcmp = n - p < (uint32_t)kMaxMatch ? n - p : (uint32_t)kMaxMatch;
+    int best = 0;
+    uint32_t cur = p - d0, start = 0;
+    for (;;) {
+        // quick reject: match[best], match[best-1] and the first two bytes
+        const bool pass = in[cur + best] == in[p + best] && in[cur + best - 1] == in[p + best - 1] &&
+                          in[cur] == in[p] && in[cur + 1] == in[p + 1];
+        if (pass) {
+            uint32_t len = maxcmp;
+            for (uint32_t k0 = 0; k0 < maxcmp; k0 += 64) {
+                const uint32_t k = k0 + (uint32_t)lane;
+                const uint64_t m = __ballot(k < maxcmp && in[cur + k] != in[p + k]);
+                if (m) { len = k0 + (uint32_t)__builtin_ctzll(m); break; }
+            }
+            if ((int)len > best) {
+                start = cur;
+                best = (int)len;
+                if (len >= nice) break;
+            }
+        }
+        // (unsigned: a link may reach back before the buffer, which is past the limit)
+        const uint32_t d = lk[cur];
+        if (d == 0 || d >= cur - limit || --chain == 0) break;
+        cur -= d;
+    }
+    *ms = start;
+    return (uint32_t)best <= lookahead ? (uint32_t)best : lookahead;
+}
+
 __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flagged) {
     __shared__ __attribute__((aligned(16))) uint32_t s_rf[kPT];
     __shared__ __attribute__((aligned(16))) uint32_t s_rq[kPT];
@@ -1007,7 +1057,10 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
     // (E), nothing pending, a new block (deflate.c state after :2030-2042); one
     // resumed at a block cut has read up to e0 and nothing pending either
     // (ParseU::flush's res)
-    uint32_t p = job.start, match_start = 0, match_length = kMinMatch - 1;
+    // match_length before the first decision: 2, or what a function switch left (zm0)
+    uint32_t p = job.start, match_start = 0, match_length = job.srec ? (uint32_t)job.zm0 : kMinMatch - 1;
+    uint32_t zprev = job.srec ? (uint32_t)job.zp0 : kMinMatch - 1;   // deflate_state's prev_length
+    const uint16_t *lk = job.link + job.ws_off[bi];
     po.block_start = p; po.S = 0; po.E = job.e0 > p ? job.e0 : p;
     po.srec = job.srec;
     bool avail = false, done = false;
@@ -1058,7 +1111,9 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
             }
             const uint32_t lookahead = po.E - p;
             // ---- bulk literals: no pending match, far from the window end ----
-            if (match_length < kMinMatch && p + 64 + kMinLookahead <= po.E) {
+            // (not while match_length is 0: each of those decisions searches
+            // from best_len 0 and may end the state, see walk_best0)
+            if (match_length < kMinMatch && match_length != 0 && p + 64 + kMinLookahead <= po.E) {
                 const uint32_t r = s_rf[p - t0 + lane];
                 const uint32_t rl = r >> 16;
                 const bool hit = rl >= kMinMatch &&
@@ -1086,6 +1141,7 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
                     }
                     avail = true;
                     p += k;
+                    zprev = kMinMatch - 1;
                     continue;
                 }
             }
@@ -1097,15 +1153,30 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
                 ci++;
             }
             const uint32_t prev_length = match_length, prev_match = match_start;
+            zprev = prev_length;
             match_length = kMinMatch - 1;
             if (lookahead >= kMinMatch && prev_length < lazy) {
-                const uint32_t r = ufl((use_q && prev_length >= good) ? s_rq[p - t0] : s_rf[p - t0]);
-                const uint32_t rl = r >> 16;
-                if (rl > prev_length) {
-                    match_length = rl;
-                    match_start = p - (r & 0xffffu);
-                    if (match_length <= 5u && (filtered || (match_length == kMinMatch && p - match_start > (uint32_t)kTooFar)))
-                        match_length = kMinMatch - 1;                  // deflate.c:1964-1975
+                if (prev_length == 0) {                    // after a function switch (DeflateJob::zm0)
+                    uint32_t ms = 0;
+                    bool searched = false;
+                    const uint32_t ml = walk_best0(in, lk, p, n, lookahead, po.S, po.max_dist, LevelCfg{good, lazy,
+                                                   ci ? job.cfg_tab[ci - 1].nice : cfg.nice,
+                                                   ci ? job.cfg_tab[ci - 1].chain : cfg.chain}, &ms, &searched, lane);
+                    if (searched) {
+                        match_length = ml;
+                        match_start = ms;
+                        if (match_length <= 5u && (filtered || (match_length == kMinMatch && p - match_start > (uint32_t)kTooFar)))
+                            match_length = kMinMatch - 1;
+                    }
+                } else {
+                    const uint32_t r = ufl((use_q && prev_length >= good) ? s_rq[p - t0] : s_rf[p - t0]);
+                    const uint32_t rl = r >> 16;
+                    if (rl > prev_length) {
+                        match_length = rl;
+                        match_start = p - (r & 0xffffu);
+                        if (match_length <= 5u && (filtered || (match_length == kMinMatch && p - match_start > (uint32_t)kTooFar)))
+                            match_length = kMinMatch - 1;              // deflate.c:1964-1975
+                    }
                 }
             }
             if (prev_length >= kMinMatch && match_length <= prev_length) {
@@ -1113,6 +1184,7 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
                 const bool bflush = po.tally1((dist << 8) | (prev_length - kMinMatch), lane);
                 p += prev_length - 1;
                 avail = false;
+                zprev = 0;                                 // the insert loop counts prev_length down to 0
                 match_length = kMinMatch - 1;
                 if (bflush) {
                     po.flush(p, false, lane);
@@ -1127,7 +1199,8 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
                 // a new job starting at p would find the same state only when
                 // nothing longer than MIN_MATCH - 1 was pending here
                 if (po.tally1(lit, lane)) {
-                    po.flush(p, false, lane, prev_length < kMinMatch);
+                    // (a match_length of 0 is no state a new job starts in)
+                    po.flush(p, false, lane, prev_length < kMinMatch && match_length != 0);
                     if (fe.pause_at(p)) {
                         if (lane == 0 && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
                         fe.i++;
@@ -1146,6 +1219,7 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
                 po.flush(p, true, lane);
             }
             if (lane == 0) job.nblocks[bi] = po.nblk;
+            if (lane == 0 && job.flush_out) job.flush_out[4] = (uint64_t)zprev | (uint64_t)match_length << 16;
         }
         t0 = p & ~15u;
         __syncthreads();
@@ -1875,7 +1949,11 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
             insert(q);
         }
     P p = start, match_start = 0;
-    uint32_t match_length = kMinMatch - 1;
+    // deflate_state's prev_length, which deflate_fast never writes: every search
+    // starts from it (2, or what deflate_slow left behind a function switch,
+    // DeflateJob::zp0); match_length as the job finds it (zm0)
+    const int best0 = kEv ? job.zp0 : kMinMatch - 1;
+    uint32_t match_length = kEv ? (uint32_t)job.zm0 : kMinMatch - 1;
     FlushEv fe = flush_ev(job);
     P lim = kEv ? (P)fe.limit(n) : n;   // input deflate() has been given
     // s->insert: strings a flush left unhashed (a resumed job starts right
@@ -1946,12 +2024,12 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
             // candidate with the longest prefix wins, stop at nice, chain, limit
             // prev_length stays MIN_MATCH-1 under deflate_fast: the budget is
             // quartered only for a deflateTune good_length <= 2 (deflate.c:1390)
-            uint32_t chain = cfg.good <= kMinMatch - 1 ? cfg.chain >> 2 : cfg.chain;
+            uint32_t chain = (uint32_t)best0 >= cfg.good ? cfg.chain >> 2 : cfg.chain;
             const int nice = lookahead < (P)cfg.nice ? (int)lookahead : (int)cfg.nice;
             const P limit = (p - po.S) > max_dist ? p - max_dist : po.S;
             const P rem = n - p;
             const int maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
-            int best = kMinMatch - 1;
+            int best = best0;
             P cur = hh;
             uint32_t sb = 0;
             const int lc = lane < maxcmp ? lane : maxcmp - 1;
@@ -1976,7 +2054,9 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
                     d = ufl(prev[cur]);
                     k = common(cur, p, maxcmp);
                 }
-                if (k > best) {
+                // from best_len 0 the quick reject also compares the bytes
+                // before the strings (scan_end1 = scan[-1]) and the first two
+                if (k > best && (best != 0 || (k >= 2 && in[(uint32_t)(cur - 1)] == in[(uint32_t)(p - 1)]))) {
                     match_start = cur;
                     best = k;
                     if (k >= nice) break;
@@ -2052,6 +2132,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     }
     if (!kEv || !job.open_end) po.flush(p, true);
     if (lead) job.nblocks[bi] = po.nblk;
+    if (kEv && lead && job.flush_out) job.flush_out[4] = (uint64_t)best0 | (uint64_t)match_length << 16;
 }
 
 // ------------------------------------------------------------------------

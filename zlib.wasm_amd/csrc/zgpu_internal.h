@@ -207,6 +207,16 @@ struct DeflateJob {
     const uint32_t *lk_head;
     uint32_t pre_from;
     int keep_head;
+    // deflate_state's prev_length / match_length where the job starts (a
+    // function switch carries them over: deflate_fast never writes
+    // prev_length and both parsers leave 0 behind a match, so the first
+    // searches after a switch may start from best_len 0, whose quick reject
+    // also tests the byte before the string, deflate.c:1356-1497).  zp0: the
+    // prev_length every deflate_fast search starts from; zm0: deflate_slow's
+    // match_length before its first decision.  2 (MIN_MATCH-1) is the clean
+    // state.  A streaming job reports both as the parse leaves them in
+    // flush_out[4] (prev_length | match_length << 16).
+    int zp0, zm0;
 };
 
 // the per-job window/hash parameters (deflate.c:440-455)
