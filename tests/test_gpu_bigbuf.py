@@ -1,0 +1,105 @@
+"""Few large buffers per sub-batch (a lone compress2, a handful of big buffers):
+k_links / k_count per segment, the lazy parse spread over many workgroups
+(k_pbig1..6) and the per-block encoder (k_enc_plan / scan / emit).  Every stream
+must equal the oracle's (our C restatement of deflate.c / trees.c, pinned to the
+reference's golden vectors) byte for byte; the 64 MiB case is checked against
+system zlib (bit-identical to the reference on the bench sample, BASELINE.md
+section 3.1), which is fast enough at that size."""
+import time
+import zlib as pyzlib
+
+import numpy as np
+import pytest
+
+import datagen
+
+pytestmark = pytest.mark.gpu
+
+KINDS = ["mix", "text", "runs", "random"]
+
+
+def _bufs(kind, n, seed):
+    return datagen.make(kind, n, seed)
+
+
+@pytest.mark.parametrize("n", [5000, 65536, 200017, (1 << 20) + 3])
+@pytest.mark.parametrize("kind", KINDS)
+def test_single_buffer_levels_wraps(zg, oracle, kind, n):
+    data = _bufs(kind, n, n % 97)
+    for i, level in enumerate((4, 5, 6, 8, 9)):
+        wrap = (i + n) % 3
+        [(st, z)] = zg.compress_batch([data], level=level, wrap=wrap)
+        rc, want = oracle.compress(data, level, wrap)
+        assert rc == 0 and st == 0, (kind, n, level, wrap, st)
+        assert z == want, (kind, n, level, wrap, len(z), len(want))
+
+
+def test_few_buffers_one_subbatch(zg, oracle):
+    """Several large buffers of different sizes in one call: lane groups and
+    block plans of consecutive buffers must not mix."""
+    sizes = [70001, 1 << 20, 333333, 4096 * 5 + 1, 2 * (1 << 20) + 77]
+    bufs = [_bufs(KINDS[i % len(KINDS)], n, 11 + i) for i, n in enumerate(sizes)]
+    for level in (4, 6, 9):
+        res = zg.compress_batch(bufs, level=level)
+        for b, (st, z) in zip(bufs, res):
+            assert st == 0
+            assert z == oracle.compress(b, level)[1], (len(b), level)
+
+
+def test_short_output_prefix(zg, oracle):
+    """compress2 into a buffer too small: Z_BUF_ERROR and the stream's prefix
+    (the block-parallel encoder clips every write at the capacity)."""
+    data = _bufs("mix", 1 << 20, 3)
+    want = oracle.compress(data, 6)[1]
+    for cap in (len(want) - 1, len(want) // 2 + 3, 1000, 7):
+        [(st, z)] = zg.compress_batch([data], level=6, caps=[cap])
+        assert st == -5, cap
+        assert z == want[:cap], cap
+
+
+def test_unaligned_device_offsets(zg, oracle):
+    """Outputs at odd device offsets next to each other: the shared words at
+    block and buffer edges are or-ed in, nothing outside a stream is touched."""
+    import torch
+    sizes = [300001, 1 << 20, 65537]
+    bufs = [_bufs(k, n, 5 + i) for i, (k, n) in enumerate(zip(("text", "mix", "runs"), sizes))]
+    wants = [oracle.compress(b, 6)[1] for b in bufs]
+    src = torch.tensor(np.frombuffer(b"".join(bufs), dtype=np.uint8), device="cuda")
+    offs = np.cumsum([0] + sizes[:-1])
+    caps = [zg.compress_bound(n) for n in sizes]
+    doffs, pos = [], 3
+    for c in caps:
+        doffs.append(pos)
+        pos += c + 5                                   # odd gaps between the streams
+    dst = torch.full((pos + 16,), 0xA5, dtype=torch.uint8, device="cuda")
+    t64 = lambda v: torch.tensor(v, dtype=torch.int64, device="cuda")
+    dlen = t64([0] * 3)
+    st = torch.zeros(3, dtype=torch.int32, device="cuda")
+    zg.deflate_batch_dev(src, t64(list(offs)), t64(sizes), dst, t64(doffs), t64(caps), dlen, st, level=6)
+    torch.cuda.synchronize()
+    h = dst.cpu().numpy()
+    dl = dlen.cpu().numpy()
+    assert list(st.cpu().numpy()) == [0, 0, 0]
+    for i in range(3):
+        assert h[doffs[i]:doffs[i] + dl[i]].tobytes() == wants[i], i
+        # the bytes between this stream's end and the next one's start keep the fill
+        end = doffs[i + 1] if i + 1 < 3 else pos
+        assert (h[doffs[i] + dl[i]:end] == 0xA5).all(), i
+    assert (h[:3] == 0xA5).all()
+
+
+def test_lone_64mib_l6_vs_system_zlib(zg):
+    """The VERDICT r2 #5 case: one 64 MiB buffer at level 6 through compress2,
+    equal to system zlib's stream; the rate is printed."""
+    import torch
+    n = 64 << 20
+    src = torch.empty(n, dtype=torch.uint8, device="cuda")
+    zg.generate_dev(src, n, 1, zg.KIND_SILESIA, seed=9)
+    data = src.cpu().numpy().tobytes()
+    want = pyzlib.compress(data, 6)
+    zg.compress2(data[:1 << 20], 6)                     # warm the context
+    t = time.perf_counter()
+    rc, z = zg.compress2(data, 6)
+    dt = time.perf_counter() - t
+    print(f"lone 64 MiB L6 compress2: {n / dt / 1e6:.0f} MB/s (host buffers in and out)")
+    assert rc == 0 and z == want

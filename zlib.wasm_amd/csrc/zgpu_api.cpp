@@ -243,6 +243,8 @@ struct Ctx {
     DevBuf ws_stg;            // k_parse_seg's symbol staging (caller's stream only)
     DevBuf ws_help;           // the a18 helpers' staging (zlib_*_simd)
     DevBuf ws_seg;            // k_match segments of sub-batches of few large buffers
+    // few large buffers: k_pbig* lane groups and records, k_enc_* block plans
+    DevBuf ws_pg, ws_plane, ws_pbuf, ws_eplan;
     DevBuf ws_ck;             // split checksum partials (few large buffers)
     DevBuf ws_srec, ws_snap;  // a streaming job's block records and head[] snapshot
     // inflate: match records, per-stream results, checks, offsets, stop codes
@@ -569,6 +571,52 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
                           hipMemcpyAsync(c.ws_seg.p, segs.data(), 4 * segs.size(), hipMemcpyHostToDevice, st) !=
                               hipSuccess))
         return zfail(__LINE__);
+    // ... and, for a batch (no streaming job), the lazy parse and the encoder
+    // too: k_pbig* over segments of pseg bytes (>= 1 KiB; ~64 Ki lanes per
+    // sub-batch), kParseLanes lanes per workgroup, k_enc_* per block.  One
+    // table holds every sub-batch's (buffer, first lane) pairs, then the
+    // per-buffer lane bases.
+    static const bool no_big = std::getenv("ZGPU_NO_BIGBUF") != nullptr;   // A/B: the one-workgroup stages
+    std::vector<uint32_t> pg, plb;
+    std::vector<size_t> pg_at(nsub + 1, 0), plb_at(nsub + 1, 0);
+    std::vector<uint32_t> pseg_of(nsub, 0), maxblk_of(nsub, 0);
+    uint64_t max_lanes = 0;
+    for (size_t sb = 0; sb < nsub; sb++) {
+        pg_at[sb] = pg.size() / 2;
+        plb_at[sb] = plb.size();
+        if (fs || no_big || seg_at[sb + 1] == seg_at[sb]) continue;
+        const uint32_t a = cuts[sb], b = cuts[sb + 1];
+        uint64_t tot = 0, mb = 0;
+        for (uint32_t i = a; i < b; i++) tot += lens[i], mb = std::max<uint64_t>(mb, lens[i] / wp.sym_limit + 2);
+        uint64_t ps = ((tot + 65535) / 65536 + 15) & ~15ull;
+        ps = ps < 1024 ? 1024 : ps > 65536 ? 65536 : ps;
+        uint64_t lanes = 0;
+        for (uint32_t i = a; i < b; i++) {
+            const uint64_t nl = std::max<uint64_t>(1, (lens[i] + ps - 1) / ps);
+            plb.push_back((uint32_t)lanes);
+            for (uint64_t j = 0; j < nl; j += kParseLanesHost) {
+                pg.push_back(i - a);
+                pg.push_back((uint32_t)j);
+            }
+            lanes += nl;
+        }
+        max_lanes = std::max(max_lanes, lanes);
+        pseg_of[sb] = (uint32_t)ps;
+        maxblk_of[sb] = (uint32_t)mb;
+    }
+    pg_at[nsub] = pg.size() / 2;
+    plb_at[nsub] = plb.size();
+    if (!pg.empty()) {
+        const size_t npg = pg.size();
+        pg.insert(pg.end(), plb.begin(), plb.end());
+        if (!c.ws_pg.ensure(4 * pg.size()) ||
+            hipMemcpyAsync(c.ws_pg.p, pg.data(), 4 * pg.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
+            !c.ws_plane.ensure(sizeof(PLane) * max_lanes) || !c.ws_pbuf.ensure(sizeof(PBuf) * max_cnt) ||
+            !c.ws_eplan.ensure(sizeof(EncPlan) * max_blk))
+            return zfail(__LINE__);
+        pg.resize(npg);
+    }
+    const size_t plb_base = pg.size();
     uint64_t *d_meta = c.ws_meta.as<uint64_t>();
     uint32_t *d_nblk = reinterpret_cast<uint32_t *>(d_meta + 2ull * count);
     uint32_t *d_check = d_nblk + max_cnt;
@@ -628,6 +676,16 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.nseg = (uint32_t)(seg_at[s + 1] - seg_at[s]);
             job.seg_len = (uint32_t)seg_len[s];
         }
+        if (pg_at[s + 1] > pg_at[s]) {
+            job.pgrp = c.ws_pg.as<uint32_t>() + 2 * pg_at[s];
+            job.npgrp = (uint32_t)(pg_at[s + 1] - pg_at[s]);
+            job.plbase = c.ws_pg.as<uint32_t>() + plb_base + plb_at[s];
+            job.pseg = pseg_of[s];
+            job.maxblk = maxblk_of[s];
+            job.plane = c.ws_plane.as<PLane>();
+            job.pbuf = c.ws_pbuf.as<PBuf>();
+            job.eplan = c.ws_eplan.as<EncPlan>();
+        }
         if (fs) {
             job.fl_pos = fs->pos;
             job.fl_type = fs->type;
@@ -683,13 +741,15 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             // the input is all there)
             if (T.run(3, st, [&] { return launch_deflate_stage(2, job, nullptr, st); })) return zfail(__LINE__);
         } else if (level >= 4) {
-            if (T.run(3, st, [&] { return launch_deflate_stage(5, job, nullptr, st); })) return zfail(__LINE__);
+            const int ps = job.pgrp ? 11 : 5;                  // few large buffers: k_pbig*
+            if (T.run(3, st, [&] { return launch_deflate_stage(ps, job, nullptr, st); })) return zfail(__LINE__);
             if (T.run(3, st, [&] { return launch_deflate_stage(6, job, nullptr, st); })) return zfail(__LINE__);
         } else if (level >= 1) {
             uint32_t *heads = c.ws_heads.as<uint32_t>();
             if (T.run(4, st, [&] { return launch_deflate_stage(3, job, heads, st); })) return zfail(__LINE__);
         }
-        if (T.run(5, st, [&] { return launch_deflate_stage(4, job, nullptr, st); })) return zfail(__LINE__);
+        const int es = job.pgrp ? 12 : 4;                      // few large buffers: k_enc_*
+        if (T.run(5, st, [&] { return launch_deflate_stage(es, job, nullptr, st); })) return zfail(__LINE__);
         return ZGPU_OK;
     };
 

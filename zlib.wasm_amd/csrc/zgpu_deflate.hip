@@ -213,7 +213,11 @@ __device__ __attribute__((always_inline)) inline void links_radix_pass(const uin
 
 // kH head entries (1 << hash_bits, <= 32768 in the default layout; 65536 for
 // memLevel 9 with kC = 2048-position chunks so head[] fits in LDS)
-template <int kC, int kH>
+// kSegs: one workgroup per segment [s0, s1) of job.seg (few large buffers,
+// see k_match): a link reaches back at most 32767 positions, so the segment
+// starts its chains empty at the chunk t0 <= s0 - 32768 and writes the links
+// of [s0, s1) only.
+template <int kC, int kH, bool kSegs = false>
 __global__ __launch_bounds__(kLThreads) void k_links(DeflateJob job) {
     static_assert(kC <= kLC && (kC & (kC - 1)) == 0, "chunk");
     __shared__ uint16_t head[kH];
@@ -222,16 +226,20 @@ __global__ __launch_bounds__(kLThreads) void k_links(DeflateJob job) {
     __shared__ uint16_t wcnt[kLWaves][256];
     __shared__ int wsum[kLWaves];
     const int tid = threadIdx.x;
-    const uint32_t bi = blockIdx.x;
+    const uint32_t bi = kSegs ? job.seg[2 * blockIdx.x] : blockIdx.x;
     const uint32_t g = job.first + bi;
     const int64_t n = (int64_t)job.src_len[g];
     const uint8_t *in = job.src + job.src_off[g];
     uint16_t *out = job.link + job.ws_off[bi];
     const WinP wp = job_win(job);
+    const int64_t s0 = kSegs ? (int64_t)job.seg[2 * blockIdx.x + 1] : 0;
+    const int64_t s1 = kSegs && s0 + (int64_t)job.seg_len < n ? s0 + (int64_t)job.seg_len : n;
+    const int64_t t0 = kSegs && s0 > 32768 ? (s0 - 32768) / kC * kC : 0;
 
-    for (int i = tid; i < kH; i += kLThreads) head[i] = 32768;   // "position -32768"
-    const int64_t lk_n = job.lk_head ? (int64_t)job.lk_n : 0;
-    for (int64_t c0 = 0; c0 < n; c0 += kC) {
+    // "position t0 - 32768": older than any chain from t0 on reaches
+    for (int i = tid; i < kH; i += kLThreads) head[i] = (uint16_t)((t0 - 32768) & 0xffff);
+    const int64_t lk_n = !kSegs && job.lk_head ? (int64_t)job.lk_n : 0;
+    for (int64_t c0 = t0; c0 < s1; c0 += kC) {
         __syncthreads();
         if (c0 + kC <= lk_n) continue;                       // links as uploaded (deflate_fast's chains)
         if (c0 <= lk_n && job.lk_head) {                     // the chains at lk_n: head[] of the uploaded state
@@ -278,7 +286,12 @@ __global__ __launch_bounds__(kLThreads) void k_links(DeflateJob job) {
             if (i == ms - 1 || (ka[i + 1] >> 13) != (key >> 13))
                 head[key >> 13] = (uint16_t)(((uint32_t)c0 + (key & (kLC - 1))) & 0xffffu);
         }
-        for (int e = tid + e0; e < cnt; e += kLThreads) out[c0 + e] = e < m ? (uint16_t)kb[e] : (uint16_t)0;
+        if (kSegs) {
+            const int w0 = s0 > c0 ? (int)(s0 - c0) : 0, w1 = (int)(s1 - c0 < cnt ? s1 - c0 : cnt);
+            for (int e = tid + w0; e < w1; e += kLThreads) out[c0 + e] = e < m ? (uint16_t)kb[e] : (uint16_t)0;
+        } else {
+            for (int e = tid + e0; e < cnt; e += kLThreads) out[c0 + e] = e < m ? (uint16_t)kb[e] : (uint16_t)0;
+        }
     }
 }
 
@@ -306,19 +319,25 @@ __device__ __attribute__((always_inline)) inline uint32_t walk_key(uint32_t c, u
 
 // 4 waves per buffer; thread t takes positions t, t + 256, ... of each staged
 // 4 KiB, without barriers between them (their order only perturbs the hint).
+// kSegs: one workgroup per segment [s0, s1) of job.seg, counting from the
+// stage at or before s0 - MAX_DIST (the window of s0) and writing [s0, s1).
+template <bool kSegs = false>
 __global__ __launch_bounds__(kCntThreads) void k_count(DeflateJob job) {
     __shared__ uint32_t cnt[16384];
     __shared__ __attribute__((aligned(16))) uint8_t s_in[kCntStage + 16];
     __shared__ __attribute__((aligned(16))) uint8_t s_out[kCntStage + 16];
     const int tid = threadIdx.x;
-    const uint32_t bi = blockIdx.x;
+    const uint32_t bi = kSegs ? job.seg[2 * blockIdx.x] : blockIdx.x;
     const uint32_t g = job.first + bi;
     const int64_t n = (int64_t)job.src_len[g];
     const uint8_t *in = job.src + job.src_off[g];
     uint8_t *key = job.key + job.ws_off[bi];
     const uint32_t chain = job.cfg.chain;
+    const int64_t s0 = kSegs ? (int64_t)job.seg[2 * blockIdx.x + 1] : 0;
+    const int64_t s1 = kSegs && s0 + (int64_t)job.seg_len < n ? s0 + (int64_t)job.seg_len : n;
+    const int64_t c0 = kSegs && s0 > kMaxDist ? (s0 - kMaxDist) / kCntStage * kCntStage : 0;
     for (int i = tid; i < 16384; i += kCntThreads) cnt[i] = 0;
-    for (int64_t t0 = 0; t0 < n; t0 += kCntStage) {
+    for (int64_t t0 = c0; t0 < s1; t0 += kCntStage) {
         __syncthreads();
         stage_bytes<kCntThreads, (kCntStage + 16) / 16 / kCntThreads + 1>(s_in, in, t0, kCntStage + 16, n, tid);
         stage_bytes<kCntThreads, (kCntStage + 16) / 16 / kCntThreads + 1>(s_out, in, t0 - kMaxDist,
@@ -328,7 +347,7 @@ __global__ __launch_bounds__(kCntThreads) void k_count(DeflateJob job) {
         for (int64_t p = t0 + tid; p < tend; p += kCntThreads) {
             const int j = (int)(p - t0);
             const int64_t q = p - kMaxDist;                   // leaves p's window
-            if (q >= 1 && q + 3 <= n) {
+            if (q >= 1 && q >= c0 && q + 3 <= n) {              // (counted: q >= c0)
                 const uint32_t h = hash3(s_out[j], s_out[j + 1], s_out[j + 2]);
                 atomicSub(&cnt[h >> 1], 1u << ((h & 1u) * 16));
             }
@@ -338,7 +357,7 @@ __global__ __launch_bounds__(kCntThreads) void k_count(DeflateJob job) {
                 const uint32_t old = atomicAdd(&cnt[h >> 1], 1u << ((h & 1u) * 16));
                 k = walk_key((old >> ((h & 1u) * 16)) & 0xffffu, chain);
             }
-            key[p] = (uint8_t)k;
+            if (!kSegs || (p >= s0 && p < s1)) key[p] = (uint8_t)k;
         }
     }
 }
@@ -1261,6 +1280,7 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
 // ------------------------------------------------------------------------
 constexpr int kSegMin = 512;
 constexpr int kParseLanes = 256;                  // segments (lanes) per buffer
+static_assert(kParseLanes == (int)kParseLanesHost, "host lane groups");
 constexpr uint32_t kEnd = 0xffffffffu;
 
 struct WCache {
@@ -1605,6 +1625,300 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
         __syncthreads();
     }
     if (lane == 0) job.nblocks[bi] = ncut + 1;
+}
+
+// ------------------------------------------------------------------------
+// k_pbig1..6 — k_parse_seg's speculative segmented lazy parse for a sub-batch
+// of few large buffers (a lone compress2, say), with a buffer's segments
+// spread over many workgroups instead of one.  The steps are k_parse_seg's;
+// each block-wide barrier of k_parse_seg becomes a kernel boundary, and what
+// its lanes kept in registers or LDS across a barrier lives in PLane records:
+//   k_pbig1  pass 1 of every segment (symbols staged, simple states recorded)
+//   k_pbig2  pass 2: run on into the next segment until the two parses meet
+//   k_pbig3  replays: the prefix before y(i-1), the run-on up to y(i)
+//   k_pbig4  per buffer: exclusive scan of the lanes' symbol counts
+//   k_pbig5  compaction into sym[] and the block cuts
+//   k_pbig6  block records (slides before each flush by binary search)
+// A buffer whose lanes do not meet within the next segment goes to
+// k_parse_slow (nblocks = kParseFallback), as with k_parse_seg.
+// DeflateJob::pgrp maps a workgroup to (buffer, first lane); a buffer has
+// ceil(n / pseg) lanes, the global index of its lane 0 is plbase[buffer].
+// ------------------------------------------------------------------------
+struct PCtx {
+    uint32_t bi, lane, nl, n, seg, gl;
+    bool active;
+    const uint8_t *in;
+    const uint32_t *rf, *rq;
+    uint32_t *sym, *stg, *sst;
+    BlockRec *blk;
+    __device__ inline uint32_t xb(uint32_t i) const {
+        const uint64_t v = (uint64_t)i * seg;
+        return v < n ? (uint32_t)v : n;
+    }
+    __device__ inline uint32_t seg_end() const { return lane + 1 >= nl ? n : xb(lane + 1); }
+};
+__device__ inline uint32_t pbig_lanes(uint32_t n, uint32_t seg) {
+    const uint32_t k = (n + seg - 1) / seg;
+    return k ? k : 1u;
+}
+__device__ inline PCtx pbig_ctx(const DeflateJob &job) {
+    PCtx c;
+    c.bi = job.pgrp[2 * blockIdx.x];
+    c.lane = job.pgrp[2 * blockIdx.x + 1] + threadIdx.x;
+    const uint32_t g = job.first + c.bi;
+    c.n = (uint32_t)job.src_len[g];
+    c.seg = job.pseg;
+    c.nl = pbig_lanes(c.n, c.seg);
+    c.active = c.lane < c.nl;
+    c.gl = job.plbase[c.bi] + c.lane;
+    c.in = job.src + job.src_off[g];
+    c.rf = job.rfull + job.ws_off[c.bi];
+    c.rq = job.rquart + job.ws_off[c.bi];
+    c.sym = job.sym + job.ws_off[c.bi];
+    c.stg = job.stage + job.ws_off[c.bi];
+    c.sst = job.pstate + (job.ws_off[c.bi] >> 4);
+    c.blk = job.blocks + job.blk_off[c.bi];
+    return c;
+}
+
+__global__ __launch_bounds__(kParseLanes) void k_pbig1(DeflateJob job) {
+    const PCtx c = pbig_ctx(job);
+    if (c.lane == 0) job.pbuf[c.bi] = PBuf{0u, kEnd, 0u, 0u};
+    if (!c.active) return;
+    const LevelCfg cfg = job.cfg;
+    const bool use_q = cfg.good < cfg.lazy, filtered = job.strategy == 1;
+    SlowLane L;
+    uint32_t sym_v, spos, slen;
+    const uint32_t x0 = c.xb(c.lane), seg_end = c.seg_end();
+    lane_init(L, x0, 0);
+    SymBuf sb{0, 0, 0, 0, 0};
+    if (x0 < seg_end) {                               // as k_parse_seg's pass 1
+        uint32_t widx = x0 >> 4, wcur = 0;
+        while (L.p < seg_end) {
+            const uint32_t wi = L.p >> 4;
+            if (wi != widx) {
+                c.sst[widx] = wcur;
+                for (uint32_t z = widx + 1; z < wi; z++) c.sst[z] = 0;
+                widx = wi;
+                wcur = 0;
+            }
+            if (L.ml < (uint32_t)kMinMatch) wcur |= 1u << (2 * (L.p & 15u) + L.avail);
+            if (slow_step(L, c.n, c.rf, c.rq, c.in, cfg, use_q, filtered, sym_v, spos, slen)) sb.push(c.stg + x0, sym_v);
+        }
+        c.sst[widx] = wcur;
+        for (uint32_t z = widx + 1; z <= (seg_end - 1) >> 4; z++) c.sst[z] = 0;
+        sb.flush(c.stg + x0);
+    }
+    PLane &r = job.plane[c.gl];
+    r.e_p = L.p; r.e_ml = L.ml; r.e_ms = L.ms; r.e_av = L.avail;
+    r.k1 = sb.k;
+}
+
+__global__ __launch_bounds__(kParseLanes) void k_pbig2(DeflateJob job) {
+    const PCtx c = pbig_ctx(job);
+    if (!c.active) return;
+    const LevelCfg cfg = job.cfg;
+    const bool use_q = cfg.good < cfg.lazy, filtered = job.strategy == 1;
+    PLane &r = job.plane[c.gl];
+    SlowLane L;
+    lane_init(L, r.e_p, r.e_av);
+    L.ml = r.e_ml; L.ms = r.e_ms;
+    uint32_t sym_v, spos, slen;
+    uint32_t y = kEnd, sig = 0;
+    bool fail = false;
+    if (c.lane + 1 < c.nl) {                          // as k_parse_seg's pass 2
+        const uint32_t next_start = c.xb(c.lane + 1);
+        const uint32_t stop = c.lane + 2 >= c.nl ? c.n : c.xb(c.lane + 2);
+        uint32_t ridx = 0xffffffffu, rw = 0;
+        for (;;) {
+            if (L.p >= c.n) { y = kEnd; break; }
+            if (L.p >= stop) { fail = true; break; }
+            if (L.p >= next_start && L.ml < (uint32_t)kMinMatch) {
+                if ((L.p >> 4) != ridx) { ridx = L.p >> 4; rw = c.sst[ridx]; }
+                if ((rw >> (2 * (L.p & 15u) + L.avail)) & 1u) { y = L.p; sig = L.avail; break; }
+            }
+            slow_step(L, c.n, c.rf, c.rq, c.in, cfg, use_q, filtered, sym_v, spos, slen);
+        }
+    }
+    r.y = y;
+    r.sig = sig;
+    if (fail) atomicOr(&job.pbuf[c.bi].fail, 1u);
+    if (y == kEnd) atomicMin(&job.pbuf[c.bi].first_end, c.lane);
+}
+
+__global__ __launch_bounds__(kParseLanes) void k_pbig3(DeflateJob job) {
+    const PCtx c = pbig_ctx(job);
+    if (!c.active || job.pbuf[c.bi].fail) return;
+    const LevelCfg cfg = job.cfg;
+    const bool use_q = cfg.good < cfg.lazy, filtered = job.strategy == 1;
+    PLane &r = job.plane[c.gl];
+    const bool mine = c.lane <= job.pbuf[c.bi].first_end;
+    const uint32_t x0 = c.xb(c.lane), seg_end = c.seg_end();
+    const uint32_t start = c.lane > 0 ? job.plane[c.gl - 1].y : 0u;
+    const uint32_t yend = r.y, end = yend == kEnd ? c.n : yend;
+    SlowLane L;
+    uint32_t sym_v, spos, slen;
+    uint32_t kstart = 0;
+    if (mine && c.lane > 0) {                         // pass-1 symbols before y(i-1) are not this lane's
+        lane_init(L, x0, 0);
+        while (L.p < start)
+            if (slow_step(L, c.n, c.rf, c.rq, c.in, cfg, use_q, filtered, sym_v, spos, slen)) kstart++;
+    }
+    uint32_t rcnt = 0;
+    uint32_t *ron = c.sst + (x0 >> 4);
+    const uint32_t rcap = (seg_end - x0 + 15u) >> 4;
+    if (mine) {                                       // the run-on, staged in the lane's dead state words
+        lane_init(L, r.e_p, r.e_av);
+        L.ml = r.e_ml; L.ms = r.e_ms;
+        while (L.p < end) {
+            if (slow_step(L, c.n, c.rf, c.rq, c.in, cfg, use_q, filtered, sym_v, spos, slen)) {
+                if (rcnt < rcap) ron[rcnt] = sym_v;
+                rcnt++;
+            }
+        }
+        if (yend == kEnd && L.avail) {                // the final pending literal
+            if (rcnt < rcap) ron[rcnt] = bget(c.in, c.n - 1, L.cb);
+            rcnt++;
+            job.pbuf[c.bi].fin = 1u;
+        }
+        if (rcnt > rcap) atomicOr(&job.pbuf[c.bi].fail, 1u);
+    }
+    r.kstart = kstart;
+    r.rcnt = rcnt;
+    r.cnt = mine ? r.k1 - kstart + rcnt : 0u;
+}
+
+constexpr int kPScanThreads = 1024;
+__global__ __launch_bounds__(kPScanThreads) void k_pbig4(DeflateJob job) {
+    __shared__ uint32_t s_wsum[kPScanThreads / 64];
+    const int tid = threadIdx.x, wl = tid & 63, wv = tid >> 6;
+    const uint32_t bi = blockIdx.x;
+    const uint32_t n = (uint32_t)job.src_len[job.first + bi];
+    const uint32_t nl = pbig_lanes(n, job.pseg);
+    PLane *pl = job.plane + job.plbase[bi];
+    if (job.pbuf[bi].fail) {
+        if (tid == 0) job.nblocks[bi] = kParseFallback;
+        return;
+    }
+    uint32_t run = 0;
+    for (uint32_t c0 = 0; c0 < nl; c0 += kPScanThreads) {
+        const uint32_t i = c0 + (uint32_t)tid;
+        const uint32_t v = i < nl ? pl[i].cnt : 0u;
+        uint32_t incl = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(incl, o, 64);
+            if (wl >= o) incl += t;
+        }
+        if (wl == 63) s_wsum[wv] = incl;
+        __syncthreads();
+        uint32_t woff = 0, tot = 0;
+        for (int k = 0; k < kPScanThreads / 64; k++) {
+            const uint32_t t = s_wsum[k];
+            if (k < wv) woff += t;
+            tot += t;
+        }
+        if (i < nl) pl[i].base = run + woff + incl - v;
+        run += tot;
+        __syncthreads();
+    }
+    if (tid == 0) job.pbuf[bi].total = run;
+}
+
+__global__ __launch_bounds__(kParseLanes) void k_pbig5(DeflateJob job) {
+    const PCtx c = pbig_ctx(job);
+    const PBuf pb = job.pbuf[c.bi];
+    if (pb.fail) return;                              // uniform: a workgroup's lanes share a buffer
+    const int wl = threadIdx.x & 63;
+    const uint32_t symlim = job_win(job).sym_limit;
+    const uint32_t total = pb.total;
+    const uint32_t ncut = total / symlim - ((pb.fin && total % symlim == 0) ? 1u : 0u);
+    uint32_t cnt = 0, base = 0, c1 = 0, x0 = 0, kstart = 0, pos0 = 0;
+    if (c.active) {
+        const PLane &r = job.plane[c.gl];
+        cnt = r.cnt;
+        base = r.base;
+        c1 = cnt - r.rcnt;
+        x0 = c.xb(c.lane);
+        kstart = r.kstart;
+        if (c.lane > 0) {
+            const PLane &q = job.plane[c.gl - 1];
+            pos0 = q.y - q.sig;                       // the lane's symbols tile the input from here
+        }
+    }
+    // as k_parse_seg's compaction: each wave copies its own lanes' symbols
+    for (int j = 0; j < 64; j++) {
+        const uint32_t jc = __shfl(cnt, j, 64), jb = __shfl(base, j, 64);
+        if (jc == 0) continue;
+        const uint32_t jc1 = __shfl(c1, j, 64), jx = __shfl(x0, j, 64), jk = __shfl(kstart, j, 64);
+        uint32_t run = __shfl(pos0, j, 64);
+        const uint32_t *s1 = c.stg + jx + jk, *s2 = c.sst + (jx >> 4);
+        for (uint32_t k = 0; k < jc; k += 64) {
+            const uint32_t idx = k + (uint32_t)wl;
+            const bool have = idx < jc;
+            const uint32_t v = have ? (idx < jc1 ? s1[idx] : s2[idx - jc1]) : 0u;
+            const uint32_t len = have ? (v < 256u ? 1u : (v & 0xffu) + (uint32_t)kMinMatch) : 0u;
+            uint32_t li = len;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(li, o, 64);
+                if (wl >= o) li += t;
+            }
+            const uint32_t sp = run + li - len;
+            run += __shfl(li, 63, 64);
+            if (have) {
+                const uint32_t gi = jb + idx;
+                c.sym[gi] = v;
+                if ((gi + 1) % symlim == 0 && (gi + 1) / symlim <= ncut) {
+                    const uint32_t b = (gi + 1) / symlim - 1;
+                    c.blk[b].in_end = (uint64_t)(sp + len);
+                    c.blk[b].pad = sp + 1;                // decision point of the flush
+                }
+            }
+        }
+    }
+}
+
+// #{k >= 1 : slide_threshold(k) <= p}: the thresholds grow with k
+__device__ inline uint32_t slides_upto(int64_t p, uint32_t n, int64_t refill, const WinP &w) {
+    uint32_t lo = 0, hi = (uint32_t)(n / w.wsize) + 2;     // slide_threshold(hi + 1) > n >= p
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (slide_threshold(mid, n, refill, w) <= p) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// one thread per block record; grid (blocks / 256, buffers)
+__global__ __launch_bounds__(256) void k_pbig6(DeflateJob job) {
+    const uint32_t bi = blockIdx.y;
+    const PBuf pb = job.pbuf[bi];
+    if (pb.fail) return;
+    const WinP wp = job_win(job);
+    const uint32_t symlim = wp.sym_limit;
+    const uint32_t n = (uint32_t)job.src_len[job.first + bi];
+    const uint32_t total = pb.total;
+    const uint32_t ncut = total / symlim - ((pb.fin && total % symlim == 0) ? 1u : 0u);
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    if (b == 0) job.nblocks[bi] = ncut + 1;
+    if (b > ncut) return;
+    BlockRec *blk = job.blocks + job.blk_off[bi];
+    const bool last = b == ncut;
+    // a record's in_end is rewritten with its own value, so the neighbour's
+    // read of it (in_start) is safe in any order
+    const uint64_t in_end = last ? n : blk[b].in_end;
+    const uint64_t pd = last ? n : blk[b].pad;
+    const uint64_t in_start = b == 0 ? 0 : blk[b - 1].in_end;
+    const uint32_t slides = slides_upto((int64_t)pd, n, kMinLookahead - 1, wp);
+    BlockRec r;
+    r.sym_start = b * symlim;
+    r.nsym = last ? total - b * symlim : symlim;
+    r.in_start = in_start;
+    r.in_end = in_end;
+    r.flags = (last ? 1u : 0u) | (in_start >= (uint64_t)wp.wsize * slides ? 2u : 0u);
+    r.pad = 0;
+    blk[b] = r;
 }
 
 // ------------------------------------------------------------------------
@@ -2607,6 +2921,75 @@ __device__ __attribute__((always_inline)) inline void stg_flush(Stage &st, int64
     }
 }
 
+// One block's histogram (_tr_tally's freq updates, deflate.h:354-372), trees
+// (build_tree / gen_bitlen / gen_codes, trees.c:499-706; the whole wave with
+// w_build or lane 0 with t_build) and type (_tr_flush_block, trees.c:997-1074)
+// into T.  Lane 0 returns the header fields and the block's length in bits
+// from its 3-bit header through END_BLOCK (static or dynamic; for a stored
+// block the input length is what counts).
+template <bool kWaveTrees>
+__device__ __attribute__((always_inline)) inline void block_plan(const DeflateJob &job, const BlockRec br,
+                                                                 const uint32_t *sym, TreeLDS &T, uint32_t *hl,
+                                                                 uint32_t *hd, int lane, int &type, int &lmax,
+                                                                 int &dmax, int &blmax, uint64_t &bits) {
+    for (int i = lane; i < kLCodes; i += 64) hl[i] = 0;
+    if (lane < kDCodes) hd[lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i = lane; i < br.nsym; i += 64) {
+        const uint32_t v = sym[br.sym_start + i];
+        const uint32_t dist = v >> 8, lc = v & 0xffu;
+        if (dist == 0) atomicAdd(&hl[lc], 1u);
+        else {
+            atomicAdd(&hl[c_ct.len_code[lc] + 257], 1u);
+            const uint32_t d = dist - 1;
+            atomicAdd(&hd[d < 256 ? c_ct.dist_code[d] : c_ct.dist_code[256 + (d >> 7)]], 1u);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int i = lane; i < kLCodes; i += 64) T.lfreq[i] = i == kEndBlock ? 1 : (uint16_t)hl[i];
+    if (lane < kDCodes) T.dfreq[lane] = (uint16_t)hd[lane];
+    if (lane < kBLCodes) T.bfreq[lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    int64_t opt_len = 0, static_len = 0;
+    TreeRef lt{T.lfreq, T.ldad, T.lcode, T.llen, 0};
+    TreeRef dt{T.dfreq, T.ddad, T.dcode, T.dlen, 0};
+    TreeRef bt{T.bfreq, T.bdad, T.bcode, T.blen, 0};
+    auto cnt = [&](int s, int, int) { T.bfreq[s]++; };
+    if constexpr (kWaveTrees) {
+        w_build(lt, T, kLCodes, c_ct.stat_llen, c_ct.xlbits, 257, kMaxBits, opt_len, static_len);
+        w_build(dt, T, kDCodes, c_ct.stat_dlen, c_ct.xdbits, 0, kMaxBits, opt_len, static_len);
+        if (lane == 0) {
+            t_rle(T.llen, lt.max_code, cnt);
+            t_rle(T.dlen, dt.max_code, cnt);
+        }
+        __builtin_amdgcn_wave_barrier();
+        w_build(bt, T, kBLCodes, nullptr, c_ct.xblbits, 0, kMaxBLBits, opt_len, static_len);
+    } else if (lane == 0) {
+        t_build(lt, T, kLCodes, c_ct.stat_llen, c_ct.xlbits, 257, kMaxBits, opt_len, static_len);
+        t_build(dt, T, kDCodes, c_ct.stat_dlen, c_ct.xdbits, 0, kMaxBits, opt_len, static_len);
+        t_rle(T.llen, lt.max_code, cnt);
+        t_rle(T.dlen, dt.max_code, cnt);
+        t_build(bt, T, kBLCodes, nullptr, c_ct.xblbits, 0, kMaxBLBits, opt_len, static_len);
+    }
+    if (lane == 0) {
+        int max_blindex;
+        for (max_blindex = kBLCodes - 1; max_blindex >= 3; max_blindex--)
+            if (T.blen[c_ct.bl_order[max_blindex]] != 0) break;
+        opt_len += 3 * ((int64_t)max_blindex + 1) + 5 + 5 + 4;
+        uint64_t opt_lenb = ((uint64_t)opt_len + 3 + 7) >> 3;
+        const uint64_t static_lenb = ((uint64_t)static_len + 3 + 7) >> 3;
+        if (static_lenb <= opt_lenb || job.strategy == 4) opt_lenb = static_lenb;   // trees.c:1035
+        const uint64_t stored_len = br.in_end - br.in_start;
+        if (stored_len + 4 <= opt_lenb && (br.flags & kBlkStored)) type = 0;       // trees.c:1027-1074
+        else if (static_lenb == opt_lenb) type = 1;
+        else type = 2;
+        lmax = lt.max_code;
+        dmax = dt.max_code;
+        blmax = max_blindex;
+        bits = type == 2 ? (uint64_t)opt_len + 3 : (uint64_t)static_len + 3;
+    }
+}
+
 template <bool kWaveTrees>
 __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
     __shared__ uint32_t stg[kStgWords];
@@ -2703,67 +3086,16 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
             // ---- trees of kEncGroup blocks at once: wave w owns block g0 + w ----
             {
                 const uint32_t kb = g0 + (uint32_t)wave;
-                TreeLDS &T = TT[wave];
-                uint32_t *hl = HL[wave], *hd = HD[wave];
                 if (kb < nblk && level != 0 && !(blk[kb].flags & kBlkMarker)) {
-                    const BlockRec br = blk[kb];
-                    // histogram (_tr_tally freq updates, deflate.h:354-372)
-                    for (int i = lane; i < kLCodes; i += 64) hl[i] = 0;
-                    if (lane < kDCodes) hd[lane] = 0;
-                    __builtin_amdgcn_wave_barrier();
-                    for (uint32_t i = lane; i < br.nsym; i += 64) {
-                        const uint32_t v = sym[br.sym_start + i];
-                        const uint32_t dist = v >> 8, lc = v & 0xffu;
-                        if (dist == 0) atomicAdd(&hl[lc], 1u);
-                        else {
-                            atomicAdd(&hl[c_ct.len_code[lc] + 257], 1u);
-                            const uint32_t d = dist - 1;
-                            atomicAdd(&hd[d < 256 ? c_ct.dist_code[d] : c_ct.dist_code[256 + (d >> 7)]], 1u);
-                        }
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    for (int i = lane; i < kLCodes; i += 64) T.lfreq[i] = i == kEndBlock ? 1 : (uint16_t)hl[i];
-                    if (lane < kDCodes) T.dfreq[lane] = (uint16_t)hd[lane];
-                    if (lane < kBLCodes) T.bfreq[lane] = 0;
-                    __builtin_amdgcn_wave_barrier();
-                    int64_t opt_len = 0, static_len = 0;
-                    TreeRef lt{T.lfreq, T.ldad, T.lcode, T.llen, 0};
-                    TreeRef dt{T.dfreq, T.ddad, T.dcode, T.dlen, 0};
-                    TreeRef bt{T.bfreq, T.bdad, T.bcode, T.blen, 0};
-                    auto cnt = [&](int s, int, int) { T.bfreq[s]++; };
-                    if constexpr (kWaveTrees) {         // the whole wave builds (w_build)
-                        w_build(lt, T, kLCodes, c_ct.stat_llen, c_ct.xlbits, 257, kMaxBits, opt_len, static_len);
-                        w_build(dt, T, kDCodes, c_ct.stat_dlen, c_ct.xdbits, 0, kMaxBits, opt_len, static_len);
-                        if (lane == 0) {
-                            t_rle(T.llen, lt.max_code, cnt);
-                            t_rle(T.dlen, dt.max_code, cnt);
-                        }
-                        __builtin_amdgcn_wave_barrier();
-                        w_build(bt, T, kBLCodes, nullptr, c_ct.xblbits, 0, kMaxBLBits, opt_len, static_len);
-                    } else if (lane == 0) {             // one lane builds (t_build)
-                        t_build(lt, T, kLCodes, c_ct.stat_llen, c_ct.xlbits, 257, kMaxBits, opt_len, static_len);
-                        t_build(dt, T, kDCodes, c_ct.stat_dlen, c_ct.xdbits, 0, kMaxBits, opt_len, static_len);
-                        t_rle(T.llen, lt.max_code, cnt);
-                        t_rle(T.dlen, dt.max_code, cnt);
-                        t_build(bt, T, kBLCodes, nullptr, c_ct.xblbits, 0, kMaxBLBits, opt_len, static_len);
-                    }
+                    int type, lmax, dmax, blmax;
+                    uint64_t bits;
+                    block_plan<kWaveTrees>(job, blk[kb], sym, TT[wave], HL[wave], HD[wave], lane, type, lmax, dmax,
+                                           blmax, bits);
                     if (lane == 0) {
-                        int max_blindex;
-                        for (max_blindex = kBLCodes - 1; max_blindex >= 3; max_blindex--)
-                            if (T.blen[c_ct.bl_order[max_blindex]] != 0) break;
-                        opt_len += 3 * ((int64_t)max_blindex + 1) + 5 + 5 + 4;
-                        uint64_t opt_lenb = ((uint64_t)opt_len + 3 + 7) >> 3;
-                        const uint64_t static_lenb = ((uint64_t)static_len + 3 + 7) >> 3;
-                        if (static_lenb <= opt_lenb || job.strategy == 4) opt_lenb = static_lenb;   // trees.c:1035
-                        const uint64_t stored_len = br.in_end - br.in_start;
-                        int type;                                   // trees.c:1027-1074
-                        if (stored_len + 4 <= opt_lenb && (br.flags & kBlkStored)) type = 0;
-                        else if (static_lenb == opt_lenb) type = 1;
-                        else type = 2;
                         s_hdr[wave].type = type;
-                        s_hdr[wave].lmax = lt.max_code;
-                        s_hdr[wave].dmax = dt.max_code;
-                        s_hdr[wave].blmax = max_blindex;
+                        s_hdr[wave].lmax = lmax;
+                        s_hdr[wave].dmax = dmax;
+                        s_hdr[wave].blmax = blmax;
                     }
                 }
             }
@@ -2923,6 +3255,335 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
 }
 
 // ------------------------------------------------------------------------
+// k_enc_plan / k_enc_scan / k_enc_emit — k_encode for a sub-batch of few large
+// buffers, with a buffer's blocks spread over many workgroups instead of one:
+//   k_enc_plan  one wave per block: block_plan (trees, type, length in bits),
+//               the code tables into EncPlan records
+//   k_enc_scan  one workgroup per buffer: every block's first output bit (a
+//               stored block aligns after its 3-bit header, the last block
+//               winds up to a byte), the output length, and zeroes the words
+//               two blocks share
+//   k_enc_emit  one workgroup per block: the block's bits at its offset,
+//               written through an LDS window as k_encode does; the words a
+//               block shares with its neighbours (its first and last) are
+//               or-ed in atomically, every other word is the block's alone
+// Block 0 also writes the zlib/gzip header, the last block the trailer.
+// ------------------------------------------------------------------------
+// a buffer's block records fit its region of the block / plan arrays (n /
+// sym_limit + 2 records, zgpu_api.cpp): the plan of block nblocks is the end mark
+__device__ inline bool enc_blocks_ok(const DeflateJob &job, uint32_t bi, uint32_t nblk) {
+    const uint64_t n = job.src_len[job.first + bi];
+    return nblk >= 1 && (uint64_t)nblk + 1 <= n / job_win(job).sym_limit + 2;
+}
+
+template <bool kWaveTrees>
+__global__ __launch_bounds__(kEncThreads) void k_enc_plan(DeflateJob job) {
+    __shared__ TreeLDS TT[kEncGroup];
+    __shared__ uint32_t HL[kEncGroup][kLCodes], HD[kEncGroup][kDCodes];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t bi = blockIdx.y;
+    const uint32_t kb = blockIdx.x * kEncGroup + (uint32_t)wave;
+    const uint32_t nblk = job.nblocks[bi];
+    if (kb >= nblk || !enc_blocks_ok(job, bi, nblk)) return;   // per wave: no workgroup barrier below
+    const BlockRec br = job.blocks[job.blk_off[bi] + kb];
+    TreeLDS &T = TT[wave];
+    int type = 0, lmax = 0, dmax = 0, blmax = 0;
+    uint64_t bits = 0;
+    block_plan<kWaveTrees>(job, br, job.sym + job.ws_off[bi], T, HL[wave], HD[wave], lane, type, lmax, dmax, blmax,
+                           bits);
+    EncPlan &P = job.eplan[job.blk_off[bi] + kb];
+    __builtin_amdgcn_wave_barrier();                  // lane 0's tables (t_build) before the copy
+    type = __shfl(type, 0, 64);
+    if (lane == 0) {
+        P.type = (uint8_t)type;
+        P.lmax = (uint16_t)lmax;
+        P.dmax = (uint16_t)dmax;
+        P.blmax = (uint16_t)blmax;
+        P.bits = bits;
+    }
+    if (type == 2) {
+        for (int i = lane; i < kLCodes; i += 64) { P.lcode[i] = T.lcode[i]; P.llen[i] = T.llen[i]; }
+        if (lane < kDCodes) { P.dcode[lane] = T.dcode[lane]; P.dlen[lane] = T.dlen[lane]; }
+        if (lane < kBLCodes) { P.bcode[lane] = T.bcode[lane]; P.blen[lane] = T.blen[lane]; }
+    }
+}
+
+constexpr int kEScanThreads = 1024;
+__device__ inline uint64_t wrap_head_bits(int wrap) { return wrap == 1 ? 16 : wrap == 2 ? 80 : 0; }
+__device__ inline uint64_t wrap_tail_bits(int wrap) { return wrap == 1 ? 32 : wrap == 2 ? 64 : 0; }
+
+// zero the bytes of output word w (4-byte aligned, of the word array that
+// starts a3 bytes before the buffer's output) that lie in [lo, hi) bytes
+__device__ inline void zero_word_bytes(uint8_t *out, uint32_t a3, int64_t w, int64_t lo, int64_t hi) {
+    for (int j = 0; j < 4; j++) {
+        const int64_t b = 4 * w + j - (int64_t)a3;
+        if (b >= lo && b < hi) out[b] = 0;
+    }
+}
+
+__global__ __launch_bounds__(kEScanThreads) void k_enc_scan(DeflateJob job) {
+    __shared__ uint64_t s_v[kEScanThreads];
+    __shared__ uint32_t s_ty[kEScanThreads];
+    __shared__ uint64_t s_off;
+    const int tid = threadIdx.x;
+    const uint32_t bi = blockIdx.x, g = job.first + bi;
+    const uint32_t nblk = job.nblocks[bi];
+    const BlockRec *blk = job.blocks + job.blk_off[bi];
+    EncPlan *pl = job.eplan + job.blk_off[bi];
+    uint8_t *out = job.dst + job.dst_off[g];
+    const int64_t cap = (int64_t)job.dst_cap[g];
+    const uint32_t a3 = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 3u);
+    const uint64_t tb = wrap_tail_bits(job.wrap);
+    if (!enc_blocks_ok(job, bi, nblk)) {                   // never expected: report, write nothing
+        if (tid == 0) { job.dst_len[g] = 0; job.status[g] = -2; }
+        return;
+    }
+    if (tid == 0) s_off = wrap_head_bits(job.wrap);
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < nblk; c0 += kEScanThreads) {
+        const uint32_t m = nblk - c0 < (uint32_t)kEScanThreads ? nblk - c0 : (uint32_t)kEScanThreads;
+        if ((uint32_t)tid < m) {
+            const uint32_t k = c0 + tid;
+            const BlockRec br = blk[k];
+            const uint32_t ty = pl[k].type;
+            s_ty[tid] = ty | (br.flags & kBlkLast ? 4u : 0u);
+            s_v[tid] = ty == 0 ? br.in_end - br.in_start : pl[k].bits;
+        }
+        __syncthreads();
+        if (tid == 0) {                                    // the offsets, in order
+            uint64_t off = s_off;
+            for (uint32_t i = 0; i < m; i++) {
+                const uint64_t st = off, v = s_v[i];
+                const uint32_t ty = s_ty[i];
+                off = (ty & 3u) == 0 ? ((off + 3 + 7) & ~7ull) + 32 + 8 * v : off + v;
+                if (ty & 4u) off = (off + 7) & ~7ull;      // bi_windup
+                s_v[i] = st;
+            }
+            s_off = off;
+        }
+        __syncthreads();
+        const uint64_t after = s_off;
+        const bool fin = c0 + m == nblk;
+        if ((uint32_t)tid < m) {
+            const uint32_t k = c0 + tid;
+            const uint64_t st = s_v[tid];
+            pl[k].start = st;
+            // the block's range of output bits: block 0 from the stream
+            // header on, the last one through the trailer
+            const int64_t rs = k == 0 ? 0 : (int64_t)st;
+            const int64_t re = (uint32_t)tid + 1 < m ? (int64_t)s_v[tid + 1] : (int64_t)after + (fin ? (int64_t)tb : 0);
+            if (re > rs) {
+                const int64_t lo = rs >> 3, hi = (re + 7) >> 3 < cap ? (re + 7) >> 3 : cap;
+                const int64_t w0 = (rs + 8 * a3) >> 5, w1 = (re - 1 + 8 * a3) >> 5;
+                zero_word_bytes(out, a3, w0, lo, hi);
+                if (w1 != w0) zero_word_bytes(out, a3, w1, lo, hi);
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const uint64_t total = s_off + tb;
+        pl[nblk].start = total;                            // the last block's range end
+        const uint64_t bytes = total >> 3;
+        job.dst_len[g] = bytes <= (uint64_t)cap ? bytes : (uint64_t)cap;
+        job.status[g] = bytes <= (uint64_t)cap ? 0 : -5;
+    }
+}
+
+__global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
+    __shared__ uint32_t stg[kStgWords];
+    __shared__ uint16_t s_lcode[kLCodes], s_dcode[kDCodes], s_bcode[kBLCodes];
+    __shared__ uint8_t s_llen[kLCodes], s_dlen[kDCodes], s_blen[kBLCodes];
+    __shared__ uint32_t wsum[kEncThreads / 64];
+    __shared__ int64_t s_obit, s_sbase;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t bi = blockIdx.y, k = blockIdx.x;
+    const uint32_t nblk = job.nblocks[bi];
+    if (k >= nblk || !enc_blocks_ok(job, bi, nblk)) return;   // uniform per workgroup
+    const uint32_t g = job.first + bi;
+    const uint8_t *in = job.src + job.src_off[g];
+    const uint32_t *sym = job.sym + job.ws_off[bi];
+    const EncPlan *pl = job.eplan + job.blk_off[bi];
+    const BlockRec br = job.blocks[job.blk_off[bi] + k];
+    const bool last = br.flags & kBlkLast;
+    const int type = pl[k].type;
+    uint8_t *out = job.dst + job.dst_off[g];
+    const int64_t cap = (int64_t)job.dst_cap[g];
+    const uint32_t a3 = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 3u);
+    uint32_t *ow = reinterpret_cast<uint32_t *>(out - a3);
+    const int64_t sh = 8 * (int64_t)a3;                   // stream bit x is bit x + sh of ow[]
+    const int64_t rs = k == 0 ? 0 : (int64_t)pl[k].start, re = (int64_t)pl[k + 1].start;
+    const int64_t wfirst = (rs + sh) >> 5, wlast = (re - 1 + sh) >> 5;
+    for (int w = tid; w < kStgWords; w += kEncThreads) stg[w] = 0;
+    if (type == 2) {
+        const EncPlan &P = pl[k];
+        for (int i = tid; i < kLCodes; i += kEncThreads) { s_lcode[i] = P.lcode[i]; s_llen[i] = P.llen[i]; }
+        if (tid < kDCodes) { s_dcode[tid] = P.dcode[tid]; s_dlen[tid] = P.dlen[tid]; }
+        if (tid < kBLCodes) { s_bcode[tid] = P.bcode[tid]; s_blen[tid] = P.blen[tid]; }
+    }
+    if (tid == 0) {
+        s_sbase = ((rs + sh) >> 5) << 5;
+        s_obit = (k == 0 ? 0 : (int64_t)pl[k].start) + sh;
+    }
+    __syncthreads();
+    int64_t sbase = s_sbase;
+    auto put = [&](uint64_t v, int nb) {                  // lane 0 only; caller ensures room
+        stg_or(stg, s_obit - sbase, v);
+        s_obit += nb;
+    };
+    // completed words below aligned bit `upto` to global (all of them: fin)
+    auto eflush = [&](int64_t upto, bool fin) {
+        const int64_t rel = upto - sbase;
+        const int full = (int)(rel >> 5);
+        const int nwords = fin ? (int)((rel + 31) >> 5) : full;
+        for (int w = tid; w < nwords; w += kEncThreads) {
+            const int64_t gw = (sbase >> 5) + w;
+            const int64_t b0 = 4 * gw - (int64_t)a3;
+            uint32_t mask = 0xffffffffu;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (b0 + j < 0 || b0 + j >= cap) mask &= ~(0xffu << (8 * j));
+            const uint32_t v = stg[w] & mask;
+            if (gw == wfirst || gw == wlast) {             // shared with a neighbour: zeroed by k_enc_scan
+                if (v) atomicOr(&ow[gw], v);
+            } else if (mask == 0xffffffffu) {
+                ow[gw] = v;
+            } else {                                       // cut by the capacity: this block's bytes only
+                uint8_t *ob = reinterpret_cast<uint8_t *>(ow + gw);
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if ((mask >> (8 * j)) & 0xffu) ob[j] = (uint8_t)(v >> (8 * j));
+            }
+        }
+        __syncthreads();
+        if (!fin) {
+            const uint32_t keep = stg[full];
+            __syncthreads();
+            for (int w = tid; w < kStgWords; w += kEncThreads) stg[w] = 0;
+            __syncthreads();
+            if (tid == 0) stg[0] = keep;
+            sbase += 32ll * full;
+            __syncthreads();
+        }
+    };
+    if (tid == 0) {
+        if (k == 0 && job.wrap == 1) {                     // zlib header (deflate.c:1004-1037)
+            uint32_t header = (8u + ((uint32_t)(job.wbits - 8) << 4)) << 8;
+            const int level = job.level;
+            uint32_t flags = (job.strategy >= 2 || level < 2) ? 0u : level < 6 ? 1u : level == 6 ? 2u : 3u;
+            header |= flags << 6;
+            header += 31 - (header % 31);
+            put(header >> 8, 8);
+            put(header & 0xffu, 8);
+        } else if (k == 0 && job.wrap == 2) {              // gzip header (deflate.c:1060-1073)
+            const int level = job.level;
+            const uint32_t xfl = level == 9 ? 2u : (job.strategy >= 2 || level < 2) ? 4u : 0u;
+            put(31, 8); put(139, 8); put(8, 8); put(0, 8);
+            put(0, 32);
+            put(xfl, 8); put(3, 8);
+        }
+        const uint64_t stored_len = br.in_end - br.in_start;
+        put((uint32_t)(type << 1) + (last ? 1u : 0u), 3);
+        if (type == 0) {
+            s_obit = (s_obit + 7) & ~7ll;
+            put((uint32_t)stored_len & 0xffffu, 16);
+            put((~(uint32_t)stored_len) & 0xffffu, 16);
+        } else if (type == 2) {                            // send_all_trees (trees.c:800-824)
+            const int lcodes = pl[k].lmax + 1, dcodes = pl[k].dmax + 1, max_blindex = pl[k].blmax;
+            put((uint32_t)(lcodes - 257), 5);
+            put((uint32_t)(dcodes - 1), 5);
+            put((uint32_t)(max_blindex + 1 - 4), 4);
+            for (int r = 0; r <= max_blindex; r++) put(s_blen[c_ct.bl_order[r]], 3);
+            auto snd = [&](int sy, int xv, int xb) {
+                put(s_bcode[sy], s_blen[sy]);
+                if (xb) put((uint32_t)xv, xb);
+            };
+            t_rle(s_llen, lcodes - 1, snd);
+            t_rle(s_dlen, dcodes - 1, snd);
+        }
+    }
+    __syncthreads();
+    if (type == 0) {                                       // stored: the raw bytes
+        const int64_t len = (int64_t)(br.in_end - br.in_start);
+        int64_t copied = 0;
+        while (copied < len) {
+            eflush(s_obit, false);
+            const int64_t room = (sbase + kStgBits - 64 - s_obit) >> 3;
+            const int64_t take = (len - copied) < room ? (len - copied) : room;
+            const int64_t ob = s_obit - sbase;
+            for (int64_t i = tid; i < take; i += kEncThreads) stg_or(stg, ob + 8 * i, in[br.in_start + copied + i]);
+            __syncthreads();
+            if (tid == 0) s_obit += 8 * take;
+            __syncthreads();
+            copied += take;
+        }
+    } else {
+        const uint16_t *lcode = type == 1 ? c_ct.stat_lcode : s_lcode;
+        const uint8_t *llen = type == 1 ? c_ct.stat_llen : s_llen;
+        for (uint32_t base = 0; base < br.nsym + 1; base += kEncThreads) {   // +1: END_BLOCK
+            const uint32_t i = base + tid;
+            uint64_t v = 0;
+            int nb = 0;
+            if (i < br.nsym) {
+                const uint32_t sy = sym[br.sym_start + i];
+                const uint32_t dist = sy >> 8, lc = sy & 0xffu;
+                if (dist == 0) {
+                    v = lcode[lc]; nb = llen[lc];
+                } else {
+                    const uint32_t code = c_ct.len_code[lc];
+                    v = lcode[code + 257]; nb = llen[code + 257];
+                    const int xl = c_ct.xlbits[code];
+                    if (xl) { v |= (uint64_t)(lc - c_ct.len_base[code]) << nb; nb += xl; }
+                    const uint32_t d = dist - 1;
+                    const uint32_t dc = d < 256 ? c_ct.dist_code[d] : c_ct.dist_code[256 + (d >> 7)];
+                    const uint32_t dcv = type == 1 ? c_ct.stat_dcode[dc] : s_dcode[dc];
+                    const int dl = type == 1 ? 5 : s_dlen[dc];
+                    v |= (uint64_t)dcv << nb; nb += dl;
+                    const int xd = c_ct.xdbits[dc];
+                    if (xd) { v |= (uint64_t)(d - c_ct.dist_base[dc]) << nb; nb += xd; }
+                }
+            } else if (i == br.nsym) {
+                v = lcode[kEndBlock]; nb = llen[kEndBlock];
+            }
+            int incl = nb;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += t;
+            }
+            if (lane == 63) wsum[wave] = (uint32_t)incl;
+            __syncthreads();
+            int wpre = 0, total = 0;
+            for (int w = 0; w < kEncThreads / 64; w++) {
+                if (w < wave) wpre += (int)wsum[w];
+                total += (int)wsum[w];
+            }
+            const int excl = wpre + incl - nb;
+            if (s_obit - sbase + total + 64 > kStgBits) eflush(s_obit, false);
+            if (nb) stg_or(stg, s_obit - sbase + excl, v);
+            __syncthreads();
+            if (tid == 0) s_obit += total;
+            __syncthreads();
+        }
+    }
+    if (last) {
+        if (s_obit - sbase + 160 > kStgBits) eflush(s_obit, false);
+        if (tid == 0) {
+            s_obit = (s_obit + 7) & ~7ll;                  // bi_windup
+            const uint32_t ck = job.check[bi];
+            if (job.wrap == 1) {                           // Adler-32, big-endian (deflate.c:1253-1256)
+                put(ck >> 24, 8); put((ck >> 16) & 0xffu, 8); put((ck >> 8) & 0xffu, 8); put(ck & 0xffu, 8);
+            } else if (job.wrap == 2) {                    // CRC-32 + ISIZE, little-endian
+                put(ck, 32);
+                put((uint32_t)job.src_len[g], 32);
+            }
+        }
+        __syncthreads();
+    }
+    eflush(s_obit, true);
+}
+
+// ------------------------------------------------------------------------
 // host-side launch
 // ------------------------------------------------------------------------
 int launch_tables_upload(const CodeTables *ct, const CrcTables *) {
@@ -2933,9 +3594,16 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     const dim3 grid(job.count);
     switch (stage) {
     case 0:
+        if (job.seg && !job.lk_head) {                          // few large buffers: per segment
+            const dim3 sgrid(job.nseg);
+            if (job.hbits > 15) hipLaunchKernelGGL((k_links<2048, 65536, true>), sgrid, dim3(kLThreads), 0, st, job);
+            else hipLaunchKernelGGL((k_links<kLC, 32768, true>), sgrid, dim3(kLThreads), 0, st, job);
+            hipLaunchKernelGGL(k_count<true>, sgrid, dim3(kCntThreads), 0, st, job);
+            break;
+        }
         if (job.hbits > 15) hipLaunchKernelGGL((k_links<2048, 65536>), grid, dim3(kLThreads), 0, st, job);
         else hipLaunchKernelGGL((k_links<kLC, 32768>), grid, dim3(kLThreads), 0, st, job);
-        hipLaunchKernelGGL(k_count, grid, dim3(kCntThreads), 0, st, job);
+        hipLaunchKernelGGL(k_count<false>, grid, dim3(kCntThreads), 0, st, job);
         break;
     case 1: {
         const int wq = (int)(job.cfg.good < job.cfg.lazy) | job.cfg_q;   // the parse reads rquart (prev_length >= good)
@@ -2971,9 +3639,31 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         else hipLaunchKernelGGL(k_encode<true>, grid, dim3(kEncThreads), 0, st, job);
         break;
     }
+    case 11: {
+        const dim3 pg(job.npgrp), bg((job.maxblk + 255) / 256, job.count);
+        hipLaunchKernelGGL(k_pbig1, pg, dim3(kParseLanes), 0, st, job);
+        hipLaunchKernelGGL(k_pbig2, pg, dim3(kParseLanes), 0, st, job);
+        hipLaunchKernelGGL(k_pbig3, pg, dim3(kParseLanes), 0, st, job);
+        hipLaunchKernelGGL(k_pbig4, grid, dim3(kPScanThreads), 0, st, job);
+        hipLaunchKernelGGL(k_pbig5, pg, dim3(kParseLanes), 0, st, job);
+        hipLaunchKernelGGL(k_pbig6, bg, dim3(256), 0, st, job);
+        break;
+    }
+    case 12: {
+        // trees on the whole wave while few blocks are in flight (latency), on
+        // one lane when many are (the other waves hide it), as for k_encode
+        const dim3 plg((job.maxblk + kEncGroup - 1) / kEncGroup, job.count), eg(job.maxblk, job.count);
+        if ((uint64_t)job.maxblk * job.count < 16384)
+            hipLaunchKernelGGL(k_enc_plan<true>, plg, dim3(kEncThreads), 0, st, job);
+        else
+            hipLaunchKernelGGL(k_enc_plan<false>, plg, dim3(kEncThreads), 0, st, job);
+        hipLaunchKernelGGL(k_enc_scan, grid, dim3(kEScanThreads), 0, st, job);
+        hipLaunchKernelGGL(k_enc_emit, eg, dim3(kEncThreads), 0, st, job);
+        break;
+    }
     case 7: hipLaunchKernelGGL(k_parse_huff, grid, dim3(kHuffThreads), 0, st, job); break;
     case 8: hipLaunchKernelGGL(k_parse_rle, grid, dim3(64), 0, st, job); break;
-    case 9: hipLaunchKernelGGL(k_count, grid, dim3(kCntThreads), 0, st, job); break;
+    case 9: hipLaunchKernelGGL(k_count<false>, grid, dim3(kCntThreads), 0, st, job); break;
     case 10: hipLaunchKernelGGL(k_parse_ev, grid, dim3(64), 0, st, job); break;
     default: return -1;
     }

@@ -93,6 +93,29 @@ constexpr uint32_t kBlkMarker = 8u;
 constexpr uint32_t kEvPause = 8u;      // DeflateJob::fl_aux
 __host__ __device__ constexpr uint32_t blk_marker_kind(uint32_t flags) { return (flags >> 4) & 7u; }
 
+// k_pbig1..6 (a sub-batch of few large buffers): the segmented lazy parse's
+// per-lane state between its kernels, and per buffer
+struct PLane {
+    uint32_t e_p, e_ml, e_ms, e_av;   // where pass 1 stopped (position, match length/start, literal pending)
+    uint32_t k1;                      // pass-1 symbols staged
+    uint32_t y, sig;                  // pass 2: where the parse meets the next lane's (~0: the end), pending literal
+    uint32_t kstart, rcnt, cnt, base; // pass-1 symbols before y(i-1), run-on symbols, the lane's count, first index
+    uint32_t pad;
+};
+struct PBuf { uint32_t fail, first_end, fin, total; };
+constexpr uint32_t kParseLanesHost = 256;   // lanes (segments) per k_pbig* / k_parse_seg workgroup
+
+// k_enc_plan -> k_enc_scan -> k_enc_emit (few large buffers): one block's
+// header fields and code tables, and where its bits start
+struct EncPlan {
+    uint16_t lcode[kLCodes], dcode[kDCodes], bcode[kBLCodes];
+    uint8_t llen[kLCodes], dlen[kDCodes], blen[kBLCodes];
+    uint8_t type, pad0;
+    uint16_t lmax, dmax, blmax;
+    uint64_t bits;           // static / dynamic: the block's bits from its 3-bit header through END_BLOCK
+    uint64_t start;          // the output bit where the block's header starts; [nblocks]: the stream's end
+};
+
 // Per-buffer workspace layout for one deflate sub-batch (device arrays).
 struct DeflateJob {
     const uint8_t *src;      // batch input base
@@ -217,6 +240,18 @@ struct DeflateJob {
     // state.  A streaming job reports both as the parse leaves them in
     // flush_out[4] (prev_length | match_length << 16).
     int zp0, zm0;
+    // a batch sub-batch of few large buffers (levels 4..9, job.seg set):
+    // the lazy parse and the encoder spread each buffer over many workgroups
+    // (k_pbig*, k_enc_plan/scan/emit).  pgrp: npgrp pairs (buffer, first lane)
+    // of kParseLanes lanes, one workgroup each; a buffer has ceil(n / pseg)
+    // lanes, its lane 0 is plane[plbase[buffer]]; maxblk: the most block
+    // records a buffer may have
+    const uint32_t *pgrp;
+    uint32_t npgrp, pseg, maxblk;
+    const uint32_t *plbase;
+    PLane *plane;
+    PBuf *pbuf;
+    EncPlan *eplan;
 };
 
 // the per-job window/hash parameters (deflate.c:440-455)
@@ -294,7 +329,9 @@ size_t checksum_scratch_bytes(uint32_t count);
 // stage: 0 links, 1 match, 2 lazy parse (sequential), 3 greedy parse (heads: 128 KiB/buffer),
 //        4 encode, 5 lazy parse (segmented), 6 lazy parse fallback for buffers flagged by 5,
 //        7 huffman-only parse, 8 rle parse, 9 walk-length keys (k_count),
-//        10 huffman-only / rle parse of a flush job (sequential)
+//        10 huffman-only / rle parse of a flush job (sequential),
+//        11 lazy parse of few large buffers (k_pbig*; 6 handles its fallbacks),
+//        12 encode of few large buffers (k_enc_plan, k_enc_scan, k_enc_emit)
 int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipStream_t st);
 // a18 helpers (zgpu_helpers.hip)
 int launch_slide_hash(uint16_t *head, uint16_t *prev, uint32_t hash_size, uint32_t window_size, uint32_t wsize,
