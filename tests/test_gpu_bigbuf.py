@@ -103,3 +103,37 @@ def test_lone_64mib_l6_vs_system_zlib(zg):
     dt = time.perf_counter() - t
     print(f"lone 64 MiB L6 compress2: {n / dt / 1e6:.0f} MB/s (host buffers in and out)")
     assert rc == 0 and z == want
+
+
+def _over_4gib_input(zg):
+    """> 4 GiB: runs of 256..4095 equal bytes, with 8 MiB of generated mixed
+    text across the 1 GiB and 2 GiB marks and across 2^32 - 1 (the end of the
+    reference's first deflate() piece, compress.c:44-54)."""
+    import torch
+    rng = np.random.default_rng(17)
+    n = (4 << 30) + (96 << 20) + 12345
+    lens = rng.integers(256, 4096, n // 2048 + 16)
+    lens = lens[: np.searchsorted(np.cumsum(lens), n) + 1]
+    data = np.repeat(rng.integers(0, 256, len(lens), dtype=np.uint8), lens)[:n].copy()
+    text = torch.empty(8 << 20, dtype=torch.uint8, device="cuda")
+    for k, at in enumerate((1 << 30, 2 << 30, (1 << 32) - 1)):
+        zg.generate_dev(text, 8 << 20, 1, zg.KIND_SILESIA, seed=30 + k)
+        data[at - (4 << 20):at + (4 << 20)] = text.cpu().numpy()
+    return data.tobytes()
+
+
+def test_compress2_over_4gib_vs_system_zlib(zg):
+    """compress2 of a buffer over 4 GiB equals system zlib's
+    stream.  Python's zlib.compress feeds deflate() as compress.c does: one
+    2^32 - 1 byte Z_NO_FLUSH piece, then Z_FINISH with the rest."""
+    import hashlib
+    data = _over_4gib_input(zg)
+    print(f"\n{len(data)} bytes generated", flush=True)
+    t = time.perf_counter()
+    want = pyzlib.compress(data, 6)
+    print(f"system zlib: {len(want)} bytes in {time.perf_counter() - t:.1f} s", flush=True)
+    t = time.perf_counter()
+    rc, z = zg.compress2(data, 6)
+    print(f"libzgpu compress2: rc {rc}, {len(z)} bytes in {time.perf_counter() - t:.1f} s", flush=True)
+    assert rc == 0
+    assert len(z) == len(want) and hashlib.sha256(z).digest() == hashlib.sha256(want).digest()

@@ -1501,11 +1501,54 @@ const char *zlibVersion(void) { return ZGPU_ZLIB_VERSION; }
 
 uLong compressBound(uLong sourceLen) { return (uLong)compress_bound64(sourceLen); }
 
+// compress2 of kMaxBuffer bytes or more.  compress.c:22-59 feeds the source
+// through deflate() in uInt-sized pieces: Z_NO_FLUSH calls of 2^32 - 1 bytes,
+// then Z_FINISH with the rest, the output in pieces of at most 2^32 - 1 bytes.
+// Here the same calls go through the streaming engine, each piece further cut
+// at every 1 GiB of input, so that no job spans 4 GiB (its kernels address a
+// buffer with 32-bit positions).  Such an extra Z_NO_FLUSH call changes
+// nothing in the stream: its only effect in the reference is fill_window calls
+// at the decision points within MIN_LOOKAHEAD of its end, and at a window
+// offset S (a multiple of w_size) those slide only when the end lies in
+// (S + 2 w_size - 262, S + 2 w_size - 1] -- never for an end at a multiple of
+// w_size.  Level 0 cuts its stored blocks by the input each call
+// offers, so it is refused here (Z_MEM_ERROR) rather than cut differently.
+static int compress2_big(Bytef *dest, uLongf *destLen, const Bytef *source, uLong sourceLen, int level) {
+    if (level == 0) { *destLen = 0; return Z_MEM_ERROR; }
+    z_stream zs;
+    std::memset(&zs, 0, sizeof(zs));
+    int err = deflateInit_(&zs, level, ZGPU_ZLIB_VERSION, (int)sizeof(z_stream));
+    if (err != Z_OK) { *destLen = 0; return err; }
+    const uint64_t kUIntMax = 0xffffffffull, kStep = 1ull << 30, n = sourceLen;
+    uint64_t left = *destLen, pos = 0, piece_end = 0;
+    zs.next_out = dest;
+    zs.avail_out = 0;
+    int flush = Z_NO_FLUSH;
+    do {
+        if (zs.avail_out == 0) {
+            zs.avail_out = (uInt)(left > kUIntMax ? kUIntMax : left);
+            left -= zs.avail_out;
+        }
+        if (zs.avail_in == 0) {
+            if (pos == piece_end) piece_end = std::min(n, piece_end + kUIntMax);   // the reference's next piece
+            const uint64_t end = std::min(piece_end, (pos / kStep + 1) * kStep);
+            zs.next_in = const_cast<Bytef *>(source) + pos;
+            zs.avail_in = (uInt)(end - pos);
+            pos = end;
+            flush = pos == n ? Z_FINISH : Z_NO_FLUSH;
+        }
+        err = deflate(&zs, flush);
+    } while (err == Z_OK);
+    *destLen = zs.total_out;
+    deflateEnd(&zs);
+    return err == Z_STREAM_END ? Z_OK : err;
+}
+
 static int compress2_body(Bytef *dest, uLongf *destLen, const Bytef *source, uLong sourceLen, int level) {
     if (!destLen) return Z_STREAM_ERROR;
     if (level != Z_DEFAULT_COMPRESSION && (level < 0 || level > 9)) { *destLen = 0; return Z_STREAM_ERROR; }
     if (!dest || (sourceLen && !source)) { *destLen = 0; return Z_STREAM_ERROR; }
-    if ((uint64_t)sourceLen >= kMaxBuffer) { *destLen = 0; return Z_MEM_ERROR; }   // 32-bit kernel positions
+    if ((uint64_t)sourceLen >= kMaxBuffer) return compress2_big(dest, destLen, source, sourceLen, level);
     size_t cap = *destLen;
     const uint8_t *s = source;
     uint8_t *d = dest;

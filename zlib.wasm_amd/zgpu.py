@@ -277,7 +277,7 @@ def compress2(data, level=6, cap=None):
     out = C.create_string_buffer(max(cap, 1))
     n = C.c_ulong(cap)
     rc = L.compress2(out, C.byref(n), data, len(data), level)
-    return rc, out.raw[: n.value]
+    return rc, C.string_at(out, n.value)
 
 
 def crc32(data, crc=0):
