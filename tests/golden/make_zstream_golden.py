@@ -277,6 +277,30 @@ def sessions_r3():
         S.append({"name": f"strategy-{a}-{sa}-{sb}", "ops": [
             ["init", a, 15, 8, sa], ["deflate", part(mix, 0, 80000), 0], ["params", a, sb],
             ["deflate", part(mix, 80000, 200000), 4]]})
+    # deflatePrime with input pending (deflate.c:731-757): the bits go into
+    # bi_buf at once, after the blocks flushed so far and ahead of the block
+    # in progress
+    for lv, wb, st in ((6, -15, 0), (6, 15, 0), (1, -15, 0), (3, 31, 0), (9, -15, 1), (5, -15, 2), (4, -15, 3),
+                       (2, -15, 2)):
+        d = mix if lv >= 4 else text
+        S.append({"name": f"prime-pending-L{lv}-w{wb}-s{st}", "ops": [
+            ["init", lv, wb, 8, st], ["deflate", part(d, 0, 70000), 0], ["prime", 5, 19],
+            ["deflate", part(d, 70000, d[2]), 4]]})
+    S.append({"name": "prime-pending-twice", "ops": [
+        ["init", 6, -15, 8, 0], ["deflate", part(mix, 0, 50000), 0], ["prime", 3, 5], ["prime", 16, 0xBEEF],
+        ["deflate", part(mix, 50000, 120000), 0], ["prime", 7, 77], ["deflate", part(mix, 120000, 200000), 4]]})
+    S.append({"name": "prime-pending-then-sync", "ops": [
+        ["init", 6, -15, 8, 0], ["deflate", part(mix, 0, 90000), 0], ["prime", 6, 44],
+        ["deflate", part(mix, 90000, 150000), 2], ["deflate", part(mix, 150000, 200000), 4]]})
+    S.append({"name": "prime-pending-zero-bits", "ops": [
+        ["init", 6, -15, 8, 0], ["deflate", part(mix, 0, 60000), 0], ["prime", 0, 1],
+        ["deflate", part(mix, 60000, 200000), 4]]})
+    S.append({"name": "prime-pending-small-calls", "ops": [
+        ["init", 6, -15, 8, 0], ["deflate", part(mix, 0, 80000), 0, 3000], ["prime", 9, 300],
+        ["deflate", part(mix, 80000, 200000), 4, 3000]]})
+    S.append({"name": "prime-pending-L1-short", "ops": [
+        ["init", 1, -15, 8, 0], ["deflate", part(text, 0, 500), 0], ["prime", 4, 3],
+        ["deflate", part(text, 500, 150000), 4]]})
     return S
 
 

@@ -894,7 +894,7 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
         // k_match's clamps: the flush events only (not the Z_NO_FLUSH stops)
         std::vector<uint64_t> ml;
         for (uint32_t i = 0; i < fh->n; i++)
-            if (fh->type[i] != 0 && fh->type[i] != kEvPause) ml.push_back(fh->pos[i]);
+            if (fh->type[i] != 0 && fh->type[i] != kEvPause && fh->type[i] != kEvPrime) ml.push_back(fh->pos[i]);
         uint64_t *d_ml = d_mb + 8;
         uint64_t *d_aux = d_ml + fh->n;
         uint32_t *d_evb = reinterpret_cast<uint32_t *>(d_aux + fh->n);
@@ -1762,6 +1762,7 @@ struct internal_state {
     uint32_t exit_p = kMinMatch - 1, exit_m = kMinMatch - 1;
     uint32_t zl_p = kMinMatch - 1, zl_m = kMinMatch - 1;
     uint64_t zl_pos = ~0ull;
+    bool prime_due = false;              // a deflatePrime event no job has written yet
 };
 
 namespace {
@@ -1844,6 +1845,7 @@ int deflate_part(internal_state *s, bool closed) {
     for (size_t i = 0; i < nev; i++) {
         pos[i] = s->ev_pos[s->res_ev + i] - base;
         if (s->ev_type[s->res_ev + i] == kEvPause) aux[i] = s->ev_aux[s->res_ev + i] - base;
+        if (s->ev_type[s->res_ev + i] == kEvPrime) aux[i] = s->ev_aux[s->res_ev + i];   // value | bits << 16
     }
     const uint8_t *sp = s->in.data() + (base - s->in_base);
     size_t sl = s->in_base + s->in.size() - base;
@@ -2007,6 +2009,7 @@ int deflate_part(internal_state *s, bool closed) {
     s->job_ev = s->res_ev;
     s->job_closed = closed;
     s->stale = false;
+    s->prime_due = false;
     // the items before the resume point were handed out by earlier calls
     s->t -= (size_t)(s->res_item + 1);
     s->res_item = -1;
@@ -2409,6 +2412,7 @@ int run_items(z_streamp strm, internal_state *s, uint32_t own, bool *full) {
         queue_to(s, (size_t)(it.end_bit >> 3));
         drain(strm, s);
         if (it.kind == kItMarker) {               // block_done: the flush's marker (deflate.c:1211-1233)
+            if (s->ev_type[it.ev] == kEvPrime) continue;   // a deflatePrime's bits (the parse stands behind them)
             s->rd = it.in_end;
             if (it.ev != own) continue;           // an earlier flush left without bits (Z_BLOCK)
             s->ev_done = own + 1;
@@ -2581,7 +2585,7 @@ static int deflate_body(z_streamp strm, int flush) {
         // block holds lit_bufsize - 1 symbols, each covering >= 1 input byte
         // below P) hands out nothing: no job
         bool skip = false;
-        if (flush == Z_NO_FLUSH && s->t == s->items.size() && !s->job_closed) {
+        if (flush == Z_NO_FLUSH && s->t == s->items.size() && !s->job_closed && !s->prime_due) {
             size_t x0 = s->res_pos;
             for (size_t k = s->t; k-- > 0;)
                 if (s->items[k].kind != kItStop) { x0 = (size_t)s->items[k].in_end; break; }
@@ -2894,7 +2898,34 @@ int deflatePrime(z_streamp strm, int bits, int value) {
     if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
     if (bits < 0 || bits > 16) return Z_BUF_ERROR;
-    if (s->finished || pending_input(s)) return unsupported(strm, "deflatePrime: input pending since the last flush");
+    // deflate.c:741-744: no room ahead of the symbol buffer for more bits (the
+    // pending output handed out so far reaches into it)
+    const size_t lit_bufsize = size_t(1) << (s->mem_level + 6);
+    if (s->out_pos < s->out.size() && s->out_pos + 2 > lit_bufsize) return Z_BUF_ERROR;
+    if (!s->finished && pending_input(s)) {
+        // With input pending the reference writes the bits into bi_buf at
+        // once: after the blocks flushed so far, ahead of the block in
+        // progress.  The parse stands at the last call's stop there; the bits
+        // become an event at that stop (kEvPrime), which the next job's parse
+        // turns into a marker record that k_encode writes.
+        if (s->level == 0 || s->ev_type.empty() || s->ev_done != s->ev_type.size() || s->tentative ||
+            (s->ev_type.back() != 0 && s->ev_type.back() != kEvPrime))
+            return unsupported(strm, "deflatePrime: input pending after a call that did not reach its end");
+        if (bits == 0) return Z_OK;
+        try {
+            const uint32_t v = (uint32_t)value & ((1u << bits) - 1u);
+            s->ev_pos.push_back(s->ev_pos.back());
+            s->ev_type.push_back(kEvPrime);
+            s->ev_aux.push_back((uint64_t)v | ((uint64_t)bits << 16));
+            s->ev_done = s->ev_type.size();
+            s->stale = true;
+            s->prime_due = true;
+            return Z_OK;
+        } catch (const std::bad_alloc &) {
+            return Z_MEM_ERROR;
+        }
+    }
+    if (s->finished) return unsupported(strm, "deflatePrime: after Z_STREAM_END");
     try {
         uint32_t nb = (uint32_t)(s->res_bits & 7);
         uint64_t acc = (s->res_byte & ((1u << nb) - 1u)) | ((uint64_t)((uint32_t)value & ((1u << bits) - 1u)) << nb);

@@ -722,8 +722,11 @@ struct FlushEv {
     uint32_t n, i;
     // a flush call's input ends at p
     __device__ inline bool at(int64_t p) const {
-        return i < n && kind() != 0 && kind() != kEvPause && (int64_t)ufl64(pos[i]) == p;
+        return i < n && kind() != 0 && kind() != kEvPause && kind() != kEvPrime && (int64_t)ufl64(pos[i]) == p;
     }
+    // a deflatePrime call right after the stop just passed (kEvPrime)
+    __device__ inline bool prime() const { return i < n && kind() == kEvPrime; }
+    __device__ inline uint32_t prime_arg() const { return (uint32_t)ufl64(aux[i]); }
     // the end of a Z_NO_FLUSH call's input, reached: all of it read (E == lim)
     __device__ inline bool stop_at(int64_t e, int64_t lim) const { return i < n && kind() == 0 && e == lim; }
     // the block just flushed ends where a call stopped on a full output buffer
@@ -911,15 +914,16 @@ struct ParseOutT {
         blk_nsym = 0;
     }
     // the bits a deflate(flush) call appends after its blocks (kBlkMarker)
-    __device__ inline void marker(P strstart, uint32_t kind) {
+    // (a prime's marker stands inside the block in progress: no resume point)
+    __device__ inline void marker(P strstart, uint32_t kind, uint32_t arg = 0) {
         BlockRec r;
         r.sym_start = blk_sym_start;
         r.nsym = 0;
         r.in_start = r.in_end = (uint64_t)strstart;
         r.flags = kBlkMarker | (kind << 4);
-        r.pad = 0;
+        r.pad = arg;
         if (lead) blk[nblk] = r;
-        rec(strstart, true);
+        rec(strstart, kind != kMarkPrime);
         nblk++;
     }
     // fill_window (deflate.c:251-368), bookkeeping only; n = the end of the
@@ -980,17 +984,17 @@ struct ParseU {                     // wave-uniform parse output state
         nsym++;
         return ++blk_nsym == sym_limit;
     }
-    __device__ inline void marker(uint32_t strstart, uint32_t kind, int lane) {   // see ParseOut::marker
+    __device__ inline void marker(uint32_t strstart, uint32_t kind, int lane, uint32_t arg = 0) {   // see ParseOut::marker
         if (lane == 0) {
             BlockRec r;
             r.sym_start = blk_sym_start;
             r.nsym = 0;
             r.in_start = r.in_end = strstart;
             r.flags = kBlkMarker | (kind << 4);
-            r.pad = 0;
+            r.pad = arg;
             blk[nblk] = r;
         }
-        rec(strstart, true, lane);
+        rec(strstart, kind != kMarkPrime, lane);
         nblk++;
     }
     __device__ inline void fill(uint32_t p, uint32_t n) {                   // fill_window bookkeeping
@@ -1103,6 +1107,11 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
                 while (fe.stop_at(po.E, lim) && po.E - p < (uint32_t)kMinLookahead) {
                     if (lane == 0 && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
                     fe.i++;
+                    while (fe.prime()) {                          // deflatePrime: its bits go out here
+                        if (lane == 0 && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+                        po.marker(p, kMarkPrime, lane, fe.prime_arg());
+                        fe.i++;
+                    }
                     if (fe.i == fe.n && job.open_end) { done = true; break; }
                     lim = (uint32_t)fe.limit(n);
                     po.fill(p, lim);
@@ -2065,6 +2074,11 @@ __global__ __launch_bounds__(64) void k_parse_ev(DeflateJob job) {
             while (fe.stop_at(po.E, lim) && (rle ? po.E - p <= kMaxMatch : po.E == p)) {
                 if (job.ev_blk) job.ev_blk[fe.i] = po.nblk;
                 fe.i++;
+                while (fe.prime()) {                              // deflatePrime: its bits go out here
+                    if (job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+                    po.marker(p, kMarkPrime, fe.prime_arg());
+                    fe.i++;
+                }
                 if (fe.i == fe.n && job.open_end) { done = true; break; }
                 lim = fe.limit(n);
                 po.fill(p, lim);
@@ -2306,6 +2320,11 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
             while (kEv && fe.stop_at(po.E, lim) && po.E - p < kMinLookahead) {
                 if (lead && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
                 fe.i++;
+                while (fe.prime()) {                              // deflatePrime: its bits go out here
+                    if (lead && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+                    po.marker(p, kMarkPrime, fe.prime_arg());
+                    fe.i++;
+                }
                 if (fe.i == fe.n && job.open_end) { done = true; break; }
                 lim = (P)fe.limit(n);
                 fill();
@@ -3119,6 +3138,9 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
                         s_obit = (s_obit + 7) & ~7ll;
                         put(0, 16);
                         put(0xffffu, 16);
+                    } else if (kind == kMarkPrime) {       // deflatePrime's bits (deflate.c:731-757)
+                        const uint32_t nb = br.pad >> 16;
+                        if (nb) put(br.pad & ((1u << nb) - 1u), (int)nb);
                     }
                     stream_rec(k);
                 }

@@ -91,6 +91,12 @@ constexpr uint32_t kBlkStored = 2u;   // stored-eligible (block_start still in t
 // stored block), Z_BLOCK 5 (nothing).
 constexpr uint32_t kBlkMarker = 8u;
 constexpr uint32_t kEvPause = 8u;      // DeflateJob::fl_aux
+// a deflatePrime call with input pending (deflate.c:731-757): an event at the
+// stop of the deflate() call before it, fl_aux = value | bits << 16; the parse
+// writes a marker of kind kMarkPrime there (its bits in BlockRec::pad), which
+// k_encode turns into the bits, ahead of the block in progress
+constexpr uint32_t kEvPrime = 16u;
+constexpr uint32_t kMarkPrime = 6u;
 __host__ __device__ constexpr uint32_t blk_marker_kind(uint32_t flags) { return (flags >> 4) & 7u; }
 
 // k_pbig1..6 (a sub-batch of few large buffers): the segmented lazy parse's
