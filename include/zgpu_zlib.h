@@ -115,7 +115,7 @@ int deflateReset(z_streamp strm);                                       /* zlib.
 int deflateCopy(z_streamp dest, z_streamp source);                      /* zlib.h:603 */
 int deflatePending(z_streamp strm, unsigned *pending, int *bits);       /* zlib.h:746 */
 
-/* gzip header (zlib.h gz_header) for deflateSetHeader */
+/* gzip header (zlib.h gz_header) for deflateSetHeader / inflateGetHeader */
 typedef struct gz_header_s {
     int text;
     uLong time;
@@ -170,6 +170,12 @@ int inflateInit2_(z_streamp strm, int windowBits, const char *version,
 int inflate(z_streamp strm, int flush);                                 /* zlib.h:405 */
 int inflateEnd(z_streamp strm);                                         /* zlib.h:525 */
 int inflateReset(z_streamp strm);                                       /* zlib.h:980 */
+int inflateGetHeader(z_streamp strm, gz_headerp head);                  /* zlib.h inflateGetHeader; inflate.c:1330 */
+int inflateSync(z_streamp strm);                                        /* zlib.h inflateSync; inflate.c:1375 */
+int inflateCopy(z_streamp dest, z_streamp source);                      /* zlib.h inflateCopy; inflate.c:1439 */
+/* inflate(flush): Z_NO_FLUSH, Z_SYNC_FLUSH, Z_FINISH and Z_BLOCK (stop at the
+ * next block boundary, or after a zlib / gzip header; strm->data_type as
+ * inflate.c sets it there); Z_TREES is refused (Z_STREAM_ERROR) */
 
 #define inflateInit(strm) \
     inflateInit_((strm), ZGPU_ZLIB_VERSION, (int)sizeof(z_stream))

@@ -99,17 +99,20 @@ def test_no_probe_or_variant_kernels_shipped():
 
 
 def test_oversize_buffers_refused_before_gpu_work(lib):
-    """Kernels address a buffer with 32-bit positions: buffers of 4 GiB - 64 KiB
-    or more are refused up front, never truncated into a stream that
-    covers only n mod 2^32 bytes.  The guard fires before any device access, so
-    a small real buffer passed with a huge length is never read."""
+    """Kernels address a buffer with 32-bit positions.  The batch API refuses
+    buffers of 4 GiB - 64 KiB or more up front, never truncating
+    them into a stream that covers only n mod 2^32 bytes; compress2 takes them
+    through the streaming engine in compress.c's pieces (levels 1-9, checked
+    against system zlib on the GPU: test_gpu_bigbuf.py) and refuses level 0,
+    whose stored blocks follow the pieces' input.  Both refusals fire before
+    any access, so a small real buffer passed with a huge length is never read."""
     buf = C.create_string_buffer(64)
     out = C.create_string_buffer(64)
     big = (1 << 32) + 5
     lib.compress2.restype = C.c_int
     lib.compress2.argtypes = [C.c_void_p, C.POINTER(C.c_ulong), C.c_void_p, C.c_ulong, C.c_int]
     dl = C.c_ulong(64)
-    assert lib.compress2(out, C.byref(dl), buf, big, 6) == -4 and dl.value == 0      # Z_MEM_ERROR
+    assert lib.compress2(out, C.byref(dl), buf, big, 0) == -4 and dl.value == 0      # Z_MEM_ERROR
     lib.zgpu_compress_batch.restype = C.c_int
     src = (C.c_void_p * 1)(C.cast(buf, C.c_void_p))
     dst = (C.c_void_p * 1)(C.cast(out, C.c_void_p))

@@ -65,3 +65,26 @@ def test_inflate_with_dictionary(zg):
     _, z = run_zsession(L, [("init", 6, -15, 8, 0), ("dict", dic), ("deflate", data, 4)])
     rcs, out = run_isession(L, z, -15, dic, 3000)
     assert out == data and rcs[-1] == 1
+
+
+def test_inflate_api_sessions_golden(zg):
+    """inflate(Z_BLOCK), inflateGetHeader, inflateSync and inflateCopy
+    (inflate.c:1267-1269, :1330, :1375, :1439) replayed on libzgpu.so against
+    the compiled reference's results (tests/golden/isession_golden.json): every
+    call's return code, avail_in, total_in, total_out and (Z_BLOCK) data_type,
+    each stream's output, the gz_header fields."""
+    import json
+    import os
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, "golden"))
+    from make_isession_golden import run
+    g = json.load(open(os.path.join(here, "golden", "isession_golden.json")))
+    L = zg.load()
+    bad = []
+    for sess in g["sessions"]:
+        r = run(L, sess)
+        if r["res"] != sess["res"] or r["outs"] != sess["outs"] or r["hdr"] != sess["hdr"]:
+            bad.append(sess["name"])
+    print("BAD SESSIONS:", bad)
+    assert not bad

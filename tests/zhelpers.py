@@ -366,7 +366,9 @@ def _bind_zstream(L):
             ("inflateInit2_", C.c_int, [P, C.c_int, C.c_char_p, C.c_int]),
             ("inflate", C.c_int, [P, C.c_int]), ("inflateEnd", C.c_int, [P]),
             ("inflateSetDictionary", C.c_int, [P, C.c_void_p, C.c_uint]),
-            ("deflateBound", C.c_ulong, [P, C.c_ulong])):
+            ("deflateBound", C.c_ulong, [P, C.c_ulong]),
+            ("inflateGetHeader", C.c_int, [P, C.POINTER(GzHeader)]),
+            ("inflateSync", C.c_int, [P]), ("inflateCopy", C.c_int, [P, P])):
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
@@ -485,6 +487,108 @@ def run_isession(L, z, wbits=15, dictionary=None, chunk=1 << 30, version=b"1.3.1
             break
     L.inflateEnd(C.byref(s))
     return rcs, bytes(out)
+
+
+def run_iops(L, z, ops, version=b"1.3.1.1-motley"):
+    """A scripted z_stream inflate session over the compressed bytes z on
+    library L (the reference or libzgpu.so); returns (per-op results, the
+    output of each stream, the gz_header fields).  ops:
+      ("init", windowBits)            inflateInit2_
+      ("header", extra_max, name_max, comm_max)   inflateGetHeader
+      ("feed", n)                     n more bytes of z become available input
+      ("skip", n)                     the next n bytes of z are dropped (a damaged stretch)
+      ("inflate", flush, out)         one call with `out` bytes of output space
+      ("loop", flush, out)            calls until Z_STREAM_END, an error, or a call that
+                                      makes no progress
+      ("sync",)                       inflateSync
+      ("copy",)                       inflateCopy of the active stream; ("use", k) drives stream k
+      ("dict", hex)                   inflateSetDictionary
+    Each call records (rc, avail_in, total_in, total_out[, data_type when the
+    flush is Z_BLOCK and rc is Z_OK]), inflateSync (rc, avail_in, total_in)."""
+    _bind_zstream(L)
+    zb = C.create_string_buffer(bytes(z), max(len(z), 1))
+    base = C.addressof(zb)
+    streams = [ZStream()]
+    outs = [bytearray()]
+    cur = [0]
+    act = 0
+    end = 0                              # end of the input made available so far
+    res, keep = [], []
+    hdr = None
+
+    def call(flush, n):
+        nonlocal end
+        s = streams[act]
+        ob = C.create_string_buffer(max(n, 1))
+        s.next_out, s.avail_out = C.addressof(ob), n
+        rc = L.inflate(C.byref(s), flush)
+        outs[act].extend(ob.raw[: n - s.avail_out])
+        got = n - s.avail_out
+        r = [rc, s.avail_in, s.total_in, s.total_out]
+        if flush == 5 and rc == 0:
+            r.append(s.data_type)
+        return r, got
+
+    for op in ops:
+        k = op[0]
+        s = streams[act]
+        if k == "init":
+            res.append(L.inflateInit2_(C.byref(s), op[1], version, C.sizeof(ZStream)))
+            s.next_in, s.avail_in = base, 0
+        elif k == "header":
+            hdr = GzHeader()
+            bufs = [C.create_string_buffer(b"\xee" * max(m, 1), max(m, 1)) for m in op[1:4]]
+            keep.extend(bufs)
+            hdr.extra, hdr.extra_max = C.addressof(bufs[0]), op[1]
+            hdr.name, hdr.name_max = C.addressof(bufs[1]), op[2]
+            hdr.comment, hdr.comm_max = C.addressof(bufs[2]), op[3]
+            hdr.done = 7
+            hdr._bufs = bufs
+            res.append(L.inflateGetHeader(C.byref(s), C.byref(hdr)))
+        elif k in ("feed", "skip"):
+            at = (s.next_in or base) - base
+            if k == "skip":
+                at = min(len(z), at + op[1])
+                end = max(end, at)
+            else:
+                end = min(len(z), max(end, at) + op[1])
+            s.next_in, s.avail_in = base + at, end - at
+        elif k == "inflate":
+            r, _ = call(op[1], op[2])
+            res.append(r)
+        elif k == "loop":
+            seq = []
+            for _ in range(100000):
+                r, got = call(op[1], op[2])
+                seq.append(r)
+                if r[0] != 0 or (got == 0 and streams[act].avail_in == 0):
+                    break
+            res.append(seq)
+        elif k == "sync":
+            rc = L.inflateSync(C.byref(s))
+            res.append([rc, s.avail_in, s.total_in])
+        elif k == "copy":
+            d = ZStream()
+            res.append(L.inflateCopy(C.byref(d), C.byref(s)))
+            streams.append(d)
+            outs.append(bytearray())
+        elif k == "use":
+            act = op[1]
+        elif k == "dict":
+            d = bytes.fromhex(op[1])
+            res.append(L.inflateSetDictionary(C.byref(s), d, len(d)))
+        else:
+            raise ValueError(k)
+    for s in streams:
+        L.inflateEnd(C.byref(s))
+    fields = None
+    if hdr is not None:
+        raw = lambda p, m: None if not p else C.string_at(p, m).hex()
+        fields = {"text": hdr.text, "time": hdr.time, "xflags": hdr.xflags, "os": hdr.os,
+                  "extra_len": hdr.extra_len, "extra": raw(hdr.extra, hdr.extra_max),
+                  "name": raw(hdr.name, hdr.name_max), "comment": raw(hdr.comment, hdr.comm_max),
+                  "hcrc": hdr.hcrc, "done": hdr.done}
+    return res, [bytes(o) for o in outs], fields
 
 
 def run_dsession(L, data, plan, level=6, wbits=15, mem=8, strategy=0, version=b"1.3.1.1-motley",

@@ -1006,6 +1006,8 @@ struct InflateResumeDev {          // InflateJob's resume arrays (device, per st
     const uint64_t *res_bit;
     const uint32_t *res_hist;
     uint64_t *blk_out;
+    uint32_t stop_mode;            // InflateJob::stop_mode
+    uint64_t *zstate_out;          // InflateJob::zstate_out
 };
 
 int inflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
@@ -1067,6 +1069,8 @@ int inflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.res_bit = rs->res_bit;
             job.res_hist = rs->res_hist;
             job.blk_out = rs->blk_out;
+            job.stop_mode = rs->stop_mode;
+            job.zstate_out = rs->zstate_out;
         }
         if (T.run(3, st, [&] { return launch_inflate_stage(0, job, st); })) return ZGPU_MEM_ERROR;
         if (T.run(4, st, [&] { return launch_inflate_stage(1, job, st); })) return ZGPU_MEM_ERROR;
@@ -1149,10 +1153,12 @@ struct InflateTry {
     uint32_t stop;
     int status;
     uint64_t put, used, blk_bit, blk_put;
+    uint64_t zstate;               // InflateJob::zstate_out
 };
 
 int inflate_try_locked(Ctx &c, const uint8_t *in, size_t n, bool resume, uint64_t start_bit, const uint8_t *hist,
-                       size_t hist_len, size_t cap, int wrap, int wbits, std::vector<uint8_t> &out, InflateTry &t) {
+                       size_t hist_len, size_t cap, int wrap, int wbits, std::vector<uint8_t> &out, InflateTry &t,
+                       uint32_t stop_mode = 0) {
     if (!c.ws_io.ensure(n + 64) || !c.ws_io2.ensure(cap + 64) || !c.ws_small.ensure(8 * 16 + 64) ||
         !c.ws_istop.ensure(64))
         return ZGPU_MEM_ERROR;
@@ -1162,6 +1168,7 @@ int inflate_try_locked(Ctx &c, const uint8_t *in, size_t n, bool resume, uint64_
     uint64_t *d_rbit = m + 7;
     uint32_t *d_hist = reinterpret_cast<uint32_t *>(m + 8);
     uint64_t *d_blk = m + 9;
+    uint64_t *d_zs = m + 11;
     uint32_t *d_stop = c.ws_istop.as<uint32_t>();
     hipStream_t st = c.own;
     const uint64_t meta[4] = {0, (uint64_t)n, 0, (uint64_t)cap};
@@ -1173,15 +1180,15 @@ int inflate_try_locked(Ctx &c, const uint8_t *in, size_t n, bool resume, uint64_
         hipMemcpyAsync(d_rbit, &rbit, 8, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(d_hist, &hl, 4, hipMemcpyHostToDevice, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
-    const InflateResumeDev rs{resume ? d_rbit : nullptr, resume ? d_hist : nullptr, d_blk};
+    const InflateResumeDev rs{resume ? d_rbit : nullptr, resume ? d_hist : nullptr, d_blk, stop_mode, d_zs};
     int rc = inflate_dev_locked(c, d_in, m, m + 1, d_out, m + 2, m + 3, m + 4, m + 5, d_st, d_stop, 1,
                                 resume ? 0 : wrap, wbits, st, &rs);
     if (rc) return rc;
-    uint64_t res[2], blk[2];
+    uint64_t res[2], blk[3];
     int32_t status = 0;
     uint32_t stop = 0;
     if (copy_sync(res, m + 4, 16, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        copy_sync(blk, d_blk, 16, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        copy_sync(blk, d_blk, 24, hipMemcpyDeviceToHost, st) != hipSuccess ||
         copy_sync(&status, d_st, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         copy_sync(&stop, d_stop, 4, hipMemcpyDeviceToHost, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
@@ -1193,6 +1200,7 @@ int inflate_try_locked(Ctx &c, const uint8_t *in, size_t n, bool resume, uint64_
     t.used = res[1];
     t.blk_bit = blk[0];
     t.blk_put = blk[1];
+    t.zstate = blk[2];
     return ZGPU_OK;
 }
 
@@ -1749,6 +1757,17 @@ struct internal_state {
     uint32_t dict_id = 0;
     bool need_dict = false;              // inflate: Z_NEED_DICT answered, waiting for the dictionary
     uint32_t want_dict = 0;              // its DICTID
+    gz_header *ihead = nullptr;          // inflateGetHeader: filled as the gzip header arrives
+    // inflateSync (inflate.c:1375-1437): the search's progress (bytes of
+    // 00 00 ff ff seen), and after a sync point was found the stream's tail
+    // rule: 1 the trailer is read but not checked, 2 no trailer (no header had
+    // been read: the rest is raw)
+    bool isyncing = false;
+    uint32_t isync_have = 0;
+    int isync = 0;
+    int idt = 0;                         // strm->data_type at the last inflate(Z_BLOCK) stop
+    bool itype = false;                  // the resume point is a block boundary (inflate.c mode TYPE)
+    bool itail = false;                  // Z_BLOCK stopped after the last block: the trailer is next
     // configuration rows changed with input pending (deflateParams within the
     // same function, deflateTune; deflate.c:760-820): row cfg_row[k] governs
     // the current part's decision points from part position cfg_pos[k] on,
@@ -3070,6 +3089,8 @@ int inflateReset(z_streamp strm) {
     s->out_pos = 0; s->finished = 0; s->tried = 0; s->cap = 0; s->result = Z_OK;
     s->in_base = 0; s->imode = 0; s->igz = 0; s->res_bit = s->res_put = s->ideliv = 0; s->icheck = 0;
     s->need_dict = false; s->want_dict = 0;
+    s->ihead = nullptr;                                                // inflateResetKeep: head = Z_NULL
+    s->isyncing = false; s->isync_have = 0; s->isync = 0; s->idt = 0; s->itype = false; s->itail = false;
     strm->total_in = strm->total_out = 0;
     strm->msg = nullptr;
     strm->adler = s->wrap & 1;
@@ -3081,13 +3102,49 @@ namespace {
 // far: from the stream start until a block is complete, then from the last
 // block boundary.  Sets s->out (bytes not handed out yet), s->finished and
 // s->result; `took` input bytes of this call may be handed back past the end.
-int inflate_attempt(z_streamp strm, internal_state *s, size_t took) {
+int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block = false) {
     const uint64_t in_end = s->in_base + s->in.size();
     if (s->cap == 0) s->cap = std::max<size_t>(4 * s->in.size(), 1 << 16);
     const bool is_check = s->wrap != 0;
     auto check_of = [&](uint32_t init, const uint8_t *p, size_t n) -> uint32_t {
         return s->igz ? (uint32_t)crc32_z(init, p, n) : (uint32_t)adler32_z(init, p, n);
     };
+    if (s->itail) {
+        // the last block is out (an inflate(Z_BLOCK) stopped after it): the
+        // trailer, byte aligned after it (inflate.c TYPEDO .. LENGTH)
+        const uint64_t tpos = (s->res_bit + 7) >> 3;
+        const uint64_t need = !s->wrap || s->isync == 2 ? 0 : s->igz ? 8 : 4;
+        if (in_end < tpos + need) {
+            s->tried = in_end;
+            return Z_OK;
+        }
+        const uint8_t *tr = s->in.data() + (tpos - s->in_base);
+        bool ok = true;
+        if (!s->isync && need == 4) {
+            ok = ((uint32_t)tr[0] << 24 | (uint32_t)tr[1] << 16 | (uint32_t)tr[2] << 8 | tr[3]) == s->icheck;
+            if (!ok) strm->msg = const_cast<char *>("incorrect data check");
+        } else if (!s->isync && need == 8) {
+            const uint32_t c = tr[0] | (uint32_t)tr[1] << 8 | (uint32_t)tr[2] << 16 | (uint32_t)tr[3] << 24;
+            const uint32_t z = tr[4] | (uint32_t)tr[5] << 8 | (uint32_t)tr[6] << 16 | (uint32_t)tr[7] << 24;
+            ok = c == s->icheck && z == (uint32_t)s->res_put;
+            if (!ok) strm->msg = const_cast<char *>(c != s->icheck ? "incorrect data check" : "incorrect length check");
+        }
+        s->finished = 1;
+        s->itail = false;
+        if (ok) {
+            const uint64_t used = tpos + need;
+            const size_t back = (size_t)std::min<uint64_t>(in_end - used, took);
+            strm->next_in -= back;
+            strm->avail_in += (uInt)back;
+            strm->total_in = used;
+            if (s->wrap && !s->isync) strm->adler = s->icheck;
+            s->result = Z_STREAM_END;
+        } else {
+            s->result = Z_DATA_ERROR;
+        }
+        s->in.clear();
+        return Z_OK;
+    }
     for (;;) {
         const bool resume = s->imode == 1;
         const size_t hl = resume ? s->hist.size() : 0;
@@ -3097,9 +3154,12 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took) {
         {
             Lease L;
             rc = L.rc;
+            // inflate(Z_BLOCK): stop after the header (zlib / gzip, from the
+            // start) or at the end of the next block
+            const uint32_t mode = !block ? 0u : ((!resume && s->wrap) ? 1u : 2u) | (resume && s->itype ? 4u : 0u);
             if (!rc) rc = inflate_try_locked(*L.c, s->in.data(), s->in.size(), resume,
                                              resume ? s->res_bit - 8ull * s->in_base : 0, s->hist.data(), hl,
-                                             hl + s->cap, s->wrap, s->wbits, o, t);
+                                             hl + s->cap, s->wrap, s->wbits, o, t, mode);
         }
         if (rc) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : rc;
         if (t.stop == kIFull) {                                  // grow the output and decode again
@@ -3118,6 +3178,42 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took) {
                                            o.begin() + (std::ptrdiff_t)(upto - obase));
         };
         const uint64_t put_abs = obase + t.put;
+        if (t.stop == kIBlock) {
+            // inflate(Z_BLOCK) at a block boundary (or before the first block):
+            // the output through it, the resume point there, and the input after
+            // the byte holding the boundary handed back -- the reference stops
+            // there with that byte's unused bits in its bit buffer
+            // (strm->data_type = bits + 128, inflate.c:1267-1269)
+            append_new(put_abs);
+            uint64_t bb = t.blk_bit, bp = t.blk_put;
+            if (resume) { bb += 8ull * s->in_base; bp += obase; }
+            if (!resume) {
+                s->igz = (s->wrap & 2) && s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b;
+                s->icheck = s->igz ? 0u : 1u;
+            }
+            if (is_check && !s->isync)
+                s->icheck = check_of(s->icheck, o.data() + (s->res_put - obase), (size_t)(bp - s->res_put));
+            const uint64_t h0 = bp > 32768 ? bp - 32768 : 0;
+            s->hist.assign(o.begin() + (std::ptrdiff_t)(h0 - obase), o.begin() + (std::ptrdiff_t)(bp - obase));
+            s->res_bit = bb;
+            s->res_put = bp;
+            s->imode = 1;
+            const uint64_t used_abs = (bb + 7) >> 3;
+            const size_t back = (size_t)std::min<uint64_t>(in_end - used_abs, took);
+            strm->next_in -= back;
+            strm->avail_in += (uInt)back;
+            strm->total_in -= back;
+            s->in.resize(s->in.size() - back);
+            const uint64_t drop = (bb >> 3) - s->in_base;         // input before the boundary's byte
+            s->in.erase(s->in.begin(), s->in.begin() + (std::ptrdiff_t)drop);
+            s->in_base += drop;
+            s->tried = 0;
+            s->itype = true;
+            const bool last = (t.zstate >> 32) & 1u;
+            s->itail = last;                                     // only the trailer is left
+            s->idt = (int)((8 - (bb & 7)) & 7) + (last ? 64 : 0) + 128;
+            return Z_OK;
+        }
         if (!resume && t.stop == kIDict) {
             // a zlib header with FDICT: Z_NEED_DICT with the header (2 bytes +
             // DICTID) consumed and the rest handed back (inflate.c DICTID/DICT);
@@ -3164,7 +3260,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took) {
         }
         if (resume && t.stop == kIEnd) {                         // the final block: check the trailer
             const uint64_t tpos = s->in_base + t.used;
-            const uint64_t need = !s->wrap ? 0 : s->igz ? 8 : 4;
+            const uint64_t need = !s->wrap || s->isync == 2 ? 0 : s->igz ? 8 : 4;
             if (in_end >= tpos + need) {
                 append_new(put_abs);
                 s->finished = 1;
@@ -3173,7 +3269,9 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took) {
                 if (is_check) ck = check_of(ck, o.data() + (s->res_put - obase), (size_t)(put_abs - s->res_put));
                 const uint8_t *tr = s->in.data() + (tpos - s->in_base);
                 bool ok = true;
-                if (s->wrap && !s->igz) {
+                if (s->isync) {
+                    // after inflateSync the trailer is read, not checked (wrap &= ~4)
+                } else if (s->wrap && !s->igz) {
                     ok = ((uint32_t)tr[0] << 24 | (uint32_t)tr[1] << 16 | (uint32_t)tr[2] << 8 | tr[3]) == ck;
                     if (!ok) strm->msg = const_cast<char *>("incorrect data check");
                 } else if (s->igz) {
@@ -3188,7 +3286,8 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took) {
                     strm->next_in -= back;
                     strm->avail_in += (uInt)back;
                     strm->total_in = used;
-                    if (s->wrap) strm->adler = ck;
+                    if (s->wrap && !s->isync) strm->adler = ck;
+                    s->idt = 64;                                 // the last block, done
                 } else {
                     s->result = Z_DATA_ERROR;
                 }
@@ -3201,6 +3300,8 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took) {
         // the stream goes on: hand out its prefix, move the resume point
         append_new(put_abs);
         s->tried = in_end;
+        if (block)                                               // where the input ran out (inflate.c:1267-1269)
+            s->idt = (int)(t.zstate & 0xffffffffu) + ((t.zstate >> 32) & 1u ? 64 : 0) + ((t.zstate >> 33) & 1u ? 128 : 0);
         uint64_t bb = t.blk_bit, bp = t.blk_put;
         if (resume) { bb += 8ull * s->in_base; bp += obase; }
         if (bb && bb > s->res_bit) {
@@ -3214,6 +3315,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took) {
             s->res_bit = bb;
             s->res_put = bp;
             s->imode = 1;
+            s->itype = true;
             const uint64_t drop = (bb >> 3) - s->in_base;        // input before the boundary's byte
             s->in.erase(s->in.begin(), s->in.begin() + (std::ptrdiff_t)drop);
             s->in_base += drop;
@@ -3223,28 +3325,98 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took) {
 }
 }  // namespace
 
+// The gzip header as far as it has arrived, into inflateGetHeader's gz_header
+// (inflate.c HEAD .. HCRC: text, time, xflags, os, extra_len, extra / name /
+// comment up to their max, hcrc, done = 1 once complete; done = -1 for a zlib
+// stream; extra / name / comment set to Z_NULL when the flag is absent).
+void gz_header_fill(internal_state *s) {
+    gz_header *h = s->ihead;
+    if (!h || h->done != 0 || s->in_base != 0) return;
+    const uint8_t *b = s->in.data();
+    const size_t m = s->in.size();
+    if (m < 2) return;
+    if (!(b[0] == 0x1f && b[1] == 0x8b)) { h->done = -1; return; }
+    if (m < 4) return;
+    const unsigned flags = b[2] | (unsigned)b[3] << 8;
+    if ((flags & 0xffu) != Z_DEFLATED || (flags & 0xe000u)) return;   // BAD: no more fields
+    h->text = (int)((flags >> 8) & 1u);
+    if (m < 8) return;
+    h->time = (uLong)b[4] | (uLong)b[5] << 8 | (uLong)b[6] << 16 | (uLong)b[7] << 24;
+    if (m < 10) return;
+    h->xflags = b[8];
+    h->os = b[9];
+    size_t p = 10;
+    if (flags & 0x0400u) {
+        if (m < 12) return;
+        const unsigned xlen = b[10] | (unsigned)b[11] << 8;
+        h->extra_len = xlen;
+        p = 12;
+        const size_t have = std::min<size_t>(xlen, m - p);
+        if (h->extra) std::memcpy(h->extra, b + p, std::min<size_t>(have, h->extra_max));
+        if (have < xlen) return;
+        p += xlen;
+    } else {
+        h->extra = nullptr;
+    }
+    for (int k = 0; k < 2; k++) {                               // FNAME, FCOMMENT
+        Bytef *&dst = k ? h->comment : h->name;
+        const uInt max = k ? h->comm_max : h->name_max;
+        if (!(flags & (k ? 0x1000u : 0x0800u))) { dst = nullptr; continue; }
+        size_t q = p;
+        while (q < m && b[q]) q++;
+        const bool end = q < m;
+        if (dst) std::memcpy(dst, b + p, std::min<size_t>((end ? q + 1 : q) - p, max));
+        if (!end) return;
+        p = q + 1;
+    }
+    if (flags & 0x0200u) {                                      // FHCRC: a mismatch is BAD (the decode says so)
+        if (m < p + 2) return;
+        const uint32_t c = (uint32_t)crc32_z(0, b, p);
+        if ((c & 0xffffu) != (uint32_t)(b[p] | b[p + 1] << 8)) return;
+    }
+    h->hcrc = (int)((flags >> 9) & 1u);
+    h->done = 1;
+}
+
+// a zlib / gzip header has been read (inflate.c's state->flags != -1)
+bool inflate_header_seen(const internal_state *s) {
+    if (!s->wrap) return false;
+    if (s->imode == 1 || s->ideliv || s->finished || s->in_base) return true;
+    const uint8_t *b = s->in.data();
+    const size_t m = s->in.size();
+    if (m < 2) return false;
+    if (!((s->wrap & 2) && b[0] == 0x1f && b[1] == 0x8b)) return true;   // a zlib header (checked by the decode)
+    return m >= 4;                                              // gzip: FLAGS read (inflate.c FLAGS sets state->flags)
+}
+
 static int inflate_body(z_streamp strm, int flush) {
     if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
     if (!strm->next_out || (strm->avail_in && !strm->next_in)) return Z_STREAM_ERROR;   // inflate.c:610-612
-    if (flush == Z_BLOCK || flush == 6 /* Z_TREES */) return Z_STREAM_ERROR;           // documented gap
+    if (flush == 6 /* Z_TREES */) return Z_STREAM_ERROR;                               // documented gap
     if (s->need_dict) return Z_NEED_DICT;                      // inflate.c DICT: until the dictionary is set
-    const size_t took = s->finished ? 0 : strm->avail_in;
+    // Z_BLOCK: while the block the last call stopped at is still being handed
+    // out, the reference reads no more input
+    const bool block = flush == Z_BLOCK;
+    const size_t took = s->finished || (block && s->out_pos < s->out.size()) ? 0 : strm->avail_in;
     if (took) {
         s->in.insert(s->in.end(), strm->next_in, strm->next_in + took);
         strm->next_in += took;
         strm->avail_in = 0;
         strm->total_in += took;
     }
+    gz_header_fill(s);
     // Decode what has arrived whenever input arrives: a stream that is still
     // open (a sync-flushed connection, a file read in pieces) hands out every
     // byte its input decodes to so far, as inflate() does (inflate.c:622-1221).
     // Each attempt resumes at the last complete block (inflate_attempt).
     const uint64_t in_end = s->in_base + s->in.size();
-    if (!s->finished && (took || (flush == Z_FINISH && s->tried != in_end))) {
-        if (int rc = inflate_attempt(strm, s, took)) return rc;
+    if (!s->finished && (took || s->itail || (flush == Z_FINISH && s->tried != in_end))) {
+        if (block) s->idt = 0;
+        if (int rc = inflate_attempt(strm, s, took, block)) return rc;
         if (s->need_dict) return Z_NEED_DICT;
     }
+    if (block) strm->data_type = s->idt;
     size_t give = 0;
     if (s->out_pos < s->out.size() || s->finished) {
         give = std::min<size_t>(strm->avail_out, s->out.size() - s->out_pos);
@@ -3297,6 +3469,85 @@ int inflateEnd(z_streamp strm) {
     if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
     free_state(strm, strm->state);
     strm->state = nullptr;
+    return Z_OK;
+}
+
+// inflateGetHeader (inflate.c:1330-1340): gzip streams only; the fields are
+// filled as the header arrives (gz_header_fill)
+int inflateGetHeader(z_streamp strm, gz_headerp head) {
+    if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    if ((s->wrap & 2) == 0 || !head) return Z_STREAM_ERROR;
+    s->ihead = head;
+    head->done = 0;
+    gz_header_fill(s);
+    return Z_OK;
+}
+
+// inflateSync (inflate.c:1375-1437): skip input up to and through the next
+// 00 00 ff ff (a Z_SYNC_FLUSH / Z_FULL_FLUSH point; a search split over calls
+// goes on where it stopped), then restart on a new block with no window and
+// no check value: a stream whose header was read keeps its trailer, unchecked;
+// one without (raw, or no header yet) ends with its last block.  The bits
+// the reference may hold in its bit buffer are not searched: this engine
+// holds none between calls.
+int inflateSync(z_streamp strm) {
+    if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    if (strm->avail_in == 0) return Z_BUF_ERROR;
+    if (!s->isyncing) {
+        s->isyncing = true;
+        s->isync_have = 0;
+    }
+    uint32_t got = s->isync_have;
+    uInt len = 0;
+    while (len < strm->avail_in && got < 4) {                   // syncsearch (inflate.c:1352-1373)
+        const uint8_t c = strm->next_in[len];
+        if (c == (got < 2 ? 0 : 0xff)) got++;
+        else if (c) got = 0;
+        else got = 4 - got;
+        len++;
+    }
+    s->isync_have = got;
+    strm->next_in += len;
+    strm->avail_in -= len;
+    strm->total_in += len;
+    if (got != 4) return Z_DATA_ERROR;
+    const bool hdr = inflate_header_seen(s);
+    if (hdr && s->imode == 0 && s->in.size() >= 2)
+        s->igz = (s->wrap & 2) && s->in[0] == 0x1f && s->in[1] == 0x8b;
+    s->isync = hdr ? 1 : 2;
+    try {
+        s->in.clear();
+        s->out.clear();
+        s->hist.clear();
+    } catch (const std::bad_alloc &) {
+        return Z_MEM_ERROR;
+    }
+    s->out_pos = 0;
+    s->in_base = strm->total_in;
+    s->finished = 0;
+    s->result = Z_OK;
+    s->tried = 0;
+    s->imode = 1;
+    s->res_bit = 8ull * s->in_base;
+    s->res_put = s->ideliv;
+    s->icheck = s->igz ? 0u : 1u;
+    s->need_dict = false;
+    s->isyncing = false;
+    s->itype = true;                                            // mode TYPE
+    s->itail = false;
+    if (hdr) strm->adler = s->igz ? 0 : 1;                      // inflateReset: adler = wrap & 1
+    return Z_OK;
+}
+
+// inflateCopy (inflate.c:1439-1485): a deep copy of the stream and its state
+int inflateCopy(z_streamp dest, z_streamp source) {
+    if (!dest || !source || !source->state || !source->state->inflating) return Z_STREAM_ERROR;
+    *dest = *source;
+    internal_state *s = new_state(dest, source->state);
+    if (!s) return Z_MEM_ERROR;
+    dest->state = s;
     return Z_OK;
 }
 

@@ -233,6 +233,8 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
     bool gz = false;
     uint64_t blk_bit = 0;                            // the last block boundary reached
     uint32_t blk_put = 0;
+    uint32_t zlast = 0;                              // BFINAL of the current block (data_type)
+    bool ztype = (job.stop_mode & 4u) != 0;          // waiting at a block header in mode TYPE
     if (job.res_bit) {
         seek(r, (uint32_t)(rb >> 3));
         refill(S, r, in, n, lane);
@@ -309,12 +311,23 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
         }
     }
 
+    if (wrap && !job.res_bit) ztype = true;                     // after the header: TYPE (raw starts in TYPEDO)
+    if (wrap && !job.res_bit && (job.stop_mode & 1u)) {        // Z_BLOCK: before the first block
+        blk_bit = bitpos(r);
+        blk_put = put;
+        stop = kIBlock;
+        used = blk_bit >> 3;
+        goto done;
+    }
+
     // ---------------- blocks (inflate.c:827-1181) ----------------
     for (;;) {
         refill(S, r, in, n, lane);
         if (bitpos(r) + 3 > inbits) { stop = kIInEnd; used = n; goto done; }
         const uint32_t last = (uint32_t)r.hold & 1u, type = ((uint32_t)r.hold >> 1) & 3u;
         dropb(r, 3);
+        zlast = last;
+        ztype = false;
         if (type == 3) { stop = kIData; used = ceil_used(); goto done; }
         if (type == 0) {                                             // STORED, COPY
             dropb(r, r.bits & 7u);
@@ -377,7 +390,10 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
                     refill(S, r, in, n, lane);
                     const uint32_t e = uni(S.ct[(uint32_t)r.hold & 127u]);
                     const uint32_t L = (e >> 9) & 15u, sym = e & 0x1ffu;
-                    if (bitpos(r) + L > inbits) { stop = kIInEnd; used = n; goto done; }
+                    // a repeat code and its extra bits are read together (inflate.c
+                    // CODELENS: NEEDBITS(here.bits + 2/3/7)), so a short input keeps both
+                    const uint32_t xb = sym == 16 ? 2u : sym == 17 ? 3u : sym == 18 ? 7u : 0u;
+                    if (bitpos(r) + L + xb > inbits) { stop = kIInEnd; used = n; goto done; }
                     dropb(r, L);
                     if (sym == kSymBad || sym < 16) {                // empty code-length code: 0 per bit
                         if (lane == 0) S.lens[have] = (uint16_t)(sym == kSymBad ? 0 : sym);
@@ -458,10 +474,19 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
                 if (copy < len) { stop = kIFull; used = ceil_used(); goto done; }
             }
         }
+        ztype = true;                                // END_BLOCK: mode TYPE
+        if (job.stop_mode & 2u) {                    // Z_BLOCK: stop at it (after the last block too)
+            blk_bit = bitpos(r);
+            blk_put = put;
+            stop = kIBlock;
+            used = (blk_bit + 7) >> 3;
+            goto done;
+        }
         if (last) break;
         blk_bit = bitpos(r);                         // a block boundary: resumable here
         blk_put = put;
     }
+    ztype = false;                                   // TYPEDO -> CHECK
 
     // ---------------- CHECK, LENGTH (inflate.c:1183-1221) ----------------
     dropb(r, r.bits & 7u);
@@ -513,6 +538,10 @@ done:
         if (job.blk_out) {
             job.blk_out[2 * (uint64_t)g] = blk_bit;
             job.blk_out[2 * (uint64_t)g + 1] = blk_put;
+        }
+        if (job.zstate_out) {
+            const uint64_t bp = bitpos(r);
+            job.zstate_out[g] = (bp <= inbits ? inbits - bp : 0) | (uint64_t)zlast << 32 | (uint64_t)(ztype ? 1 : 0) << 33;
         }
     }
 }

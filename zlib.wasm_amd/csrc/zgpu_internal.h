@@ -277,7 +277,8 @@ __host__ __device__ inline WinP win_params(int wbits, int hbits) {
 
 // ---- inflate ----
 // where k_inflate_decode stopped (zo_inflate_run's codes)
-enum InflateStop : uint32_t { kIEnd = 0, kIData = 1, kIDict = 2, kIFull = 3, kIInEnd = 4 };
+// (kIBlock: inflate(Z_BLOCK)'s stop at a block boundary, InflateJob::stop_mode)
+enum InflateStop : uint32_t { kIEnd = 0, kIData = 1, kIDict = 2, kIFull = 3, kIInEnd = 4, kIBlock = 5 };
 
 struct InflateRec {          // per stream, written by k_inflate_decode
     uint64_t put;            // output bytes produced
@@ -319,6 +320,17 @@ struct InflateJob {
     const uint64_t *res_bit;
     const uint32_t *res_hist;
     uint64_t *blk_out;
+    // inflate(Z_BLOCK) (inflate.c TYPE: "if (flush == Z_BLOCK) goto inf_leave"):
+    // bit 0 stop right after a zlib / gzip header, bit 1 at the end of the
+    // first block that is not the last; the stop (kIBlock) is the boundary in
+    // blk_out
+    uint32_t stop_mode;
+    // the state inflate.c would report in strm->data_type where the decode
+    // stopped (or null): input bits it would hold (inbits - the bit after the
+    // last symbol part decoded) | BFINAL of the current block << 32 | waiting
+    // at a block header (mode TYPE) << 33.  stop_mode bit 2: the decode starts
+    // in mode TYPE (resumed at a boundary), not TYPEDO / HEAD
+    uint64_t *zstate_out;
 };
 int launch_inflate_stage(int stage, const InflateJob &job, hipStream_t st);
 

@@ -47,7 +47,7 @@ EXPORTED_SYMBOLS = (
     "crc32_combine", "crc32_combine64", "crc32_combine_gen", "crc32_combine_gen64",
     "crc32_combine_op", "adler32", "adler32_z", "adler32_combine", "adler32_combine64",
     "uncompress", "uncompress2", "inflateInit_", "inflateInit2_", "inflate", "inflateEnd",
-    "inflateReset", "deflateSetDictionary", "deflateParams", "deflateTune", "deflatePrime",
+    "inflateReset", "inflateGetHeader", "inflateSync", "inflateCopy", "deflateSetDictionary", "deflateParams", "deflateTune", "deflatePrime",
     "deflateSetHeader", "inflateSetDictionary",
     # include/zgpu_wasm.h
     "zlib_compress_buffer", "zlib_crc32", "zlib_adler32", "zlib_compress_bound",
