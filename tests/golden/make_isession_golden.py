@@ -28,13 +28,22 @@ def build_z(spec):
     data = datagen.make(*spec["data"])
     fmt = spec.get("fmt", "zlib")
     wb = {"zlib": 15, "raw": -15, "gzip": -15}[fmt]
-    c = zlib.compressobj(spec.get("level", 6), zlib.DEFLATED, wb, 8, spec.get("strategy", 0))
+    if "zdict" in spec:
+        c = zlib.compressobj(spec.get("level", 6), zlib.DEFLATED, wb, 8, spec.get("strategy", 0),
+                             zdict=datagen.make(*spec["zdict"]))
+    else:
+        c = zlib.compressobj(spec.get("level", 6), zlib.DEFLATED, wb, 8, spec.get("strategy", 0))
     body, pos = b"", 0
     for at, fl in spec.get("cuts", []):
         body += c.compress(data[pos:at]) + c.flush(fl)
         pos = at
     body += c.compress(data[pos:]) + c.flush(Z_FINISH)
     if fmt != "gzip":
+        if "cinfo" in spec:                  # a header that claims a smaller window than the stream uses
+            cmf = (spec["cinfo"] << 4) | 8
+            flg = body[1] & 0xe0
+            flg |= 31 - ((cmf * 256 + flg) % 31)
+            body = bytes([cmf, flg]) + body[2:]
         return body
     g = spec.get("gz", {})
     flg = (1 if g.get("text") else 0) | (2 if g.get("hcrc") else 0) | (4 if "extra" in g else 0) | \
@@ -80,7 +89,7 @@ def sessions():
     gzs = [
         {"text": 1, "time": 0x5f5e0ff1, "xfl": 2, "os": 11, "name": b"file.txt".hex(), "comment": b"a comment".hex()},
         {"time": 7, "extra": (b"AB\x04\x00wxyz" + bytes(range(40))).hex(), "hcrc": 1},
-        {"name": b"n" * 300 .hex() if False else (b"n" * 300).hex(), "comment": b"".hex(), "hcrc": 1, "os": 255},
+        {"name": (b"n" * 300).hex(), "comment": b"".hex(), "hcrc": 1, "os": 255},
         {},
     ]
     for i, gz in enumerate(gzs):
@@ -125,6 +134,15 @@ def sessions():
     S.append({"name": "copy-after-block", "spec": {"data": mix, "fmt": "gzip", "cuts": [[70000, Z_SYNC_FLUSH]]},
               "ops": [["init", 31], ["feed", 1 << 30], ["inflate", Z_BLOCK, 1 << 20], ["inflate", Z_BLOCK, 1 << 20],
                       ["copy"], ["use", 1], ["loop", Z_NO_FLUSH, 1 << 20], ["use", 0], ["loop", Z_BLOCK, 1 << 20]]})
+    # inflateSetDictionary keeps 1 << windowBits of inflateInit2_ (not of the
+    # header's CINFO): a stream whose header claims a 512-byte window but which
+    # reaches 30 KiB into the dictionary decodes
+    for cinfo in (1, 7):
+        for wb in (15, 0):
+            S.append({"name": f"dict-window-cinfo{cinfo}-w{wb}", "spec": {
+                "data": ["text", 60000, 51], "zdict": ["text", 32768, 52], "fmt": "zlib", "cinfo": cinfo},
+                "ops": [["init", wb], ["feed", 1 << 30], ["loop", Z_NO_FLUSH, 1 << 20], ["dict", ["text", 32768, 52]],
+                        ["loop", Z_NO_FLUSH, 1 << 20]]})
     return S
 
 

@@ -489,6 +489,11 @@ def run_isession(L, z, wbits=15, dictionary=None, chunk=1 << 30, version=b"1.3.1
     return rcs, bytes(out)
 
 
+def _gen_bytes(spec):
+    import datagen
+    return datagen.make(*spec)
+
+
 def run_iops(L, z, ops, version=b"1.3.1.1-motley"):
     """A scripted z_stream inflate session over the compressed bytes z on
     library L (the reference or libzgpu.so); returns (per-op results, the
@@ -502,7 +507,7 @@ def run_iops(L, z, ops, version=b"1.3.1.1-motley"):
                                       makes no progress
       ("sync",)                       inflateSync
       ("copy",)                       inflateCopy of the active stream; ("use", k) drives stream k
-      ("dict", hex)                   inflateSetDictionary
+      ("dict", hex | [kind, n, seed])  inflateSetDictionary (given, or datagen bytes)
     Each call records (rc, avail_in, total_in, total_out[, data_type when the
     flush is Z_BLOCK and rc is Z_OK]), inflateSync (rc, avail_in, total_in)."""
     _bind_zstream(L)
@@ -575,7 +580,7 @@ def run_iops(L, z, ops, version=b"1.3.1.1-motley"):
         elif k == "use":
             act = op[1]
         elif k == "dict":
-            d = bytes.fromhex(op[1])
+            d = bytes.fromhex(op[1]) if isinstance(op[1], str) else _gen_bytes(op[1])
             res.append(L.inflateSetDictionary(C.byref(s), d, len(d)))
         else:
             raise ValueError(k)

@@ -1768,6 +1768,7 @@ struct internal_state {
     int idt = 0;                         // strm->data_type at the last inflate(Z_BLOCK) stop
     bool itype = false;                  // the resume point is a block boundary (inflate.c mode TYPE)
     bool itail = false;                  // Z_BLOCK stopped after the last block: the trailer is next
+    uint64_t iadj = 0;                   // input consumed that total_in does not count (Z_NEED_DICT's call)
     // configuration rows changed with input pending (deflateParams within the
     // same function, deflateTune; deflate.c:760-820): row cfg_row[k] governs
     // the current part's decision points from part position cfg_pos[k] on,
@@ -2496,13 +2497,15 @@ static int deflate_body(z_streamp strm, int flush) {
     const size_t P = s->rd + strm->avail_in;                   // the input this call offers ends here
     if (P > C && (uint64_t)(P - s->in_base) >= kMaxBuffer) return Z_MEM_ERROR;   // 32-bit kernel positions
 
-    // the first call asks for Z_FINISH with everything: one batch job, when
-    // its output fits (otherwise the timeline below pauses like zlib)
-    if (flush == Z_FINISH && !s->header_done && !s->flushed && C == 0 && s->level != 0) {
-        size_t cap = (size_t)strm->avail_in + (strm->avail_in >> 2) + 1024;   // any windowBits / memLevel
-        std::vector<uint8_t> tmp(cap);
+    // the first call asks for Z_FINISH with everything and has room for any
+    // result (deflateBound): one batch job straight into next_out (ADVICE r2:
+    // with less room the timeline below pauses like zlib, without a job whose
+    // result might not fit and would be thrown away)
+    if (flush == Z_FINISH && !s->header_done && !s->flushed && C == 0 && s->level != 0 &&
+        strm->avail_out >= deflateBound(strm, strm->avail_in)) {
+        size_t cap = strm->avail_out;
         const uint8_t *sp = strm->next_in;
-        uint8_t *dp = tmp.data();
+        uint8_t *dp = strm->next_out;
         size_t sl = strm->avail_in;
         int st = 0;
         int rc;
@@ -2513,8 +2516,7 @@ static int deflate_body(z_streamp strm, int flush) {
                                                nullptr, s->wbits, s->mem_level, s->tuned ? &s->tune : nullptr);
         }
         if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
-        if (cap <= strm->avail_out) {
-            std::memcpy(strm->next_out, tmp.data(), cap);
+        {
             strm->next_out += cap;
             strm->avail_out -= (uInt)cap;
             strm->total_out += cap;
@@ -3091,6 +3093,7 @@ int inflateReset(z_streamp strm) {
     s->need_dict = false; s->want_dict = 0;
     s->ihead = nullptr;                                                // inflateResetKeep: head = Z_NULL
     s->isyncing = false; s->isync_have = 0; s->isync = 0; s->idt = 0; s->itype = false; s->itail = false;
+    s->iadj = 0;
     strm->total_in = strm->total_out = 0;
     strm->msg = nullptr;
     strm->adler = s->wrap & 1;
@@ -3136,7 +3139,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             const size_t back = (size_t)std::min<uint64_t>(in_end - used, took);
             strm->next_in -= back;
             strm->avail_in += (uInt)back;
-            strm->total_in = used;
+            strm->total_in = used - s->iadj;
             if (s->wrap && !s->isync) strm->adler = s->icheck;
             s->result = Z_STREAM_END;
         } else {
@@ -3178,6 +3181,14 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
                                            o.begin() + (std::ptrdiff_t)(upto - obase));
         };
         const uint64_t put_abs = obase + t.put;
+        // a data error: the reference stops reading there (inflate.c BAD), so
+        // this call's input after the bytes used goes back to the caller
+        auto give_back_after = [&](uint64_t used_abs) {
+            const size_t back = (size_t)std::min<uint64_t>(in_end > used_abs ? in_end - used_abs : 0, took);
+            strm->next_in -= back;
+            strm->avail_in += (uInt)back;
+            strm->total_in = used_abs - s->iadj;
+        };
         if (t.stop == kIBlock) {
             // inflate(Z_BLOCK) at a block boundary (or before the first block):
             // the output through it, the resume point there, and the input after
@@ -3221,7 +3232,11 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             const size_t keep = 6, back = std::min<size_t>(s->in.size() - keep, took);
             strm->next_in -= back;
             strm->avail_in += (uInt)back;
-            strm->total_in -= back;
+            // inflate.c returns Z_NEED_DICT from DICT straight after RESTORE(),
+            // not through inf_leave: what this call consumed is never added to
+            // total_in (here, or later)
+            strm->total_in -= took;
+            s->iadj += took - back;
             s->in.resize(s->in.size() - back);
             s->need_dict = true;
             s->want_dict = ((uint32_t)s->in[2] << 24) | ((uint32_t)s->in[3] << 16) | ((uint32_t)s->in[4] << 8) | s->in[5];
@@ -3237,13 +3252,14 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
                 const size_t back = std::min<size_t>(extra, took);
                 strm->next_in -= back;
                 strm->avail_in += (uInt)back;
-                strm->total_in = t.used;
+                strm->total_in = t.used - s->iadj;
                 if (s->wrap) strm->adler = s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b
                                                ? crc32_z(0, o.data(), o.size())
                                                : adler32_z(1, o.data(), o.size());
             } else {
                 s->result = Z_DATA_ERROR;
                 strm->msg = const_cast<char *>("invalid or corrupt deflate stream");
+                give_back_after(t.used);
             }
             s->in.clear();
             s->in.shrink_to_fit();
@@ -3254,6 +3270,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             s->finished = 1;
             s->result = Z_DATA_ERROR;
             strm->msg = const_cast<char *>("invalid or corrupt deflate stream");
+            give_back_after(s->in_base + t.used);
             s->in.clear();
             s->in.shrink_to_fit();
             return Z_OK;
@@ -3285,7 +3302,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
                     const size_t back = std::min<size_t>(in_end - used, took);
                     strm->next_in -= back;
                     strm->avail_in += (uInt)back;
-                    strm->total_in = used;
+                    strm->total_in = used - s->iadj;
                     if (s->wrap && !s->isync) strm->adler = ck;
                     s->idt = 64;                                 // the last block, done
                 } else {
@@ -3449,7 +3466,9 @@ int inflateSetDictionary(z_streamp strm, const Bytef *dictionary, uInt dictLengt
             strm->msg = const_cast<char *>("inflateSetDictionary: raw streams before their first input only");
             return Z_STREAM_ERROR;
         }
-        const int wb = s->need_dict ? (s->in[0] >> 4) + 8 : (s->wbits ? s->wbits : 15);
+        // updatewindow keeps 1 << state->wbits bytes: inflateInit2_'s windowBits,
+        // or, when that is 0, the zlib header's CINFO + 8 (inflate.c HEAD)
+        const int wb = s->wbits ? s->wbits : s->need_dict ? (s->in[0] >> 4) + 8 : 15;
         const size_t wsize = size_t(1) << wb, keep = std::min<size_t>(dictLength, wsize);
         s->hist.assign(dictionary + (dictLength - keep), dictionary + dictLength);
         s->res_bit = s->need_dict ? 48 : 0;                    // after CMF, FLG and DICTID
@@ -3525,7 +3544,7 @@ int inflateSync(z_streamp strm) {
         return Z_MEM_ERROR;
     }
     s->out_pos = 0;
-    s->in_base = strm->total_in;
+    s->in_base = strm->total_in + s->iadj;                     // absolute input position
     s->finished = 0;
     s->result = Z_OK;
     s->tried = 0;
