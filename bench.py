@@ -142,7 +142,10 @@ class Dist:
         if not self.cpu:
             torch.cuda.set_device(self.local)
         self.backend = None
-        if self.world > 1:
+        # under a launcher the collectives run even with one rank, so the RCCL
+        # path is the one a single-GPU box exercises too (tests/test_gpu.py)
+        self.pg = self.world > 1 or "MASTER_ADDR" in os.environ
+        if self.pg:
             if self.cpu:
                 dist.init_process_group("gloo")
             else:
@@ -151,13 +154,13 @@ class Dist:
             assert dist.get_world_size() == self.world
 
     def barrier(self):
-        if self.world > 1:
+        if self.pg:
             dist.barrier()
         if not self.cpu:
             torch.cuda.synchronize()
 
     def _reduce(self, vals, op):
-        if self.world == 1:
+        if not self.pg:
             return [float(v) for v in vals]
         t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=self.dev)
         dist.all_reduce(t, op=op)
@@ -172,14 +175,14 @@ class Dist:
     def gather(self, vals):
         """all_gather of a fixed-length int64 vector per rank."""
         t = torch.tensor(vals, dtype=torch.int64, device=self.dev)
-        if self.world == 1:
+        if not self.pg:
             return [t.tolist()]
         out = [torch.empty_like(t) for _ in range(self.world)]
         dist.all_gather(out, t)
         return [o.tolist() for o in out]
 
     def close(self):
-        if self.world > 1:
+        if self.pg:
             dist.destroy_process_group()
 
 

@@ -602,17 +602,26 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         }
         max_lanes = std::max(max_lanes, lanes);
         pseg_of[sb] = (uint32_t)ps;
-        maxblk_of[sb] = (uint32_t)mb;
     }
     pg_at[nsub] = pg.size() / 2;
     plb_at[nsub] = plb.size();
+    // The block-parallel encoder (k_enc_plan / scan / emit, §4.6b) for every
+    // batch job at levels 1..9: one workgroup per block instead of one per
+    // buffer (a 4096 x 1 MiB L6 sub-batch: 42 -> ~10 ms).  Streaming jobs
+    // (markers, resumed output bits) and level 0 keep k_encode.
+    const bool block_enc = !fs && level >= 1 && !no_big;
+    for (size_t sb = 0; sb < nsub && block_enc; sb++) {
+        uint64_t mb = 0;
+        for (uint32_t i = cuts[sb]; i < cuts[sb + 1]; i++) mb = std::max<uint64_t>(mb, lens[i] / wp.sym_limit + 2);
+        maxblk_of[sb] = (uint32_t)mb;
+    }
+    if (block_enc && !c.ws_eplan.ensure(sizeof(EncPlan) * max_blk)) return zfail(__LINE__);
     if (!pg.empty()) {
         const size_t npg = pg.size();
         pg.insert(pg.end(), plb.begin(), plb.end());
         if (!c.ws_pg.ensure(4 * pg.size()) ||
             hipMemcpyAsync(c.ws_pg.p, pg.data(), 4 * pg.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
-            !c.ws_plane.ensure(sizeof(PLane) * max_lanes) || !c.ws_pbuf.ensure(sizeof(PBuf) * max_cnt) ||
-            !c.ws_eplan.ensure(sizeof(EncPlan) * max_blk))
+            !c.ws_plane.ensure(sizeof(PLane) * max_lanes) || !c.ws_pbuf.ensure(sizeof(PBuf) * max_cnt))
             return zfail(__LINE__);
         pg.resize(npg);
     }
@@ -681,9 +690,11 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.npgrp = (uint32_t)(pg_at[s + 1] - pg_at[s]);
             job.plbase = c.ws_pg.as<uint32_t>() + plb_base + plb_at[s];
             job.pseg = pseg_of[s];
-            job.maxblk = maxblk_of[s];
             job.plane = c.ws_plane.as<PLane>();
             job.pbuf = c.ws_pbuf.as<PBuf>();
+        }
+        if (block_enc) {
+            job.maxblk = maxblk_of[s];
             job.eplan = c.ws_eplan.as<EncPlan>();
         }
         if (fs) {
@@ -748,7 +759,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             uint32_t *heads = c.ws_heads.as<uint32_t>();
             if (T.run(4, st, [&] { return launch_deflate_stage(3, job, heads, st); })) return zfail(__LINE__);
         }
-        const int es = job.pgrp ? 12 : 4;                      // few large buffers: k_enc_*
+        const int es = job.eplan ? 12 : 4;                      // batch jobs: k_enc_* (§4.6b)
         if (T.run(5, st, [&] { return launch_deflate_stage(es, job, nullptr, st); })) return zfail(__LINE__);
         return ZGPU_OK;
     };
