@@ -308,7 +308,12 @@ __global__ __launch_bounds__(kLThreads) void k_links(DeflateJob job) {
 // lengths share a wave) and decides no result.
 // ------------------------------------------------------------------------
 constexpr int kCntStage = 4096;
-constexpr int kCntThreads = 256;
+// 1024 threads (16 waves) per buffer: the LDS atomics' latency is hidden by
+// more waves (k_count 14.3 -> 9.5 ms per 4 GiB L6 sub-batch); the wider
+// unordered step perturbs the hint slightly (k_match +1.7 ms), net -2.7 ms
+// (profiles/r03n_ab_links_count.log).  Prefetching the next stage into
+// registers gained nothing here or in k_links.
+constexpr int kCntThreads = 1024;
 
 __device__ __attribute__((always_inline)) inline uint32_t walk_key(uint32_t c, uint32_t chain) {
     if (c > chain) c = chain;
@@ -317,7 +322,7 @@ __device__ __attribute__((always_inline)) inline uint32_t walk_key(uint32_t c, u
     return k < 255 ? k : 255;
 }
 
-// 4 waves per buffer; thread t takes positions t, t + 256, ... of each staged
+// 16 waves per buffer; thread t takes positions t, t + 1024, ... of each staged
 // 4 KiB, without barriers between them (their order only perturbs the hint).
 // kSegs: one workgroup per segment [s0, s1) of job.seg, counting from the
 // stage at or before s0 - MAX_DIST (the window of s0) and writing [s0, s1).
