@@ -2542,10 +2542,16 @@ constexpr int kEncThreads = 256;
 constexpr int kStgWords = 2048;                 // 8 KiB output staging window
 constexpr int kEncGroup = kEncThreads / 64;     // blocks whose trees are built at once (one per wave)
 constexpr int kStgBits = kStgWords * 32;
+// k_enc_emit's staging window (4 KiB): small enough that a k_enc_emit
+// workgroup (5.0 KiB of LDS) fits beside k_match's 153.6 KiB on a CU, so the
+// pipeline runs both at once: 10426 -> 10606 MB/s on the C4 shard
+// (profiles/r03q_ab_coresident_encode.log)
+constexpr int kEmitStgWords = 1024;
+constexpr int kEmitStgBits = kEmitStgWords * 32;
 constexpr int kWNodeSlots = (kHeapSize + 63) / 64;   // w_build: tree nodes per lane (9)
 constexpr unsigned kEncWaveBuildMax = 1024;          // w_build below this many buffers per launch
 
-struct TreeLDS {
+struct TreeLDSLane {                     // what the one-lane build (t_build) uses
     // leaves: freq/code; all nodes: dad/len (internal-node freqs live in heap keys)
     uint16_t lfreq[kLCodes], lcode[kLCodes], ldad[kHeapSize];
     uint8_t llen[kHeapSize + 1];
@@ -2555,6 +2561,8 @@ struct TreeLDS {
     uint8_t blen[2 * kBLCodes + 2];
     uint32_t heap[kHeapSize + 1];        // packed keys, see hkey()
     uint16_t bl_count[kMaxBits + 1];
+};
+struct TreeLDS : TreeLDSLane {
     uint32_t pj[kWNodeSlots * 64];       // w_build: pointer-jumping exchange (dad | depth << 16)
 };
 
@@ -2608,7 +2616,7 @@ __device__ void t_gen_codes(TreeRef &t, const uint16_t *bl_count) {       // gen
 
 // build_tree + gen_bitlen (trees.c:540-706); slen == nullptr for the bl tree.
 // Single lane; opt_len/static_len accumulate in registers.
-__device__ void t_build(TreeRef &t, TreeLDS &h, int elems, const uint8_t *slen, const uint8_t *extra,
+__device__ void t_build(TreeRef &t, TreeLDSLane &h, int elems, const uint8_t *slen, const uint8_t *extra,
                         int xbase, int max_length, int64_t &opt_len, int64_t &static_len) {
     uint32_t *heap = h.heap;
     int max_code = -1, heap_len = 0, heap_max = kHeapSize;
@@ -3013,9 +3021,9 @@ __device__ __attribute__((always_inline)) inline void stg_flush(Stage &st, int64
 // into T.  Lane 0 returns the header fields and the block's length in bits
 // from its 3-bit header through END_BLOCK (static or dynamic; for a stored
 // block the input length is what counts).
-template <bool kWaveTrees>
+template <bool kWaveTrees, typename TL>
 __device__ __attribute__((always_inline)) inline void block_plan(const DeflateJob &job, const BlockRec br,
-                                                                 const uint32_t *sym, TreeLDS &T, uint32_t *hl,
+                                                                 const uint32_t *sym, TL &T, uint32_t *hl,
                                                                  uint32_t *hd, int lane, int &type, int &lmax,
                                                                  int &dmax, int &blmax, uint64_t &bits) {
     for (int i = lane; i < kLCodes; i += 64) hl[i] = 0;
@@ -3397,7 +3405,46 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_plan(DeflateJob job) {
     }
 }
 
-constexpr int kEScanThreads = 1024;
+// k_enc_plan for batches (one-lane tree builds): one wave per block and the
+// smallest tree storage (no w_build exchange; the symbol histograms share the
+// heap's words, dead before the build starts), 5.6 KiB of LDS, so that plan
+// workgroups fit beside k_match's 153.6 KiB on a CU while the pipeline runs
+// both: 10606 -> 10807 MB/s on the C4 shard with the smaller k_enc_emit
+// (profiles/r03q_ab_coresident_encode.log)
+__global__ __launch_bounds__(64) void k_enc_plan1(DeflateJob job) {
+    __shared__ TreeLDSLane T;
+    const int lane = threadIdx.x;
+    const uint32_t bi = blockIdx.y;
+    const uint32_t kb = blockIdx.x;
+    const uint32_t nblk = job.nblocks[bi];
+    if (kb >= nblk || !enc_blocks_ok(job, bi, nblk)) return;
+    const BlockRec br = job.blocks[job.blk_off[bi] + kb];
+    static_assert(sizeof(T.heap) >= sizeof(uint32_t) * (kLCodes + kDCodes), "histograms in the heap's words");
+    uint32_t *hl = T.heap, *hd = T.heap + kLCodes;
+    int type = 0, lmax = 0, dmax = 0, blmax = 0;
+    uint64_t bits = 0;
+    block_plan<false>(job, br, job.sym + job.ws_off[bi], T, hl, hd, lane, type, lmax, dmax, blmax, bits);
+    EncPlan &P = job.eplan[job.blk_off[bi] + kb];
+    __builtin_amdgcn_wave_barrier();                  // lane 0's tables (t_build) before the copy
+    type = __shfl(type, 0, 64);
+    if (lane == 0) {
+        P.type = (uint8_t)type;
+        P.lmax = (uint16_t)lmax;
+        P.dmax = (uint16_t)dmax;
+        P.blmax = (uint16_t)blmax;
+        P.bits = bits;
+    }
+    if (type == 2) {
+        for (int i = lane; i < kLCodes; i += 64) { P.lcode[i] = T.lcode[i]; P.llen[i] = T.llen[i]; }
+        if (lane < kDCodes) { P.dcode[lane] = T.dcode[lane]; P.dlen[lane] = T.dlen[lane]; }
+        if (lane < kBLCodes) { P.bcode[lane] = T.bcode[lane]; P.blen[lane] = T.blen[lane]; }
+    }
+}
+
+// 256 threads (3 KiB of LDS): a k_enc_scan workgroup fits beside k_match on a CU, as k_enc_plan1 and
+// k_enc_emit do (no measurable change on the C4 shard: profiles/r03r_ab_scan256.log); the offsets
+// are a serial walk over the blocks either way
+constexpr int kEScanThreads = 256;
 __device__ inline uint64_t wrap_head_bits(int wrap) { return wrap == 1 ? 16 : wrap == 2 ? 80 : 0; }
 __device__ inline uint64_t wrap_tail_bits(int wrap) { return wrap == 1 ? 32 : wrap == 2 ? 64 : 0; }
 
@@ -3480,7 +3527,7 @@ __global__ __launch_bounds__(kEScanThreads) void k_enc_scan(DeflateJob job) {
 }
 
 __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
-    __shared__ uint32_t stg[kStgWords];
+    __shared__ uint32_t stg[kEmitStgWords];
     __shared__ uint16_t s_lcode[kLCodes], s_dcode[kDCodes], s_bcode[kBLCodes];
     __shared__ uint8_t s_llen[kLCodes], s_dlen[kDCodes], s_blen[kBLCodes];
     __shared__ uint32_t wsum[kEncThreads / 64];
@@ -3503,7 +3550,7 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
     const int64_t sh = 8 * (int64_t)a3;                   // stream bit x is bit x + sh of ow[]
     const int64_t rs = k == 0 ? 0 : (int64_t)pl[k].start, re = (int64_t)pl[k + 1].start;
     const int64_t wfirst = (rs + sh) >> 5, wlast = (re - 1 + sh) >> 5;
-    for (int w = tid; w < kStgWords; w += kEncThreads) stg[w] = 0;
+    for (int w = tid; w < kEmitStgWords; w += kEncThreads) stg[w] = 0;
     if (type == 2) {
         const EncPlan &P = pl[k];
         for (int i = tid; i < kLCodes; i += kEncThreads) { s_lcode[i] = P.lcode[i]; s_llen[i] = P.llen[i]; }
@@ -3548,7 +3595,7 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
         if (!fin) {
             const uint32_t keep = stg[full];
             __syncthreads();
-            for (int w = tid; w < kStgWords; w += kEncThreads) stg[w] = 0;
+            for (int w = tid; w < kEmitStgWords; w += kEncThreads) stg[w] = 0;
             __syncthreads();
             if (tid == 0) stg[0] = keep;
             sbase += 32ll * full;
@@ -3597,7 +3644,7 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
         int64_t copied = 0;
         while (copied < len) {
             eflush(s_obit, false);
-            const int64_t room = (sbase + kStgBits - 64 - s_obit) >> 3;
+            const int64_t room = (sbase + kEmitStgBits - 64 - s_obit) >> 3;
             const int64_t take = (len - copied) < room ? (len - copied) : room;
             const int64_t ob = s_obit - sbase;
             for (int64_t i = tid; i < take; i += kEncThreads) stg_or(stg, ob + 8 * i, in[br.in_start + copied + i]);
@@ -3648,7 +3695,7 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
                 total += (int)wsum[w];
             }
             const int excl = wpre + incl - nb;
-            if (s_obit - sbase + total + 64 > kStgBits) eflush(s_obit, false);
+            if (s_obit - sbase + total + 64 > kEmitStgBits) eflush(s_obit, false);
             if (nb) stg_or(stg, s_obit - sbase + excl, v);
             __syncthreads();
             if (tid == 0) s_obit += total;
@@ -3656,7 +3703,7 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
         }
     }
     if (last) {
-        if (s_obit - sbase + 160 > kStgBits) eflush(s_obit, false);
+        if (s_obit - sbase + 160 > kEmitStgBits) eflush(s_obit, false);
         if (tid == 0) {
             s_obit = (s_obit + 7) & ~7ll;                  // bi_windup
             const uint32_t ck = job.check[bi];
@@ -3745,7 +3792,7 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         if ((uint64_t)job.maxblk * job.count < 16384)
             hipLaunchKernelGGL(k_enc_plan<true>, plg, dim3(kEncThreads), 0, st, job);
         else
-            hipLaunchKernelGGL(k_enc_plan<false>, plg, dim3(kEncThreads), 0, st, job);
+            hipLaunchKernelGGL(k_enc_plan1, dim3(job.maxblk, job.count), dim3(64), 0, st, job);
         hipLaunchKernelGGL(k_enc_scan, grid, dim3(kEScanThreads), 0, st, job);
         hipLaunchKernelGGL(k_enc_emit, eg, dim3(kEncThreads), 0, st, job);
         break;
