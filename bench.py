@@ -420,9 +420,16 @@ def cpu_baselines(a, sample, want, level):
     sys1 = zb.zb_compress_rate(ptrs, lens, len(bufs), level, 1, secs / 2, C.byref(done))
     sysn = zb.zb_compress_rate(ptrs, lens, len(bufs), level, allt, secs, C.byref(done))
     sysn_b = done.value
+    err = None
+    if sys1 < 0 or sysn < 0:     # a zlib call or an allocation failed inside zb_compress_rate
+        err = f"system zlib compress2 failed in the timing loop (1 thread: {sys1}, {allt} threads: {sysn})"
     progress(f"cpu baseline: oracle port, 1 thread then {allt}")
     port1, _ = _timed_threads(lambda b: o.compress(b, level), sample, 1, secs / 4)
     portn, portn_b = _timed_threads(lambda b: o.compress(b, level), sample, allt, secs / 2)
+    if err:
+        return {"value": None, "unit": "MB/s", "cores": allt, "kind": "reference", "error": err,
+                "port": {"value": round(portn, 2), "per_core_1thread": round(port1, 2), "cores": allt},
+                "host": host}
     return {"value": round(sysn, 2), "unit": "MB/s", "cores": allt,
             "kind": "reference",
             "kind_note": f"system zlib {ver} compress2() (upstream zlib: the deflate.c/trees.c the reference "
@@ -459,6 +466,9 @@ def checksum_cpu_baseline(a, which, c):
     secs = max(1.0, a.cpu_seconds / 4)
     one = fn(buf, nb * c["n"], c["n"], 1, secs / 2, C.byref(done))
     alln = fn(buf, nb * c["n"], c["n"], allt, secs, C.byref(done))
+    if one < 0 or alln < 0:
+        return {"value": None, "unit": "GB/s", "cores": allt, "kind": "reference",
+                "error": f"system zlib {which}() timing failed (1 thread: {one}, {allt} threads: {alln})"}
     out = {"value": round(alln / 1e3, 3), "unit": "GB/s", "cores": allt, "kind": "reference",
            "kind_note": f"system zlib {zb.zb_zlib_version().decode()} {which}()",
            "per_core_1thread": round(one / 1e3, 3),
@@ -651,10 +661,11 @@ def main(argv=None):
         cpu = None
         if not a.no_cpu and sample and D.world == 1:
             cpu = cpu_baselines(a, sample, want, a.level)
-            cpu["gpu_over_cpu"] = {"vs_value": round(mbps / cpu["value"], 2),
-                                   "vs_one_core": round(mbps / cpu["per_core_1thread"], 1),
-                                   "vs_all_host_cpus_linear_estimate":
-                                       round(mbps / cpu["all_host_cpus_linear_estimate"], 3)}
+            if cpu["value"] is not None:
+                cpu["gpu_over_cpu"] = {"vs_value": round(mbps / cpu["value"], 2),
+                                       "vs_one_core": round(mbps / cpu["per_core_1thread"], 1),
+                                       "vs_all_host_cpus_linear_estimate":
+                                           round(mbps / cpu["all_host_cpus_linear_estimate"], 3)}
         line = {
             "metric": METRIC,
             "value": round(mbps, 1),

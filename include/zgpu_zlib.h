@@ -114,6 +114,10 @@ uLong deflateBound(z_streamp strm, uLong sourceLen);                    /* zlib.
 int deflateReset(z_streamp strm);                                       /* zlib.h:621 */
 int deflateCopy(z_streamp dest, z_streamp source);                      /* zlib.h:603 */
 int deflatePending(z_streamp strm, unsigned *pending, int *bits);       /* zlib.h:746 */
+int deflateUsed(z_streamp strm, int *bits);                             /* zlib.h deflateUsed; deflate.c:723 */
+int deflateGetDictionary(z_streamp strm, Bytef *dictionary,
+                         uInt *dictLength);                             /* zlib.h deflateGetDictionary; deflate.c:616 */
+int deflateResetKeep(z_streamp strm);                                   /* zlib.h deflateResetKeep; deflate.c:635 */
 
 /* gzip header (zlib.h gz_header) for deflateSetHeader / inflateGetHeader */
 typedef struct gz_header_s {
@@ -158,6 +162,9 @@ uLong crc32_combine64(uLong crc1, uLong crc2, int64_t len2);
 uLong crc32_combine_gen(long len2);                                     /* zlib.h:1784 */
 uLong crc32_combine_gen64(int64_t len2);
 uLong crc32_combine_op(uLong crc1, uLong crc2, uLong op);               /* zlib.h:1790 */
+const char *zError(int err);                                            /* zlib.h zError; zutil.c:131 */
+uLong zlibCompileFlags(void);                                           /* zlib.h zlibCompileFlags; zutil.c:31 */
+const uint32_t *get_crc_table(void);                                    /* zlib.h get_crc_table; crc32.c:549 */
 
 int uncompress(Bytef *dest, uLongf *destLen, const Bytef *source,
                uLong sourceLen);                                        /* zlib.h:1289 */
@@ -176,6 +183,26 @@ int inflateCopy(z_streamp dest, z_streamp source);                      /* zlib.
 /* inflate(flush): Z_NO_FLUSH, Z_SYNC_FLUSH, Z_FINISH and Z_BLOCK (stop at the
  * next block boundary, or after a zlib / gzip header; strm->data_type as
  * inflate.c sets it there); Z_TREES is refused (Z_STREAM_ERROR) */
+int inflateReset2(z_streamp strm, int windowBits);                      /* zlib.h inflateReset2; inflate.c:153 */
+int inflateResetKeep(z_streamp strm);                                   /* zlib.h inflateResetKeep; inflate.c:105 */
+int inflatePrime(z_streamp strm, int bits, int value);                  /* zlib.h inflatePrime; inflate.c:223
+                                                                           (raw streams before their first input) */
+int inflateGetDictionary(z_streamp strm, Bytef *dictionary,
+                         uInt *dictLength);                             /* zlib.h inflateGetDictionary; inflate.c:1278 */
+int inflateSyncPoint(z_streamp strm);                                   /* zlib.h inflateSyncPoint; inflate.c:1431 */
+int inflateUndermine(z_streamp strm, int subvert);                      /* zlib.h inflateUndermine; inflate.c:1483 */
+int inflateValidate(z_streamp strm, int check);                         /* zlib.h inflateValidate; inflate.c:1498 */
+long inflateMark(z_streamp strm);                                       /* zlib.h inflateMark; inflate.c:1510 */
+unsigned long inflateCodesUsed(z_streamp strm);                         /* zlib.h inflateCodesUsed; inflate.c:1521 */
+typedef unsigned (*in_func)(void *, const unsigned char **);            /* zlib.h in_func */
+typedef int (*out_func)(void *, unsigned char *, unsigned);             /* zlib.h out_func */
+int inflateBackInit_(z_streamp strm, int windowBits, unsigned char *window,
+                     const char *version, int stream_size);             /* zlib.h inflateBackInit_; infback.c:25 */
+int inflateBack(z_streamp strm, in_func in, void *in_desc,
+                out_func out, void *out_desc);                          /* zlib.h inflateBack; infback.c:250 */
+int inflateBackEnd(z_streamp strm);                                     /* zlib.h inflateBackEnd; infback.c:632 */
+#define inflateBackInit(strm, windowBits, window) \
+    inflateBackInit_((strm), (windowBits), (window), ZGPU_ZLIB_VERSION, (int)sizeof(z_stream))
 
 #define inflateInit(strm) \
     inflateInit_((strm), ZGPU_ZLIB_VERSION, (int)sizeof(z_stream))

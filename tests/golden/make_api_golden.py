@@ -1,0 +1,261 @@
+"""Golden sessions of the zlib.h calls added in round 4, from the compiled
+reference (oracle/_ref/libzref.so, built from /root/reference by
+oracle/Makefile): deflateUsed, deflateGetDictionary, deflateResetKeep,
+inflateReset2, inflateResetKeep, inflatePrime, inflateGetDictionary,
+inflateSyncPoint, inflateUndermine, inflateValidate, inflateMark,
+inflateCodesUsed and inflateBackInit_ / inflateBack / inflateBackEnd.
+
+Every compressed input is rebuilt from its spec with Python's zlib (system
+zlib; build_z in make_isession_golden.py) -- no stream made by the reference
+is stored, only the ops and what the reference returned (codes, counters,
+lengths and sha256 prefixes of outputs and windows).  The same runners
+(tests/zhelpers.py run_iops / run_zsession / run_back) replay them against
+libzgpu.so on the GPU (tests/test_gpu_zstream.py).
+Run from tests/golden: python3 make_api_golden.py"""
+import hashlib
+import json
+import os
+import sys
+import zlib
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+import datagen  # noqa: E402
+from make_isession_golden import build_z  # noqa: E402
+from zhelpers import Reference, run_back, run_iops, run_zsession  # noqa: E402
+
+Z_NO_FLUSH, Z_PARTIAL_FLUSH, Z_SYNC_FLUSH, Z_FULL_FLUSH, Z_FINISH, Z_BLOCK = 0, 1, 2, 3, 4, 5
+BIG = 1 << 30
+
+
+def build(spec):
+    """build_z, plus: "concat" (several specs back to back), "xor_tail" (flip
+    the last byte: a wrong check value), "zdict_tail" (a raw stream
+    compressed against the tail of other data), "shift" (the stream from bit k on,
+    repacked into bytes, for inflatePrime with its first k bits), "chop" (drop
+    the last n bytes), "garbage" (bytes appended after the stream)."""
+    if "concat" in spec:
+        z = b"".join(build(s) for s in spec["concat"])
+    elif "zdict_tail" in spec:                   # a raw stream against the tail of other data
+        kind, n, seed, tail = spec["zdict_tail"]
+        c = zlib.compressobj(spec.get("level", 6), zlib.DEFLATED, -15, 8, 0,
+                             zdict=datagen.make(kind, n, seed)[-tail:])
+        z = c.compress(datagen.make(*spec["data"])) + c.flush()
+    else:
+        z = build_z(spec)
+    if spec.get("xor_tail"):
+        z = z[:-1] + bytes([z[-1] ^ 0x5a])
+    if spec.get("shift"):
+        k = spec["shift"]
+        z = (int.from_bytes(z, "little") >> k).to_bytes(len(z), "little")
+    if spec.get("chop"):
+        z = z[:-spec["chop"]]
+    if spec.get("garbage"):
+        z = z + bytes(range(spec["garbage"]))
+    return z
+
+
+def prime_value(spec):
+    """The first `shift` bits of the unshifted stream (inflatePrime's value)."""
+    s = dict(spec)
+    k = s.pop("shift")
+    z = build(s)
+    return int.from_bytes(z[:4], "little") & ((1 << k) - 1)
+
+
+def sync_point(spec):
+    """Bytes of the stream up to a Z_SYNC_FLUSH marker's LEN/NLEN (00 00 ff ff):
+    the stored block's header byte is in, its length is not."""
+    z = build(spec)
+    return z.find(b"\x00\x00\xff\xff", 3)
+
+
+def watch(k):
+    return [["mark"], ["codes"], ["syncpoint"], ["getdict"]][:k]
+
+
+def inflate_sessions():
+    S = []
+    text = ["text", 150000, 61]
+    mix = ["mix", 200000, 62]
+    # the window, inflateMark, inflateCodesUsed and inflateSyncPoint as the
+    # input arrives in pieces (ample output space)
+    for fmt, wb in (("zlib", 15), ("gzip", 31), ("raw", -15)):
+        for data, level in ((text, 6), (mix, 9), (mix, 1)):
+            spec = {"data": data, "level": level, "fmt": fmt, "cuts": [[70000, Z_SYNC_FLUSH]]}
+            ops = [["init", wb]] + watch(4)
+            for _ in range(12):
+                ops += [["feed", 3001], ["inflate", Z_NO_FLUSH, 1 << 20]] + watch(4)
+            ops += [["feed", BIG], ["loop", Z_NO_FLUSH, 1 << 20]] + watch(4)
+            S.append({"name": f"watch-{fmt}-{data[0]}-L{level}", "spec": spec, "ops": ops})
+    # single bytes across a dynamic block header: CODES table sizes, back counts
+    spec = {"data": ["text", 20000, 63], "level": 6, "fmt": "raw"}
+    ops = [["init", -15]]
+    for _ in range(400):
+        ops += [["feed", 1], ["inflate", Z_NO_FLUSH, 1 << 20], ["mark"], ["codes"]]
+    S.append({"name": "watch-bytes-raw", "spec": spec, "ops": ops})
+    # the window after a one-call Z_FINISH (never made), small output pieces
+    for flush in (Z_FINISH, Z_NO_FLUSH):
+        S.append({"name": f"getdict-one-call-{flush}", "spec": {"data": text, "fmt": "zlib"},
+                  "ops": [["init", 15], ["feed", BIG], ["inflate", flush, 1 << 20], ["getdict"], ["codes"]]})
+    S.append({"name": "getdict-small-out", "spec": {"data": mix, "fmt": "zlib"},
+              "ops": [["init", 15], ["feed", BIG]] + [["inflate", Z_NO_FLUSH, 7000], ["getdict"]] * 40 +
+                     [["loop", Z_FINISH, 1 << 20], ["getdict"]]})
+    S.append({"name": "getdict-after-setdict", "spec": {"data": ["text", 60000, 64], "zdict": ["text", 40000, 65],
+                                                         "fmt": "raw"},
+              "ops": [["init", -15], ["dict", ["text", 40000, 65]], ["getdict"], ["feed", BIG],
+                      ["loop", Z_NO_FLUSH, 1 << 20], ["getdict"]]})
+    S.append({"name": "getdict-small-window", "spec": {"data": ["text", 30000, 66], "fmt": "raw"},
+              "ops": [["init", -9], ["feed", BIG], ["loop", Z_NO_FLUSH, 1 << 20], ["getdict"]]})
+    # inflateSyncPoint right before a sync marker's LEN/NLEN
+    for fmt, wb in (("raw", -15), ("zlib", 15)):
+        for level in (6, 1):
+            spec = {"data": text, "level": level, "fmt": fmt, "cuts": [[50000, Z_SYNC_FLUSH]]}
+            at = sync_point(spec)
+            for d in (0, -1, 1, 2):
+                S.append({"name": f"syncpoint-{fmt}-L{level}-{d}", "spec": spec,
+                          "ops": [["init", wb], ["feed", at + d], ["inflate", Z_NO_FLUSH, 1 << 20], ["syncpoint"],
+                                  ["mark"], ["feed", BIG], ["loop", Z_NO_FLUSH, 1 << 20], ["syncpoint"]]})
+    # inflateValidate(0): a wrong check value goes unnoticed, adler keeps its start
+    for fmt, wb in (("zlib", 15), ("gzip", 31), ("zlib", 47), ("gzip", 47)):
+        for bad in (0, 1):
+            for chk in (0, 1):
+                spec = {"data": ["mix", 50000, 67], "fmt": fmt, "xor_tail": bad}
+                S.append({"name": f"validate-{fmt}-w{wb}-bad{bad}-chk{chk}", "spec": spec,
+                          "ops": [["init", wb], ["validate", chk], ["feed", BIG], ["loop", Z_NO_FLUSH, 1 << 20],
+                                  ["adler"]]})
+    S.append({"name": "validate-pieces", "spec": {"data": ["mix", 80000, 68], "fmt": "zlib", "xor_tail": 1},
+              "ops": [["init", 15], ["validate", 0]] + [["feed", 9000], ["inflate", Z_NO_FLUSH, 1 << 20]] * 12 +
+                     [["adler"]]})
+    # inflateReset2 / inflateReset / inflateResetKeep between concatenated streams
+    two = {"concat": [{"data": ["text", 40000, 69], "fmt": "zlib"}, {"data": ["mix", 30000, 70], "fmt": "raw"}]}
+    S.append({"name": "reset2-zlib-then-raw", "spec": two,
+              "ops": [["init", 15], ["feed", BIG], ["loop", Z_NO_FLUSH, 1 << 20], ["reset2", -15],
+                      ["loop", Z_NO_FLUSH, 1 << 20], ["getdict"], ["reset2", 99], ["reset2", -16], ["reset2", 7]]})
+    keep = {"concat": [{"data": ["text", 50000, 71], "fmt": "raw"},
+                       {"data": ["text", 30000, 72], "fmt": "raw", "zdict_tail": ["text", 50000, 71, 32768]}]}
+    for op in ("resetkeep", "reset2"):
+        S.append({"name": f"{op}-raw-window", "spec": keep,
+                  "ops": [["init", -15], ["feed", BIG], ["loop", Z_NO_FLUSH, 1 << 20], ["getdict"],
+                          [op] + ([-15] if op == "reset2" else []), ["getdict"], ["loop", Z_NO_FLUSH, 1 << 20],
+                          ["getdict"]]})
+    S.append({"name": "reset-zlib-twice", "spec": {"concat": [{"data": ["mix", 20000, 73], "fmt": "zlib"},
+                                                              {"data": ["mix", 20000, 74], "fmt": "zlib"}]},
+              "ops": [["init", 15], ["feed", BIG], ["loop", Z_NO_FLUSH, 1 << 20], ["reset"], ["getdict"],
+                      ["loop", Z_NO_FLUSH, 1 << 20]]})
+    # inflatePrime: a raw stream from bit k on, its first k bits primed (zran.c)
+    for k in (1, 3, 7, 8, 13):
+        spec = {"data": ["mix", 40000, 75], "level": 6, "fmt": "raw", "shift": k}
+        v = prime_value(spec)
+        parts = [["prime", k - k // 2, v & ((1 << (k - k // 2)) - 1)], ["prime", k // 2, v >> (k - k // 2)]] \
+            if k > 1 else [["prime", k, v]]
+        S.append({"name": f"prime-{k}", "spec": spec,
+                  "ops": [["init", -15]] + parts + [["feed", BIG], ["loop", Z_NO_FLUSH, 1 << 20]]})
+    spec = {"data": ["text", 30000, 76], "zdict": ["text", 20000, 77], "fmt": "raw", "shift": 5}
+    S.append({"name": "prime-dict", "spec": spec,
+              "ops": [["init", -15], ["prime", 5, prime_value(spec)], ["dict", ["text", 20000, 77]], ["feed", BIG],
+                      ["loop", Z_NO_FLUSH, 1 << 20]]})
+    S.append({"name": "prime-clear-and-limits", "spec": {"data": ["text", 5000, 78], "fmt": "raw"},
+              "ops": [["init", -15], ["prime", -1, 0], ["prime", 0, 5], ["prime", 17, 0], ["prime", 16, 0],
+                      ["prime", 16, 0], ["prime", 1, 0], ["prime", -1, 0], ["feed", BIG],
+                      ["loop", Z_NO_FLUSH, 1 << 20]]})
+    S.append({"name": "undermine", "spec": {"data": ["text", 5000, 79], "fmt": "zlib"},
+              "ops": [["init", 15], ["undermine", 1], ["undermine", 0], ["feed", BIG], ["loop", Z_NO_FLUSH, 1 << 20]]})
+    return S
+
+
+def deflate_sessions():
+    S = []
+    t = datagen.make("text", 100000, 81)
+    m = datagen.make("mix", 100000, 82)
+    for level in (0, 1, 6, 9):
+        for wb in (15, -15, 31):
+            ops = [["init", level, wb, 8, 0], ["used"], ["getdict"]]
+            for i, fl in enumerate((Z_NO_FLUSH, Z_SYNC_FLUSH, Z_PARTIAL_FLUSH, Z_BLOCK, Z_NO_FLUSH, Z_SYNC_FLUSH)):
+                ops += [["deflate", m[i * 9000:(i + 1) * 9000], fl], ["used"], ["getdict"]]
+            ops += [["deflate", t[:40000], Z_NO_FLUSH], ["used"], ["getdict"],
+                    ["deflate", t[40000:], Z_FINISH], ["used"], ["getdict"]]
+            S.append({"name": f"used-getdict-L{level}-w{wb}", "ops": ops})
+        S.append({"name": f"used-one-shot-L{level}", "ops": [["init", level, 15, 8, 0], ["deflate", m, Z_FINISH],
+                                                             ["used"], ["getdict"]]})
+        S.append({"name": f"used-small-out-L{level}", "ops": [["init", level, 15, 8, 0],
+                                                              ["deflate", t[:60000], Z_NO_FLUSH, 4000], ["used"],
+                                                              ["getdict"], ["deflate", t[60000:], Z_FINISH, 4000],
+                                                              ["used"]]})
+    for strategy in (1, 2, 3, 4):
+        S.append({"name": f"used-strategy-{strategy}", "ops": [["init", 6, 15, 8, strategy],
+                                                               ["deflate", m[:50000], Z_SYNC_FLUSH], ["used"],
+                                                               ["deflate", m[50000:], Z_FINISH], ["used"]]})
+    for wb in (-15, 15, -10):
+        S.append({"name": f"getdict-setdict-w{wb}", "ops": [["init", 6, wb, 8, 0], ["dict", t[:50000]], ["getdict"],
+                                                            ["deflate", m[:20000], Z_NO_FLUSH], ["getdict"],
+                                                            ["deflate", b"", Z_FINISH], ["getdict"]]})
+        S.append({"name": f"getdict-setdict-L0-w{wb}", "ops": [["init", 0, wb, 8, 0], ["dict", t[:500]], ["getdict"],
+                                                               ["deflate", m[:20000], Z_SYNC_FLUSH], ["getdict"]]})
+    S.append({"name": "resetkeep-fresh", "ops": [["init", 6, 15, 8, 0], ["resetkeep"], ["deflate", m, Z_FINISH],
+                                                 ["used"], ["reset"], ["resetkeep"], ["deflate", t, Z_FINISH]]})
+    return S
+
+
+def back_cases():
+    C = []
+    for kind, level in (("text", 6), ("mix", 9), ("runs", 1), ("mix", 0)):
+        for wbits in (15, 9):
+            for chunk, first in ((BIG, 0), (4096, 0), (777, 100)):
+                C.append({"name": f"back-{kind}-L{level}-w{wbits}-c{chunk}-f{first}",
+                          "spec": {"data": [kind, 90000, 91], "level": level, "fmt": "raw"},
+                          "wbits": wbits, "in_chunk": chunk, "first": first})
+    small = {"data": ["text", 1500, 92], "level": 6, "fmt": "raw"}
+    C.append({"name": "back-bytes", "spec": small, "wbits": 15, "in_chunk": 1, "first": 0})
+    C.append({"name": "back-truncated", "spec": dict(small, chop=5), "wbits": 15, "in_chunk": 64, "first": 0})
+    C.append({"name": "back-garbage-after", "spec": dict(small, garbage=40), "wbits": 15, "in_chunk": BIG, "first": 0})
+    C.append({"name": "back-out-fails", "spec": {"data": ["mix", 90000, 93], "fmt": "raw"}, "wbits": 10,
+              "in_chunk": BIG, "first": 0, "out_fail_at": 3})
+    C.append({"name": "back-corrupt", "spec": {"data": ["text", 9000, 94], "fmt": "zlib"}, "wbits": 15,
+              "in_chunk": BIG, "first": 0})
+    return C
+
+
+def run_inflate(L, sess):
+    z = build(sess["spec"])
+    res, outs, _ = run_iops(L, z, sess["ops"])
+    return {"res": res, "outs": [[len(o), hashlib.sha256(o).hexdigest()] for o in outs]}
+
+
+def run_deflate(L, sess):
+    ops = [[o[0], bytes.fromhex(o[1])] + o[2:] if o[0] in ("deflate", "dict") else o for o in sess["ops"]]
+    rcs, out = run_zsession(L, ops)
+    return {"res": rcs, "out": [len(out), hashlib.sha256(out).hexdigest()]}
+
+
+def run_backcase(L, case):
+    z = build(case["spec"])
+    rc0, rc, out, unused, null_in, rc2, calls = run_back(L, z, case["wbits"], case["in_chunk"], case["first"],
+                                                         case.get("out_fail_at"))
+    return {"res": [rc0, rc, unused, null_in, rc2], "out": [len(out), hashlib.sha256(out).hexdigest()]}
+
+
+def jsonable(sess):
+    """deflate ops carry bytes: stored as hex"""
+    return dict(sess, ops=[[o[0], o[1].hex()] + o[2:] if o[0] in ("deflate", "dict") else o for o in sess["ops"]])
+
+
+def main():
+    ref = Reference()
+    out = {"reference": ref.version.decode(), "inflate": [], "deflate": [], "back": []}
+    for sess in inflate_sessions():
+        out["inflate"].append(dict(sess, **run_inflate(ref.L, sess)))
+    for sess in deflate_sessions():
+        js = jsonable(sess)
+        out["deflate"].append(dict(js, **run_deflate(ref.L, js)))
+    for case in back_cases():
+        out["back"].append(dict(case, **run_backcase(ref.L, case)))
+    path = os.path.join(HERE, "api_golden.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=0, sort_keys=True)
+    print(f"wrote {path}: {len(out['inflate'])} inflate, {len(out['deflate'])} deflate, {len(out['back'])} back")
+
+
+if __name__ == "__main__":
+    main()

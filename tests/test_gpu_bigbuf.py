@@ -122,18 +122,40 @@ def _over_4gib_input(zg):
     return data.tobytes()
 
 
-def test_compress2_over_4gib_vs_system_zlib(zg):
+@pytest.mark.parametrize("level", [6, 0])
+def test_compress2_over_4gib_vs_system_zlib(zg, level):
     """compress2 of a buffer over 4 GiB equals system zlib's
     stream.  Python's zlib.compress feeds deflate() as compress.c does: one
-    2^32 - 1 byte Z_NO_FLUSH piece, then Z_FINISH with the rest."""
+    2^32 - 1 byte Z_NO_FLUSH piece, then Z_FINISH with the rest.  Level 0's
+    stored blocks follow those pieces."""
     import hashlib
     data = _over_4gib_input(zg)
     print(f"\n{len(data)} bytes generated", flush=True)
     t = time.perf_counter()
-    want = pyzlib.compress(data, 6)
-    print(f"system zlib: {len(want)} bytes in {time.perf_counter() - t:.1f} s", flush=True)
+    want = pyzlib.compress(data, level)
+    print(f"system zlib L{level}: {len(want)} bytes in {time.perf_counter() - t:.1f} s", flush=True)
     t = time.perf_counter()
-    rc, z = zg.compress2(data, 6)
+    rc, z = zg.compress2(data, level)
     print(f"libzgpu compress2: rc {rc}, {len(z)} bytes in {time.perf_counter() - t:.1f} s", flush=True)
     assert rc == 0
     assert len(z) == len(want) and hashlib.sha256(z).digest() == hashlib.sha256(want).digest()
+
+
+@pytest.mark.parametrize("limit_mb", [None, "1"])
+def test_mem_level_1_large_buffer_plan_fallback(zg, monkeypatch, limit_mb):
+    """at memLevel 1 a block holds at most 126 symbols, so the
+    block-parallel encoder's plans (~1 KiB per possible block) of a large
+    buffer are big.  When they cannot be allocated (forced here with
+    ZGPU_EPLAN_LIMIT_MB) the job encodes with k_encode instead of failing;
+    both paths give system zlib's stream (deflateInit2(6, 8, 15, 1))."""
+    import torch
+    if limit_mb:
+        monkeypatch.setenv("ZGPU_EPLAN_LIMIT_MB", limit_mb)
+    n = 24 << 20
+    src = torch.empty(n, dtype=torch.uint8, device="cuda")
+    zg.generate_dev(src, n, 1, zg.KIND_SILESIA, seed=21)
+    data = src.cpu().numpy().tobytes()
+    co = pyzlib.compressobj(6, pyzlib.DEFLATED, 15, 1)
+    want = co.compress(data) + co.flush()
+    [(st, z)] = zg.compress_batch2([data], level=6, window_bits=15, mem_level=1)
+    assert st == 0 and z == want

@@ -90,3 +90,37 @@ def test_inflate_api_sessions_golden(zg):
             bad.append(sess["name"])
     print("BAD SESSIONS:", bad)
     assert not bad
+
+
+def test_round4_zlib_h_calls_golden(zg):
+    """The zlib.h calls added in round 4 replayed on libzgpu.so against the
+    compiled reference's results (tests/golden/api_golden.json,
+    make_api_golden.py): deflateUsed, deflateGetDictionary, deflateResetKeep
+    (deflate.c:616-728), inflateReset2, inflateResetKeep, inflatePrime,
+    inflateGetDictionary, inflateSyncPoint, inflateUndermine, inflateValidate,
+    inflateMark, inflateCodesUsed (inflate.c:105-1527) with every call's return
+    code and counters around them, and inflateBack over in() / out() callbacks
+    (infback.c): return code, output, unused input."""
+    import json
+    import os
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, "golden"))
+    from make_api_golden import run_backcase, run_deflate, run_inflate
+    g = json.load(open(os.path.join(here, "golden", "api_golden.json")))
+    L = zg.load()
+    bad = []
+    for sess in g["inflate"]:
+        r = run_inflate(L, sess)
+        if r["res"] != sess["res"] or r["outs"] != sess["outs"]:
+            bad.append(sess["name"])
+    for sess in g["deflate"]:
+        r = run_deflate(L, sess)
+        if r["res"] != sess["res"] or r["out"] != sess["out"]:
+            bad.append(sess["name"])
+    for case in g["back"]:
+        r = run_backcase(L, case)
+        if r["res"] != case["res"] or r["out"] != case["out"]:
+            bad.append(case["name"])
+    print("BAD SESSIONS:", bad)
+    assert not bad

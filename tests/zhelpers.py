@@ -6,6 +6,7 @@
   the GPU box), so tests that need it skip when it is absent.
 """
 import ctypes as C
+import hashlib
 import os
 import subprocess
 
@@ -368,7 +369,20 @@ def _bind_zstream(L):
             ("inflateSetDictionary", C.c_int, [P, C.c_void_p, C.c_uint]),
             ("deflateBound", C.c_ulong, [P, C.c_ulong]),
             ("inflateGetHeader", C.c_int, [P, C.POINTER(GzHeader)]),
-            ("inflateSync", C.c_int, [P]), ("inflateCopy", C.c_int, [P, P])):
+            ("inflateSync", C.c_int, [P]), ("inflateCopy", C.c_int, [P, P]),
+            # the rest of zlib.h's z_stream calls (round 4)
+            ("deflateUsed", C.c_int, [P, C.POINTER(C.c_int)]),
+            ("deflateGetDictionary", C.c_int, [P, C.c_void_p, C.POINTER(C.c_uint)]),
+            ("deflateResetKeep", C.c_int, [P]), ("deflateReset", C.c_int, [P]),
+            ("inflateReset", C.c_int, [P]), ("inflateReset2", C.c_int, [P, C.c_int]),
+            ("inflateResetKeep", C.c_int, [P]), ("inflatePrime", C.c_int, [P, C.c_int, C.c_int]),
+            ("inflateGetDictionary", C.c_int, [P, C.c_void_p, C.POINTER(C.c_uint)]),
+            ("inflateSyncPoint", C.c_int, [P]), ("inflateUndermine", C.c_int, [P, C.c_int]),
+            ("inflateValidate", C.c_int, [P, C.c_int]), ("inflateMark", C.c_long, [P]),
+            ("inflateCodesUsed", C.c_ulong, [P]),
+            ("inflateBackInit_", C.c_int, [P, C.c_int, C.c_void_p, C.c_char_p, C.c_int]),
+            ("inflateBack", C.c_int, [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+            ("inflateBackEnd", C.c_int, [P])):
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
@@ -448,6 +462,20 @@ def run_zsession(L, ops, version=b"1.3.1.1-motley"):
             rcs.append(seq)
         elif k == "bound":
             rcs.append(int(L.deflateBound(C.byref(s), op[1])))
+        elif k == "used":                        # deflateUsed
+            b = C.c_int(-99)
+            rcs.append([L.deflateUsed(C.byref(s), C.byref(b)), b.value])
+        elif k == "getdict":                     # deflateGetDictionary: rc, length, sha256
+            n = C.c_uint(0)
+            rc = L.deflateGetDictionary(C.byref(s), None, C.byref(n))
+            buf = C.create_string_buffer(max(n.value, 1))
+            n2 = C.c_uint(0)
+            rc2 = L.deflateGetDictionary(C.byref(s), buf, C.byref(n2))
+            rcs.append([rc, rc2, n2.value, hashlib.sha256(buf.raw[:n2.value]).hexdigest()[:16]])
+        elif k == "resetkeep":
+            rcs.append(L.deflateResetKeep(C.byref(s)))
+        elif k == "reset":
+            rcs.append(L.deflateReset(C.byref(s)))
         else:
             raise ValueError(k)
     L.deflateEnd(C.byref(s))
@@ -582,6 +610,37 @@ def run_iops(L, z, ops, version=b"1.3.1.1-motley"):
         elif k == "dict":
             d = bytes.fromhex(op[1]) if isinstance(op[1], str) else _gen_bytes(op[1])
             res.append(L.inflateSetDictionary(C.byref(s), d, len(d)))
+        # the rest of zlib.h's inflate calls (round 4)
+        elif k == "getdict":                     # inflateGetDictionary: rc, length, sha256
+            n = C.c_uint(0)
+            rc = L.inflateGetDictionary(C.byref(s), None, C.byref(n))
+            buf = C.create_string_buffer(max(n.value, 1))
+            n2 = C.c_uint(0)
+            rc2 = L.inflateGetDictionary(C.byref(s), buf, C.byref(n2))
+            res.append([rc, rc2, n2.value, hashlib.sha256(buf.raw[:n2.value]).hexdigest()[:16]])
+        elif k == "mark":
+            res.append(int(L.inflateMark(C.byref(s))))
+        elif k == "codes":
+            res.append(int(L.inflateCodesUsed(C.byref(s))))
+        elif k == "syncpoint":
+            res.append(L.inflateSyncPoint(C.byref(s)))
+        elif k == "validate":
+            res.append(L.inflateValidate(C.byref(s), op[1]))
+        elif k == "undermine":
+            res.append(L.inflateUndermine(C.byref(s), op[1]))
+        elif k == "reset":
+            res.append([L.inflateReset(C.byref(s)), s.total_in, s.total_out, s.adler])
+            outs[act] = bytearray()
+        elif k == "reset2":
+            res.append([L.inflateReset2(C.byref(s), op[1]), s.adler])
+            outs[act] = bytearray()
+        elif k == "resetkeep":
+            res.append([L.inflateResetKeep(C.byref(s)), s.adler])
+            outs[act] = bytearray()
+        elif k == "prime":
+            res.append(L.inflatePrime(C.byref(s), op[1], op[2]))
+        elif k == "adler":
+            res.append(int(s.adler))
         else:
             raise ValueError(k)
     for s in streams:
@@ -632,3 +691,46 @@ def run_dsession(L, data, plan, level=6, wbits=15, mem=8, strategy=0, version=b"
             break
     L.deflateEnd(C.byref(s))
     return recs, bytes(out)
+
+
+IN_FUNC = C.CFUNCTYPE(C.c_uint, C.c_void_p, C.POINTER(C.c_void_p))
+OUT_FUNC = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint)
+
+
+def run_back(L, z, wbits=15, in_chunk=1 << 30, first=0, out_fail_at=None, version=b"1.3.1.1-motley"):
+    """inflateBackInit_ / inflateBack / inflateBackEnd over the raw stream z on
+    library L: in() hands out `in_chunk` bytes per call (after `first` bytes
+    given up front in next_in), out() collects (and fails on call number
+    `out_fail_at`).  Returns (init rc, back rc, output, unused input length,
+    next_in is NULL, end rc, out() calls)."""
+    _bind_zstream(L)
+    s = ZStream()
+    win = C.create_string_buffer(1 << wbits)
+    rc0 = L.inflateBackInit_(C.byref(s), wbits, win, version, C.sizeof(ZStream))
+    zb = C.create_string_buffer(bytes(z), max(len(z), 1))
+    base = C.addressof(zb)
+    pos = [first]
+    out = bytearray()
+    ncall = [0]
+
+    def fin(_desc, pbuf):
+        n = min(in_chunk, len(z) - pos[0])
+        pbuf[0] = base + pos[0]
+        pos[0] += n
+        return n
+
+    def fout(_desc, buf, n):
+        ncall[0] += 1
+        if out_fail_at is not None and ncall[0] == out_fail_at:
+            return 1
+        out.extend(C.string_at(buf, n))
+        return 0
+
+    fi, fo = IN_FUNC(fin), OUT_FUNC(fout)
+    s.next_in = base if first else None
+    s.avail_in = first
+    rc = L.inflateBack(C.byref(s), C.cast(fi, C.c_void_p), None, C.cast(fo, C.c_void_p), None)
+    unused = s.avail_in if s.next_in else -1
+    null_in = not s.next_in
+    rc2 = L.inflateBackEnd(C.byref(s))
+    return rc0, rc, bytes(out), unused, null_in, rc2, ncall[0]

@@ -244,7 +244,7 @@ struct Ctx {
     DevBuf ws_help;           // the a18 helpers' staging (zlib_*_simd)
     DevBuf ws_seg;            // k_match segments of sub-batches of few large buffers
     // few large buffers: k_pbig* lane groups and records, k_enc_* block plans
-    DevBuf ws_pg, ws_plane, ws_pbuf, ws_eplan;
+    DevBuf ws_pg, ws_plane, ws_pbuf, ws_eplan, ws_wind;
     DevBuf ws_ck;             // split checksum partials (few large buffers)
     DevBuf ws_srec, ws_snap;  // a streaming job's block records and head[] snapshot
     // inflate: match records, per-stream results, checks, offsets, stop codes
@@ -454,7 +454,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
                        uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
                        uint64_t *dst_len, int32_t *status, uint32_t count, int level, int wrap,
                        int strategy, hipStream_t st, const FlushSpec *fs = nullptr, int wbits = 15,
-                       int mem_level = 8, const LevelCfg *tune = nullptr) {
+                       int mem_level = 8, const LevelCfg *tune = nullptr, uint8_t *d_wind = nullptr) {
     if (level == -1) level = 6;
     if (level < 0 || level > 9 || wrap < 0 || wrap > 2 || strategy < 0 || strategy > 4 || wbits < 9 ||
         wbits > 15 || mem_level < 1 || mem_level > 9)
@@ -609,13 +609,23 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     // batch job at levels 1..9: one workgroup per block instead of one per
     // buffer (a 4096 x 1 MiB L6 sub-batch: 42 -> ~10 ms).  Streaming jobs
     // (markers, resumed output bits) and level 0 keep k_encode.
-    const bool block_enc = !fs && level >= 1 && !no_big;
+    bool block_enc = !fs && level >= 1 && !no_big;
     for (size_t sb = 0; sb < nsub && block_enc; sb++) {
         uint64_t mb = 0;
         for (uint32_t i = cuts[sb]; i < cuts[sb + 1]; i++) mb = std::max<uint64_t>(mb, lens[i] / wp.sym_limit + 2);
         maxblk_of[sb] = (uint32_t)mb;
     }
-    if (block_enc && !c.ws_eplan.ensure(sizeof(EncPlan) * max_blk)) return zfail(__LINE__);
+    // The plans take sizeof(EncPlan) (~1 KiB) per possible block: at memLevel 1
+    // (a block per 127 symbols) a 1 GiB buffer needs ~8.7 GB of them.  When that
+    // allocation fails the job encodes with k_encode instead (one workgroup per
+    // buffer, no plan workspace) rather than failing.
+    // (ZGPU_EPLAN_LIMIT_MB, tests: treat a larger plan workspace as unavailable)
+    const char *eplan_lim = std::getenv("ZGPU_EPLAN_LIMIT_MB");
+    if (block_enc && eplan_lim && sizeof(EncPlan) * max_blk > (uint64_t)std::atoll(eplan_lim) << 20) block_enc = false;
+    if (block_enc && !c.ws_eplan.ensure(sizeof(EncPlan) * max_blk)) {
+        (void)hipGetLastError();
+        block_enc = false;
+    }
     if (!pg.empty()) {
         const size_t npg = pg.size();
         pg.insert(pg.end(), plb.begin(), plb.end());
@@ -680,6 +690,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         for (uint32_t i = a; i < b; i++)
             if (lens[i] >= (1ull << 31) - (1ull << 16)) job.pos31 = 0;
         job.check = d_check;
+        job.wind = d_wind ? d_wind + a : nullptr;
         if (seg_at[s + 1] > seg_at[s]) {
             job.seg = c.ws_seg.as<uint32_t>() + 2 * seg_at[s];
             job.nseg = (uint32_t)(seg_at[s + 1] - seg_at[s]);
@@ -853,7 +864,7 @@ struct FlushHost {
 int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
                          size_t *dst_len, int *status, size_t count, int level, int wrap, int strategy,
                          FlushHost *fh = nullptr, int wbits = 15, int mem_level = 8,
-                         const LevelCfg *tune = nullptr) {
+                         const LevelCfg *tune = nullptr, uint8_t *wind_out = nullptr) {
     if (count == 0) return ZGPU_OK;
     for (size_t i = 0; i < count; i++)
         if (src_len[i] >= kMaxBuffer) return ZGPU_STREAM_ERROR;
@@ -950,10 +961,14 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
         }
     }
     if (fh) ZTRACE("chl: launch n %u open %d\n", fh->n, fh->open_end);
+    if (wind_out && !c.ws_wind.ensure(count + 64)) return ZGPU_MEM_ERROR;
     int rc = deflate_dev_locked(c, d_in, d_so, d_sl, d_out, d_do, d_dc, d_dl, d_st, (uint32_t)count,
-                                level, wrap, strategy, st, fh ? &fs : nullptr, wbits, mem_level, tune);
+                                level, wrap, strategy, st, fh ? &fs : nullptr, wbits, mem_level, tune,
+                                wind_out ? c.ws_wind.as<uint8_t>() : nullptr);
     if (fh) ZTRACE("chl: ran rc %d\n", rc);
     if (rc) return rc;
+    if (wind_out && copy_sync(wind_out, c.ws_wind.p, count, hipMemcpyDeviceToHost, st) != hipSuccess)
+        return ZGPU_MEM_ERROR;
     if (fh && copy_sync(fh->out, fs.out, 64, hipMemcpyDeviceToHost, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
     if (fh && fh->rec_out) {
@@ -1082,6 +1097,7 @@ int inflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.blk_out = rs->blk_out;
             job.stop_mode = rs->stop_mode;
             job.zstate_out = rs->zstate_out;
+            job.zcodes = rs->zstate_out != nullptr;
         }
         if (T.run(3, st, [&] { return launch_inflate_stage(0, job, st); })) return ZGPU_MEM_ERROR;
         if (T.run(4, st, [&] { return launch_inflate_stage(1, job, st); })) return ZGPU_MEM_ERROR;
@@ -1165,6 +1181,8 @@ struct InflateTry {
     int status;
     uint64_t put, used, blk_bit, blk_put;
     uint64_t zstate;               // InflateJob::zstate_out
+    int64_t zmark;                 // inflateMark where the input ran out
+    uint32_t zcodes;               // inflateCodesUsed of the last dynamic block decoded (~0: none)
 };
 
 int inflate_try_locked(Ctx &c, const uint8_t *in, size_t n, bool resume, uint64_t start_bit, const uint8_t *hist,
@@ -1195,11 +1213,11 @@ int inflate_try_locked(Ctx &c, const uint8_t *in, size_t n, bool resume, uint64_
     int rc = inflate_dev_locked(c, d_in, m, m + 1, d_out, m + 2, m + 3, m + 4, m + 5, d_st, d_stop, 1,
                                 resume ? 0 : wrap, wbits, st, &rs);
     if (rc) return rc;
-    uint64_t res[2], blk[3];
+    uint64_t res[2], blk[4];
     int32_t status = 0;
     uint32_t stop = 0;
     if (copy_sync(res, m + 4, 16, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        copy_sync(blk, d_blk, 24, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        copy_sync(blk, d_blk, 32, hipMemcpyDeviceToHost, st) != hipSuccess ||
         copy_sync(&status, d_st, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         copy_sync(&stop, d_stop, 4, hipMemcpyDeviceToHost, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
@@ -1212,6 +1230,8 @@ int inflate_try_locked(Ctx &c, const uint8_t *in, size_t n, bool resume, uint64_
     t.blk_bit = blk[0];
     t.blk_put = blk[1];
     t.zstate = blk[2];
+    t.zmark = (int32_t)(uint32_t)blk[3];
+    t.zcodes = (uint32_t)(blk[3] >> 32);
     return ZGPU_OK;
 }
 
@@ -1531,9 +1551,8 @@ uLong compressBound(uLong sourceLen) { return (uLong)compress_bound64(sourceLen)
 // offset S (a multiple of w_size) those slide only when the end lies in
 // (S + 2 w_size - 262, S + 2 w_size - 1] -- never for an end at a multiple of
 // w_size.  Level 0 cuts its stored blocks by the input each call
-// offers, so it is refused here (Z_MEM_ERROR) rather than cut differently.
+// offers, so it gets the reference's pieces unchanged.
 static int compress2_big(Bytef *dest, uLongf *destLen, const Bytef *source, uLong sourceLen, int level) {
-    if (level == 0) { *destLen = 0; return Z_MEM_ERROR; }
     z_stream zs;
     std::memset(&zs, 0, sizeof(zs));
     int err = deflateInit_(&zs, level, ZGPU_ZLIB_VERSION, (int)sizeof(z_stream));
@@ -1550,7 +1569,9 @@ static int compress2_big(Bytef *dest, uLongf *destLen, const Bytef *source, uLon
         }
         if (zs.avail_in == 0) {
             if (pos == piece_end) piece_end = std::min(n, piece_end + kUIntMax);   // the reference's next piece
-            const uint64_t end = std::min(piece_end, (pos / kStep + 1) * kStep);
+            // level 0: exactly the reference's pieces (its stored blocks follow
+            // each call's input; the level-0 path cuts its own device jobs)
+            const uint64_t end = level == 0 ? piece_end : std::min(piece_end, (pos / kStep + 1) * kStep);
             zs.next_in = const_cast<Bytef *>(source) + pos;
             zs.avail_in = (uInt)(end - pos);
             pos = end;
@@ -1626,6 +1647,32 @@ uLong adler32_combine64(uLong adler1, uLong adler2, int64_t len2) {
 }
 uLong adler32_combine(uLong adler1, uLong adler2, long len2) { return adler32_combine64(adler1, adler2, len2); }
 
+// zutil.c:131 zError: z_errmsg[Z_NEED_DICT - err] (zutil.c:12-23); a code
+// outside Z_VERSION_ERROR..Z_NEED_DICT gets "" here instead of a read past the table
+const char *zError(int err) {
+    static const char *const msg[10] = {"need dictionary", "stream end", "", "file error", "stream error",
+                                        "data error", "insufficient memory", "buffer error",
+                                        "incompatible version", ""};
+    return err <= 2 && err >= -6 ? msg[2 - err] : "";
+}
+
+// zutil.c:31 zlibCompileFlags: type sizes in bits 0..7 (uInt, uLong, voidpf,
+// z_off_t: 0 = 16-bit, 1 = 32, 2 = 64), no debug / assembler / dynamic-table /
+// FASTEST options.  The reference compiled here reports 0xa9.
+uLong zlibCompileFlags(void) {
+    auto sz = [](size_t b) -> uLong { return b == 2 ? 0 : b == 4 ? 1 : b == 8 ? 2 : 3; };
+    return sz(sizeof(uInt)) | sz(sizeof(uLong)) << 2 | sz(sizeof(voidpf)) << 4 | sz(sizeof(int64_t)) << 6;
+}
+
+// crc32.c:549 get_crc_table: the byte-wise table of the reflected polynomial
+// 0xedb88320 (the one crc32_z's byte loop uses); built once, never freed
+const uint32_t *get_crc_table(void) {
+    static CrcTables t;
+    static std::once_flag once;
+    std::call_once(once, [] { build_crc_tables(t); });
+    return t.byte;
+}
+
 // The stream state and its buffers are allocated through the caller's
 // zalloc / zfree, as deflateInit2_ / inflateInit2_ do (deflate.c:393-406,
 // zutil.c:286-294): ZAlloc is a std allocator over them (malloc / free when
@@ -1670,6 +1717,7 @@ struct StreamItem {
     uint32_t ev;             // a stop's or marker's event index (internal_state::ev_*), else ~0u
     uint32_t rec;            // the job's record index (blocks, markers)
     uint8_t kind, pbyte, res;
+    uint8_t wu;              // bi_used at the record's last bi_windup, 0: none (deflateUsed)
 };
 enum : uint8_t { kItStop = 0, kItBlock = 1, kItMarker = 2, kItFinal = 3 };
 
@@ -1677,7 +1725,7 @@ struct internal_state {
     ZAlloc<uint8_t> al;
     explicit internal_state(const ZAlloc<uint8_t> &a = {})
         : al(a), in(a), out(a), ev_pos(a), ev_type(a), ev_aux(a), fast_head(a), fast_prev(a), l0_hist(a), hist(a), body(a),
-          items(ZAlloc<StreamItem>(a)), evb(ZAlloc<uint32_t>(a)), cfg_pos(a), cfg_row(ZAlloc<LevelCfg>(a)) {}
+          items(ZAlloc<StreamItem>(a)), evb(ZAlloc<uint32_t>(a)), iwin(a), cfg_pos(a), cfg_row(ZAlloc<LevelCfg>(a)) {}
     int level, wrap, strategy;
     zvec<uint8_t> in, out;          // deflate: the input since the last Z_FULL_FLUSH; output queue
     size_t out_pos;
@@ -1780,6 +1828,21 @@ struct internal_state {
     bool itype = false;                  // the resume point is a block boundary (inflate.c mode TYPE)
     bool itail = false;                  // Z_BLOCK stopped after the last block: the trailer is next
     uint64_t iadj = 0;                   // input consumed that total_in does not count (Z_NEED_DICT's call)
+    // inflate's sliding window as inflate.c keeps it (updatewindow, inflate.c:391-434): created by
+    // the first call that writes output unless that call ends the stream under Z_FINISH (or stops
+    // on an error), then fed every call's output; inflateSetDictionary presets it.  What
+    // inflateGetDictionary returns and inflateResetKeep carries into a raw stream.
+    zvec<uint8_t> iwin;
+    bool iwin_on = false;
+    bool ivalid = true;                  // inflateValidate: the check values are verified (wrap & 4)
+    // where the last decode left inflate.c's state (InflateJob::zstate_out): mode STORED with no bits
+    // held (inflateSyncPoint), inflateMark's value, inflateCodesUsed of the last dynamic block
+    bool isyncpt = false;
+    int64_t imark = -65536;
+    uint32_t icodes = 0;
+    uint32_t iprime_n = 0;               // inflatePrime's bits before the stream's first input
+    unsigned char *iback_win = nullptr;  // inflateBackInit_: the caller's window (1 << wbits bytes)
+    uint64_t iprime_v = 0;
     // configuration rows changed with input pending (deflateParams within the
     // same function, deflateTune; deflate.c:760-820): row cfg_row[k] governs
     // the current part's decision points from part position cfg_pos[k] on,
@@ -1794,6 +1857,7 @@ struct internal_state {
     uint32_t zl_p = kMinMatch - 1, zl_m = kMinMatch - 1;
     uint64_t zl_pos = ~0ull;
     bool prime_due = false;              // a deflatePrime event no job has written yet
+    int bi_used = 0;                     // deflateUsed: ((bi_valid - 1) & 7) + 1 at the last bi_windup, 0: none
 };
 
 namespace {
@@ -2019,6 +2083,7 @@ int deflate_part(internal_state *s, bool closed) {
         StreamItem it{};
         it.end_bit = bit0 + rec[4ull * j];
         it.pbyte = (uint8_t)rec[4ull * j + 1];
+        it.wu = (uint8_t)((rec[4ull * j + 1] >> 8) & 15u);
         it.in_end = base + (rec[4ull * j + 2] & 0xffffffffu);
         it.S = base + (rec[4ull * j + 2] >> 32);
         it.E = base + (rec[4ull * j + 3] & 0xffffffffu);
@@ -2312,16 +2377,41 @@ int deflate_stored_call(z_streamp strm, internal_state *s, int flush) {
         plan.push_back(r);
         if (flush == Z_FULL_FLUSH) strstart = block_start = 0;
     }
-    if (!plan.empty()) {
-        std::vector<uint8_t> body((size_t)compress_bound64(bpos) + 64 + 8 * plan.size());
-        const uint8_t *sp = buf.data();
+    {   // deflateUsed: _tr_stored_block winds up after each header, the final block once more
+        uint32_t b = (uint32_t)(s->res_bits & 7);
+        for (const BlockRec &r : plan) {
+            const uint32_t mk = (r.flags & kBlkMarker) ? blk_marker_kind(r.flags) : 0;
+            if (!(r.flags & kBlkMarker) || mk == 2 || mk == 3) {
+                s->bi_used = (int)((b + 2) & 7) + 1;
+                b = 0;
+                if (r.flags & kBlkLast) s->bi_used = 8;
+            } else if (mk == 1) {
+                b = (b + 10) & 7;                          // _tr_align: a static empty block, bi_flush
+            }
+        }
+    }
+    // The call's blocks go to the device as jobs of at most kL0Job input bytes
+    // (the kernels address a job's input with 32-bit positions; a compress2 of
+    // 4 GiB and more offers 2^32 - 1 bytes to one call, compress.c:44-54).  A
+    // stored block ends byte-aligned, so a job after the first starts at a
+    // whole byte and the jobs' outputs simply follow each other.
+    constexpr uint64_t kL0Job = 1ull << 30;
+    for (size_t i0 = 0; i0 < plan.size();) {
+        const uint64_t base = plan[i0].in_start;
+        size_t i1 = i0 + 1;
+        while (i1 < plan.size() && plan[i1].in_end - base <= kL0Job) i1++;
+        std::vector<BlockRec> sub(plan.begin() + (std::ptrdiff_t)i0, plan.begin() + (std::ptrdiff_t)i1);
+        for (BlockRec &r : sub) r.in_start -= base, r.in_end -= base;
+        const uint64_t jn = sub.back().in_end;
+        std::vector<uint8_t> body((size_t)compress_bound64(jn) + 64 + 8 * sub.size());
+        const uint8_t *sp = buf.data() + base;
         uint8_t *dp = body.data();
-        size_t sl = bpos, cap = body.size();
+        size_t sl = jn, cap = body.size();
         int st = 0;
         FlushHost fh{nullptr, nullptr, 0, 1, 0, (uint32_t)(s->res_bits & 7),
                      s->res_byte & ((1u << (s->res_bits & 7)) - 1u), {0, 0, 0, 0}};
-        fh.plan = plan.data();
-        fh.nplan = (uint32_t)plan.size();
+        fh.plan = sub.data();
+        fh.nplan = (uint32_t)sub.size();
         {
             Lease L;
             int rc = L.rc;
@@ -2335,6 +2425,7 @@ int deflate_stored_call(z_streamp strm, internal_state *s, int flush) {
         s->part_out = jb + cap;
         s->res_bits = ((uint64_t)jb << 3) + fh.out[1];
         s->res_byte = (uint32_t)fh.out[3];
+        i0 = i1;
     }
     s->in.assign(buf.begin() + (std::ptrdiff_t)bpos, buf.end());   // the window's unsent bytes
     {   // the window: the last strstart bytes read (deflate.c:1733-1790 keep them contiguous)
@@ -2425,6 +2516,7 @@ int run_items(z_streamp strm, internal_state *s, uint32_t own, bool *full) {
         }
         if (it.E > s->rd) s->rd = it.E;
         s->proc_bits = it.end_bit;
+        if (it.wu) s->bi_used = it.wu;
         if (it.kind == kItFinal) {                // FLUSH_BLOCK(s, 1), then the trailer
             queue_to(s, s->body_at + s->body.size());
             s->rd = s->in_base + s->in.size();
@@ -2506,7 +2598,8 @@ static int deflate_body(z_streamp strm, int flush) {
     }
     const size_t C = s->in_base + s->in.size();                // part position of the input copied so far
     const size_t P = s->rd + strm->avail_in;                   // the input this call offers ends here
-    if (P > C && (uint64_t)(P - s->in_base) >= kMaxBuffer) return Z_MEM_ERROR;   // 32-bit kernel positions
+    // 32-bit kernel positions (level 0 cuts its own jobs: deflate_stored_call)
+    if (s->level != 0 && P > C && (uint64_t)(P - s->in_base) >= kMaxBuffer) return Z_MEM_ERROR;
 
     // the first call asks for Z_FINISH with everything and has room for any
     // result (deflateBound): one batch job straight into next_out (ADVICE r2:
@@ -2523,8 +2616,11 @@ static int deflate_body(z_streamp strm, int flush) {
         {
             Lease L;
             rc = L.rc;
+            uint8_t wind = 0;
             if (!rc) rc = compress_host_locked(*L.c, &sp, &sl, &dp, &cap, &st, 1, s->level, s->wrap, s->strategy,
-                                               nullptr, s->wbits, s->mem_level, s->tuned ? &s->tune : nullptr);
+                                               nullptr, s->wbits, s->mem_level, s->tuned ? &s->tune : nullptr,
+                                               &wind);
+            s->bi_used = wind;
         }
         if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
         {
@@ -2683,6 +2779,43 @@ int deflateCopy(z_streamp dest, z_streamp source) {             // deflate.c:127
 
 // Bytes generated and not yet handed out; bits: those of a partial last byte
 // after the last block or marker handed out (deflate.c:739-747).
+// deflateUsed (deflate.c:723-728): bi_used, the bits of the last output byte
+// the most recent bi_windup completed (1..8; trees.c winds up after a stored
+// block's header and after the final block), 0 before any.  Taken from the
+// encoder's records (k_encode / k_enc_scan report it).
+int deflateUsed(z_streamp strm, int *bits) {
+    if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
+    if (bits) *bits = strm->state->bi_used;
+    return Z_OK;
+}
+
+// deflateGetDictionary (deflate.c:616-633): the window's last
+// min(strstart + lookahead, w_size) bytes -- the input fill_window has read
+// (s->rd) back to the window offset S where the reference stands: the last
+// record handed out (a stop, block or marker), or the resume point.  Level 0:
+// deflate_stored's window.  After a Z_FULL_FLUSH the part starts anew here (its
+// window empty), so bytes from before the flush are not returned.
+int deflateGetDictionary(z_streamp strm, Bytef *dictionary, uInt *dictLength) {
+    if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
+    const internal_state *s = strm->state;
+    const uint64_t wsize = uint64_t(1) << s->wbits;
+    const uint8_t *src = nullptr;
+    size_t len = 0;
+    if (s->level == 0) {
+        len = (size_t)std::min<uint64_t>(std::min<uint64_t>((uint64_t)s->st_strstart, s->l0_hist.size()), wsize);
+        src = s->l0_hist.data() + (s->l0_hist.size() - len);
+    } else {
+        const uint64_t S = s->t > 0 ? s->items[s->t - 1].S : s->res_S;
+        const uint64_t E = std::min<uint64_t>(s->rd, s->in_base + s->in.size());
+        const uint64_t lo = std::max<uint64_t>(S, s->in_base);
+        len = E > lo ? (size_t)std::min<uint64_t>(E - lo, wsize) : 0;
+        src = s->in.data() + (E - len - s->in_base);
+    }
+    if (dictionary && len) std::memcpy(dictionary, src, len);
+    if (dictLength) *dictLength = (uInt)len;
+    return Z_OK;
+}
+
 int deflatePending(z_streamp strm, unsigned *pending, int *bits) {
     if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
@@ -2698,6 +2831,21 @@ int unsupported(z_streamp strm, const char *why) {
 }
 int deflate_fn(int level) { return level == 0 ? 0 : level <= 3 ? 1 : 2; }   // stored, fast, slow
 }  // namespace
+
+// deflateResetKeep (deflate.c:635-671): deflateReset without lm_init, so the
+// next stream keeps the window, the hash chains and strstart of this one and
+// may refer back into it.  Taken where that state is the initial one (nothing
+// compressed or preset since deflateInit / deflateReset), where it is exactly
+// deflateReset; a window carried into a new stream is not modelled
+// (Z_STREAM_ERROR with strm->msg, never a different stream).
+int deflateResetKeep(z_streamp strm) {
+    if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    const bool fresh = s->in_base + s->in.size() == 0 && s->rd == 0 && !s->flushed && !s->dict_set &&
+                       s->l0_hist.empty() && s->st_strstart == 0 && strm->total_in == 0;
+    if (!fresh) return unsupported(strm, "deflateResetKeep: a window carried into the next stream is not modelled");
+    return deflateReset(strm);
+}
 
 // deflateSetDictionary (deflate.c:550-613).  Accepted on a zlib stream
 // before its first deflate() call and on a raw stream whenever the window holds
@@ -3105,9 +3253,147 @@ int inflateReset(z_streamp strm) {
     s->ihead = nullptr;                                                // inflateResetKeep: head = Z_NULL
     s->isyncing = false; s->isync_have = 0; s->isync = 0; s->idt = 0; s->itype = false; s->itail = false;
     s->iadj = 0;
+    s->iwin.clear(); s->iwin_on = false;                               // wsize = whave = wnext = 0
+    s->isyncpt = false; s->imark = -65536; s->icodes = 0; s->iprime_n = 0; s->iprime_v = 0;
     strm->total_in = strm->total_out = 0;
     strm->msg = nullptr;
     strm->adler = s->wrap & 1;
+    return Z_OK;
+}
+
+// the window size updatewindow allocates: 1 << wbits (inflateInit2_'s, or the
+// zlib header's CINFO + 8 when that was 0, 15 for gzip)
+static size_t inflate_wsize(const internal_state *s) {
+    int wb = s->wbits;
+    if (!wb) wb = s->igz || s->in.empty() || s->in_base ? 15 : (s->in[0] >> 4) + 8;
+    return size_t(1) << wb;
+}
+
+// inflateResetKeep (inflate.c:105-128): inflateReset without forgetting the
+// window.  A raw stream then decodes with it in front of its output, as it
+// would after inflateSetDictionary; a zlib / gzip stream decodes from its header
+// (a valid one never reaches back past its own start).
+int inflateResetKeep(z_streamp strm) {
+    if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    try {
+        zvec<uint8_t> win(s->iwin);
+        const bool on = s->iwin_on;
+        inflateReset(strm);
+        s->iwin.swap(win);
+        s->iwin_on = on;
+        if (s->wrap == 0 && !s->iwin.empty()) {
+            s->hist.assign(s->iwin.begin(), s->iwin.end());
+            s->res_bit = 0;
+            s->res_put = s->ideliv = s->hist.size();
+            s->icheck = 1;
+            s->imode = 1;
+        }
+    } catch (const std::bad_alloc &) {
+        return Z_MEM_ERROR;
+    }
+    return Z_OK;
+}
+
+// inflateReset2 (inflate.c:153-191): new windowBits (same rules as
+// inflateInit2_), the window dropped when its size changes, then inflateReset
+int inflateReset2(z_streamp strm, int windowBits) {
+    if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    int wrap;
+    if (windowBits < 0) {
+        if (windowBits < -15) return Z_STREAM_ERROR;
+        wrap = 0;
+        windowBits = -windowBits;
+    } else {
+        wrap = ((windowBits >> 4) + 5) & 3;
+        if (windowBits < 48) windowBits &= 15;
+    }
+    if (windowBits && (windowBits < 8 || windowBits > 15)) return Z_STREAM_ERROR;
+    s->wrap = wrap;
+    s->wbits = windowBits;
+    return inflateReset(strm);
+}
+
+// inflateUndermine (inflate.c:1483-1496): the reference is built without
+// INFLATE_ALLOW_INVALID_DISTANCE_TOOFAR_ARRR, so it refuses to subvert the
+// distance check and answers Z_DATA_ERROR
+int inflateUndermine(z_streamp strm, int subvert) {
+    (void)subvert;
+    if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
+    return Z_DATA_ERROR;
+}
+
+// inflateValidate (inflate.c:1498-1508): check != 0 verifies the trailer's
+// Adler-32 / CRC-32 + ISIZE (the default); 0 reads them unchecked, and
+// strm->adler keeps its start value as inflate.c then computes no check
+int inflateValidate(z_streamp strm, int check) {
+    if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    s->ivalid = check && s->wrap;
+    return Z_OK;
+}
+
+// inflateGetDictionary (inflate.c:1278-1296): the window's bytes, oldest first
+int inflateGetDictionary(z_streamp strm, Bytef *dictionary, uInt *dictLength) {
+    if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    if (dictionary && !s->iwin.empty()) std::memcpy(dictionary, s->iwin.data(), s->iwin.size());
+    if (dictLength) *dictLength = (uInt)s->iwin.size();
+    return Z_OK;
+}
+
+// inflateSyncPoint (inflate.c:1431-1437): 1 when inflate stands in mode STORED
+// with no bits held -- the input ran out right after a stored block's header
+// byte (a Z_SYNC_FLUSH / Z_FULL_FLUSH point whose 00 00 ff ff is not here yet)
+int inflateSyncPoint(z_streamp strm) {
+    if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
+    const internal_state *s = strm->state;
+    return !s->finished && s->out_pos == s->out.size() && s->isyncpt ? 1 : 0;
+}
+
+// inflateMark (inflate.c:1510-1519): where the input ran out, (back << 16) +
+// (a stored block's bytes still to copy): back = -1 at a block boundary, in a
+// header or a stored block, else the bits of the length / distance symbol
+// already consumed (0 in mode LEN).  A call that stopped on a full output
+// buffer (the reference then stands in mode LIT / MATCH / COPY mid-output) is
+// not modelled: the value is the one at the end of the input decoded so far.
+long inflateMark(z_streamp strm) {
+    if (!strm || !strm->state || !strm->state->inflating) return -(1L << 16);
+    const internal_state *s = strm->state;
+    return s->finished ? -(1L << 16) : (long)s->imark;
+}
+
+// inflateCodesUsed (inflate.c:1521-1527): the code-table entries the last
+// dynamic block's literal/length and distance tables took (inftrees.c
+// inflate_table at lenbits 9 / distbits 6); 0 after a reset.  Reported by the
+// decode (zgpu_inflate.hip codes_used).
+unsigned long inflateCodesUsed(z_streamp strm) {
+    if (!strm || !strm->state || !strm->state->inflating) return (unsigned long)-1;
+    return strm->state->icodes;
+}
+
+// inflatePrime (inflate.c:223-239): bits inserted ahead of the input.  Taken
+// on a raw stream before its first input (zran.c's pattern: inflateReset2(-15),
+// inflatePrime, inflateSetDictionary, then the stream from a byte offset): the
+// bits lead the decode as a virtual prefix that total_in does not count.  Bits
+// primed in the middle of a stream or ahead of a zlib / gzip header are not
+// modelled (Z_STREAM_ERROR with strm->msg).
+int inflatePrime(z_streamp strm, int bits, int value) {
+    if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    if (bits == 0) return Z_OK;
+    const bool start = s->in.empty() && s->in_base == 0 && !s->finished && s->res_bit == 0 && strm->total_in == 0;
+    if (bits < 0) {                                   // hold = bits = 0
+        if (!start) return unsupported(strm, "inflatePrime: clearing the bit buffer mid-stream is not modelled");
+        s->iprime_n = 0;
+        s->iprime_v = 0;
+        return Z_OK;
+    }
+    if (bits > 16 || s->iprime_n + (uint32_t)bits > 32) return Z_STREAM_ERROR;
+    if (!start || s->wrap != 0) return unsupported(strm, "inflatePrime: raw streams before their first input only");
+    s->iprime_v |= (uint64_t)((uint32_t)value & ((1u << bits) - 1u)) << s->iprime_n;
+    s->iprime_n += (uint32_t)bits;
     return Z_OK;
 }
 
@@ -3134,10 +3420,10 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
         }
         const uint8_t *tr = s->in.data() + (tpos - s->in_base);
         bool ok = true;
-        if (!s->isync && need == 4) {
+        if (!s->isync && s->ivalid && need == 4) {
             ok = ((uint32_t)tr[0] << 24 | (uint32_t)tr[1] << 16 | (uint32_t)tr[2] << 8 | tr[3]) == s->icheck;
             if (!ok) strm->msg = const_cast<char *>("incorrect data check");
-        } else if (!s->isync && need == 8) {
+        } else if (!s->isync && s->ivalid && need == 8) {
             const uint32_t c = tr[0] | (uint32_t)tr[1] << 8 | (uint32_t)tr[2] << 16 | (uint32_t)tr[3] << 24;
             const uint32_t z = tr[4] | (uint32_t)tr[5] << 8 | (uint32_t)tr[6] << 16 | (uint32_t)tr[7] << 24;
             ok = c == s->icheck && z == (uint32_t)s->res_put;
@@ -3151,7 +3437,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             strm->next_in -= back;
             strm->avail_in += (uInt)back;
             strm->total_in = used - s->iadj;
-            if (s->wrap && !s->isync) strm->adler = s->icheck;
+            if (s->wrap && !s->isync && s->ivalid) strm->adler = s->icheck;
             s->result = Z_STREAM_END;
         } else {
             s->result = Z_DATA_ERROR;
@@ -3161,6 +3447,10 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
     }
     for (;;) {
         const bool resume = s->imode == 1;
+        // inflateValidate(strm, 0) on a zlib / gzip stream: the decode stops after
+        // the header and goes on raw from there, so that the trailer is read on
+        // the host, unchecked
+        const bool hdr_stop = !s->ivalid && s->wrap && !resume && !block;
         const size_t hl = resume ? s->hist.size() : 0;
         std::vector<uint8_t> o;
         InflateTry t{};
@@ -3170,12 +3460,19 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             rc = L.rc;
             // inflate(Z_BLOCK): stop after the header (zlib / gzip, from the
             // start) or at the end of the next block
-            const uint32_t mode = !block ? 0u : ((!resume && s->wrap) ? 1u : 2u) | (resume && s->itype ? 4u : 0u);
+            const uint32_t mode = hdr_stop ? 1u
+                                  : !block ? 0u : ((!resume && s->wrap) ? 1u : 2u) | (resume && s->itype ? 4u : 0u);
             if (!rc) rc = inflate_try_locked(*L.c, s->in.data(), s->in.size(), resume,
                                              resume ? s->res_bit - 8ull * s->in_base : 0, s->hist.data(), hl,
                                              hl + s->cap, s->wrap, s->wbits, o, t, mode);
         }
         if (rc) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : rc;
+        if (t.stop != kIFull) {
+            if (t.zcodes != 0xffffffffu) s->icodes = t.zcodes;
+            const bool in_end_stop = t.stop == kIInEnd;
+            s->isyncpt = in_end_stop && ((t.zstate >> 34) & 1u);
+            s->imark = in_end_stop ? t.zmark : -65536;
+        }
         if (t.stop == kIFull) {                                  // grow the output and decode again
             if (s->cap >= (size_t(1) << 31)) return Z_MEM_ERROR;
             s->cap *= 2;
@@ -3200,6 +3497,21 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             strm->avail_in += (uInt)back;
             strm->total_in = used_abs - s->iadj;
         };
+        if (t.stop == kIBlock && hdr_stop) {                     // the header read: resume raw after it
+            uint64_t bb = t.blk_bit;
+            s->igz = (s->wrap & 2) && s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b;
+            s->icheck = s->igz ? 0u : 1u;
+            s->hist.clear();
+            s->res_bit = bb;
+            s->res_put = 0;
+            s->imode = 1;
+            s->itype = true;
+            const uint64_t drop = (bb >> 3) - s->in_base;
+            s->in.erase(s->in.begin(), s->in.begin() + (std::ptrdiff_t)drop);
+            s->in_base += drop;
+            s->tried = 0;
+            continue;
+        }
         if (t.stop == kIBlock) {
             // inflate(Z_BLOCK) at a block boundary (or before the first block):
             // the output through it, the resume point there, and the input after
@@ -3297,8 +3609,9 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
                 if (is_check) ck = check_of(ck, o.data() + (s->res_put - obase), (size_t)(put_abs - s->res_put));
                 const uint8_t *tr = s->in.data() + (tpos - s->in_base);
                 bool ok = true;
-                if (s->isync) {
-                    // after inflateSync the trailer is read, not checked (wrap &= ~4)
+                if (s->isync || !s->ivalid) {
+                    // after inflateSync, or with inflateValidate(strm, 0), the trailer
+                    // is read, not checked (wrap &= ~4)
                 } else if (s->wrap && !s->igz) {
                     ok = ((uint32_t)tr[0] << 24 | (uint32_t)tr[1] << 16 | (uint32_t)tr[2] << 8 | tr[3]) == ck;
                     if (!ok) strm->msg = const_cast<char *>("incorrect data check");
@@ -3314,7 +3627,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
                     strm->next_in -= back;
                     strm->avail_in += (uInt)back;
                     strm->total_in = used - s->iadj;
-                    if (s->wrap && !s->isync) strm->adler = ck;
+                    if (s->wrap && !s->isync && s->ivalid) strm->adler = ck;
                     s->idt = 64;                                 // the last block, done
                 } else {
                     s->result = Z_DATA_ERROR;
@@ -3427,6 +3740,22 @@ static int inflate_body(z_streamp strm, int flush) {
     // out, the reference reads no more input
     const bool block = flush == Z_BLOCK;
     const size_t took = s->finished || (block && s->out_pos < s->out.size()) ? 0 : strm->avail_in;
+    if (took && s->iprime_n) {
+        // inflatePrime's bits: P virtual bytes in front of the input, the primed
+        // bits their last ones (a decode reads each byte from bit 0 up), the
+        // decode resumed raw from there; total_in does not count the P bytes
+        const uint32_t P = (s->iprime_n + 7) / 8;
+        const uint64_t v = s->iprime_v << (8 * P - s->iprime_n);
+        for (uint32_t k = 0; k < P; k++) s->in.push_back((uint8_t)(v >> (8 * k)));
+        s->iadj += P;
+        s->res_bit = 8ull * P - s->iprime_n;
+        s->res_put = s->ideliv;
+        if (!s->imode) s->hist.clear();
+        s->imode = 1;
+        s->icheck = 1;
+        s->iprime_n = 0;
+        s->iprime_v = 0;
+    }
     if (took) {
         s->in.insert(s->in.end(), strm->next_in, strm->next_in + took);
         strm->next_in += took;
@@ -3482,6 +3811,8 @@ int inflateSetDictionary(z_streamp strm, const Bytef *dictionary, uInt dictLengt
         const int wb = s->wbits ? s->wbits : s->need_dict ? (s->in[0] >> 4) + 8 : 15;
         const size_t wsize = size_t(1) << wb, keep = std::min<size_t>(dictLength, wsize);
         s->hist.assign(dictionary + (dictLength - keep), dictionary + dictLength);
+        s->iwin.assign(s->hist.begin(), s->hist.end());        // updatewindow(dictionary + dictLength, dictLength)
+        s->iwin_on = true;
         s->res_bit = s->need_dict ? 48 : 0;                    // after CMF, FLG and DICTID
         s->res_put = s->ideliv = s->hist.size();               // the window counts as handed out
         s->icheck = 1;
@@ -3493,6 +3824,97 @@ int inflateSetDictionary(z_streamp strm, const Bytef *dictionary, uInt dictLengt
     } catch (const std::bad_alloc &) {
         return Z_MEM_ERROR;
     }
+}
+
+// inflateBackInit_ / inflateBack / inflateBackEnd (infback.c:25-640): a raw
+// deflate stream pulled through in() and pushed through out() in pieces of at
+// most the caller's window (1 << windowBits bytes).  The decode is the
+// streaming inflate() above, fed whatever in() returns; its output is staged
+// in the caller's window and handed to out() whenever the window is full, at
+// the stream end and before any error return, as infback.c's inf_leave does.
+// Unused input is left in strm->next_in / avail_in; total_in / total_out are
+// not touched.  Returns Z_STREAM_END, Z_DATA_ERROR, Z_MEM_ERROR or Z_BUF_ERROR
+// (in() gave no input: strm->next_in is then Z_NULL; or out() returned nonzero).
+int inflateBackInit_(z_streamp strm, int windowBits, unsigned char *window, const char *version, int stream_size) {
+    if (!version || version[0] != ZGPU_ZLIB_VERSION[0] || stream_size != (int)sizeof(z_stream))
+        return Z_VERSION_ERROR;                                       // infback.c:30-32
+    if (!strm || !window || windowBits < 8 || windowBits > 15) return Z_STREAM_ERROR;
+    strm->msg = nullptr;
+    internal_state *s = new_state(strm);
+    if (!s) return Z_MEM_ERROR;
+    s->inflating = 1;
+    s->wrap = 0;
+    s->wbits = windowBits;
+    s->iback_win = window;
+    s->out_pos = 0;
+    s->finished = 0;
+    strm->state = s;
+    return Z_OK;
+}
+
+int inflateBack(z_streamp strm, in_func in, void *in_desc, out_func out, void *out_desc) {
+    if (!strm || !strm->state || !strm->state->inflating || !strm->state->iback_win || !in || !out)
+        return Z_STREAM_ERROR;
+    internal_state *s = strm->state;
+    const uLong tin = strm->total_in, tout = strm->total_out, adl = strm->adler;
+    if (int rc = inflateReset(strm)) return rc;                          // mode = TYPE, whave = 0
+    unsigned char *win = s->iback_win;
+    const unsigned wsize = 1u << s->wbits;
+    const unsigned char *next = strm->next_in;
+    unsigned have = next ? strm->avail_in : 0;
+    unsigned left = wsize;                                               // window bytes still free
+    int ret = Z_BUF_ERROR;
+    for (;;) {
+        if (have == 0) {
+            have = in(in_desc, &next);
+            if (have == 0) { next = nullptr; ret = Z_BUF_ERROR; break; }
+        }
+        strm->next_in = next;
+        strm->avail_in = have;
+        strm->next_out = win + (wsize - left);
+        strm->avail_out = left;
+        const int r = inflate(strm, Z_NO_FLUSH);
+        next = strm->next_in;
+        have = strm->avail_in;
+        left = strm->avail_out;
+        if (r == Z_STREAM_END) { ret = Z_STREAM_END; break; }
+        if (r == Z_DATA_ERROR || r == Z_MEM_ERROR || r == Z_STREAM_ERROR) { ret = r; break; }
+        if (left == 0) {                                                 // the window is full
+            if (out(out_desc, win, wsize)) { ret = Z_BUF_ERROR; left = wsize; break; }
+            left = wsize;
+        }
+        // the decode keeps what it has not handed out yet: drain it into the window
+        while (s->out_pos < s->out.size() && left) {
+            strm->next_in = next;
+            strm->avail_in = 0;
+            strm->next_out = win + (wsize - left);
+            strm->avail_out = left;
+            const int r2 = inflate(strm, Z_NO_FLUSH);
+            left = strm->avail_out;
+            if (left == 0) {
+                if (out(out_desc, win, wsize)) { ret = Z_BUF_ERROR; left = wsize; goto leave; }
+                left = wsize;
+            }
+            if (r2 == Z_STREAM_END) { ret = Z_STREAM_END; goto leave; }
+            if (r2 != Z_OK) { ret = r2; goto leave; }
+        }
+    }
+leave:
+    // inf_leave: the window's leftover output, then the unused input
+    if (left < wsize && out(out_desc, win, wsize - left) && ret == Z_STREAM_END) ret = Z_BUF_ERROR;
+    strm->next_in = next;
+    strm->avail_in = next ? have : 0;
+    strm->total_in = tin;
+    strm->total_out = tout;
+    strm->adler = adl;
+    return ret;
+}
+
+int inflateBackEnd(z_streamp strm) {
+    if (!strm || !strm->state || !strm->state->inflating || !strm->state->iback_win) return Z_STREAM_ERROR;
+    free_state(strm, strm->state);
+    strm->state = nullptr;
+    return Z_OK;
 }
 
 int inflateEnd(z_streamp strm) {
@@ -3567,7 +3989,10 @@ int inflateSync(z_streamp strm) {
     s->isyncing = false;
     s->itype = true;                                            // mode TYPE
     s->itail = false;
-    if (hdr) strm->adler = s->igz ? 0 : 1;                      // inflateReset: adler = wrap & 1
+    // inflate.c:1410-1416: wrap &= ~4, then inflateReset's adler = wrap & 1 --
+    // the stream's wrap setting (1 zlib, 2 gzip, 3 auto-detect), not the header
+    // found: an auto-detecting stream reports 1 after a gzip header too
+    if (hdr) strm->adler = (uLong)(s->wrap & 1);
     return Z_OK;
 }
 
@@ -3591,7 +4016,29 @@ int deflate(z_streamp strm, int flush) {
 }
 int inflate(z_streamp strm, int flush) {
     try {
-        return inflate_body(strm, flush);
+        const bool ok = strm && strm->state && strm->state->inflating;
+        const Bytef *next0 = ok ? strm->next_out : nullptr;
+        const uInt out0 = ok ? strm->avail_out : 0;
+        const int rc = inflate_body(strm, flush);
+        if (ok && strm->state) {
+            // updatewindow's condition (inflate.c:1249-1256): the window exists, or
+            // this call wrote output, did not stop on an error and did not end the
+            // stream under Z_FINISH
+            internal_state *s = strm->state;
+            const size_t n = out0 - strm->avail_out;
+            const bool bad = rc == Z_DATA_ERROR || rc == Z_MEM_ERROR || rc == Z_STREAM_ERROR;
+            if (s->iwin_on || (n && !bad && (rc != Z_STREAM_END || flush != Z_FINISH))) {
+                s->iwin_on = true;
+                const size_t ws = inflate_wsize(s);
+                if (n >= ws) {
+                    s->iwin.assign(next0 + (n - ws), next0 + n);
+                } else {
+                    s->iwin.insert(s->iwin.end(), next0, next0 + n);
+                    if (s->iwin.size() > ws) s->iwin.erase(s->iwin.begin(), s->iwin.end() - (std::ptrdiff_t)ws);
+                }
+            }
+        }
+        return rc;
     } catch (const std::bad_alloc &) {
         return Z_MEM_ERROR;
     }

@@ -3114,13 +3114,18 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
         stg_or(stg, s_obit - st.sbase, v);
         s_obit += nb;
     };
-    // a streaming job's record k (tid 0): the output bit after it and the
-    // partial byte there (still in the staging window)
+    // bi_used at the record's last bi_windup (trees.c: ((bi_valid - 1) & 7) + 1,
+    // deflateUsed), 0 when the record has none (tid 0)
+    int wu = 0, wu_last = 0;
+    auto windup_mark = [&]() { wu = wu_last = (int)((s_obit - 1) & 7) + 1; };
+    // a streaming job's record k (tid 0): the output bit after it, the
+    // partial byte there (still in the staging window) and wu << 8
     auto stream_rec = [&](uint32_t k) {
         if (!job.srec) return;
         const int64_t r = s_obit - st.sbase;
         job.srec[4ull * k] = (uint64_t)s_obit;
-        job.srec[4ull * k + 1] = (stg[r >> 5] >> (((r >> 3) & 3) * 8)) & ((1u << (r & 7)) - 1u);
+        job.srec[4ull * k + 1] = ((stg[r >> 5] >> (((r >> 3) & 3) * 8)) & ((1u << (r & 7)) - 1u)) | (uint64_t)wu << 8;
+        wu = 0;
     };
 
     if (tid == 0) {
@@ -3174,6 +3179,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
             done += len;
             if (last) break;
         } while (true);
+        wu_last = 8;                                    // the final block's bi_windup, byte aligned already
     } else {
         const uint32_t nblk = job.nblocks[bi];
         for (uint32_t g0 = 0; g0 < nblk; g0 += kEncGroup) {
@@ -3210,6 +3216,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
                         put(0, 7);                      // END_BLOCK in the static tree
                     } else if (kind == 2 || kind == 3) {   // _tr_stored_block(s, 0, 0, 0)
                         put(0, 3);
+                        windup_mark();
                         s_obit = (s_obit + 7) & ~7ll;
                         put(0, 16);
                         put(0xffffu, 16);
@@ -3229,6 +3236,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
                 const uint64_t stored_len = br.in_end - br.in_start;
                 put((uint32_t)(type << 1) + (last ? 1u : 0u), 3);
                 if (type == 0) {
+                    windup_mark();
                     s_obit = (s_obit + 7) & ~7ll;
                     put((uint32_t)stored_len & 0xffffu, 16);
                     put((~(uint32_t)stored_len) & 0xffffu, 16);
@@ -3316,7 +3324,10 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
                     __syncthreads();
                 }
             }
-            if (last && tid == 0) s_obit = (s_obit + 7) & ~7ll;   // bi_windup
+            if (last && tid == 0) {                  // bi_windup
+                windup_mark();
+                s_obit = (s_obit + 7) & ~7ll;
+            }
             __syncthreads();
             if (job.srec) {                      // a streaming job: where this block ends
                 if (tid == 0) stream_rec(k);
@@ -3328,6 +3339,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
     // trailer
     __syncthreads();
     if (s_obit - st.sbase + 96 > kStgBits) stg_flush(st, s_obit, false);
+    if (tid == 0 && job.wind) job.wind[bi] = (uint8_t)wu_last;
     if (tid == 0) {
         const uint32_t ck = job.check[bi];
         if (job.wrap == 1) {                    // Adler-32, big-endian (deflate.c:1253-1256)
@@ -3492,6 +3504,7 @@ __global__ __launch_bounds__(kEScanThreads) void k_enc_scan(DeflateJob job) {
                 const uint64_t st = off, v = s_v[i];
                 const uint32_t ty = s_ty[i];
                 off = (ty & 3u) == 0 ? ((off + 3 + 7) & ~7ull) + 32 + 8 * v : off + v;
+                if ((ty & 4u) && job.wind) job.wind[bi] = (uint8_t)(((off - 1) & 7) + 1);   // deflateUsed
                 if (ty & 4u) off = (off + 7) & ~7ull;      // bi_windup
                 s_v[i] = st;
             }
@@ -3716,6 +3729,10 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
         }
         __syncthreads();
     }
+    // the bits written must be the bits k_enc_scan placed (block_plan's
+    // opt_len / static_len): a difference would overlap or gap the
+    // neighbouring blocks, so it is reported as an error, never as bytes
+    if (tid == 0 && s_obit != re + sh) job.status[g] = -2;
     eflush(s_obit, true);
 }
 

@@ -207,6 +207,65 @@ __device__ __attribute__((always_inline)) inline uint64_t bitpos(const Rd &r) {
 __device__ __attribute__((always_inline)) inline void dropb(Rd &r, uint32_t k) { r.hold >>= k; r.bits -= k; }
 __device__ __attribute__((always_inline)) inline void seek(Rd &r, uint32_t byte) { r.hold = 0; r.bits = 0; r.ipos = byte; }
 
+// inflateCodesUsed (inflate.c:1521-1527): the code-table entries inftrees.c's
+// inflate_table uses for a code of n lengths at root bits (inflate.c's lenbits 9
+// / distbits 6): 1 << root for the root table (root clamped to [min, max]
+// length) plus, for every run of codes longer than root that shares its top root
+// bits, a sub-table of 1 << curr entries, curr grown while the codes still to
+// place overfill it (inftrees.c:214-300).  2 for a code with no lengths.
+// Uniform across the wave; run only for streams that ask (InflateJob::zcodes).
+__device__ uint32_t codes_used(const uint16_t *lens, int n, int root, int lane) {
+    uint32_t cnt[16];
+#pragma unroll
+    for (int L = 0; L < 16; L++) cnt[L] = 0;
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        const int i = c0 + lane;
+        const uint32_t l = i < n ? lens[i] : 0u;
+#pragma unroll
+        for (int L = 1; L < 16; L++) cnt[L] += (uint32_t)__popcll(__ballot(i < n && l == (uint32_t)L));
+    }
+    int max = 15;
+    while (max >= 1 && cnt[max] == 0) max--;
+    if (max == 0) return 2;
+    int min = 1;
+    while (min < max && cnt[min] == 0) min++;
+    if (root > max) root = max;
+    if (root < min) root = min;
+    uint32_t used = 1u << root, code = 0, next[16], rem[16];
+    next[0] = 0;
+    rem[0] = 0;
+    for (int L = 1; L < 16; L++) {
+        code = (code + (L > 1 ? cnt[L - 1] : 0u)) << 1;
+        next[L] = code;
+        rem[L] = cnt[L];
+    }
+    uint32_t low = 0xffffffffu;
+    for (int L = root + 1; L <= max; L++) {
+        for (int c0 = 0; c0 < n; c0 += 64) {
+            const int i = c0 + lane;
+            uint64_t m = __ballot(i < n && lens[i] == (uint16_t)L);
+            while (m) {
+                m &= m - 1;
+                const uint32_t key = next[L] >> (L - root);
+                if (key != low) {
+                    int curr = L - root, left = 1 << curr;
+                    while (curr + root < max) {
+                        left -= (int)rem[curr + root];
+                        if (left <= 0) break;
+                        curr++;
+                        left <<= 1;
+                    }
+                    used += 1u << curr;
+                    low = key;
+                }
+                next[L]++;
+                rem[L]--;
+            }
+        }
+    }
+    return used;
+}
+
 __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
     __shared__ InfLDS S;
     const int lane = threadIdx.x;
@@ -235,6 +294,11 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
     uint32_t blk_put = 0;
     uint32_t zlast = 0;                              // BFINAL of the current block (data_type)
     bool ztype = (job.stop_mode & 4u) != 0;          // waiting at a block header in mode TYPE
+    bool zstored = false;                            // stopped in mode STORED with no bits held (inflateSyncPoint)
+    // inflateMark's value where the input ran out (inflate.c:1510-1519): back << 16, plus a stored
+    // block's bytes left (COPY); back = -1 outside a length/distance symbol
+    int64_t zmark = -65536;
+    uint32_t zcodes = 0xffffffffu;                   // inflateCodesUsed of the last dynamic block (none: ~0)
     if (job.res_bit) {
         seek(r, (uint32_t)(rb >> 3));
         refill(S, r, in, n, lane);
@@ -332,7 +396,7 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
         if (type == 0) {                                             // STORED, COPY
             dropb(r, r.bits & 7u);
             refill(S, r, in, n, lane);
-            if (bitpos(r) + 32 > inbits) { stop = kIInEnd; used = n; goto done; }
+            if (bitpos(r) + 32 > inbits) { zstored = bitpos(r) == inbits; stop = kIInEnd; used = n; goto done; }
             const uint32_t len = (uint32_t)r.hold & 0xffffu, nlen = ((uint32_t)r.hold >> 16) & 0xffffu;
             if (len != (nlen ^ 0xffffu)) { stop = kIData; used = (bitpos(r) >> 3) + 4; goto done; }
             dropb(r, 32);
@@ -347,6 +411,7 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
             ob = put;
             seek(r, bp + cnt);
             if (cnt < len) {
+                zmark = -65536 + (int64_t)(len - cnt);      // COPY: length bytes still to copy
                 if (put == cap) { stop = kIFull; used = bp + cnt; } else { stop = kIInEnd; used = n; }
                 goto done;
             }
@@ -431,13 +496,15 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
                 if (!build_code<kDRoot>(S.lens + nlen, (int)ndist, kDists, S.dt, &S.dcan, lane)) {
                     stop = kIData; used = ceil_used(); goto done;
                 }
+                if (job.zcodes)
+                    zcodes = codes_used(S.lens, (int)nlen, 9, lane) + codes_used(S.lens + nlen, (int)ndist, 6, lane);
             }
             // ---------------- LEN .. MATCH / LIT ----------------
             for (;;) {
                 refill(S, r, in, n, lane);
                 uint32_t L;
                 const uint32_t sym = dec_code<kLRoot>(S.lt, &S.lcan, r.hold, L);
-                if (bitpos(r) + L > inbits) { stop = kIInEnd; used = n; goto done; }
+                if (bitpos(r) + L > inbits) { zmark = 0; stop = kIInEnd; used = n; goto done; }   // LEN: back 0
                 dropb(r, L);
                 if (sym < 256) {
                     if (put == cap) { stop = kIFull; used = ceil_used(); goto done; }
@@ -450,17 +517,17 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
                 if (sym == 256) break;
                 if (sym > 285) { stop = kIData; used = ceil_used(); goto done; }   // kSymBad, 286, 287
                 const uint32_t ls = sym - 257, xl = c_lext[ls];
-                if (bitpos(r) + xl > inbits) { stop = kIInEnd; used = n; goto done; }
+                if (bitpos(r) + xl > inbits) { zmark = (int64_t)L << 16; stop = kIInEnd; used = n; goto done; }
                 const uint32_t len = c_lbase[ls] + ((uint32_t)r.hold & ((1u << xl) - 1u));
                 dropb(r, xl);
                 refill(S, r, in, n, lane);
                 uint32_t DL;
                 const uint32_t ds = dec_code<kDRoot>(S.dt, &S.dcan, r.hold, DL);
-                if (bitpos(r) + DL > inbits) { stop = kIInEnd; used = n; goto done; }
+                if (bitpos(r) + DL > inbits) { zmark = (int64_t)(L + xl) << 16; stop = kIInEnd; used = n; goto done; }
                 dropb(r, DL);
                 if (ds > 29) { stop = kIData; used = ceil_used(); goto done; }
                 const uint32_t xd = c_dext[ds];
-                if (bitpos(r) + xd > inbits) { stop = kIInEnd; used = n; goto done; }
+                if (bitpos(r) + xd > inbits) { zmark = (int64_t)(L + xl + DL) << 16; stop = kIInEnd; used = n; goto done; }
                 const uint32_t dist = c_dbase[ds] + ((uint32_t)r.hold & ((1u << xd) - 1u));
                 dropb(r, xd);
                 if (put == cap) { stop = kIFull; used = ceil_used(); goto done; }    // MATCH: room first
@@ -541,7 +608,9 @@ done:
         }
         if (job.zstate_out) {
             const uint64_t bp = bitpos(r);
-            job.zstate_out[g] = (bp <= inbits ? inbits - bp : 0) | (uint64_t)zlast << 32 | (uint64_t)(ztype ? 1 : 0) << 33;
+            job.zstate_out[2 * (uint64_t)g] = (bp <= inbits ? inbits - bp : 0) | (uint64_t)zlast << 32 |
+                                              (uint64_t)(ztype ? 1 : 0) << 33 | (uint64_t)(zstored ? 1 : 0) << 34;
+            job.zstate_out[2 * (uint64_t)g + 1] = (uint64_t)(uint32_t)(int32_t)zmark | (uint64_t)zcodes << 32;
         }
     }
 }

@@ -149,6 +149,7 @@ struct DeflateJob {
     BlockRec *blocks;        // [Σ(n/16383 + 2)]
     uint32_t *nblocks;       // [count]
     uint32_t *check;         // [count] adler32 / crc32 of the input (trailer)
+    uint8_t *wind;           // [count] or null: bi_used at the stream's last bi_windup (deflateUsed)
     // deflate(flush) calls of a streaming job (count == 1, zgpu_api.cpp deflate()):
     // the input position where each flush call ended (ascending) and its kind
     // (Z_PARTIAL_FLUSH 1, Z_SYNC_FLUSH 2, Z_FULL_FLUSH 3 -- only as the job's
@@ -331,6 +332,10 @@ struct InflateJob {
     // at a block header (mode TYPE) << 33.  stop_mode bit 2: the decode starts
     // in mode TYPE (resumed at a boundary), not TYPEDO / HEAD
     uint64_t *zstate_out;
+    // [2g + 1] of zstate_out: inflateMark's value where the input ran out (low 32 bits, signed) and
+    // inflateCodesUsed of the last dynamic block (high 32 bits; ~0: none in this decode), computed
+    // only when zcodes is set
+    int zcodes;
 };
 int launch_inflate_stage(int stage, const InflateJob &job, hipStream_t st);
 

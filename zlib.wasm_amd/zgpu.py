@@ -49,6 +49,10 @@ EXPORTED_SYMBOLS = (
     "uncompress", "uncompress2", "inflateInit_", "inflateInit2_", "inflate", "inflateEnd",
     "inflateReset", "inflateGetHeader", "inflateSync", "inflateCopy", "deflateSetDictionary", "deflateParams", "deflateTune", "deflatePrime",
     "deflateSetHeader", "inflateSetDictionary",
+    "zError", "zlibCompileFlags", "get_crc_table", "deflateUsed", "deflateGetDictionary",
+    "deflateResetKeep", "inflateReset2", "inflateResetKeep", "inflatePrime", "inflateGetDictionary",
+    "inflateSyncPoint", "inflateUndermine", "inflateValidate", "inflateMark", "inflateCodesUsed",
+    "inflateBackInit_", "inflateBack", "inflateBackEnd",
     # include/zgpu_wasm.h
     "zlib_compress_buffer", "zlib_crc32", "zlib_adler32", "zlib_compress_bound",
     "zlib_get_version", "zlib_compress_simd", "zlib_compress_simd_full",
