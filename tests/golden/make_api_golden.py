@@ -166,35 +166,40 @@ def inflate_sessions():
 
 
 def deflate_sessions():
+    """deflate ops carry a data slice [kind, n, seed, start, end] (datagen),
+    made into bytes when the session runs (run_deflate)"""
     S = []
-    t = datagen.make("text", 100000, 81)
-    m = datagen.make("mix", 100000, 82)
+    t = ["text", 100000, 81]
+    m = ["mix", 100000, 82]
+    sl = lambda d, a, b: d + [a, b]
     for level in (0, 1, 6, 9):
         for wb in (15, -15, 31):
             ops = [["init", level, wb, 8, 0], ["used"], ["getdict"]]
             for i, fl in enumerate((Z_NO_FLUSH, Z_SYNC_FLUSH, Z_PARTIAL_FLUSH, Z_BLOCK, Z_NO_FLUSH, Z_SYNC_FLUSH)):
-                ops += [["deflate", m[i * 9000:(i + 1) * 9000], fl], ["used"], ["getdict"]]
-            ops += [["deflate", t[:40000], Z_NO_FLUSH], ["used"], ["getdict"],
-                    ["deflate", t[40000:], Z_FINISH], ["used"], ["getdict"]]
+                ops += [["deflate", sl(m, i * 9000, (i + 1) * 9000), fl], ["used"], ["getdict"]]
+            ops += [["deflate", sl(t, 0, 40000), Z_NO_FLUSH], ["used"], ["getdict"],
+                    ["deflate", sl(t, 40000, 100000), Z_FINISH], ["used"], ["getdict"]]
             S.append({"name": f"used-getdict-L{level}-w{wb}", "ops": ops})
-        S.append({"name": f"used-one-shot-L{level}", "ops": [["init", level, 15, 8, 0], ["deflate", m, Z_FINISH],
+        S.append({"name": f"used-one-shot-L{level}", "ops": [["init", level, 15, 8, 0],
+                                                             ["deflate", sl(m, 0, 100000), Z_FINISH],
                                                              ["used"], ["getdict"]]})
         S.append({"name": f"used-small-out-L{level}", "ops": [["init", level, 15, 8, 0],
-                                                              ["deflate", t[:60000], Z_NO_FLUSH, 4000], ["used"],
-                                                              ["getdict"], ["deflate", t[60000:], Z_FINISH, 4000],
+                                                              ["deflate", sl(t, 0, 60000), Z_NO_FLUSH, 4000], ["used"],
+                                                              ["getdict"], ["deflate", sl(t, 60000, 100000), Z_FINISH, 4000],
                                                               ["used"]]})
     for strategy in (1, 2, 3, 4):
         S.append({"name": f"used-strategy-{strategy}", "ops": [["init", 6, 15, 8, strategy],
-                                                               ["deflate", m[:50000], Z_SYNC_FLUSH], ["used"],
-                                                               ["deflate", m[50000:], Z_FINISH], ["used"]]})
+                                                               ["deflate", sl(m, 0, 50000), Z_SYNC_FLUSH], ["used"],
+                                                               ["deflate", sl(m, 50000, 100000), Z_FINISH], ["used"]]})
     for wb in (-15, 15, -10):
-        S.append({"name": f"getdict-setdict-w{wb}", "ops": [["init", 6, wb, 8, 0], ["dict", t[:50000]], ["getdict"],
-                                                            ["deflate", m[:20000], Z_NO_FLUSH], ["getdict"],
-                                                            ["deflate", b"", Z_FINISH], ["getdict"]]})
-        S.append({"name": f"getdict-setdict-L0-w{wb}", "ops": [["init", 0, wb, 8, 0], ["dict", t[:500]], ["getdict"],
-                                                               ["deflate", m[:20000], Z_SYNC_FLUSH], ["getdict"]]})
-    S.append({"name": "resetkeep-fresh", "ops": [["init", 6, 15, 8, 0], ["resetkeep"], ["deflate", m, Z_FINISH],
-                                                 ["used"], ["reset"], ["resetkeep"], ["deflate", t, Z_FINISH]]})
+        S.append({"name": f"getdict-setdict-w{wb}", "ops": [["init", 6, wb, 8, 0], ["dict", sl(t, 0, 50000)], ["getdict"],
+                                                            ["deflate", sl(m, 0, 20000), Z_NO_FLUSH], ["getdict"],
+                                                            ["deflate", sl(m, 0, 0), Z_FINISH], ["getdict"]]})
+        S.append({"name": f"getdict-setdict-L0-w{wb}", "ops": [["init", 0, wb, 8, 0], ["dict", sl(t, 0, 500)], ["getdict"],
+                                                               ["deflate", sl(m, 0, 20000), Z_SYNC_FLUSH], ["getdict"]]})
+    S.append({"name": "resetkeep-fresh", "ops": [["init", 6, 15, 8, 0], ["resetkeep"],
+                                                 ["deflate", sl(m, 0, 100000), Z_FINISH], ["used"], ["reset"],
+                                                 ["resetkeep"], ["deflate", sl(t, 0, 100000), Z_FINISH]]})
     return S
 
 
@@ -223,8 +228,13 @@ def run_inflate(L, sess):
     return {"res": res, "outs": [[len(o), hashlib.sha256(o).hexdigest()] for o in outs]}
 
 
+def _slice(spec):
+    kind, n, seed, a, b = spec
+    return datagen.make(kind, n, seed)[a:b]
+
+
 def run_deflate(L, sess):
-    ops = [[o[0], bytes.fromhex(o[1])] + o[2:] if o[0] in ("deflate", "dict") else o for o in sess["ops"]]
+    ops = [[o[0], _slice(o[1])] + o[2:] if o[0] in ("deflate", "dict") else o for o in sess["ops"]]
     rcs, out = run_zsession(L, ops)
     return {"res": rcs, "out": [len(out), hashlib.sha256(out).hexdigest()]}
 
@@ -236,24 +246,18 @@ def run_backcase(L, case):
     return {"res": [rc0, rc, unused, null_in, rc2], "out": [len(out), hashlib.sha256(out).hexdigest()]}
 
 
-def jsonable(sess):
-    """deflate ops carry bytes: stored as hex"""
-    return dict(sess, ops=[[o[0], o[1].hex()] + o[2:] if o[0] in ("deflate", "dict") else o for o in sess["ops"]])
-
-
 def main():
     ref = Reference()
     out = {"reference": ref.version.decode(), "inflate": [], "deflate": [], "back": []}
     for sess in inflate_sessions():
         out["inflate"].append(dict(sess, **run_inflate(ref.L, sess)))
     for sess in deflate_sessions():
-        js = jsonable(sess)
-        out["deflate"].append(dict(js, **run_deflate(ref.L, js)))
+        out["deflate"].append(dict(sess, **run_deflate(ref.L, sess)))
     for case in back_cases():
         out["back"].append(dict(case, **run_backcase(ref.L, case)))
     path = os.path.join(HERE, "api_golden.json")
     with open(path, "w") as f:
-        json.dump(out, f, indent=0, sort_keys=True)
+        json.dump(out, f, separators=(",", ":"), sort_keys=True)
     print(f"wrote {path}: {len(out['inflate'])} inflate, {len(out['deflate'])} deflate, {len(out['back'])} back")
 
 
