@@ -674,7 +674,7 @@ def run_dsession(L, data, plan, level=6, wbits=15, mem=8, strategy=0, version=b"
     ib = C.create_string_buffer(bytes(data), max(len(data), 1))
     base = C.addressof(ib)
     out, recs, offered = bytearray(), [], 0
-    ob = C.create_string_buffer(1 << 20)
+    ob = C.create_string_buffer(max([1 << 20] + [p[2] for p in plan]))
     for new, flush, avail, loop in plan:
         offered = min(len(data), offered + new)
         while True:

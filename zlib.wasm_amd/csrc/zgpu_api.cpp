@@ -1034,6 +1034,7 @@ struct InflateResumeDev {          // InflateJob's resume arrays (device, per st
     uint64_t *blk_out;
     uint32_t stop_mode;            // InflateJob::stop_mode
     uint64_t *zstate_out;          // InflateJob::zstate_out
+    uint32_t dmax = 0;             // InflateJob::dmax
 };
 
 int inflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
@@ -1098,6 +1099,7 @@ int inflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.stop_mode = rs->stop_mode;
             job.zstate_out = rs->zstate_out;
             job.zcodes = rs->zstate_out != nullptr;
+            job.dmax = rs->dmax;
         }
         if (T.run(3, st, [&] { return launch_inflate_stage(0, job, st); })) return ZGPU_MEM_ERROR;
         if (T.run(4, st, [&] { return launch_inflate_stage(1, job, st); })) return ZGPU_MEM_ERROR;
@@ -1187,7 +1189,7 @@ struct InflateTry {
 
 int inflate_try_locked(Ctx &c, const uint8_t *in, size_t n, bool resume, uint64_t start_bit, const uint8_t *hist,
                        size_t hist_len, size_t cap, int wrap, int wbits, std::vector<uint8_t> &out, InflateTry &t,
-                       uint32_t stop_mode = 0) {
+                       uint32_t stop_mode = 0, uint32_t dmax = 0) {
     if (!c.ws_io.ensure(n + 64) || !c.ws_io2.ensure(cap + 64) || !c.ws_small.ensure(8 * 16 + 64) ||
         !c.ws_istop.ensure(64))
         return ZGPU_MEM_ERROR;
@@ -1209,7 +1211,7 @@ int inflate_try_locked(Ctx &c, const uint8_t *in, size_t n, bool resume, uint64_
         hipMemcpyAsync(d_rbit, &rbit, 8, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(d_hist, &hl, 4, hipMemcpyHostToDevice, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
-    const InflateResumeDev rs{resume ? d_rbit : nullptr, resume ? d_hist : nullptr, d_blk, stop_mode, d_zs};
+    const InflateResumeDev rs{resume ? d_rbit : nullptr, resume ? d_hist : nullptr, d_blk, stop_mode, d_zs, dmax};
     int rc = inflate_dev_locked(c, d_in, m, m + 1, d_out, m + 2, m + 3, m + 4, m + 5, d_st, d_stop, 1,
                                 resume ? 0 : wrap, wbits, st, &rs);
     if (rc) return rc;
@@ -1835,6 +1837,10 @@ struct internal_state {
     zvec<uint8_t> iwin;
     bool iwin_on = false;
     bool ivalid = true;                  // inflateValidate: the check values are verified (wrap & 4)
+    // strm->adler as inflate.c keeps it on a zlib / gzip stream: 1 (zlib, after DICT) or 0 (gzip,
+    // after its header), then the check of every byte written (inflate.c inf_leave UPDATE_CHECK)
+    bool iadl_on = false;
+    uint32_t iadl = 0;
     // where the last decode left inflate.c's state (InflateJob::zstate_out): mode STORED with no bits
     // held (inflateSyncPoint), inflateMark's value, inflateCodesUsed of the last dynamic block
     bool isyncpt = false;
@@ -2624,6 +2630,18 @@ static int deflate_body(z_streamp strm, int flush) {
         }
         if (rc || st) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : (rc ? rc : st);
         {
+            // the window as the reference leaves it, for deflateGetDictionary: all
+            // input read (E = n) and the window offset of the final fill_window,
+            // which with all input present depends on n alone: the k-th slide
+            // happens once strstart - S >= w_size + MAX_DIST (deflate.c:277)
+            const uint64_t w = uint64_t(1) << s->wbits, maxd = w - kMinLookahead;
+            uint64_t S = 0;
+            while (S + w + maxd <= sl) S += w;
+            const size_t keep = (size_t)std::min<uint64_t>(sl, w);
+            s->in.assign(sp + (sl - keep), sp + sl);
+            s->in_base = sl - keep;
+            s->rd = s->rd_seen = sl;
+            s->res_S = S;
             strm->next_out += cap;
             strm->avail_out -= (uInt)cap;
             strm->total_out += cap;
@@ -3255,9 +3273,10 @@ int inflateReset(z_streamp strm) {
     s->iadj = 0;
     s->iwin.clear(); s->iwin_on = false;                               // wsize = whave = wnext = 0
     s->isyncpt = false; s->imark = -65536; s->icodes = 0; s->iprime_n = 0; s->iprime_v = 0;
+    s->iadl_on = false; s->iadl = 0;
     strm->total_in = strm->total_out = 0;
     strm->msg = nullptr;
-    strm->adler = s->wrap & 1;
+    if (s->wrap) strm->adler = s->wrap & 1;                           // inflateResetKeep: only when wrapped
     return Z_OK;
 }
 
@@ -3464,7 +3483,8 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
                                   : !block ? 0u : ((!resume && s->wrap) ? 1u : 2u) | (resume && s->itype ? 4u : 0u);
             if (!rc) rc = inflate_try_locked(*L.c, s->in.data(), s->in.size(), resume,
                                              resume ? s->res_bit - 8ull * s->in_base : 0, s->hist.data(), hl,
-                                             hl + s->cap, s->wrap, s->wbits, o, t, mode);
+                                             hl + s->cap, s->wrap, s->wbits, o, t, mode,
+                                             s->iback_win ? 1u << s->wbits : 0u);
         }
         if (rc) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : rc;
         if (t.stop != kIFull) {
@@ -3569,6 +3589,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
         if (!resume && t.stop != kIInEnd) {                      // the whole stream in one attempt
             append_new(put_abs);
             s->finished = 1;
+            s->igz = (s->wrap & 2) && s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b;
             if (t.stop == kIEnd) {
                 s->result = Z_STREAM_END;
                 const size_t extra = in_end - t.used;            // give back input past the stream end
@@ -3641,6 +3662,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
         // the stream goes on: hand out its prefix, move the resume point
         append_new(put_abs);
         s->tried = in_end;
+        if (!resume) s->igz = (s->wrap & 2) && s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b;
         if (block)                                               // where the input ran out (inflate.c:1267-1269)
             s->idt = (int)(t.zstate & 0xffffffffu) + ((t.zstate >> 32) & 1u ? 64 : 0) + ((t.zstate >> 33) & 1u ? 128 : 0);
         uint64_t bb = t.blk_bit, bp = t.blk_put;
@@ -4027,7 +4049,25 @@ int inflate(z_streamp strm, int flush) {
             internal_state *s = strm->state;
             const size_t n = out0 - strm->avail_out;
             const bool bad = rc == Z_DATA_ERROR || rc == Z_MEM_ERROR || rc == Z_STREAM_ERROR;
-            if (s->iwin_on || (n && !bad && (rc != Z_STREAM_END || flush != Z_FINISH))) {
+            // the check value of a zlib / gzip stream as each call leaves it: the
+            // running check of the bytes written, from 1 (zlib) / 0 (gzip) once the
+            // header is in; none after inflateSync or with inflateValidate(0)
+            if (s->wrap && !s->isync && !s->iback_win && !s->need_dict) {
+                if (!s->iadl_on && (n || s->imode == 1 || s->finished)) {
+                    s->iadl_on = true;
+                    s->iadl = s->igz ? 0u : 1u;
+                }
+                if (s->iadl_on) {
+                    if (n && s->ivalid)
+                        s->iadl = s->igz ? (uint32_t)crc32_z(s->iadl, next0, n) : (uint32_t)adler32_z(s->iadl, next0, n);
+                    strm->adler = s->iadl;
+                }
+            }
+            // inflate.c CHECK resets its output count (out = left) before inf_leave's
+            // updatewindow: the call that completes a zlib / gzip stream adds
+            // nothing to the window
+            const bool checked = rc == Z_STREAM_END && s->wrap != 0;
+            if (!checked && (s->iwin_on || (n && !bad && (rc != Z_STREAM_END || flush != Z_FINISH)))) {
                 s->iwin_on = true;
                 const size_t ws = inflate_wsize(s);
                 if (n >= ws) {

@@ -449,6 +449,8 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
                 if (!build_code<kCRoot>(S.lens, 19, kCodes, S.ct, nullptr, lane)) {
                     stop = kIData; used = ceil_used(); goto done;
                 }
+                // mode CODELENS: state->next holds the code-length code's table (inflateCodesUsed)
+                const uint32_t zcl = job.zcodes ? codes_used(S.lens, 19, 7, lane) : 0u;
                 uint32_t have = 0;
                 const uint32_t total = nlen + ndist;
                 while (have < total) {
@@ -458,7 +460,7 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
                     // a repeat code and its extra bits are read together (inflate.c
                     // CODELENS: NEEDBITS(here.bits + 2/3/7)), so a short input keeps both
                     const uint32_t xb = sym == 16 ? 2u : sym == 17 ? 3u : sym == 18 ? 7u : 0u;
-                    if (bitpos(r) + L + xb > inbits) { stop = kIInEnd; used = n; goto done; }
+                    if (bitpos(r) + L + xb > inbits) { zcodes = zcl; stop = kIInEnd; used = n; goto done; }
                     dropb(r, L);
                     if (sym == kSymBad || sym < 16) {                // empty code-length code: 0 per bit
                         if (lane == 0) S.lens[have] = (uint16_t)(sym == kSymBad ? 0 : sym);
@@ -531,7 +533,8 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
                 const uint32_t dist = c_dbase[ds] + ((uint32_t)r.hold & ((1u << xd) - 1u));
                 dropb(r, xd);
                 if (put == cap) { stop = kIFull; used = ceil_used(); goto done; }    // MATCH: room first
-                if (dist > put) { stop = kIData; used = ceil_used(); goto done; }    // too far back
+                // too far back (inflateBack: beyond its window, infback.c:494-499)
+                if (dist > put || (job.dmax && dist > job.dmax)) { stop = kIData; used = ceil_used(); goto done; }
                 const uint32_t copy = len < cap - put ? len : cap - put;
                 if (lane == 0) S.mbuf[nm & (kMBuf - 1)] = (uint64_t)put | ((uint64_t)copy << 32) | ((uint64_t)dist << 41);
                 nm++;

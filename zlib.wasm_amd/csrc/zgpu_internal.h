@@ -336,6 +336,7 @@ struct InflateJob {
     // inflateCodesUsed of the last dynamic block (high 32 bits; ~0: none in this decode), computed
     // only when zcodes is set
     int zcodes;
+    uint32_t dmax;           // inflateBack: distances beyond its window (1 << windowBits) are errors; 0: none
 };
 int launch_inflate_stage(int stage, const InflateJob &job, hipStream_t st);
 
