@@ -31,14 +31,25 @@
  * that ran out of output space is repeated with the same flush (zlib.h) --
  * given more input instead, the stream stays valid but may differ.
  * deflateSetDictionary, deflateSetHeader, deflatePrime, deflateTune and
- * deflateParams give the reference's stream where the change takes effect at a
- * point this library's model knows exactly: before the first deflate() call, or
- * right after a flush with no input pending (deflateParams flushes with Z_BLOCK
- * itself when the level's function or the strategy changes, as deflate.c does).
- * A change the model cannot place -- tuning a stream with unflushed input,
- * switching to or from level 0, Z_HUFFMAN_ONLY or Z_RLE, or between
- * deflate_fast and deflate_slow levels after data, a dictionary at level 0 --
- * returns Z_STREAM_ERROR with strm->msg set, never a different stream.
+ * deflateParams give the reference's stream: deflateParams flushes with Z_BLOCK
+ * itself when the level's function or the strategy changes (as deflate.c does)
+ * and switches between level 0, deflate_fast and deflate_slow levels; a level
+ * change within one function, and deflateTune, take effect at the next decision
+ * even with input pending.  What the model cannot place returns Z_STREAM_ERROR
+ * with strm->msg set, never a different stream (zgpu_api.cpp, `unsupported`):
+ *   - deflateParams to or from Z_HUFFMAN_ONLY / Z_RLE after data (levels 1..9);
+ *   - deflatePrime with input pending after a call that did not reach its end,
+ *     or after Z_STREAM_END;
+ *   - deflateSetDictionary after the stream has ended;
+ *   - deflateResetKeep on a stream that has taken input (the window it would
+ *     carry into the next stream);
+ *   - inflatePrime other than on a raw stream before its first input;
+ *   - inflate(Z_TREES).
+ * inflateUndermine returns Z_DATA_ERROR (as a reference built without
+ * INFLATE_ALLOW_INVALID_DISTANCE_TOOFAR_ARRR does).  inflateBack reports a
+ * distance beyond its window at the first such distance; where out() fails,
+ * the input left in next_in / avail_in may differ from the reference's (whose
+ * bit buffer has pulled bytes ahead).
  */
 #ifndef ZGPU_ZLIB_H
 #define ZGPU_ZLIB_H

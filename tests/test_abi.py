@@ -167,22 +167,31 @@ def test_oversize_buffers_refused_before_gpu_work(lib):
     assert lib.zgpu_compress_batch(src, sl, dst, dln, st, C.c_size_t(1), 6, 1) == -2  # ZGPU_STREAM_ERROR
 
 
-def test_checksums_never_abort_without_gpu(lib):
-    """crc32()/adler32() cannot report errors in zlib's API; without a usable
-    GPU they must return (0) instead of ending the host process."""
+def test_checksums_fail_loudly_without_gpu(lib):
+    """crc32()/adler32() cannot report errors in zlib's API and there is no CPU
+    path: without a usable GPU a call ends the process with a message naming
+    the call (a returned 0 would be a silently wrong check
+    value); ZGPU_CHECKSUM_ERROR=zero opts into returning 0 with a message on
+    every failed call."""
     import subprocess
     import sys
     code = ("import ctypes as C, torch; L = C.CDLL(%r); L.crc32.restype = C.c_ulong; "
             "L.crc32.argtypes = [C.c_ulong, C.c_char_p, C.c_uint]; "
             "L.adler32.restype = C.c_ulong; L.adler32.argtypes = [C.c_ulong, C.c_char_p, C.c_uint]; "
-            "print(L.crc32(0, b'abc', 3), L.adler32(1, b'abc', 3))" % LIB)
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
-                       env=dict(os.environ, HIP_VISIBLE_DEVICES="-1"))
+            "print(L.crc32(0, b'abc', 3), L.adler32(1, b'abc', 3), flush=True)" % LIB)
     import torch
     if torch.cuda.is_available():
         pytest.skip("a GPU is visible")
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="-1")
+    env.pop("ZGPU_CHECKSUM_ERROR", None)              # conftest's setting for the host-side tests
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "crc32 of 3 bytes failed" in r.stderr, (r.returncode, r.stderr[-500:])
+    assert r.stdout == ""
+    env["ZGPU_CHECKSUM_ERROR"] = "zero"
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stderr
     assert r.stdout.split() == ["0", "0"]
+    assert "crc32 of 3 bytes failed" in r.stderr and "adler32 of 3 bytes failed" in r.stderr
 
 
 def test_deflateinit2_params_and_bound_vs_reference_golden(lib):

@@ -40,3 +40,36 @@ def test_stream_sessions_vs_reference(zg, stream_golden):
             k = next((i for i, (a, b) in enumerate(zip(recs, c["recs"])) if a != b), min(len(recs), len(c["recs"])))
             bad.append((tag, k, recs[k:k + 2], c["recs"][k:k + 2], len(recs), len(c["recs"])))
     assert not bad, bad[:4]
+
+
+_REPLAY = r"""
+import hashlib, json, os, sys
+sys.path.insert(0, sys.argv[1])
+import datagen, zgpu
+from zhelpers import run_dsession
+L = zgpu.load()
+bad = []
+for c in json.load(open(os.path.join(sys.argv[1], "golden", "stream_golden.json")))["cases"]:
+    data = datagen.make(c["kind"], c["n"], c["seed"])
+    recs, whole = run_dsession(L, data, [tuple(p) for p in c["plan"]], c["level"], c["wbits"], c["mem"],
+                               c["strategy"])
+    if [list(r) for r in recs] != c["recs"] or hashlib.sha256(whole).hexdigest() != c["sha256"]:
+        bad.append((c["kind"], c["n"], c["level"], c["strategy"], c["wbits"], c["mem"]))
+print("BAD", json.dumps(bad))
+"""
+
+
+def test_stream_sessions_on_segmented_parse(zg):
+    """The same sessions with every streaming job whose events are Z_NO_FLUSH
+    stops parsed by k_pbig1..5 + k_pbig6s (ZGPU_SEG_STREAM_MIN=0; by default
+    only jobs of >= 1 MiB are), in a child process since the library reads
+    the setting once."""
+    import subprocess
+    import sys
+    env = dict(os.environ, ZGPU_SEG_STREAM_MIN="0",
+               PYTHONPATH=os.pathsep.join([os.path.join(os.path.dirname(HERE), "zlib.wasm_amd"),
+                                           os.environ.get("PYTHONPATH", "")]))
+    r = subprocess.run([sys.executable, "-c", _REPLAY, HERE], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("BAD ")][-1]
+    assert json.loads(line[4:]) == [], line

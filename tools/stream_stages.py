@@ -6,6 +6,7 @@ import faulthandler
 import os
 import sys
 import time
+import zlib
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "zlib.wasm_amd"))
@@ -31,8 +32,10 @@ def main():
         tm = zgpu.stage_timing_read()
         zgpu.stage_timing(False)
         st = ", ".join(f"{name} {m:.0f} ms ({k})" for name, (m, k) in tm.items() if k)
-        print(f"L{level} {mib} MiB streaming job: {dt * 1e3:.0f} ms wall ({mib * 1.048576 / dt:.0f} MB/s); {st}",
-              flush=True)
+        c = zlib.compressobj(level)                 # the same two calls on the system zlib
+        ok = whole == c.compress(data) + c.flush()
+        print(f"L{level} {mib} MiB streaming job: {dt * 1e3:.0f} ms wall ({mib * 1.048576 / dt:.0f} MB/s); {st};"
+              f" {'identical to' if ok else 'DIFFERS from'} the system zlib", flush=True)
 
 
 if __name__ == "__main__":

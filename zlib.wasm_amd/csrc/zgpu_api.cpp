@@ -244,13 +244,15 @@ struct Ctx {
     DevBuf ws_help;           // the a18 helpers' staging (zlib_*_simd)
     DevBuf ws_seg;            // k_match segments of sub-batches of few large buffers
     // few large buffers: k_pbig* lane groups and records, k_enc_* block plans
-    DevBuf ws_pg, ws_plane, ws_pbuf, ws_eplan, ws_wind;
+    DevBuf ws_pg, ws_plane, ws_pbuf, ws_eplan, ws_wind, ws_tl;
     DevBuf ws_ck;             // split checksum partials (few large buffers)
     DevBuf ws_srec, ws_snap;  // a streaming job's block records and head[] snapshot
     // inflate: match records, per-stream results, checks, offsets, stop codes
     DevBuf ws_mrec, ws_irec, ws_ick, ws_imeta, ws_istop;
     hipStream_t aux = nullptr;
     hipEvent_t ev_links[2] = {nullptr, nullptr}, ev_match[2] = {nullptr, nullptr};
+    // pinned host staging of single small crc32()/adler32() calls (checksum_small)
+    uint8_t *pin = nullptr;
 };
 
 // One entry per HIP device: its static tables and a pool of contexts.  A call
@@ -419,6 +421,7 @@ struct FlushSpec {
     uint32_t lk_n = 0, pre_from = 0;
     int keep_head = 0;
     int zp0 = kMinMatch - 1, zm0 = kMinMatch - 1;   // DeflateJob::zp0 / zm0
+    int seg_parse = 0;             // the job's stops are all Z_NO_FLUSH: k_pbig* may parse it (k_pbig6s)
 };
 
 // deflateInit2_'s windowBits / memLevel rules (deflate.c:400-425): negative
@@ -584,15 +587,16 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     for (size_t sb = 0; sb < nsub; sb++) {
         pg_at[sb] = pg.size() / 2;
         plb_at[sb] = plb.size();
-        if (fs || no_big || seg_at[sb + 1] == seg_at[sb]) continue;
+        if ((fs && !fs->seg_parse) || no_big || seg_at[sb + 1] == seg_at[sb]) continue;
         const uint32_t a = cuts[sb], b = cuts[sb + 1];
-        uint64_t tot = 0, mb = 0;
-        for (uint32_t i = a; i < b; i++) tot += lens[i], mb = std::max<uint64_t>(mb, lens[i] / wp.sym_limit + 2);
+        const uint64_t st0 = fs ? fs->start : 0;            // a streaming job parses from its resume point
+        uint64_t tot = 0;
+        for (uint32_t i = a; i < b; i++) tot += lens[i] - st0;
         uint64_t ps = ((tot + 65535) / 65536 + 15) & ~15ull;
         ps = ps < 1024 ? 1024 : ps > 65536 ? 65536 : ps;
         uint64_t lanes = 0;
         for (uint32_t i = a; i < b; i++) {
-            const uint64_t nl = std::max<uint64_t>(1, (lens[i] + ps - 1) / ps);
+            const uint64_t nl = std::max<uint64_t>(1, (lens[i] - st0 + ps - 1) / ps);
             plb.push_back((uint32_t)lanes);
             for (uint64_t j = 0; j < nl; j += kParseLanesHost) {
                 pg.push_back(i - a);
@@ -605,11 +609,18 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     }
     pg_at[nsub] = pg.size() / 2;
     plb_at[nsub] = plb.size();
+    // k_pbig6s's timeline: a slide per window and two entries per stop at most
+    uint32_t ntl = 0;
+    if (fs && !pg.empty()) {
+        ntl = (uint32_t)(lens[0] / wp.wsize + 2ull * fs->n + 8);
+        if (!c.ws_tl.ensure(16ull * ntl + 4ull * fs->n + 64)) return zfail(__LINE__);
+    }
     // The block-parallel encoder (k_enc_plan / scan / emit, §4.6b) for every
     // batch job at levels 1..9: one workgroup per block instead of one per
-    // buffer (a 4096 x 1 MiB L6 sub-batch: 42 -> ~10 ms).  Streaming jobs
-    // (markers, resumed output bits) and level 0 keep k_encode.
-    bool block_enc = !fs && level >= 1 && !no_big;
+    // buffer (a 4096 x 1 MiB L6 sub-batch: 42 -> ~10 ms), and for streaming
+    // jobs with Z_NO_FLUSH stops only (resumed at a partial byte, records from
+    // k_enc_rec).  Other streaming jobs (markers) and level 0 keep k_encode.
+    bool block_enc = (!fs || fs->seg_parse) && level >= 1 && !no_big;
     for (size_t sb = 0; sb < nsub && block_enc; sb++) {
         uint64_t mb = 0;
         for (uint32_t i = cuts[sb]; i < cuts[sb + 1]; i++) mb = std::max<uint64_t>(mb, lens[i] / wp.sym_limit + 2);
@@ -703,6 +714,10 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.pseg = pseg_of[s];
             job.plane = c.ws_plane.as<PLane>();
             job.pbuf = c.ws_pbuf.as<PBuf>();
+            if (ntl) {
+                job.tl = c.ws_tl.as<uint32_t>();
+                job.ntl = ntl;
+            }
         }
         if (block_enc) {
             job.maxblk = maxblk_of[s];
@@ -758,9 +773,15 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             if (T.run(4, st, [&] { return launch_deflate_stage(7, job, nullptr, st); })) return zfail(__LINE__);
         } else if (rle) {
             if (T.run(4, st, [&] { return launch_deflate_stage(8, job, nullptr, st); })) return zfail(__LINE__);
+        } else if (level >= 4 && fs && job.pgrp) {
+            // a streaming job with Z_NO_FLUSH stops only: the segmented parse,
+            // fill_window's bookkeeping and the stops replayed over its blocks
+            // (k_pbig6s); what it cannot place goes to the sequential parse
+            if (T.run(3, st, [&] { return launch_deflate_stage(13, job, nullptr, st); })) return zfail(__LINE__);
+            if (T.run(3, st, [&] { return launch_deflate_stage(6, job, nullptr, st); })) return zfail(__LINE__);
         } else if (level >= 4 && fs) {
-            // flush jobs: the sequential lazy parse (the segmented one assumes
-            // the input is all there)
+            // flush jobs: the sequential lazy parse (the segmented one does not
+            // model a flush's effect on the parse)
             if (T.run(3, st, [&] { return launch_deflate_stage(2, job, nullptr, st); })) return zfail(__LINE__);
         } else if (level >= 4) {
             const int ps = job.pgrp ? 11 : 5;                  // few large buffers: k_pbig*
@@ -856,7 +877,14 @@ struct FlushHost {
     uint32_t lk_n = 0, pre_from = 0;
     int keep_head = 0;
     int zp0 = kMinMatch - 1, zm0 = kMinMatch - 1;   // DeflateJob::zp0 / zm0
+    int seg_parse = 0;                 // see FlushSpec
 };
+
+// streaming jobs on the segmented parse (FlushHost::seg_parse): at least this
+// much input to parse, and at most this many window slides (k_pbig6s replays
+// them one by one on one lane)
+constexpr uint64_t kSegStreamMin = 1ull << 20;
+constexpr uint64_t kSegStreamSlides = 1ull << 18;
 
 // debug trace of the streaming deflate() engine (ZGPU_STREAM_TRACE)
 #define ZTRACE(...) do { static const bool on_ = std::getenv("ZGPU_STREAM_TRACE") != nullptr; \
@@ -946,6 +974,7 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
         fs.keep_head = fh->keep_head;
         fs.zp0 = fh->zp0;
         fs.zm0 = fh->zm0;
+        fs.seg_parse = fh->seg_parse;
         if (fh->rec_out) {
             const size_t sym_limit = (size_t(1) << (mem_level + 6)) - 1;         // lit_bufsize - 1
             const size_t nrec = src_len[0] / sym_limit + 4 + 2ull * fh->n + fh->nplan;
@@ -1607,18 +1636,55 @@ int compress(Bytef *dest, uLongf *destLen, const Bytef *source, uLong sourceLen)
     return compress2(dest, destLen, source, sourceLen, Z_DEFAULT_COMPRESSION);
 }
 
+// A single call of up to kSmallCk bytes (zlib users checksum chunk by chunk):
+// the bytes are copied into the context's pinned staging buffer, the kernel
+// reads them there over the host link and writes the result back into it --
+// one launch and one synchronisation, no DMA copies or device metadata.
+constexpr size_t kSmallCk = 64 * 1024;
+constexpr size_t kPinBytes = kSmallCk + 64;
+int checksum_small(bool is_crc, uint32_t init, const uint8_t *buf, size_t len, uint32_t *res) {
+    Lease L;
+    if (L.rc) return L.rc;
+    Ctx &c = *L.c;
+    if (!c.pin && hipHostMalloc(reinterpret_cast<void **>(&c.pin), kPinBytes, hipHostMallocDefault) != hipSuccess) {
+        c.pin = nullptr;
+        return ZGPU_MEM_ERROR;
+    }
+    uint64_t *meta = reinterpret_cast<uint64_t *>(c.pin);   // offset, length, init | result
+    uint32_t *w = reinterpret_cast<uint32_t *>(meta + 2);
+    meta[0] = 0;
+    meta[1] = len;
+    w[0] = init;
+    w[1] = 0;
+    if (len) std::memcpy(c.pin + 64, buf, len);
+    // splitting one buffer over many waves pays from ~16 KiB on
+    const size_t ckb = len > 16384 ? checksum_scratch_bytes(1) : 0;
+    void *ck = ckb && c.ws_ck.ensure(ckb) ? c.ws_ck.p : nullptr;
+    const int rc = is_crc ? launch_crc32(c.pin + 64, meta, meta + 1, w, w + 1, 1, ck, ckb, c.own)
+                          : launch_adler32(c.pin + 64, meta, meta + 1, w, w + 1, 1, ck, ckb, c.own);
+    if (rc || hipStreamSynchronize(c.own) != hipSuccess) return ZGPU_MEM_ERROR;
+    *res = reinterpret_cast<volatile uint32_t *>(w)[1];
+    return ZGPU_OK;
+}
+
 static uint32_t checksum_one(bool is_crc, uint32_t init, const Bytef *buf, size_t len) {
     const uint8_t *p = buf;
     uint32_t out = 0;
-    int rc = is_crc ? zgpu_crc32_batch(&p, &len, &init, &out, 1) : zgpu_adler32_batch(&p, &len, &init, &out, 1);
+    const int rc = len <= kSmallCk ? checksum_small(is_crc, init, p, len, &out)
+                   : is_crc      ? zgpu_crc32_batch(&p, &len, &init, &out, 1)
+                                 : zgpu_adler32_batch(&p, &len, &init, &out, 1);
     if (rc) {
-        // zlib's crc32()/adler32() have no error return and a library must not
-        // end its host process: report once on stderr and return 0 (the value
-        // of crc32(0, Z_NULL, 0)); there is no CPU fallback.
-        static std::atomic<bool> said{false};
-        if (!said.exchange(true))
-            std::fprintf(stderr, "libzgpu: %s failed on the GPU (rc %d); returning 0\n",
-                         is_crc ? "crc32" : "adler32", rc);
+        // zlib's crc32()/adler32() have no error return and there is no CPU
+        // path: a failed GPU call ends the process with a message (a wrong
+        // check value would be silent).  ZGPU_CHECKSUM_ERROR=zero returns 0
+        // instead (crc32(0, Z_NULL, 0)'s value), reported once on stderr.
+        static const bool zero = [] {
+            const char *e = std::getenv("ZGPU_CHECKSUM_ERROR");
+            return e && std::strcmp(e, "zero") == 0;
+        }();
+        std::fprintf(stderr, "libzgpu: %s of %zu bytes failed on the GPU (rc %d)%s\n", is_crc ? "crc32" : "adler32",
+                     len, rc, zero ? "; returning 0 (ZGPU_CHECKSUM_ERROR=zero)" : "");
+        if (!zero) std::abort();
         return 0;
     }
     return out;
@@ -2026,6 +2092,21 @@ int deflate_part(internal_state *s, bool closed) {
         fh.snap_head = &s->snap_head;
         fh.snap_prev = &s->snap_prev;
     }
+    // With Z_NO_FLUSH stops only (a large deflate() call and its Z_FINISH,
+    // compress2 over 4 GiB) the lazy parse is the whole-input one from the
+    // resume point -- a stop only holds fill_window back -- so the segmented
+    // parse runs it and k_pbig6s places the stops and window offsets
+    static const bool no_seg_stream = std::getenv("ZGPU_NO_SEGSTREAM") != nullptr;   // A/B
+    static const uint64_t seg_min = [] {      // ZGPU_SEG_STREAM_MIN (tests): a smaller minimum
+        const char *e = std::getenv("ZGPU_SEG_STREAM_MIN");
+        return e ? (uint64_t)std::atoll(e) : kSegStreamMin;
+    }();
+    bool stops_only = slow && !no_seg_stream && cpos.empty() && !fh.head_in && fh.lk_n == 0 &&
+                      fh.zp0 == kMinMatch - 1 && fh.zm0 == kMinMatch - 1 && sl - fh.start >= seg_min &&
+                      ((sl - fh.start) >> s->wbits) <= kSegStreamSlides;
+    if (!closed && nev == 0) stops_only = false;
+    for (size_t i = 0; stops_only && i < nev; i++) stops_only = s->ev_type[s->res_ev + i] == 0;
+    fh.seg_parse = stops_only ? 1 : 0;
     ZTRACE("part: base %zu nev %zu sl %zu cap %zu start %u bit0 %u e0 %u cut %d fast %d\n", base, nev, sl, cap,
            fh.start, fh.bit0, fh.e0, fh.cut, (int)fast);
     {

@@ -1722,13 +1722,14 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
 // ------------------------------------------------------------------------
 struct PCtx {
     uint32_t bi, lane, nl, n, seg, gl;
+    uint32_t st;             // where lane 0 starts: 0, or a streaming job's resume point (job.start)
     bool active;
     const uint8_t *in;
     const uint32_t *rf, *rq;
     uint32_t *sym, *stg, *sst;
     BlockRec *blk;
     __device__ inline uint32_t xb(uint32_t i) const {
-        const uint64_t v = (uint64_t)i * seg;
+        const uint64_t v = (uint64_t)st + (uint64_t)i * seg;
         return v < n ? (uint32_t)v : n;
     }
     __device__ inline uint32_t seg_end() const { return lane + 1 >= nl ? n : xb(lane + 1); }
@@ -1744,7 +1745,8 @@ __device__ inline PCtx pbig_ctx(const DeflateJob &job) {
     const uint32_t g = job.first + c.bi;
     c.n = (uint32_t)job.src_len[g];
     c.seg = job.pseg;
-    c.nl = pbig_lanes(c.n, c.seg);
+    c.st = job.start;
+    c.nl = pbig_lanes(c.n - c.st, c.seg);
     c.active = c.lane < c.nl;
     c.gl = job.plbase[c.bi] + c.lane;
     c.in = job.src + job.src_off[g];
@@ -1870,7 +1872,7 @@ __global__ __launch_bounds__(kPScanThreads) void k_pbig4(DeflateJob job) {
     const int tid = threadIdx.x, wl = tid & 63, wv = tid >> 6;
     const uint32_t bi = blockIdx.x;
     const uint32_t n = (uint32_t)job.src_len[job.first + bi];
-    const uint32_t nl = pbig_lanes(n, job.pseg);
+    const uint32_t nl = pbig_lanes(n - job.start, job.pseg);
     PLane *pl = job.plane + job.plbase[bi];
     if (job.pbuf[bi].fail) {
         if (tid == 0) job.nblocks[bi] = kParseFallback;
@@ -1909,7 +1911,8 @@ __global__ __launch_bounds__(kParseLanes) void k_pbig5(DeflateJob job) {
     const uint32_t symlim = job_win(job).sym_limit;
     const uint32_t total = pb.total;
     const uint32_t ncut = total / symlim - ((pb.fin && total % symlim == 0) ? 1u : 0u);
-    uint32_t cnt = 0, base = 0, c1 = 0, x0 = 0, kstart = 0, pos0 = 0;
+    uint32_t cnt = 0, base = 0, c1 = 0, x0 = 0, kstart = 0, pos0 = c.st;
+    const bool filtered = job.strategy == 1;
     if (c.active) {
         const PLane &r = job.plane[c.gl];
         cnt = r.cnt;
@@ -1949,6 +1952,20 @@ __global__ __launch_bounds__(kParseLanes) void k_pbig5(DeflateJob job) {
                     const uint32_t b = (gi + 1) / symlim - 1;
                     c.blk[b].in_end = (uint64_t)(sp + len);
                     c.blk[b].pad = sp + 1;                // decision point of the flush
+                    // a streaming job's resume flag (k_pbig6s): a block cut by a
+                    // literal leaves the simple state only when the search at the
+                    // literal found nothing usable (k_parse_slow's flush res).
+                    // rfull is the longest of the searches the parse may read
+                    // there (rquart walks a prefix of the same chain).
+                    if (job.srec) {
+                        bool usable = false;
+                        if (v < 256u) {
+                            const uint32_t r = c.rf[sp], rl = r >> 16;
+                            usable = rl >= (uint32_t)kMinMatch &&
+                                     !(rl <= 5u && (filtered || (rl == (uint32_t)kMinMatch && (r & 0xffffu) > (uint32_t)kTooFar)));
+                        }
+                        c.blk[b].flags = usable ? 1u : 0u;
+                    }
                 }
             }
         }
@@ -1995,6 +2012,140 @@ __global__ __launch_bounds__(256) void k_pbig6(DeflateJob job) {
     r.flags = (last ? 1u : 0u) | (in_start >= (uint64_t)wp.wsize * slides ? 2u : 0u);
     r.pad = 0;
     blk[b] = r;
+}
+
+// ------------------------------------------------------------------------
+// k_pbig6s — the block records of a streaming job parsed by k_pbig1..5, one
+// workgroup.  The job's events are Z_NO_FLUSH stops only, so its symbols and
+// block cuts are those of a parse of the whole input from job.start; what
+// the stops change is fill_window's bookkeeping (the window offset S and the
+// input read E recorded per block, k_parse_slow's ParseU::fill), which
+// blocks come before each stop (ev_blk) and, for an open job, where it ends.
+// That bookkeeping changes only at decision points p with E - p < 262
+// (deflate.c:1941-1944 / :251-368): a slide once p - S >= w_size + MAX_DIST,
+// a read up to min(S + 2 w_size, the call's input end), a stop when that end
+// is reached.  Lane 0 replays the changes in order as thresholds "at the first
+// decision point >= x" (a timeline: from x on the state is (S, E)); each block
+// then looks its flush decision point up.  Where a slide and a threshold
+// closer than 257 bytes (any 257 consecutive positions hold a decision point:
+// a match skips at most 256) meet with no decision point known between them,
+// the order is undetermined here and the job goes to k_parse_slow.
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pbig6s(DeflateJob job) {
+    __shared__ uint32_t s_ntl, s_bad, s_nb;
+    const int tid = threadIdx.x;
+    const PBuf pb = job.pbuf[0];
+    if (pb.fail) return;                              // k_pbig4 flagged it already
+    const WinP wp = job_win(job);
+    const uint32_t symlim = wp.sym_limit, W = (uint32_t)wp.wsize, MD = (uint32_t)wp.max_dist;
+    const uint32_t n = (uint32_t)job.src_len[job.first];
+    const uint32_t total = pb.total;
+    const uint32_t ncut = total / symlim - ((pb.fin && total % symlim == 0) ? 1u : 0u);
+    const uint32_t st = job.start, nev = job.nfl;
+    BlockRec *blk = job.blocks + job.blk_off[0];
+    uint4 *tl = reinterpret_cast<uint4 *>(job.tl);
+    uint32_t *ez = job.tl + 4ull * job.ntl;           // per stop: the point it triggers at
+    // a decision point known in [a, b): the start or a block's flush point
+    auto has_dp = [&](uint32_t a, uint32_t b) -> bool {
+        if (st >= a && st < b) return true;
+        uint32_t lo = 0, hi = ncut;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (blk[mid].pad < a) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo < ncut && blk[lo].pad < b;
+    };
+    if (tid == 0) {
+        uint32_t S = 0, E = job.e0 > st ? job.e0 : st, i = 0;
+        uint32_t lim = nev ? (uint32_t)job.fl_pos[0] : n;
+        uint32_t k = 0, bad = 0;
+        tl[k++] = make_uint4(0u, S, E, 0u);
+        for (;;) {
+            if (k + 2 > job.ntl) { bad = 1; break; }
+            const uint32_t Z = E > (uint32_t)kMinLookahead - 1 ? E - ((uint32_t)kMinLookahead - 1) : 0u;
+            const uint32_t Ts = S + W + MD;
+            if (E == lim && i == nev) {               // all input read (closed): slides to the end
+                const uint32_t x = Z > Ts ? Z : Ts;
+                if (x > n) break;
+                S += W;
+                tl[k++] = make_uint4(x, S, E, 0u);
+                continue;
+            }
+            // a read (E < lim) or a stop (E == lim) at the first decision point
+            // p >= Z, where the slide test runs first: p >= Ts?
+            bool slide;
+            if (Z >= Ts) slide = true;
+            else if (Ts - Z >= 257u || has_dp(Z, Ts)) slide = false;
+            else { bad = 1; break; }
+            if (slide) S += W;
+            if (E < lim) {
+                const uint32_t e = S + 2 * W;
+                E = e < lim ? e : lim;
+                tl[k++] = make_uint4(Z, S, E, 0u);
+                continue;
+            }
+            ez[i++] = Z;                              // the stop: need_more, then the next call's read
+            if (i == nev && job.open_end) {
+                tl[k++] = make_uint4(Z, S, E, 0u);
+                break;
+            }
+            lim = i < nev ? (uint32_t)job.fl_pos[i] : n;
+            const uint32_t e = S + 2 * W;
+            E = e < lim ? e : lim;
+            tl[k++] = make_uint4(Z, S, E, 0u);
+        }
+        s_ntl = k;
+        s_bad = bad;
+    }
+    __syncthreads();
+    if (s_bad) {
+        if (tid == 0) job.nblocks[0] = kParseFallback;
+        return;
+    }
+    const uint32_t ntl = s_ntl;
+    // blocks before each stop: those flushed at a decision point below its trigger
+    for (uint32_t i = tid; i < nev; i += 256) {
+        uint32_t lo = 0, hi = ncut;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (blk[mid].pad < ez[i]) lo = mid + 1;
+            else hi = mid;
+        }
+        if (job.ev_blk) job.ev_blk[i] = lo;
+        if (i + 1 == nev && job.open_end) s_nb = lo;
+    }
+    if (tid == 0 && !(nev && job.open_end)) s_nb = ncut + 1;
+    __syncthreads();
+    const uint32_t nb = s_nb;
+    for (uint32_t b = tid; b < nb; b += 256) {
+        const bool last = !job.open_end && b == ncut;
+        const uint32_t in_end = last ? n : (uint32_t)blk[b].in_end;
+        const uint32_t pd = last ? n : blk[b].pad;
+        const bool res = last || blk[b].flags == 0u;
+        const uint32_t in_start = b == 0 ? st : (uint32_t)blk[b - 1].in_end;
+        uint32_t lo = 0, hi = ntl - 1;                // the last timeline entry at or before pd
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (tl[mid].x <= pd) lo = mid;
+            else hi = mid - 1;
+        }
+        const uint4 t = tl[lo];
+        job.srec[4ull * b + 2] = ((uint64_t)t.y << 32) | in_end;
+        job.srec[4ull * b + 3] = (uint64_t)t.z | (res ? 1ull << 63 : 0ull);
+        BlockRec r;
+        r.sym_start = b * symlim;
+        r.nsym = last ? total - b * symlim : symlim;
+        r.in_start = in_start;
+        r.in_end = in_end;
+        r.flags = (last ? 1u : 0u) | (in_start >= t.y ? 2u : 0u);
+        r.pad = 0;
+        blk[b] = r;
+    }
+    if (tid == 0) {
+        job.nblocks[0] = nb;
+        if (job.flush_out) job.flush_out[4] = (uint64_t)(kMinMatch - 1) | (uint64_t)(kMinMatch - 1) << 16;
+    }
 }
 
 // ------------------------------------------------------------------------
@@ -3029,14 +3180,27 @@ __device__ __attribute__((always_inline)) inline void block_plan(const DeflateJo
     for (int i = lane; i < kLCodes; i += 64) hl[i] = 0;
     if (lane < kDCodes) hd[lane] = 0;
     __builtin_amdgcn_wave_barrier();
-    for (uint32_t i = lane; i < br.nsym; i += 64) {
-        const uint32_t v = sym[br.sym_start + i];
-        const uint32_t dist = v >> 8, lc = v & 0xffu;
-        if (dist == 0) atomicAdd(&hl[lc], 1u);
-        else {
-            atomicAdd(&hl[c_ct.len_code[lc] + 257], 1u);
-            const uint32_t d = dist - 1;
-            atomicAdd(&hd[d < 256 ? c_ct.dist_code[d] : c_ct.dist_code[256 + (d >> 7)]], 1u);
+    // eight symbols per lane in flight: the wave's loads go out together
+    // instead of one dependent round trip per 64 symbols (a lone block's
+    // histogram is one wave's latency chain)
+    constexpr uint32_t kHU = 8;
+    for (uint32_t i0 = 0; i0 < br.nsym; i0 += 64 * kHU) {
+        uint32_t v[kHU];
+#pragma unroll
+        for (uint32_t u = 0; u < kHU; u++) {
+            const uint32_t i = i0 + 64 * u + (uint32_t)lane;
+            v[u] = i < br.nsym ? sym[br.sym_start + i] : 0xffffffffu;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kHU; u++) {
+            if (v[u] == 0xffffffffu) continue;
+            const uint32_t dist = v[u] >> 8, lc = v[u] & 0xffu;
+            if (dist == 0) atomicAdd(&hl[lc], 1u);
+            else {
+                atomicAdd(&hl[c_ct.len_code[lc] + 257], 1u);
+                const uint32_t d = dist - 1;
+                atomicAdd(&hd[d < 256 ? c_ct.dist_code[d] : c_ct.dist_code[256 + (d >> 7)]], 1u);
+            }
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -3276,13 +3440,16 @@ __global__ __launch_bounds__(kEncThreads) void k_encode(DeflateJob job) {
             } else {
                 const uint16_t *lcode = type == 1 ? c_ct.stat_lcode : T.lcode;
                 const uint8_t *llen = type == 1 ? c_ct.stat_llen : T.llen;
+                uint32_t nxt = (uint32_t)tid < br.nsym ? sym[br.sym_start + tid] : 0u;   // loaded a batch ahead
                 for (uint32_t base = 0; base < br.nsym + 1; base += kEncThreads) {
                     // +1: the END_BLOCK code rides in the last batch
                     const uint32_t i = base + tid;
+                    const uint32_t cur = nxt;
+                    if (i + kEncThreads < br.nsym) nxt = sym[br.sym_start + i + kEncThreads];
                     uint64_t v = 0;
                     int nb = 0;
                     if (i < br.nsym) {
-                        const uint32_t s = sym[br.sym_start + i];
+                        const uint32_t s = cur;
                         const uint32_t dist = s >> 8, lc = s & 0xffu;
                         if (dist == 0) {
                             v = lcode[lc]; nb = llen[lc];
@@ -3482,11 +3649,20 @@ __global__ __launch_bounds__(kEScanThreads) void k_enc_scan(DeflateJob job) {
     const int64_t cap = (int64_t)job.dst_cap[g];
     const uint32_t a3 = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 3u);
     const uint64_t tb = wrap_tail_bits(job.wrap);
+    if (job.srec && nblk == 0) {                           // a streaming job that stops before its first block
+        if (tid == 0) {
+            if (cap > 0) out[0] = (uint8_t)job.byte0;      // the partial byte it resumed at, as k_encode leaves it
+            job.dst_len[g] = 0;
+            job.status[g] = 0;
+            if (job.flush_out) { job.flush_out[1] = job.bit0; job.flush_out[3] = job.byte0; }
+        }
+        return;
+    }
     if (!enc_blocks_ok(job, bi, nblk)) {                   // never expected: report, write nothing
         if (tid == 0) { job.dst_len[g] = 0; job.status[g] = -2; }
         return;
     }
-    if (tid == 0) s_off = wrap_head_bits(job.wrap);
+    if (tid == 0) s_off = wrap_head_bits(job.wrap) + job.bit0;   // a resumed streaming job: after the partial byte
     __syncthreads();
     for (uint32_t c0 = 0; c0 < nblk; c0 += kEScanThreads) {
         const uint32_t m = nblk - c0 < (uint32_t)kEScanThreads ? nblk - c0 : (uint32_t)kEScanThreads;
@@ -3503,9 +3679,14 @@ __global__ __launch_bounds__(kEScanThreads) void k_enc_scan(DeflateJob job) {
             for (uint32_t i = 0; i < m; i++) {
                 const uint64_t st = off, v = s_v[i];
                 const uint32_t ty = s_ty[i];
+                // bi_used at the block's last bi_windup (deflateUsed): after a
+                // stored block's header, at the end of the last block
+                uint32_t wu = (ty & 3u) == 0 ? (uint32_t)((off + 3 - 1) & 7) + 1 : 0u;
                 off = (ty & 3u) == 0 ? ((off + 3 + 7) & ~7ull) + 32 + 8 * v : off + v;
-                if ((ty & 4u) && job.wind) job.wind[bi] = (uint8_t)(((off - 1) & 7) + 1);   // deflateUsed
+                if (ty & 4u) wu = (uint32_t)((off - 1) & 7) + 1;
+                if ((ty & 4u) && job.wind) job.wind[bi] = (uint8_t)wu;
                 if (ty & 4u) off = (off + 7) & ~7ull;      // bi_windup
+                if (job.srec) pl[c0 + i].pad0 = (uint8_t)wu;   // k_enc_rec
                 s_v[i] = st;
             }
             s_off = off;
@@ -3616,6 +3797,7 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
         }
     };
     if (tid == 0) {
+        if (k == 0 && job.bit0) put(job.byte0, (int)job.bit0);   // a resumed streaming job's partial byte
         if (k == 0 && job.wrap == 1) {                     // zlib header (deflate.c:1004-1037)
             uint32_t header = (8u + ((uint32_t)(job.wbits - 8) << 4)) << 8;
             const int level = job.level;
@@ -3669,12 +3851,16 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
     } else {
         const uint16_t *lcode = type == 1 ? c_ct.stat_lcode : s_lcode;
         const uint8_t *llen = type == 1 ? c_ct.stat_llen : s_llen;
+        // the next batch's symbols are loaded while this one is scanned and placed
+        uint32_t nxt = (uint32_t)tid < br.nsym ? sym[br.sym_start + tid] : 0u;
         for (uint32_t base = 0; base < br.nsym + 1; base += kEncThreads) {   // +1: END_BLOCK
             const uint32_t i = base + tid;
+            const uint32_t cur = nxt;
+            if (i + kEncThreads < br.nsym) nxt = sym[br.sym_start + i + kEncThreads];
             uint64_t v = 0;
             int nb = 0;
             if (i < br.nsym) {
-                const uint32_t sy = sym[br.sym_start + i];
+                const uint32_t sy = cur;
                 const uint32_t dist = sy >> 8, lc = sy & 0xffu;
                 if (dist == 0) {
                     v = lcode[lc]; nb = llen[lc];
@@ -3734,6 +3920,28 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
     // neighbouring blocks, so it is reported as an error, never as bytes
     if (tid == 0 && s_obit != re + sh) job.status[g] = -2;
     eflush(s_obit, true);
+}
+
+// a streaming job's records from the block encoder (k_encode's stream_rec):
+// srec[4k] the output bit after block k, srec[4k + 1] the partial byte there
+// and bi_used << 8; flush_out[1] / [3] the end bit and its partial byte.  One
+// thread per block, after k_enc_emit has written every byte.
+__global__ __launch_bounds__(256) void k_enc_rec(DeflateJob job) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t nblk = job.nblocks[0];
+    if (k >= nblk || !enc_blocks_ok(job, 0, nblk)) return;
+    const uint32_t g = job.first;
+    const EncPlan *pl = job.eplan + job.blk_off[0];
+    const uint8_t *out = job.dst + job.dst_off[g];
+    const uint64_t cap = job.dst_cap[g];
+    const uint64_t e = pl[k + 1].start;
+    const uint32_t part = (e & 7) && (e >> 3) < cap ? out[e >> 3] & ((1u << (e & 7)) - 1u) : 0u;
+    job.srec[4ull * k] = e;
+    job.srec[4ull * k + 1] = part | (uint64_t)pl[k].pad0 << 8;
+    if (k + 1 == nblk && job.flush_out) {
+        job.flush_out[1] = e;
+        job.flush_out[3] = part;
+    }
 }
 
 // ------------------------------------------------------------------------
@@ -3802,6 +4010,16 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         hipLaunchKernelGGL(k_pbig6, bg, dim3(256), 0, st, job);
         break;
     }
+    case 13: {                                              // a streaming job: k_pbig1..5, k_pbig6s
+        const dim3 pg(job.npgrp);
+        hipLaunchKernelGGL(k_pbig1, pg, dim3(kParseLanes), 0, st, job);
+        hipLaunchKernelGGL(k_pbig2, pg, dim3(kParseLanes), 0, st, job);
+        hipLaunchKernelGGL(k_pbig3, pg, dim3(kParseLanes), 0, st, job);
+        hipLaunchKernelGGL(k_pbig4, grid, dim3(kPScanThreads), 0, st, job);
+        hipLaunchKernelGGL(k_pbig5, pg, dim3(kParseLanes), 0, st, job);
+        hipLaunchKernelGGL(k_pbig6s, dim3(1), dim3(256), 0, st, job);
+        break;
+    }
     case 12: {
         // trees on the whole wave while few blocks are in flight (latency), on
         // one lane when many are (the other waves hide it), as for k_encode
@@ -3812,6 +4030,7 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
             hipLaunchKernelGGL(k_enc_plan1, dim3(job.maxblk, job.count), dim3(64), 0, st, job);
         hipLaunchKernelGGL(k_enc_scan, grid, dim3(kEScanThreads), 0, st, job);
         hipLaunchKernelGGL(k_enc_emit, eg, dim3(kEncThreads), 0, st, job);
+        if (job.srec) hipLaunchKernelGGL(k_enc_rec, dim3((job.maxblk + 255) / 256), dim3(256), 0, st, job);
         break;
     }
     case 7: hipLaunchKernelGGL(k_parse_huff, grid, dim3(kHuffThreads), 0, st, job); break;

@@ -259,6 +259,11 @@ struct DeflateJob {
     PLane *plane;
     PBuf *pbuf;
     EncPlan *eplan;
+    // a streaming job parsed by k_pbig1..5 (Z_NO_FLUSH stops only, see
+    // k_pbig6s): workspace for fill_window's timeline, ntl entries of 4 words
+    // (first decision point, S, E, -) and then one trigger point per event
+    uint32_t *tl;
+    uint32_t ntl;
 };
 
 // the per-job window/hash parameters (deflate.c:440-455)
