@@ -210,7 +210,7 @@ def back_cases():
             for chunk, first in ((BIG, 0), (4096, 0), (777, 100)):
                 # a w9 window gets a stream made with a w9 window: with distances
                 # beyond the window the reference's inflate_fast loop copies stale
-                # window bytes before it reports the error (DESIGN 8.4), not a
+                # window bytes before it reports the error (DESIGN 4.12), not a
                 # behaviour to pin
                 spec = {"data": [kind, 90000, 91], "level": level, "fmt": "raw"}
                 if wbits < 15:
@@ -253,7 +253,7 @@ def run_backcase(L, case):
         # where out() fails, the reference's bit buffer has pulled input bytes
         # ahead of the failing symbol (infback.c PULLBYTE / inflate_fast's
         # 2-byte loads); the decode here has read the whole input: the unused
-        # count is not pinned (DESIGN 8.4)
+        # count is not pinned (DESIGN 4.12)
         unused = None
     return {"res": json.loads(json.dumps([rc0, rc, unused, null_in, rc2])),
             "out": [len(out), hashlib.sha256(out).hexdigest()]}
