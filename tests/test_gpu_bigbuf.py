@@ -125,14 +125,27 @@ def _over_4gib_input(zg):
 @pytest.mark.parametrize("level", [6, 0])
 def test_compress2_over_4gib_vs_system_zlib(zg, level):
     """compress2 of a buffer over 4 GiB equals system zlib's
-    stream.  Python's zlib.compress feeds deflate() as compress.c does: one
-    2^32 - 1 byte Z_NO_FLUSH piece, then Z_FINISH with the rest.  Level 0's
-    stored blocks follow those pieces."""
+    compress2 (called through ctypes, so compress.c's own calls: one 2^32 - 1
+    byte Z_NO_FLUSH piece, then Z_FINISH with the rest, the output space in
+    pieces of at most 2^32 - 1 bytes).  Level 0's stored blocks follow those
+    pieces; Python's zlib.compress grows its output buffer step by
+    step, which cuts level-0 blocks differently, so it is not the oracle here."""
+    import ctypes
+    import ctypes.util
     import hashlib
     data = _over_4gib_input(zg)
     print(f"\n{len(data)} bytes generated", flush=True)
+    libz = ctypes.CDLL(ctypes.util.find_library("z") or "libz.so.1")
+    libz.compress2.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulong), ctypes.c_char_p, ctypes.c_ulong,
+                               ctypes.c_int]
+    libz.compressBound.restype = ctypes.c_ulong
+    libz.compressBound.argtypes = [ctypes.c_ulong]
     t = time.perf_counter()
-    want = pyzlib.compress(data, level)
+    wbuf = ctypes.create_string_buffer(libz.compressBound(len(data)))
+    wlen = ctypes.c_ulong(len(wbuf))
+    assert libz.compress2(wbuf, ctypes.byref(wlen), data, len(data), level) == 0
+    want = bytes(memoryview(wbuf)[:wlen.value])
+    del wbuf
     print(f"system zlib L{level}: {len(want)} bytes in {time.perf_counter() - t:.1f} s", flush=True)
     t = time.perf_counter()
     rc, z = zg.compress2(data, level)

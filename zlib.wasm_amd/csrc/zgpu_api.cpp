@@ -621,7 +621,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     // jobs with Z_NO_FLUSH stops only (resumed at a partial byte, records from
     // k_enc_rec).  Other streaming jobs (markers) and level 0 keep k_encode.
     bool block_enc = (!fs || fs->seg_parse) && level >= 1 && !no_big;
-    for (size_t sb = 0; sb < nsub && block_enc; sb++) {
+    for (size_t sb = 0; sb < nsub; sb++) {            // (k_pbig6's grid too: set for every path)
         uint64_t mb = 0;
         for (uint32_t i = cuts[sb]; i < cuts[sb + 1]; i++) mb = std::max<uint64_t>(mb, lens[i] / wp.sym_limit + 2);
         maxblk_of[sb] = (uint32_t)mb;
@@ -719,10 +719,8 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
                 job.ntl = ntl;
             }
         }
-        if (block_enc) {
-            job.maxblk = maxblk_of[s];
-            job.eplan = c.ws_eplan.as<EncPlan>();
-        }
+        job.maxblk = maxblk_of[s];
+        if (block_enc) job.eplan = c.ws_eplan.as<EncPlan>();
         if (fs) {
             job.fl_pos = fs->pos;
             job.fl_type = fs->type;
@@ -2381,9 +2379,7 @@ int deflate_stored_call(z_streamp strm, internal_state *s, int flush) {
     uint64_t bpos = 0;                                          // buf position of the next byte to send
     auto read = [&](uint64_t n) {                               // read_buf (deflate.c:218-239)
         if (!n) return;
-        buf.insert(buf.end(), strm->next_in, strm->next_in + n);
-        if (s->wrap == 1) s->check = (uint32_t)adler32_z(s->check, strm->next_in, n);
-        else if (s->wrap == 2) s->check = (uint32_t)crc32_z(s->check, strm->next_in, n);
+        buf.insert(buf.end(), strm->next_in, strm->next_in + n);   // (the check: once per call, below)
         strm->next_in += n;
         strm->avail_in -= (uInt)n;
         strm->total_in += n;
@@ -2512,9 +2508,17 @@ int deflate_stored_call(z_streamp strm, internal_state *s, int flush) {
         s->part_out = jb + cap;
         s->res_bits = ((uint64_t)jb << 3) + fh.out[1];
         s->res_byte = (uint32_t)fh.out[3];
+        // hand the job's bytes out now: the plan fits the caller's space (aout),
+        // and the queue stays one job's size (a zalloc'd buffer is under 4 GiB)
+        drain(strm, s);
         i0 = i1;
     }
     s->in.assign(buf.begin() + (std::ptrdiff_t)bpos, buf.end());   // the window's unsent bytes
+    {   // read_buf's running check over everything this call read (one contiguous run from in0)
+        const uint64_t rd = used0 - strm->avail_in;
+        if (rd && s->wrap == 1) s->check = (uint32_t)adler32_z(s->check, in0, rd);
+        else if (rd && s->wrap == 2) s->check = (uint32_t)crc32_z(s->check, in0, rd);
+    }
     {   // the window: the last strstart bytes read (deflate.c:1733-1790 keep them contiguous)
         const uint64_t rd = used0 - strm->avail_in, keep = (uint64_t)strstart;
         if (rd >= keep) {

@@ -281,7 +281,7 @@ def compress2(data, level=6, cap=None):
     out = C.create_string_buffer(max(cap, 1))
     n = C.c_ulong(cap)
     rc = L.compress2(out, C.byref(n), data, len(data), level)
-    return rc, C.string_at(out, n.value)
+    return rc, bytes(memoryview(out)[:n.value])           # (string_at's size is a C int)
 
 
 def crc32(data, crc=0):
