@@ -159,6 +159,7 @@ void build_crc_tables(CrcTables &t) {
             const uint32_t c = t.s4[k - 1][v];
             t.s4[k][v] = (c >> 8) ^ t.byte[c & 0xffu];
         }
+    for (int i = 0; i < 48; i++) t.xrow[i] = x2nmodp((int64_t)(kCrcRow << i), 3);
     const uint64_t a64[kCrcSh64Tabs] = {64, 128, 256, 512, 1024, 2048, 64 * 15, 64 * 63};
     for (int k = 0; k < kCrcSh64Tabs; k++) {
         const uint32_t op = x2nmodp((int64_t)a64[k], 3);

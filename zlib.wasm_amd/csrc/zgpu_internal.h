@@ -71,7 +71,9 @@ struct CrcTables {
     uint32_t byte[256];
     uint32_t s4[4][256];
     uint32_t sh64[kCrcSh64Tabs][8][16];
+    uint32_t xrow[48];        // x^(8 kCrcRow 2^i) mod P: k_crc32_fin's shifts over whole rows
 };
+constexpr uint64_t kCrcRow = 64 * 64;           // k_crc32_part's row: 64 lanes x 64 bytes
 constexpr uint64_t kCrcSegment = 64 * 1024;   // bytes per checksum work item
 
 // Per-buffer deflate block record written by the parse, read by the encoder.
