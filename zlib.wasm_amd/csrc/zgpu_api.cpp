@@ -721,6 +721,8 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             }
         }
         job.maxblk = maxblk_of[s];
+        static const int fcmp64 = std::getenv("ZGPU_FAST_CMP64") != nullptr;   // A/B: k_parse_fast's compare
+        job.fcmp = fcmp64;
         if (block_enc) job.eplan = c.ws_eplan.as<EncPlan>();
         if (fs) {
             job.fl_pos = fs->pos;

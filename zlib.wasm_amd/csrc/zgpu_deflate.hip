@@ -2594,12 +2594,18 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
                 int k;
                 if (kOne) {
                     // link and candidate bytes in one round trip; cur + lc < n
-                    // since cur < p and maxcmp <= n - p
+                    // since cur < p and maxcmp <= n - p.  Only the first kC0
+                    // candidate bytes are loaded (most compares end there): a
+                    // 16-byte span crosses a cache line far less often than 64
+                    // (DeflateJob::fcmp: 64, the round-3 compare)
+                    const int c0 = job.fcmp ? 64 : 16;
                     const uint32_t dv = prev[vg((uint32_t)cur)];
-                    const uint32_t cbyte = in[(uint32_t)(cur + lc)];
+                    uint32_t cbyte = 0;
+                    if (lane < c0) cbyte = in[(uint32_t)(cur + lc)];
                     __builtin_amdgcn_sched_barrier(0);       // both loads issued before either is used
-                    const uint64_t m = __ballot(lane < maxcmp && cbyte != sb);
-                    k = m ? (int)__builtin_ctzll(m) : common_from(cur, p, maxcmp, 64);
+                    const int mc = maxcmp < c0 ? maxcmp : c0;
+                    const uint64_t m = __ballot(lane < mc && cbyte != sb);
+                    k = m ? (int)__builtin_ctzll(m) : (maxcmp <= c0 ? maxcmp : common_from(cur, p, maxcmp, c0));
                     d = ufl(dv);
                 } else {
                     d = ufl(prev[cur]);

@@ -43,6 +43,7 @@ struct InfLDS {
     uint16_t lt[1 << kLRoot], dt[1 << kDRoot], ct[1 << kCRoot];
     Canon lcan, dcan;
     uint16_t lens[320];
+    uint32_t cu[48];                  // codes_used's count / next code / codes left per length
 };
 
 __device__ __constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
@@ -214,56 +215,60 @@ __device__ __attribute__((always_inline)) inline void seek(Rd &r, uint32_t byte)
 // bits, a sub-table of 1 << curr entries, curr grown while the codes still to
 // place overfill it (inftrees.c:214-300).  2 for a code with no lengths.
 // Uniform across the wave; run only for streams that ask (InflateJob::zcodes).
-__device__ uint32_t codes_used(const uint16_t *lens, int n, int root, int lane) {
-    uint32_t cnt[16];
-#pragma unroll
-    for (int L = 0; L < 16; L++) cnt[L] = 0;
-    for (int c0 = 0; c0 < n; c0 += 64) {
-        const int i = c0 + lane;
-        const uint32_t l = i < n ? lens[i] : 0u;
-#pragma unroll
-        for (int L = 1; L < 16; L++) cnt[L] += (uint32_t)__popcll(__ballot(i < n && l == (uint32_t)L));
-    }
-    int max = 15;
-    while (max >= 1 && cnt[max] == 0) max--;
-    if (max == 0) return 2;
-    int min = 1;
-    while (min < max && cnt[min] == 0) min++;
-    if (root > max) root = max;
-    if (root < min) root = min;
-    uint32_t used = 1u << root, code = 0, next[16], rem[16];
-    next[0] = 0;
-    rem[0] = 0;
-    for (int L = 1; L < 16; L++) {
-        code = (code + (L > 1 ? cnt[L - 1] : 0u)) << 1;
-        next[L] = code;
-        rem[L] = cnt[L];
-    }
-    uint32_t low = 0xffffffffu;
-    for (int L = root + 1; L <= max; L++) {
-        for (int c0 = 0; c0 < n; c0 += 64) {
-            const int i = c0 + lane;
-            uint64_t m = __ballot(i < n && lens[i] == (uint16_t)L);
-            while (m) {
-                m &= m - 1;
-                const uint32_t key = next[L] >> (L - root);
-                if (key != low) {
-                    int curr = L - root, left = 1 << curr;
-                    while (curr + root < max) {
-                        left -= (int)rem[curr + root];
-                        if (left <= 0) break;
-                        curr++;
-                        left <<= 1;
+// Lane 0 walks the lengths with its per-length tables in LDS (cu): dynamically
+// indexed register arrays would put k_inflate_decode's frame in scratch and
+// raise its register count for a call that only inflateCodesUsed needs.
+__device__ __attribute__((noinline)) uint32_t codes_used(const uint16_t *lens, int n, int root, uint32_t *cu,
+                                                         int lane) {
+    __syncthreads();
+    uint32_t used = 0;
+    if (lane == 0) {
+        uint32_t *cnt = cu, *next = cu + 16, *rem = cu + 32;
+        for (int L = 0; L < 16; L++) cnt[L] = 0;
+        for (int i = 0; i < n; i++) cnt[lens[i] & 15u]++;
+        cnt[0] = 0;
+        int max = 15;
+        while (max >= 1 && cnt[max] == 0) max--;
+        if (max == 0) {
+            used = 2;
+        } else {
+            int min = 1;
+            while (min < max && cnt[min] == 0) min++;
+            if (root > max) root = max;
+            if (root < min) root = min;
+            used = 1u << root;
+            uint32_t code = 0;
+            next[0] = rem[0] = 0;
+            for (int L = 1; L < 16; L++) {
+                code = (code + (L > 1 ? cnt[L - 1] : 0u)) << 1;
+                next[L] = code;
+                rem[L] = cnt[L];
+            }
+            uint32_t low = 0xffffffffu;
+            for (int L = root + 1; L <= max; L++) {
+                for (int i = 0; i < n; i++) {
+                    if (lens[i] != (uint16_t)L) continue;
+                    const uint32_t key = next[L] >> (L - root);
+                    if (key != low) {
+                        int curr = L - root, left = 1 << curr;
+                        while (curr + root < max) {
+                            left -= (int)rem[curr + root];
+                            if (left <= 0) break;
+                            curr++;
+                            left <<= 1;
+                        }
+                        used += 1u << curr;
+                        low = key;
                     }
-                    used += 1u << curr;
-                    low = key;
+                    next[L]++;
+                    rem[L]--;
                 }
-                next[L]++;
-                rem[L]--;
             }
         }
+        cu[47] = used;
     }
-    return used;
+    __syncthreads();
+    return cu[47];
 }
 
 __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
@@ -450,7 +455,7 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
                     stop = kIData; used = ceil_used(); goto done;
                 }
                 // mode CODELENS: state->next holds the code-length code's table (inflateCodesUsed)
-                const uint32_t zcl = job.zcodes ? codes_used(S.lens, 19, 7, lane) : 0u;
+                const uint32_t zcl = job.zcodes ? codes_used(S.lens, 19, 7, S.cu, lane) : 0u;
                 uint32_t have = 0;
                 const uint32_t total = nlen + ndist;
                 while (have < total) {
@@ -499,7 +504,7 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
                     stop = kIData; used = ceil_used(); goto done;
                 }
                 if (job.zcodes)
-                    zcodes = codes_used(S.lens, (int)nlen, 9, lane) + codes_used(S.lens + nlen, (int)ndist, 6, lane);
+                    zcodes = codes_used(S.lens, (int)nlen, 9, S.cu, lane) + codes_used(S.lens + nlen, (int)ndist, 6, S.cu, lane);
             }
             // ---------------- LEN .. MATCH / LIT ----------------
             for (;;) {

@@ -266,6 +266,7 @@ struct DeflateJob {
     // (first decision point, S, E, -) and then one trigger point per event
     uint32_t *tl;
     uint32_t ntl;
+    int fcmp;                // k_parse_fast: load 64 candidate bytes per chain step (A/B; 0: 16 first)
 };
 
 // the per-job window/hash parameters (deflate.c:440-455)
