@@ -33,11 +33,14 @@
  * deflateSetDictionary, deflateSetHeader, deflatePrime, deflateTune and
  * deflateParams give the reference's stream: deflateParams flushes with Z_BLOCK
  * itself when the level's function or the strategy changes (as deflate.c does)
- * and switches between level 0, deflate_fast and deflate_slow levels; a level
+ * and switches between level 0, deflate_fast and deflate_slow levels, and
+ * between deflate_slow and Z_HUFFMAN_ONLY / Z_RLE (gzsetparams' pattern); a level
  * change within one function, and deflateTune, take effect at the next decision
  * even with input pending.  What the model cannot place returns Z_STREAM_ERROR
  * with strm->msg set, never a different stream (zgpu_api.cpp, `unsupported`):
- *   - deflateParams to or from Z_HUFFMAN_ONLY / Z_RLE after data (levels 1..9);
+ *   - deflateParams to or from Z_HUFFMAN_ONLY / Z_RLE after data other than
+ *     between deflate_slow levels (4..9, memLevel <= 8) and those strategies,
+ *     and back to deflate_slow after a first call of a single byte;
  *   - deflatePrime with input pending after a call that did not reach its end,
  *     or after Z_STREAM_END;
  *   - deflateSetDictionary after the stream has ended;

@@ -197,6 +197,33 @@ def deflate_sessions():
                                                             ["deflate", sl(m, 0, 0), Z_FINISH], ["getdict"]]})
         S.append({"name": f"getdict-setdict-L0-w{wb}", "ops": [["init", 0, wb, 8, 0], ["dict", sl(t, 0, 500)], ["getdict"],
                                                                ["deflate", sl(m, 0, 20000), Z_SYNC_FLUSH], ["getdict"]]})
+    # deflateParams between deflate_slow and Z_HUFFMAN_ONLY / Z_RLE after data
+    # (deflate.c:760-803; the gzsetparams pattern, gzwrite.c:587)
+    for strat in (2, 3):
+        for level, wb in ((6, 15), (9, -15), (5, 31), (6, -9)):
+            S.append({"name": f"params-hr{strat}-L{level}-w{wb}", "ops": [
+                ["init", level, wb, 8, 0], ["deflate", sl(m, 0, 30000), Z_NO_FLUSH], ["params", level, strat],
+                ["deflate", sl(m, 30000, 50000), Z_NO_FLUSH], ["params", level, 0],
+                ["deflate", sl(m, 50000, 100000), Z_FINISH], ["used"]]})
+    S.append({"name": "params-hr-toggles-L9", "ops": [
+        ["init", 9, -15, 8, 0], ["deflate", sl(t, 0, 20000), Z_SYNC_FLUSH], ["params", 9, 3],
+        ["deflate", sl(t, 20000, 26000), Z_NO_FLUSH], ["params", 9, 0], ["deflate", sl(t, 26000, 60000), Z_NO_FLUSH],
+        ["params", 9, 2], ["deflate", sl(t, 60000, 61000), Z_NO_FLUSH], ["params", 9, 0],
+        ["deflate", sl(t, 61000, 100000), Z_FINISH]]})
+    S.append({"name": "params-hr-gzsetparams", "ops": [
+        ["init", 6, 31, 8, 0], ["deflate", sl(m, 0, 40000), Z_NO_FLUSH], ["params", 6, 2],
+        ["deflate", sl(m, 40000, 41000), Z_NO_FLUSH], ["params", 5, 0], ["deflate", sl(m, 41000, 100000), Z_FINISH]]})
+    S.append({"name": "params-hr-huff-rle-slow", "ops": [
+        ["init", 7, 15, 8, 0], ["deflate", sl(t, 0, 35000), Z_NO_FLUSH], ["params", 7, 2],
+        ["deflate", sl(t, 35000, 45000), Z_NO_FLUSH], ["params", 7, 3], ["deflate", sl(t, 45000, 52000), Z_NO_FLUSH],
+        ["params", 8, 0], ["deflate", sl(t, 52000, 100000), Z_FINISH]]})
+    S.append({"name": "params-hr-small-out", "ops": [
+        ["init", 6, 15, 8, 0], ["deflate", sl(m, 0, 30000), Z_NO_FLUSH, 3000], ["params", 6, 2],
+        ["deflate", sl(m, 30000, 60000), Z_NO_FLUSH, 3000], ["params", 6, 0],
+        ["deflate", sl(m, 60000, 100000), Z_FINISH, 3000]]})
+    S.append({"name": "params-hr-immediate", "ops": [
+        ["init", 6, 15, 8, 0], ["deflate", sl(t, 0, 30000), Z_NO_FLUSH], ["params", 6, 2], ["params", 6, 0],
+        ["deflate", sl(t, 30000, 100000), Z_FINISH]]})
     S.append({"name": "resetkeep-fresh", "ops": [["init", 6, 15, 8, 0], ["resetkeep"],
                                                  ["deflate", sl(m, 0, 100000), Z_FINISH], ["used"], ["reset"],
                                                  ["resetkeep"], ["deflate", sl(t, 0, 100000), Z_FINISH]]})

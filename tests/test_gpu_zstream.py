@@ -124,3 +124,30 @@ def test_round4_zlib_h_calls_golden(zg):
             bad.append(case["name"])
     print("BAD SESSIONS:", bad)
     assert not bad
+
+
+def test_params_huff_rle_refusals(zg):
+    """deflateParams between deflate_slow and Z_HUFFMAN_ONLY / Z_RLE after data
+    is modelled (test_round4_zlib_h_calls_golden's params-hr-* sessions); the
+    switches it does not model return Z_STREAM_ERROR with strm->msg set and
+    leave the stream usable: from or to deflate_fast levels, memLevel 9, and a
+    stretch whose first call offered a single byte (zgpu_api.cpp deflateParams)."""
+    import zlib as pyzlib
+    L = zg.load()
+    d = datagen.make("text", 60000, 31)
+    cases = [
+        ([["init", 2, 15, 8, 0], ["deflate", d[:20000], 0], ["params", 2, 2]], -2),   # fast -> huff
+        ([["init", 6, 15, 9, 0], ["deflate", d[:20000], 0], ["params", 6, 3]], -2),   # memLevel 9
+        ([["init", 6, 15, 8, 0], ["deflate", d[:20000], 0], ["params", 6, 2],
+          ["deflate", d[20000:30000], 0], ["params", 2, 0]], -2),                       # huff -> fast
+        ([["init", 6, 15, 8, 0], ["deflate", d[:20000], 0], ["params", 6, 2],
+          ["deflate", d[20000:20001], 0], ["deflate", d[20001:30000], 0], ["params", 6, 0]], -2),   # 1-byte call
+    ]
+    for ops, want in cases:
+        full = ops + [["deflate", d[len(d) - 10000:], 4]]
+        rcs, z = run_zsession(L, full)
+        assert rcs[len(ops) - 1] == want, (ops[-1], rcs)
+        assert rcs[-1][-1] == 1, rcs                                    # the stream still finishes
+        got = pyzlib.decompressobj().decompress(z)
+        fed = b"".join(op[1] for op in full if op[0] == "deflate")
+        assert got == fed

@@ -423,6 +423,7 @@ struct FlushSpec {
     int keep_head = 0;
     int zp0 = kMinMatch - 1, zm0 = kMinMatch - 1;   // DeflateJob::zp0 / zm0
     int seg_parse = 0;             // the job's stops are all Z_NO_FLUSH: k_pbig* may parse it (k_pbig6s)
+    SkipSpec sk{};                 // DeflateJob::sk
 };
 
 // deflateInit2_'s windowBits / memLevel rules (deflate.c:400-425): negative
@@ -752,6 +753,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.keep_head = fs->keep_head;
             job.zp0 = fs->zp0;
             job.zm0 = fs->zm0;
+            job.sk = fs->sk;
             if (slow && fs->head_in) {                  // k_links resumes deflate_fast's chains
                 job.lk_n = fs->lk_n;
                 job.lk_head = c.ws_heads.as<uint32_t>();
@@ -879,6 +881,7 @@ struct FlushHost {
     int keep_head = 0;
     int zp0 = kMinMatch - 1, zm0 = kMinMatch - 1;   // DeflateJob::zp0 / zm0
     int seg_parse = 0;                 // see FlushSpec
+    SkipSpec sk{};                     // see FlushSpec
 };
 
 // streaming jobs on the segmented parse (FlushHost::seg_parse): at least this
@@ -976,6 +979,7 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
         fs.zp0 = fh->zp0;
         fs.zm0 = fh->zm0;
         fs.seg_parse = fh->seg_parse;
+        fs.sk = fh->sk;
         if (fh->rec_out) {
             const size_t sym_limit = (size_t(1) << (mem_level + 6)) - 1;         // lit_bufsize - 1
             const size_t nrec = src_len[0] / sym_limit + 4 + 2ull * fh->n + fh->nplan;
@@ -1794,7 +1798,8 @@ struct internal_state {
     ZAlloc<uint8_t> al;
     explicit internal_state(const ZAlloc<uint8_t> &a = {})
         : al(a), in(a), out(a), ev_pos(a), ev_type(a), ev_aux(a), fast_head(a), fast_prev(a), l0_hist(a), hist(a), body(a),
-          items(ZAlloc<StreamItem>(a)), evb(ZAlloc<uint32_t>(a)), iwin(a), cfg_pos(a), cfg_row(ZAlloc<LevelCfg>(a)) {}
+          items(ZAlloc<StreamItem>(a)), evb(ZAlloc<uint32_t>(a)), iwin(a), cfg_pos(a), cfg_row(ZAlloc<LevelCfg>(a)),
+          hr(ZAlloc<HrStretch>(a)) {}
     int level, wrap, strategy;
     zvec<uint8_t> in, out;          // deflate: the input since the last Z_FULL_FLUSH; output queue
     size_t out_pos;
@@ -1931,6 +1936,18 @@ struct internal_state {
     uint64_t zl_pos = ~0ull;
     bool prime_due = false;              // a deflatePrime event no job has written yet
     int bi_used = 0;                     // deflateUsed: ((bi_valid - 1) & 7) + 1 at the last bi_windup, 0: none
+    // Stretches of the current part parsed by deflate_huff / deflate_rle between
+    // deflate_slow stretches (deflateParams after data, deflate.c:760-803):
+    // [a, b) part positions, b = ~0 while open.  Neither function inserts
+    // strings, so the chains after b leave [a, b) out (DeflateJob::sk); the
+    // first fill_window of the stretch still hashes the two s->insert strings
+    // before a that deflate_slow's flush left (deflate.c:306-325), when it
+    // reads at least 2 bytes (first_end: where the first call after a ended),
+    // and the rolling ins_h is set afresh by every fill_window that reads
+    // (deflate.c:307-310), so the strings after b hash as usual.
+    struct HrStretch { uint64_t a, b, first_end; };
+    std::vector<HrStretch, ZAlloc<HrStretch>> hr;
+    bool hr_lost = false;                // an open stretch's part ended (Z_FULL_FLUSH)
 };
 
 namespace {
@@ -2093,6 +2110,19 @@ int deflate_part(internal_state *s, bool closed) {
         fh.snap_head = &s->snap_head;
         fh.snap_prev = &s->snap_prev;
     }
+    // deflate_huff / deflate_rle stretches in this job's window (slow jobs)
+    if (slow) {
+        const uint64_t end = base + sl;
+        for (const internal_state::HrStretch &h : s->hr) {
+            if (h.b == ~0ull) continue;                          // open: this job is no slow job then
+            const uint64_t a = std::max(h.a, (uint64_t)base), b = std::min(h.b, end);
+            if (a >= b) continue;
+            if (fh.sk.n == kMaxSkip) return Z_STREAM_ERROR;
+            fh.sk.a[fh.sk.n] = (uint32_t)(a - base);
+            fh.sk.b[fh.sk.n] = (uint32_t)(b - base);
+            fh.sk.n++;
+        }
+    }
     // With Z_NO_FLUSH stops only (a large deflate() call and its Z_FINISH,
     // compress2 over 4 GiB) the lazy parse is the whole-input one from the
     // resume point -- a stop only holds fill_window back -- so the segmented
@@ -2211,6 +2241,8 @@ void advance_check(internal_state *s, size_t end) {
 
 // a Z_FULL_FLUSH closes the part: the next starts with an empty window
 void close_part(internal_state *s) {
+    if (!s->hr.empty() && s->hr.back().b == ~0ull) s->hr_lost = true;   // ins_h now stale from another part
+    s->hr.clear();
     s->in.clear();
     s->in_base = 0;
     s->ck_pos = 0;
@@ -2754,6 +2786,8 @@ static int deflate_body(z_streamp strm, int flush) {
     s->flushed = true;
     if (P > C) {                                                // copy what is new
         s->in.insert(s->in.end(), strm->next_in + (C - s->rd), strm->next_in + (P - s->rd));
+        if (!s->hr.empty() && s->hr.back().b == ~0ull && !s->hr.back().first_end && P > s->hr.back().a)
+            s->hr.back().first_end = P;                              // an open huff/rle stretch's first call
     } else if (P < C) {                                         // offered less than before: drop the rest
         s->in.resize(P - s->in_base);
         s->stale = true;
@@ -2936,6 +2970,10 @@ int unsupported(z_streamp strm, const char *why) {
     return Z_STREAM_ERROR;
 }
 int deflate_fn(int level) { return level == 0 ? 0 : level <= 3 ? 1 : 2; }   // stored, fast, slow
+// the function deflate() runs (deflate.c:1190-1193): stored, fast, slow, huff 3, rle 4
+int fn_of(int level, int strategy) {
+    return level == 0 ? 0 : strategy == Z_HUFFMAN_ONLY ? 3 : strategy == Z_RLE ? 4 : deflate_fn(level);
+}
 }  // namespace
 
 // deflateResetKeep (deflate.c:635-671): deflateReset without lm_init, so the
@@ -3140,11 +3178,23 @@ int deflateParams(z_streamp strm, int level, int strategy) {
     if (level == Z_DEFAULT_COMPRESSION) level = 6;
     if (level < 0 || level > 9 || strategy < 0 || strategy > Z_FIXED) return Z_STREAM_ERROR;
     const bool started = s->last_flush != -2;
-    if (started && !s->finished) {
-        const bool own_fn = strategy == Z_HUFFMAN_ONLY || strategy == Z_RLE ||
-                            s->strategy == Z_HUFFMAN_ONLY || s->strategy == Z_RLE;
-        if (strategy != s->strategy && own_fn && level != 0 && s->level != 0)
-            return unsupported(strm, "deflateParams: a switch to or from Z_HUFFMAN_ONLY / Z_RLE after data is not modelled");
+    // deflate_slow <-> deflate_huff / deflate_rle after data: the stretch the
+    // latter parse is left out of the chains (internal_state::hr)
+    const int of = fn_of(s->level, s->strategy), nf = fn_of(level, strategy);
+    const bool enter_hr = started && !s->finished && of < 3 && nf >= 3 && level != 0 && s->level != 0;
+    const bool leave_hr = started && !s->finished && of >= 3 && nf < 3 && level != 0 && s->level != 0;
+    if (enter_hr) {
+        const uint64_t X = s->in_base + s->in.size();           // where the Z_BLOCK flush will stand
+        if (of != 2 || s->mem_level > 8 || X < 2)
+            return unsupported(strm, "deflateParams: a switch to Z_HUFFMAN_ONLY / Z_RLE after data is modelled "
+                                     "from deflate_slow levels (memLevel <= 8) only");
+    }
+    if (leave_hr) {
+        const bool ok = nf == 2 && !s->hr_lost && !s->hr.empty() && s->hr.back().b == ~0ull &&
+                        (s->hr.back().first_end == 0 || s->hr.back().first_end >= s->hr.back().a + 2);
+        if (!ok)
+            return unsupported(strm, "deflateParams: a switch from Z_HUFFMAN_ONLY / Z_RLE after data is modelled "
+                                     "back to deflate_slow levels only, after a first call of at least 2 bytes");
     }
     if ((strategy != s->strategy || deflate_fn(level) != deflate_fn(s->level)) && started) {
         const int err = deflate(strm, Z_BLOCK);
@@ -3152,7 +3202,19 @@ int deflateParams(z_streamp strm, int level, int strategy) {
         if (strm->avail_in || pending_input(s)) return Z_BUF_ERROR;
     }
     try {
-        if (started && !s->finished && deflate_fn(level) != deflate_fn(s->level)) {
+        if (enter_hr) {
+            internal_state::HrStretch h{};
+            h.a = s->in_base + s->in.size();
+            h.b = ~0ull;
+            s->hr.push_back(h);
+            s->hr_lost = false;
+        }
+        if (leave_hr) {
+            internal_state::HrStretch &h = s->hr.back();
+            h.b = s->in_base + s->in.size();
+            if (h.b == h.a) s->hr.pop_back();                    // no input in between: nothing skipped, ins_h fresh
+        }
+        if (started && !s->finished && (deflate_fn(level) != deflate_fn(s->level) || enter_hr || leave_hr)) {
             // the parse state the next function inherits (deflate_slow rewrites
             // prev_length at every decision, deflate_fast only match_length,
             // deflate_stored neither)

@@ -139,6 +139,9 @@ __device__ inline void stage_words(uint32_t *dst, const uint32_t *src, int64_t s
 // ------------------------------------------------------------------------
 constexpr int kLC = 8192;
 constexpr int kLThreads = 1024;
+// the sort key of a position k_links does not insert (SkipSpec): past every
+// real hash (hash_bits <= 15 there), so those keys sort last and touch no head
+constexpr uint32_t kSkipHash = 1u << 15;
 constexpr int kLWaves = kLThreads / 64;
 constexpr int kLPer = kLC / kLThreads;
 
@@ -266,8 +269,15 @@ __global__ __launch_bounds__(kLThreads) void k_links(DeflateJob job) {
         // again: only the chunk's positions from e0 on are keyed and sorted
         const int e0 = lk_n > c0 ? (int)(lk_n - c0) : 0;
         const int ms = m > e0 ? m - e0 : 0;
-        for (int e = e0 + tid; e < m; e += kLThreads)
-            ka[e - e0] = hashp(stage[e], stage[e + 1], stage[e + 2], wp) << 13 | (uint32_t)e;
+        for (int e = e0 + tid; e < m; e += kLThreads) {
+            uint32_t h = hashp(stage[e], stage[e + 1], stage[e + 2], wp);
+            if (job.sk.n) {                                  // huff/rle stretches (SkipSpec)
+                const uint32_t p = (uint32_t)c0 + (uint32_t)e;
+                for (uint32_t k = 0; k < job.sk.n; k++)
+                    if (p >= job.sk.a[k] && p < job.sk.b[k]) h = kSkipHash;
+            }
+            ka[e - e0] = h << 13 | (uint32_t)e;
+        }
         links_radix_pass(ka, kb, ms, 13, wcnt, wsum, tid);
         links_radix_pass(kb, ka, ms, 21, wcnt, wsum, tid);
         // sorted: ka[i] = hash << 13 | e, hashes ascending, e ascending within a hash
@@ -276,14 +286,15 @@ __global__ __launch_bounds__(kLThreads) void k_links(DeflateJob job) {
             const uint32_t h = key >> 13, e = key & (kLC - 1);
             const uint32_t p = (uint32_t)c0 + e;
             uint32_t d;
-            if (i > 0 && (ka[i - 1] >> 13) == h) d = e - (ka[i - 1] & (kLC - 1));
+            if (h == kSkipHash) d = 0;                                       // not inserted (SkipSpec)
+            else if (i > 0 && (ka[i - 1] >> 13) == h) d = e - (ka[i - 1] & (kLC - 1));
             else d = (p - head[h]) & 0xffffu;
             kb[e] = (d != 0 && d <= 32767u && d != p) ? d : 0u;               // position 0 is NIL
         }
         __syncthreads();
         for (int i = tid; i < ms; i += kLThreads) {
             const uint32_t key = ka[i];
-            if (i == ms - 1 || (ka[i + 1] >> 13) != (key >> 13))
+            if ((key >> 13) != kSkipHash && (i == ms - 1 || (ka[i + 1] >> 13) != (key >> 13)))
                 head[key >> 13] = (uint16_t)(((uint32_t)c0 + (key & (kLC - 1))) & 0xffffu);
         }
         if (kSegs) {

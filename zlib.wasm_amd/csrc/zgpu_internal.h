@@ -124,6 +124,15 @@ struct EncPlan {
     uint64_t start;          // the output bit where the block's header starts; [nblocks]: the stream's end
 };
 
+// k_links for a streaming job whose window holds deflate_huff / deflate_rle
+// stretches (zgpu_api.cpp internal_state::hr): positions [a[k], b[k]) are not
+// inserted (no link, head[] untouched).  Buffer-relative.
+constexpr int kMaxSkip = 8;
+struct SkipSpec {
+    uint32_t n;
+    uint32_t a[kMaxSkip], b[kMaxSkip];
+};
+
 // Per-buffer workspace layout for one deflate sub-batch (device arrays).
 struct DeflateJob {
     const uint8_t *src;      // batch input base
@@ -267,6 +276,7 @@ struct DeflateJob {
     uint32_t *tl;
     uint32_t ntl;
     int fcmp;                // k_parse_fast: load 64 candidate bytes per chain step (A/B; 0: 16 first)
+    SkipSpec sk;             // k_links: huff/rle stretches of a streaming job (n = 0: none)
 };
 
 // the per-job window/hash parameters (deflate.c:440-455)
