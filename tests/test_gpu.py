@@ -368,6 +368,39 @@ def test_small_single_buffers_tile_segments(zg, oracle):
         assert rc == 0 and z == oracle.compress(bufs[-1], 6)[1]
 
 
+def _syszlib(b, level, wbits=15, mem_level=8):
+    c = pyzlib.compressobj(level, pyzlib.DEFLATED, wbits, mem_level)
+    return c.compress(bytes(b)) + c.flush()
+
+
+@pytest.mark.parametrize("level", [1, 2, 3])
+def test_fast_levels_lds_parse(zg, level):
+    """Few buffers at L1-3 parse with head[], prev[] and the window in LDS
+    (k_parse_fast<kLds>): 16-bit head entries swept every 16 Ki positions, a
+    32 Ki prev ring and a 32 Ki byte ring filled to p + 262.  Streams equal
+    system zlib's for lone buffers across sweeps and ring wraps, tiny and empty
+    buffers, smaller windows and memLevels, and a batch above the LDS variant's
+    256-buffer limit (the HBM variant) beside one below it."""
+    cases = [[datagen.make("text", 64 * 1024, 81)], [datagen.make("mix", (3 << 20) + 17, 82)],
+             [datagen.make("runs", 70000, 83)], [datagen.make("records", (1 << 20) + 1, 84)],
+             [b"", b"a", b"ab", b"abc", bytes(300), datagen.make("markup", 32768 + 262, 85)]]
+    for bufs in cases:
+        got = zg.compress_batch(bufs, level=level)
+        for b, (st, z) in zip(bufs, got):
+            assert st == 0 and z == _syszlib(b, level), (len(b), level)
+    b = datagen.make("mix", 200000, 86)
+    for wb, ml in ((9, 8), (12, 5), (15, 1), (15, 9), (-13, 7)):
+        (st, z), = zg.compress_batch2([b], level=level, window_bits=wb, mem_level=ml)
+        assert st == 0 and z == _syszlib(b, level, wb, ml), (wb, ml)
+    rng = np.random.default_rng(87)
+    for count in (200, 300):
+        bufs = [datagen.make(("text", "mix", "runs")[i % 3], int(rng.integers(1, 40000)), 900 + i)
+                for i in range(count)]
+        got = zg.compress_batch(bufs, level=level)
+        for b, (st, z) in zip(bufs, got):
+            assert st == 0 and z == _syszlib(b, level), (len(b), count)
+
+
 def test_wasm_production_entry_points(zg, oracle):
     """The reference's production path: Zlib.compress -> zlib_compress_buffer,
     and the zlib_crc32 / zlib_adler32 exports (src/wasm_module.c:35,66,74),

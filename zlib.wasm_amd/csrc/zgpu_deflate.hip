@@ -2380,8 +2380,29 @@ __global__ __launch_bounds__(64) void k_parse_ev(DeflateJob job) {
 // whose state lives in SGPRs, and 64-bit positions doubled its scalar
 // arithmetic (add/addc pairs, 64-bit compares) -- at 28 waves per CU sharing
 // one scalar unit, scalar issue is what bounds it.
-template <bool kEv, bool kOne, typename P>
+//
+// kLds (batch jobs of few buffers, hash_bits <= 15): one wave per CU, with
+// head[], prev[] and the window's bytes in the CU's 160 KiB of LDS instead of
+// HBM, so a chain step waits for LDS rather than an L2 / HBM round trip.
+//   s_head: hash_size 16-bit entries, a position's low 16 bits; the age
+//           p - entry (mod 64 Ki) is exact for entries under 64 Ki positions
+//           old, and a sweep every 16 Ki positions turns every entry older than
+//           32 Ki into one that reads as older (an age >= 32768 is no candidate:
+//           MAX_DIST < 32768)
+//   s_prev: prev[] as a 32 Ki ring (a chain only steps between positions within
+//           MAX_DIST of p)
+//   s_ring: in[q] at q mod 32 Ki for q in [p - MAX_DIST, p + 262): the
+//           candidates (> p - MAX_DIST, their byte before, up to 258 after) and
+//           the scan side (p .. p + 257) of every compare.  Filled byte-exact
+//           to p + 262 from a prefetched 128-byte register window.
+constexpr uint32_t kFastRing = 32768;
+template <bool kEv, bool kOne, typename P, bool kLds = false>
 __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *heads) {
+    static_assert(!kLds || (!kEv && kOne), "the LDS variant serves batch jobs");
+    __shared__ uint16_t s_head[kLds ? 32768 : 1];
+    __shared__ uint16_t s_prev[kLds ? kFastRing : 1];
+    __shared__ uint8_t s_ring[kLds ? kFastRing : 1];
+    constexpr uint32_t kRM = kFastRing - 1;
     const int lane = threadIdx.x;
     const bool lead = lane == 0;
     const uint32_t bi = blockIdx.x;
@@ -2396,8 +2417,11 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     uint32_t ci = 0;                                     // configuration changes acted on
     // a resumed flush job (start > 0) finds head[] and prev[] as the last job
     // left them, rebased to its buffer (zgpu_api.cpp deflate_part)
-    if (!kEv || job.start == 0 || (job.dict && !job.keep_head))
+    if (kLds) {
+        for (int i = lane; i < (int)hsize; i += 64) s_head[i] = 0x8000;   // "32 Ki before position 0"
+    } else if (!kEv || job.start == 0 || (job.dict && !job.keep_head)) {
         for (int i = lane; i < (int)hsize; i += 64) head[i] = 0;
+    }
     __threadfence_block();
     __syncthreads();
 
@@ -2455,6 +2479,13 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     };
     auto insert = [&](P q) -> P {           // INSERT_STRING
         const uint32_t h = whash(q);
+        if (kLds) {
+            const uint32_t age = ufl(((uint32_t)q - (uint32_t)s_head[h]) & 0xffffu);   // one address: uniform
+            const P hh = (age != 0 && age < 32768u) ? q - (P)age : 0;
+            s_prev[(uint32_t)q & kRM] = hh != 0 ? (uint16_t)age : (uint16_t)0;
+            s_head[h] = (uint16_t)q;
+            return hh;
+        }
         const P hh = ufl(head[kOne ? vg(h) : h]);
         const P d = q - hh;
         // kOne: every lane stores the same (uniform) value, which keeps the
@@ -2493,7 +2524,8 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
         for (; k0 < maxcmp; k0 += 64) {
             const int kk = k0 + lane;
             const int kc = kk < maxcmp ? kk : maxcmp - 1;
-            const uint32_t x = in[(uint32_t)(a + kc)], y = in[(uint32_t)(pp + kc)];   // unconditional loads
+            const uint32_t x = kLds ? (uint32_t)s_ring[(uint32_t)(a + kc) & kRM] : (uint32_t)in[(uint32_t)(a + kc)];
+            const uint32_t y = kLds ? (uint32_t)s_ring[(uint32_t)(pp + kc) & kRM] : (uint32_t)in[(uint32_t)(pp + kc)];
             const uint64_t m = __ballot((kk < maxcmp) & (x != y));
             if (m) return k0 + __builtin_ctzll(m);
         }
@@ -2505,6 +2537,21 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
             wsee(q);
             insert(q);
         }
+    // kLds: the byte ring's fill point rf, and the 64-aligned register window
+    // [fb, fb + 128) it is filled from (f1 is loaded 64 bytes before it is needed)
+    P rf = 0, fb = 0, sweep_at = 16384;
+    uint32_t f0 = 0, f1 = 0;
+    if (kLds && n > 0) { f0 = ld(lane); f1 = ld(64 + lane); }
+    auto ring_fill = [&](P target) {
+        while (rf < target) {
+            if (rf >= fb + 64) { f0 = f1; fb += 64; f1 = ld(fb + 64 + lane); }
+            const P e = target < fb + 64 ? target : fb + 64;
+            const P q = fb + lane;
+            if (q >= rf && q < e) s_ring[(uint32_t)q & kRM] = (uint8_t)f0;
+            rf = e;
+        }
+    };
+    auto rbyte = [&](P x) -> uint32_t { return kLds ? (uint32_t)s_ring[(uint32_t)x & kRM] : (uint32_t)in[(uint32_t)x]; };
     P p = start, match_start = 0;
     // deflate_state's prev_length, which deflate_fast never writes: every search
     // starts from it (2, or what deflate_slow left behind a function switch,
@@ -2576,6 +2623,16 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
             }
         }
         wsee(p);
+        if (kLds) {
+            if (p >= sweep_at) {                          // s_head: entries 32 Ki old read as older
+                for (uint32_t i = (uint32_t)lane; i < hsize; i += 64) {
+                    const uint32_t age = ((uint32_t)p - (uint32_t)s_head[i]) & 0xffffu;
+                    if (age == 0 || age >= 32768u) s_head[i] = (uint16_t)((uint32_t)p - 32768u);
+                }
+                sweep_at = p + 16384;
+            }
+            ring_fill(n - p > 262 ? p + 262 : n);         // slot of p - 32506 is the next to go
+        }
         if (kEv)                                         // deflateParams / deflateTune
             while (ci < job.ncfg && p >= (P)job.cfg_pos[ci]) cfg = job.cfg_tab[ci++];
         P lookahead = po.E - p;
@@ -2609,10 +2666,10 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
                     // candidate bytes are loaded (most compares end there): a
                     // 16-byte span crosses a cache line far less often than 64
                     // (DeflateJob::fcmp: 64, the round-3 compare)
-                    const int c0 = job.fcmp ? 64 : 16;
-                    const uint32_t dv = prev[vg((uint32_t)cur)];
+                    const int c0 = (kLds || job.fcmp) ? 64 : 16;
+                    const uint32_t dv = kLds ? (uint32_t)s_prev[(uint32_t)cur & kRM] : (uint32_t)prev[vg((uint32_t)cur)];
                     uint32_t cbyte = 0;
-                    if (lane < c0) cbyte = in[(uint32_t)(cur + lc)];
+                    if (lane < c0) cbyte = rbyte(cur + lc);
                     __builtin_amdgcn_sched_barrier(0);       // both loads issued before either is used
                     const int mc = maxcmp < c0 ? maxcmp : c0;
                     const uint64_t m = __ballot(lane < mc && cbyte != sb);
@@ -2624,7 +2681,7 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
                 }
                 // from best_len 0 the quick reject also compares the bytes
                 // before the strings (scan_end1 = scan[-1]) and the first two
-                if (k > best && (best != 0 || (k >= 2 && in[(uint32_t)(cur - 1)] == in[(uint32_t)(p - 1)]))) {
+                if (k > best && (best != 0 || (k >= 2 && rbyte(cur - 1) == rbyte(p - 1)))) {
                     match_start = cur;
                     best = k;
                     if (k >= nice) break;
@@ -2659,7 +2716,13 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
                         if ((uint32_t)lane == k) h = hk;
                     }
                 }
-                const P hh0 = mine ? (P)head[h] : 0;
+                P hh0 = 0;
+                if (kLds) {
+                    const uint32_t age = mine ? ((uint32_t)q - (uint32_t)s_head[h]) & 0xffffu : 0u;
+                    hh0 = (age != 0 && age < 32768u) ? q - (P)age : 0;
+                } else {
+                    hh0 = mine ? (P)head[h] : 0;
+                }
                 P hq = hh0;
                 bool last = mine;
                 for (uint32_t k = 0; k < cntk; k++) {
@@ -2672,8 +2735,14 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
                 }
                 if (mine) {
                     const P dd = q - hq;
-                    prev[q] = (hq != 0 && dd <= 32767) ? (uint16_t)dd : 0;
-                    if (last) head[h] = (uint32_t)q;
+                    const uint16_t lk = (hq != 0 && dd <= 32767) ? (uint16_t)dd : 0;
+                    if (kLds) {
+                        s_prev[(uint32_t)q & kRM] = lk;
+                        if (last) s_head[h] = (uint16_t)q;
+                    } else {
+                        prev[q] = lk;
+                        if (last) head[h] = (uint32_t)q;
+                    }
                 }
             } else if (match_length <= cfg.lazy && lookahead >= kMinMatch) {
                 // deflateTune's longer max_insert_length: one insert at a time
@@ -4002,7 +4071,16 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     case 6: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 1); break;
     case 3: {
         const bool ev = job.nfl || job.start || job.srec;
+        // few buffers (a lone compress2 at L1-3): head / prev / window in LDS, one wave per CU
+        static const uint32_t lds_max = [] {
+            const char *e = std::getenv("ZGPU_FAST_LDS_MAX");     // A/B: 0 turns the variant off
+            return e ? (uint32_t)std::atoi(e) : 256u;
+        }();
         if (ev) hipLaunchKernelGGL((k_parse_fast<true, true, int64_t>), grid, dim3(64), 0, st, job, heads);
+        else if (job.count <= lds_max && job.hbits <= 15 && job.pos31)
+            hipLaunchKernelGGL((k_parse_fast<false, true, int32_t, true>), grid, dim3(64), 0, st, job, heads);
+        else if (job.count <= lds_max && job.hbits <= 15)
+            hipLaunchKernelGGL((k_parse_fast<false, true, int64_t, true>), grid, dim3(64), 0, st, job, heads);
         else if (job.pos31) hipLaunchKernelGGL((k_parse_fast<false, true, int32_t>), grid, dim3(64), 0, st, job, heads);
         else hipLaunchKernelGGL((k_parse_fast<false, true, int64_t>), grid, dim3(64), 0, st, job, heads);
         break;
