@@ -1,0 +1,125 @@
+"""Randomized differential sessions of the streaming deflate(): seeded random
+z_stream call sequences (levels 1-9, strategies 0-3, zlib / raw / gzip
+wrappers, windowBits 9..15, memLevel 1..9, every flush kind, input chunks of
+0 bytes to 200 KB, output buffers down to 1 byte, preset dictionaries) replayed
+on libzgpu.so and on the system zlib of the machine the test runs on, call by
+call: every return code and the whole stream must be equal.
+
+The system zlib (1.2.11 on the GPU image) is upstream zlib, whose deflate
+levels 1-9 produce the reference's (1.3.1.1-motley) bytes (BASELINE.md 3.1,
+the bench's byte-identical CPU baseline).  Left out, because they changed
+between those versions: level 0 (deflate_stored's 1.2.12 fixes), Z_FIXED
+(1.3's _tr_flush_block weighs a stored block against the fixed-code length),
+deflateParams (1.2.12 moved its flush condition from high_water to
+last_flush) and deflatePrime (its Z_BUF_ERROR threshold follows the symbol
+buffer layout); the reference's own sessions pin those
+(tests/golden/zstream_golden.json, api_golden.json)."""
+import ctypes
+import ctypes.util
+import random
+
+import pytest
+
+import datagen
+from zhelpers import run_zsession
+
+pytestmark = pytest.mark.gpu
+
+KINDS = ("text", "mix", "runs", "records", "markup", "random")
+FLUSHES = (0, 0, 0, 1, 2, 3, 5)           # Z_NO_FLUSH (more often), PARTIAL, SYNC, FULL, BLOCK
+
+
+def _session(rng):
+    level = rng.randint(1, 9)
+    strategy = rng.choice((0, 0, 0, 1, 2, 3))
+    wb = rng.choice((15, 15, 9, 10, 12, 13, 14))
+    wrap = rng.choice(("zlib", "raw", "gzip"))
+    wbits = {"zlib": wb, "raw": -wb, "gzip": wb + 16}[wrap]
+    mem = rng.choice((8, 8, 1, 2, 5, 7, 9))
+    ops = [["init", level, wbits, mem, strategy]]
+    if wrap != "gzip" and rng.random() < 0.15:
+        ops.append(["dict", datagen.make("text", rng.randint(1, 40000), rng.randint(0, 999))])
+    total = rng.randint(0, 600000)
+    data = b"".join(datagen.make(rng.choice(KINDS), max(1, total // 3), rng.randint(0, 10 ** 6))
+                    for _ in range(3))[:total]
+    pos, ncall = 0, rng.randint(1, 10)
+    for i in range(ncall):
+        last = i == ncall - 1
+        n = len(data) - pos if last else min(len(data) - pos, rng.choice((0, 1, 2, 100, 5000, 70000, 200000)))
+        op = ["deflate", data[pos:pos + n], 4 if last else rng.choice(FLUSHES)]
+        if rng.random() < 0.25:                  # small output buffers, zpipe-style loop
+            op.append(rng.choice((1, 7, 64, 1000, 16384)) if n + len(data) < 20000 else
+                      rng.choice((1000, 16384, 65536)))
+        ops.append(op)
+        pos += n
+    return ops
+
+
+def _system_zlib():
+    name = ctypes.util.find_library("z") or "libz.so.1"
+    return ctypes.CDLL(name)
+
+
+@pytest.mark.parametrize("block", range(4))
+def test_random_deflate_sessions_vs_system_zlib(zg, block):
+    libz = _system_zlib()
+    L = zg.load()
+    rng = random.Random(20261017 + block)
+    bad = []
+    for k in range(30):
+        ops = _session(rng)
+        rz, z = run_zsession(libz, ops)
+        rg, g = run_zsession(L, ops)
+        if rz != rg or z != g:
+            bad.append((k, [o[:1] + ([len(o[1])] if o[0] in ("deflate", "dict") else list(o[1:2])) + list(o[2:])
+                            for o in ops], rz, rg, len(z), len(g)))
+    assert not bad, bad[:3]
+
+
+def _istream(rng, libz):
+    """A stream from system zlib (any level and strategy, flushes inside) and
+    a random inflate call sequence over it: input fed in random pieces, calls
+    with Z_NO_FLUSH / Z_SYNC_FLUSH / Z_BLOCK and output space of 1 byte to 1 MiB,
+    sometimes cut short (a truncated stream)."""
+    level = rng.randint(0, 9)
+    strategy = rng.choice((0, 0, 1, 2, 3, 4))
+    wb = rng.choice((15, 15, 9, 11, 14))
+    wrap = rng.choice(("zlib", "raw", "gzip"))
+    wbits = {"zlib": wb, "raw": -wb, "gzip": wb + 16}[wrap]
+    total = rng.randint(0, 400000)
+    data = b"".join(datagen.make(rng.choice(KINDS), max(1, total // 2), rng.randint(0, 10 ** 6))
+                    for _ in range(2))[:total]
+    cuts = sorted(rng.randint(0, len(data)) for _ in range(rng.randint(0, 4)))
+    zops, pos = [["init", level, wbits, 8, strategy]], 0
+    for c in cuts + [len(data)]:
+        zops.append(["deflate", data[pos:c], 4 if c == len(data) else rng.choice((0, 1, 2, 3, 5))])
+        pos = c
+    _, z = run_zsession(libz, zops)
+    if rng.random() < 0.15:
+        z = z[:rng.randint(0, len(z))]
+    dec = {"zlib": rng.choice((wb, 15, 47)), "raw": -15 if rng.random() < 0.5 else -wb,
+           "gzip": rng.choice((wb + 16, 31, 47))}[wrap]
+    ops = [["init", dec]]
+    if wrap == "gzip" and rng.random() < 0.5:
+        ops.append(["header", rng.choice((0, 4, 64)), rng.choice((0, 8, 256)), rng.choice((0, 8, 256))])
+    for _ in range(rng.randint(1, 25)):
+        ops.append(["feed", rng.choice((1, 3, 100, 4096, 70000, 1 << 30))])
+        ops.append(["inflate", rng.choice((0, 0, 2, 5)), rng.choice((1, 100, 5000, 1 << 16, 1 << 20))])
+    ops += [["feed", 1 << 30], ["loop", 0, 1 << 20]]
+    return z, ops
+
+
+@pytest.mark.parametrize("block", range(3))
+def test_random_inflate_sessions_vs_system_zlib(zg, block):
+    from zhelpers import run_iops
+    libz = _system_zlib()
+    L = zg.load()
+    rng = random.Random(4242 + block)
+    bad = []
+    for k in range(30):
+        z, ops = _istream(rng, libz)
+        rz = run_iops(libz, z, ops)
+        rg = run_iops(L, z, ops)
+        if rz != rg:
+            bad.append((k, len(z), ops[:3], rz[0][:6], rg[0][:6]))
+    assert not bad, bad[:3]

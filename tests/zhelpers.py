@@ -383,7 +383,10 @@ def _bind_zstream(L):
             ("inflateBackInit_", C.c_int, [P, C.c_int, C.c_void_p, C.c_char_p, C.c_int]),
             ("inflateBack", C.c_int, [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
             ("inflateBackEnd", C.c_int, [P])):
-        f = getattr(L, name)
+        try:
+            f = getattr(L, name)
+        except AttributeError:                   # an older system zlib (no deflateUsed, ...)
+            continue
         f.restype = res
         f.argtypes = args
 
