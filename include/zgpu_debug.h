@@ -17,6 +17,9 @@ extern "C" {
 #endif
 int zgpu_debug_stages(const uint8_t *src, size_t n, int level, uint16_t *link,
                       uint32_t *rfull, uint32_t *rquart);
+/* streams the block-parallel decode of a lone stream finished so far (the
+ * others went through the sequential decode) */
+uint64_t zgpu_debug_par_inflates(void);
 #ifdef __cplusplus
 }
 #endif

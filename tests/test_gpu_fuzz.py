@@ -76,11 +76,11 @@ def test_random_deflate_sessions_vs_system_zlib(zg, block):
     assert not bad, bad[:3]
 
 
-def _istream(rng, libz):
+def _istream(rng, libz, small_out=False):
     """A stream from system zlib (any level and strategy, flushes inside) and
     a random inflate call sequence over it: input fed in random pieces, calls
-    with Z_NO_FLUSH / Z_SYNC_FLUSH / Z_BLOCK and output space of 1 byte to 1 MiB,
-    sometimes cut short (a truncated stream)."""
+    with Z_NO_FLUSH / Z_SYNC_FLUSH / Z_BLOCK, sometimes cut short (a truncated
+    stream).  Output space per call: 1 MiB, or (small_out) 1 byte to 1 MiB."""
     level = rng.randint(0, 9)
     strategy = rng.choice((0, 0, 1, 2, 3, 4))
     wb = rng.choice((15, 15, 9, 11, 14))
@@ -104,13 +104,16 @@ def _istream(rng, libz):
         ops.append(["header", rng.choice((0, 4, 64)), rng.choice((0, 8, 256)), rng.choice((0, 8, 256))])
     for _ in range(rng.randint(1, 25)):
         ops.append(["feed", rng.choice((1, 3, 100, 4096, 70000, 1 << 30))])
-        ops.append(["inflate", rng.choice((0, 0, 2, 5)), rng.choice((1, 100, 5000, 1 << 16, 1 << 20))])
+        ops.append(["inflate", rng.choice((0, 0, 2, 5)),
+                    rng.choice((1, 100, 5000, 1 << 16, 1 << 20)) if small_out else 1 << 20])
     ops += [["feed", 1 << 30], ["loop", 0, 1 << 20]]
     return z, ops
 
 
 @pytest.mark.parametrize("block", range(3))
 def test_random_inflate_sessions_vs_system_zlib(zg, block):
+    """Every call's status, avail_in, total_in, total_out (and Z_BLOCK's
+    data_type), the output and the gzip header fields."""
     from zhelpers import run_iops
     libz = _system_zlib()
     L = zg.load()
@@ -122,4 +125,25 @@ def test_random_inflate_sessions_vs_system_zlib(zg, block):
         rg = run_iops(L, z, ops)
         if rz != rg:
             bad.append((k, len(z), ops[:3], rz[0][:6], rg[0][:6]))
+    assert not bad, bad[:3]
+
+
+@pytest.mark.parametrize("block", range(2))
+def test_random_inflate_small_output_vs_system_zlib(zg, block):
+    """Output space down to 1 byte per call: the output, the gzip header
+    fields and the last call's status, avail_in, total_in and total_out equal
+    the reference's.  Between calls the input taken runs ahead of zlib's
+    whenever the output space ends before the input does (this inflate()
+    decodes all the input it is given)."""
+    from zhelpers import run_iops
+    libz = _system_zlib()
+    L = zg.load()
+    rng = random.Random(7373 + block)
+    bad = []
+    for k in range(30):
+        z, ops = _istream(rng, libz, small_out=True)
+        rz = run_iops(libz, z, ops)
+        rg = run_iops(L, z, ops)
+        if rz[1] != rg[1] or rz[2] != rg[2] or rz[0][-1][-1] != rg[0][-1][-1]:
+            bad.append((k, len(z), ops[:3], rz[0][-1][-1:], rg[0][-1][-1:]))
     assert not bad, bad[:3]

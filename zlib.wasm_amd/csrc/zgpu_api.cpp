@@ -250,6 +250,9 @@ struct Ctx {
     DevBuf ws_srec, ws_snap;  // a streaming job's block records and head[] snapshot
     // inflate: match records, per-stream results, checks, offsets, stop codes
     DevBuf ws_mrec, ws_irec, ws_ick, ws_imeta, ws_istop;
+    // the block-parallel decode of a lone stream (inflate_par): candidate lists,
+    // per-block jobs and records, output symbols
+    DevBuf ws_par1, ws_par2, ws_pjob, ws_psym;
     hipStream_t aux = nullptr;
     hipEvent_t ev_links[2] = {nullptr, nullptr}, ev_match[2] = {nullptr, nullptr};
     // pinned host staging of single small crc32()/adler32() calls (checksum_small)
@@ -1062,6 +1065,7 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
 // match records (a match writes >= 3 bytes, the last one may be cut short).
 // stop_out (device, optional): InflateStop per stream.
 // ------------------------------------------------------------------------
+constexpr uint64_t kParInflateMin = 256 * 1024;   // inflate_par: lone streams from this many compressed bytes
 struct InflateResumeDev {          // InflateJob's resume arrays (device, per stream)
     const uint64_t *res_bit;
     const uint32_t *res_hist;
@@ -1071,10 +1075,259 @@ struct InflateResumeDev {          // InflateJob's resume arrays (device, per st
     uint32_t dmax = 0;             // InflateJob::dmax
 };
 
+// ------------------------------------------------------------------------
+// The block-parallel decode of a lone stream (a large uncompress, say): a
+// stream decodes on one wave at about 8 MB/s, and a lone one leaves the rest of
+// the GPU idle.  Its dynamic and stored blocks are found by trying every bit
+// offset as a block header (k_infl_scan1 / k_infl_scan2: inftrees.c's rules
+// on the header and both codes); every candidate is decoded count-only for its
+// end and output length (k_inflate_decode, InflateJob::count_only); the chain
+// of ends is followed from the first block (a fixed-code block, which no scan
+// can tell from noise, is decoded count-only when the chain reaches it).  Then
+// all blocks of the chain decode at once at their output offsets, k_infl_sym
+// resolves each block's matches with the bytes before it as references, and
+// one k_infl_resolve launch per block, in stream order, turns the references
+// into bytes.  The check value and the trailer are compared last.  Anything
+// else -- an error anywhere, FDICT, a gzip FHCRC, output beyond the capacity,
+// a candidate list overflow -- returns 0 and the caller runs the exact
+// sequential path, which reports what uncompress2 would.
+// Returns 1 (done: out_len, used), 0 (not taken), < 0 a device error.
+// ------------------------------------------------------------------------
 int inflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
                        uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap, uint64_t *dst_len,
                        uint64_t *src_used, int32_t *status, uint32_t *stop_out, uint32_t count, int wrap,
-                       int wbits, hipStream_t st, const InflateResumeDev *rs = nullptr) {
+                       int wbits, hipStream_t st, const InflateResumeDev *rs = nullptr);
+
+std::atomic<uint64_t> g_par_inflates{0};          // streams the block-parallel decode finished (zgpu_debug.h)
+
+int inflate_par_locked(Ctx &c, const uint8_t *in, uint64_t n, uint8_t *out, uint64_t cap, int wrap, int wbits,
+                       hipStream_t st, uint64_t &out_len, uint64_t &used) {
+    if (n < 64 || n >= (1ull << 31) || cap >= (1ull << 31)) return 0;
+    // ---- the stream header, on the host (inflate.c HEAD .. gzip header)
+    std::vector<uint8_t> h((size_t)std::min<uint64_t>(n, 65536));
+    if (copy_sync(h.data(), in, h.size(), hipMemcpyDeviceToHost, st) != hipSuccess) return -1;
+    uint64_t hb = 0;
+    int kind = 0;                                   // 0 raw, 1 zlib, 2 gzip
+    if (wrap) {
+        if ((wrap & 2) && h[0] == 0x1f && h[1] == 0x8b) {
+            const uint32_t flags = h[3];
+            if (h[2] != 8 || (flags & 0xe0) || (flags & 0x02)) return 0;   // FHCRC: the exact path checks it
+            size_t p = 10;
+            if (flags & 0x04) {
+                if (p + 2 > h.size()) return 0;
+                p += 2 + (h[p] | ((size_t)h[p + 1] << 8));
+            }
+            for (uint32_t f = 0x08; f <= 0x10; f <<= 1) {
+                if (!(flags & f)) continue;
+                while (p < h.size() && h[p] != 0) p++;
+                if (p >= h.size()) return 0;
+                p++;
+            }
+            if (p >= h.size()) return 0;
+            hb = p;
+            kind = 2;
+        } else {
+            const uint32_t cmf = h[0], flg = h[1], wlen = (cmf >> 4) + 8;
+            if (!(wrap & 1) || ((cmf << 8) + flg) % 31 || (cmf & 15) != 8 || wlen > 15 ||
+                (wbits && wlen > (uint32_t)wbits) || (flg & 0x20))
+                return 0;
+            hb = 2;
+            kind = 1;
+        }
+    }
+    // ---- candidate block headers
+    const uint64_t b0 = 8 * hb, b1 = 8 * n;
+    const uint32_t lcap = (uint32_t)std::min<uint64_t>((b1 - b0) / 16 + 65536, 1ull << 26);
+    if (!c.ws_par1.ensure(8ull * lcap + 64) || !c.ws_par2.ensure(8ull * lcap + 64) || !c.ws_imeta.ensure(64))
+        return -1;
+    uint64_t *l1 = c.ws_par1.as<uint64_t>(), *l2 = c.ws_par2.as<uint64_t>();
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(c.ws_imeta.as<uint64_t>() + 4);   // two list counters
+    uint32_t k1 = 0, k2 = 0;
+    if (hipMemsetAsync(cnt, 0, 8, st) != hipSuccess || launch_infl_scan1(in, n, b0, b1, l1, lcap, cnt, st) ||
+        copy_sync(&k1, cnt, 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+        return -1;
+    if (k1 > lcap) return 0;
+    if (launch_infl_scan2(in, n, l1, k1, l2, lcap, cnt + 1, st) ||
+        copy_sync(&k2, cnt + 1, 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+        return -1;
+    if (k2 > lcap) return 0;
+    std::vector<uint64_t> cand(k2);
+    if (k2 && copy_sync(cand.data(), l2, 8ull * k2, hipMemcpyDeviceToHost, st) != hipSuccess) return -1;
+    std::sort(cand.begin(), cand.end());
+    // ---- count-only decodes: where each candidate block ends, what it makes
+    struct Span { uint64_t end; uint64_t out; uint32_t stop, last; };
+    auto spans = [&](const std::vector<uint64_t> &bits, std::vector<Span> &res) -> int {
+        const uint32_t K = (uint32_t)bits.size();
+        res.assign(K, Span{0, 0, kIData, 0});
+        if (K == 0) return 0;
+        // per job: src_off src_len res_bit dst_off dst_cap dst_len blk_out[2] zstate[2] | res_hist | status | rec
+        const size_t bytes = 8ull * K * 10 + 4ull * K * 2 + sizeof(InflateRec) * K + 256;
+        if (!c.ws_pjob.ensure(bytes)) return -1;
+        uint64_t *d = c.ws_pjob.as<uint64_t>();
+        uint64_t *soff = d, *slen = d + K, *rbit = d + 2 * K, *doff = d + 3 * K, *dcap = d + 4 * K, *dlen = d + 5 * K;
+        uint64_t *blk = d + 6 * K, *zs = d + 8 * K;
+        uint32_t *hist = reinterpret_cast<uint32_t *>(d + 10 * K);
+        int32_t *stv = reinterpret_cast<int32_t *>(hist + K);
+        InflateRec *rec = reinterpret_cast<InflateRec *>((reinterpret_cast<uintptr_t>(stv + K) + 63) & ~(uintptr_t)63);
+        std::vector<uint64_t> zero(K, 0), nn(K, n);
+        std::vector<uint32_t> hh(K, 32768u);
+        if (hipMemcpyAsync(soff, zero.data(), 8ull * K, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(slen, nn.data(), 8ull * K, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(rbit, bits.data(), 8ull * K, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(doff, zero.data(), 8ull * K, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(dcap, zero.data(), 8ull * K, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(hist, hh.data(), 4ull * K, hipMemcpyHostToDevice, st) != hipSuccess)
+            return -1;
+        InflateJob job{};
+        job.src = in; job.src_off = soff; job.src_len = slen;
+        job.dst = out; job.dst_off = doff; job.dst_cap = dcap; job.dst_len = dlen;
+        job.status = stv; job.first = 0; job.count = K; job.wrap = 0;
+        job.mrec_off = soff; job.mrec = nullptr;
+        job.rec = rec;
+        job.res_bit = rbit; job.res_hist = hist; job.blk_out = blk;
+        job.stop_mode = 2 | 4;                   // stop at the block's end (the last one's too), start in TYPE
+        job.zstate_out = zs;                     // bit 32: BFINAL of the block
+        job.count_only = 1;
+        if (launch_inflate_stage(0, job, st)) return -1;
+        std::vector<InflateRec> r(K);
+        std::vector<uint64_t> bo(2ull * K), z(2ull * K);
+        if (copy_sync(r.data(), rec, sizeof(InflateRec) * K, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            copy_sync(bo.data(), blk, 16ull * K, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            copy_sync(z.data(), zs, 16ull * K, hipMemcpyDeviceToHost, st) != hipSuccess)
+            return -1;
+        for (uint32_t k = 0; k < K; k++) {
+            res[k].stop = r[k].stop;
+            res[k].last = (z[2ull * k] >> 32) & 1u;
+            res[k].out = r[k].put >= 32768 ? r[k].put - 32768 : 0;
+            res[k].end = bo[2ull * k];           // the bit after its END_BLOCK code
+        }
+        return 0;
+    };
+    std::vector<Span> sp;
+    if (spans(cand, sp)) return -1;
+    // ---- the chain of blocks from the first one
+    struct Blk { uint64_t bit, o0, out; bool last; };
+    std::vector<Blk> chain;
+    uint64_t b = b0, total = 0;
+    int misses = 0;
+    for (;;) {
+        const auto it = std::lower_bound(cand.begin(), cand.end(), b);
+        Span s;
+        if (it != cand.end() && *it == b) {
+            s = sp[(size_t)(it - cand.begin())];
+        } else {                                    // a fixed-code block (or a stored one the scan missed)
+            if (++misses > 16) return 0;
+            std::vector<Span> one;
+            if (spans(std::vector<uint64_t>{b}, one)) return -1;
+            s = one[0];
+        }
+        if (s.stop != kIBlock || s.end <= b) return 0;
+        chain.push_back(Blk{b, total, s.out, s.last != 0});
+        total += s.out;
+        if (total > cap) return 0;
+        b = s.end;
+        if (s.last) break;
+    }
+    const uint64_t tb = (b + 7) >> 3;               // the trailer's first byte (inflate.c CHECK: BYTEBITS)
+    const uint64_t tlen = kind == 1 ? 4 : kind == 2 ? 8 : 0;
+    if (tb + tlen > n) return 0;
+    // ---- every block at its output offset: literals in place, matches as records
+    const uint32_t NB = (uint32_t)chain.size();
+    std::vector<uint64_t> soff(NB, 0), slen(NB, n), rbit(NB), doff(NB), dcap(NB), moff(NB);
+    std::vector<uint32_t> hist(NB);
+    uint64_t mtot = 0;
+    for (uint32_t k = 0; k < NB; k++) {
+        const Blk &B = chain[k];
+        hist[k] = (uint32_t)std::min<uint64_t>(32768, B.o0);
+        rbit[k] = B.bit;
+        doff[k] = B.o0 - hist[k];
+        dcap[k] = hist[k] + B.out;
+        moff[k] = mtot;
+        mtot += B.out / 3 + 2;
+    }
+    const size_t jb = 8ull * NB * 9 + 4ull * NB * 2 + sizeof(InflateRec) * NB + 256;
+    if (!c.ws_pjob.ensure(jb) || !c.ws_mrec.ensure(8 * mtot + 64) || !c.ws_psym.ensure(4 * total + 64)) return -1;
+    uint64_t *d = c.ws_pjob.as<uint64_t>();
+    uint64_t *d_soff = d, *d_slen = d + NB, *d_rbit = d + 2 * NB, *d_doff = d + 3 * NB, *d_dcap = d + 4 * NB;
+    uint64_t *d_dlen = d + 5 * NB, *d_blk = d + 6 * NB, *d_moff = d + 8 * NB;
+    uint32_t *d_hist = reinterpret_cast<uint32_t *>(d + 9 * NB);
+    int32_t *d_stv = reinterpret_cast<int32_t *>(d_hist + NB);
+    InflateRec *d_rec = reinterpret_cast<InflateRec *>((reinterpret_cast<uintptr_t>(d_stv + NB) + 63) & ~(uintptr_t)63);
+    if (hipMemcpyAsync(d_soff, soff.data(), 8ull * NB, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_slen, slen.data(), 8ull * NB, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_rbit, rbit.data(), 8ull * NB, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_doff, doff.data(), 8ull * NB, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_dcap, dcap.data(), 8ull * NB, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_moff, moff.data(), 8ull * NB, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_hist, hist.data(), 4ull * NB, hipMemcpyHostToDevice, st) != hipSuccess)
+        return -1;
+    InflateJob job{};
+    job.src = in; job.src_off = d_soff; job.src_len = d_slen;
+    job.dst = out; job.dst_off = d_doff; job.dst_cap = d_dcap; job.dst_len = d_dlen;
+    job.status = d_stv; job.first = 0; job.count = NB; job.wrap = 0;
+    job.mrec_off = d_moff; job.mrec = c.ws_mrec.as<uint64_t>();
+    job.rec = d_rec;
+    job.res_bit = d_rbit; job.res_hist = d_hist; job.blk_out = d_blk;
+    job.stop_mode = 2 | 4;
+    if (c.timer.run(3, st, [&] { return launch_inflate_stage(0, job, st); })) return -1;
+    std::vector<InflateRec> r(NB);
+    if (copy_sync(r.data(), d_rec, sizeof(InflateRec) * NB, hipMemcpyDeviceToHost, st) != hipSuccess) return -1;
+    std::vector<ParBlkHost> pb;
+    for (uint32_t k = 0; k < NB; k++) {
+        const Blk &B = chain[k];
+        if (r[k].put != hist[k] + B.out || r[k].stop != (uint32_t)kIBlock) return 0;
+        if (r[k].nmatch) pb.push_back(ParBlkHost{B.o0, B.o0 + B.out, B.o0 - hist[k], moff[k], r[k].nmatch, 0});
+    }
+    // ---- matches: symbols per block, then references block by block
+    if (!pb.empty()) {
+        if (!c.ws_par1.ensure(sizeof(ParBlkHost) * pb.size() + 64)) return -1;
+        uint32_t *sym = c.ws_psym.as<uint32_t>();
+        if (hipMemcpyAsync(c.ws_par1.p, pb.data(), sizeof(ParBlkHost) * pb.size(), hipMemcpyHostToDevice, st) !=
+                hipSuccess ||
+            c.timer.run(4, st, [&] {
+                int e = launch_infl_sym(out, sym, c.ws_par1.p, (uint32_t)pb.size(), c.ws_mrec.as<uint64_t>(), st);
+                for (size_t k = 0; !e && k < pb.size(); k++) e = launch_infl_resolve(out, sym, pb[k].o0, pb[k].o1, st);
+                return e;
+            }))
+            return -1;
+    }
+    // ---- the check value against the trailer
+    uint8_t t[8] = {0};
+    if (tlen && copy_sync(t, in + tb, tlen, hipMemcpyDeviceToHost, st) != hipSuccess) return -1;
+    if (kind) {
+        uint64_t *m = c.ws_imeta.ensure(64) ? c.ws_imeta.as<uint64_t>() : nullptr;
+        if (!m) return -1;
+        const uint64_t ol[2] = {0, total};
+        uint32_t *ck = reinterpret_cast<uint32_t *>(m + 2);
+        const size_t ckb = checksum_scratch_bytes(1);
+        void *scr = ckb && c.ws_ck.ensure(ckb) ? c.ws_ck.p : nullptr;
+        uint32_t got = 0;
+        if (hipMemcpyAsync(m, ol, 16, hipMemcpyHostToDevice, st) != hipSuccess ||
+            c.timer.run(0, st, [&] {
+                return kind == 1 ? launch_adler32(out, m, m + 1, nullptr, ck, 1, scr, ckb, st)
+                                 : launch_crc32(out, m, m + 1, nullptr, ck, 1, scr, ckb, st);
+            }) ||
+            copy_sync(&got, ck, 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+            return -1;
+        if (kind == 1) {
+            const uint32_t want = (uint32_t)t[0] << 24 | (uint32_t)t[1] << 16 | (uint32_t)t[2] << 8 | t[3];
+            if (got != want) return 0;
+        } else {
+            const uint32_t want = t[0] | (uint32_t)t[1] << 8 | (uint32_t)t[2] << 16 | (uint32_t)t[3] << 24;
+            const uint32_t isz = t[4] | (uint32_t)t[5] << 8 | (uint32_t)t[6] << 16 | (uint32_t)t[7] << 24;
+            if (got != want || isz != (uint32_t)total) return 0;
+        }
+    }
+    out_len = total;
+    used = tb + tlen;
+    g_par_inflates.fetch_add(1);
+    return 1;
+}
+
+int inflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, const uint64_t *src_len,
+                       uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap, uint64_t *dst_len,
+                       uint64_t *src_used, int32_t *status, uint32_t *stop_out, uint32_t count, int wrap,
+                       int wbits, hipStream_t st, const InflateResumeDev *rs) {
     if (wrap < 0 || wrap > 3) return ZGPU_STREAM_ERROR;
     if (count == 0) return ZGPU_OK;
     std::vector<uint64_t> lens(count), caps(count);
@@ -1084,6 +1337,33 @@ int inflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         return ZGPU_MEM_ERROR;
     for (uint32_t i = 0; i < count; i++)
         if (lens[i] >= (1ull << 32) || caps[i] >= (1ull << 32)) return ZGPU_STREAM_ERROR;   // per-stream limit
+    // a lone large stream: the block-parallel decode when it applies
+    static const bool no_par = std::getenv("ZGPU_NO_PAR_INFLATE") != nullptr;    // A/B
+    static const uint64_t par_min = [] {                 // ZGPU_PAR_INFLATE_MIN (tests): compressed bytes
+        const char *e = std::getenv("ZGPU_PAR_INFLATE_MIN");
+        return e ? (uint64_t)std::atoll(e) : (uint64_t)kParInflateMin;
+    }();
+    if (count == 1 && !rs && !no_par && lens[0] >= par_min && caps[0] > 0) {
+        uint64_t so = 0, dof = 0;
+        if (copy_sync(&so, src_off, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            copy_sync(&dof, dst_off, 8, hipMemcpyDeviceToHost, st) != hipSuccess)
+            return ZGPU_MEM_ERROR;
+        uint64_t olen = 0, used = 0;
+        const int pr = inflate_par_locked(c, src + so, lens[0], dst + dof, caps[0], wrap, wbits, st, olen, used);
+        if (pr < 0) return ZGPU_MEM_ERROR;
+        if (pr == 1) {
+            const int32_t zok = 0;
+            const uint32_t send = kIEnd;
+            if (hipMemcpyAsync(dst_len, &olen, 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+                (src_used && hipMemcpyAsync(src_used, &used, 8, hipMemcpyHostToDevice, st) != hipSuccess) ||
+                (status && hipMemcpyAsync(status, &zok, 4, hipMemcpyHostToDevice, st) != hipSuccess) ||
+                (stop_out && hipMemcpyAsync(stop_out, &send, 4, hipMemcpyHostToDevice, st) != hipSuccess))
+                return ZGPU_MEM_ERROR;
+            const int rc = hip_ok(hipStreamSynchronize(st));
+            c.timer.collect();
+            return rc;
+        }
+    }
     const uint64_t budget = c.inflight;
     std::vector<uint32_t> cuts{0};
     {
@@ -1533,6 +1813,8 @@ int zgpu_generate_dev(uint8_t *dst, uint64_t len, uint32_t count, int kind, uint
     return launch_generate(dst, len, count, kind, seed, first_index, static_cast<hipStream_t>(stream))
                ? ZGPU_STREAM_ERROR : ZGPU_OK;
 }
+
+uint64_t zgpu_debug_par_inflates(void) { return g_par_inflates.load(); }
 
 int zgpu_debug_stages(const uint8_t *src, size_t n, int level, uint16_t *link, uint32_t *rfull,
                       uint32_t *rquart) {
@@ -3621,6 +3903,39 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
         // the host, unchecked
         const bool hdr_stop = !s->ivalid && s->wrap && !resume && !block;
         const size_t hl = resume ? s->hist.size() : 0;
+        // inflate(Z_BLOCK) stops after the header only in the call that reads
+        // its last byte (inflate.c: mode TYPE is reached there); when an earlier
+        // call already took the whole header, the decode is mid-block and this
+        // call runs to the end of the first block
+        bool hdr_done = false;
+        if (block && !resume && s->wrap && s->in.size() >= took) {
+            const size_t before = s->in.size() - took;          // input the earlier calls gave
+            const uint8_t *h = s->in.data();
+            size_t hlen = 0;                                    // 0: not complete in `before` bytes
+            if (before >= 2 && (s->wrap & 2) && h[0] == 0x1f && h[1] == 0x8b) {
+                if (before >= 10) {
+                    const uint32_t fl = h[3];
+                    size_t p = 10;
+                    bool ok = true;
+                    if (fl & 0x04) {
+                        ok = before >= p + 2;
+                        if (ok) p += 2 + (h[p] | ((size_t)h[p + 1] << 8));
+                    }
+                    for (uint32_t f = 0x08; ok && f <= 0x10; f <<= 1) {
+                        if (!(fl & f)) continue;
+                        while (p < before && h[p] != 0) p++;
+                        ok = p < before;
+                        p++;
+                    }
+                    if (ok && (fl & 0x02)) p += 2;
+                    if (ok && p <= before) hlen = p;
+                }
+            } else if (before >= 2) {
+                hlen = (h[1] & 0x20) ? 6 : 2;                   // FDICT: the DICTID too
+                if (hlen > before) hlen = 0;
+            }
+            hdr_done = hlen != 0;
+        }
         std::vector<uint8_t> o;
         InflateTry t{};
         int rc;
@@ -3630,7 +3945,8 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             // inflate(Z_BLOCK): stop after the header (zlib / gzip, from the
             // start) or at the end of the next block
             const uint32_t mode = hdr_stop ? 1u
-                                  : !block ? 0u : ((!resume && s->wrap) ? 1u : 2u) | (resume && s->itype ? 4u : 0u);
+                                  : !block ? 0u
+                                           : ((!resume && s->wrap && !hdr_done) ? 1u : 2u) | (resume && s->itype ? 4u : 0u);
             if (!rc) rc = inflate_try_locked(*L.c, s->in.data(), s->in.size(), resume,
                                              resume ? s->res_bit - 8ull * s->in_base : 0, s->hist.data(), hl,
                                              hl + s->cap, s->wrap, s->wbits, o, t, mode,

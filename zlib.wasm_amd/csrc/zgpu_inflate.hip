@@ -278,10 +278,11 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
     const uint32_t n = (uint32_t)job.src_len[g];
     const uint8_t *in = job.src + job.src_off[g];
     const uint64_t cap0 = job.dst_cap[g];
-    const bool probe = cap0 == 0;
-    const uint32_t cap = probe ? 1u : (uint32_t)cap0;
-    uint8_t *out = job.dst + job.dst_off[g];
-    uint64_t *mrec = job.mrec + job.mrec_off[bi];
+    const bool counting = job.count_only != 0;
+    const bool probe = cap0 == 0 && !counting;
+    const uint32_t cap = counting ? 0xffffffffu : probe ? 1u : (uint32_t)cap0;
+    uint8_t *out = counting ? nullptr : job.dst + job.dst_off[g];
+    uint64_t *mrec = counting ? nullptr : job.mrec + job.mrec_off[bi];
     const uint64_t inbits = (uint64_t)n * 8;
     const int wrap = job.wrap;
 
@@ -304,6 +305,10 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
     // block's bytes left (COPY); back = -1 outside a length/distance symbol
     int64_t zmark = -65536;
     uint32_t zcodes = 0xffffffffu;                   // inflateCodesUsed of the last dynamic block (none: ~0)
+    // a gzip header cut short: the bits inflate.c holds there (-1: from the reader).  Its
+    // fields come in NEEDBITS groups (magic 16, CM+FLG 16, MTIME 32, XFL+OS 16, XLEN 16, HCRC
+    // 16 bits) with extra / name / comment bytes taken as they come (inflate.c:629-807)
+    int64_t zhold = -1;
     if (job.res_bit) {
         seek(r, (uint32_t)(rb >> 3));
         refill(S, r, in, n, lane);
@@ -315,13 +320,13 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
     auto ceil_used = [&]() -> uint64_t { return (bitpos(r) + 7) >> 3; };
     auto flush_obuf = [&](uint32_t upto) {          // output bytes [ob, upto), upto <= ob + kOBuf
         __syncthreads();
-        if (!probe)
+        if (!probe && !counting)
             for (uint32_t i = (uint32_t)lane; i < upto - ob; i += 64) out[ob + i] = S.obuf[i];
         __syncthreads();
     };
     auto flush_mbuf = [&](uint32_t k) {             // the last k staged records
         __syncthreads();
-        if ((uint32_t)lane < k) mrec[nm - k + (uint32_t)lane] = S.mbuf[lane];
+        if (!counting && (uint32_t)lane < k) mrec[nm - k + (uint32_t)lane] = S.mbuf[lane];
         __syncthreads();
     };
 
@@ -333,16 +338,16 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
         if ((wrap & 2) && h16 == 0x8b1fu) {
             gz = true;
             // header fields straight from global memory (a few bytes)
-            if (n < 4) { stop = kIInEnd; used = n; goto done; }
+            if (n < 4) { zhold = 8ll * (n - 2); stop = kIInEnd; used = n; goto done; }
             const uint32_t flags = in[2] | ((uint32_t)in[3] << 8);
             if ((flags & 0xffu) != 8u || (flags & 0xe000u)) { stop = kIData; used = 4; goto done; }
             uint32_t p = 10;
-            if (n < p) { stop = kIInEnd; used = n; goto done; }
+            if (n < p) { zhold = 8ll * (n < 8 ? n - 4 : n - 8); stop = kIInEnd; used = n; goto done; }
             if (flags & 0x0400u) {                                   // FEXTRA
-                if (n < p + 2) { stop = kIInEnd; used = n; goto done; }
+                if (n < p + 2) { zhold = 8ll * (n - p); stop = kIInEnd; used = n; goto done; }
                 const uint32_t xlen = in[p] | ((uint32_t)in[p + 1] << 8);
                 p += 2;
-                if (n - p < xlen) { stop = kIInEnd; used = n; goto done; }
+                if (n - p < xlen) { zhold = 0; stop = kIInEnd; used = n; goto done; }
                 p += xlen;
             }
             for (uint32_t f = 0x0800u; f <= 0x1000u; f <<= 1) {      // FNAME, FCOMMENT
@@ -353,11 +358,11 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
                     const uint64_t m = __ballot(x < n && in[x] == 0);
                     if (m) z = q + (uint32_t)__builtin_ctzll(m);
                 }
-                if (z == 0xffffffffu) { stop = kIInEnd; used = n; goto done; }
+                if (z == 0xffffffffu) { zhold = 0; stop = kIInEnd; used = n; goto done; }
                 p = z + 1;
             }
             if (flags & 0x0200u) {                                   // FHCRC
-                if (n < p + 2) { stop = kIInEnd; used = n; goto done; }
+                if (n < p + 2) { zhold = 8ll * (n - p); stop = kIInEnd; used = n; goto done; }
                 uint32_t c = 0xffffffffu;
                 for (uint32_t q = 0; q < p; q++) c = job.crc_byte[(c ^ in[q]) & 0xffu] ^ (c >> 8);
                 c = ~c;
@@ -411,7 +416,7 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
             if (cnt > n - bp) cnt = n - bp;
             if (cnt > cap - put) cnt = cap - put;
             if (probe) { if (cnt) pbyte = in[bp]; }
-            else for (uint32_t i = (uint32_t)lane; i < cnt; i += 64) out[put + i] = in[bp + i];
+            else if (!counting) for (uint32_t i = (uint32_t)lane; i < cnt; i += 64) out[put + i] = in[bp + i];
             put += cnt;
             ob = put;
             seek(r, bp + cnt);
@@ -616,7 +621,8 @@ done:
         }
         if (job.zstate_out) {
             const uint64_t bp = bitpos(r);
-            job.zstate_out[2 * (uint64_t)g] = (bp <= inbits ? inbits - bp : 0) | (uint64_t)zlast << 32 |
+            const uint64_t held = zhold >= 0 ? (uint64_t)zhold : (bp <= inbits ? inbits - bp : 0);
+            job.zstate_out[2 * (uint64_t)g] = held | (uint64_t)zlast << 32 |
                                               (uint64_t)(ztype ? 1 : 0) << 33 | (uint64_t)(zstored ? 1 : 0) << 34;
             job.zstate_out[2 * (uint64_t)g + 1] = (uint64_t)(uint32_t)(int32_t)zmark | (uint64_t)zcodes << 32;
         }
@@ -716,6 +722,241 @@ __global__ void k_inflate_finish(InflateJob job) {
     if (job.stop_out) job.stop_out[g] = stop;
     job.dst_len[g] = probe ? 0 : rc.put;
     if (job.src_used) job.src_used[g] = used;
+}
+
+// ------------------------------------------------------------------------
+// Block-parallel decode of a lone large stream (zgpu_api.cpp inflate_par).
+// deflate's blocks are found without decoding what precedes them: every bit
+// offset is tried as a block header, the candidates that pass are decoded
+// count-only (k_inflate_decode, InflateJob::count_only) for their end, and the
+// host follows the chain of ends from the first block.  Then every block of
+// the chain is decoded at its output offset (literals in place, matches as
+// records), k_infl_sym resolves each block's matches with the bytes before
+// the block as references (an output position), and k_infl_resolve replaces
+// the references block by block in stream order.
+// ------------------------------------------------------------------------
+// 64 bits of the stream from bit b (zero past n)
+__device__ inline uint64_t bits_at(const uint8_t *in, uint64_t n, uint64_t b) {
+    const uint64_t B = b >> 3;
+    uint64_t lo = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) lo |= (uint64_t)(B + k < n ? in[B + k] : 0) << (8 * k);
+    const uint32_t sh = (uint32_t)(b & 7);
+    const uint64_t nx = B + 8 < n ? in[B + 8] : 0;
+    return sh ? (lo >> sh) | (nx << (64 - sh)) : lo;
+}
+
+// k_infl_scan1: bit offsets [b0, b1) that could hold a stored block header
+// (LEN == ~NLEN at the next byte, the block inside the input) or a dynamic one
+// (HLIT <= 29, HDIST <= 29, a complete code-length code: inftrees.c's CODES
+// rule).  Candidates are appended to list (at most cap; *cnt counts all).
+__global__ __launch_bounds__(256) void k_infl_scan1(const uint8_t *in, uint64_t n, uint64_t b0, uint64_t b1,
+                                                   uint64_t *list, uint32_t cap, uint32_t *cnt) {
+    const uint64_t b = b0 + (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b >= b1) return;
+    const uint64_t w = bits_at(in, n, b);
+    const uint32_t type = (uint32_t)(w >> 1) & 3u;
+    bool ok = false;
+    if (type == 0) {
+        const uint64_t p = (b + 3 + 7) >> 3;
+        if (p + 4 <= n) {
+            const uint32_t len = in[p] | ((uint32_t)in[p + 1] << 8), nlen = in[p + 2] | ((uint32_t)in[p + 3] << 8);
+            ok = len == (nlen ^ 0xffffu) && p + 4 + len <= n;
+        }
+    } else if (type == 2) {
+        const uint32_t hlit = (uint32_t)(w >> 3) & 31u, hdist = (uint32_t)(w >> 8) & 31u;
+        const uint32_t ncode = ((uint32_t)(w >> 13) & 15u) + 4;
+        if (hlit <= 29 && hdist <= 29) {
+            const uint64_t v = bits_at(in, n, b + 17);               // 3 bits per code-length code length
+            uint32_t kraft = 0;
+            for (uint32_t i = 0; i < ncode; i++) {
+                const uint32_t l = (uint32_t)(v >> (3 * i)) & 7u;
+                if (l) kraft += 128u >> l;
+            }
+            ok = kraft == 128u;
+        }
+    }
+    if (ok) {
+        const uint32_t k = atomicAdd(cnt, 1u);
+        if (k < cap) list[k] = b;
+    }
+}
+
+// k_infl_scan2: one thread per scan1 candidate; a dynamic header's code
+// lengths are decoded with its code-length code and both codes checked as
+// inflate_table would (over-subscribed: never; incomplete: only a single
+// 1-bit code; END_BLOCK present; no repeat before the first length and no
+// run past HLIT + HDIST).  Survivors go to out (the stored ones pass).
+struct BitRd {
+    const uint8_t *in;
+    uint64_t n, pos;          // next bit
+    __device__ inline uint32_t get(uint32_t k) {     // k <= 32
+        const uint64_t v = bits_at(in, n, pos);
+        pos += k;
+        return k == 32 ? (uint32_t)v : (uint32_t)v & ((1u << k) - 1u);
+    }
+};
+__global__ __launch_bounds__(256) void k_infl_scan2(const uint8_t *in, uint64_t n, const uint64_t *list,
+                                                   uint32_t count, uint64_t *out, uint32_t cap, uint32_t *cnt) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= count) return;
+    const uint64_t b = list[t];
+    BitRd r{in, n, b};
+    const uint32_t hdr = r.get(3);
+    bool ok = true;
+    if (((hdr >> 1) & 3u) == 2u) {
+        const uint32_t nlen = r.get(5) + 257, ndist = r.get(5) + 1, ncode = r.get(4) + 4;
+        uint64_t cl = 0;                                            // 3 bits per symbol 0..18
+        for (uint32_t i = 0; i < ncode; i++) cl |= (uint64_t)r.get(3) << (3 * c_order[i]);
+        uint32_t ccnt[8];
+#pragma unroll
+        for (int l = 0; l < 8; l++) ccnt[l] = 0;
+        for (uint32_t s2 = 0; s2 < 19; s2++) {
+            const uint32_t l = (uint32_t)(cl >> (3 * s2)) & 7u;
+#pragma unroll
+            for (int q = 1; q < 8; q++) ccnt[q] += l == (uint32_t)q;
+        }
+        const uint32_t total = nlen + ndist;
+        uint32_t have = 0, prev = 0;
+        uint32_t lk = 0, dk = 0, lmax = 0, dmax = 0, l256 = 0;      // Kraft sums in 2^-15 units
+        auto put_len = [&](uint32_t l, uint32_t rep) {
+            // lengths l for symbols have .. have + rep - 1
+            const uint32_t la = have < nlen ? (have + rep < nlen ? rep : nlen - have) : 0;
+            if (l) {
+                lk += la << (15 - l);
+                dk += (rep - la) << (15 - l);
+                if (la) lmax = lmax > l ? lmax : l;
+                if (rep > la) dmax = dmax > l ? dmax : l;
+                if (have <= 256 && 256 < have + rep) l256 = l;
+            }
+            have += rep;
+        };
+        while (ok && have < total) {
+            // canonical decode, one bit at a time (codes are sent MSB first)
+            uint32_t code = 0, first = 0, sym = 0xffu;
+#pragma unroll
+            for (int l = 1; l < 8; l++) {
+                if (sym == 0xffu) {
+                    code |= r.get(1);
+                    const uint32_t c = ccnt[l];
+                    if (code - first < c) {
+                        uint32_t k = code - first;                  // the k-th symbol of length l
+                        for (uint32_t s2 = 0; s2 < 19; s2++)
+                            if (((uint32_t)(cl >> (3 * s2)) & 7u) == (uint32_t)l) {
+                                if (k == 0) { sym = s2; break; }
+                                k--;
+                            }
+                    } else {
+                        first = (first + c) << 1;
+                        code <<= 1;
+                    }
+                }
+            }
+            if (sym == 0xffu) { ok = false; break; }
+            if (sym < 16) { put_len(sym, 1); prev = sym; continue; }
+            uint32_t rep, l = 0;
+            if (sym == 16) { if (have == 0) { ok = false; break; } l = prev; rep = 3 + r.get(2); }
+            else if (sym == 17) rep = 3 + r.get(3);
+            else rep = 11 + r.get(7);
+            if (have + rep > total) { ok = false; break; }
+            put_len(l, rep);
+            prev = l;
+        }
+        if (ok) ok = l256 != 0 && lk <= 32768u && dk <= 32768u && (lk == 32768u || lmax == 1) &&
+                     (dk == 32768u || dmax <= 1) && r.pos <= 8 * n;
+    }
+    if (ok) {
+        const uint32_t k = atomicAdd(cnt, 1u);
+        if (k < cap) out[k] = b;
+    }
+}
+
+// k_infl_sym: one workgroup per block of the chain.  The block's output
+// [o0, o1) holds its literals (k_inflate_decode wrote them); its matches
+// (records pos | len << 32 | dist << 41, pos relative to o0 - hist) are
+// resolved in order through a 40 Ki-entry LDS ring of 32-bit symbols: a byte
+// b is 0x80000000 | b, a byte before o0 is its output position.  sym[o0, o1)
+// receives the block's symbols.
+struct ParBlk { uint64_t o0, o1, base, moff; uint32_t nm, pad; };
+constexpr uint32_t kSWin = 40960;
+__global__ __launch_bounds__(64) void k_infl_sym(const uint8_t *out, uint32_t *sym, const ParBlk *blks,
+                                                 const uint64_t *mrec) {
+    __shared__ uint32_t W[kSWin];
+    const int lane = threadIdx.x;
+    const ParBlk B = blks[blockIdx.x];
+    if (B.nm == 0) return;
+    const uint64_t *M = mrec + B.moff;
+    const uint32_t o0 = (uint32_t)B.o0, o1 = (uint32_t)B.o1, base = (uint32_t)B.base, nm = B.nm;
+    auto slot = [](uint32_t p) { return p % kSWin; };
+    uint32_t loaded = o0, done = o0, mi = 0, mbase = 0;
+    uint64_t mreg = (uint32_t)lane < nm ? M[lane] : 0;
+    for (uint32_t c0 = o0; c0 < o1 && mi < nm; c0 += kChunk) {
+        const uint32_t c1 = c0 + kChunk < o1 ? c0 + kChunk : o1;
+        const uint32_t want = c1 + 258 < o1 ? c1 + 258 : o1;
+        for (uint32_t p = loaded + (uint32_t)lane; p < want; p += 64) W[slot(p)] = 0x80000000u | out[p];
+        loaded = want;
+        __syncthreads();
+        while (mi < nm) {
+            if (mi - mbase >= 64) {
+                mbase = mi;
+                mreg = mbase + (uint32_t)lane < nm ? M[mbase + lane] : 0;
+            }
+            const int k = (int)(mi - mbase);
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mreg, k);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mreg >> 32), k);
+            const uint32_t pos = base + lo;
+            if (pos >= c1) break;
+            const uint32_t len = hi & 511u, dist = hi >> 9;
+            const uint32_t s0 = pos - dist;
+            // every source is before pos (j % dist when the match overlaps itself)
+            for (uint32_t j = (uint32_t)lane; j < len; j += 64) {
+                const uint32_t s = dist >= len ? s0 + j : s0 + j % dist;
+                W[slot(pos + j)] = s < o0 ? s : W[slot(s)];
+            }
+            mi++;
+        }
+        __syncthreads();
+        for (uint32_t p = c0 + (uint32_t)lane; p < c1; p += 64) sym[p] = W[slot(p)];
+        done = c1;
+        __syncthreads();
+    }
+    // the last chunk's overhang (tails of its matches), then literals only
+    for (uint32_t p = done + (uint32_t)lane; p < loaded; p += 64) sym[p] = W[slot(p)];
+    for (uint32_t p = loaded + (uint32_t)lane; p < o1; p += 64) sym[p] = 0x80000000u | out[p];
+}
+
+// k_infl_resolve: one block's symbols into bytes; its references point before
+// the block, whose bytes the launches before this one made final.
+__global__ __launch_bounds__(256) void k_infl_resolve(uint8_t *out, const uint32_t *sym, uint64_t o0, uint64_t o1) {
+    const uint64_t p = o0 + (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= o1) return;
+    const uint32_t v = sym[p];
+    out[p] = (v & 0x80000000u) ? (uint8_t)v : out[v];
+}
+
+int launch_infl_scan1(const uint8_t *in, uint64_t n, uint64_t b0, uint64_t b1, uint64_t *list, uint32_t cap,
+                      uint32_t *cnt, hipStream_t st) {
+    if (b1 <= b0) return 0;
+    hipLaunchKernelGGL(k_infl_scan1, dim3((unsigned)((b1 - b0 + 255) / 256)), dim3(256), 0, st, in, n, b0, b1, list,
+                       cap, cnt);
+    return (int)hipGetLastError();
+}
+int launch_infl_scan2(const uint8_t *in, uint64_t n, const uint64_t *list, uint32_t count, uint64_t *out,
+                      uint32_t cap, uint32_t *cnt, hipStream_t st) {
+    if (count == 0) return 0;
+    hipLaunchKernelGGL(k_infl_scan2, dim3((count + 255) / 256), dim3(256), 0, st, in, n, list, count, out, cap, cnt);
+    return (int)hipGetLastError();
+}
+int launch_infl_sym(const uint8_t *out, uint32_t *sym, const void *blks, uint32_t nblk, const uint64_t *mrec,
+                    hipStream_t st) {
+    if (nblk == 0) return 0;
+    hipLaunchKernelGGL(k_infl_sym, dim3(nblk), dim3(64), 0, st, out, sym, (const ParBlk *)blks, mrec);
+    return (int)hipGetLastError();
+}
+int launch_infl_resolve(uint8_t *out, const uint32_t *sym, uint64_t o0, uint64_t o1, hipStream_t st) {
+    if (o1 <= o0) return 0;
+    hipLaunchKernelGGL(k_infl_resolve, dim3((unsigned)((o1 - o0 + 255) / 256)), dim3(256), 0, st, out, sym, o0, o1);
+    return (int)hipGetLastError();
 }
 
 int launch_inflate_stage(int stage, const InflateJob &job, hipStream_t st) {
