@@ -252,7 +252,7 @@ struct Ctx {
     DevBuf ws_mrec, ws_irec, ws_ick, ws_imeta, ws_istop;
     // the block-parallel decode of a lone stream (inflate_par): candidate lists,
     // per-block jobs and records, output symbols
-    DevBuf ws_par1, ws_par2, ws_pjob, ws_psym;
+    DevBuf ws_par1, ws_par2, ws_pjob, ws_psym, ws_pslot;
     hipStream_t aux = nullptr;
     hipEvent_t ev_links[2] = {nullptr, nullptr}, ev_match[2] = {nullptr, nullptr};
     // pinned host staging of single small crc32()/adler32() calls (checksum_small)
@@ -1154,41 +1154,51 @@ int inflate_par_locked(Ctx &c, const uint8_t *in, uint64_t n, uint8_t *out, uint
     std::vector<uint64_t> cand(k2);
     if (k2 && copy_sync(cand.data(), l2, 8ull * k2, hipMemcpyDeviceToHost, st) != hipSuccess) return -1;
     std::sort(cand.begin(), cand.end());
-    // ---- count-only decodes: where each candidate block ends, what it makes
-    struct Span { uint64_t end; uint64_t out; uint32_t stop, last; };
-    auto spans = [&](const std::vector<uint64_t> &bits, std::vector<Span> &res) -> int {
+    // ---- every candidate decoded once, each in a slot of its own: where it ends, what it makes.
+    // Slot k holds the block's literals at [k * kSlot + 32 KiB, +kSlot) behind a pretend 32 KiB
+    // window (so no distance stops it; k_infl_sym checks them against the real output) and its
+    // matches as records.  A block longer than its slot, or one the scan missed, is measured
+    // count-only and decoded in place below.
+    constexpr uint64_t kSlot = 256 * 1024, kSlotRec = kSlot / 3 + 2;
+    struct Span { uint64_t end, out; uint32_t stop, last, nm; int64_t slot; };
+    uint8_t *slots = nullptr;
+    uint64_t *mrec = nullptr;
+    auto spans = [&](const std::vector<uint64_t> &bits, std::vector<Span> &res, bool write) -> int {
         const uint32_t K = (uint32_t)bits.size();
-        res.assign(K, Span{0, 0, kIData, 0});
+        res.assign(K, Span{0, 0, kIData, 0, 0, -1});
         if (K == 0) return 0;
-        // per job: src_off src_len res_bit dst_off dst_cap dst_len blk_out[2] zstate[2] | res_hist | status | rec
-        const size_t bytes = 8ull * K * 10 + 4ull * K * 2 + sizeof(InflateRec) * K + 256;
+        // per job: src_off src_len res_bit dst_off dst_cap dst_len blk_out[2] zstate[2] mrec_off | res_hist |
+        // status | rec
+        const size_t bytes = 8ull * K * 11 + 4ull * K * 2 + sizeof(InflateRec) * K + 256;
         if (!c.ws_pjob.ensure(bytes)) return -1;
         uint64_t *d = c.ws_pjob.as<uint64_t>();
         uint64_t *soff = d, *slen = d + K, *rbit = d + 2 * K, *doff = d + 3 * K, *dcap = d + 4 * K, *dlen = d + 5 * K;
-        uint64_t *blk = d + 6 * K, *zs = d + 8 * K;
-        uint32_t *hist = reinterpret_cast<uint32_t *>(d + 10 * K);
+        uint64_t *blk = d + 6 * K, *zs = d + 8 * K, *mo = d + 10 * K;
+        uint32_t *hist = reinterpret_cast<uint32_t *>(d + 11 * K);
         int32_t *stv = reinterpret_cast<int32_t *>(hist + K);
         InflateRec *rec = reinterpret_cast<InflateRec *>((reinterpret_cast<uintptr_t>(stv + K) + 63) & ~(uintptr_t)63);
-        std::vector<uint64_t> zero(K, 0), nn(K, n);
+        std::vector<uint64_t> zero(K, 0), nn(K, n), dof(K), cp(K, 32768 + kSlot), mof(K);
         std::vector<uint32_t> hh(K, 32768u);
+        for (uint32_t k = 0; k < K; k++) { dof[k] = write ? k * kSlot : 0; mof[k] = write ? k * kSlotRec : 0; }
         if (hipMemcpyAsync(soff, zero.data(), 8ull * K, hipMemcpyHostToDevice, st) != hipSuccess ||
             hipMemcpyAsync(slen, nn.data(), 8ull * K, hipMemcpyHostToDevice, st) != hipSuccess ||
             hipMemcpyAsync(rbit, bits.data(), 8ull * K, hipMemcpyHostToDevice, st) != hipSuccess ||
-            hipMemcpyAsync(doff, zero.data(), 8ull * K, hipMemcpyHostToDevice, st) != hipSuccess ||
-            hipMemcpyAsync(dcap, zero.data(), 8ull * K, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(doff, dof.data(), 8ull * K, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(dcap, cp.data(), 8ull * K, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(mo, mof.data(), 8ull * K, hipMemcpyHostToDevice, st) != hipSuccess ||
             hipMemcpyAsync(hist, hh.data(), 4ull * K, hipMemcpyHostToDevice, st) != hipSuccess)
             return -1;
         InflateJob job{};
         job.src = in; job.src_off = soff; job.src_len = slen;
-        job.dst = out; job.dst_off = doff; job.dst_cap = dcap; job.dst_len = dlen;
+        job.dst = write ? slots : out; job.dst_off = doff; job.dst_cap = dcap; job.dst_len = dlen;
         job.status = stv; job.first = 0; job.count = K; job.wrap = 0;
-        job.mrec_off = soff; job.mrec = nullptr;
+        job.mrec_off = mo; job.mrec = write ? mrec : nullptr;
         job.rec = rec;
         job.res_bit = rbit; job.res_hist = hist; job.blk_out = blk;
         job.stop_mode = 2 | 4;                   // stop at the block's end (the last one's too), start in TYPE
         job.zstate_out = zs;                     // bit 32: BFINAL of the block
-        job.count_only = 1;
-        if (launch_inflate_stage(0, job, st)) return -1;
+        job.count_only = write ? 0 : 1;
+        if (c.timer.run(3, st, [&] { return launch_inflate_stage(0, job, st); })) return -1;
         std::vector<InflateRec> r(K);
         std::vector<uint64_t> bo(2ull * K), z(2ull * K);
         if (copy_sync(r.data(), rec, sizeof(InflateRec) * K, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -1200,29 +1210,38 @@ int inflate_par_locked(Ctx &c, const uint8_t *in, uint64_t n, uint8_t *out, uint
             res[k].last = (z[2ull * k] >> 32) & 1u;
             res[k].out = r[k].put >= 32768 ? r[k].put - 32768 : 0;
             res[k].end = bo[2ull * k];           // the bit after its END_BLOCK code
+            res[k].nm = r[k].nmatch;
+            res[k].slot = write ? (int64_t)k : -1;
         }
         return 0;
     };
+    const bool write = (uint64_t)cand.size() * kSlot <= (4ull << 30);    // slots for every candidate fit 4 GiB
+    if (write) {
+        if (!c.ws_pslot.ensure(cand.size() * kSlot + 32768 + 64) || !c.ws_mrec.ensure(8 * cand.size() * kSlotRec + 64))
+            return -1;
+        slots = c.ws_pslot.as<uint8_t>();
+        mrec = c.ws_mrec.as<uint64_t>();
+    }
     std::vector<Span> sp;
-    if (spans(cand, sp)) return -1;
+    if (spans(cand, sp, write)) return -1;
     // ---- the chain of blocks from the first one
-    struct Blk { uint64_t bit, o0, out; bool last; };
+    struct Blk { uint64_t bit, o0, out; bool last; uint32_t nm; int64_t slot; };
     std::vector<Blk> chain;
     uint64_t b = b0, total = 0;
     int misses = 0;
     for (;;) {
         const auto it = std::lower_bound(cand.begin(), cand.end(), b);
         Span s;
-        if (it != cand.end() && *it == b) {
-            s = sp[(size_t)(it - cand.begin())];
-        } else {                                    // a fixed-code block (or a stored one the scan missed)
+        if (it != cand.end() && *it == b) s = sp[(size_t)(it - cand.begin())];
+        if (!(it != cand.end() && *it == b) || s.stop == kIFull) {
+            // a fixed-code block (or a stored one the scan missed), or one longer than its slot
             if (++misses > 16) return 0;
             std::vector<Span> one;
-            if (spans(std::vector<uint64_t>{b}, one)) return -1;
+            if (spans(std::vector<uint64_t>{b}, one, false)) return -1;
             s = one[0];
         }
         if (s.stop != kIBlock || s.end <= b) return 0;
-        chain.push_back(Blk{b, total, s.out, s.last != 0});
+        chain.push_back(Blk{b, total, s.out, s.last != 0, s.nm, s.slot});
         total += s.out;
         if (total > cap) return 0;
         b = s.end;
@@ -1231,65 +1250,94 @@ int inflate_par_locked(Ctx &c, const uint8_t *in, uint64_t n, uint8_t *out, uint
     const uint64_t tb = (b + 7) >> 3;               // the trailer's first byte (inflate.c CHECK: BYTEBITS)
     const uint64_t tlen = kind == 1 ? 4 : kind == 2 ? 8 : 0;
     if (tb + tlen > n) return 0;
-    // ---- every block at its output offset: literals in place, matches as records
-    const uint32_t NB = (uint32_t)chain.size();
-    std::vector<uint64_t> soff(NB, 0), slen(NB, n), rbit(NB), doff(NB), dcap(NB), moff(NB);
-    std::vector<uint32_t> hist(NB);
+    // ---- blocks without a slot: decoded at their output offset, literals in place, matches as records
+    // after the slots' records
+    std::vector<uint32_t> ip;                        // chain indexes of those blocks
+    for (uint32_t k = 0; k < (uint32_t)chain.size(); k++)
+        if (chain[k].slot < 0) ip.push_back(k);
+    const uint32_t NB = (uint32_t)ip.size();
+    std::vector<uint64_t> moff(NB), hist(NB);
     uint64_t mtot = 0;
-    for (uint32_t k = 0; k < NB; k++) {
-        const Blk &B = chain[k];
-        hist[k] = (uint32_t)std::min<uint64_t>(32768, B.o0);
-        rbit[k] = B.bit;
-        doff[k] = B.o0 - hist[k];
-        dcap[k] = hist[k] + B.out;
-        moff[k] = mtot;
-        mtot += B.out / 3 + 2;
+    for (uint32_t j = 0; j < NB; j++) {
+        hist[j] = std::min<uint64_t>(32768, chain[ip[j]].o0);
+        moff[j] = mtot;
+        mtot += chain[ip[j]].out / 3 + 2;
     }
-    const size_t jb = 8ull * NB * 9 + 4ull * NB * 2 + sizeof(InflateRec) * NB + 256;
-    if (!c.ws_pjob.ensure(jb) || !c.ws_mrec.ensure(8 * mtot + 64) || !c.ws_psym.ensure(4 * total + 64)) return -1;
-    uint64_t *d = c.ws_pjob.as<uint64_t>();
-    uint64_t *d_soff = d, *d_slen = d + NB, *d_rbit = d + 2 * NB, *d_doff = d + 3 * NB, *d_dcap = d + 4 * NB;
-    uint64_t *d_dlen = d + 5 * NB, *d_blk = d + 6 * NB, *d_moff = d + 8 * NB;
-    uint32_t *d_hist = reinterpret_cast<uint32_t *>(d + 9 * NB);
-    int32_t *d_stv = reinterpret_cast<int32_t *>(d_hist + NB);
-    InflateRec *d_rec = reinterpret_cast<InflateRec *>((reinterpret_cast<uintptr_t>(d_stv + NB) + 63) & ~(uintptr_t)63);
-    if (hipMemcpyAsync(d_soff, soff.data(), 8ull * NB, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_slen, slen.data(), 8ull * NB, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_rbit, rbit.data(), 8ull * NB, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_doff, doff.data(), 8ull * NB, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_dcap, dcap.data(), 8ull * NB, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_moff, moff.data(), 8ull * NB, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_hist, hist.data(), 4ull * NB, hipMemcpyHostToDevice, st) != hipSuccess)
-        return -1;
-    InflateJob job{};
-    job.src = in; job.src_off = d_soff; job.src_len = d_slen;
-    job.dst = out; job.dst_off = d_doff; job.dst_cap = d_dcap; job.dst_len = d_dlen;
-    job.status = d_stv; job.first = 0; job.count = NB; job.wrap = 0;
-    job.mrec_off = d_moff; job.mrec = c.ws_mrec.as<uint64_t>();
-    job.rec = d_rec;
-    job.res_bit = d_rbit; job.res_hist = d_hist; job.blk_out = d_blk;
-    job.stop_mode = 2 | 4;
-    if (c.timer.run(3, st, [&] { return launch_inflate_stage(0, job, st); })) return -1;
-    std::vector<InflateRec> r(NB);
-    if (copy_sync(r.data(), d_rec, sizeof(InflateRec) * NB, hipMemcpyDeviceToHost, st) != hipSuccess) return -1;
-    std::vector<ParBlkHost> pb;
-    for (uint32_t k = 0; k < NB; k++) {
-        const Blk &B = chain[k];
-        if (r[k].put != hist[k] + B.out || r[k].stop != (uint32_t)kIBlock) return 0;
-        if (r[k].nmatch) pb.push_back(ParBlkHost{B.o0, B.o0 + B.out, B.o0 - hist[k], moff[k], r[k].nmatch, 0});
+    // their records in a buffer of their own (the slots' stay where the candidates' decode put them)
+    if (!c.ws_par2.ensure(8 * mtot + 64) || !c.ws_psym.ensure(4 * total + 64)) return -1;
+    uint64_t *mrec_ip = c.ws_par2.as<uint64_t>();
+    if (NB) {
+        std::vector<uint64_t> soff(NB, 0), slen(NB, n), rbit(NB), doff(NB), dcap(NB);
+        std::vector<uint32_t> h32(NB);
+        for (uint32_t j = 0; j < NB; j++) {
+            const Blk &B = chain[ip[j]];
+            h32[j] = (uint32_t)hist[j];
+            rbit[j] = B.bit;
+            doff[j] = B.o0 - hist[j];
+            dcap[j] = hist[j] + B.out;
+        }
+        const size_t jb = 8ull * NB * 9 + 4ull * NB * 2 + sizeof(InflateRec) * NB + 256;
+        if (!c.ws_pjob.ensure(jb)) return -1;
+        uint64_t *d = c.ws_pjob.as<uint64_t>();
+        uint64_t *d_soff = d, *d_slen = d + NB, *d_rbit = d + 2 * NB, *d_doff = d + 3 * NB, *d_dcap = d + 4 * NB;
+        uint64_t *d_dlen = d + 5 * NB, *d_blk = d + 6 * NB, *d_moff = d + 8 * NB;
+        uint32_t *d_hist = reinterpret_cast<uint32_t *>(d + 9 * NB);
+        int32_t *d_stv = reinterpret_cast<int32_t *>(d_hist + NB);
+        InflateRec *d_rec = reinterpret_cast<InflateRec *>((reinterpret_cast<uintptr_t>(d_stv + NB) + 63) & ~(uintptr_t)63);
+        if (hipMemcpyAsync(d_soff, soff.data(), 8ull * NB, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(d_slen, slen.data(), 8ull * NB, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(d_rbit, rbit.data(), 8ull * NB, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(d_doff, doff.data(), 8ull * NB, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(d_dcap, dcap.data(), 8ull * NB, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(d_moff, moff.data(), 8ull * NB, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(d_hist, h32.data(), 4ull * NB, hipMemcpyHostToDevice, st) != hipSuccess)
+            return -1;
+        InflateJob job{};
+        job.src = in; job.src_off = d_soff; job.src_len = d_slen;
+        job.dst = out; job.dst_off = d_doff; job.dst_cap = d_dcap; job.dst_len = d_dlen;
+        job.status = d_stv; job.first = 0; job.count = NB; job.wrap = 0;
+        job.mrec_off = d_moff; job.mrec = mrec_ip;
+        job.rec = d_rec;
+        job.res_bit = d_rbit; job.res_hist = d_hist; job.blk_out = d_blk;
+        job.stop_mode = 2 | 4;
+        if (c.timer.run(3, st, [&] { return launch_inflate_stage(0, job, st); })) return -1;
+        std::vector<InflateRec> r(NB);
+        if (copy_sync(r.data(), d_rec, sizeof(InflateRec) * NB, hipMemcpyDeviceToHost, st) != hipSuccess) return -1;
+        for (uint32_t j = 0; j < NB; j++) {
+            Blk &B = chain[ip[j]];
+            if (r[j].put != hist[j] + B.out || r[j].stop != (uint32_t)kIBlock) return 0;
+            B.nm = r[j].nmatch;
+        }
     }
     // ---- matches: symbols per block, then references block by block
+    std::vector<ParBlkHost> pb;
+    size_t j = 0;
+    for (const Blk &B : chain) {
+        if (B.slot >= 0) {                           // from its slot (copied even when literal-only)
+            pb.push_back(ParBlkHost{B.o0, B.o0 + B.out, B.o0 - 32768, (uint64_t)B.slot * kSlotRec,
+                                    (uint64_t)B.slot * kSlot + 32768, B.nm, 0});
+        } else {
+            if (B.nm) pb.push_back(ParBlkHost{B.o0, B.o0 + B.out, B.o0 - hist[j], moff[j], ~0ull, B.nm, 0});
+            j++;
+        }
+    }
     if (!pb.empty()) {
-        if (!c.ws_par1.ensure(sizeof(ParBlkHost) * pb.size() + 64)) return -1;
+        if (!c.ws_par1.ensure(sizeof(ParBlkHost) * pb.size() + 64) || !c.ws_imeta.ensure(64)) return -1;
         uint32_t *sym = c.ws_psym.as<uint32_t>();
+        uint32_t *err = reinterpret_cast<uint32_t *>(c.ws_imeta.as<uint64_t>() + 5);
+        uint32_t e_host = 0;
         if (hipMemcpyAsync(c.ws_par1.p, pb.data(), sizeof(ParBlkHost) * pb.size(), hipMemcpyHostToDevice, st) !=
                 hipSuccess ||
+            hipMemsetAsync(err, 0, 4, st) != hipSuccess ||
             c.timer.run(4, st, [&] {
-                int e = launch_infl_sym(out, sym, c.ws_par1.p, (uint32_t)pb.size(), c.ws_mrec.as<uint64_t>(), st);
-                for (size_t k = 0; !e && k < pb.size(); k++) e = launch_infl_resolve(out, sym, pb[k].o0, pb[k].o1, st);
+                int e = launch_infl_sym(out, slots, sym, c.ws_par1.p, (uint32_t)pb.size(), mrec, mrec_ip, err, st);
+                for (size_t k = 0; !e && k < pb.size(); k++)
+                    if (pb[k].nm) e = launch_infl_resolve(out, sym, pb[k].o0, pb[k].o1, st);
                 return e;
-            }))
+            }) ||
+            copy_sync(&e_host, err, 4, hipMemcpyDeviceToHost, st) != hipSuccess)
             return -1;
+        if (e_host) return 0;                        // a distance before the stream's start: the exact path reports it
     }
     // ---- the check value against the trailer
     uint8_t t[8] = {0};

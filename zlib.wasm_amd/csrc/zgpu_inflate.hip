@@ -871,29 +871,39 @@ __global__ __launch_bounds__(256) void k_infl_scan2(const uint8_t *in, uint64_t 
     }
 }
 
-// k_infl_sym: one workgroup per block of the chain.  The block's output
-// [o0, o1) holds its literals (k_inflate_decode wrote them); its matches
-// (records pos | len << 32 | dist << 41, pos relative to o0 - hist) are
-// resolved in order through a 40 Ki-entry LDS ring of 32-bit symbols: a byte
-// b is 0x80000000 | b, a byte before o0 is its output position.  sym[o0, o1)
-// receives the block's symbols.
-struct ParBlk { uint64_t o0, o1, base, moff; uint32_t nm, pad; };
+// k_infl_sym: one workgroup per block of the chain.  The block's output is
+// [o0, o1); its literals are in place (out) or, decoded in a candidate's slot,
+// at lit + (p - o0) (ParBlk::lit != ~0); its matches (records pos | len << 32 |
+// dist << 41, pos relative to o0 - base_hist) are resolved in order through a
+// 40 Ki-entry LDS ring of 32-bit symbols: a byte b is 0x80000000 | b, a byte
+// before o0 is its output position.  sym[o0, o1) receives the block's
+// symbols; a literal-only block from a slot is copied to out instead.  A match
+// reaching before the stream's first byte sets *err (inflate.c: "invalid
+// distance too far back"; the slot decode could not see it).
+struct ParBlk { uint64_t o0, o1, base, moff, lit; uint32_t nm, pad; };
 constexpr uint32_t kSWin = 40960;
-__global__ __launch_bounds__(64) void k_infl_sym(const uint8_t *out, uint32_t *sym, const ParBlk *blks,
-                                                 const uint64_t *mrec) {
+__global__ __launch_bounds__(64) void k_infl_sym(uint8_t *out, const uint8_t *slots, uint32_t *sym,
+                                                 const ParBlk *blks, const uint64_t *mrec_slots,
+                                                 const uint64_t *mrec_inplace, uint32_t *err) {
     __shared__ uint32_t W[kSWin];
     const int lane = threadIdx.x;
     const ParBlk B = blks[blockIdx.x];
-    if (B.nm == 0) return;
-    const uint64_t *M = mrec + B.moff;
     const uint32_t o0 = (uint32_t)B.o0, o1 = (uint32_t)B.o1, base = (uint32_t)B.base, nm = B.nm;
+    const bool inplace = B.lit == ~0ull;
+    const uint8_t *lit = inplace ? out + o0 : slots + B.lit;       // the block's byte p at lit[p - o0]
+    if (nm == 0) {
+        if (!inplace)
+            for (uint32_t p = o0 + (uint32_t)lane; p < o1; p += 64) out[p] = lit[p - o0];
+        return;
+    }
+    const uint64_t *M = (inplace ? mrec_inplace : mrec_slots) + B.moff;
     auto slot = [](uint32_t p) { return p % kSWin; };
-    uint32_t loaded = o0, done = o0, mi = 0, mbase = 0;
+    uint32_t loaded = o0, done = o0, mi = 0, mbase = 0, bad = 0;
     uint64_t mreg = (uint32_t)lane < nm ? M[lane] : 0;
     for (uint32_t c0 = o0; c0 < o1 && mi < nm; c0 += kChunk) {
         const uint32_t c1 = c0 + kChunk < o1 ? c0 + kChunk : o1;
         const uint32_t want = c1 + 258 < o1 ? c1 + 258 : o1;
-        for (uint32_t p = loaded + (uint32_t)lane; p < want; p += 64) W[slot(p)] = 0x80000000u | out[p];
+        for (uint32_t p = loaded + (uint32_t)lane; p < want; p += 64) W[slot(p)] = 0x80000000u | lit[p - o0];
         loaded = want;
         __syncthreads();
         while (mi < nm) {
@@ -907,11 +917,12 @@ __global__ __launch_bounds__(64) void k_infl_sym(const uint8_t *out, uint32_t *s
             const uint32_t pos = base + lo;
             if (pos >= c1) break;
             const uint32_t len = hi & 511u, dist = hi >> 9;
+            bad |= dist > pos;
             const uint32_t s0 = pos - dist;
             // every source is before pos (j % dist when the match overlaps itself)
             for (uint32_t j = (uint32_t)lane; j < len; j += 64) {
-                const uint32_t s = dist >= len ? s0 + j : s0 + j % dist;
-                W[slot(pos + j)] = s < o0 ? s : W[slot(s)];
+                const uint32_t s2 = dist >= len ? s0 + j : s0 + j % dist;
+                W[slot(pos + j)] = s2 < o0 ? s2 : W[slot(s2)];
             }
             mi++;
         }
@@ -922,7 +933,8 @@ __global__ __launch_bounds__(64) void k_infl_sym(const uint8_t *out, uint32_t *s
     }
     // the last chunk's overhang (tails of its matches), then literals only
     for (uint32_t p = done + (uint32_t)lane; p < loaded; p += 64) sym[p] = W[slot(p)];
-    for (uint32_t p = loaded + (uint32_t)lane; p < o1; p += 64) sym[p] = 0x80000000u | out[p];
+    for (uint32_t p = loaded + (uint32_t)lane; p < o1; p += 64) sym[p] = 0x80000000u | lit[p - o0];
+    if (bad && lane == 0) atomicOr(err, 1u);
 }
 
 // k_infl_resolve: one block's symbols into bytes; its references point before
@@ -947,10 +959,11 @@ int launch_infl_scan2(const uint8_t *in, uint64_t n, const uint64_t *list, uint3
     hipLaunchKernelGGL(k_infl_scan2, dim3((count + 255) / 256), dim3(256), 0, st, in, n, list, count, out, cap, cnt);
     return (int)hipGetLastError();
 }
-int launch_infl_sym(const uint8_t *out, uint32_t *sym, const void *blks, uint32_t nblk, const uint64_t *mrec,
-                    hipStream_t st) {
+int launch_infl_sym(uint8_t *out, const uint8_t *slots, uint32_t *sym, const void *blks, uint32_t nblk,
+                    const uint64_t *mrec_slots, const uint64_t *mrec_inplace, uint32_t *err, hipStream_t st) {
     if (nblk == 0) return 0;
-    hipLaunchKernelGGL(k_infl_sym, dim3(nblk), dim3(64), 0, st, out, sym, (const ParBlk *)blks, mrec);
+    hipLaunchKernelGGL(k_infl_sym, dim3(nblk), dim3(64), 0, st, out, slots, sym, (const ParBlk *)blks, mrec_slots,
+                       mrec_inplace, err);
     return (int)hipGetLastError();
 }
 int launch_infl_resolve(uint8_t *out, const uint32_t *sym, uint64_t o0, uint64_t o1, hipStream_t st) {

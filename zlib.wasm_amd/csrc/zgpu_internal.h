@@ -362,13 +362,13 @@ struct InflateJob {
 };
 int launch_inflate_stage(int stage, const InflateJob &job, hipStream_t st);
 // the block-parallel decode of a lone stream (zgpu_inflate.hip, zgpu_api.cpp inflate_par)
-struct ParBlkHost { uint64_t o0, o1, base, moff; uint32_t nm, pad; };   // = zgpu_inflate.hip ParBlk
+struct ParBlkHost { uint64_t o0, o1, base, moff, lit; uint32_t nm, pad; };   // = zgpu_inflate.hip ParBlk
 int launch_infl_scan1(const uint8_t *in, uint64_t n, uint64_t b0, uint64_t b1, uint64_t *list, uint32_t cap,
                       uint32_t *cnt, hipStream_t st);
 int launch_infl_scan2(const uint8_t *in, uint64_t n, const uint64_t *list, uint32_t count, uint64_t *out,
                       uint32_t cap, uint32_t *cnt, hipStream_t st);
-int launch_infl_sym(const uint8_t *out, uint32_t *sym, const void *blks, uint32_t nblk, const uint64_t *mrec,
-                    hipStream_t st);
+int launch_infl_sym(uint8_t *out, const uint8_t *slots, uint32_t *sym, const void *blks, uint32_t nblk,
+                    const uint64_t *mrec_slots, const uint64_t *mrec_inplace, uint32_t *err, hipStream_t st);
 int launch_infl_resolve(uint8_t *out, const uint32_t *sym, uint64_t o0, uint64_t o1, hipStream_t st);
 
 // launchers (return hipError_t as int)
