@@ -147,3 +147,32 @@ def test_random_inflate_small_output_vs_system_zlib(zg, block):
         if rz[1] != rg[1] or rz[2] != rg[2] or rz[0][-1][-1] != rg[0][-1][-1]:
             bad.append((k, len(z), ops[:3], rz[0][-1][-1:], rg[0][-1][-1:]))
     assert not bad, bad[:3]
+
+
+@pytest.mark.parametrize("block", range(3))
+def test_random_batches_vs_system_zlib(zg, block):
+    """The batched hot path (zgpu_compress_batch2) on random batches: 200-1500
+    buffers of 0 bytes to 300 KB from every generator kind, one random setting
+    per batch (level 1-9, strategy 0-3, zlib / raw / gzip, windowBits 9-15,
+    memLevel 1-9); every stream equal to system zlib's (compressobj with the
+    same parameters)."""
+    import zlib as pyzlib
+    rng = random.Random(99 + block)
+    for _ in range(4):
+        level = rng.randint(1, 9)
+        strategy = rng.choice((0, 0, 1, 2, 3))
+        wb = rng.choice((15, 15, 9, 12, 14))
+        wbits = rng.choice((wb, -wb, wb + 16))
+        mem = rng.choice((8, 8, 1, 4, 9))
+        count = rng.randint(200, 1500)
+        bufs = [datagen.make(rng.choice(KINDS), rng.choice((0, 1, 2, 3, 100, 5000, 70000, 300000,
+                                                            rng.randint(0, 300000))), rng.randint(0, 10 ** 6))
+                for _ in range(count)]
+        got = zg.compress_batch2(bufs, level=level, window_bits=wbits, mem_level=mem, strategy=strategy)
+        bad = []
+        for i, (b, (st, z)) in enumerate(zip(bufs, got)):
+            c = pyzlib.compressobj(level, pyzlib.DEFLATED, wbits, mem, strategy)
+            want = c.compress(b) + c.flush()
+            if st != 0 or z != want:
+                bad.append((i, len(b), st, len(z), len(want)))
+        assert not bad, (level, strategy, wbits, mem, count, bad[:5])
