@@ -1065,7 +1065,7 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
 // match records (a match writes >= 3 bytes, the last one may be cut short).
 // stop_out (device, optional): InflateStop per stream.
 // ------------------------------------------------------------------------
-constexpr uint64_t kParInflateMin = 256 * 1024;   // inflate_par: lone streams from this many compressed bytes
+constexpr uint64_t kParInflateMin = 32 * 1024;    // inflate_par: lone streams from this many compressed bytes (tools/par_threshold.py)
 struct InflateResumeDev {          // InflateJob's resume arrays (device, per stream)
     const uint64_t *res_bit;
     const uint32_t *res_hist;
