@@ -463,6 +463,16 @@ def run_zsession(L, ops, version=b"1.3.1.1-motley"):
                 if rc < 0 or rc == 1 or (s.avail_in == 0 and s.avail_out != 0):
                     break
             rcs.append(seq)
+        elif k == "deflate1":                    # ONE call with `out` bytes of space (a flush may stay pending)
+            data, flush, n = op[1], op[2], op[3]
+            ib = C.create_string_buffer(data, len(data))
+            keep.append(ib)
+            s.next_in, s.avail_in = C.addressof(ib), len(data)
+            ob = C.create_string_buffer(max(n, 1))
+            s.next_out, s.avail_out = C.addressof(ob), n
+            rc = L.deflate(C.byref(s), flush)
+            out.extend(ob.raw[: n - s.avail_out])
+            rcs.append([rc, s.avail_in, s.avail_out])
         elif k == "bound":
             rcs.append(int(L.deflateBound(C.byref(s), op[1])))
         elif k == "used":                        # deflateUsed
