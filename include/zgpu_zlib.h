@@ -28,8 +28,10 @@
  * deflate_stored's blocks as its first loop cuts them (a small avail_out that
  * makes the reference cut shorter blocks is not modelled).  After Z_FINISH the
  * caller continues with Z_FINISH until Z_STREAM_END (zlib.h); a flush call
- * that ran out of output space is repeated with the same flush (zlib.h) --
- * given more input instead, the stream stays valid but may differ.
+ * that ran out of output space and is given more input instead of the same
+ * flush again goes on as the reference does (tests/test_gpu_fuzz.py), except
+ * when a preset dictionary's 6-byte zlib header takes all of the first call's
+ * output space: the stream stays valid but may differ.
  * deflateSetDictionary, deflateSetHeader, deflatePrime, deflateTune and
  * deflateParams give the reference's stream: deflateParams flushes with Z_BLOCK
  * itself when the level's function or the strategy changes (as deflate.c does)

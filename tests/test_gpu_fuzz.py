@@ -78,14 +78,12 @@ def _pending_session(rng):
     return ops
 
 
-@pytest.mark.parametrize("block", [0, pytest.param(1, marks=pytest.mark.xfail(
-    reason="documented gap (DESIGN.md 4.10): a call whose output space is already full when deflate_slow "
-           "starts stops at the first lazy literal (need_more) and its flush never happens; the engine "
-           "applies the flush", strict=False))])
+@pytest.mark.parametrize("block", range(4))
 def test_random_pending_flush_sessions_vs_system_zlib(zg, block):
     """Every single call's status / avail_in / avail_out and the stream.
     Seed block 1 holds session 21: a gzip stream whose first Z_BLOCK call
-    gets exactly the 10 header bytes of output space."""
+    gets exactly the 10 header bytes of output space (see
+    test_first_call_output_space_is_the_header)."""
     libz = _system_zlib()
     L = zg.load()
     rng = random.Random(3131 + block)
@@ -216,3 +214,41 @@ def test_random_batches_vs_system_zlib(zg, block):
             if st != 0 or z != want:
                 bad.append((i, len(b), st, len(z), len(want)))
         assert not bad, (level, strategy, wbits, mem, count, bad[:5])
+
+
+def _header_sessions():
+    """First calls whose output space is exactly the header (zlib 2 bytes,
+    gzip 10): the compress function then runs with no output space."""
+    S = []
+    data = b"".join(datagen.make(k, 40000, 77) for k in ("text", "mix", "runs"))
+    for level in (1, 3, 4, 6, 9):
+        for strategy in (0, 2, 3):
+            for wbits, hl in ((15, 2), (31, 10)):
+                for n in (0, 1, 2, 5000, 100000):
+                    for flush in (0, 1, 2, 3, 4, 5):
+                        # the calls after the first re-present what it left (zlib.h: next_in / avail_in);
+                        # after Z_FINISH only Z_FINISH follows, with no new input (zlib.h)
+                        fin = flush == 4
+                        S.append([["init", level, wbits, 8, strategy], ["deflate1", data[:n], flush, hl],
+                                  ["deflate1", b"", flush, 7, True],
+                                  ["deflate", b"" if fin else data[n:n + 3000], 4 if fin else 2, None, True],
+                                  ["deflate", b"" if fin else data[n + 3000:n + 9000], 4]])
+    return S
+
+
+def test_first_call_output_space_is_the_header(zg):
+    """deflate_slow stops at its first lazy literal and the call's flush never
+    happens; one byte, or deflate_fast / _huff / _rle, cut the block without
+    the flush's marker; fill_window reads at most window_size bytes (the
+    100000-byte calls).  Every call's status / avail_in / avail_out and the
+    stream equal system zlib's."""
+    libz = _system_zlib()
+    L = zg.load()
+    bad = []
+    for k, ops in enumerate(_header_sessions()):
+        rz, z = run_zsession(libz, ops)
+        rg, g = run_zsession(L, ops)
+        if rz != rg or z != g:
+            bad.append((k, ops[0], [len(ops[1][1]), ops[1][2]], rz, rg, len(z), len(g)))
+    kinds = sorted({(b[1][1], b[1][4], b[1][2], b[2][0], b[2][1]) for b in bad})
+    assert not bad, (len(bad), kinds[:20], bad[:2])

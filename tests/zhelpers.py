@@ -404,6 +404,7 @@ def run_zsession(L, ops, version=b"1.3.1.1-motley"):
     _bind_zstream(L)
     s = ZStream()
     out, rcs, keep = bytearray(), [], []
+    left = b""                                   # input the last "deflate1" call did not take
     obuf_n = 1 << 16
 
     def with_out(call, extra=0):
@@ -442,11 +443,13 @@ def run_zsession(L, ops, version=b"1.3.1.1-motley"):
             rcs.append(L.deflateSetHeader(C.byref(s), C.byref(h)))
         elif k == "deflate":
             data, flush = op[1], op[2]
+            if len(op) > 4 and op[4]:
+                data = left + data
             ib = C.create_string_buffer(data, len(data))
             keep.append(ib)
             s.next_in, s.avail_in = C.addressof(ib), len(data)
             seq = []
-            if len(op) > 3:                      # small output buffers: one call per `out` bytes
+            if len(op) > 3 and op[3]:            # small output buffers: one call per `out` bytes
                 ob = C.create_string_buffer(op[3])
                 for _ in range(200000):
                     s.next_out, s.avail_out = C.addressof(ob), op[3]
@@ -465,6 +468,8 @@ def run_zsession(L, ops, version=b"1.3.1.1-motley"):
             rcs.append(seq)
         elif k == "deflate1":                    # ONE call with `out` bytes of space (a flush may stay pending)
             data, flush, n = op[1], op[2], op[3]
+            if len(op) > 4 and op[4]:            # "cont": the input the last call left comes first (zlib.h)
+                data = left + data
             ib = C.create_string_buffer(data, len(data))
             keep.append(ib)
             s.next_in, s.avail_in = C.addressof(ib), len(data)
@@ -473,6 +478,7 @@ def run_zsession(L, ops, version=b"1.3.1.1-motley"):
             rc = L.deflate(C.byref(s), flush)
             out.extend(ob.raw[: n - s.avail_out])
             rcs.append([rc, s.avail_in, s.avail_out])
+            left = data[len(data) - s.avail_in:] if s.avail_in else b""
         elif k == "bound":
             rcs.append(int(L.deflateBound(C.byref(s), op[1])))
         elif k == "used":                        # deflateUsed

@@ -3053,7 +3053,7 @@ static int deflate_body(z_streamp strm, int flush) {
         return Z_STREAM_END;
     }
     const size_t C = s->in_base + s->in.size();                // part position of the input copied so far
-    const size_t P = s->rd + strm->avail_in;                   // the input this call offers ends here
+    size_t P = s->rd + strm->avail_in;                         // the input this call offers ends here
     // 32-bit kernel positions (level 0 cuts its own jobs: deflate_stored_call)
     if (s->level != 0 && P > C && (uint64_t)(P - s->in_base) >= kMaxBuffer) return Z_MEM_ERROR;
 
@@ -3104,12 +3104,37 @@ static int deflate_body(z_streamp strm, int flush) {
             return Z_STREAM_END;
         }
     }
+    bool force_skip = false;
     if (!s->header_done) {                                      // deflate.c:1002-1073
         queue_header(s);
         drain(strm, s);
         if (s->out_pos < s->out.size()) {
             s->last_flush = -1;
             return Z_OK;
+        }
+        // The header took the last byte of output space, so the compress
+        // function runs with avail_out == 0 (a call that starts with none gets
+        // Z_BUF_ERROR, and pending output that fills it returns before; only the
+        // header's call gets here).  deflate_slow stops at its first lazy literal
+        // (need_more, at strstart 2 with no history): the call's flush never
+        // happens, and fill_window has read at most window_size bytes.  With one
+        // byte, and for deflate_fast / _huff / _rle, the input's end is reached:
+        // FLUSH_BLOCK cuts the block and returns need_more before the flush's
+        // marker.  Without input the flush goes ahead (its marker waits).
+        const size_t avail = P - s->rd;
+        const bool slow_fn = s->level >= 4 && s->strategy != Z_HUFFMAN_ONLY && s->strategy != Z_RLE;
+        if (strm->avail_out == 0 && s->level != 0 && !s->dict_set) {
+            // whatever the compress function returns then (need_more, or a marker
+            // left pending), deflate() leaves with last_flush = -1: the next call
+            // with no input is no Z_BUF_ERROR
+            if (avail > 0 || flush != Z_NO_FLUSH) s->last_flush = -1;
+            if (avail > 0 && slow_fn && avail >= 2) {
+                P = std::min<size_t>(P, s->rd + (size_t(2) << s->wbits));
+                flush = Z_NO_FLUSH;
+                force_skip = true;
+            } else if (avail > 0 && flush != Z_NO_FLUSH && flush != Z_FINISH) {
+                flush = Z_BLOCK;
+            }
         }
     }
     if (s->level == 0) return deflate_stored_call(strm, s, flush);
@@ -3188,7 +3213,7 @@ static int deflate_body(z_streamp strm, int flush) {
             for (size_t k = s->t; k-- > 0;)
                 if (s->items[k].kind != kItStop) { x0 = (size_t)s->items[k].in_end; break; }
             const size_t sym_limit = ((size_t)1 << (s->mem_level + 6)) - 1;
-            skip = P < x0 + sym_limit;
+            skip = force_skip || P < x0 + sym_limit;
         }
         if (skip) {
             s->rd = P;
