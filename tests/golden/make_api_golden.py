@@ -128,6 +128,14 @@ def inflate_sessions():
     S.append({"name": "validate-pieces", "spec": {"data": ["mix", 80000, 68], "fmt": "zlib", "xor_tail": 1},
               "ops": [["init", 15], ["validate", 0]] + [["feed", 9000], ["inflate", Z_NO_FLUSH, 1 << 20]] * 12 +
                      [["adler"]]})
+    # inflateReset2 turns the check back on after inflateValidate(0) (inflate.c:157,
+    # wrap = (windowBits >> 4) + 5); inflateReset keeps it off
+    for fmt, wb in (("zlib", 15), ("gzip", 31)):
+        for op in (["reset2", wb], ["reset"]):
+            S.append({"name": f"validate0-{op[0]}-{fmt}-bad", "spec": {"data": ["mix", 30000, 79], "fmt": fmt,
+                                                                       "xor_tail": 1},
+                      "ops": [["init", wb], ["validate", 0], op, ["feed", BIG], ["loop", Z_NO_FLUSH, 1 << 20],
+                              ["adler"]]})
     # inflateReset2 / inflateReset / inflateResetKeep between concatenated streams
     two = {"concat": [{"data": ["text", 40000, 69], "fmt": "zlib"}, {"data": ["mix", 30000, 70], "fmt": "raw"}]}
     S.append({"name": "reset2-zlib-then-raw", "spec": two,

@@ -73,3 +73,22 @@ def test_stream_sessions_on_segmented_parse(zg):
     assert r.returncode == 0, r.stderr[-2000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("BAD ")][-1]
     assert json.loads(line[4:]) == [], line
+
+
+@pytest.mark.parametrize("level", [1, 6])
+def test_one_large_call_then_finish_vs_system_zlib(zg, level):
+    """The session the round-4 r04c run crashed in (glibc heap corruption,
+    then a SIGSEGV inside deflate()): 16 MiB of Silesia-style mix offered to
+    ONE deflate(Z_NO_FLUSH) call with room for all of it, then Z_FINISH
+    (tools/stream_stages.py 16).  Every device-reported length and record count
+    is now checked against the host buffer it sizes before any copy
+    (zgpu_api.cpp compress_host_locked); the stream must equal the system
+    zlib's for the same two calls."""
+    import zlib
+    data = datagen.make("mix", 16 << 20, 5)
+    cap = len(data) + (len(data) >> 8) + (1 << 16)
+    recs, whole = run_dsession(zg.load(), data, [(len(data), 0, cap, True), (0, 4, cap, True)], level)
+    c = zlib.compressobj(level)
+    want = c.compress(data) + c.flush()
+    assert recs[-1][0] == 1, recs
+    assert hashlib.sha256(whole).hexdigest() == hashlib.sha256(want).hexdigest()

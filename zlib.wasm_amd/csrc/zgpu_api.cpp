@@ -184,6 +184,11 @@ struct DevBuf {
         cap = want;
         return true;
     }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
     template <typename T> T *as() const { return static_cast<T *>(p); }
 };
 
@@ -1008,11 +1013,19 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
         return ZGPU_MEM_ERROR;
     if (fh && copy_sync(fh->out, fs.out, 64, hipMemcpyDeviceToHost, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
+    // Every count and length the device reports is checked against the host
+    // buffer it sizes before anything is copied into host memory: a kernel
+    // fault must end in an error code, never in a write past a host buffer
+    // (the r04c run's heap corruption had this signature).
     if (fh && fh->rec_out) {
         uint32_t nb = 0;
         if (copy_sync(&nb, c.ws_meta.as<uint64_t>() + 2, 4, hipMemcpyDeviceToHost, st) != hipSuccess)
             return ZGPU_MEM_ERROR;
         ZTRACE("chl: nb %u\n", nb);
+        if ((size_t)nb > c.ws_srec.cap / 32) {
+            ZTRACE("chl: %u records reported, %zu fit\n", nb, c.ws_srec.cap / 32);
+            return ZGPU_MEM_ERROR;
+        }
         fh->rec_out->resize(4ull * nb);
         fh->evb_out->resize(fh->n);
         if ((nb && copy_sync(fh->rec_out->data(), fs.srec, 32ull * nb, hipMemcpyDeviceToHost, st) != hipSuccess) ||
@@ -1025,6 +1038,7 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
             if (copy_sync(&k, fs.snap + hsize, 4, hipMemcpyDeviceToHost, st) != hipSuccess) return ZGPU_MEM_ERROR;
             if (k < nb) {
                 const uint64_t S = (*fh->rec_out)[4ull * k + 2] >> 32, x = (*fh->rec_out)[4ull * k + 2] & 0xffffffffu;
+                if (x > src_len[0] || S > x || 2 * x > c.ws_link.cap) return ZGPU_MEM_ERROR;
                 fh->snap_head->resize(hsize);
                 fh->snap_prev->resize(x > S ? x - S : 0);
                 if (copy_sync(fh->snap_head->data(), fs.snap, 4ull * hsize, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -1038,6 +1052,8 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
     if (fh && fh->head_out && fh->n) {
         const uint64_t S = fh->out[2], end = fh->pos[fh->n - 1];
         const size_t hsize = size_t(1) << (mem_level + 7);
+        if (end > src_len[0] || S > end || 2 * end > c.ws_link.cap || 4 * hsize > c.ws_heads.cap)
+            return ZGPU_MEM_ERROR;
         fh->head_out->resize(hsize);
         fh->prev_out->resize(end > S ? end - S : 0);
         if (copy_sync(fh->head_out->data(), c.ws_heads.p, 4ull * hsize, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -1050,6 +1066,12 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
     if (copy_sync(ol.data(), d_dl, 8 * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
         copy_sync(os.data(), d_st, 4 * count, hipMemcpyDeviceToHost, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
+    for (size_t i = 0; i < count; i++)
+        if (ol[i] > dcap[i]) {
+            ZTRACE("chl: buffer %zu: %lu bytes reported, capacity %lu\n", i, (unsigned long)ol[i],
+                   (unsigned long)dcap[i]);
+            return ZGPU_MEM_ERROR;
+        }
     for (size_t i = 0; i < count; i++) {
         if (ol[i] && copy_sync(dst[i], d_out + dofs[i], ol[i], hipMemcpyDeviceToHost, st) != hipSuccess)
             return ZGPU_MEM_ERROR;
@@ -1138,8 +1160,11 @@ int inflate_par_locked(Ctx &c, const uint8_t *in, uint64_t n, uint8_t *out, uint
     // ---- candidate block headers
     const uint64_t b0 = 8 * hb, b1 = 8 * n;
     const uint32_t lcap = (uint32_t)std::min<uint64_t>((b1 - b0) / 16 + 65536, 1ull << 26);
+    // A workspace this path cannot get is no error: the exact sequential decode
+    // runs instead.  `nomem` clears the failed allocation's error.
+    auto nomem = [] { (void)hipGetLastError(); return 0; };
     if (!c.ws_par1.ensure(8ull * lcap + 64) || !c.ws_par2.ensure(8ull * lcap + 64) || !c.ws_imeta.ensure(64))
-        return -1;
+        return nomem();
     uint64_t *l1 = c.ws_par1.as<uint64_t>(), *l2 = c.ws_par2.as<uint64_t>();
     uint32_t *cnt = reinterpret_cast<uint32_t *>(c.ws_imeta.as<uint64_t>() + 4);   // two list counters
     uint32_t k1 = 0, k2 = 0;
@@ -1170,7 +1195,7 @@ int inflate_par_locked(Ctx &c, const uint8_t *in, uint64_t n, uint8_t *out, uint
         // per job: src_off src_len res_bit dst_off dst_cap dst_len blk_out[2] zstate[2] mrec_off | res_hist |
         // status | rec
         const size_t bytes = 8ull * K * 11 + 4ull * K * 2 + sizeof(InflateRec) * K + 256;
-        if (!c.ws_pjob.ensure(bytes)) return -1;
+        if (!c.ws_pjob.ensure(bytes)) return 1;
         uint64_t *d = c.ws_pjob.as<uint64_t>();
         uint64_t *soff = d, *slen = d + K, *rbit = d + 2 * K, *doff = d + 3 * K, *dcap = d + 4 * K, *dlen = d + 5 * K;
         uint64_t *blk = d + 6 * K, *zs = d + 8 * K, *mo = d + 10 * K;
@@ -1215,15 +1240,25 @@ int inflate_par_locked(Ctx &c, const uint8_t *in, uint64_t n, uint8_t *out, uint
         }
         return 0;
     };
-    const bool write = (uint64_t)cand.size() * kSlot <= (4ull << 30);    // slots for every candidate fit 4 GiB
+    // slots (and their match records, 2.7 B per slot byte) for every candidate
+    // when they fit 4x the in-flight budget; otherwise, or when the allocation
+    // fails, every candidate is measured count-only and decoded in place
+    bool write = (uint64_t)cand.size() * (kSlot + 8 * kSlotRec) <= 4 * (uint64_t)c.inflight;
+    struct SlotsBack {            // slots beyond the in-flight budget go back when the call ends
+        Ctx &c;
+        ~SlotsBack() { if (c.ws_pslot.cap > c.inflight) c.ws_pslot.release(); }
+    } slots_back{c};
     if (write) {
-        if (!c.ws_pslot.ensure(cand.size() * kSlot + 32768 + 64) || !c.ws_mrec.ensure(8 * cand.size() * kSlotRec + 64))
-            return -1;
-        slots = c.ws_pslot.as<uint8_t>();
-        mrec = c.ws_mrec.as<uint64_t>();
+        if (!c.ws_pslot.ensure(cand.size() * kSlot + 32768 + 64) || !c.ws_mrec.ensure(8 * cand.size() * kSlotRec + 64)) {
+            (void)hipGetLastError();
+            write = false;
+        } else {
+            slots = c.ws_pslot.as<uint8_t>();
+            mrec = c.ws_mrec.as<uint64_t>();
+        }
     }
     std::vector<Span> sp;
-    if (spans(cand, sp, write)) return -1;
+    if (int e = spans(cand, sp, write)) return e > 0 ? nomem() : -1;
     // ---- the chain of blocks from the first one
     struct Blk { uint64_t bit, o0, out; bool last; uint32_t nm; int64_t slot; };
     std::vector<Blk> chain;
@@ -1237,7 +1272,7 @@ int inflate_par_locked(Ctx &c, const uint8_t *in, uint64_t n, uint8_t *out, uint
             // a fixed-code block (or a stored one the scan missed), or one longer than its slot
             if (++misses > 16) return 0;
             std::vector<Span> one;
-            if (spans(std::vector<uint64_t>{b}, one, false)) return -1;
+            if (int e = spans(std::vector<uint64_t>{b}, one, false)) return e > 0 ? nomem() : -1;
             s = one[0];
         }
         if (s.stop != kIBlock || s.end <= b) return 0;
@@ -1264,7 +1299,7 @@ int inflate_par_locked(Ctx &c, const uint8_t *in, uint64_t n, uint8_t *out, uint
         mtot += chain[ip[j]].out / 3 + 2;
     }
     // their records in a buffer of their own (the slots' stay where the candidates' decode put them)
-    if (!c.ws_par2.ensure(8 * mtot + 64) || !c.ws_psym.ensure(4 * total + 64)) return -1;
+    if (!c.ws_par2.ensure(8 * mtot + 64) || !c.ws_psym.ensure(4 * total + 64)) return nomem();
     uint64_t *mrec_ip = c.ws_par2.as<uint64_t>();
     if (NB) {
         std::vector<uint64_t> soff(NB, 0), slen(NB, n), rbit(NB), doff(NB), dcap(NB);
@@ -1277,7 +1312,7 @@ int inflate_par_locked(Ctx &c, const uint8_t *in, uint64_t n, uint8_t *out, uint
             dcap[j] = hist[j] + B.out;
         }
         const size_t jb = 8ull * NB * 9 + 4ull * NB * 2 + sizeof(InflateRec) * NB + 256;
-        if (!c.ws_pjob.ensure(jb)) return -1;
+        if (!c.ws_pjob.ensure(jb)) return nomem();
         uint64_t *d = c.ws_pjob.as<uint64_t>();
         uint64_t *d_soff = d, *d_slen = d + NB, *d_rbit = d + 2 * NB, *d_doff = d + 3 * NB, *d_dcap = d + 4 * NB;
         uint64_t *d_dlen = d + 5 * NB, *d_blk = d + 6 * NB, *d_moff = d + 8 * NB;
@@ -1322,7 +1357,7 @@ int inflate_par_locked(Ctx &c, const uint8_t *in, uint64_t n, uint8_t *out, uint
         }
     }
     if (!pb.empty()) {
-        if (!c.ws_par1.ensure(sizeof(ParBlkHost) * pb.size() + 64) || !c.ws_imeta.ensure(64)) return -1;
+        if (!c.ws_par1.ensure(sizeof(ParBlkHost) * pb.size() + 64) || !c.ws_imeta.ensure(64)) return nomem();
         uint32_t *sym = c.ws_psym.as<uint32_t>();
         uint32_t *err = reinterpret_cast<uint32_t *>(c.ws_imeta.as<uint64_t>() + 5);
         uint32_t e_host = 0;
@@ -1524,6 +1559,8 @@ int uncompress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_
         copy_sync(os.data(), d_st, 4 * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
         copy_sync(ostop.data(), d_stop, 4 * count, hipMemcpyDeviceToHost, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
+    for (size_t i = 0; i < count; i++)
+        if (ol[i] > dcap[i] || ou[i] > sl[i]) return ZGPU_MEM_ERROR;   // device-reported sizes (see compress_host_locked)
     for (size_t i = 0; i < count; i++) {
         if (ol[i] && copy_sync(dst[i], d_out + dofs[i], ol[i], hipMemcpyDeviceToHost, st) != hipSuccess)
             return ZGPU_MEM_ERROR;
@@ -1585,6 +1622,7 @@ int inflate_try_locked(Ctx &c, const uint8_t *in, size_t n, bool resume, uint64_
         copy_sync(&status, d_st, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         copy_sync(&stop, d_stop, 4, hipMemcpyDeviceToHost, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
+    if (res[0] > cap || res[1] > n) return ZGPU_MEM_ERROR;      // device-reported sizes (see compress_host_locked)
     out.resize(res[0]);
     if (res[0] && copy_sync(out.data(), d_out, res[0], hipMemcpyDeviceToHost, st) != hipSuccess) return ZGPU_MEM_ERROR;
     t.stop = stop;
@@ -2024,6 +2062,37 @@ static uint32_t checksum_one(bool is_crc, uint32_t init, const Bytef *buf, size_
     }
     return out;
 }
+
+// The check values deflate() / inflate() and the dictionary calls compute for
+// themselves (running checks, trailers, gzip header CRCs) go through these
+// instead of the public crc32_z / adler32_z: a failed GPU call there is an
+// error code of the call (Z_MEM_ERROR through the entry points' existing
+// std::bad_alloc handlers), never the end of the host process.  Only the public
+// crc32() / adler32(), which have no error return, end the process.
+struct GpuCheckFailed : std::bad_alloc {
+    const char *what() const noexcept override { return "libzgpu: GPU checksum failed"; }
+};
+static uint32_t ck_internal(bool is_crc, uint32_t init, const Bytef *buf, size_t len) {
+    if (buf == nullptr) return is_crc ? 0u : 1u;
+    const uint8_t *p = buf;
+    uint32_t out = 0;
+    const int rc = len <= kSmallCk ? checksum_small(is_crc, init, p, len, &out)
+                   : is_crc      ? zgpu_crc32_batch(&p, &len, &init, &out, 1)
+                                 : zgpu_adler32_batch(&p, &len, &init, &out, 1);
+    if (rc) {
+        // ZGPU_CHECKSUM_ERROR=zero (host-side tests on machines without a GPU):
+        // 0, as the public calls return then
+        static const bool zero = [] {
+            const char *e = std::getenv("ZGPU_CHECKSUM_ERROR");
+            return e && std::strcmp(e, "zero") == 0;
+        }();
+        if (zero) return 0;
+        throw GpuCheckFailed();
+    }
+    return out;
+}
+static inline uint32_t ck_crc32(uint32_t crc, const Bytef *buf, size_t len) { return ck_internal(true, crc, buf, len); }
+static inline uint32_t ck_adler32(uint32_t a, const Bytef *buf, size_t len) { return ck_internal(false, a, buf, len); }
 
 uLong crc32_z(uLong crc, const Bytef *buf, size_t len) {
     if (buf == nullptr) return 0;                      // crc32.c:700
@@ -2565,7 +2634,7 @@ void advance_check(internal_state *s, size_t end) {
     if (!s->wrap || s->ck_pos >= end) return;
     const uint8_t *p = s->in.data() + (s->ck_pos - s->in_base);
     const size_t n = end - s->ck_pos;
-    s->check = s->wrap == 2 ? (uint32_t)crc32_z(s->check, p, n) : (uint32_t)adler32_z(s->check, p, n);
+    s->check = s->wrap == 2 ? ck_crc32(s->check, p, n) : ck_adler32(s->check, p, n);
     s->ck_pos = end;
 }
 
@@ -2690,7 +2759,7 @@ void queue_header(internal_state *s) {                          // deflate.c:100
         if (h->comment)
             for (const Bytef *p = h->comment;; p++) { g.push_back(*p); if (!*p) break; }
         if (h->hcrc) {                                          // the header's CRC-32, low 16 bits
-            const uint32_t c = (uint32_t)crc32_z(0, g.data(), g.size());
+            const uint32_t c = ck_crc32(0, g.data(), g.size());
             g.push_back((uint8_t)(c & 0xff));
             g.push_back((uint8_t)((c >> 8) & 0xff));
         }
@@ -2881,8 +2950,8 @@ int deflate_stored_call(z_streamp strm, internal_state *s, int flush) {
     s->in.assign(buf.begin() + (std::ptrdiff_t)bpos, buf.end());   // the window's unsent bytes
     {   // read_buf's running check over everything this call read (one contiguous run from in0)
         const uint64_t rd = used0 - strm->avail_in;
-        if (rd && s->wrap == 1) s->check = (uint32_t)adler32_z(s->check, in0, rd);
-        else if (rd && s->wrap == 2) s->check = (uint32_t)crc32_z(s->check, in0, rd);
+        if (rd && s->wrap == 1) s->check = ck_adler32(s->check, in0, rd);
+        else if (rd && s->wrap == 2) s->check = ck_crc32(s->check, in0, rd);
     }
     {   // the window: the last strstart bytes read (deflate.c:1733-1790 keep them contiguous)
         const uint64_t rd = used0 - strm->avail_in, keep = (uint64_t)strstart;
@@ -3095,7 +3164,7 @@ static int deflate_body(z_streamp strm, int flush) {
             strm->next_out += cap;
             strm->avail_out -= (uInt)cap;
             strm->total_out += cap;
-            strm->adler = s->wrap == 2 ? crc32_z(0, sp, sl) : (s->wrap == 1 ? adler32_z(1, sp, sl) : strm->adler);
+            strm->adler = s->wrap == 2 ? ck_crc32(0, sp, sl) : (s->wrap == 1 ? ck_adler32(1, sp, sl) : strm->adler);
             strm->next_in += sl;
             strm->total_in += sl;
             strm->avail_in = 0;
@@ -3364,7 +3433,7 @@ int deflateSetDictionary(z_streamp strm, const Bytef *dictionary, uInt dictLengt
     if (s->level != 0 && pending_input(s)) return Z_STREAM_ERROR;        // s->lookahead != 0
     if (s->finished) return unsupported(strm, "deflateSetDictionary: the stream has ended");
     try {
-        if (s->wrap == 1) strm->adler = adler32_z(strm->adler, dictionary, dictLength);
+        if (s->wrap == 1) strm->adler = ck_adler32(strm->adler, dictionary, dictLength);
         const uint64_t wsize = uint64_t(1) << s->wbits;
         bool reset = false;
         if (dictLength >= wsize) {                      // the tail replaces the history
@@ -3836,6 +3905,9 @@ int inflateReset2(z_streamp strm, int windowBits) {
     if (windowBits && (windowBits < 8 || windowBits > 15)) return Z_STREAM_ERROR;
     s->wrap = wrap;
     s->wbits = windowBits;
+    // inflate.c:157's wrap = (windowBits >> 4) + 5 carries bit 4 (check the
+    // trailer) again: an earlier inflateValidate(strm, 0) ends here
+    s->ivalid = wrap != 0;
     return inflateReset(strm);
 }
 
@@ -3931,7 +4003,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
     if (s->cap == 0) s->cap = std::max<size_t>(4 * s->in.size(), 1 << 16);
     const bool is_check = s->wrap != 0;
     auto check_of = [&](uint32_t init, const uint8_t *p, size_t n) -> uint32_t {
-        return s->igz ? (uint32_t)crc32_z(init, p, n) : (uint32_t)adler32_z(init, p, n);
+        return s->igz ? ck_crc32(init, p, n) : ck_adler32(init, p, n);
     };
     if (s->itail) {
         // the last block is out (an inflate(Z_BLOCK) stopped after it): the
@@ -4137,8 +4209,8 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
                 strm->avail_in += (uInt)back;
                 strm->total_in = t.used - s->iadj;
                 if (s->wrap) strm->adler = s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b
-                                               ? crc32_z(0, o.data(), o.size())
-                                               : adler32_z(1, o.data(), o.size());
+                                               ? ck_crc32(0, o.data(), o.size())
+                                               : ck_adler32(1, o.data(), o.size());
             } else {
                 s->result = Z_DATA_ERROR;
                 strm->msg = const_cast<char *>("invalid or corrupt deflate stream");
@@ -4273,7 +4345,7 @@ void gz_header_fill(internal_state *s) {
     }
     if (flags & 0x0200u) {                                      // FHCRC: a mismatch is BAD (the decode says so)
         if (m < p + 2) return;
-        const uint32_t c = (uint32_t)crc32_z(0, b, p);
+        const uint32_t c = ck_crc32(0, b, p);
         if ((c & 0xffffu) != (uint32_t)(b[p] | b[p + 1] << 8)) return;
     }
     h->hcrc = (int)((flags >> 9) & 1u);
@@ -4362,7 +4434,7 @@ int inflateSetDictionary(z_streamp strm, const Bytef *dictionary, uInt dictLengt
     if (dictLength && !dictionary) return Z_STREAM_ERROR;
     try {
         if (s->need_dict) {
-            if ((uint32_t)adler32_z(1, dictionary, dictLength) != s->want_dict) return Z_DATA_ERROR;
+            if (ck_adler32(1, dictionary, dictLength) != s->want_dict) return Z_DATA_ERROR;
         } else if (!s->in.empty() || s->ideliv || s->imode) {
             strm->msg = const_cast<char *>("inflateSetDictionary: raw streams before their first input only");
             return Z_STREAM_ERROR;
@@ -4598,7 +4670,7 @@ int inflate(z_streamp strm, int flush) {
                 }
                 if (s->iadl_on) {
                     if (n && s->ivalid)
-                        s->iadl = s->igz ? (uint32_t)crc32_z(s->iadl, next0, n) : (uint32_t)adler32_z(s->iadl, next0, n);
+                        s->iadl = s->igz ? ck_crc32(s->iadl, next0, n) : ck_adler32(s->iadl, next0, n);
                     strm->adler = s->iadl;
                 }
             }
