@@ -4037,6 +4037,567 @@ int launch_tables_upload(const CodeTables *ct, const CrcTables *) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(c_ct), ct, sizeof(CodeTables));
 }
 
+// ------------------------------------------------------------------------
+// The sorted-run longest_match (round 5): k_bsort, k_bwork, k_match2 for
+// batch jobs at levels 4..9 (hash_bits <= 15).
+//
+// longest_match's candidates for position p are the earlier positions with
+// p's hash, most recent first, while they lie within MAX_DIST (deflate.c
+// :1356-1497 over the prev[] chain).  k_match walks that
+// chain link by link: every step is a dependent LDS round trip, and the walk is
+// bound by their latency.  Here the chain is not followed but
+// read: each block of kSortBlock positions is sorted by (hash, position)
+// (k_bsort), so a position's candidates are the entries just before its own in
+// its block, then its hash's run in the block before, then in the one before
+// that -- three contiguous runs whose bounds are known up front (k_bwork).
+// Every candidate's address is then a function of its rank alone, so a lane's
+// next candidates can be loaded before the current one is tested.
+// ------------------------------------------------------------------------
+constexpr int kBSThreads = 1024;
+constexpr int kBSWaves = kBSThreads / 64;
+constexpr int kBSPer = kSortBlock / kBSThreads;     // keys per thread (16)
+constexpr int kBSlice = 4096;                       // k_bwork's count-sorted slices
+static_assert(kSortBlock == 16384, "positions are 14-bit block-relative in the sort keys");
+
+// the sub-batch buffer a flat block belongs to: the last bi with bblk[bi] <= g
+__device__ inline uint32_t block_buffer(const uint32_t *bblk, uint32_t count, uint32_t g) {
+    uint32_t lo = 0, hi = count - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (bblk[mid] <= g) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// One stable counting-sort pass (8-bit digit at `shift`) of src[0..m) into dst:
+// wave w owns elements w*1024 + j*64 + lane; equal digits within a wave step
+// are ranked with ballots, counts scanned digit-major across the 16 waves.
+__device__ __attribute__((always_inline)) inline void bs_radix_pass(const uint32_t *src, uint32_t *dst, int m,
+                                                                    int shift, uint16_t (*wcnt)[256], int *wsum,
+                                                                    int tid) {
+    const int lane = tid & 63, wave = tid >> 6;
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (int k = tid; k < kBSWaves * 256; k += kBSThreads) (&wcnt[0][0])[k] = 0;
+    __syncthreads();
+    uint32_t key[kBSPer], rank[kBSPer];
+#pragma unroll
+    for (int j = 0; j < kBSPer; j++) {
+        const int e = wave * (64 * kBSPer) + j * 64 + lane;
+        const bool valid = e < m;
+        key[j] = valid ? src[e] : 0u;
+        const uint32_t d = (key[j] >> shift) & 0xffu;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const uint64_t bb = __ballot((d >> b) & 1u);
+            peers &= ((d >> b) & 1u) ? bb : ~bb;
+        }
+        rank[j] = 0;
+        if (valid) {
+            const uint32_t base = wcnt[wave][d];
+            rank[j] = base + (uint32_t)__popcll(peers & below);
+            if ((peers & below) == 0) wcnt[wave][d] = (uint16_t)(base + __popcll(peers));
+        }
+    }
+    __syncthreads();
+    int v[4], tot = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int idx = tid * 4 + k;
+        v[k] = wcnt[idx & (kBSWaves - 1)][idx >> 4];
+        tot += v[k];
+    }
+    int incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int wbase = 0;
+    for (int w = 0; w < wave; w++) wbase += wsum[w];
+    int run = wbase + incl - tot;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int idx = tid * 4 + k;
+        wcnt[idx & (kBSWaves - 1)][idx >> 4] = (uint16_t)run;
+        run += v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kBSPer; j++) {
+        const int e = wave * (64 * kBSPer) + j * 64 + lane;
+        if (e < m) dst[wcnt[wave][(key[j] >> shift) & 0xffu] + rank[j]] = key[j];
+    }
+    __syncthreads();
+}
+
+// k_bsort — one workgroup per block: its inserted positions (p <= n-3,
+// INSERT_STRING needs MIN_MATCH bytes of lookahead) sorted by (hash, position)
+// into srt, and the block's hash table off[0 .. hash_size] into boff.
+__global__ __launch_bounds__(kBSThreads) void k_bsort(DeflateJob job) {
+    __shared__ uint32_t ka[kSortBlock], kb[kSortBlock];
+    __shared__ __attribute__((aligned(16))) uint8_t by[kSortBlock + 16];
+    __shared__ uint16_t wcnt[kBSWaves][256];
+    __shared__ int wsum[kBSWaves];
+    const int tid = threadIdx.x;
+    const uint32_t g = blockIdx.x;
+    const uint32_t bi = block_buffer(job.bblk, job.count, g);
+    const int64_t p0 = (int64_t)(g - job.bblk[bi]) * kSortBlock;
+    const int64_t n = (int64_t)job.src_len[job.first + bi];
+    const uint8_t *in = job.src + job.src_off[job.first + bi];
+    const WinP wp = job_win(job);
+    const int hsize = (int)wp.mask + 1;
+    stage_bytes<kBSThreads, (kSortBlock + 16) / 16 / kBSThreads + 1>(by, in, p0, kSortBlock + 16, n, tid);
+    __syncthreads();
+    const int m = (int)(n - 2 - p0 <= 0 ? 0 : (n - 2 - p0 < kSortBlock ? n - 2 - p0 : kSortBlock));
+    for (int e = tid; e < m; e += kBSThreads) ka[e] = hashp(by[e], by[e + 1], by[e + 2], wp) << 14 | (uint32_t)e;
+    bs_radix_pass(ka, kb, m, 14, wcnt, wsum, tid);
+    bs_radix_pass(kb, ka, m, 22, wcnt, wsum, tid);
+    uint16_t *S = job.srt + job.ws_off[bi] + p0;
+    for (int i = tid; i < m; i += kBSThreads) S[i] = (uint16_t)(ka[i] & (kSortBlock - 1));
+    // off[h] = entries with a hash below h: a run's start is marked at its
+    // hash, then a suffix minimum fills the hashes without entries
+    uint16_t *off = reinterpret_cast<uint16_t *>(kb);
+    for (int h = tid; h < hsize; h += kBSThreads) off[h] = 0xffffu;
+    __syncthreads();
+    for (int i = tid; i < m; i += kBSThreads) {
+        const uint32_t h = ka[i] >> 14;
+        if (i == 0 || (ka[i - 1] >> 14) != h) off[h] = (uint16_t)i;
+    }
+    __syncthreads();
+    const int per = (hsize + kBSThreads - 1) / kBSThreads;      // hashes per thread (32 at hash_bits 15)
+    const int h0 = tid * per, h1 = min(h0 + per, hsize);
+    uint32_t smin = 0xffffu;
+    for (int h = h0; h < h1; h++) smin = min(smin, (uint32_t)off[h]);
+    // suffix minimum of the threads' minima: over the wave, then over the waves
+    const int lane = tid & 63, wave = tid >> 6;
+    uint32_t suf = smin;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_down((int)suf, o, 64);
+        if (lane + o < 64) suf = min(suf, t);
+    }
+    if (lane == 0) wsum[wave] = (int)suf;
+    __syncthreads();
+    uint32_t carry = (uint32_t)m;                                // past the last run: every entry is below
+    for (int w = wave + 1; w < kBSWaves; w++) carry = min(carry, (uint32_t)wsum[w]);
+    {
+        const uint32_t nxt = (uint32_t)__shfl_down((int)suf, 1, 64);   // minimum of the later lanes of this wave
+        if (lane < 63) carry = min(carry, nxt);
+    }
+    uint16_t *go = job.boff + (size_t)g * kSortOffStride;
+    for (int h = h1 - 1; h >= h0; h--) {
+        carry = min(carry, (uint32_t)off[h]);
+        go[h] = (uint16_t)carry;
+    }
+    if (tid == 0) go[hsize] = (uint16_t)m;
+}
+
+// k_bwork — one workgroup per block: a work item per sorted entry i of the
+// block (position rel, hash h): its own run's candidates (the n0 entries
+// before i), and h's runs in the two blocks before (end e1 / e2, length
+// n1 / n2).  Each 4096-entry slice is counting-sorted by the candidate count
+// (capped at the chain budget; k_count's key), longest first, so the 64
+// walks of a wave have similar lengths (tools/model/model_sortwalk.c: 98.6 %
+// SIMT utilisation at L6 against 78 % in plain sorted order).
+__global__ __launch_bounds__(kBSThreads) void k_bwork(DeflateJob job) {
+    __shared__ uint16_t S[kSortBlock];
+    __shared__ uint16_t off[kSortOffStride];
+    __shared__ __attribute__((aligned(16))) uint8_t by[kSortBlock + 16];
+    __shared__ int s_hist[kSortBlock / kBSlice][64], s_base[kSortBlock / kBSlice][64];
+    const int tid = threadIdx.x;
+    const uint32_t g = blockIdx.x;
+    const uint32_t bi = block_buffer(job.bblk, job.count, g);
+    const uint32_t b = g - job.bblk[bi];
+    const int64_t p0 = (int64_t)b * kSortBlock;
+    const int64_t n = (int64_t)job.src_len[job.first + bi];
+    const uint8_t *in = job.src + job.src_off[job.first + bi];
+    const WinP wp = job_win(job);
+    const int hsize = (int)wp.mask + 1;
+    const int m = (int)(n - 2 - p0 <= 0 ? 0 : (n - 2 - p0 < kSortBlock ? n - 2 - p0 : kSortBlock));
+    const uint16_t *gS = job.srt + job.ws_off[bi] + p0;
+    const uint16_t *gO = job.boff + (size_t)g * kSortOffStride;
+    for (int i = tid; i < m; i += kBSThreads) S[i] = gS[i];
+    for (int h = tid; h <= hsize; h += kBSThreads) off[h] = gO[h];
+    stage_bytes<kBSThreads, (kSortBlock + 16) / 16 / kBSThreads + 1>(by, in, p0, kSortBlock + 16, n, tid);
+    if (tid < (kSortBlock / kBSlice) * 64) (&s_hist[0][0])[tid] = 0;
+    __syncthreads();
+    const uint16_t *o1 = b >= 1 ? job.boff + (size_t)(g - 1) * kSortOffStride : nullptr;
+    const uint16_t *o2 = b >= 2 ? job.boff + (size_t)(g - 2) * kSortOffStride : nullptr;
+    const uint32_t chain = job.cfg.chain;
+    uint4 it[kBSPer];
+    int bk[kBSPer], rk[kBSPer];
+#pragma unroll
+    for (int u = 0; u < kBSPer; u++) {
+        const int i = tid + u * kBSThreads;
+        rk[u] = 0;
+        bk[u] = 0;
+        it[u] = make_uint4(0, 0, 0, 0);
+        if (i >= m) continue;
+        const uint32_t rel = S[i];
+        const uint32_t h = hashp(by[rel], by[rel + 1], by[rel + 2], wp);
+        const uint32_t n0 = (uint32_t)i - off[h];
+        const uint32_t s1 = o1 ? o1[h] : 0u, e1 = o1 ? o1[h + 1] : 0u;
+        const uint32_t s2 = o2 ? o2[h] : 0u, e2 = o2 ? o2[h + 1] : 0u;
+        it[u] = make_uint4((uint32_t)i | rel << 16, n0 | (e1 - s1) << 16, e1 | e2 << 16, e2 - s2);
+        const uint32_t c = n0 + (e1 - s1) + (e2 - s2);
+        bk[u] = 63 - (int)(walk_key(c, chain) >> 2);
+    }
+#pragma unroll
+    for (int u = 0; u < kBSPer; u++)
+        if (tid + u * kBSThreads < m) rk[u] = atomicAdd(&s_hist[u / (kBSlice / kBSThreads)][bk[u]], 1);
+    __syncthreads();
+    if (tid < (kSortBlock / kBSlice) * 64) {                  // exclusive scan per slice
+        const int sl = tid >> 6, l = tid & 63;
+        const int v = s_hist[sl][l];
+        int incl = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o, 64);
+            if (l >= o) incl += t;
+        }
+        s_base[sl][l] = incl - v;
+    }
+    __syncthreads();
+    uint4 *W = job.work + job.ws_off[bi] + p0;
+#pragma unroll
+    for (int u = 0; u < kBSPer; u++) {
+        const int sl = u / (kBSlice / kBSThreads);
+        if (tid + u * kBSThreads < m) W[sl * kBSlice + s_base[sl][bk[u]] + rk[u]] = it[u];
+    }
+}
+
+// k_match2 — levels 4..9, one 1024-thread workgroup per buffer (or per range
+// of blocks of a large buffer).  LDS holds, for the blocks b-2, b-1, b of the
+// current block b, their sorted entries as byte-ring offsets (Sr, 96 KiB) and
+// their bytes (Bw, 48 KiB + pad); between blocks both slide down by one block.
+// A work item (k_bwork) gives a position's three candidate runs; candidate k
+// is Sr[base(k) - k], so the walk needs no link: every candidate's load is
+// independent of the previous one's.  The walk is dwq_walk's (deferred
+// compares, kDU steps per exit test) with the link chase replaced by that
+// index, and it equals longest_match (deflate.c:1356-1497) for every position.
+constexpr int kM2Threads = 1024;
+constexpr int kM2Pad = 304;                       // bytes past block b: compares read <= 258 + 16 + 3 past a position
+constexpr int kM2Ring = 3 * kSortBlock;
+
+// 4 bytes at any offset of the byte ring
+__device__ __attribute__((always_inline)) inline uint32_t b4(const uint8_t *B, int q) {
+#ifdef ZGPU_LDS_UNALIGNED
+    uint32_t x;
+    asm volatile("ds_read_b32 %0, %1" : "=v"(x) : "v"((uint32_t)(uintptr_t)(B + q)));
+    return x;
+#else
+    return lds32u(B, q);
+#endif
+}
+// 16 bytes at any offset: 5 aligned dwords, 4 byte-aligns
+__device__ __attribute__((always_inline)) inline void b16(const uint8_t *B, int q, uint32_t &x0, uint32_t &x1,
+                                                          uint32_t &x2, uint32_t &x3) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(B + (q & ~3));
+    const uint32_t sh = (uint32_t)(q & 3);
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+    x0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    x2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+    x3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
+}
+// LCP of the scan at s (its first 16 bytes in S) and candidate m, capped at maxcmp
+__device__ __attribute__((always_inline)) inline int blcp16(const uint8_t *B, int m, int s, const Scan16 &S,
+                                                            int maxcmp) {
+    uint32_t a0, a1, a2, a3;
+    b16(B, m, a0, a1, a2, a3);
+    int k = diff16(a0 ^ S.s0, a1 ^ S.s1, a2 ^ S.s2, a3 ^ S.s3);
+    while (k >= 16 && k < maxcmp) {
+        uint32_t c0, c1, c2, c3;
+        b16(B, m + k, a0, a1, a2, a3);
+        b16(B, s + k, c0, c1, c2, c3);
+        const int r = diff16(a0 ^ c0, a1 ^ c1, a2 ^ c2, a3 ^ c3);
+        k += r;
+        if (r < 16) break;
+    }
+    return k < maxcmp ? k : maxcmp;
+}
+
+// One position's longest_match from its work item.  Every lane of the wave
+// calls this together (the flushes are wave-wide decisions taken with ballots).
+//   Sr, B: the rings; vp: the position's ring offset; lim: ring offset of the
+//   limit (candidates must lie above it; the head may equal it, deflate.c
+//   :1955 vs :1492); A0/B1/B2, n0/n01/n012: candidate k is Sr[base(k) - k]
+//   with base A0 for k < n0, B1 for k < n01, B2 below n012 (none after).
+__device__ __attribute__((always_inline)) inline uint32_t m2_cand(const uint16_t *Sr, uint32_t k, int A0, int B1,
+                                                                  int B2, uint32_t n0, uint32_t n01, uint32_t n012) {
+    int idx = k < n0 ? A0 - (int)k : (k < n01 ? B1 - (int)k : B2 - (int)k);
+    idx = idx < 0 ? 0 : idx;
+    const int q = (int)Sr[idx];
+    return k < n012 ? (uint32_t)q : 0xffffffffu;       // none: below every limit (tested as signed)
+}
+struct DWQ2 {
+    int occ;
+    int q[kDQ];
+    uint32_t scan01, scanE;
+    int be;            // best - 1
+    bool alive;        // no candidate at or below the limit seen yet
+};
+__device__ __attribute__((always_inline)) inline void m2_walk(const uint16_t *Sr, const uint8_t *B, int vp, int lim,
+                                                              int A0, int B1, int B2, uint32_t n0, uint32_t n01,
+                                                              uint32_t n012, int64_t p, int64_t n,
+                                                              const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
+                                                              int want_q) {
+    const int64_t rem = n - p;
+    const int nice = rem < cfg.nice ? (int)rem : cfg.nice;
+    const int maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
+    const uint32_t chain = (uint32_t)cfg.chain;
+    const uint32_t qc = want_q ? chain >> 2 : chain;
+    Scan16 S;
+    b16(B, vp, S.s0, S.s1, S.s2, S.s3);
+    int best = kMinMatch - 1, bq = vp;
+    uint32_t count = 0;
+    bool walking = true, need_q = want_q != 0;
+    auto rec = [&](int bb, int q) { return bb >= kMinMatch ? (((uint32_t)bb << 16) | (uint32_t)(vp - q)) : 0u; };
+#pragma unroll
+    for (int k = 0; k < kD0; k++) {                 // the chain's head, compared by the whole wave
+        if (walking) {
+            const int q = (int)m2_cand(Sr, count, A0, B1, B2, n0, n01, n012);
+            const int len = blcp16(B, q, vp, S, maxcmp);
+            if (len > best) { best = len; bq = q; }
+            count++;
+            const int qn = (int)m2_cand(Sr, count, A0, B1, B2, n0, n01, n012);
+            if (best >= nice || qn <= lim || count >= chain) walking = false;
+            if (need_q && count == qc && walking) {
+                rq[p] = rec(best, bq);
+                need_q = false;
+            }
+        }
+    }
+    if (!walking) {
+        const uint32_t r = rec(best, bq);
+        if (need_q) rq[p] = r;
+        rf[p] = r;
+        return;
+    }
+    DWQ2 w;
+    w.occ = 0;
+#pragma unroll
+    for (int j = 0; j < kDQ; j++) w.q[j] = 0;
+    w.scan01 = S.s0 & 0xffffu;
+    w.be = best - 1;
+    w.scanE = b4(B, vp + w.be) & 0xffffu;
+    w.alive = true;
+    count = ufl(count);
+    auto step = [&](uint32_t k) {
+        const int q = (int)m2_cand(Sr, k, A0, B1, B2, n0, n01, n012);
+        const bool in = q > lim;
+        const int qs = in ? q : 0;
+        const uint32_t c01 = b4(B, qs) & 0xffffu, cE = b4(B, qs + w.be) & 0xffffu;
+        const bool pass = w.alive & in & (c01 == w.scan01) & (cE == w.scanE);
+        w.alive = w.alive & in;
+#pragma unroll
+        for (int j = kDQ - 1; j > 0; j--) w.q[j] = pass ? w.q[j - 1] : w.q[j];
+        w.q[0] = pass ? q : w.q[0];
+        w.occ += pass ? 1 : 0;
+    };
+    for (;;) {
+        const uint32_t end = count < qc ? qc : chain;
+        const int best0 = best;
+        for (;;) {
+            if (end - count >= (uint32_t)kDU) {
+#pragma unroll
+                for (int u = 0; u < kDU; u++) step(count + u);
+                count += kDU;
+            } else {
+                step(count);
+                count += 1;
+            }
+            const uint64_t walkers = __ballot(w.alive), full = __ballot(w.occ >= kDQ - (kDU - 1));
+            if (count >= end || walkers == 0 || full != 0) break;
+        }
+        walking = w.alive && count < chain;
+        if (walking) {                                  // the next candidate must lie above the limit too
+            const int qn = (int)m2_cand(Sr, count, A0, B1, B2, n0, n01, n012);
+            walking = qn > lim;
+        }
+        static_assert(kDQ % 2 == 0, "entries are taken in pairs");
+#pragma unroll
+        for (int j = kDQ - 1; j >= 1; j -= 2) {
+            const bool c1 = j < w.occ, c0 = j - 1 < w.occ;
+            if (__ballot(c0) != 0) {
+                const int l1 = c1 ? blcp16(B, w.q[j], vp, S, maxcmp) : 0;
+                const int l0 = c0 ? blcp16(B, w.q[j - 1], vp, S, maxcmp) : 0;
+                if (c1 && l1 > best) {
+                    best = l1;
+                    bq = w.q[j];
+                    if (l1 >= nice) { walking = false; w.occ = 0; }
+                }
+                if (c0 && j - 1 < w.occ && l0 > best) {
+                    best = l0;
+                    bq = w.q[j - 1];
+                    if (l0 >= nice) { walking = false; w.occ = 0; }
+                }
+            }
+        }
+        w.occ = 0;
+        const bool fin = !walking;
+        if (need_q && (count >= qc || fin)) {          // deflate.c:1390-1392 (chain >>= 2)
+            rq[p] = rec(best, bq);
+            need_q = false;
+        }
+        if (fin) break;
+        if (best != best0) {                           // the quick reject now tests the new best
+            w.be = best - 1;
+            w.scanE = b4(B, vp + w.be) & 0xffffu;
+        }
+    }
+    rf[p] = rec(best, bq);
+}
+
+// What a thread stages of block b: 16 sorted entries, 16 bytes (+ pad).
+struct M2Pre {
+    uint4 s0, s1;
+    uint4 by, pad;
+};
+__device__ __attribute__((always_inline)) inline void m2_prefetch(M2Pre &P, const uint16_t *gS, int m,
+                                                                  const uint8_t *in, int64_t p0, int64_t n, int tid) {
+    const int e = 16 * tid;
+    if (e + 16 <= m) {
+        P.s0 = *reinterpret_cast<const uint4 *>(gS + e);
+        P.s1 = *reinterpret_cast<const uint4 *>(gS + e + 8);
+    } else {
+        uint32_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int j = 0; j < 16; j++)
+            if (e + j < m) v[j >> 1] |= (uint32_t)gS[e + j] << (16 * (j & 1));
+        P.s0 = make_uint4(v[0], v[1], v[2], v[3]);
+        P.s1 = make_uint4(v[4], v[5], v[6], v[7]);
+    }
+    auto ld16 = [&](int64_t x) -> uint4 {
+        if (x >= 0 && x + 16 <= n) {
+            const uintptr_t a = reinterpret_cast<uintptr_t>(in + x);
+            const uint32_t sh = (uint32_t)(a & 3u);
+            const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+            if (sh == 0) return make_uint4(q[0], q[1], q[2], q[3]);
+            const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
+            return make_uint4(__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                              __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh));
+        }
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (int j = 0; j < 16; j++)
+            if (x + j >= 0 && x + j < n) w[j >> 2] |= (uint32_t)in[x + j] << (8 * (j & 3));
+        return make_uint4(w[0], w[1], w[2], w[3]);
+    };
+    P.by = ld16(p0 + e);
+    if (tid < kM2Pad / 16) P.pad = ld16(p0 + kSortBlock + e);
+}
+
+template <bool kSegs = false>
+__global__ __launch_bounds__(kM2Threads) void k_match2(DeflateJob job, int want_q) {
+    __shared__ __attribute__((aligned(16))) uint16_t Sr[kM2Ring];
+    __shared__ __attribute__((aligned(16))) uint8_t Bw[kM2Ring + kM2Pad];
+    __shared__ uint32_t next_c;
+    const int tid = threadIdx.x, lane = tid & 63;
+    // one workgroup per buffer, or (kSegs: job.seg pairs (buffer, first
+    // block), job.seg_len blocks each) per range of blocks; a range first
+    // stages the two blocks before its first one without walking them
+    const uint32_t bi = kSegs ? job.seg[2 * blockIdx.x] : blockIdx.x;
+    const uint32_t g = job.first + bi;
+    const int64_t n = (int64_t)job.src_len[g];
+    const uint8_t *in = job.src + job.src_off[g];
+    const uint32_t nblk = (uint32_t)((n + kSortBlock - 1) / kSortBlock);
+    const uint32_t w0 = kSegs ? job.seg[2 * blockIdx.x + 1] : 0u;
+    const uint32_t w1 = kSegs ? min(nblk, w0 + job.seg_len) : nblk;
+    const uint32_t t0 = w0 >= 2 ? w0 - 2 : 0u;
+    const uint16_t *gS = job.srt + job.ws_off[bi];
+    const uint4 *gW = job.work + job.ws_off[bi];
+    uint32_t *rf = job.rfull + job.ws_off[bi];
+    uint32_t *rq = job.rquart + job.ws_off[bi];
+    const LevelCfg cfg = job.cfg;
+    const int64_t max_dist = job_win(job).max_dist;
+    auto mcount = [&](uint32_t b) -> int {
+        const int64_t r = n - 2 - (int64_t)b * kSortBlock;
+        return r <= 0 ? 0 : (r < kSortBlock ? (int)r : kSortBlock);
+    };
+    M2Pre P;
+    if (t0 < w1) m2_prefetch(P, gS + (size_t)t0 * kSortBlock, mcount(t0), in, (int64_t)t0 * kSortBlock, n, tid);
+    for (uint32_t b = t0; b < w1; b++) {
+        const int64_t p0 = (int64_t)b * kSortBlock;
+        const int m = mcount(b);
+        // slide both rings down one block (b-1 -> slot 0, b -> slot 1); each
+        // thread moves its chunks in increasing order, and a chunk's source is
+        // one this same thread moves later, so nothing is overwritten unread
+        if (b > t0) {
+            uint4 *dS = reinterpret_cast<uint4 *>(Sr);
+            for (int c = tid; c < 2 * kSortBlock / 8; c += kM2Threads) {
+                uint4 v = dS[c + kSortBlock / 8];
+                typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+                auto sub = [](uint32_t x) {
+                    const us2 d = {(unsigned short)kSortBlock, (unsigned short)kSortBlock};
+                    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(us2, x) - d);
+                };
+                v = make_uint4(sub(v.x), sub(v.y), sub(v.z), sub(v.w));
+                dS[c] = v;
+            }
+            uint4 *dB = reinterpret_cast<uint4 *>(Bw);
+            for (int c = tid; c < 2 * kSortBlock / 16; c += kM2Threads) dB[c] = dB[c + kSortBlock / 16];
+            __syncthreads();
+        }
+        // block b into slot 2: entries as ring offsets (2 * kSortBlock + rel)
+        {
+            const uint32_t o = 2u * kSortBlock * 0x10001u;
+            uint4 *dS = reinterpret_cast<uint4 *>(Sr + 2 * kSortBlock + 16 * tid);
+            dS[0] = make_uint4(P.s0.x + o, P.s0.y + o, P.s0.z + o, P.s0.w + o);
+            dS[1] = make_uint4(P.s1.x + o, P.s1.y + o, P.s1.z + o, P.s1.w + o);
+            *reinterpret_cast<uint4 *>(Bw + 2 * kSortBlock + 16 * tid) = P.by;
+            if (tid < kM2Pad / 16) *reinterpret_cast<uint4 *>(Bw + 3 * kSortBlock + 16 * tid) = P.pad;
+        }
+        if (tid == 0) next_c = 0;
+        __syncthreads();
+        if (b + 1 < w1)                                 // lands during the walks
+            m2_prefetch(P, gS + (size_t)(b + 1) * kSortBlock, mcount(b + 1), in, p0 + kSortBlock, n, tid);
+        if (b >= w0) {
+            // positions the sort left out (p > n-3: no INSERT_STRING, no search)
+            for (int64_t x = p0 + m + tid; x < n && x < p0 + kSortBlock; x += kM2Threads) {
+                rf[x] = 0;
+                if (want_q) rq[x] = 0;
+            }
+            const int64_t base = p0 - 2 * kSortBlock;   // absolute position of ring offset 0
+            const uint4 *W = gW + p0;
+            for (;;) {
+                uint32_t c = 0;
+                if (lane == 0) c = atomicAdd(&next_c, 64u);
+                c = ufl(__shfl((int)c, 0, 64));
+                if (c >= (uint32_t)m) break;
+                const uint32_t j = c + lane;
+                if (j >= (uint32_t)m) continue;
+                const uint4 it = W[j];
+                const int i = (int)(it.x & 0xffffu), rel = (int)(it.x >> 16);
+                const uint32_t n0 = it.y & 0xffffu, n1 = it.y >> 16, e1 = it.z & 0xffffu, e2 = it.z >> 16;
+                const uint32_t n2 = it.w;
+                const int64_t p = p0 + rel;
+                const int vp = 2 * kSortBlock + rel;
+                // deflate.c:1955: the head must be within MAX_DIST (and not NIL,
+                // position 0); the chain continues above max(p - MAX_DIST, 0)
+                const int64_t labs = p > max_dist ? p - max_dist : 0;
+                const int lim = (int)(labs - base);
+                const uint32_t n01 = n0 + n1, n012 = n01 + n2;
+                const int A0 = 2 * kSortBlock + i - 1;
+                const int B1 = kSortBlock + (int)e1 - 1 + (int)n0;
+                const int B2 = (int)e2 - 1 + (int)n01;
+                const int h = (int)m2_cand(Sr, 0, A0, B1, B2, n0, n01, n012);
+                const int64_t hq = base + h;
+                if (n012 == 0 || hq < 1 || p - hq > max_dist) {
+                    rf[p] = 0;
+                    if (want_q) rq[p] = 0;
+                    continue;
+                }
+                m2_walk(Sr, Bw, vp, lim, A0, B1, B2, n0, n01, n012, p, n, cfg, rf, rq, want_q);
+            }
+        }
+        __syncthreads();
+    }
+}
+
 int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipStream_t st) {
     const dim3 grid(job.count);
     switch (stage) {

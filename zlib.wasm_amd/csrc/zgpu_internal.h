@@ -277,7 +277,28 @@ struct DeflateJob {
     uint32_t ntl;
     int fcmp;                // k_parse_fast: load 64 candidate bytes per chain step (A/B; 0: 16 first)
     SkipSpec sk;             // k_links: huff/rle stretches of a streaming job (n = 0: none)
+    // The sorted-run longest_match (k_bsort / k_bwork / k_match2, batch jobs at
+    // levels 4..9, hash_bits <= 15).  Each buffer is cut into blocks of
+    // kSortBlock positions; bblk[i] is buffer i's first block in the
+    // sub-batch's flat block numbering (count + 1 entries).
+    //  srt  [Σn] u16, position-indexed: block b's inserted positions (p <=
+    //       n-3), block-relative, sorted by (hash, position): the candidates of
+    //       a position in its block are the entries just before its own
+    //       within its hash's run;
+    //  boff [blocks * kSortOffStride] u16: per block, off[h] = the entries
+    //       with a hash below h (h = 0 .. hash_size), i.e. hash h's run;
+    //  work [Σn] uint4, position-indexed: per block, one work item per
+    //       sorted entry (its index, position, and its hash's runs in the
+    //       block and the two before it), each 4096-entry slice ordered by
+    //       candidate count so that walks of similar length share a wave.
+    const uint32_t *bblk;
+    uint16_t *srt;
+    uint16_t *boff;
+    uint4 *work;
 };
+// k_bsort's block (positions) and the stride of its per-block hash table
+constexpr int kSortBlock = 16384;
+constexpr int kSortOffStride = 32776;          // >= 32768 + 1, a multiple of 8
 
 // the per-job window/hash parameters (deflate.c:440-455)
 struct WinP {
