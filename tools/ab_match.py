@@ -14,9 +14,10 @@ import zgpu  # noqa: E402
 lib = sys.argv[1]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 level = int(sys.argv[3]) if len(sys.argv) > 3 else 6
-kind = {"silesia": zgpu.KIND_SILESIA, "enwik": zgpu.KIND_ENWIK}[sys.argv[4] if len(sys.argv) > 4 else "silesia"]
+kind = {"silesia": zgpu.KIND_SILESIA, "enwik": zgpu.KIND_ENWIK,
+        "vocab": zgpu.KIND_SMALLVOCAB}[sys.argv[4] if len(sys.argv) > 4 else "silesia"]
 zgpu.load(lib)
-n, B = 1 << 20, int(sys.argv[5]) if len(sys.argv) > 5 else 4096
+n, B = int(sys.argv[6]) if len(sys.argv) > 6 else 1 << 20, int(sys.argv[5]) if len(sys.argv) > 5 else 4096
 src = torch.empty(n * B, dtype=torch.uint8, device="cuda")
 zgpu.generate_dev(src, n, B, kind, seed=2025)
 cap = (zgpu.compress_bound(n) + 15) // 16 * 16
@@ -42,7 +43,8 @@ h_dst, dl = dst.cpu(), dlen.cpu()
 ok = all(h_dst[i * cap:i * cap + int(dl[i])].numpy().tobytes() ==
          zlib.compress(src[i * n:(i + 1) * n].cpu().numpy().tobytes(), level) for i in range(0, B, B // 8))
 key = "match" if level >= 4 else "parse_greedy"
-print(f"{lib}: {key} {stg[key][0] / stg[key][1]:.1f} ms/launch, step {el * 1e3:.1f} ms, exact {ok}",
+import os  # noqa: E402
+print(f"{lib} MATCH2={os.environ.get('ZGPU_MATCH2', '0')}: {key} {stg[key][0] / stg[key][1]:.1f} ms/launch, step {el * 1e3:.1f} ms, exact {ok}",
       flush=True)
 print("  stages ms per launch:", {k: round(v[0] / max(v[1], 1) * (v[1] / reps), 2) for k, v in stg.items() if v[1]},
       flush=True)

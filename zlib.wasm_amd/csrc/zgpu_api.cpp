@@ -253,6 +253,7 @@ struct Ctx {
     DevBuf ws_pg, ws_plane, ws_pbuf, ws_eplan, ws_wind, ws_tl;
     DevBuf ws_ck;             // split checksum partials (few large buffers)
     DevBuf ws_srec, ws_snap;  // a streaming job's block records and head[] snapshot
+    DevBuf ws_srt, ws_boff, ws_work, ws_bblk;   // the sorted-run match (k_bsort / k_bwork / k_match2)
     // inflate: match records, per-stream results, checks, offsets, stop codes
     DevBuf ws_mrec, ws_irec, ws_ick, ws_imeta, ws_istop;
     // the block-parallel decode of a lone stream (inflate_par): candidate lists,
@@ -260,6 +261,7 @@ struct Ctx {
     DevBuf ws_par1, ws_par2, ws_pjob, ws_psym, ws_pslot;
     hipStream_t aux = nullptr;
     hipEvent_t ev_links[2] = {nullptr, nullptr}, ev_match[2] = {nullptr, nullptr};
+    hipEvent_t ev_tail[2] = {nullptr, nullptr};   // the sorted-run pipeline: tail(s) done, slot s & 1 free
     // pinned host staging of single small crc32()/adler32() calls (checksum_small)
     uint8_t *pin = nullptr;
 };
@@ -584,6 +586,36 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
                           hipMemcpyAsync(c.ws_seg.p, segs.data(), 4 * segs.size(), hipMemcpyHostToDevice, st) !=
                               hipSuccess))
         return zfail(__LINE__);
+    // The sorted-run longest_match (k_bsort / k_bwork / k_match2) for batch
+    // jobs at levels 4..9 with hash_bits <= 15 and no per-segment match
+    // (ZGPU_MATCH2=0 keeps the chain-walk k_match everywhere).  Per sub-batch:
+    // its buffers' flat block numbering (bblk), sorted entries and work items
+    // (position-indexed, one slot: all three kernels run on one stream), and
+    // a hash table per block.
+    static const int match2_env = [] { const char *e = std::getenv("ZGPU_MATCH2"); return e ? std::atoi(e) : 0; }();
+    bool m2 = match2_env == 1 && slow && !fs && hbits <= 15 && segs.empty();
+    std::vector<uint32_t> bblk;
+    std::vector<size_t> bblk_at(nsub + 1, 0);
+    uint64_t max_sblk = 0;
+    if (m2) {
+        for (size_t sb = 0; sb < nsub; sb++) {
+            bblk_at[sb] = bblk.size();
+            uint32_t acc = 0;
+            for (uint32_t i = cuts[sb]; i < cuts[sb + 1]; i++) {
+                bblk.push_back(acc);
+                acc += (uint32_t)((lens[i] + kSortBlock - 1) / kSortBlock);
+            }
+            bblk.push_back(acc);
+            max_sblk = std::max<uint64_t>(max_sblk, acc);
+        }
+        bblk_at[nsub] = bblk.size();
+        if (!c.ws_srt.ensure(2 * max_pos + 64) || !c.ws_work.ensure(16 * max_pos + 64) ||
+            !c.ws_boff.ensure(2ull * kSortOffStride * max_sblk + 64) || !c.ws_bblk.ensure(4 * bblk.size() + 64) ||
+            hipMemcpyAsync(c.ws_bblk.p, bblk.data(), 4 * bblk.size(), hipMemcpyHostToDevice, st) != hipSuccess) {
+            (void)hipGetLastError();
+            m2 = false;                                 // no room: the chain-walk path
+        }
+    }
     // ... and, for a batch (no streaming job), the lazy parse and the encoder
     // too: k_pbig* over segments of pseg bytes (>= 1 KiB; ~64 Ki lanes per
     // sub-batch), kParseLanes lanes per workgroup, k_enc_* per block.  One
@@ -730,6 +762,13 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             }
         }
         job.maxblk = maxblk_of[s];
+        if (m2) {
+            job.bblk = c.ws_bblk.as<uint32_t>() + bblk_at[s];
+            job.srt = c.ws_srt.as<uint16_t>();
+            job.boff = c.ws_boff.as<uint16_t>();
+            job.work = c.ws_work.as<uint4>();
+            job.nsblk = bblk[bblk_at[s + 1] - 1];
+        }
         static const int fcmp64 = std::getenv("ZGPU_FAST_CMP64") != nullptr;   // A/B: k_parse_fast's compare
         job.fcmp = fcmp64;
         if (block_enc) job.eplan = c.ws_eplan.as<EncPlan>();
@@ -807,7 +846,29 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         return ZGPU_OK;
     };
 
-    if (!piped) {
+    if (m2) {
+        // aux (or the caller's stream): [wait tail(s-2)] sort, work items, match of s;
+        // caller's: [wait match(s)] tail(s).  S / work / boff have one slot (the
+        // aux stream orders them); rfull / rquart / pstate alternate (slot s & 1),
+        // and match(s) waits for tail(s-2), the last reader of its slot.
+        hipStream_t ax = piped ? c.aux : st;
+        if (piped)
+            for (int k = 0; k < 2; k++)
+                if (!c.ev_tail[k] && hipEventCreateWithFlags(&c.ev_tail[k], hipEventDisableTiming) != hipSuccess)
+                    return zfail(__LINE__);
+        for (size_t s = 0; s < nsub; s++) {
+            const DeflateJob job = make_job(s);
+            if (piped && s >= 2 && hipStreamWaitEvent(ax, c.ev_tail[s & 1], 0) != hipSuccess) return zfail(__LINE__);
+            if (T.run(1, ax, [&] { return launch_deflate_stage(14, job, nullptr, ax); })) return zfail(__LINE__);
+            if (T.run(2, ax, [&] { return launch_deflate_stage(15, job, nullptr, ax); })) return zfail(__LINE__);
+            if (piped) {
+                if (hipEventRecord(c.ev_match[s & 1], ax) != hipSuccess) return zfail(__LINE__);
+                if (hipStreamWaitEvent(st, c.ev_match[s & 1], 0) != hipSuccess) return zfail(__LINE__);
+            }
+            if (int rc = tail(s, job)) return rc;
+            if (piped && hipEventRecord(c.ev_tail[s & 1], st) != hipSuccess) return zfail(__LINE__);
+        }
+    } else if (!piped) {
         for (size_t s = 0; s < nsub; s++) {
             const DeflateJob job = make_job(s);
             if (slow) {

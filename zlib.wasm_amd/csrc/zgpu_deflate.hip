@@ -4689,6 +4689,17 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         if (job.srec) hipLaunchKernelGGL(k_enc_rec, dim3((job.maxblk + 255) / 256), dim3(256), 0, st, job);
         break;
     }
+    case 14:                                                // the sorted-run match: sort, work items
+        if (job.nsblk) {
+            hipLaunchKernelGGL(k_bsort, dim3(job.nsblk), dim3(kBSThreads), 0, st, job);
+            hipLaunchKernelGGL(k_bwork, dim3(job.nsblk), dim3(kBSThreads), 0, st, job);
+        }
+        break;
+    case 15: {
+        const int wq = (int)(job.cfg.good < job.cfg.lazy) | job.cfg_q;
+        hipLaunchKernelGGL(k_match2<false>, grid, dim3(kM2Threads), 0, st, job, wq);
+        break;
+    }
     case 7: hipLaunchKernelGGL(k_parse_huff, grid, dim3(kHuffThreads), 0, st, job); break;
     case 8: hipLaunchKernelGGL(k_parse_rle, grid, dim3(64), 0, st, job); break;
     case 9: hipLaunchKernelGGL(k_count<false>, grid, dim3(kCntThreads), 0, st, job); break;

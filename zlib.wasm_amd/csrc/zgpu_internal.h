@@ -292,6 +292,7 @@ struct DeflateJob {
     //       block and the two before it), each 4096-entry slice ordered by
     //       candidate count so that walks of similar length share a wave.
     const uint32_t *bblk;
+    uint32_t nsblk;          // blocks in the sub-batch (k_bsort / k_bwork grid)
     uint16_t *srt;
     uint16_t *boff;
     uint4 *work;
