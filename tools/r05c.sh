@@ -1,0 +1,13 @@
+#!/bin/bash
+# L1-3 from the sorted runs (ZGPU_FAST_SRT=1): lone-buffer speed and exactness
+# against the one-wave k_parse_fast, then the L1-3 goldens with it on
+set -o pipefail
+O=gpurun_out/r05c
+mkdir -p $O
+export TMPDIR=/tmp
+ZGPU_FAST_SRT=1 timeout -k 10 200 python3 -u tools/lone_fast.py 1,2,3 1,16 text,mix > $O/lone_srt.log 2>&1 || { echo "srt failed"; tail -20 $O/lone_srt.log; exit 1; }
+grep -v amdgpu.ids $O/lone_srt.log
+timeout -k 10 200 python3 -u tools/lone_fast.py 1,3 1 text,mix > $O/lone_fast.log 2>&1 || { echo "fast failed"; tail -20 $O/lone_fast.log; exit 1; }
+grep -v amdgpu.ids $O/lone_fast.log
+ZGPU_FAST_SRT=1 timeout -k 10 600 python3 -u -m pytest tests/test_gpu.py -x -q --timeout 300 --timeout-method thread -k "golden or fast or sweep or batch" > $O/tests.log 2>&1 || { echo "tests failed"; tail -30 $O/tests.log; exit 1; }
+tail -2 $O/tests.log

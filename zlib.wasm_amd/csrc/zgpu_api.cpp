@@ -594,10 +594,14 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     // a hash table per block.
     static const int match2_env = [] { const char *e = std::getenv("ZGPU_MATCH2"); return e ? std::atoi(e) : 0; }();
     bool m2 = match2_env == 1 && slow && !fs && hbits <= 15 && segs.empty();
+    // levels 1..3 of a batch job from the same sorted runs (k_bwork<true> +
+    // k_parse_srt; ZGPU_FAST_SRT=1)
+    static const int fsrt_env = [] { const char *e = std::getenv("ZGPU_FAST_SRT"); return e ? std::atoi(e) : 0; }();
+    bool fsrt = fsrt_env == 1 && level >= 1 && level <= 3 && !huff && !rle && !fs && hbits <= 15;
     std::vector<uint32_t> bblk;
     std::vector<size_t> bblk_at(nsub + 1, 0);
     uint64_t max_sblk = 0;
-    if (m2) {
+    if (m2 || fsrt) {
         for (size_t sb = 0; sb < nsub; sb++) {
             bblk_at[sb] = bblk.size();
             uint32_t acc = 0;
@@ -613,7 +617,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             !c.ws_boff.ensure(2ull * kSortOffStride * max_sblk + 64) || !c.ws_bblk.ensure(4 * bblk.size() + 64) ||
             hipMemcpyAsync(c.ws_bblk.p, bblk.data(), 4 * bblk.size(), hipMemcpyHostToDevice, st) != hipSuccess) {
             (void)hipGetLastError();
-            m2 = false;                                 // no room: the chain-walk path
+            m2 = fsrt = false;                          // no room: the chain-walk paths
         }
     }
     // ... and, for a batch (no streaming job), the lazy parse and the encoder
@@ -762,7 +766,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             }
         }
         job.maxblk = maxblk_of[s];
-        if (m2) {
+        if (m2 || fsrt) {
             job.bblk = c.ws_bblk.as<uint32_t>() + bblk_at[s];
             job.srt = c.ws_srt.as<uint16_t>();
             job.boff = c.ws_boff.as<uint16_t>();
@@ -837,6 +841,9 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             const int ps = job.pgrp ? 11 : 5;                  // few large buffers: k_pbig*
             if (T.run(3, st, [&] { return launch_deflate_stage(ps, job, nullptr, st); })) return zfail(__LINE__);
             if (T.run(3, st, [&] { return launch_deflate_stage(6, job, nullptr, st); })) return zfail(__LINE__);
+        } else if (level >= 1 && fsrt) {
+            if (T.run(1, st, [&] { return launch_deflate_stage(14, job, nullptr, st); })) return zfail(__LINE__);
+            if (T.run(4, st, [&] { return launch_deflate_stage(16, job, nullptr, st); })) return zfail(__LINE__);
         } else if (level >= 1) {
             uint32_t *heads = c.ws_heads.as<uint32_t>();
             if (T.run(4, st, [&] { return launch_deflate_stage(3, job, heads, st); })) return zfail(__LINE__);

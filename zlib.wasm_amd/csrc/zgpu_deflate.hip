@@ -4204,6 +4204,10 @@ __global__ __launch_bounds__(kBSThreads) void k_bsort(DeflateJob job) {
 // (capped at the chain budget; k_count's key), longest first, so the 64
 // walks of a wave have similar lengths (tools/model/model_sortwalk.c: 98.6 %
 // SIMT utilisation at L6 against 78 % in plain sorted order).
+// kPos (levels 1..3, k_parse_srt): the items are stored by position
+// instead (work[rel] for the block's position rel; no count sort), for the
+// sequential parse to read in position order.
+template <bool kPos>
 __global__ __launch_bounds__(kBSThreads) void k_bwork(DeflateJob job) {
     __shared__ uint16_t S[kSortBlock];
     __shared__ uint16_t off[kSortOffStride];
@@ -4244,9 +4248,14 @@ __global__ __launch_bounds__(kBSThreads) void k_bwork(DeflateJob job) {
         const uint32_t s1 = o1 ? o1[h] : 0u, e1 = o1 ? o1[h + 1] : 0u;
         const uint32_t s2 = o2 ? o2[h] : 0u, e2 = o2 ? o2[h + 1] : 0u;
         it[u] = make_uint4((uint32_t)i | rel << 16, n0 | (e1 - s1) << 16, e1 | e2 << 16, e2 - s2);
+        if (kPos) {
+            job.work[job.ws_off[bi] + p0 + rel] = it[u];
+            continue;
+        }
         const uint32_t c = n0 + (e1 - s1) + (e2 - s2);
         bk[u] = 63 - (int)(walk_key(c, chain) >> 2);
     }
+    if (kPos) return;
 #pragma unroll
     for (int u = 0; u < kBSPer; u++)
         if (tid + u * kBSThreads < m) rk[u] = atomicAdd(&s_hist[u / (kBSlice / kBSThreads)][bk[u]], 1);
@@ -4598,6 +4607,253 @@ __global__ __launch_bounds__(kM2Threads) void k_match2(DeflateJob job, int want_
     }
 }
 
+// ------------------------------------------------------------------------
+// k_parse_srt — deflate_fast (levels 1..3, deflate.c:1824-1915) of a batch
+// job from the sorted runs (k_bsort, k_bwork<true>).  One wave per buffer,
+// the CU's LDS holding the sorted entries and bytes of the blocks b-2..b of
+// the parse position (as k_match2) and a bitmap of the positions deflate_fast
+// has inserted (blocks b-2..b+1).
+//
+// deflate_fast searches the chain of INSERTED positions: a position strictly
+// inside a match longer than max_insert_length is not inserted (:1873-1897).
+// That chain is the sorted run of p's hash, most recent first, without the
+// positions whose bit is clear (exact).  So a decision
+// reads up to 64 candidates at once -- lane k takes the k-th same-hash
+// position before p -- tests their bits, takes the first `chain` inserted ones
+// above the limit (the head at exactly MAX_DIST included, deflate.c:1853) and
+// compares them side by side; the first reaching nice, else the first
+// longest, is longest_match's result (:1417-1497).  No link is chased and no
+// head[] / prev[] is kept: the run info of the next 64 positions is loaded
+// ahead, and every other access is to LDS.
+// ------------------------------------------------------------------------
+constexpr int kPSBits = 4 * kSortBlock / 32;        // bitmap words: blocks b-2 .. b+1
+
+template <typename P>
+__global__ __launch_bounds__(64) void k_parse_srt(DeflateJob job) {
+    __shared__ __attribute__((aligned(16))) uint16_t Sr[kM2Ring];
+    __shared__ __attribute__((aligned(16))) uint8_t Bw[kM2Ring + kM2Pad];
+    __shared__ uint32_t Bi[kPSBits];
+    const int lane = threadIdx.x;
+    const uint64_t below = (1ull << lane) - 1ull;
+    const uint32_t bi = blockIdx.x;
+    const uint32_t g = job.first + bi;
+    const P n = (P)job.src_len[g];
+    const uint8_t *in = job.src + job.src_off[g];
+    const uint16_t *gS = job.srt + job.ws_off[bi];
+    const uint4 *gW = job.work + job.ws_off[bi];
+    const WinP wp = job_win(job);
+    const LevelCfg cfg = job.cfg;
+    ParseOutT<P> po;
+    po.sym = job.sym + job.ws_off[bi];
+    po.blk = job.blocks + job.blk_off[bi];
+    po.nsym = po.blk_nsym = po.blk_sym_start = po.nblk = 0;
+    po.win(wp);
+    po.block_start = 0; po.S = 0; po.E = 0;
+    po.lead = true;
+    po.vaddr = true;
+    const P max_dist = (P)wp.max_dist;
+    auto mcount = [&](P b) -> int {
+        const P r = n - 2 - b * kSortBlock;
+        return r <= 0 ? 0 : (r < kSortBlock ? (int)r : kSortBlock);
+    };
+    auto ld16 = [&](P x) -> uint4 {                     // 16 input bytes from x, zero outside [0, n)
+        if (x >= 0 && x + 16 <= n) {
+            const uintptr_t a = reinterpret_cast<uintptr_t>(in + x);
+            const uint32_t sh = (uint32_t)(a & 3u);
+            const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+            if (sh == 0) return make_uint4(q[0], q[1], q[2], q[3]);
+            const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
+            return make_uint4(__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                              __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh));
+        }
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (int j = 0; j < 16; j++)
+            if (x + j >= 0 && x + j < n) w[j >> 2] |= (uint32_t)in[x + j] << (8 * (j & 3));
+        return make_uint4(w[0], w[1], w[2], w[3]);
+    };
+    // block b into ring slot 2 (entries as ring offsets), its bytes + pad, and
+    // its bitmap slot b+1 (slot 3) cleared; slide first unless b == 0
+    auto load_block = [&](P b) {
+        if (b > 0) {
+            uint4 *dS = reinterpret_cast<uint4 *>(Sr);
+            typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+            auto sub = [](uint32_t x) {
+                const us2 d = {(unsigned short)kSortBlock, (unsigned short)kSortBlock};
+                return __builtin_bit_cast(uint32_t, __builtin_bit_cast(us2, x) - d);
+            };
+            for (int c = lane; c < 2 * kSortBlock / 8; c += 64) {
+                const uint4 v = dS[c + kSortBlock / 8];
+                dS[c] = make_uint4(sub(v.x), sub(v.y), sub(v.z), sub(v.w));
+            }
+            uint4 *dB = reinterpret_cast<uint4 *>(Bw);
+            for (int c = lane; c < 2 * kSortBlock / 16; c += 64) dB[c] = dB[c + kSortBlock / 16];
+            for (int c = lane; c < 3 * kSortBlock / 32; c += 64) Bi[c] = Bi[c + kSortBlock / 32];
+        } else {
+            for (int c = lane; c < kPSBits; c += 64) Bi[c] = 0;
+        }
+        for (int c = lane; c < kSortBlock / 32; c += 64) Bi[3 * kSortBlock / 32 + c] = 0;
+        const int m = mcount(b);
+        const uint16_t *src = gS + b * kSortBlock;
+        for (int e = 8 * lane; e < kSortBlock; e += 512) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (e + 8 <= m) v = *reinterpret_cast<const uint4 *>(src + e);
+            else if (e < m) {
+                uint32_t w[4] = {0, 0, 0, 0};
+                for (int j = 0; j < 8 && e + j < m; j++) w[j >> 1] |= (uint32_t)src[e + j] << (16 * (j & 1));
+                v = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+            const uint32_t o = 2u * kSortBlock * 0x10001u;
+            *reinterpret_cast<uint4 *>(Sr + 2 * kSortBlock + e) = make_uint4(v.x + o, v.y + o, v.z + o, v.w + o);
+        }
+        const P p0 = b * kSortBlock;
+        for (int c = lane; c < (kSortBlock + kM2Pad) / 16; c += 64)
+            *reinterpret_cast<uint4 *>(Bw + 2 * kSortBlock + 16 * c) = ld16(p0 + 16 * c);
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+    };
+    // run info of positions [rb, rb + 64) in lanes (cur), the next 64 (nxt)
+    P rb = 0;
+    uint4 cur = make_uint4(0, 0, 0, 0), nxt = cur;
+    auto ri_load = [&](P x) -> uint4 { return x + lane < n ? gW[x + lane] : make_uint4(0, 0, 0, 0); };
+    P blk = 0;                                          // the block in ring slot 2
+    if (n > 0) {
+        load_block(0);
+        cur = ri_load(0);
+        nxt = ri_load(64);
+    }
+    const P nblk = (n + kSortBlock - 1) / kSortBlock;
+    P p = 0;
+    uint32_t match_length = 0;
+    while (p < n) {
+        if (po.E - p < kMinLookahead) po.fill(p, n);
+        while (p >= (blk + 1) * kSortBlock && blk + 1 < nblk) load_block(++blk);
+        if (p >= rb + 64) {
+            if (p < rb + 128) { cur = nxt; rb += 64; }
+            else { rb = p & ~(P)63; cur = ri_load(rb); }
+            nxt = ri_load(rb + 64);
+        }
+        const P base = blk * kSortBlock - 2 * kSortBlock;   // absolute position of ring offset 0
+        const P lookahead = po.E - p;
+        const int vp = (int)(p - base);
+        uint32_t best = kMinMatch - 1, bq = 0;
+        if (lookahead >= kMinMatch) {
+            // INSERT_STRING(p): its bit goes in after the search (p is no candidate of itself)
+            const int o = (int)(p - rb);
+            const uint32_t ix = (uint32_t)__builtin_amdgcn_readlane((int)cur.x, o);
+            const uint32_t iy = (uint32_t)__builtin_amdgcn_readlane((int)cur.y, o);
+            const uint32_t iz = (uint32_t)__builtin_amdgcn_readlane((int)cur.z, o);
+            const uint32_t n2 = (uint32_t)__builtin_amdgcn_readlane((int)cur.w, o);
+            const int i = (int)(ix & 0xffffu);
+            const uint32_t n0 = iy & 0xffffu, n01 = n0 + (iy >> 16), n012 = n01 + n2;
+            const int A0 = 2 * kSortBlock + i - 1, B1 = kSortBlock + (int)(iz & 0xffffu) - 1 + (int)n0,
+                      B2 = (int)(iz >> 16) - 1 + (int)n01;
+            const P limit = (p - po.S) > max_dist ? p - max_dist : po.S;
+            const int lim = (int)(limit - base);
+            const int nice = lookahead < (P)cfg.nice ? (int)lookahead : (int)cfg.nice;
+            const P rem = n - p;
+            const int maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
+            uint32_t chain = cfg.chain;                   // prev_length == 2 < good: no quartering
+            bool head = false, done = n012 == 0;
+            for (uint32_t k0 = 0; !done; k0 += 64) {
+                const uint32_t k = k0 + (uint32_t)lane;
+                const int q = (int)m2_cand(Sr, k, A0, B1, B2, n0, n01, n012);
+                const bool valid = k < n012;
+                const bool ins = valid && ((Bi[(uint32_t)q >> 5] >> ((uint32_t)q & 31u)) & 1u);
+                const uint64_t insm = __ballot(ins);
+                uint64_t elig;
+                int hl = -1;
+                if (!head) {
+                    if (insm == 0) {                      // no inserted candidate in these 64
+                        if (k0 + 64 >= n012) break;
+                        continue;
+                    }
+                    // the head (hash_head): within the window and MAX_DIST, else no search
+                    hl = __builtin_ctzll(insm);
+                    const int hq = __builtin_amdgcn_readlane(q, hl);
+                    const P hqa = base + hq;
+                    if (!(hqa > po.S && p - hqa <= max_dist)) break;
+                    head = true;
+                }
+                // after the head, the chain visits inserted candidates while they
+                // lie above the limit (positions only go down from lane to lane),
+                // `chain` of them at most
+                elig = __ballot(ins && (lane == hl || q > lim));
+                const uint64_t stopm = __ballot(ins && lane != hl && q <= lim);
+                const uint64_t vis = elig;
+                const uint32_t pre = (uint32_t)__popcll(vis & below);
+                const bool mine = ((vis >> lane) & 1ull) && pre < chain;
+                const uint32_t nv = (uint32_t)min((uint64_t)chain, (uint64_t)__popcll(vis));
+                int len = 0;
+                if (mine) {
+                    uint32_t a0, a1, a2, a3, c0, c1, c2, c3;
+                    b16(Bw, q, a0, a1, a2, a3);
+                    b16(Bw, vp, c0, c1, c2, c3);
+                    len = diff16(a0 ^ c0, a1 ^ c1, a2 ^ c2, a3 ^ c3);
+                    while (len >= 16 && len < nice) {
+                        b16(Bw, q + len, a0, a1, a2, a3);
+                        b16(Bw, vp + len, c0, c1, c2, c3);
+                        const int r = diff16(a0 ^ c0, a1 ^ c1, a2 ^ c2, a3 ^ c3);
+                        len += r;
+                        if (r < 16) break;
+                    }
+                    len = len < nice ? len : nice;
+                }
+                // the first to reach nice, else the first longest (strictly longer wins)
+                const uint64_t nm = __ballot(mine && len >= nice);
+                int wl = -1, wlen = 0;
+                if (nm) {
+                    wl = __builtin_ctzll(nm);
+                    wlen = nice;
+                } else {
+                    uint32_t key = mine ? ((uint32_t)len << 8) | (uint32_t)(63 - lane) : 0u;
+#pragma unroll
+                    for (int sh = 1; sh < 64; sh <<= 1) key = max(key, (uint32_t)__shfl_xor((int)key, sh, 64));
+                    key = ufl(key);
+                    if ((key >> 8) > best) { wl = 63 - (int)(key & 0xffu); wlen = (int)(key >> 8); }
+                }
+                if (wl >= 0 && (uint32_t)wlen > best) {
+                    best = (uint32_t)wlen;
+                    bq = (uint32_t)__builtin_amdgcn_readlane(q, wl);
+                }
+                chain -= nv;
+                done = nm != 0 || chain == 0 || stopm != 0 || k0 + 64 >= n012;
+            }
+            if (best >= (uint32_t)nice && best >= kMinMatch) {
+                // the winner's true length, past nice up to maxcmp (64 bytes a round)
+                int L = (int)best;
+                while (L < maxcmp) {
+                    const int kk = L + lane;
+                    const int kc = kk < maxcmp ? kk : maxcmp - 1;
+                    const uint64_t mm = __ballot((kk < maxcmp) & (Bw[bq + kc] != Bw[vp + kc]));
+                    if (mm) { L += __builtin_ctzll(mm); break; }
+                    L += 64;
+                    if (L > maxcmp) L = maxcmp;
+                }
+                best = (uint32_t)(L < maxcmp ? L : maxcmp);
+            }
+            if (lane == 0) atomicOr(&Bi[(uint32_t)vp >> 5], 1u << ((uint32_t)vp & 31u));
+        }
+        match_length = best <= (uint32_t)lookahead ? best : (uint32_t)lookahead;
+        bool bflush;
+        if (match_length >= kMinMatch) {
+            bflush = po.tally(((uint32_t)(vp - (int)bq) << 8) | (match_length - kMinMatch));
+            const P la = lookahead - (P)match_length;
+            if (match_length <= cfg.lazy && la >= kMinMatch) {
+                // the strings inside a short match are inserted (deflate.c:1873-1884)
+                const uint32_t v = (uint32_t)vp + (uint32_t)lane + 1u;
+                if ((uint32_t)lane < match_length - 1u) atomicOr(&Bi[v >> 5], 1u << (v & 31u));
+            }
+            p += match_length;
+        } else {
+            bflush = po.tally((uint32_t)Bw[vp]);
+            p++;
+        }
+        if (bflush) po.flush(p, false);
+    }
+    po.flush(p, true);
+    if (lane == 0) job.nblocks[bi] = po.nblk;
+}
+
 int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipStream_t st) {
     const dim3 grid(job.count);
     switch (stage) {
@@ -4692,8 +4948,13 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     case 14:                                                // the sorted-run match: sort, work items
         if (job.nsblk) {
             hipLaunchKernelGGL(k_bsort, dim3(job.nsblk), dim3(kBSThreads), 0, st, job);
-            hipLaunchKernelGGL(k_bwork, dim3(job.nsblk), dim3(kBSThreads), 0, st, job);
+            if (job.level >= 4) hipLaunchKernelGGL(k_bwork<false>, dim3(job.nsblk), dim3(kBSThreads), 0, st, job);
+            else hipLaunchKernelGGL(k_bwork<true>, dim3(job.nsblk), dim3(kBSThreads), 0, st, job);
         }
+        break;
+    case 16:                                                // levels 1..3 from the sorted runs
+        if (job.pos31) hipLaunchKernelGGL(k_parse_srt<int32_t>, grid, dim3(64), 0, st, job);
+        else hipLaunchKernelGGL(k_parse_srt<int64_t>, grid, dim3(64), 0, st, job);
         break;
     case 15: {
         const int wq = (int)(job.cfg.good < job.cfg.lazy) | job.cfg_q;
