@@ -296,6 +296,11 @@ struct DeflateJob {
     uint16_t *srt;
     uint16_t *boff;
     uint4 *work;
+    // k_parse_srt of a streaming job (levels 1..3, Z_NO_FLUSH stops only):
+    // the inserted-position bitmap it leaves (1 bit per position), from which
+    // k_srt_chains rebuilds head[] and prev[] at the last cut (job.snap,
+    // job.link) for the job that resumes there on k_parse_fast
+    uint32_t *ins_bits;
 };
 // k_bsort's block (positions) and the stride of its per-block hash table
 constexpr int kSortBlock = 16384;
