@@ -1,6 +1,7 @@
 #!/bin/bash
 # L1-3 from the sorted runs (ZGPU_FAST_SRT=1): lone-buffer speed and exactness
-# against the one-wave k_parse_fast, then the L1-3 goldens with it on
+# against the one-wave k_parse_fast, the L1-3 goldens, the stream sessions and
+# a 256 MiB L1 streaming job with it on
 set -o pipefail
 O=gpurun_out/r05c
 mkdir -p $O
@@ -11,3 +12,7 @@ timeout -k 10 200 python3 -u tools/lone_fast.py 1,3 1 text,mix > $O/lone_fast.lo
 grep -v amdgpu.ids $O/lone_fast.log
 ZGPU_FAST_SRT=1 timeout -k 10 600 python3 -u -m pytest tests/test_gpu.py -x -q --timeout 300 --timeout-method thread -k "golden or fast or sweep or batch" > $O/tests.log 2>&1 || { echo "tests failed"; tail -30 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
+ZGPU_FAST_SRT=1 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_stream.py -x -q --timeout 300 --timeout-method thread > $O/stream_tests.log 2>&1 || { echo "stream tests failed"; tail -30 $O/stream_tests.log; exit 1; }
+tail -2 $O/stream_tests.log
+ZGPU_FAST_SRT=1 timeout -k 10 300 python3 -u tools/stream_stages.py 256 1 > $O/stream256.log 2>&1 || { echo "stream256 failed"; tail -20 $O/stream256.log; exit 1; }
+grep -v amdgpu.ids $O/stream256.log

@@ -1,7 +1,7 @@
 """Where a large streaming deflate() job spends its time (one GPU): one
 deflate(Z_NO_FLUSH) call with N MiB of input, then Z_FINISH, at levels 1/6/9,
 with the library's per-stage HIP-event timing (zgpu_stage_timing) around it.
-Usage: python tools/stream_stages.py [MiB]"""
+Usage: python tools/stream_stages.py [MiB] [levels, e.g. 1,6,9]"""
 import faulthandler
 import os
 import sys
@@ -21,7 +21,8 @@ def main():
     faulthandler.enable()
     cap = len(data) + (len(data) >> 8) + (1 << 16)
     L = zgpu.load()
-    for level in (1, 6, 9):
+    levels = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 6, 9]
+    for level in levels:
         print(f"L{level} {mib} MiB ...", flush=True)
         zgpu.compress2(data[:65536], level)
         zgpu.stage_timing(True)

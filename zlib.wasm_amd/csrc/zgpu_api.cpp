@@ -254,6 +254,7 @@ struct Ctx {
     DevBuf ws_ck;             // split checksum partials (few large buffers)
     DevBuf ws_srec, ws_snap;  // a streaming job's block records and head[] snapshot
     DevBuf ws_srt, ws_boff, ws_work, ws_bblk;   // the sorted-run match (k_bsort / k_bwork / k_match2)
+    DevBuf ws_ibits;                            // k_parse_srt's inserted-position bitmap (streaming jobs)
     // inflate: match records, per-stream results, checks, offsets, stop codes
     DevBuf ws_mrec, ws_irec, ws_ick, ws_imeta, ws_istop;
     // the block-parallel decode of a lone stream (inflate_par): candidate lists,
@@ -434,6 +435,7 @@ struct FlushSpec {
     int zp0 = kMinMatch - 1, zm0 = kMinMatch - 1;   // DeflateJob::zp0 / zm0
     int seg_parse = 0;             // the job's stops are all Z_NO_FLUSH: k_pbig* may parse it (k_pbig6s)
     SkipSpec sk{};                 // DeflateJob::sk
+    int srt_parse = 0;             // levels 1..3, stops only, from the stream's start: k_parse_srt<kEv>
 };
 
 // deflateInit2_'s windowBits / memLevel rules (deflate.c:400-425): negative
@@ -597,7 +599,11 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     // levels 1..3 of a batch job from the same sorted runs (k_bwork<true> +
     // k_parse_srt; ZGPU_FAST_SRT=1)
     static const int fsrt_env = [] { const char *e = std::getenv("ZGPU_FAST_SRT"); return e ? std::atoi(e) : 0; }();
-    bool fsrt = fsrt_env == 1 && level >= 1 && level <= 3 && !huff && !rle && !fs && hbits <= 15;
+    bool fsrt = fsrt_env == 1 && level >= 1 && level <= 3 && !huff && !rle && (!fs || fs->srt_parse) && hbits <= 15;
+    if (fsrt && fs && (!c.ws_ibits.ensure(max_pos / 8 + 256) || !fs->snap)) {
+        (void)hipGetLastError();
+        return zfail(__LINE__);
+    }
     std::vector<uint32_t> bblk;
     std::vector<size_t> bblk_at(nsub + 1, 0);
     uint64_t max_sblk = 0;
@@ -772,6 +778,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.boff = c.ws_boff.as<uint16_t>();
             job.work = c.ws_work.as<uint4>();
             job.nsblk = bblk[bblk_at[s + 1] - 1];
+            if (fs) job.ins_bits = c.ws_ibits.as<uint32_t>();
         }
         static const int fcmp64 = std::getenv("ZGPU_FAST_CMP64") != nullptr;   // A/B: k_parse_fast's compare
         job.fcmp = fcmp64;
@@ -957,6 +964,7 @@ struct FlushHost {
     int keep_head = 0;
     int zp0 = kMinMatch - 1, zm0 = kMinMatch - 1;   // DeflateJob::zp0 / zm0
     int seg_parse = 0;                 // see FlushSpec
+    int srt_parse = 0;                 // see FlushSpec
     SkipSpec sk{};                     // see FlushSpec
 };
 
@@ -1055,6 +1063,7 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
         fs.zp0 = fh->zp0;
         fs.zm0 = fh->zm0;
         fs.seg_parse = fh->seg_parse;
+        fs.srt_parse = fh->srt_parse;
         fs.sk = fh->sk;
         if (fh->rec_out) {
             const size_t sym_limit = (size_t(1) << (mem_level + 6)) - 1;         // lit_bufsize - 1
@@ -2605,6 +2614,18 @@ int deflate_part(internal_state *s, bool closed) {
     if (!closed && nev == 0) stops_only = false;
     for (size_t i = 0; stops_only && i < nev; i++) stops_only = s->ev_type[s->res_ev + i] == 0;
     fh.seg_parse = stops_only ? 1 : 0;
+    // deflate_fast over Z_NO_FLUSH stops from the stream's start (a large
+    // deflate() call, compress2 over 4 GiB at levels 1..3): k_parse_srt, the
+    // block-parallel encoder, and the chains at the last cut rebuilt for the
+    // job that resumes there (k_srt_chains)
+    {
+        static const int fsrt_env = [] { const char *e = std::getenv("ZGPU_FAST_SRT"); return e ? std::atoi(e) : 0; }();
+        bool srt = fsrt_env == 1 && fast && s->mem_level <= 8 && fh.start == 0 && !fh.dict && !fh.head_in &&
+                   cpos.empty() && fh.lk_n == 0 && fh.zp0 == kMinMatch - 1 && fh.zm0 == kMinMatch - 1 &&
+                   fh.sk.n == 0 && sl >= seg_min && (closed || nev > 0);
+        for (size_t i = 0; srt && i < nev; i++) srt = s->ev_type[s->res_ev + i] == 0;
+        if (srt) fh.srt_parse = fh.seg_parse = 1;
+    }
     ZTRACE("part: base %zu nev %zu sl %zu cap %zu start %u bit0 %u e0 %u cut %d fast %d\n", base, nev, sl, cap,
            fh.start, fh.bit0, fh.e0, fh.cut, (int)fast);
     {
