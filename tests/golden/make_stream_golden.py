@@ -76,6 +76,29 @@ def main():
         cases.append({"kind": kind, "n": n, "seed": seed, "level": level, "strategy": strategy, "wbits": wbits,
                       "mem": mem, "plan": plan, "recs": recs, "len": len(whole),
                       "sha256": hashlib.sha256(whole).hexdigest()})
+    # level 0 with output buffers smaller than a stored block (round 5: deflate_stored
+    # then cuts blocks by avail_out and goes through the pending buffer,
+    # deflate.c:1635-1815); their own rng, so the sessions above stay as they were
+    rng0 = np.random.default_rng(1977)
+    for t in range(30):
+        kind = kinds[t % 7]
+        out = [1, 7, 100, 700, 5000, 40000][t % 6]
+        n = int(rng0.choice([300, 3000, 5000])) if out <= 7 else int(rng0.choice([3000, 70000, 200000]))
+        wbits = int(rng0.choice([15, -15, 31, 9]))
+        data = datagen.make(kind, n, 2000 + t)
+        if t % 3 == 0:
+            plan = [(n, 0, out, True), (0, 4, out, True)]
+        elif t % 3 == 1:
+            plan = zpipe_plan(rng0, n, int(rng0.choice([1000, 3000, 70000])), out, t % 2 == 1)
+        else:
+            plan = free_plan(rng0, n)
+            plan = [(take, f, min(o, out) if out > 7 else out, loop) for take, f, o, loop in plan]
+        recs, whole = run_dsession(ref.L, data, plan, 0, wbits, 8, 0)
+        if len(recs) >= 6000 or not recs or recs[-1][0] != 1:
+            continue
+        cases.append({"kind": kind, "n": n, "seed": 2000 + t, "level": 0, "strategy": 0, "wbits": wbits,
+                      "mem": 8, "plan": plan, "recs": recs, "len": len(whole),
+                      "sha256": hashlib.sha256(whole).hexdigest()})
     with open(os.path.join(HERE, "stream_golden.json"), "w") as f:
         json.dump({"reference": ref.version.decode(), "cases": cases}, f, separators=(",", ":"))
     print(len(cases), "cases", sum(len(c["recs"]) for c in cases), "calls")
