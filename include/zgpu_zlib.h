@@ -25,8 +25,10 @@
  * avail_out is used up, consuming only the input the reference had read by
  * then (avail_in / total_in).  The parse runs on the GPU, one job per call that
  * can complete a block, resumed at the last block cut handed out.  Level 0:
- * deflate_stored's blocks as its first loop cuts them (a small avail_out that
- * makes the reference cut shorter blocks is not modelled).  After Z_FINISH the
+ * deflate_stored's blocks as the reference cuts them, by min_block and by the
+ * output space of each call (a small avail_out gives shorter blocks through the
+ * pending buffer, deflate.c:1635-1815; tests/golden/stream_golden.json holds
+ * 28 level-0 sessions with output buffers from 1 byte up).  After Z_FINISH the
  * caller continues with Z_FINISH until Z_STREAM_END (zlib.h); a flush call
  * that ran out of output space and is given more input instead of the same
  * flush again goes on as the reference does (tests/test_gpu_fuzz.py), except
@@ -36,13 +38,15 @@
  * deflateParams give the reference's stream: deflateParams flushes with Z_BLOCK
  * itself when the level's function or the strategy changes (as deflate.c does)
  * and switches between level 0, deflate_fast and deflate_slow levels, and
- * between deflate_slow and Z_HUFFMAN_ONLY / Z_RLE (gzsetparams' pattern); a level
+ * between deflate_slow or deflate_fast levels and Z_HUFFMAN_ONLY / Z_RLE
+ * (gzsetparams' pattern; back to the function the stretch began from); a level
  * change within one function, and deflateTune, take effect at the next decision
  * even with input pending.  What the model cannot place returns Z_STREAM_ERROR
  * with strm->msg set, never a different stream (zgpu_api.cpp, `unsupported`):
  *   - deflateParams to or from Z_HUFFMAN_ONLY / Z_RLE after data other than
- *     between deflate_slow levels (4..9, memLevel <= 8) and those strategies,
- *     and back to deflate_slow after a first call of a single byte;
+ *     between deflate_slow levels (4..9, memLevel <= 8) or deflate_fast
+ *     levels (1..3) and those strategies and back to the same function, and
+ *     back after a first call of a single byte;
  *   - deflatePrime with input pending after a call that did not reach its end,
  *     or after Z_STREAM_END;
  *   - deflateSetDictionary after the stream has ended;

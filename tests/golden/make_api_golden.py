@@ -232,6 +232,32 @@ def deflate_sessions():
     S.append({"name": "params-hr-immediate", "ops": [
         ["init", 6, 15, 8, 0], ["deflate", sl(t, 0, 30000), Z_NO_FLUSH], ["params", 6, 2], ["params", 6, 0],
         ["deflate", sl(t, 30000, 100000), Z_FINISH]]})
+    # the same from deflate_fast levels (round 5): the chains resume from the
+    # snapshot at the Z_BLOCK flush, the stretch left out of what is inserted
+    for strat in (2, 3):
+        for level, wb in ((1, 15), (2, -15), (3, 31), (1, -9), (3, 12)):
+            S.append({"name": f"params-hrf{strat}-L{level}-w{wb}", "ops": [
+                ["init", level, wb, 8, 0], ["deflate", sl(m, 0, 30000), Z_NO_FLUSH], ["params", level, strat],
+                ["deflate", sl(m, 30000, 50000), Z_NO_FLUSH], ["params", level, 0],
+                ["deflate", sl(m, 50000, 100000), Z_FINISH], ["used"]]})
+    S.append({"name": "params-hrf-toggles-L2", "ops": [
+        ["init", 2, -15, 8, 0], ["deflate", sl(t, 0, 20000), Z_SYNC_FLUSH], ["params", 2, 3],
+        ["deflate", sl(t, 20000, 26000), Z_NO_FLUSH], ["params", 1, 0], ["deflate", sl(t, 26000, 60000), Z_NO_FLUSH],
+        ["params", 3, 2], ["deflate", sl(t, 60000, 61000), Z_NO_FLUSH], ["params", 3, 0],
+        ["deflate", sl(t, 61000, 100000), Z_FINISH]]})
+    S.append({"name": "params-hrf-gzsetparams", "ops": [
+        ["init", 1, 31, 8, 0], ["deflate", sl(m, 0, 40000), Z_NO_FLUSH], ["params", 1, 2],
+        ["deflate", sl(m, 40000, 41000), Z_NO_FLUSH], ["params", 1, 0], ["deflate", sl(m, 41000, 100000), Z_FINISH]]})
+    S.append({"name": "params-hrf-long-stretch", "ops": [
+        ["init", 3, 15, 8, 0], ["deflate", sl(t, 0, 20000), Z_NO_FLUSH], ["params", 3, 3],
+        ["deflate", sl(t, 20000, 70000), Z_NO_FLUSH], ["params", 3, 0], ["deflate", sl(t, 70000, 100000), Z_FINISH]]})
+    S.append({"name": "params-hrf-small-out", "ops": [
+        ["init", 1, 15, 8, 0], ["deflate", sl(m, 0, 30000), Z_NO_FLUSH, 3000], ["params", 1, 2],
+        ["deflate", sl(m, 30000, 60000), Z_NO_FLUSH, 3000], ["params", 2, 0],
+        ["deflate", sl(m, 60000, 100000), Z_FINISH, 3000]]})
+    S.append({"name": "params-hrf-mem5", "ops": [
+        ["init", 2, 15, 5, 0], ["deflate", sl(t, 0, 30000), Z_NO_FLUSH], ["params", 2, 2],
+        ["deflate", sl(t, 30000, 45000), Z_NO_FLUSH], ["params", 2, 0], ["deflate", sl(t, 45000, 100000), Z_FINISH]]})
     S.append({"name": "resetkeep-fresh", "ops": [["init", 6, 15, 8, 0], ["resetkeep"],
                                                  ["deflate", sl(m, 0, 100000), Z_FINISH], ["used"], ["reset"],
                                                  ["resetkeep"], ["deflate", sl(t, 0, 100000), Z_FINISH]]})

@@ -127,16 +127,19 @@ def test_round4_zlib_h_calls_golden(zg):
 
 
 def test_params_huff_rle_refusals(zg):
-    """deflateParams between deflate_slow and Z_HUFFMAN_ONLY / Z_RLE after data
-    is modelled (test_round4_zlib_h_calls_golden's params-hr-* sessions); the
-    switches it does not model return Z_STREAM_ERROR with strm->msg set and
-    leave the stream usable: from or to deflate_fast levels, memLevel 9, and a
-    stretch whose first call offered a single byte (zgpu_api.cpp deflateParams)."""
+    """deflateParams between deflate_slow or deflate_fast and Z_HUFFMAN_ONLY /
+    Z_RLE after data is modelled (test_round4_zlib_h_calls_golden's params-hr-*
+    and params-hrf-* sessions); the switches it does not model return
+    Z_STREAM_ERROR with strm->msg set and leave the stream usable: a stretch
+    left for the other function than it began from, memLevel 9 from
+    deflate_slow, and a stretch whose first call offered a single byte
+    (zgpu_api.cpp deflateParams)."""
     import zlib as pyzlib
     L = zg.load()
     d = datagen.make("text", 60000, 31)
     cases = [
-        ([["init", 2, 15, 8, 0], ["deflate", d[:20000], 0], ["params", 2, 2]], -2),   # fast -> huff
+        ([["init", 2, 15, 8, 0], ["deflate", d[:20000], 0], ["params", 2, 2],
+          ["deflate", d[20000:30000], 0], ["params", 6, 0]], -2),                       # fast -> huff -> slow
         ([["init", 6, 15, 9, 0], ["deflate", d[:20000], 0], ["params", 6, 3]], -2),   # memLevel 9
         ([["init", 6, 15, 8, 0], ["deflate", d[:20000], 0], ["params", 6, 2],
           ["deflate", d[20000:30000], 0], ["params", 2, 0]], -2),                       # huff -> fast

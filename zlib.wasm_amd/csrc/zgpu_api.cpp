@@ -2421,7 +2421,7 @@ struct internal_state {
     // reads at least 2 bytes (first_end: where the first call after a ended),
     // and the rolling ins_h is set afresh by every fill_window that reads
     // (deflate.c:307-310), so the strings after b hash as usual.
-    struct HrStretch { uint64_t a, b, first_end; };
+    struct HrStretch { uint64_t a, b, first_end; int fn; };   // fn: fn_of() before the stretch (1 fast, 2 slow)
     std::vector<HrStretch, ZAlloc<HrStretch>> hr;
     bool hr_lost = false;                // an open stretch's part ended (Z_FULL_FLUSH)
 };
@@ -2586,8 +2586,10 @@ int deflate_part(internal_state *s, bool closed) {
         fh.snap_head = &s->snap_head;
         fh.snap_prev = &s->snap_prev;
     }
-    // deflate_huff / deflate_rle stretches in this job's window (slow jobs)
-    if (slow) {
+    // deflate_huff / deflate_rle stretches in this job's window: slow jobs
+    // leave them out of k_links; fast jobs out of the strings k_parse_fast
+    // inserts before it starts (pre_from .. pre_ins)
+    if (slow || (fast && fh.dict)) {
         const uint64_t end = base + sl;
         for (const internal_state::HrStretch &h : s->hr) {
             if (h.b == ~0ull) continue;                          // open: this job is no slow job then
@@ -3697,17 +3699,21 @@ int deflateParams(z_streamp strm, int level, int strategy) {
     const bool enter_hr = started && !s->finished && of < 3 && nf >= 3 && level != 0 && s->level != 0;
     const bool leave_hr = started && !s->finished && of >= 3 && nf < 3 && level != 0 && s->level != 0;
     if (enter_hr) {
+        // from deflate_slow (k_links keys the stretch past every hash: memLevel
+        // <= 8) or from deflate_fast (its chains resume from the snapshot at the
+        // flush, the stretch left out of the strings inserted there)
         const uint64_t X = s->in_base + s->in.size();           // where the Z_BLOCK flush will stand
-        if (of != 2 || s->mem_level > 8 || X < 2)
+        if ((of != 2 && of != 1) || (of == 2 && s->mem_level > 8) || X < 2)
             return unsupported(strm, "deflateParams: a switch to Z_HUFFMAN_ONLY / Z_RLE after data is modelled "
-                                     "from deflate_slow levels (memLevel <= 8) only");
+                                     "from deflate_fast and deflate_slow levels (memLevel <= 8 for the latter) only");
     }
     if (leave_hr) {
-        const bool ok = nf == 2 && !s->hr_lost && !s->hr.empty() && s->hr.back().b == ~0ull &&
+        const bool ok = !s->hr_lost && !s->hr.empty() && s->hr.back().b == ~0ull && nf == s->hr.back().fn &&
                         (s->hr.back().first_end == 0 || s->hr.back().first_end >= s->hr.back().a + 2);
         if (!ok)
             return unsupported(strm, "deflateParams: a switch from Z_HUFFMAN_ONLY / Z_RLE after data is modelled "
-                                     "back to deflate_slow levels only, after a first call of at least 2 bytes");
+                                     "back to the function the stretch began from (deflate_fast or deflate_slow "
+                                     "levels), after a first call of at least 2 bytes");
     }
     if ((strategy != s->strategy || deflate_fn(level) != deflate_fn(s->level)) && started) {
         const int err = deflate(strm, Z_BLOCK);
@@ -3719,6 +3725,7 @@ int deflateParams(z_streamp strm, int level, int strategy) {
             internal_state::HrStretch h{};
             h.a = s->in_base + s->in.size();
             h.b = ~0ull;
+            h.fn = of;
             s->hr.push_back(h);
             s->hr_lost = false;
         }

@@ -2534,6 +2534,10 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
 
     if (kEv && job.dict)                                  // a preset dictionary's strings, or a window
         for (P q = (P)job.pre_from; q < (P)job.pre_ins; q++) {   // parsed by a function that inserts all
+            bool skip = false;                           // but a deflate_huff / deflate_rle stretch (SkipSpec)
+            for (uint32_t k = 0; k < job.sk.n; k++)
+                if ((uint32_t)q >= job.sk.a[k] && (uint32_t)q < job.sk.b[k]) skip = true;
+            if (skip) continue;
             wsee(q);
             insert(q);
         }
