@@ -16,3 +16,5 @@ ZGPU_FAST_SRT=1 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_stream.py 
 tail -2 $O/stream_tests.log
 ZGPU_FAST_SRT=1 timeout -k 10 300 python3 -u tools/stream_stages.py 256 1 > $O/stream256.log 2>&1 || { echo "stream256 failed"; tail -20 $O/stream256.log; exit 1; }
 grep -v amdgpu.ids $O/stream256.log
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_zstream.py -x -q --timeout 300 --timeout-method thread > $O/zstream_tests.log 2>&1 || { echo "zstream tests failed"; tail -30 $O/zstream_tests.log; exit 1; }
+tail -2 $O/zstream_tests.log

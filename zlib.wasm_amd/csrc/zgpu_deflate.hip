@@ -4348,13 +4348,24 @@ __device__ __attribute__((always_inline)) inline uint32_t m2_cand(const uint16_t
     const int q = (int)Sr[idx];
     return k < n012 ? (uint32_t)q : 0xffffffffu;       // none: below every limit (tested as signed)
 }
+// The quick reject with aligned 2-byte reads only (a ds_read_u16 at an odd
+// byte address is split: tools/lds_probe.hip, 6x the cycles of an aligned
+// read).  longest_match rejects a candidate whose bytes best-1, best or 0, 1
+// differ from the scan's (deflate.c:1449-1452); any pair of positions within
+// [0, best] is as sound a filter for "longer than best" (the result is the
+// same: only compares decide), so each test takes the pair at the even byte
+// address next to the one zlib reads -- bytes (best-1, best) or (best-2,
+// best-1), and (0, 1) or (1, 2) -- against the scan's pair at the same offset.
 struct DWQ2 {
     int occ;
     int q[kDQ];
-    uint32_t scan01, scanE;
+    uint32_t scan01, scan12, scanE1, scanE2;   // the scan's pairs at 0, 1, best-1, best-2
     int be;            // best - 1
     bool alive;        // no candidate at or below the limit seen yet
 };
+__device__ __attribute__((always_inline)) inline uint32_t ldu16e(const uint8_t *B, int x) {   // x even
+    return (uint32_t)*reinterpret_cast<const uint16_t *>(B + x);
+}
 __device__ __attribute__((always_inline)) inline void m2_walk(const uint16_t *Sr, const uint8_t *B, int vp, int lim,
                                                               int A0, int B1, int B2, uint32_t n0, uint32_t n01,
                                                               uint32_t n012, int64_t p, int64_t n,
@@ -4397,16 +4408,20 @@ __device__ __attribute__((always_inline)) inline void m2_walk(const uint16_t *Sr
 #pragma unroll
     for (int j = 0; j < kDQ; j++) w.q[j] = 0;
     w.scan01 = S.s0 & 0xffffu;
+    w.scan12 = (S.s0 >> 8) & 0xffffu;
     w.be = best - 1;
-    w.scanE = b4(B, vp + w.be) & 0xffffu;
+    w.scanE1 = b4(B, vp + w.be) & 0xffffu;
+    w.scanE2 = b4(B, vp + w.be - 1) & 0xffffu;
     w.alive = true;
     count = ufl(count);
     auto step = [&](uint32_t k) {
         const int q = (int)m2_cand(Sr, k, A0, B1, B2, n0, n01, n012);
         const bool in = q > lim;
         const int qs = in ? q : 0;
-        const uint32_t c01 = b4(B, qs) & 0xffffu, cE = b4(B, qs + w.be) & 0xffffu;
-        const bool pass = w.alive & in & (c01 == w.scan01) & (cE == w.scanE);
+        const int xe = qs + w.be;
+        const uint32_t c01 = ldu16e(B, (qs + 1) & ~1), cE = ldu16e(B, xe & ~1);
+        const uint32_t s01 = (qs & 1) ? w.scan12 : w.scan01, sE = (xe & 1) ? w.scanE2 : w.scanE1;
+        const bool pass = w.alive & in & (c01 == s01) & (cE == sE);
         w.alive = w.alive & in;
 #pragma unroll
         for (int j = kDQ - 1; j > 0; j--) w.q[j] = pass ? w.q[j - 1] : w.q[j];
@@ -4461,7 +4476,8 @@ __device__ __attribute__((always_inline)) inline void m2_walk(const uint16_t *Sr
         if (fin) break;
         if (best != best0) {                           // the quick reject now tests the new best
             w.be = best - 1;
-            w.scanE = b4(B, vp + w.be) & 0xffffu;
+            w.scanE1 = b4(B, vp + w.be) & 0xffffu;
+            w.scanE2 = b4(B, vp + w.be - 1) & 0xffffu;
         }
     }
     rf[p] = rec(best, bq);
