@@ -18,3 +18,7 @@ ZGPU_FAST_SRT=1 timeout -k 10 300 python3 -u tools/stream_stages.py 256 1 > $O/s
 grep -v amdgpu.ids $O/stream256.log
 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_zstream.py -x -q --timeout 300 --timeout-method thread > $O/zstream_tests.log 2>&1 || { echo "zstream tests failed"; tail -30 $O/zstream_tests.log; exit 1; }
 tail -2 $O/zstream_tests.log
+for m in 1 0; do
+  ZGPU_FAST_SRT=$m timeout -k 10 300 python3 -u tools/ab_match.py zlib.wasm_amd/libzgpu.so 1 1 enwik 16384 >> $O/c3_ab.log 2>&1 || { echo "c3 ab failed"; tail -20 $O/c3_ab.log; exit 1; }
+done
+grep -v amdgpu.ids $O/c3_ab.log

@@ -492,7 +492,12 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     // keep ~6 B of workspace per in-flight byte (L4-9: ~25) and their parse is
     // one sequential lane per buffer, so they get 4x the budget: more buffers
     // in flight is what their throughput scales with.
-    const uint64_t budget = (level >= 1 && level <= 3) || strategy == 2 || strategy == 3
+    // (levels 1..3 from the sorted runs keep ~28 B per byte: the plain budget, at most 4 GiB)
+    static const int fsrt_env0 = [] { const char *e = std::getenv("ZGPU_FAST_SRT"); return e ? std::atoi(e) : 0; }();
+    const bool fsrt_want = fsrt_env0 == 1 && level >= 1 && level <= 3 && strategy != 2 && strategy != 3 &&
+                           (!fs || fs->srt_parse) && hbits <= 15;
+    const uint64_t budget = fsrt_want ? std::min<uint64_t>(c.inflight, 4ull << 30)
+                            : (level >= 1 && level <= 3) || strategy == 2 || strategy == 3
                                 ? 4 * (uint64_t)c.inflight : (uint64_t)c.inflight;
     std::vector<uint32_t> cuts{0};
     {
@@ -598,8 +603,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     bool m2 = match2_env == 1 && slow && !fs && hbits <= 15 && segs.empty();
     // levels 1..3 of a batch job from the same sorted runs (k_bwork<true> +
     // k_parse_srt; ZGPU_FAST_SRT=1)
-    static const int fsrt_env = [] { const char *e = std::getenv("ZGPU_FAST_SRT"); return e ? std::atoi(e) : 0; }();
-    bool fsrt = fsrt_env == 1 && level >= 1 && level <= 3 && !huff && !rle && (!fs || fs->srt_parse) && hbits <= 15;
+    bool fsrt = fsrt_want;
     if (fsrt && fs && (!c.ws_ibits.ensure(max_pos / 8 + 256) || !fs->snap)) {
         (void)hipGetLastError();
         return zfail(__LINE__);

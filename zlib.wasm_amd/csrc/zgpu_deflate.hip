@@ -4653,10 +4653,13 @@ constexpr int kPSBits = 4 * kSortBlock / 32;        // bitmap words: blocks b-2 
 // each call's input end, the parse stops as deflate_fast's need_more does
 // (deflate.c:1841-1844), every block cut writes its record (srec), and the
 // bitmap goes to job.ins_bits for k_srt_chains.
-template <typename P, bool kEv = false>
+// kG (batches of many buffers): the sorted entries and the bytes are read
+// from global memory (L2) instead of LDS rings, so that a wave needs only its
+// 8 KiB bitmap and 20 parses share a CU instead of one.
+template <typename P, bool kEv = false, bool kG = false>
 __global__ __launch_bounds__(64) void k_parse_srt(DeflateJob job) {
-    __shared__ __attribute__((aligned(16))) uint16_t Sr[kM2Ring];
-    __shared__ __attribute__((aligned(16))) uint8_t Bw[kM2Ring + kM2Pad];
+    __shared__ __attribute__((aligned(16))) uint16_t Sr[kG ? 8 : kM2Ring];
+    __shared__ __attribute__((aligned(16))) uint8_t Bw[kG ? 16 : kM2Ring + kM2Pad];
     __shared__ uint32_t Bi[kPSBits];
     const int lane = threadIdx.x;
     const uint64_t below = (1ull << lane) - 1ull;
@@ -4698,11 +4701,45 @@ __global__ __launch_bounds__(64) void k_parse_srt(DeflateJob job) {
             if (x + j >= 0 && x + j < n) w[j >> 2] |= (uint32_t)in[x + j] << (8 * (j & 3));
         return make_uint4(w[0], w[1], w[2], w[3]);
     };
+    P blk = 0;                                          // the block in ring slot 2
+    P gbase = -2 * (P)kSortBlock;                       // absolute position of ring offset 0 (kG)
+    // ring accessors: LDS, or (kG) the same offsets mapped to global memory
+    auto sr = [&](int idx) -> uint32_t {                // ring entry idx (slot idx >> 14)
+        if (!kG) return Sr[idx];
+        const P b = blk - 2 + (idx >> 14);
+        return (uint32_t)(idx & ~(kSortBlock - 1)) + (uint32_t)gS[b * kSortBlock + (idx & (kSortBlock - 1))];
+    };
+    auto bw = [&](int x) -> uint32_t {                  // ring byte x
+        if (!kG) return Bw[x];
+        const P a = gbase + x;
+        return a < n ? (uint32_t)in[a] : 0u;
+    };
+    auto b16r = [&](int x, uint32_t &a0, uint32_t &a1, uint32_t &a2, uint32_t &a3) {
+        if (!kG) { b16(Bw, x, a0, a1, a2, a3); return; }
+        const uint4 v = ld16(gbase + x);
+        a0 = v.x; a1 = v.y; a2 = v.z; a3 = v.w;
+    };
+    auto cand = [&](uint32_t k, int A0, int B1, int B2, uint32_t n0, uint32_t n01, uint32_t n012) -> int {
+        const int idx = k < n0 ? A0 - (int)k : (k < n01 ? B1 - (int)k : B2 - (int)k);
+        int q = -1;
+        if (k < n012) q = (int)sr(idx);                 // only real entries are read (kG: global memory)
+        return q;
+    };
     // block b into ring slot 2 (entries as ring offsets), its bytes + pad, and
     // its bitmap slot b+1 (slot 3) cleared; slide first unless b == 0
     auto load_block = [&](P b) {
         if (kEv && b >= 3)                              // block b-3's bits leave the ring: keep them
             for (int c = lane; c < kSortBlock / 32; c += 64) gbits[(b - 3) * (kSortBlock / 32) + c] = Bi[c];
+        gbase = (b - 2) * (P)kSortBlock;
+        if (kG) {                                       // only the bitmap lives in LDS
+            if (b > 0)
+                for (int c = lane; c < 3 * kSortBlock / 32; c += 64) Bi[c] = Bi[c + kSortBlock / 32];
+            else
+                for (int c = lane; c < kPSBits; c += 64) Bi[c] = 0;
+            for (int c = lane; c < kSortBlock / 32; c += 64) Bi[3 * kSortBlock / 32 + c] = 0;
+            __syncthreads();
+            return;
+        }
         if (b > 0) {
             uint4 *dS = reinterpret_cast<uint4 *>(Sr);
             typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -4744,7 +4781,6 @@ __global__ __launch_bounds__(64) void k_parse_srt(DeflateJob job) {
     P rb = 0;
     uint4 cur = make_uint4(0, 0, 0, 0), nxt = cur;
     auto ri_load = [&](P x) -> uint4 { return x + lane < n ? gW[x + lane] : make_uint4(0, 0, 0, 0); };
-    P blk = 0;                                          // the block in ring slot 2
     if (n > 0) {
         load_block(0);
         cur = ri_load(0);
@@ -4802,7 +4838,7 @@ __global__ __launch_bounds__(64) void k_parse_srt(DeflateJob job) {
             bool head = false, done = n012 == 0;
             for (uint32_t k0 = 0; !done; k0 += 64) {
                 const uint32_t k = k0 + (uint32_t)lane;
-                const int q = (int)m2_cand(Sr, k, A0, B1, B2, n0, n01, n012);
+                const int q = cand(k, A0, B1, B2, n0, n01, n012);
                 const bool valid = k < n012;
                 const bool ins = valid && ((Bi[(uint32_t)q >> 5] >> ((uint32_t)q & 31u)) & 1u);
                 const uint64_t insm = __ballot(ins);
@@ -4833,12 +4869,12 @@ __global__ __launch_bounds__(64) void k_parse_srt(DeflateJob job) {
                 int len = 0;
                 if (mine) {
                     uint32_t a0, a1, a2, a3, c0, c1, c2, c3;
-                    b16(Bw, q, a0, a1, a2, a3);
-                    b16(Bw, vp, c0, c1, c2, c3);
+                    b16r(q, a0, a1, a2, a3);
+                    b16r(vp, c0, c1, c2, c3);
                     len = diff16(a0 ^ c0, a1 ^ c1, a2 ^ c2, a3 ^ c3);
                     while (len >= 16 && len < nice) {
-                        b16(Bw, q + len, a0, a1, a2, a3);
-                        b16(Bw, vp + len, c0, c1, c2, c3);
+                        b16r(q + len, a0, a1, a2, a3);
+                        b16r(vp + len, c0, c1, c2, c3);
                         const int r = diff16(a0 ^ c0, a1 ^ c1, a2 ^ c2, a3 ^ c3);
                         len += r;
                         if (r < 16) break;
@@ -4871,7 +4907,7 @@ __global__ __launch_bounds__(64) void k_parse_srt(DeflateJob job) {
                 while (L < maxcmp) {
                     const int kk = L + lane;
                     const int kc = kk < maxcmp ? kk : maxcmp - 1;
-                    const uint64_t mm = __ballot((kk < maxcmp) & (Bw[bq + kc] != Bw[vp + kc]));
+                    const uint64_t mm = __ballot((kk < maxcmp) & (bw((int)bq + kc) != bw(vp + kc)));
                     if (mm) { L += __builtin_ctzll(mm); break; }
                     L += 64;
                     if (L > maxcmp) L = maxcmp;
@@ -4894,7 +4930,7 @@ __global__ __launch_bounds__(64) void k_parse_srt(DeflateJob job) {
             p += match_length;
             match_length = 0;
         } else {
-            bflush = po.tally((uint32_t)Bw[vp]);
+            bflush = po.tally(bw(vp));
             p++;
         }
         if (bflush) {
@@ -5071,10 +5107,18 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         if (job.nfl) {                                      // a streaming job of stops (one buffer)
             hipLaunchKernelGGL((k_parse_srt<int64_t, true>), grid, dim3(64), 0, st, job);
             if (job.snap) hipLaunchKernelGGL(k_srt_chains, dim3(1), dim3(64), 0, st, job);
-        } else if (job.pos31) {
-            hipLaunchKernelGGL(k_parse_srt<int32_t>, grid, dim3(64), 0, st, job);
         } else {
-            hipLaunchKernelGGL(k_parse_srt<int64_t>, grid, dim3(64), 0, st, job);
+            // few buffers: rings in LDS (one parse per CU); many: the rings'
+            // data from L2 and 20 parses per CU (ZGPU_SRT_LDS_MAX: the limit)
+            static const uint32_t lds_max = [] {
+                const char *e = std::getenv("ZGPU_SRT_LDS_MAX");
+                return e ? (uint32_t)std::atoi(e) : 512u;
+            }();
+            const bool gl = job.count > lds_max;
+            if (job.pos31 && gl) hipLaunchKernelGGL((k_parse_srt<int32_t, false, true>), grid, dim3(64), 0, st, job);
+            else if (job.pos31) hipLaunchKernelGGL(k_parse_srt<int32_t>, grid, dim3(64), 0, st, job);
+            else if (gl) hipLaunchKernelGGL((k_parse_srt<int64_t, false, true>), grid, dim3(64), 0, st, job);
+            else hipLaunchKernelGGL(k_parse_srt<int64_t>, grid, dim3(64), 0, st, job);
         }
         break;
     case 15: {
