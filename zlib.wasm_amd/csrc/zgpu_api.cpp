@@ -255,6 +255,7 @@ struct Ctx {
     DevBuf ws_srec, ws_snap;  // a streaming job's block records and head[] snapshot
     DevBuf ws_srt, ws_boff, ws_work, ws_bblk;   // the sorted-run match (k_bsort / k_bwork / k_match2)
     DevBuf ws_ibits;                            // k_parse_srt's inserted-position bitmap (streaming jobs)
+    DevBuf ws_m2seg;                            // k_match2's (buffer, first block) ranges
     // inflate: match records, per-stream results, checks, offsets, stop codes
     DevBuf ws_mrec, ws_irec, ws_ick, ws_imeta, ws_istop;
     // the block-parallel decode of a lone stream (inflate_par): candidate lists,
@@ -600,7 +601,35 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     // (position-indexed, one slot: all three kernels run on one stream), and
     // a hash table per block.
     static const int match2_env = [] { const char *e = std::getenv("ZGPU_MATCH2"); return e ? std::atoi(e) : 0; }();
-    bool m2 = match2_env == 1 && slow && !fs && hbits <= 15 && segs.empty();
+    bool m2 = match2_env == 1 && slow && !fs && hbits <= 15;
+    // few large buffers: k_match2 per range of m2_segb blocks (buffer, first
+    // block) where the chain walk would go per byte segment (segs)
+    std::vector<uint32_t> m2segs;
+    std::vector<size_t> m2seg_at(nsub + 1, 0);
+    std::vector<uint32_t> m2segb(nsub, 1);
+    if (m2) {
+        for (size_t sb = 0; sb < nsub; sb++) {
+            m2seg_at[sb] = m2segs.size() / 2;
+            if (seg_at[sb + 1] == seg_at[sb]) continue;
+            const uint32_t a = cuts[sb], b = cuts[sb + 1];
+            uint64_t tot = 0;
+            for (uint32_t i = a; i < b; i++) tot += (lens[i] + kSortBlock - 1) / kSortBlock;
+            const uint32_t segb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(16, tot / 256));
+            m2segb[sb] = segb;
+            for (uint32_t i = a; i < b; i++) {
+                const uint64_t nb = (lens[i] + kSortBlock - 1) / kSortBlock;
+                for (uint64_t o = 0; o < nb; o += segb) {
+                    m2segs.push_back(i - a);
+                    m2segs.push_back((uint32_t)o);
+                }
+            }
+        }
+        m2seg_at[nsub] = m2segs.size() / 2;
+        if (!m2segs.empty() && (!c.ws_m2seg.ensure(4 * m2segs.size()) ||
+                                hipMemcpyAsync(c.ws_m2seg.p, m2segs.data(), 4 * m2segs.size(), hipMemcpyHostToDevice,
+                                               st) != hipSuccess))
+            return zfail(__LINE__);
+    }
     // levels 1..3 of a batch job from the same sorted runs (k_bwork<true> +
     // k_parse_srt; ZGPU_FAST_SRT=1)
     bool fsrt = fsrt_want;
@@ -783,6 +812,11 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.work = c.ws_work.as<uint4>();
             job.nsblk = bblk[bblk_at[s + 1] - 1];
             if (fs) job.ins_bits = c.ws_ibits.as<uint32_t>();
+            if (m2) {                                   // k_match2's ranges of blocks (or none)
+                job.seg = m2seg_at[s + 1] > m2seg_at[s] ? c.ws_m2seg.as<uint32_t>() + 2 * m2seg_at[s] : nullptr;
+                job.nseg = (uint32_t)(m2seg_at[s + 1] - m2seg_at[s]);
+                job.seg_len = m2segb[s];
+            }
         }
         static const int fcmp64 = std::getenv("ZGPU_FAST_CMP64") != nullptr;   // A/B: k_parse_fast's compare
         job.fcmp = fcmp64;

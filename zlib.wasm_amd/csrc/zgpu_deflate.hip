@@ -5123,7 +5123,8 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         break;
     case 15: {
         const int wq = (int)(job.cfg.good < job.cfg.lazy) | job.cfg_q;
-        hipLaunchKernelGGL(k_match2<false>, grid, dim3(kM2Threads), 0, st, job, wq);
+        if (job.seg) hipLaunchKernelGGL(k_match2<true>, dim3(job.nseg), dim3(kM2Threads), 0, st, job, wq);
+        else hipLaunchKernelGGL(k_match2<false>, grid, dim3(kM2Threads), 0, st, job, wq);
         break;
     }
     case 7: hipLaunchKernelGGL(k_parse_huff, grid, dim3(kHuffThreads), 0, st, job); break;
