@@ -258,6 +258,7 @@ struct Ctx {
     DevBuf ws_m2seg;                            // k_match2's (buffer, first block) ranges
     // inflate: match records, per-stream results, checks, offsets, stop codes
     DevBuf ws_mrec, ws_irec, ws_ick, ws_imeta, ws_istop;
+    DevBuf ws_iidx;           // the streaming inflate()'s consumption index (InflateJob::eidx / bidx)
     // the block-parallel decode of a lone stream (inflate_par): candidate lists,
     // per-block jobs and records, output symbols
     DevBuf ws_par1, ws_par2, ws_pjob, ws_psym, ws_pslot;
@@ -1210,6 +1211,9 @@ struct InflateResumeDev {          // InflateJob's resume arrays (device, per st
     uint32_t stop_mode;            // InflateJob::stop_mode
     uint64_t *zstate_out;          // InflateJob::zstate_out
     uint32_t dmax = 0;             // InflateJob::dmax
+    uint64_t *eidx = nullptr, *bidx = nullptr;   // InflateJob::eidx / bidx / icnt (null: no index)
+    uint32_t *icnt = nullptr;
+    uint32_t ecap = 0, bcap = 0;
 };
 
 // ------------------------------------------------------------------------
@@ -1612,6 +1616,11 @@ int inflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.zstate_out = rs->zstate_out;
             job.zcodes = rs->zstate_out != nullptr;
             job.dmax = rs->dmax;
+            job.eidx = rs->eidx;
+            job.bidx = rs->bidx;
+            job.icnt = rs->icnt;
+            job.ecap = rs->ecap;
+            job.bcap = rs->bcap;
         }
         if (T.run(3, st, [&] { return launch_inflate_stage(0, job, st); })) return ZGPU_MEM_ERROR;
         if (T.run(4, st, [&] { return launch_inflate_stage(1, job, st); })) return ZGPU_MEM_ERROR;
@@ -1700,13 +1709,25 @@ struct InflateTry {
     int64_t zmark;                 // inflateMark where the input ran out
     uint32_t zcodes;               // inflateCodesUsed of the last dynamic block decoded (~0: none)
 };
+// The consumption index of one streaming attempt (InflateJob::eidx / bidx),
+// relative to the attempt's input and output arrays: e[2k], e[2k + 1] per
+// symbol (output end | stored << 32 | BFINAL << 33; the input bit after its
+// codes, a stored run's first byte); b = (bit, output) of each block
+// boundary; ne / nb = those met (ne > e.size() / 2: the index stops short of
+// the decode's end)
+struct InflateIndex {
+    std::vector<uint64_t> e, b;
+    uint32_t ne = 0, nb = 0;
+};
+constexpr uint32_t kIdxCap = 1u << 20, kIdxBCap = 1u << 14;
 
 int inflate_try_locked(Ctx &c, const uint8_t *in, size_t n, bool resume, uint64_t start_bit, const uint8_t *hist,
                        size_t hist_len, size_t cap, int wrap, int wbits, std::vector<uint8_t> &out, InflateTry &t,
-                       uint32_t stop_mode = 0, uint32_t dmax = 0) {
+                       uint32_t stop_mode = 0, uint32_t dmax = 0, InflateIndex *ix = nullptr) {
     if (!c.ws_io.ensure(n + 64) || !c.ws_io2.ensure(cap + 64) || !c.ws_small.ensure(8 * 16 + 64) ||
         !c.ws_istop.ensure(64))
         return ZGPU_MEM_ERROR;
+    if (ix && !c.ws_iidx.ensure(16ull * kIdxCap + 16ull * kIdxBCap + 64)) ix = nullptr;
     uint8_t *d_in = c.ws_io.as<uint8_t>(), *d_out = c.ws_io2.as<uint8_t>();
     uint64_t *m = c.ws_small.as<uint64_t>();          // so sl do dc dl used | st | rbit hist | blk[2]
     int32_t *d_st = reinterpret_cast<int32_t *>(m + 6);
@@ -1725,7 +1746,14 @@ int inflate_try_locked(Ctx &c, const uint8_t *in, size_t n, bool resume, uint64_
         hipMemcpyAsync(d_rbit, &rbit, 8, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(d_hist, &hl, 4, hipMemcpyHostToDevice, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
-    const InflateResumeDev rs{resume ? d_rbit : nullptr, resume ? d_hist : nullptr, d_blk, stop_mode, d_zs, dmax};
+    InflateResumeDev rs{resume ? d_rbit : nullptr, resume ? d_hist : nullptr, d_blk, stop_mode, d_zs, dmax};
+    if (ix) {
+        rs.eidx = c.ws_iidx.as<uint64_t>();
+        rs.bidx = rs.eidx + 2ull * kIdxCap;
+        rs.icnt = reinterpret_cast<uint32_t *>(rs.bidx + 2ull * kIdxBCap);
+        rs.ecap = kIdxCap;
+        rs.bcap = kIdxBCap;
+    }
     int rc = inflate_dev_locked(c, d_in, m, m + 1, d_out, m + 2, m + 3, m + 4, m + 5, d_st, d_stop, 1,
                                 resume ? 0 : wrap, wbits, st, &rs);
     if (rc) return rc;
@@ -1749,6 +1777,22 @@ int inflate_try_locked(Ctx &c, const uint8_t *in, size_t n, bool resume, uint64_
     t.zstate = blk[2];
     t.zmark = (int32_t)(uint32_t)blk[3];
     t.zcodes = (uint32_t)(blk[3] >> 32);
+    if (ix) {
+        uint32_t cnt[2];
+        if (copy_sync(cnt, rs.icnt, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return ZGPU_MEM_ERROR;
+        ix->ne = cnt[0];
+        ix->nb = cnt[1];
+        ix->e.resize(2ull * std::min(cnt[0], kIdxCap));
+        ix->b.resize(2ull * std::min(cnt[1], kIdxBCap));
+        if ((!ix->e.empty() &&
+             copy_sync(ix->e.data(), rs.eidx, 8 * ix->e.size(), hipMemcpyDeviceToHost, st) != hipSuccess) ||
+            (!ix->b.empty() &&
+             copy_sync(ix->b.data(), rs.bidx, 8 * ix->b.size(), hipMemcpyDeviceToHost, st) != hipSuccess))
+            return ZGPU_MEM_ERROR;
+        for (size_t k = 0; k < ix->e.size(); k += 2)          // device-reported positions (compress_host_locked)
+            if ((uint32_t)ix->e[k] > cap + 258 || ix->e[k + 1] > ((ix->e[k] >> 32) & 1u ? n : 8ull * n))
+                return ZGPU_MEM_ERROR;
+    }
     return ZGPU_OK;
 }
 
@@ -2370,6 +2414,19 @@ struct internal_state {
     uint64_t res_bit = 0, res_put = 0, ideliv = 0;
     uint32_t icheck = 0;    // Adler-32 / CRC-32 of the output before res_put
     zvec<uint8_t> hist;
+    // exact input accounting (inflate.c inf_leave: a call whose output space
+    // ends first stops reading after the symbol it has no room for): cons =
+    // absolute input consumed as the caller was told; in's bytes from cons on
+    // were handed back and are expected again (held_at: the next_in they were
+    // handed back at).  ix: the last decode's symbol index (InflateIndex::e)
+    // with its input / output origins, the output it starts at and whether it
+    // reaches the decode's end; fin_used: a finished stream's input end (the
+    // trailer included); acct_done: the attempt set next_in / total_in itself
+    uint64_t cons = 0, fin_used = 0;
+    const Bytef *held_at = nullptr;
+    std::vector<uint64_t> ix;
+    uint64_t ix_ibase = 0, ix_obase = 0, ix_o0 = 0;
+    bool ix_all = false, acct_done = false;
     // deflateTune (deflate.c:805-820): the jobs' good/lazy/nice/chain
     bool tuned = false;
     LevelCfg tune{};
@@ -3982,6 +4039,7 @@ int inflateReset(z_streamp strm) {
     s->iwin.clear(); s->iwin_on = false;                               // wsize = whave = wnext = 0
     s->isyncpt = false; s->imark = -65536; s->icodes = 0; s->iprime_n = 0; s->iprime_v = 0;
     s->iadl_on = false; s->iadl = 0;
+    s->cons = s->fin_used = 0; s->held_at = nullptr; s->ix.clear(); s->ix_all = false;
     strm->total_in = strm->total_out = 0;
     strm->msg = nullptr;
     if (s->wrap) strm->adler = s->wrap & 1;                           // inflateResetKeep: only when wrapped
@@ -4128,6 +4186,52 @@ int inflatePrime(z_streamp strm, int bits, int value) {
 }
 
 namespace {
+uint32_t stream_check(const internal_state *s, uint32_t init, const uint8_t *p, size_t n) {
+    return s->igz ? ck_crc32(init, p, n) : ck_adler32(init, p, n);
+}
+
+// the symbol index of a decode whose output array o starts at absolute output
+// obase, hist_len bytes of window in front (InflateIndex); `whole`: the decode
+// ran to its own end (not cut at its output capacity)
+void keep_index(internal_state *s, InflateIndex &ix, uint64_t obase, size_t hist_len, bool whole) {
+    s->ix.swap(ix.e);
+    s->ix_ibase = s->in_base;
+    s->ix_obase = obase;
+    s->ix_o0 = obase + hist_len;
+    s->ix_all = whole && 2ull * ix.ne <= s->ix.size();
+}
+
+// the resume point (res_bit, res_put, hist, icheck) moved to the last block
+// boundary of a decode (output o from absolute output obase) whose output is
+// at most xlim, when that is past the current one; input before the
+// boundary's byte is dropped
+void advance_resume(internal_state *s, const std::vector<uint8_t> &o, uint64_t obase, const InflateIndex &ix,
+                    const InflateTry &t, uint64_t xlim) {
+    const bool resume = s->imode == 1;
+    const uint64_t ib = resume ? 8ull * s->in_base : 0, ob = resume ? obase : 0;
+    uint64_t bb = 0, bp = 0;
+    auto take = [&](uint64_t b, uint64_t p) {
+        if (b && p + ob <= xlim && b + ib > bb) { bb = b + ib; bp = p + ob; }
+    };
+    for (size_t k = 0; k + 1 < ix.b.size(); k += 2) take(ix.b[k], ix.b[k + 1]);
+    take(t.blk_bit, t.blk_put);
+    if (!bb || bb <= s->res_bit) return;
+    if (!resume) {
+        s->igz = (s->wrap & 2) && s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b;
+        s->icheck = s->igz ? 0u : 1u;
+    }
+    if (s->wrap != 0) s->icheck = stream_check(s, s->icheck, o.data() + (s->res_put - obase), (size_t)(bp - s->res_put));
+    const uint64_t h0 = bp > 32768 ? bp - 32768 : 0;              // the window before the new point
+    s->hist.assign(o.begin() + (std::ptrdiff_t)(h0 - obase), o.begin() + (std::ptrdiff_t)(bp - obase));
+    s->res_bit = bb;
+    s->res_put = bp;
+    s->imode = 1;
+    s->itype = true;
+    const uint64_t drop = (bb >> 3) - s->in_base;                 // input before the boundary's byte
+    s->in.erase(s->in.begin(), s->in.begin() + (std::ptrdiff_t)drop);
+    s->in_base += drop;
+}
+
 // One decode attempt of the streaming inflate() over the input gathered so
 // far: from the stream start until a block is complete, then from the last
 // block boundary.  Sets s->out (bytes not handed out yet), s->finished and
@@ -4161,6 +4265,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
         }
         s->finished = 1;
         s->itail = false;
+        s->acct_done = true;
         if (ok) {
             const uint64_t used = tpos + need;
             const size_t back = (size_t)std::min<uint64_t>(in_end - used, took);
@@ -4217,6 +4322,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
         }
         std::vector<uint8_t> o;
         InflateTry t{};
+        InflateIndex ixo;
         int rc;
         {
             Lease L;
@@ -4229,7 +4335,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             if (!rc) rc = inflate_try_locked(*L.c, s->in.data(), s->in.size(), resume,
                                              resume ? s->res_bit - 8ull * s->in_base : 0, s->hist.data(), hl,
                                              hl + s->cap, s->wrap, s->wbits, o, t, mode,
-                                             s->iback_win ? 1u << s->wbits : 0u);
+                                             s->iback_win ? 1u << s->wbits : 0u, &ixo);
         }
         if (rc) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : rc;
         if (t.stop != kIFull) {
@@ -4244,6 +4350,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             continue;
         }
         const uint64_t obase = resume ? s->res_put - hl : 0;     // absolute output byte of o[0]
+        keep_index(s, ixo, obase, hl, t.stop != kIFull);
         auto append_new = [&](uint64_t upto) {                   // decoded bytes beyond those kept
             const uint64_t have = s->ideliv + (s->out.size() - s->out_pos);
             if (s->out_pos) {
@@ -4254,14 +4361,6 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
                                            o.begin() + (std::ptrdiff_t)(upto - obase));
         };
         const uint64_t put_abs = obase + t.put;
-        // a data error: the reference stops reading there (inflate.c BAD), so
-        // this call's input after the bytes used goes back to the caller
-        auto give_back_after = [&](uint64_t used_abs) {
-            const size_t back = (size_t)std::min<uint64_t>(in_end > used_abs ? in_end - used_abs : 0, took);
-            strm->next_in -= back;
-            strm->avail_in += (uInt)back;
-            strm->total_in = used_abs - s->iadj;
-        };
         if (t.stop == kIBlock && hdr_stop) {                     // the header read: resume raw after it
             uint64_t bb = t.blk_bit;
             s->igz = (s->wrap & 2) && s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b;
@@ -4297,11 +4396,8 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             s->res_bit = bb;
             s->res_put = bp;
             s->imode = 1;
-            const uint64_t used_abs = (bb + 7) >> 3;
+            const uint64_t used_abs = (bb + 7) >> 3;              // the input after it goes back (inflate_body)
             const size_t back = (size_t)std::min<uint64_t>(in_end - used_abs, took);
-            strm->next_in -= back;
-            strm->avail_in += (uInt)back;
-            strm->total_in -= back;
             s->in.resize(s->in.size() - back);
             const uint64_t drop = (bb >> 3) - s->in_base;         // input before the boundary's byte
             s->in.erase(s->in.begin(), s->in.begin() + (std::ptrdiff_t)drop);
@@ -4317,6 +4413,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             // a zlib header with FDICT: Z_NEED_DICT with the header (2 bytes +
             // DICTID) consumed and the rest handed back (inflate.c DICTID/DICT);
             // inflateSetDictionary resumes after it
+            s->acct_done = true;
             const size_t keep = 6, back = std::min<size_t>(s->in.size() - keep, took);
             strm->next_in -= back;
             strm->avail_in += (uInt)back;
@@ -4335,23 +4432,16 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             append_new(put_abs);
             s->finished = 1;
             s->igz = (s->wrap & 2) && s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b;
+            s->fin_used = t.used;                               // the input past it goes back (inflate_body)
             if (t.stop == kIEnd) {
                 s->result = Z_STREAM_END;
-                const size_t extra = in_end - t.used;            // give back input past the stream end
-                const size_t back = std::min<size_t>(extra, took);
-                strm->next_in -= back;
-                strm->avail_in += (uInt)back;
-                strm->total_in = t.used - s->iadj;
                 if (s->wrap) strm->adler = s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b
                                                ? ck_crc32(0, o.data(), o.size())
                                                : ck_adler32(1, o.data(), o.size());
             } else {
                 s->result = Z_DATA_ERROR;
                 strm->msg = const_cast<char *>("invalid or corrupt deflate stream");
-                give_back_after(t.used);
             }
-            s->in.clear();
-            s->in.shrink_to_fit();
             return Z_OK;
         }
         if (resume && t.stop == kIData) {
@@ -4359,9 +4449,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             s->finished = 1;
             s->result = Z_DATA_ERROR;
             strm->msg = const_cast<char *>("invalid or corrupt deflate stream");
-            give_back_after(s->in_base + t.used);
-            s->in.clear();
-            s->in.shrink_to_fit();
+            s->fin_used = s->in_base + t.used;
             return Z_OK;
         }
         if (resume && t.stop == kIEnd) {                         // the final block: check the trailer
@@ -4388,18 +4476,13 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
                     if (!ok) strm->msg = const_cast<char *>(c != ck ? "incorrect data check" : "incorrect length check");
                 }
                 if (ok) {
-                    const uint64_t used = tpos + need;
-                    const size_t back = std::min<size_t>(in_end - used, took);
-                    strm->next_in -= back;
-                    strm->avail_in += (uInt)back;
-                    strm->total_in = used - s->iadj;
+                    s->fin_used = tpos + need;
                     if (s->wrap && !s->isync && s->ivalid) strm->adler = ck;
                     s->idt = 64;                                 // the last block, done
                 } else {
+                    s->fin_used = in_end;
                     s->result = Z_DATA_ERROR;
                 }
-                s->in.clear();
-                s->in.shrink_to_fit();
                 return Z_OK;
             }
             // the trailer is not all here: wait at the last block boundary
@@ -4410,24 +4493,12 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
         if (!resume) s->igz = (s->wrap & 2) && s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b;
         if (block)                                               // where the input ran out (inflate.c:1267-1269)
             s->idt = (int)(t.zstate & 0xffffffffu) + ((t.zstate >> 32) & 1u ? 64 : 0) + ((t.zstate >> 33) & 1u ? 128 : 0);
-        uint64_t bb = t.blk_bit, bp = t.blk_put;
-        if (resume) { bb += 8ull * s->in_base; bp += obase; }
-        if (bb && bb > s->res_bit) {
-            if (!resume) {
-                s->igz = (s->wrap & 2) && s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b;
-                s->icheck = s->igz ? 0u : 1u;
-            }
-            if (is_check) s->icheck = check_of(s->icheck, o.data() + (s->res_put - obase), (size_t)(bp - s->res_put));
-            const uint64_t h0 = bp > 32768 ? bp - 32768 : 0;      // the window before the new point
-            s->hist.assign(o.begin() + (std::ptrdiff_t)(h0 - obase), o.begin() + (std::ptrdiff_t)(bp - obase));
-            s->res_bit = bb;
-            s->res_put = bp;
-            s->imode = 1;
-            s->itype = true;
-            const uint64_t drop = (bb >> 3) - s->in_base;        // input before the boundary's byte
-            s->in.erase(s->in.begin(), s->in.begin() + (std::ptrdiff_t)drop);
-            s->in_base += drop;
-        }
+        // the resume point moves to the last block boundary at or before the
+        // output this call hands out: the reference may stop reading before
+        // later ones (inflate_body's accounting), and a caller that hands other
+        // bytes back decodes again from there
+        const uint64_t xlim = s->ideliv + std::min<uint64_t>(strm->avail_out, s->out.size() - s->out_pos);
+        advance_resume(s, o, obase, ixo, t, xlim);
         return Z_OK;
     }
 }
@@ -4497,16 +4568,105 @@ bool inflate_header_seen(const internal_state *s) {
     return m >= 4;                                              // gzip: FLAGS read (inflate.c FLAGS sets state->flags)
 }
 
+// Where the reference stops reading when its output space ends at absolute
+// output X with more output due: inflate.c's LIT, MATCH and COPY wait for room
+// only after the symbol's codes are read (a stored block: after the bytes
+// copied), and inf_leave returns the bytes pulled so far, the bit position
+// rounded up (inflate_fast returns the whole bytes it holds; the slow path pulls
+// a byte only when a code needs it).  From the last decode's symbol index
+// (InflateIndex); ~0 when X lies outside it.  dt: the data_type inflate.c
+// reports there (the bits it holds, + 64 in the last block; mode LIT / MATCH /
+// COPY).
+static uint64_t stall_from_index(const internal_state *s, uint64_t X, int *dt = nullptr) {
+    const std::vector<uint64_t> &e = s->ix;
+    if (X < s->ix_o0) return ~0ull;
+    size_t lo = 0, hi = e.size() / 2;                           // the first symbol whose output ends past X
+    while (lo < hi) {
+        const size_t m = (lo + hi) / 2;
+        if ((uint32_t)e[2 * m] + s->ix_obase > X) hi = m;
+        else lo = m + 1;
+    }
+    if (2 * lo == e.size()) return ~0ull;
+    const uint64_t a = e[2 * lo], v = e[2 * lo + 1];
+    const int last = (a >> 33) & 1u ? 64 : 0;
+    if ((a >> 32) & 1u) {                                       // a stored run: the bytes copied before X
+        const uint64_t start = lo ? (uint32_t)e[2 * lo - 2] + s->ix_obase : s->ix_o0;
+        if (dt) *dt = last;
+        return s->ix_ibase + v + (X - start);
+    }
+    const uint64_t c = (v + 7) >> 3;
+    if (dt) *dt = (int)(8 * c - v) + last;
+    return s->ix_ibase + c;
+}
+
+// the symbol index rebuilt from the resume point (at or before X) to 4 MiB of
+// output past X, the resume point moved up to X (the index of the last attempt
+// stops kIdxCap symbols after its start)
+static int refresh_index(internal_state *s, uint64_t X) {
+    const bool resume = s->imode == 1;
+    const size_t hl = resume ? s->hist.size() : 0;
+    const uint64_t from = resume ? s->res_put : 0;
+    const uint64_t cap = hl + std::min<uint64_t>(X - from + (4u << 20), 1ull << 31);
+    std::vector<uint8_t> o;
+    InflateTry t{};
+    InflateIndex ixo;
+    int rc;
+    {
+        Lease L;
+        rc = L.rc;
+        if (!rc) rc = inflate_try_locked(*L.c, s->in.data(), s->in.size(), resume,
+                                         resume ? s->res_bit - 8ull * s->in_base : 0, s->hist.data(), hl, cap,
+                                         s->wrap, s->wbits, o, t, 0, s->iback_win ? 1u << s->wbits : 0u, &ixo);
+    }
+    if (rc) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : rc;
+    const uint64_t obase = from - hl;
+    keep_index(s, ixo, obase, hl, t.stop != kIFull);
+    if (!s->finished) advance_resume(s, o, obase, ixo, t, X);
+    return Z_OK;
+}
+
 static int inflate_body(z_streamp strm, int flush) {
     if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
     if (!strm->next_out || (strm->avail_in && !strm->next_in)) return Z_STREAM_ERROR;   // inflate.c:610-612
     if (flush == 6 /* Z_TREES */) return Z_STREAM_ERROR;                               // documented gap
     if (s->need_dict) return Z_NEED_DICT;                      // inflate.c DICT: until the dictionary is set
+    const bool block = flush == Z_BLOCK;
+    const Bytef *const next0 = strm->next_in;
+    const uInt avail0 = strm->avail_in;
+    const uLong total0 = strm->total_in;
     // Z_BLOCK: while the block the last call stopped at is still being handed
     // out, the reference reads no more input
-    const bool block = flush == Z_BLOCK;
-    const size_t took = s->finished || (block && s->out_pos < s->out.size()) ? 0 : strm->avail_in;
+    const bool taking = !(s->finished || (block && s->out_pos < s->out.size()));
+    s->acct_done = false;
+    size_t took = 0;                 // bytes new to the engine
+    bool redo = false;               // decode again: the bytes handed back came back different
+    if (taking) {
+        // the bytes the last call handed back (in from cons on) are expected
+        // first; when they come back as they went (the same next_in, or equal
+        // bytes) what they decoded to stands, else the decode goes again from
+        // the resume point (at or before the output handed out) with what came
+        const uint64_t I = s->in_base + s->in.size();
+        uint64_t held = I > s->cons ? I - s->cons : 0;
+        if (held) {
+            // (after a Z_BLOCK stop the engine may have dropped input up to the
+            // block boundary's byte, past cons: those bytes are taken as they were)
+            const bool same = avail0 >= held &&
+                              (next0 == s->held_at || s->cons < s->in_base ||
+                               std::memcmp(next0, s->in.data() + (s->cons - s->in_base), (size_t)held) == 0);
+            if (!same && s->res_put <= s->ideliv && s->cons >= s->in_base) {
+                s->in.resize((size_t)(s->cons - s->in_base));
+                s->out.clear();
+                s->out_pos = 0;
+                s->tried = 0;
+                s->ix.clear();
+                s->ix_all = false;
+                held = 0;
+                redo = true;
+            }
+        }
+        took = avail0 > held ? (size_t)(avail0 - held) : 0;
+    }
     if (took && s->iprime_n) {
         // inflatePrime's bits: P virtual bytes in front of the input, the primed
         // bits their last ones (a decode reads each byte from bit 0 up), the
@@ -4515,6 +4675,7 @@ static int inflate_body(z_streamp strm, int flush) {
         const uint64_t v = s->iprime_v << (8 * P - s->iprime_n);
         for (uint32_t k = 0; k < P; k++) s->in.push_back((uint8_t)(v >> (8 * k)));
         s->iadj += P;
+        s->cons += P;
         s->res_bit = 8ull * P - s->iprime_n;
         s->res_put = s->ideliv;
         if (!s->imode) s->hist.clear();
@@ -4523,26 +4684,31 @@ static int inflate_body(z_streamp strm, int flush) {
         s->iprime_n = 0;
         s->iprime_v = 0;
     }
-    if (took) {
-        s->in.insert(s->in.end(), strm->next_in, strm->next_in + took);
-        strm->next_in += took;
+    const uint64_t T = s->cons;      // absolute input position of next0[0]
+    if (took) s->in.insert(s->in.end(), next0 + (avail0 - took), next0 + avail0);
+    if (taking) {                    // all of it for now; the accounting below hands back what the reference leaves
+        strm->next_in = next0 + avail0;
         strm->avail_in = 0;
-        strm->total_in += took;
+        strm->total_in = total0 + avail0;
     }
     gz_header_fill(s);
     // Decode what has arrived whenever input arrives: a stream that is still
     // open (a sync-flushed connection, a file read in pieces) hands out every
     // byte its input decodes to so far, as inflate() does (inflate.c:622-1221).
-    // Each attempt resumes at the last complete block (inflate_attempt).
+    // Each attempt resumes at a block boundary (inflate_attempt).
     const uint64_t in_end = s->in_base + s->in.size();
-    if (!s->finished && (took || s->itail || (flush == Z_FINISH && s->tried != in_end))) {
+    if (!s->finished && (took || redo || s->itail || (flush == Z_FINISH && s->tried != in_end))) {
         if (block) s->idt = 0;
-        if (int rc = inflate_attempt(strm, s, took, block)) return rc;
-        if (s->need_dict) return Z_NEED_DICT;
+        if (int rc = inflate_attempt(strm, s, taking ? avail0 : 0, block)) return rc;
+        if (s->need_dict) {
+            s->cons = strm->total_in + s->iadj;
+            s->held_at = strm->next_in;
+            return Z_NEED_DICT;
+        }
     }
     if (block) strm->data_type = s->idt;
     size_t give = 0;
-    if (s->out_pos < s->out.size() || s->finished) {
+    if (s->out_pos < s->out.size()) {
         give = std::min<size_t>(strm->avail_out, s->out.size() - s->out_pos);
         std::memcpy(strm->next_out, s->out.data() + s->out_pos, give);
         s->out_pos += give;
@@ -4550,10 +4716,42 @@ static int inflate_body(z_streamp strm, int flush) {
         strm->next_out += give;
         strm->avail_out -= (uInt)give;
         strm->total_out += give;
-        if (s->finished && s->out_pos == s->out.size()) return s->result;
     }
-    if (took || give) return Z_OK;
-    return Z_BUF_ERROR;                                                // inflate.c:1265-1266: no progress
+    // the input this call consumed (inflate.c inf_leave): all of it unless the
+    // output space ended first, then up to the reference's stop at the output
+    // handed out (stall_from_index); a finished stream's up to its end
+    const bool pending = s->out_pos < s->out.size();
+    if (s->acct_done) {
+        s->cons = strm->total_in + s->iadj;
+    } else {
+        uint64_t C;
+        if (pending) {
+            int dt = -1;
+            C = stall_from_index(s, s->ideliv, &dt);
+            if (C == ~0ull) {
+                if (int rc = refresh_index(s, s->ideliv)) return rc;
+                C = stall_from_index(s, s->ideliv, &dt);
+            }
+            if (C == ~0ull) C = s->finished ? s->fin_used : s->in_base + s->in.size();
+            if (block && dt >= 0) strm->data_type = dt;        // stopped for room, not at a block boundary
+        } else {
+            C = s->finished ? s->fin_used : s->in_base + s->in.size();
+        }
+        const uint64_t used = std::min<uint64_t>(C > T ? C - T : 0, avail0);
+        strm->next_in = next0 + used;
+        strm->avail_in = avail0 - (uInt)used;
+        strm->total_in = total0 + used;
+        s->cons = T + used;
+        if (s->finished && !pending) {
+            s->in.clear();
+            s->in.shrink_to_fit();
+        }
+    }
+    s->held_at = strm->next_in;
+    if (s->finished && !pending) return s->result;
+    // inflate.c:1261-1262: no progress, or Z_FINISH short of the stream end
+    if ((strm->next_in == next0 && give == 0) || flush == Z_FINISH) return Z_BUF_ERROR;
+    return Z_OK;
 }
 
 // inflateSetDictionary (inflate.c): a zlib stream that answered Z_NEED_DICT
@@ -4632,7 +4830,9 @@ int inflateBack(z_streamp strm, in_func in, void *in_desc, out_func out, void *o
     unsigned left = wsize;                                               // window bytes still free
     int ret = Z_BUF_ERROR;
     for (;;) {
-        if (have == 0) {
+        // in() only when the decode has nothing left to hand out (infback.c
+        // pulls input when a code needs bits; a full window goes to out() first)
+        if (have == 0 && s->out_pos >= s->out.size()) {
             have = in(in_desc, &next);
             if (have == 0) { next = nullptr; ret = Z_BUF_ERROR; break; }
         }
@@ -4650,23 +4850,7 @@ int inflateBack(z_streamp strm, in_func in, void *in_desc, out_func out, void *o
             if (out(out_desc, win, wsize)) { ret = Z_BUF_ERROR; left = wsize; break; }
             left = wsize;
         }
-        // the decode keeps what it has not handed out yet: drain it into the window
-        while (s->out_pos < s->out.size() && left) {
-            strm->next_in = next;
-            strm->avail_in = 0;
-            strm->next_out = win + (wsize - left);
-            strm->avail_out = left;
-            const int r2 = inflate(strm, Z_NO_FLUSH);
-            left = strm->avail_out;
-            if (left == 0) {
-                if (out(out_desc, win, wsize)) { ret = Z_BUF_ERROR; left = wsize; goto leave; }
-                left = wsize;
-            }
-            if (r2 == Z_STREAM_END) { ret = Z_STREAM_END; goto leave; }
-            if (r2 != Z_OK) { ret = r2; goto leave; }
-        }
     }
-leave:
     // inf_leave: the window's leftover output, then the unused input
     if (left < wsize && out(out_desc, win, wsize - left) && ret == Z_STREAM_END) ret = Z_BUF_ERROR;
     strm->next_in = next;
@@ -4745,6 +4929,10 @@ int inflateSync(z_streamp strm) {
     }
     s->out_pos = 0;
     s->in_base = strm->total_in + s->iadj;                     // absolute input position
+    s->cons = s->in_base;
+    s->held_at = strm->next_in;
+    s->ix.clear();
+    s->ix_all = false;
     s->finished = 0;
     s->result = Z_OK;
     s->tried = 0;

@@ -271,6 +271,8 @@ __device__ __attribute__((noinline)) uint32_t codes_used(const uint16_t *lens, i
     return cu[47];
 }
 
+// kIdx: the streaming inflate()'s consumption index (InflateJob::eidx / bidx)
+template <bool kIdx>
 __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
     __shared__ InfLDS S;
     const int lane = threadIdx.x;
@@ -318,6 +320,16 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
     }
 
     auto ceil_used = [&]() -> uint64_t { return (bitpos(r) + 7) >> 3; };
+    uint32_t ne = 0, nbk = 0;                        // index entries / block boundaries recorded (kIdx)
+    auto index_sym = [&](uint32_t out_end, bool stored, uint64_t v) {
+        if (kIdx) {
+            if (lane == 0 && ne < job.ecap) {
+                job.eidx[2 * (uint64_t)ne] = (uint64_t)out_end | (uint64_t)stored << 32 | (uint64_t)zlast << 33;
+                job.eidx[2 * (uint64_t)ne + 1] = v;
+            }
+            ne++;
+        }
+    };
     auto flush_obuf = [&](uint32_t upto) {          // output bytes [ob, upto), upto <= ob + kOBuf
         __syncthreads();
         if (!probe && !counting)
@@ -415,6 +427,7 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
             uint32_t cnt = len;
             if (cnt > n - bp) cnt = n - bp;
             if (cnt > cap - put) cnt = cap - put;
+            if (cnt) index_sym(put + cnt, true, bp);
             if (probe) { if (cnt) pbyte = in[bp]; }
             else if (!counting) for (uint32_t i = (uint32_t)lane; i < cnt; i += 64) out[put + i] = in[bp + i];
             put += cnt;
@@ -519,6 +532,7 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
                 if (bitpos(r) + L > inbits) { zmark = 0; stop = kIInEnd; used = n; goto done; }   // LEN: back 0
                 dropb(r, L);
                 if (sym < 256) {
+                    index_sym(put + 1, false, bitpos(r));
                     if (put == cap) { stop = kIFull; used = ceil_used(); goto done; }
                     if (probe) pbyte = sym;
                     else if (lane == 0) S.obuf[put - ob] = (uint8_t)sym;
@@ -542,6 +556,7 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
                 if (bitpos(r) + xd > inbits) { zmark = (int64_t)(L + xl + DL) << 16; stop = kIInEnd; used = n; goto done; }
                 const uint32_t dist = c_dbase[ds] + ((uint32_t)r.hold & ((1u << xd) - 1u));
                 dropb(r, xd);
+                index_sym(put + len, false, bitpos(r));
                 if (put == cap) { stop = kIFull; used = ceil_used(); goto done; }    // MATCH: room first
                 // too far back (inflateBack: beyond its window, infback.c:494-499)
                 if (dist > put || (job.dmax && dist > job.dmax)) { stop = kIData; used = ceil_used(); goto done; }
@@ -565,6 +580,13 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
         if (last) break;
         blk_bit = bitpos(r);                         // a block boundary: resumable here
         blk_put = put;
+        if (kIdx) {
+            if (lane == 0 && nbk < job.bcap) {
+                job.bidx[2 * (uint64_t)nbk] = blk_bit;
+                job.bidx[2 * (uint64_t)nbk + 1] = blk_put;
+            }
+            nbk++;
+        }
     }
     ztype = false;                                   // TYPEDO -> CHECK
 
@@ -615,6 +637,10 @@ done:
         rc.pbyte = pbyte;
         job.rec[bi] = rc;
         job.dst_len[g] = probe ? 0 : put;            // the checksum kernels read this
+        if (kIdx) {
+            job.icnt[0] = ne;
+            job.icnt[1] = nbk;
+        }
         if (job.blk_out) {
             job.blk_out[2 * (uint64_t)g] = blk_bit;
             job.blk_out[2 * (uint64_t)g + 1] = blk_put;
@@ -975,7 +1001,10 @@ int launch_infl_resolve(uint8_t *out, const uint32_t *sym, uint64_t o0, uint64_t
 int launch_inflate_stage(int stage, const InflateJob &job, hipStream_t st) {
     if (job.count == 0) return 0;
     switch (stage) {
-    case 0: hipLaunchKernelGGL(k_inflate_decode, dim3(job.count), dim3(64), 0, st, job); break;
+    case 0:
+        if (job.eidx) hipLaunchKernelGGL(k_inflate_decode<true>, dim3(job.count), dim3(64), 0, st, job);
+        else hipLaunchKernelGGL(k_inflate_decode<false>, dim3(job.count), dim3(64), 0, st, job);
+        break;
     case 1: hipLaunchKernelGGL(k_inflate_copy, dim3(job.count), dim3(64), 0, st, job); break;
     case 2: hipLaunchKernelGGL(k_inflate_finish, dim3((job.count + 255) / 256), dim3(256), 0, st, job); break;
     default: return -1;

@@ -386,6 +386,14 @@ struct InflateJob {
     // records, no capacity limit; dst_len / rec / blk_out report where the
     // decode ended and how much it would have produced
     int count_only;
+    // the streaming inflate()'s consumption index (one-stream jobs; null: off): per symbol that
+    // writes output, eidx[2k] = its output end (low 32 bits) | stored run << 32 | BFINAL of its
+    // block << 33, eidx[2k + 1] = the input bit position once its codes are read (a stored run:
+    // its first input byte).  bidx[2k], [2k + 1] = bit and output position of each block
+    // boundary.  icnt[0], [1] = entries / boundaries met (may exceed ecap / bcap)
+    uint64_t *eidx, *bidx;
+    uint32_t *icnt;
+    uint32_t ecap, bcap;
 };
 int launch_inflate_stage(int stage, const InflateJob &job, hipStream_t st);
 // the block-parallel decode of a lone stream (zgpu_inflate.hip, zgpu_api.cpp inflate_par)
