@@ -9,9 +9,11 @@
  * uncompress()/uncompress2() return what the reference returns for every input
  * (valid, corrupt, truncated, short output), with the same output and the same
  * consumed length.  inflate() decodes whenever input arrives and hands out
- * every byte decoded so far; each attempt resumes at the last complete block
- * with the 32 KiB window carried (linear in the stream), and the trailer is
- * checked as inflate.c does.  inflateSetDictionary() answers Z_NEED_DICT
+ * every byte decoded so far; each attempt resumes at a block boundary with the
+ * 32 KiB window carried (linear in the stream), and the trailer is checked as
+ * inflate.c does.  A call whose output space ends first consumes the input
+ * inflate.c would (up to the codes of the symbol it has no room for) and hands
+ * the rest back in next_in / avail_in.  inflateSetDictionary() answers Z_NEED_DICT
  * (zlib streams) or presets a raw stream's window before its first input.
  *
  * deflate() semantics: deflateInit2_ accepts windowBits 8..15 (zlib), -9..-15
@@ -52,8 +54,7 @@
  *   - deflateSetDictionary after the stream has ended;
  *   - deflateResetKeep on a stream that has taken input (the window it would
  *     carry into the next stream);
- *   - inflatePrime other than on a raw stream before its first input;
- *   - inflate(Z_TREES).
+ *   - inflatePrime other than on a raw stream before its first input.
  * inflateUndermine returns Z_DATA_ERROR (as a reference built without
  * INFLATE_ALLOW_INVALID_DISTANCE_TOOFAR_ARRR does).  inflateBack reports a
  * distance beyond its window at the first such distance; where out() fails,
@@ -103,6 +104,7 @@ typedef z_stream *z_streamp;
 #define Z_FULL_FLUSH    3
 #define Z_FINISH        4
 #define Z_BLOCK         5
+#define Z_TREES         6
 #define Z_OK            0
 #define Z_STREAM_END    1
 #define Z_NEED_DICT     2                                                  /* zlib.h:183 */
@@ -200,9 +202,11 @@ int inflateReset(z_streamp strm);                                       /* zlib.
 int inflateGetHeader(z_streamp strm, gz_headerp head);                  /* zlib.h inflateGetHeader; inflate.c:1330 */
 int inflateSync(z_streamp strm);                                        /* zlib.h inflateSync; inflate.c:1375 */
 int inflateCopy(z_streamp dest, z_streamp source);                      /* zlib.h inflateCopy; inflate.c:1439 */
-/* inflate(flush): Z_NO_FLUSH, Z_SYNC_FLUSH, Z_FINISH and Z_BLOCK (stop at the
- * next block boundary, or after a zlib / gzip header; strm->data_type as
- * inflate.c sets it there); Z_TREES is refused (Z_STREAM_ERROR) */
+/* inflate(flush): Z_NO_FLUSH, Z_SYNC_FLUSH, Z_FINISH (Z_BUF_ERROR short of the
+ * stream end), Z_BLOCK (stop at the next block boundary, or after a zlib / gzip
+ * header; strm->data_type as inflate.c sets it there) and Z_TREES (also after
+ * each block header, data_type + 256).  inflateSync searches the whole bytes
+ * the reference holds in its bit buffer first (inflate.c:1388-1398). */
 int inflateReset2(z_streamp strm, int windowBits);                      /* zlib.h inflateReset2; inflate.c:153 */
 int inflateResetKeep(z_streamp strm);                                   /* zlib.h inflateResetKeep; inflate.c:105 */
 int inflatePrime(z_streamp strm, int bits, int value);                  /* zlib.h inflatePrime; inflate.c:223

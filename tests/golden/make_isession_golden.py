@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.dirname(HERE))
 import datagen  # noqa: E402
 from zhelpers import Reference, run_iops  # noqa: E402
 
-Z_NO_FLUSH, Z_SYNC_FLUSH, Z_FULL_FLUSH, Z_FINISH, Z_BLOCK = 0, 2, 3, 4, 5
+Z_NO_FLUSH, Z_SYNC_FLUSH, Z_FULL_FLUSH, Z_FINISH, Z_BLOCK, Z_TREES = 0, 2, 3, 4, 5, 6
 
 
 def build_z(spec):
@@ -125,6 +125,45 @@ def sessions():
     S.append({"name": "sync-none", "spec": {"data": text, "fmt": "zlib"}, "ops": [
         ["init", 15], ["feed", 2], ["inflate", Z_NO_FLUSH, 1 << 20], ["sync"], ["skip", 100], ["feed", 1 << 30],
         ["sync"]]})
+    # inflateSync after a call whose input ended inside a flush marker's LEN /
+    # NLEN: the reference searches the whole bytes in its bit buffer first
+    # (inflate.c:1388-1398), so the marker it was reading is found (round 5)
+    for fmt, wb in (("zlib", 15), ("gzip", 31), ("raw", -15)):
+        spec = {"data": mix, "fmt": fmt, "cuts": [[40000, Z_FULL_FLUSH], [100000, Z_SYNC_FLUSH]]}
+        z = build_z(spec)
+        m = z.find(b"\x00\x00\xff\xff", 100)
+        for k in (1, 2, 3, 4):
+            S.append({"name": f"sync-held-{fmt}-{k}", "spec": spec, "ops": [
+                ["init", wb], ["feed", m + k], ["inflate", Z_NO_FLUSH, 1 << 20], ["sync"], ["feed", 3], ["sync"],
+                ["feed", 1 << 30], ["sync"], ["loop", Z_NO_FLUSH, 1 << 20]]})
+    # output space smaller than the stream's output, all the input at once: each
+    # call stops reading where inflate.c stops for room (round 5)
+    for fmt, wb in (("zlib", 15), ("gzip", 31), ("raw", -15)):
+        for data, out in ((["text", 6000, 61], 1), (["mix", 60000, 62], 997), (mix, 65536)):
+            spec = {"data": data, "fmt": fmt, "cuts": [[len(datagen.make(*data)) // 2, Z_SYNC_FLUSH]]}
+            S.append({"name": f"smallout-{fmt}-{out}", "spec": spec,
+                      "ops": [["init", wb], ["feed", 1 << 30], ["loop", Z_NO_FLUSH, out]]})
+            S.append({"name": f"smallout-block-{fmt}-{out}", "spec": spec,
+                      "ops": [["init", wb], ["feed", 1 << 30], ["loop", Z_BLOCK, out]]})
+        S.append({"name": f"smallout-pieces-{fmt}", "spec": {"data": mix, "fmt": fmt, "cuts": [[70000, Z_SYNC_FLUSH]]},
+                  "ops": [["init", wb]] + feed_loop(30000, 7000, Z_NO_FLUSH, 3001) + [["feed", 1 << 30],
+                                                                                  ["loop", Z_NO_FLUSH, 1 << 20]]})
+    # inflate(Z_TREES): Z_BLOCK's stops and one after each block header, before
+    # its first code (mode LEN_ / COPY_, data_type + 256; round 5)
+    for fmt, wb in (("zlib", 15), ("gzip", 31), ("raw", -15)):
+        for level, st in ((6, 0), (0, 0), (6, 4), (1, 2)):
+            spec = {"data": mix, "level": level, "strategy": st, "fmt": fmt,
+                    "cuts": [[30000, Z_SYNC_FLUSH], [90000, Z_FULL_FLUSH], [91000, Z_SYNC_FLUSH]]}
+            S.append({"name": f"trees-{fmt}-L{level}-s{st}", "spec": spec,
+                      "ops": [["init", wb], ["feed", 1 << 30], ["loop", Z_TREES, 1 << 20]]})
+        spec = {"data": text, "level": 6, "fmt": fmt, "cuts": [[50000, Z_SYNC_FLUSH]]}
+        S.append({"name": f"trees-chunks-{fmt}", "spec": spec,
+                  "ops": [["init", wb]] + feed_loop(40000, 997, Z_TREES, 4001) + [["feed", 1 << 30],
+                                                                                ["loop", Z_TREES, 1 << 20]]})
+        S.append({"name": f"trees-mixed-{fmt}", "spec": spec, "ops": [
+            ["init", wb], ["feed", 30000], ["inflate", Z_NO_FLUSH, 5000], ["inflate", Z_TREES, 1 << 20],
+            ["inflate", Z_TREES, 1 << 20], ["inflate", Z_BLOCK, 100], ["inflate", Z_TREES, 1 << 20],
+            ["feed", 1 << 30], ["loop", Z_TREES, 1 << 20]]})
     # inflateCopy: two streams from one state
     for at in (2, 30000, 1 << 30):
         S.append({"name": f"copy-at-{at}", "spec": {"data": mix, "fmt": "zlib", "cuts": [[70000, Z_SYNC_FLUSH]]},

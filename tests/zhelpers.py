@@ -577,7 +577,7 @@ def run_iops(L, z, ops, version=b"1.3.1.1-motley"):
         outs[act].extend(ob.raw[: n - s.avail_out])
         got = n - s.avail_out
         r = [rc, s.avail_in, s.total_in, s.total_out]
-        if flush == 5 and rc == 0:
+        if flush in (5, 6) and rc == 0:          # Z_BLOCK, Z_TREES
             r.append(s.data_type)
         return r, got
 

@@ -254,7 +254,6 @@ struct Ctx {
     DevBuf ws_ck;             // split checksum partials (few large buffers)
     DevBuf ws_srec, ws_snap;  // a streaming job's block records and head[] snapshot
     DevBuf ws_srt, ws_boff, ws_work, ws_bblk;   // the sorted-run match (k_bsort / k_bwork / k_match2)
-    DevBuf ws_ibits;                            // k_parse_srt's inserted-position bitmap (streaming jobs)
     DevBuf ws_m2seg;                            // k_match2's (buffer, first block) ranges
     // inflate: match records, per-stream results, checks, offsets, stop codes
     DevBuf ws_mrec, ws_irec, ws_ick, ws_imeta, ws_istop;
@@ -437,7 +436,6 @@ struct FlushSpec {
     int zp0 = kMinMatch - 1, zm0 = kMinMatch - 1;   // DeflateJob::zp0 / zm0
     int seg_parse = 0;             // the job's stops are all Z_NO_FLUSH: k_pbig* may parse it (k_pbig6s)
     SkipSpec sk{};                 // DeflateJob::sk
-    int srt_parse = 0;             // levels 1..3, stops only, from the stream's start: k_parse_srt<kEv>
 };
 
 // deflateInit2_'s windowBits / memLevel rules (deflate.c:400-425): negative
@@ -495,9 +493,16 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     // one sequential lane per buffer, so they get 4x the budget: more buffers
     // in flight is what their throughput scales with.
     // (levels 1..3 from the sorted runs keep ~28 B per byte: the plain budget, at most 4 GiB)
-    static const int fsrt_env0 = [] { const char *e = std::getenv("ZGPU_FAST_SRT"); return e ? std::atoi(e) : 0; }();
-    const bool fsrt_want = fsrt_env0 == 1 && level >= 1 && level <= 3 && strategy != 2 && strategy != 3 &&
-                           (!fs || fs->srt_parse) && hbits <= 15;
+    // By default only few buffers at levels 2..3 take it (a lone 1 MiB buffer:
+    // 4.2-4.8 MB/s against 1.1-1.4 on k_parse_fast's one lane; at level 1 and
+    // for batches the chain walk is as fast or faster);
+    // ZGPU_FAST_SRT=1 / 0: always / never
+    static const int fsrt_env0 = [] { const char *e = std::getenv("ZGPU_FAST_SRT"); return e ? std::atoi(e) : -1; }();
+    uint64_t total_in = 0;
+    for (uint32_t i = 0; i < count; i++) total_in += lens[i];
+    const bool fsrt_ok = level >= 1 && level <= 3 && strategy != 2 && strategy != 3 && !fs && hbits <= 15;
+    const bool fsrt_want = fsrt_ok && (fsrt_env0 == 1 || (fsrt_env0 == -1 && level >= 2 && count <= 16 &&
+                                                           total_in <= (256ull << 20)));
     const uint64_t budget = fsrt_want ? std::min<uint64_t>(c.inflight, 4ull << 30)
                             : (level >= 1 && level <= 3) || strategy == 2 || strategy == 3
                                 ? 4 * (uint64_t)c.inflight : (uint64_t)c.inflight;
@@ -634,10 +639,6 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     // levels 1..3 of a batch job from the same sorted runs (k_bwork<true> +
     // k_parse_srt; ZGPU_FAST_SRT=1)
     bool fsrt = fsrt_want;
-    if (fsrt && fs && (!c.ws_ibits.ensure(max_pos / 8 + 256) || !fs->snap)) {
-        (void)hipGetLastError();
-        return zfail(__LINE__);
-    }
     std::vector<uint32_t> bblk;
     std::vector<size_t> bblk_at(nsub + 1, 0);
     uint64_t max_sblk = 0;
@@ -812,7 +813,6 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.boff = c.ws_boff.as<uint16_t>();
             job.work = c.ws_work.as<uint4>();
             job.nsblk = bblk[bblk_at[s + 1] - 1];
-            if (fs) job.ins_bits = c.ws_ibits.as<uint32_t>();
             if (m2) {                                   // k_match2's ranges of blocks (or none)
                 job.seg = m2seg_at[s + 1] > m2seg_at[s] ? c.ws_m2seg.as<uint32_t>() + 2 * m2seg_at[s] : nullptr;
                 job.nseg = (uint32_t)(m2seg_at[s + 1] - m2seg_at[s]);
@@ -1003,7 +1003,6 @@ struct FlushHost {
     int keep_head = 0;
     int zp0 = kMinMatch - 1, zm0 = kMinMatch - 1;   // DeflateJob::zp0 / zm0
     int seg_parse = 0;                 // see FlushSpec
-    int srt_parse = 0;                 // see FlushSpec
     SkipSpec sk{};                     // see FlushSpec
 };
 
@@ -1102,7 +1101,6 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
         fs.zp0 = fh->zp0;
         fs.zm0 = fh->zm0;
         fs.seg_parse = fh->seg_parse;
-        fs.srt_parse = fh->srt_parse;
         fs.sk = fh->sk;
         if (fh->rec_out) {
             const size_t sym_limit = (size_t(1) << (mem_level + 6)) - 1;         // lit_bufsize - 1
@@ -2424,9 +2422,16 @@ struct internal_state {
     // trailer included); acct_done: the attempt set next_in / total_in itself
     uint64_t cons = 0, fin_used = 0;
     const Bytef *held_at = nullptr;
-    std::vector<uint64_t> ix;
-    uint64_t ix_ibase = 0, ix_obase = 0, ix_o0 = 0;
+    std::vector<uint64_t> ix, ix2;                       // ix2: an earlier index that starts lower
+    uint64_t ix_ibase = 0, ix_obase = 0, ix_o0 = 0, ix2_ibase = 0, ix2_obase = 0, ix2_o0 = 0;
     bool ix_all = false, acct_done = false;
+    std::vector<uint64_t> bx;                            // the last decode's block boundaries (absolute bit, output)
+    uint64_t bx_last = ~0ull;                            // the bit of the one that ends the last block (a Z_BLOCK stop)
+    uint64_t out_at = 0;                                 // absolute output of out[0] (out_pos = ideliv - out_at)
+    // the bits inflate.c holds in its bit buffer after the last call: where the
+    // input ran out (iheld_end, from the last decode), or below 8 at a stop for
+    // room (inflateSync searches the whole bytes among them first)
+    uint32_t iheld = 0, iheld_end = 0;
     // deflateTune (deflate.c:805-820): the jobs' good/lazy/nice/chain
     bool tuned = false;
     LevelCfg tune{};
@@ -2711,18 +2716,6 @@ int deflate_part(internal_state *s, bool closed) {
     if (!closed && nev == 0) stops_only = false;
     for (size_t i = 0; stops_only && i < nev; i++) stops_only = s->ev_type[s->res_ev + i] == 0;
     fh.seg_parse = stops_only ? 1 : 0;
-    // deflate_fast over Z_NO_FLUSH stops from the stream's start (a large
-    // deflate() call, compress2 over 4 GiB at levels 1..3): k_parse_srt, the
-    // block-parallel encoder, and the chains at the last cut rebuilt for the
-    // job that resumes there (k_srt_chains)
-    {
-        static const int fsrt_env = [] { const char *e = std::getenv("ZGPU_FAST_SRT"); return e ? std::atoi(e) : 0; }();
-        bool srt = fsrt_env == 1 && fast && s->mem_level <= 8 && fh.start == 0 && !fh.dict && !fh.head_in &&
-                   cpos.empty() && fh.lk_n == 0 && fh.zp0 == kMinMatch - 1 && fh.zm0 == kMinMatch - 1 &&
-                   fh.sk.n == 0 && sl >= seg_min && (closed || nev > 0);
-        for (size_t i = 0; srt && i < nev; i++) srt = s->ev_type[s->res_ev + i] == 0;
-        if (srt) fh.srt_parse = fh.seg_parse = 1;
-    }
     ZTRACE("part: base %zu nev %zu sl %zu cap %zu start %u bit0 %u e0 %u cut %d fast %d\n", base, nev, sl, cap,
            fh.start, fh.bit0, fh.e0, fh.cut, (int)fast);
     {
@@ -4039,7 +4032,9 @@ int inflateReset(z_streamp strm) {
     s->iwin.clear(); s->iwin_on = false;                               // wsize = whave = wnext = 0
     s->isyncpt = false; s->imark = -65536; s->icodes = 0; s->iprime_n = 0; s->iprime_v = 0;
     s->iadl_on = false; s->iadl = 0;
-    s->cons = s->fin_used = 0; s->held_at = nullptr; s->ix.clear(); s->ix_all = false;
+    s->cons = s->fin_used = 0; s->held_at = nullptr; s->ix.clear(); s->ix2.clear(); s->ix_all = false;
+    s->bx.clear(); s->out_at = 0;
+    s->iheld = s->iheld_end = 0;
     strm->total_in = strm->total_out = 0;
     strm->msg = nullptr;
     if (s->wrap) strm->adler = s->wrap & 1;                           // inflateResetKeep: only when wrapped
@@ -4190,39 +4185,75 @@ uint32_t stream_check(const internal_state *s, uint32_t init, const uint8_t *p, 
     return s->igz ? ck_crc32(init, p, n) : ck_adler32(init, p, n);
 }
 
-// the symbol index of a decode whose output array o starts at absolute output
-// obase, hist_len bytes of window in front (InflateIndex); `whole`: the decode
-// ran to its own end (not cut at its output capacity)
-void keep_index(internal_state *s, InflateIndex &ix, uint64_t obase, size_t hist_len, bool whole) {
+// the symbol index and block boundaries of a decode whose output array starts
+// at absolute output obase, hist_len bytes of window in front (InflateIndex,
+// InflateTry::blk_*: the last boundary); `whole`: the decode ran to its own
+// end (not cut at its output capacity).  Of the two earlier indexes the one
+// that starts lower stays as ix2: after a Z_BLOCK stop the resume point (where
+// later decodes start) can lie past the output handed out.
+void keep_index(internal_state *s, InflateIndex &ix, const InflateTry &t, uint64_t obase, size_t hist_len,
+                bool whole) {
+    // the second index: the previous one, unless only the older one reaches
+    // the output handed out so far
+    auto covers = [&](const std::vector<uint64_t> &e, uint64_t eobase, uint64_t o0) {
+        return !e.empty() && o0 <= s->ideliv && (uint32_t)e[e.size() - 2] + eobase > s->ideliv;
+    };
+    if (!s->ix.empty() && (covers(s->ix, s->ix_obase, s->ix_o0) || !covers(s->ix2, s->ix2_obase, s->ix2_o0))) {
+        s->ix2.swap(s->ix);
+        s->ix2_ibase = s->ix_ibase;
+        s->ix2_obase = s->ix_obase;
+        s->ix2_o0 = s->ix_o0;
+    }
     s->ix.swap(ix.e);
     s->ix_ibase = s->in_base;
     s->ix_obase = obase;
     s->ix_o0 = obase + hist_len;
     s->ix_all = whole && 2ull * ix.ne <= s->ix.size();
+    const uint64_t ib = 8ull * s->in_base;                        // the decode's in[0] is in_base (0 from the start)
+    s->bx.clear();
+    s->bx_last = ~0ull;
+    auto add = [&](uint64_t b, uint64_t p, bool abs) {
+        if (!abs) { b += ib; p += obase; }
+        if (b && (s->bx.empty() || b > s->bx[s->bx.size() - 2])) {
+            s->bx.push_back(b);
+            s->bx.push_back(p);
+        }
+    };
+    if (s->imode == 1) add(s->res_bit, s->res_put, true);           // where the decode started
+    for (size_t k = 0; k + 1 < ix.b.size(); k += 2) {
+        const uint64_t b = ix.b[k] & ~(1ull << 63);
+        add(b, ix.b[k + 1], false);
+        if (ix.b[k] >> 63) s->bx_last = b + ib;
+    }
+    if (t.stop != kITrees) add(t.blk_bit, t.blk_put, false);     // (a Z_TREES stop's is a header's end)
+    if (t.stop == kIBlock && ((t.zstate >> 32) & 1u)) s->bx_last = t.blk_bit + ib;
 }
 
 // the resume point (res_bit, res_put, hist, icheck) moved to the last block
-// boundary of a decode (output o from absolute output obase) whose output is
-// at most xlim, when that is past the current one; input before the
-// boundary's byte is dropped
-void advance_resume(internal_state *s, const std::vector<uint8_t> &o, uint64_t obase, const InflateIndex &ix,
-                    const InflateTry &t, uint64_t xlim) {
-    const bool resume = s->imode == 1;
-    const uint64_t ib = resume ? 8ull * s->in_base : 0, ob = resume ? obase : 0;
+// boundary of the last decode at or before output xlim and input bit blim
+// (where the reference stands), when that is past the current one.  The check
+// and the window come from s->out, which keeps the output from the window
+// before the resume point on; input before the boundary's byte is dropped.
+void advance_resume(internal_state *s, uint64_t xlim, uint64_t blim, bool last_ok = false) {
     uint64_t bb = 0, bp = 0;
-    auto take = [&](uint64_t b, uint64_t p) {
-        if (b && p + ob <= xlim && b + ib > bb) { bb = b + ib; bp = p + ob; }
-    };
-    for (size_t k = 0; k + 1 < ix.b.size(); k += 2) take(ix.b[k], ix.b[k + 1]);
-    take(t.blk_bit, t.blk_put);
-    if (!bb || bb <= s->res_bit) return;
-    if (!resume) {
+    for (size_t k = 0; k + 1 < s->bx.size(); k += 2)      // (the last block's end only for its trailer: itail)
+        if (s->bx[k] <= blim && s->bx[k + 1] <= xlim && s->bx[k] > bb && (last_ok || s->bx[k] != s->bx_last)) {
+            bb = s->bx[k];
+            bp = s->bx[k + 1];
+        }
+    if (!bb || bb <= s->res_bit || bp < s->res_put) return;
+    const uint64_t h0 = bp > 32768 ? bp - 32768 : 0;              // the window before the new point
+    if (h0 < s->out_at || s->res_put < s->out_at || bp > s->out_at + s->out.size() ||
+        (bb >> 3) < s->in_base || (bb >> 3) > s->in_base + s->in.size())
+        return;
+    if (s->imode == 0) {
         s->igz = (s->wrap & 2) && s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b;
         s->icheck = s->igz ? 0u : 1u;
     }
-    if (s->wrap != 0) s->icheck = stream_check(s, s->icheck, o.data() + (s->res_put - obase), (size_t)(bp - s->res_put));
-    const uint64_t h0 = bp > 32768 ? bp - 32768 : 0;              // the window before the new point
-    s->hist.assign(o.begin() + (std::ptrdiff_t)(h0 - obase), o.begin() + (std::ptrdiff_t)(bp - obase));
+    const uint8_t *o = s->out.data();                              // o[x - out_at]: absolute output byte x
+    if (s->wrap != 0)
+        s->icheck = stream_check(s, s->icheck, o + (s->res_put - s->out_at), (size_t)(bp - s->res_put));
+    s->hist.assign(o + (h0 - s->out_at), o + (bp - s->out_at));
     s->res_bit = bb;
     s->res_put = bp;
     s->imode = 1;
@@ -4230,13 +4261,18 @@ void advance_resume(internal_state *s, const std::vector<uint8_t> &o, uint64_t o
     const uint64_t drop = (bb >> 3) - s->in_base;                 // input before the boundary's byte
     s->in.erase(s->in.begin(), s->in.begin() + (std::ptrdiff_t)drop);
     s->in_base += drop;
+    if (h0 > s->out_at && h0 <= s->ideliv) {                      // output before the window is not needed again
+        s->out.erase(s->out.begin(), s->out.begin() + (std::ptrdiff_t)(h0 - s->out_at));
+        s->out_at = h0;
+        s->out_pos = (size_t)(s->ideliv - s->out_at);
+    }
 }
 
 // One decode attempt of the streaming inflate() over the input gathered so
 // far: from the stream start until a block is complete, then from the last
 // block boundary.  Sets s->out (bytes not handed out yet), s->finished and
 // s->result; `took` input bytes of this call may be handed back past the end.
-int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block = false) {
+int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block = false, bool trees = false) {
     const uint64_t in_end = s->in_base + s->in.size();
     if (s->cap == 0) s->cap = std::max<size_t>(4 * s->in.size(), 1 << 16);
     const bool is_check = s->wrap != 0;
@@ -4245,7 +4281,9 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
     };
     if (s->itail) {
         // the last block is out (an inflate(Z_BLOCK) stopped after it): the
-        // trailer, byte aligned after it (inflate.c TYPEDO .. LENGTH)
+        // trailer, byte aligned after it (inflate.c TYPEDO .. LENGTH), read
+        // once the block's output is all handed out
+        if (s->out_pos < s->out.size()) return Z_OK;
         const uint64_t tpos = (s->res_bit + 7) >> 3;
         const uint64_t need = !s->wrap || s->isync == 2 ? 0 : s->igz ? 8 : 4;
         if (in_end < tpos + need) {
@@ -4292,6 +4330,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
         // call already took the whole header, the decode is mid-block and this
         // call runs to the end of the first block
         bool hdr_done = false;
+        size_t hdr_len = 0;
         if (block && !resume && s->wrap && s->in.size() >= took) {
             const size_t before = s->in.size() - took;          // input the earlier calls gave
             const uint8_t *h = s->in.data();
@@ -4319,7 +4358,14 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
                 if (hlen > before) hlen = 0;
             }
             hdr_done = hlen != 0;
+            hdr_len = hlen;
         }
+        // inflate(Z_TREES) also stops after a block header (inflate.c STORED,
+        // fixed TYPEDO, CODELENS: LEN_ / COPY_) when the reference stands at
+        // that block's start: in mode TYPE (or TYPEDO) exactly where it stopped
+        const uint64_t pref = 8 * s->cons - s->iheld;            // the reference's bit position
+        const bool at_type = resume ? pref == s->res_bit
+                                    : (s->wrap == 0 ? pref == 0 : hdr_done && pref == 8ull * hdr_len);
         std::vector<uint8_t> o;
         InflateTry t{};
         InflateIndex ixo;
@@ -4331,7 +4377,8 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             // start) or at the end of the next block
             const uint32_t mode = hdr_stop ? 1u
                                   : !block ? 0u
-                                           : ((!resume && s->wrap && !hdr_done) ? 1u : 2u) | (resume && s->itype ? 4u : 0u);
+                                           : ((!resume && s->wrap && !hdr_done) ? 1u : 2u) | (resume && s->itype ? 4u : 0u) |
+                                                 (trees && at_type ? 8u : 0u);
             if (!rc) rc = inflate_try_locked(*L.c, s->in.data(), s->in.size(), resume,
                                              resume ? s->res_bit - 8ull * s->in_base : 0, s->hist.data(), hl,
                                              hl + s->cap, s->wrap, s->wbits, o, t, mode,
@@ -4343,6 +4390,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             const bool in_end_stop = t.stop == kIInEnd;
             s->isyncpt = in_end_stop && ((t.zstate >> 34) & 1u);
             s->imark = in_end_stop ? t.zmark : -65536;
+            s->iheld_end = in_end_stop ? (uint32_t)t.zstate : 0;
         }
         if (t.stop == kIFull) {                                  // grow the output and decode again
             if (s->cap >= (size_t(1) << 31)) return Z_MEM_ERROR;
@@ -4350,15 +4398,15 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             continue;
         }
         const uint64_t obase = resume ? s->res_put - hl : 0;     // absolute output byte of o[0]
-        keep_index(s, ixo, obase, hl, t.stop != kIFull);
-        auto append_new = [&](uint64_t upto) {                   // decoded bytes beyond those kept
-            const uint64_t have = s->ideliv + (s->out.size() - s->out_pos);
-            if (s->out_pos) {
-                s->out.erase(s->out.begin(), s->out.begin() + (std::ptrdiff_t)s->out_pos);
-                s->out_pos = 0;
+        keep_index(s, ixo, t, obase, hl, t.stop != kIFull);
+        auto append_new = [&](uint64_t upto) {                   // s->out from out_at: o's bytes replace those it covers
+            if (obase <= s->out_at) {
+                s->out.assign(o.begin() + (std::ptrdiff_t)(s->out_at - obase), o.begin() + (std::ptrdiff_t)(upto - obase));
+            } else {
+                s->out.resize((size_t)(obase - s->out_at));
+                s->out.insert(s->out.end(), o.begin(), o.begin() + (std::ptrdiff_t)(upto - obase));
             }
-            if (upto > have) s->out.insert(s->out.end(), o.begin() + (std::ptrdiff_t)(have - obase),
-                                           o.begin() + (std::ptrdiff_t)(upto - obase));
+            s->out_pos = (size_t)(s->ideliv - s->out_at);
         };
         const uint64_t put_abs = obase + t.put;
         if (t.stop == kIBlock && hdr_stop) {                     // the header read: resume raw after it
@@ -4407,6 +4455,23 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             const bool last = (t.zstate >> 32) & 1u;
             s->itail = last;                                     // only the trailer is left
             s->idt = (int)((8 - (bb & 7)) & 7) + (last ? 64 : 0) + 128;
+            s->iheld_end = (uint32_t)((8 - (bb & 7)) & 7);
+            return Z_OK;
+        }
+        if (t.stop == kITrees) {
+            // inflate(Z_TREES) after a block header: the header read (up to its
+            // byte), no output; the decode resumes at the block's start, which
+            // the reference has read past (the next Z_TREES / Z_BLOCK call runs
+            // to the block's end), data_type + 256 (inflate.c:1267-1270)
+            append_new(put_abs);
+            const uint64_t hb = t.blk_bit + 8ull * (resume ? s->in_base : 0);
+            const uint64_t used_abs = (hb + 7) >> 3;              // the input after it goes back (inflate_body)
+            s->in.resize(s->in.size() - (size_t)std::min<uint64_t>(in_end - used_abs, took));
+            s->tried = 0;
+            s->itype = false;
+            const bool last = (t.zstate >> 32) & 1u;
+            s->iheld_end = (uint32_t)(8 * used_abs - hb);
+            s->idt = (int)s->iheld_end + (last ? 64 : 0) + 256;
             return Z_OK;
         }
         if (!resume && t.stop == kIDict) {
@@ -4493,12 +4558,8 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
         if (!resume) s->igz = (s->wrap & 2) && s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b;
         if (block)                                               // where the input ran out (inflate.c:1267-1269)
             s->idt = (int)(t.zstate & 0xffffffffu) + ((t.zstate >> 32) & 1u ? 64 : 0) + ((t.zstate >> 33) & 1u ? 128 : 0);
-        // the resume point moves to the last block boundary at or before the
-        // output this call hands out: the reference may stop reading before
-        // later ones (inflate_body's accounting), and a caller that hands other
-        // bytes back decodes again from there
-        const uint64_t xlim = s->ideliv + std::min<uint64_t>(strm->avail_out, s->out.size() - s->out_pos);
-        advance_resume(s, o, obase, ixo, t, xlim);
+        // the resume point moves after the output is handed out (inflate_body):
+        // to the last block boundary the reference has passed
         return Z_OK;
     }
 }
@@ -4577,26 +4638,32 @@ bool inflate_header_seen(const internal_state *s) {
 // (InflateIndex); ~0 when X lies outside it.  dt: the data_type inflate.c
 // reports there (the bits it holds, + 64 in the last block; mode LIT / MATCH /
 // COPY).
-static uint64_t stall_from_index(const internal_state *s, uint64_t X, int *dt = nullptr) {
-    const std::vector<uint64_t> &e = s->ix;
-    if (X < s->ix_o0) return ~0ull;
+static uint64_t stall_in(const std::vector<uint64_t> &e, uint64_t ibase, uint64_t obase, uint64_t o0, uint64_t X,
+                         int *dt, uint32_t *held) {
+    if (X < o0) return ~0ull;
     size_t lo = 0, hi = e.size() / 2;                           // the first symbol whose output ends past X
     while (lo < hi) {
         const size_t m = (lo + hi) / 2;
-        if ((uint32_t)e[2 * m] + s->ix_obase > X) hi = m;
+        if ((uint32_t)e[2 * m] + obase > X) hi = m;
         else lo = m + 1;
     }
     if (2 * lo == e.size()) return ~0ull;
     const uint64_t a = e[2 * lo], v = e[2 * lo + 1];
     const int last = (a >> 33) & 1u ? 64 : 0;
     if ((a >> 32) & 1u) {                                       // a stored run: the bytes copied before X
-        const uint64_t start = lo ? (uint32_t)e[2 * lo - 2] + s->ix_obase : s->ix_o0;
+        const uint64_t start = lo ? (uint32_t)e[2 * lo - 2] + obase : o0;
         if (dt) *dt = last;
-        return s->ix_ibase + v + (X - start);
+        if (held) *held = 0;
+        return ibase + v + (X - start);
     }
     const uint64_t c = (v + 7) >> 3;
     if (dt) *dt = (int)(8 * c - v) + last;
-    return s->ix_ibase + c;
+    if (held) *held = (uint32_t)(8 * c - v);
+    return ibase + c;
+}
+static uint64_t stall_from_index(const internal_state *s, uint64_t X, int *dt = nullptr, uint32_t *held = nullptr) {
+    const uint64_t c = stall_in(s->ix, s->ix_ibase, s->ix_obase, s->ix_o0, X, dt, held);
+    return c != ~0ull ? c : stall_in(s->ix2, s->ix2_ibase, s->ix2_obase, s->ix2_o0, X, dt, held);
 }
 
 // the symbol index rebuilt from the resume point (at or before X) to 4 MiB of
@@ -4607,6 +4674,7 @@ static int refresh_index(internal_state *s, uint64_t X) {
     const size_t hl = resume ? s->hist.size() : 0;
     const uint64_t from = resume ? s->res_put : 0;
     const uint64_t cap = hl + std::min<uint64_t>(X - from + (4u << 20), 1ull << 31);
+    if (from > X) return Z_OK;                                  // a Z_BLOCK stop's resume point: past X
     std::vector<uint8_t> o;
     InflateTry t{};
     InflateIndex ixo;
@@ -4619,9 +4687,7 @@ static int refresh_index(internal_state *s, uint64_t X) {
                                          s->wrap, s->wbits, o, t, 0, s->iback_win ? 1u << s->wbits : 0u, &ixo);
     }
     if (rc) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : rc;
-    const uint64_t obase = from - hl;
-    keep_index(s, ixo, obase, hl, t.stop != kIFull);
-    if (!s->finished) advance_resume(s, o, obase, ixo, t, X);
+    keep_index(s, ixo, t, from - hl, hl, t.stop != kIFull);
     return Z_OK;
 }
 
@@ -4629,15 +4695,19 @@ static int inflate_body(z_streamp strm, int flush) {
     if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
     if (!strm->next_out || (strm->avail_in && !strm->next_in)) return Z_STREAM_ERROR;   // inflate.c:610-612
-    if (flush == 6 /* Z_TREES */) return Z_STREAM_ERROR;                               // documented gap
     if (s->need_dict) return Z_NEED_DICT;                      // inflate.c DICT: until the dictionary is set
-    const bool block = flush == Z_BLOCK;
+    // Z_TREES: Z_BLOCK's stops and one after each block header (inflate.c)
+    const bool trees = flush == Z_TREES;
+    const bool block = flush == Z_BLOCK || trees;
     const Bytef *const next0 = strm->next_in;
     const uInt avail0 = strm->avail_in;
     const uLong total0 = strm->total_in;
     // Z_BLOCK: while the block the last call stopped at is still being handed
     // out, the reference reads no more input
-    const bool taking = !(s->finished || (block && s->out_pos < s->out.size()));
+    // Z_BLOCK after a stop at a block's end whose output is still being handed
+    // out (the resume point past it): the reference reads no more input
+    const bool taking = !(s->finished || (block && s->res_put > s->ideliv));
+    const uint64_t pref0 = 8 * s->cons - s->iheld;             // the reference's bit position
     s->acct_done = false;
     size_t took = 0;                 // bytes new to the engine
     bool redo = false;               // decode again: the bytes handed back came back different
@@ -4656,10 +4726,10 @@ static int inflate_body(z_streamp strm, int flush) {
                                std::memcmp(next0, s->in.data() + (s->cons - s->in_base), (size_t)held) == 0);
             if (!same && s->res_put <= s->ideliv && s->cons >= s->in_base) {
                 s->in.resize((size_t)(s->cons - s->in_base));
-                s->out.clear();
-                s->out_pos = 0;
+                s->out.resize(s->out_pos);                      // what was handed out stays (the window)
                 s->tried = 0;
                 s->ix.clear();
+                s->ix2.clear();
                 s->ix_all = false;
                 held = 0;
                 redo = true;
@@ -4697,9 +4767,12 @@ static int inflate_body(z_streamp strm, int flush) {
     // byte its input decodes to so far, as inflate() does (inflate.c:622-1221).
     // Each attempt resumes at a block boundary (inflate_attempt).
     const uint64_t in_end = s->in_base + s->in.size();
-    if (!s->finished && (took || redo || s->itail || (flush == Z_FINISH && s->tried != in_end))) {
+    // (the trailer after a Z_BLOCK stop at the last block is read once its
+    // output is all handed out)
+    const bool tail_due = s->itail && s->out_pos >= s->out.size();
+    if (!s->finished && (took || redo || tail_due || (flush == Z_FINISH && s->tried != in_end))) {
         if (block) s->idt = 0;
-        if (int rc = inflate_attempt(strm, s, taking ? avail0 : 0, block)) return rc;
+        if (int rc = inflate_attempt(strm, s, taking ? avail0 : 0, block, trees)) return rc;
         if (s->need_dict) {
             s->cons = strm->total_in + s->iadj;
             s->held_at = strm->next_in;
@@ -4707,9 +4780,17 @@ static int inflate_body(z_streamp strm, int flush) {
         }
     }
     if (block) strm->data_type = s->idt;
+    // Z_BLOCK with output of an earlier call still to hand out: the reference
+    // decodes on only to the end of the block it is in (inflate.c TYPE), the
+    // first boundary past the output handed out
+    uint64_t cap_put = ~0ull, cap_bit = 0;
+    if (block && s->out_pos < s->out.size())
+        for (size_t k = 0; k + 1 < s->bx.size(); k += 2)
+            if (s->bx[k] > pref0 && s->bx[k + 1] >= s->ideliv) { cap_bit = s->bx[k]; cap_put = s->bx[k + 1]; break; }
     size_t give = 0;
     if (s->out_pos < s->out.size()) {
         give = std::min<size_t>(strm->avail_out, s->out.size() - s->out_pos);
+        if (cap_put != ~0ull) give = (size_t)std::min<uint64_t>(give, cap_put - s->ideliv);
         std::memcpy(strm->next_out, s->out.data() + s->out_pos, give);
         s->out_pos += give;
         s->ideliv += give;
@@ -4725,12 +4806,19 @@ static int inflate_body(z_streamp strm, int flush) {
         s->cons = strm->total_in + s->iadj;
     } else {
         uint64_t C;
-        if (pending) {
+        s->iheld = s->iheld_end;
+        if (s->ideliv == cap_put) {
+            // at the block's end, mode TYPE: the bits after its end-of-block code held
+            C = (cap_bit + 7) >> 3;
+            s->iheld = (uint32_t)(8 * C - cap_bit);
+            strm->data_type = (int)s->iheld + 128 + (cap_bit == s->bx_last ? 64 : 0);
+            if (cap_bit == s->bx_last && !s->finished) s->itail = true;   // the trailer next
+        } else if (pending) {
             int dt = -1;
-            C = stall_from_index(s, s->ideliv, &dt);
+            C = stall_from_index(s, s->ideliv, &dt, &s->iheld);
             if (C == ~0ull) {
                 if (int rc = refresh_index(s, s->ideliv)) return rc;
-                C = stall_from_index(s, s->ideliv, &dt);
+                C = stall_from_index(s, s->ideliv, &dt, &s->iheld);
             }
             if (C == ~0ull) C = s->finished ? s->fin_used : s->in_base + s->in.size();
             if (block && dt >= 0) strm->data_type = dt;        // stopped for room, not at a block boundary
@@ -4745,10 +4833,13 @@ static int inflate_body(z_streamp strm, int flush) {
         if (s->finished && !pending) {
             s->in.clear();
             s->in.shrink_to_fit();
+        } else if (!s->finished) {
+            // the resume point to the last boundary the reference has passed
+            advance_resume(s, s->ideliv, 8 * s->cons - s->iheld, s->itail);
         }
     }
     s->held_at = strm->next_in;
-    if (s->finished && !pending) return s->result;
+    if (s->finished && !pending && s->ideliv != cap_put) return s->result;
     // inflate.c:1261-1262: no progress, or Z_FINISH short of the stream end
     if ((strm->next_in == next0 && give == 0) || flush == Z_FINISH) return Z_BUF_ERROR;
     return Z_OK;
@@ -4897,12 +4988,22 @@ int inflateGetHeader(z_streamp strm, gz_headerp head) {
 int inflateSync(z_streamp strm) {
     if (!strm || !strm->state || !strm->state->inflating) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
-    if (strm->avail_in == 0) return Z_BUF_ERROR;
-    if (!s->isyncing) {
-        s->isyncing = true;
-        s->isync_have = 0;
-    }
+    if (strm->avail_in == 0 && (s->isyncing || s->iheld < 8)) return Z_BUF_ERROR;   // inflate.c:1385
     uint32_t got = s->isync_have;
+    if (!s->isyncing) {
+        // inflate.c:1388-1398: the whole bytes in the bit buffer (the last input
+        // consumed, after its oldest bits & 7 are dropped) are searched first
+        s->isyncing = true;
+        got = 0;
+        const uint64_t k = s->iheld / 8;
+        if (k && s->cons >= s->in_base + k && s->cons - s->in_base <= s->in.size())
+            for (const uint8_t *b = s->in.data() + (s->cons - k - s->in_base), *e = b + k; b < e && got < 4; b++) {
+                if (*b == (got < 2 ? 0 : 0xff)) got++;
+                else if (*b) got = 0;
+                else got = 4 - got;
+            }
+        s->iheld = 0;
+    }
     uInt len = 0;
     while (len < strm->avail_in && got < 4) {                   // syncsearch (inflate.c:1352-1373)
         const uint8_t c = strm->next_in[len];
@@ -4928,6 +5029,9 @@ int inflateSync(z_streamp strm) {
         return Z_MEM_ERROR;
     }
     s->out_pos = 0;
+    s->out_at = s->ideliv;
+    s->bx.clear();
+    s->ix2.clear();
     s->in_base = strm->total_in + s->iadj;                     // absolute input position
     s->cons = s->in_base;
     s->held_at = strm->next_in;

@@ -2567,6 +2567,11 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     // s->insert: strings a flush left unhashed (a resumed job starts right
     // after a flush at its window offset + start; none at a block cut)
     P pend = (kEv && job.cut) ? 0 : p < kMinMatch - 1 ? p : kMinMatch - 1;
+    // right after a deflate_huff / deflate_rle stretch (a SkipSpec range ending
+    // at the start): their flush leaves s->insert = 0 (deflate.c:2108, 2144)
+    if (kEv)
+        for (uint32_t k = 0; k < job.sk.n; k++)
+            if ((P)job.sk.b[k] == p) pend = 0;
     // a streaming job keeps head[] as it stands at its last cut (the block or
     // marker record snap[hsize]): a later job resumes there
     auto snapshot = [&]() {
@@ -4648,15 +4653,10 @@ __global__ __launch_bounds__(kM2Threads) void k_match2(DeflateJob job, int want_
 // ------------------------------------------------------------------------
 constexpr int kPSBits = 4 * kSortBlock / 32;        // bitmap words: blocks b-2 .. b+1
 
-// kEv: a streaming job whose events are Z_NO_FLUSH stops only, parsed from
-// its start (zgpu_api.cpp deflate_part's srt jobs): fill_window runs up to
-// each call's input end, the parse stops as deflate_fast's need_more does
-// (deflate.c:1841-1844), every block cut writes its record (srec), and the
-// bitmap goes to job.ins_bits for k_srt_chains.
 // kG (batches of many buffers): the sorted entries and the bytes are read
 // from global memory (L2) instead of LDS rings, so that a wave needs only its
 // 8 KiB bitmap and 20 parses share a CU instead of one.
-template <typename P, bool kEv = false, bool kG = false>
+template <typename P, bool kG = false>
 __global__ __launch_bounds__(64) void k_parse_srt(DeflateJob job) {
     __shared__ __attribute__((aligned(16))) uint16_t Sr[kG ? 8 : kM2Ring];
     __shared__ __attribute__((aligned(16))) uint8_t Bw[kG ? 16 : kM2Ring + kM2Pad];
@@ -4679,9 +4679,7 @@ __global__ __launch_bounds__(64) void k_parse_srt(DeflateJob job) {
     po.block_start = 0; po.S = 0; po.E = 0;
     po.lead = true;
     po.vaddr = true;
-    if (kEv) po.srec = job.srec;
     const P max_dist = (P)wp.max_dist;
-    uint32_t *gbits = kEv ? job.ins_bits + job.ws_off[bi] / 32 : nullptr;   // ws_off % 64 == 0
     auto mcount = [&](P b) -> int {
         const P r = n - 2 - b * kSortBlock;
         return r <= 0 ? 0 : (r < kSortBlock ? (int)r : kSortBlock);
@@ -4728,8 +4726,6 @@ __global__ __launch_bounds__(64) void k_parse_srt(DeflateJob job) {
     // block b into ring slot 2 (entries as ring offsets), its bytes + pad, and
     // its bitmap slot b+1 (slot 3) cleared; slide first unless b == 0
     auto load_block = [&](P b) {
-        if (kEv && b >= 3)                              // block b-3's bits leave the ring: keep them
-            for (int c = lane; c < kSortBlock / 32; c += 64) gbits[(b - 3) * (kSortBlock / 32) + c] = Bi[c];
         gbase = (b - 2) * (P)kSortBlock;
         if (kG) {                                       // only the bitmap lives in LDS
             if (b > 0)
@@ -4789,23 +4785,10 @@ __global__ __launch_bounds__(64) void k_parse_srt(DeflateJob job) {
     const P nblk = (n + kSortBlock - 1) / kSortBlock;
     P p = 0;
     uint32_t match_length = kMinMatch - 1;
-    FlushEv fe = flush_ev(job);
-    P lim = kEv ? (P)fe.limit(n) : n;                   // input deflate() has been given
+    const P lim = n;
     while (p < n) {
         if (po.E - p < kMinLookahead) {
             po.fill(p, lim);
-            if (kEv) {
-                // a Z_NO_FLUSH call's input is used up: need_more (deflate.c:1841-1844)
-                bool stop = false;
-                while (fe.stop_at(po.E, lim) && po.E - p < kMinLookahead) {
-                    if (lane == 0 && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
-                    fe.i++;
-                    if (fe.i == fe.n && job.open_end) { stop = true; break; }
-                    lim = (P)fe.limit(n);
-                    po.fill(p, lim);
-                }
-                if (stop || po.E == p) break;
-            }
         }
         while (p >= (blk + 1) * kSortBlock && blk + 1 < nblk) load_block(++blk);
         if (p >= rb + 64) {
@@ -4933,76 +4916,10 @@ __global__ __launch_bounds__(64) void k_parse_srt(DeflateJob job) {
             bflush = po.tally(bw(vp));
             p++;
         }
-        if (bflush) {
-            po.flush(p, false);
-            if (kEv && lane == 0 && job.snap) job.snap[0] = po.nblk - 1;    // the last cut's record (k_srt_chains)
-        }
+        if (bflush) po.flush(p, false);
     }
-    if (!kEv || !job.open_end) po.flush(p, true);
+    po.flush(p, true);
     if (lane == 0) job.nblocks[bi] = po.nblk;
-    if (kEv) {
-        for (int sl = 0; sl < 4; sl++) {                // the ring's blocks blk-2 .. blk+1
-            const P b = blk - 2 + sl;
-            if (b < 0 || b * kSortBlock >= n + 64) continue;
-            for (int c = lane; c < kSortBlock / 32; c += 64) gbits[b * (kSortBlock / 32) + c] = Bi[sl * (kSortBlock / 32) + c];
-        }
-        if (lane == 0 && job.flush_out) job.flush_out[4] = (uint64_t)(kMinMatch - 1) | (uint64_t)match_length << 16;
-    }
-}
-
-// k_srt_chains — after a streaming k_parse_srt job: head[] and prev[] as
-// deflate_fast leaves them at the job's last block cut x (record snap[0]),
-// for a later job resuming there on k_parse_fast: every inserted position q in
-// [x - 65536, x), in order, takes prev[q] = the distance to the last inserted
-// position with its hash (0: none within 32767) and becomes head[hash]
-// (INSERT_STRING, deflate.c:160-163).  Only chains reaching back from x
-// matter to the resumed parse (its limit is above x - 32768), so older
-// positions of the window keep prev 0.  One wave; head[] in LDS.
-__global__ __launch_bounds__(64) void k_srt_chains(DeflateJob job) {
-    __shared__ uint32_t hd[32768];
-    const int lane = threadIdx.x;
-    const uint32_t g = job.first;
-    const int64_t n = (int64_t)job.src_len[g];
-    const uint8_t *in = job.src + job.src_off[g];
-    const WinP wp = job_win(job);
-    const uint32_t hsize = wp.mask + 1;
-    const uint32_t k = job.snap[0];
-    if (k == 0xffffffffu || job.nblocks[0] == 0) {       // no cut: nothing resumes from this job
-        if (lane == 0) job.snap[hsize] = 0xffffffffu;
-        return;
-    }
-    const int64_t x = (int64_t)(job.srec[4ull * k + 2] & 0xffffffffu);
-    const int64_t S = (int64_t)(job.srec[4ull * k + 2] >> 32);
-    const uint32_t *bits = job.ins_bits + job.ws_off[0] / 32;
-    uint16_t *prev = job.link + job.ws_off[0];
-    for (uint32_t h = lane; h < hsize; h += 64) hd[h] = 0;
-    const int64_t a = x > 65536 ? x - 65536 : 0;
-    for (int64_t q = S + lane; q < a; q += 64) prev[q] = 0;
-    __syncthreads();
-    for (int64_t c = a & ~(int64_t)63; c < x; c += 64) {
-        const int64_t q = c + lane;
-        const bool ins = q >= a && q < x && q + 2 < n && ((bits[q >> 5] >> (q & 31)) & 1u);
-        const uint32_t h = ins ? hashp(in[q], in[q + 1], in[q + 2], wp) : 0xffffffffu;
-        int64_t pq = ins ? (int64_t)hd[h] : 0;        // head before this chunk (0: none)
-        bool last = ins;
-        for (int j = 0; j < 64; j++) {                // equal hashes inside the chunk: in order
-            const uint32_t hj = (uint32_t)__builtin_amdgcn_readlane((int)h, j);
-            if (ins && hj == h) {
-                if (j < lane) pq = c + j;
-                if (j > lane) last = false;
-            }
-        }
-        if (ins) {
-            const int64_t d = q - pq;
-            prev[q] = (pq != 0 && d <= 32767) ? (uint16_t)d : (uint16_t)0;
-            if (last) hd[h] = (uint32_t)q;
-        } else if (q >= a && q < x) {
-            prev[q] = 0;                               // no chain reaches it
-        }
-        __syncthreads();
-    }
-    for (uint32_t h = lane; h < hsize; h += 64) job.snap[h] = hd[h];
-    if (lane == 0) job.snap[hsize] = k;
 }
 
 int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipStream_t st) {
@@ -5104,10 +5021,7 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         }
         break;
     case 16:                                                // levels 1..3 from the sorted runs
-        if (job.nfl) {                                      // a streaming job of stops (one buffer)
-            hipLaunchKernelGGL((k_parse_srt<int64_t, true>), grid, dim3(64), 0, st, job);
-            if (job.snap) hipLaunchKernelGGL(k_srt_chains, dim3(1), dim3(64), 0, st, job);
-        } else {
+        {
             // few buffers: rings in LDS (one parse per CU); many: the rings'
             // data from L2 and 20 parses per CU (ZGPU_SRT_LDS_MAX: the limit)
             static const uint32_t lds_max = [] {
@@ -5115,9 +5029,9 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
                 return e ? (uint32_t)std::atoi(e) : 512u;
             }();
             const bool gl = job.count > lds_max;
-            if (job.pos31 && gl) hipLaunchKernelGGL((k_parse_srt<int32_t, false, true>), grid, dim3(64), 0, st, job);
+            if (job.pos31 && gl) hipLaunchKernelGGL((k_parse_srt<int32_t, true>), grid, dim3(64), 0, st, job);
             else if (job.pos31) hipLaunchKernelGGL(k_parse_srt<int32_t>, grid, dim3(64), 0, st, job);
-            else if (gl) hipLaunchKernelGGL((k_parse_srt<int64_t, false, true>), grid, dim3(64), 0, st, job);
+            else if (gl) hipLaunchKernelGGL((k_parse_srt<int64_t, true>), grid, dim3(64), 0, st, job);
             else hipLaunchKernelGGL(k_parse_srt<int64_t>, grid, dim3(64), 0, st, job);
         }
         break;

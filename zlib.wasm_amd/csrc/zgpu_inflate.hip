@@ -422,6 +422,13 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
             const uint32_t len = (uint32_t)r.hold & 0xffffu, nlen = ((uint32_t)r.hold >> 16) & 0xffffu;
             if (len != (nlen ^ 0xffffu)) { stop = kIData; used = (bitpos(r) >> 3) + 4; goto done; }
             dropb(r, 32);
+            if (job.stop_mode & 8u) {                                // Z_TREES: mode COPY_, before the bytes
+                blk_bit = bitpos(r);
+                blk_put = put;
+                stop = kITrees;
+                used = blk_bit >> 3;
+                goto done;
+            }
             const uint32_t bp = (uint32_t)(bitpos(r) >> 3);
             flush_obuf(put);
             uint32_t cnt = len;
@@ -524,6 +531,13 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
                 if (job.zcodes)
                     zcodes = codes_used(S.lens, (int)nlen, 9, S.cu, lane) + codes_used(S.lens + nlen, (int)ndist, 6, S.cu, lane);
             }
+            if (job.stop_mode & 8u) {                                // Z_TREES: mode LEN_, before the first code
+                blk_bit = bitpos(r);
+                blk_put = put;
+                stop = kITrees;
+                used = ceil_used();
+                goto done;
+            }
             // ---------------- LEN .. MATCH / LIT ----------------
             for (;;) {
                 refill(S, r, in, n, lane);
@@ -577,16 +591,16 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
             used = (blk_bit + 7) >> 3;
             goto done;
         }
-        if (last) break;
-        blk_bit = bitpos(r);                         // a block boundary: resumable here
-        blk_put = put;
-        if (kIdx) {
+        if (kIdx) {                                  // the index: every block's end, the last one flagged
             if (lane == 0 && nbk < job.bcap) {
-                job.bidx[2 * (uint64_t)nbk] = blk_bit;
-                job.bidx[2 * (uint64_t)nbk + 1] = blk_put;
+                job.bidx[2 * (uint64_t)nbk] = bitpos(r) | (uint64_t)last << 63;
+                job.bidx[2 * (uint64_t)nbk + 1] = put;
             }
             nbk++;
         }
+        if (last) break;
+        blk_bit = bitpos(r);                         // a block boundary: resumable here
+        blk_put = put;
     }
     ztype = false;                                   // TYPEDO -> CHECK
 

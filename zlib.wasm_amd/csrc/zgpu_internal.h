@@ -296,11 +296,6 @@ struct DeflateJob {
     uint16_t *srt;
     uint16_t *boff;
     uint4 *work;
-    // k_parse_srt of a streaming job (levels 1..3, Z_NO_FLUSH stops only):
-    // the inserted-position bitmap it leaves (1 bit per position), from which
-    // k_srt_chains rebuilds head[] and prev[] at the last cut (job.snap,
-    // job.link) for the job that resumes there on k_parse_fast
-    uint32_t *ins_bits;
 };
 // k_bsort's block (positions) and the stride of its per-block hash table
 constexpr int kSortBlock = 16384;
@@ -324,7 +319,7 @@ __host__ __device__ inline WinP win_params(int wbits, int hbits) {
 // ---- inflate ----
 // where k_inflate_decode stopped (zo_inflate_run's codes)
 // (kIBlock: inflate(Z_BLOCK)'s stop at a block boundary, InflateJob::stop_mode)
-enum InflateStop : uint32_t { kIEnd = 0, kIData = 1, kIDict = 2, kIFull = 3, kIInEnd = 4, kIBlock = 5 };
+enum InflateStop : uint32_t { kIEnd = 0, kIData = 1, kIDict = 2, kIFull = 3, kIInEnd = 4, kIBlock = 5, kITrees = 6 };
 
 struct InflateRec {          // per stream, written by k_inflate_decode
     uint64_t put;            // output bytes produced
@@ -369,7 +364,9 @@ struct InflateJob {
     // inflate(Z_BLOCK) (inflate.c TYPE: "if (flush == Z_BLOCK) goto inf_leave"):
     // bit 0 stop right after a zlib / gzip header, bit 1 at the end of the
     // first block that is not the last; the stop (kIBlock) is the boundary in
-    // blk_out
+    // blk_out.  bit 3 (inflate(Z_TREES), inflate.c STORED / TABLE .. LEN_):
+    // stop after the first block header, before its first code (kITrees, the
+    // header's end in blk_out)
     uint32_t stop_mode;
     // the state inflate.c would report in strm->data_type where the decode
     // stopped (or null): input bits it would hold (inbits - the bit after the
@@ -389,8 +386,9 @@ struct InflateJob {
     // the streaming inflate()'s consumption index (one-stream jobs; null: off): per symbol that
     // writes output, eidx[2k] = its output end (low 32 bits) | stored run << 32 | BFINAL of its
     // block << 33, eidx[2k + 1] = the input bit position once its codes are read (a stored run:
-    // its first input byte).  bidx[2k], [2k + 1] = bit and output position of each block
-    // boundary.  icnt[0], [1] = entries / boundaries met (may exceed ecap / bcap)
+    // its first input byte).  bidx[2k], [2k + 1] = bit and output position of each block's
+    // end (the last block's: bit | 1 << 63).  icnt[0], [1] = entries / ends met (may exceed
+    // ecap / bcap)
     uint64_t *eidx, *bidx;
     uint32_t *icnt;
     uint32_t ecap, bcap;
