@@ -500,7 +500,11 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     static const int fsrt_env0 = [] { const char *e = std::getenv("ZGPU_FAST_SRT"); return e ? std::atoi(e) : -1; }();
     uint64_t total_in = 0;
     for (uint32_t i = 0; i < count; i++) total_in += lens[i];
-    const bool fsrt_ok = level >= 1 && level <= 3 && strategy != 2 && strategy != 3 && !fs && hbits <= 15;
+    // (k_parse_srt takes a search's chain whole: good_match above prev_length 2, as
+    // configuration_table's L1-3 rows have it, and at most 64 strings inserted per match)
+    const LevelCfg fcfg = tune ? *tune : kLevelCfg[level];
+    const bool fsrt_ok = level >= 1 && level <= 3 && strategy != 2 && strategy != 3 && !fs && hbits <= 15 &&
+                         fcfg.good > kMinMatch - 1 && fcfg.lazy <= 64;
     const bool fsrt_want = fsrt_ok && (fsrt_env0 == 1 || (fsrt_env0 == -1 && level >= 2 && count <= 16 &&
                                                            total_in <= (256ull << 20)));
     const uint64_t budget = fsrt_want ? std::min<uint64_t>(c.inflight, 4ull << 30)
@@ -2425,6 +2429,7 @@ struct internal_state {
     std::vector<uint64_t> ix, ix2;                       // ix2: an earlier index that starts lower
     uint64_t ix_ibase = 0, ix_obase = 0, ix_o0 = 0, ix2_ibase = 0, ix2_obase = 0, ix2_o0 = 0;
     bool ix_all = false, acct_done = false;
+    bool hdr_stop_now = false;                           // this call's decode stopped after a block header (Z_TREES)
     std::vector<uint64_t> bx;                            // the last decode's block boundaries (absolute bit, output)
     uint64_t bx_last = ~0ull;                            // the bit of the one that ends the last block (a Z_BLOCK stop)
     uint64_t out_at = 0;                                 // absolute output of out[0] (out_pos = ideliv - out_at)
@@ -4225,7 +4230,7 @@ void keep_index(internal_state *s, InflateIndex &ix, const InflateTry &t, uint64
         add(b, ix.b[k + 1], false);
         if (ix.b[k] >> 63) s->bx_last = b + ib;
     }
-    if (t.stop != kITrees) add(t.blk_bit, t.blk_put, false);     // (a Z_TREES stop's is a header's end)
+    add(t.blk_bit, t.blk_put, false);
     if (t.stop == kIBlock && ((t.zstate >> 32) & 1u)) s->bx_last = t.blk_bit + ib;
 }
 
@@ -4398,7 +4403,7 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             continue;
         }
         const uint64_t obase = resume ? s->res_put - hl : 0;     // absolute output byte of o[0]
-        keep_index(s, ixo, t, obase, hl, t.stop != kIFull);
+        if (t.stop != kITrees) keep_index(s, ixo, t, obase, hl, t.stop != kIFull);   // (a header stop adds nothing)
         auto append_new = [&](uint64_t upto) {                   // s->out from out_at: o's bytes replace those it covers
             if (obase <= s->out_at) {
                 s->out.assign(o.begin() + (std::ptrdiff_t)(s->out_at - obase), o.begin() + (std::ptrdiff_t)(upto - obase));
@@ -4462,13 +4467,14 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             // inflate(Z_TREES) after a block header: the header read (up to its
             // byte), no output; the decode resumes at the block's start, which
             // the reference has read past (the next Z_TREES / Z_BLOCK call runs
-            // to the block's end), data_type + 256 (inflate.c:1267-1270)
-            append_new(put_abs);
+            // to the block's end), data_type + 256 (inflate.c:1267-1270); the
+            // output an earlier decode left beyond stays
             const uint64_t hb = t.blk_bit + 8ull * (resume ? s->in_base : 0);
             const uint64_t used_abs = (hb + 7) >> 3;              // the input after it goes back (inflate_body)
             s->in.resize(s->in.size() - (size_t)std::min<uint64_t>(in_end - used_abs, took));
             s->tried = 0;
             s->itype = false;
+            s->hdr_stop_now = true;
             const bool last = (t.zstate >> 32) & 1u;
             s->iheld_end = (uint32_t)(8 * used_abs - hb);
             s->idt = (int)s->iheld_end + (last ? 64 : 0) + 256;
@@ -4556,8 +4562,9 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
         append_new(put_abs);
         s->tried = in_end;
         if (!resume) s->igz = (s->wrap & 2) && s->in.size() >= 2 && s->in[0] == 0x1f && s->in[1] == 0x8b;
-        if (block)                                               // where the input ran out (inflate.c:1267-1269)
-            s->idt = (int)(t.zstate & 0xffffffffu) + ((t.zstate >> 32) & 1u ? 64 : 0) + ((t.zstate >> 33) & 1u ? 128 : 0);
+        // where the input ran out (inflate.c:1267-1269): what a later Z_BLOCK
+        // call reports once the output is all handed out
+        s->idt = (int)(t.zstate & 0xffffffffu) + ((t.zstate >> 32) & 1u ? 64 : 0) + ((t.zstate >> 33) & 1u ? 128 : 0);
         // the resume point moves after the output is handed out (inflate_body):
         // to the last block boundary the reference has passed
         return Z_OK;
@@ -4709,6 +4716,7 @@ static int inflate_body(z_streamp strm, int flush) {
     const bool taking = !(s->finished || (block && s->res_put > s->ideliv));
     const uint64_t pref0 = 8 * s->cons - s->iheld;             // the reference's bit position
     s->acct_done = false;
+    s->hdr_stop_now = false;
     size_t took = 0;                 // bytes new to the engine
     bool redo = false;               // decode again: the bytes handed back came back different
     if (taking) {
@@ -4770,7 +4778,10 @@ static int inflate_body(z_streamp strm, int flush) {
     // (the trailer after a Z_BLOCK stop at the last block is read once its
     // output is all handed out)
     const bool tail_due = s->itail && s->out_pos >= s->out.size();
-    if (!s->finished && (took || redo || tail_due || (flush == Z_FINISH && s->tried != in_end))) {
+    // Z_TREES with the reference at a block's start: the header stop needs a
+    // decode even when no new input came (the index knows no header ends)
+    const bool trees_due = trees && !s->finished && s->imode == 1 && pref0 == s->res_bit;
+    if (!s->finished && (took || redo || tail_due || trees_due || (flush == Z_FINISH && s->tried != in_end))) {
         if (block) s->idt = 0;
         if (int rc = inflate_attempt(strm, s, taking ? avail0 : 0, block, trees)) return rc;
         if (s->need_dict) {
@@ -4784,11 +4795,11 @@ static int inflate_body(z_streamp strm, int flush) {
     // decodes on only to the end of the block it is in (inflate.c TYPE), the
     // first boundary past the output handed out
     uint64_t cap_put = ~0ull, cap_bit = 0;
-    if (block && s->out_pos < s->out.size())
+    if (block && s->out_pos < s->out.size() && !s->hdr_stop_now)
         for (size_t k = 0; k + 1 < s->bx.size(); k += 2)
             if (s->bx[k] > pref0 && s->bx[k + 1] >= s->ideliv) { cap_bit = s->bx[k]; cap_put = s->bx[k + 1]; break; }
     size_t give = 0;
-    if (s->out_pos < s->out.size()) {
+    if (s->out_pos < s->out.size() && !s->hdr_stop_now) {      // (stopped after a header: no output)
         give = std::min<size_t>(strm->avail_out, s->out.size() - s->out_pos);
         if (cap_put != ~0ull) give = (size_t)std::min<uint64_t>(give, cap_put - s->ideliv);
         std::memcpy(strm->next_out, s->out.data() + s->out_pos, give);
@@ -4801,7 +4812,7 @@ static int inflate_body(z_streamp strm, int flush) {
     // the input this call consumed (inflate.c inf_leave): all of it unless the
     // output space ended first, then up to the reference's stop at the output
     // handed out (stall_from_index); a finished stream's up to its end
-    const bool pending = s->out_pos < s->out.size();
+    const bool pending = s->out_pos < s->out.size() && !s->hdr_stop_now;
     if (s->acct_done) {
         s->cons = strm->total_in + s->iadj;
     } else {
