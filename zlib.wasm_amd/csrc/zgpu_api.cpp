@@ -2430,6 +2430,7 @@ struct internal_state {
     uint64_t ix_ibase = 0, ix_obase = 0, ix_o0 = 0, ix2_ibase = 0, ix2_obase = 0, ix2_o0 = 0;
     bool ix_all = false, acct_done = false;
     bool hdr_stop_now = false;                           // this call's decode stopped after a block header (Z_TREES)
+    bool after_hdr = false;                              // the reference stands after a block header (LEN_ / COPY_)
     std::vector<uint64_t> bx;                            // the last decode's block boundaries (absolute bit, output)
     uint64_t bx_last = ~0ull;                            // the bit of the one that ends the last block (a Z_BLOCK stop)
     uint64_t out_at = 0;                                 // absolute output of out[0] (out_pos = ideliv - out_at)
@@ -4038,7 +4039,7 @@ int inflateReset(z_streamp strm) {
     s->isyncpt = false; s->imark = -65536; s->icodes = 0; s->iprime_n = 0; s->iprime_v = 0;
     s->iadl_on = false; s->iadl = 0;
     s->cons = s->fin_used = 0; s->held_at = nullptr; s->ix.clear(); s->ix2.clear(); s->ix_all = false;
-    s->bx.clear(); s->out_at = 0;
+    s->bx.clear(); s->out_at = 0; s->after_hdr = false;
     s->iheld = s->iheld_end = 0;
     strm->total_in = strm->total_out = 0;
     strm->msg = nullptr;
@@ -4797,7 +4798,12 @@ static int inflate_body(z_streamp strm, int flush) {
     uint64_t cap_put = ~0ull, cap_bit = 0;
     if (block && s->out_pos < s->out.size() && !s->hdr_stop_now)
         for (size_t k = 0; k + 1 < s->bx.size(); k += 2)
-            if (s->bx[k] > pref0 && s->bx[k + 1] >= s->ideliv) { cap_bit = s->bx[k]; cap_put = s->bx[k + 1]; break; }
+            // (past a header stop the block's end may be where the reference stands: an empty stored block)
+            if ((s->bx[k] > pref0 || (s->after_hdr && s->bx[k] == pref0)) && s->bx[k + 1] >= s->ideliv) {
+                cap_bit = s->bx[k];
+                cap_put = s->bx[k + 1];
+                break;
+            }
     size_t give = 0;
     if (s->out_pos < s->out.size() && !s->hdr_stop_now) {      // (stopped after a header: no output)
         give = std::min<size_t>(strm->avail_out, s->out.size() - s->out_pos);
@@ -4848,6 +4854,8 @@ static int inflate_body(z_streamp strm, int flush) {
             // the resume point to the last boundary the reference has passed
             advance_resume(s, s->ideliv, 8 * s->cons - s->iheld, s->itail);
         }
+        s->after_hdr = s->hdr_stop_now ||
+                       (s->after_hdr && give == 0 && s->ideliv != cap_put && 8 * s->cons - s->iheld == pref0);
     }
     s->held_at = strm->next_in;
     if (s->finished && !pending && s->ideliv != cap_put) return s->result;
@@ -5043,6 +5051,7 @@ int inflateSync(z_streamp strm) {
     s->out_at = s->ideliv;
     s->bx.clear();
     s->ix2.clear();
+    s->after_hdr = false;
     s->in_base = strm->total_in + s->iadj;                     // absolute input position
     s->cons = s->in_base;
     s->held_at = strm->next_in;
