@@ -114,7 +114,7 @@ def test_random_deflate_sessions_vs_system_zlib(zg, block):
     assert not bad, bad[:3]
 
 
-def _istream(rng, libz, small_out=False):
+def _istream(rng, libz, small_out=False, flushes=(0, 0, 2, 5)):
     """A stream from system zlib (any level and strategy, flushes inside) and
     a random inflate call sequence over it: input fed in random pieces, calls
     with Z_NO_FLUSH / Z_SYNC_FLUSH / Z_BLOCK, sometimes cut short (a truncated
@@ -142,7 +142,7 @@ def _istream(rng, libz, small_out=False):
         ops.append(["header", rng.choice((0, 4, 64)), rng.choice((0, 8, 256)), rng.choice((0, 8, 256))])
     for _ in range(rng.randint(1, 25)):
         ops.append(["feed", rng.choice((1, 3, 100, 4096, 70000, 1 << 30))])
-        ops.append(["inflate", rng.choice((0, 0, 2, 5)),
+        ops.append(["inflate", rng.choice(flushes),
                     rng.choice((1, 100, 5000, 1 << 16, 1 << 20)) if small_out else 1 << 20])
     ops += [["feed", 1 << 30], ["loop", 0, 1 << 20]]
     return z, ops
@@ -181,6 +181,28 @@ def test_random_inflate_small_output_vs_system_zlib(zg, block):
     bad = []
     for k in range(30):
         z, ops = _istream(rng, libz, small_out=True)
+        rz = run_iops(libz, z, ops)
+        rg = run_iops(L, z, ops)
+        if rz != rg:
+            first = next((i for i, (a, b) in enumerate(zip(rz[0], rg[0])) if a != b), None)
+            bad.append((k, len(z), first, ops[:3], rz[0][first] if first is not None else None,
+                        rg[0][first] if first is not None else None))
+    assert not bad, bad[:3]
+
+
+@pytest.mark.parametrize("block", range(2))
+def test_random_inflate_trees_vs_system_zlib(zg, block):
+    """inflate(Z_TREES) among Z_NO_FLUSH / Z_BLOCK calls, output space down to
+    1 byte: every call's status, avail_in, total_in, total_out and data_type
+    (+ 256 at a block header's end, inflate.c LEN_ / COPY_), the output and
+    the gzip header fields equal the system zlib's."""
+    from zhelpers import run_iops
+    libz = _system_zlib()
+    L = zg.load()
+    rng = random.Random(6161 + block)
+    bad = []
+    for k in range(30):
+        z, ops = _istream(rng, libz, small_out=True, flushes=(0, 5, 6, 6))
         rz = run_iops(libz, z, ops)
         rg = run_iops(L, z, ops)
         if rz != rg:

@@ -64,6 +64,16 @@ for block in (0, 1):
         if nbad < 12:
             nbad += show(f"fuzz{block}.{k}", ops, rz, rg, len(z))
 print("fuzz sessions differing (first 12 shown):", nbad)
+nt = 0
+for block in (0, 1):
+    rng = random.Random(6161 + block)
+    for k in range(30):
+        z, ops = T._istream(rng, libz, small_out=True, flushes=(0, 5, 6, 6))
+        rz = run_iops(libz, z, ops)
+        rg = run_iops(L, z, ops)
+        if nt < 8:
+            nt += show(f"trees{block}.{k}", ops, rz, rg, len(z))
+print("Z_TREES fuzz sessions differing (first 8 shown):", nt)
 g = json.load(open(os.path.join(R, "tests", "golden", "isession_golden.json")))["sessions"]
 nb = 0
 for sess in g:

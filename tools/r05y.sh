@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: PMC FETCH_SIZE / WRITE_SIZE passes (separate runs) of the C4, C3
 # and C5 launch shapes, copied into profiles/ for bench.py's roofline, then
-# the C3 and C5 bench lines that read them
+# (the C3 / C5 bench lines that read them: tools/r05x.sh)
 set -o pipefail
 T=${1:-r05y}
 O=gpurun_out/$T
@@ -16,6 +16,7 @@ pass() {   # tag counter shape args...
   timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d $O/$tag -o run -- python3 bench.py "$@" > $O/$tag.json 2> $O/$tag.err || { echo "pmc $tag failed"; tail -5 $O/$tag.err; exit 1; }
   local lc=$(echo $ctr | sed 's/_SIZE//' | tr 'A-Z' 'a-z')
   cp "$(pick $O/$tag)" profiles/${T}_pmc_${lc}_${shape}.csv
+  cp "$(pick $O/$tag)" $O/${T}_pmc_${lc}_${shape}.csv
   echo "pmc $tag ok"
 }
 pass c4f FETCH_SIZE L6_4096x1048576 $A4
@@ -24,7 +25,3 @@ pass c3f FETCH_SIZE L1_16384x1048576 $A3
 pass c3w WRITE_SIZE L1_16384x1048576 $A3
 pass c5f FETCH_SIZE L9_256x16777216 $A5
 pass c5w WRITE_SIZE L9_256x16777216 $A5
-timeout -k 10 400 python3 -u bench.py --level 1 --kind enwik --buffers 65536 --steps 3 --warmup 1 > $O/bench_C3_65536x1MiB_L1.json 2> $O/bench_C3.err || { echo "C3 bench failed"; tail -20 $O/bench_C3.err; exit 1; }
-cut -c1-400 $O/bench_C3_65536x1MiB_L1.json
-timeout -k 10 400 python3 -u bench.py --level 9 --kind vocab --buffer-bytes 16777216 --buffers 256 --steps 3 --warmup 1 > $O/bench_C5_256x16MiB_L9.json 2> $O/bench_C5.err || { echo "C5 bench failed"; tail -20 $O/bench_C5.err; exit 1; }
-cut -c1-400 $O/bench_C5_256x16MiB_L9.json
