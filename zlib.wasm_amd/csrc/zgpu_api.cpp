@@ -1213,6 +1213,7 @@ struct InflateResumeDev {          // InflateJob's resume arrays (device, per st
     uint32_t stop_mode;            // InflateJob::stop_mode
     uint64_t *zstate_out;          // InflateJob::zstate_out
     uint32_t dmax = 0;             // InflateJob::dmax
+    uint64_t trees_after = 0;      // InflateJob::trees_after
     uint64_t *eidx = nullptr, *bidx = nullptr;   // InflateJob::eidx / bidx / icnt (null: no index)
     uint32_t *icnt = nullptr;
     uint32_t ecap = 0, bcap = 0;
@@ -1618,6 +1619,7 @@ int inflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.zstate_out = rs->zstate_out;
             job.zcodes = rs->zstate_out != nullptr;
             job.dmax = rs->dmax;
+            job.trees_after = rs->trees_after;
             job.eidx = rs->eidx;
             job.bidx = rs->bidx;
             job.icnt = rs->icnt;
@@ -1725,7 +1727,8 @@ constexpr uint32_t kIdxCap = 1u << 20, kIdxBCap = 1u << 14;
 
 int inflate_try_locked(Ctx &c, const uint8_t *in, size_t n, bool resume, uint64_t start_bit, const uint8_t *hist,
                        size_t hist_len, size_t cap, int wrap, int wbits, std::vector<uint8_t> &out, InflateTry &t,
-                       uint32_t stop_mode = 0, uint32_t dmax = 0, InflateIndex *ix = nullptr) {
+                       uint32_t stop_mode = 0, uint32_t dmax = 0, InflateIndex *ix = nullptr,
+                       uint64_t trees_after = 0) {
     if (!c.ws_io.ensure(n + 64) || !c.ws_io2.ensure(cap + 64) || !c.ws_small.ensure(8 * 16 + 64) ||
         !c.ws_istop.ensure(64))
         return ZGPU_MEM_ERROR;
@@ -1749,6 +1752,7 @@ int inflate_try_locked(Ctx &c, const uint8_t *in, size_t n, bool resume, uint64_
         hipMemcpyAsync(d_hist, &hl, 4, hipMemcpyHostToDevice, st) != hipSuccess)
         return ZGPU_MEM_ERROR;
     InflateResumeDev rs{resume ? d_rbit : nullptr, resume ? d_hist : nullptr, d_blk, stop_mode, d_zs, dmax};
+    rs.trees_after = trees_after;
     if (ix) {
         rs.eidx = c.ws_iidx.as<uint64_t>();
         rs.bidx = rs.eidx + 2ull * kIdxCap;
@@ -2433,6 +2437,7 @@ struct internal_state {
     bool after_hdr = false;                              // the reference stands after a block header (LEN_ / COPY_)
     std::vector<uint64_t> bx;                            // the last decode's block boundaries (absolute bit, output)
     uint64_t bx_last = ~0ull;                            // the bit of the one that ends the last block (a Z_BLOCK stop)
+    std::vector<uint64_t> hx;                            // its block headers' ends (absolute bit | BFINAL << 63, output)
     uint64_t out_at = 0;                                 // absolute output of out[0] (out_pos = ideliv - out_at)
     // the bits inflate.c holds in its bit buffer after the last call: where the
     // input ran out (iheld_end, from the last decode), or below 8 at a stop for
@@ -4039,7 +4044,7 @@ int inflateReset(z_streamp strm) {
     s->isyncpt = false; s->imark = -65536; s->icodes = 0; s->iprime_n = 0; s->iprime_v = 0;
     s->iadl_on = false; s->iadl = 0;
     s->cons = s->fin_used = 0; s->held_at = nullptr; s->ix.clear(); s->ix2.clear(); s->ix_all = false;
-    s->bx.clear(); s->out_at = 0; s->after_hdr = false;
+    s->bx.clear(); s->hx.clear(); s->out_at = 0; s->after_hdr = false;
     s->iheld = s->iheld_end = 0;
     strm->total_in = strm->total_out = 0;
     strm->msg = nullptr;
@@ -4226,8 +4231,14 @@ void keep_index(internal_state *s, InflateIndex &ix, const InflateTry &t, uint64
         }
     };
     if (s->imode == 1) add(s->res_bit, s->res_put, true);           // where the decode started
+    s->hx.clear();
     for (size_t k = 0; k + 1 < ix.b.size(); k += 2) {
-        const uint64_t b = ix.b[k] & ~(1ull << 63);
+        const uint64_t b = ix.b[k] & ~(3ull << 62);
+        if ((ix.b[k] >> 62) & 1u) {                                  // a header's end (Z_TREES stops)
+            s->hx.push_back((b + ib) | (ix.b[k] & (1ull << 63)));
+            s->hx.push_back(ix.b[k + 1] + obase);
+            continue;
+        }
         add(b, ix.b[k + 1], false);
         if (ix.b[k] >> 63) s->bx_last = b + ib;
     }
@@ -4336,7 +4347,6 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
         // call already took the whole header, the decode is mid-block and this
         // call runs to the end of the first block
         bool hdr_done = false;
-        size_t hdr_len = 0;
         if (block && !resume && s->wrap && s->in.size() >= took) {
             const size_t before = s->in.size() - took;          // input the earlier calls gave
             const uint8_t *h = s->in.data();
@@ -4364,14 +4374,13 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
                 if (hlen > before) hlen = 0;
             }
             hdr_done = hlen != 0;
-            hdr_len = hlen;
         }
         // inflate(Z_TREES) also stops after a block header (inflate.c STORED,
-        // fixed TYPEDO, CODELENS: LEN_ / COPY_) when the reference stands at
-        // that block's start: in mode TYPE (or TYPEDO) exactly where it stopped
+        // fixed TYPEDO, CODELENS: LEN_ / COPY_) that the reference has not
+        // finished reading: one ending past where it stands
         const uint64_t pref = 8 * s->cons - s->iheld;            // the reference's bit position
-        const bool at_type = resume ? pref == s->res_bit
-                                    : (s->wrap == 0 ? pref == 0 : hdr_done && pref == 8ull * hdr_len);
+        const uint64_t ib = resume ? 8ull * s->in_base : 0;
+        const uint64_t trees_after = pref > ib ? pref - ib : 0;
         std::vector<uint8_t> o;
         InflateTry t{};
         InflateIndex ixo;
@@ -4384,11 +4393,11 @@ int inflate_attempt(z_streamp strm, internal_state *s, size_t took, bool block =
             const uint32_t mode = hdr_stop ? 1u
                                   : !block ? 0u
                                            : ((!resume && s->wrap && !hdr_done) ? 1u : 2u) | (resume && s->itype ? 4u : 0u) |
-                                                 (trees && at_type ? 8u : 0u);
+                                                 (trees ? 8u : 0u);
             if (!rc) rc = inflate_try_locked(*L.c, s->in.data(), s->in.size(), resume,
                                              resume ? s->res_bit - 8ull * s->in_base : 0, s->hist.data(), hl,
                                              hl + s->cap, s->wrap, s->wbits, o, t, mode,
-                                             s->iback_win ? 1u << s->wbits : 0u, &ixo);
+                                             s->iback_win ? 1u << s->wbits : 0u, &ixo, trees_after);
         }
         if (rc) return rc == ZGPU_ENODEV ? Z_MEM_ERROR : rc;
         if (t.stop != kIFull) {
@@ -4796,7 +4805,8 @@ static int inflate_body(z_streamp strm, int flush) {
     // decodes on only to the end of the block it is in (inflate.c TYPE), the
     // first boundary past the output handed out
     uint64_t cap_put = ~0ull, cap_bit = 0;
-    if (block && s->out_pos < s->out.size() && !s->hdr_stop_now)
+    bool cap_hdr = false, cap_last = false;             // Z_TREES: the stop is a header's end (BFINAL of its block)
+    if (block && s->out_pos < s->out.size() && !s->hdr_stop_now) {
         for (size_t k = 0; k + 1 < s->bx.size(); k += 2)
             // (past a header stop the block's end may be where the reference stands: an empty stored block)
             if ((s->bx[k] > pref0 || (s->after_hdr && s->bx[k] == pref0)) && s->bx[k + 1] >= s->ideliv) {
@@ -4804,6 +4814,20 @@ static int inflate_body(z_streamp strm, int flush) {
                 cap_put = s->bx[k + 1];
                 break;
             }
+        if (trees)                                      // ... or the end of a header the reference has not read
+            for (size_t k = 0; k + 1 < s->hx.size(); k += 2) {
+                const uint64_t hb = s->hx[k] & ~(1ull << 63);
+                if (hb > pref0 && s->hx[k + 1] >= s->ideliv) {
+                    if (cap_put == ~0ull || hb < cap_bit) {
+                        cap_bit = hb;
+                        cap_put = s->hx[k + 1];
+                        cap_hdr = true;
+                        cap_last = s->hx[k] >> 63;
+                    }
+                    break;
+                }
+            }
+    }
     size_t give = 0;
     if (s->out_pos < s->out.size() && !s->hdr_stop_now) {      // (stopped after a header: no output)
         give = std::min<size_t>(strm->avail_out, s->out.size() - s->out_pos);
@@ -4815,6 +4839,11 @@ static int inflate_body(z_streamp strm, int flush) {
         strm->avail_out -= (uInt)give;
         strm->total_out += give;
     }
+    // the last block's output all handed out after a Z_BLOCK stop at its end:
+    // a call that does not stop at block ends reads the trailer too (inflate.c
+    // TYPEDO .. CHECK .. DONE)
+    if (!block && s->itail && !s->finished && !s->acct_done && s->out_pos >= s->out.size())
+        if (int rc = inflate_attempt(strm, s, taking ? avail0 : 0, false)) return rc;
     // the input this call consumed (inflate.c inf_leave): all of it unless the
     // output space ended first, then up to the reference's stop at the output
     // handed out (stall_from_index); a finished stream's up to its end
@@ -4824,7 +4853,12 @@ static int inflate_body(z_streamp strm, int flush) {
     } else {
         uint64_t C;
         s->iheld = s->iheld_end;
-        if (s->ideliv == cap_put) {
+        if (s->ideliv == cap_put && cap_hdr) {
+            // after a block header, mode LEN_ / COPY_ (Z_TREES)
+            C = (cap_bit + 7) >> 3;
+            s->iheld = (uint32_t)(8 * C - cap_bit);
+            strm->data_type = (int)s->iheld + 256 + (cap_last ? 64 : 0);
+        } else if (s->ideliv == cap_put) {
             // at the block's end, mode TYPE: the bits after its end-of-block code held
             C = (cap_bit + 7) >> 3;
             s->iheld = (uint32_t)(8 * C - cap_bit);
@@ -4854,7 +4888,7 @@ static int inflate_body(z_streamp strm, int flush) {
             // the resume point to the last boundary the reference has passed
             advance_resume(s, s->ideliv, 8 * s->cons - s->iheld, s->itail);
         }
-        s->after_hdr = s->hdr_stop_now ||
+        s->after_hdr = s->hdr_stop_now || (s->ideliv == cap_put && cap_hdr) ||
                        (s->after_hdr && give == 0 && s->ideliv != cap_put && 8 * s->cons - s->iheld == pref0);
     }
     s->held_at = strm->next_in;
@@ -5050,6 +5084,7 @@ int inflateSync(z_streamp strm) {
     s->out_pos = 0;
     s->out_at = s->ideliv;
     s->bx.clear();
+    s->hx.clear();
     s->ix2.clear();
     s->after_hdr = false;
     s->in_base = strm->total_in + s->iadj;                     // absolute input position

@@ -321,6 +321,15 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
 
     auto ceil_used = [&]() -> uint64_t { return (bitpos(r) + 7) >> 3; };
     uint32_t ne = 0, nbk = 0;                        // index entries / block boundaries recorded (kIdx)
+    auto index_hdr = [&]() {                         // a block header's end: bit | 1 << 62 | BFINAL << 63
+        if (kIdx) {
+            if (lane == 0 && nbk < job.bcap) {
+                job.bidx[2 * (uint64_t)nbk] = bitpos(r) | 1ull << 62 | (uint64_t)zlast << 63;
+                job.bidx[2 * (uint64_t)nbk + 1] = put;
+            }
+            nbk++;
+        }
+    };
     auto index_sym = [&](uint32_t out_end, bool stored, uint64_t v) {
         if (kIdx) {
             if (lane == 0 && ne < job.ecap) {
@@ -422,7 +431,8 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
             const uint32_t len = (uint32_t)r.hold & 0xffffu, nlen = ((uint32_t)r.hold >> 16) & 0xffffu;
             if (len != (nlen ^ 0xffffu)) { stop = kIData; used = (bitpos(r) >> 3) + 4; goto done; }
             dropb(r, 32);
-            if (job.stop_mode & 8u) {                                // Z_TREES: mode COPY_, before the bytes
+            index_hdr();
+            if ((job.stop_mode & 8u) && bitpos(r) > job.trees_after) {   // Z_TREES: mode COPY_, before the bytes
                 blk_bit = bitpos(r);
                 blk_put = put;
                 stop = kITrees;
@@ -531,7 +541,8 @@ __global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
                 if (job.zcodes)
                     zcodes = codes_used(S.lens, (int)nlen, 9, S.cu, lane) + codes_used(S.lens + nlen, (int)ndist, 6, S.cu, lane);
             }
-            if (job.stop_mode & 8u) {                                // Z_TREES: mode LEN_, before the first code
+            index_hdr();
+            if ((job.stop_mode & 8u) && bitpos(r) > job.trees_after) {   // Z_TREES: mode LEN_, before the first code
                 blk_bit = bitpos(r);
                 blk_put = put;
                 stop = kITrees;

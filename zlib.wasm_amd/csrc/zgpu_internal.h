@@ -365,8 +365,8 @@ struct InflateJob {
     // bit 0 stop right after a zlib / gzip header, bit 1 at the end of the
     // first block that is not the last; the stop (kIBlock) is the boundary in
     // blk_out.  bit 3 (inflate(Z_TREES), inflate.c STORED / TABLE .. LEN_):
-    // stop after the first block header, before its first code (kITrees, the
-    // header's end in blk_out)
+    // stop after the first block header that ends past trees_after, before its
+    // first code (kITrees, the header's end in blk_out)
     uint32_t stop_mode;
     // the state inflate.c would report in strm->data_type where the decode
     // stopped (or null): input bits it would hold (inbits - the bit after the
@@ -379,6 +379,9 @@ struct InflateJob {
     // only when zcodes is set
     int zcodes;
     uint32_t dmax;           // inflateBack: distances beyond its window (1 << windowBits) are errors; 0: none
+    // stop_mode bit 3: only a header that ends past this input bit (where the
+    // reference stands: a header it has begun but not finished, or one after it)
+    uint64_t trees_after;
     // count only (the block-parallel decode's dry run): no output, no match
     // records, no capacity limit; dst_len / rec / blk_out report where the
     // decode ended and how much it would have produced
