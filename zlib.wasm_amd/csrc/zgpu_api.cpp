@@ -4791,7 +4791,9 @@ static int inflate_body(z_streamp strm, int flush) {
     // Z_TREES with the reference at a block's start: the header stop needs a
     // decode even when no new input came (the index knows no header ends)
     const bool trees_due = trees && !s->finished && s->imode == 1 && pref0 == s->res_bit;
+    bool decoded = false;
     if (!s->finished && (took || redo || tail_due || trees_due || (flush == Z_FINISH && s->tried != in_end))) {
+        decoded = true;
         if (block) s->idt = 0;
         if (int rc = inflate_attempt(strm, s, taking ? avail0 : 0, block, trees)) return rc;
         if (s->need_dict) {
@@ -4818,7 +4820,7 @@ static int inflate_body(z_streamp strm, int flush) {
             for (size_t k = 0; k + 1 < s->hx.size(); k += 2) {
                 const uint64_t hb = s->hx[k] & ~(1ull << 63);
                 if (hb > pref0 && s->hx[k + 1] >= s->ideliv) {
-                    if (cap_put == ~0ull || hb < cap_bit) {
+                    if (cap_put == ~0ull || hb <= cap_bit) {    // (an empty stored block: its header stop comes first)
                         cap_bit = hb;
                         cap_put = s->hx[k + 1];
                         cap_hdr = true;
@@ -4888,8 +4890,11 @@ static int inflate_body(z_streamp strm, int flush) {
             // the resume point to the last boundary the reference has passed
             advance_resume(s, s->ideliv, 8 * s->cons - s->iheld, s->itail);
         }
+        // the reference stands after a header: it stopped there this call, or
+        // stood there before and nothing moved it
         s->after_hdr = s->hdr_stop_now || (s->ideliv == cap_put && cap_hdr) ||
-                       (s->after_hdr && give == 0 && s->ideliv != cap_put && 8 * s->cons - s->iheld == pref0);
+                       (s->after_hdr && !decoded && give == 0 && s->ideliv != cap_put &&
+                        8 * s->cons - s->iheld == pref0);
     }
     s->held_at = strm->next_in;
     if (s->finished && !pending && s->ideliv != cap_put) return s->result;
