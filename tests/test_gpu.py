@@ -70,7 +70,9 @@ def test_checksum_device_api_unaligned(zg, oracle):
 
 @pytest.mark.parametrize("level", [4, 6, 9])
 @pytest.mark.parametrize("kind,n", [("text", 16383), ("mix", 200000), ("runs", 70000),
-                                    ("records", 100000), ("four", 50000)])
+                                    ("records", 100000), ("four", 50000),
+                                    # >= 128 KiB: k_links keeps head[] in the key region (k_links_gh)
+                                    ("text", 300001), ("runs", 131072)])
 def test_stage_links_and_match_vs_oracle(zg, oracle, level, kind, n):
     """Per-position intermediates of the GPU pipeline == the oracle's
     position-parallel formulation (zo_pp_links / zo_pp_match)."""

@@ -791,6 +791,10 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         job.pos31 = 1;
         for (uint32_t i = a; i < b; i++)
             if (lens[i] >= (1ull << 31) - (1ull << 16)) job.pos31 = 0;
+        static const int lgh_env = [] { const char *e = std::getenv("ZGPU_LINKS_GH"); return e ? std::atoi(e) : 1; }();
+        job.links_gh = lgh_env && slow && hbits <= 15;
+        for (uint32_t i = a; i < b && job.links_gh; i++)
+            if (lens[i] < kLinksGhMin) job.links_gh = 0;
         job.check = d_check;
         job.wind = d_wind ? d_wind + a : nullptr;
         if (seg_at[s + 1] > seg_at[s]) {
@@ -2093,6 +2097,7 @@ int zgpu_debug_stages(const uint8_t *src, size_t n, int level, uint16_t *link, u
     job.rfull = c.ws_rf.as<uint32_t>();
     job.rquart = c.ws_rq.as<uint32_t>();
     job.key = c.ws_key.as<uint8_t>();
+    job.links_gh = n >= kLinksGhMin;                  // as the batch path picks k_links' head[] place
     if (launch_deflate_stage(0, job, nullptr, st) || launch_deflate_stage(1, job, nullptr, st) ||
         hipStreamSynchronize(st) != hipSuccess)
         return ZGPU_MEM_ERROR;

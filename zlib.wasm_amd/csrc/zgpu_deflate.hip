@@ -146,9 +146,13 @@ constexpr int kLWaves = kLThreads / 64;
 constexpr int kLPer = kLC / kLThreads;
 
 // One stable counting-sort pass of src[0..m) into dst by the 8-bit digit at
-// `shift`.  Wave w owns elements w*512 + j*64 + lane; equal digits within a
+// `shift` (dst may be src: every key is in registers before the first
+// barrier).  Wave w owns elements w*512 + j*64 + lane; equal digits within a
 // wave step are ranked with ballots, counts are scanned digit-major across
-// waves, so the scatter keeps element order within a digit.
+// waves, so the scatter keeps element order within a digit.  (Round 5: equal
+// digits found through a per-wave table of 256 lane masks, each lane ORing its
+// bit into its digit's entry and reading it back, took a quarter of the vector
+// instructions and ran slower: 45.7 against 43.4 ms per 4 GiB.)
 __device__ __attribute__((always_inline)) inline void links_radix_pass(const uint32_t *src, uint32_t *dst, int m,
                                                                        int shift, uint16_t (*wcnt)[256],
                                                                        int *wsum, int tid) {
@@ -157,8 +161,6 @@ __device__ __attribute__((always_inline)) inline void links_radix_pass(const uin
     for (int k = tid; k < kLWaves * 256; k += kLThreads) (&wcnt[0][0])[k] = 0;
     __syncthreads();
     uint32_t key[kLPer], rank[kLPer];
-    const uint64_t all = __ballot(1);
-    (void)all;
 #pragma unroll
     for (int j = 0; j < kLPer; j++) {
         const int e = wave * (64 * kLPer) + j * 64 + lane;
@@ -220,12 +222,21 @@ __device__ __attribute__((always_inline)) inline void links_radix_pass(const uin
 // see k_match): a link reaches back at most 32767 positions, so the segment
 // starts its chains empty at the chunk t0 <= s0 - 32768 and writes the links
 // of [s0, s1) only.
-template <int kC, int kH, bool kSegs = false>
-__global__ __launch_bounds__(kLThreads) void k_links(DeflateJob job) {
-    static_assert(kC <= kLC && (kC & (kC - 1)) == 0, "chunk");
-    __shared__ uint16_t head[kH];
-    __shared__ uint32_t ka[kC], kb[kC];
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kC + 16];
+// kGH (job.links_gh: every buffer >= kLinksGhMin bytes, no segments, no
+// uploaded chains): head[] holds 32-bit positions in the buffer's key[] region
+// (k_count overwrites it next on the same stream) instead of LDS, so it needs
+// no sweep and the workgroup takes 56 KiB of LDS instead of 120: two fit a CU
+// and one's barriers overlap the other's work.  LDS otherwise: head 64 KiB,
+// keys 32 KiB (sorted in place), links 16 KiB (holding the chunk's bytes until
+// the keys are made), counts 8 KiB.
+template <int kC, int kH, bool kSegs, bool kGH>
+__device__ __attribute__((always_inline)) inline void links_body(const DeflateJob &job) {
+    static_assert(kC <= kLC && (kC & (kC - 1)) == 0 && kC >= 32, "chunk");
+    static_assert(!kGH || (!kSegs && kH == 32768), "global head: the default layout, whole buffers");
+    __shared__ uint16_t head[kGH ? 1 : kH];
+    __shared__ uint32_t ka[kC];
+    __shared__ __attribute__((aligned(16))) uint16_t lk[kC];      // links by chunk index
+    uint8_t *const stage = reinterpret_cast<uint8_t *>(lk);       // first the chunk's kC + 16 bytes
     __shared__ uint16_t wcnt[kLWaves][256];
     __shared__ int wsum[kLWaves];
     const int tid = threadIdx.x;
@@ -239,13 +250,18 @@ __global__ __launch_bounds__(kLThreads) void k_links(DeflateJob job) {
     const int64_t s1 = kSegs && s0 + (int64_t)job.seg_len < n ? s0 + (int64_t)job.seg_len : n;
     const int64_t t0 = kSegs && s0 > 32768 ? (s0 - 32768) / kC * kC : 0;
 
+    uint32_t *const ghead = kGH ? reinterpret_cast<uint32_t *>(job.key + job.ws_off[bi]) : nullptr;
     // "position t0 - 32768": older than any chain from t0 on reaches
-    for (int i = tid; i < kH; i += kLThreads) head[i] = (uint16_t)((t0 - 32768) & 0xffff);
-    const int64_t lk_n = !kSegs && job.lk_head ? (int64_t)job.lk_n : 0;
+    if constexpr (kGH)
+        for (int i = tid; i < kH; i += kLThreads) ghead[i] = (uint32_t)-32768;
+    else
+        for (int i = tid; i < kH; i += kLThreads) head[i] = (uint16_t)((t0 - 32768) & 0xffff);
+    const int64_t lk_n = !kSegs && !kGH && job.lk_head ? (int64_t)job.lk_n : 0;
     for (int64_t c0 = t0; c0 < s1; c0 += kC) {
         __syncthreads();
         if (c0 + kC <= lk_n) continue;                       // links as uploaded (deflate_fast's chains)
-        if (c0 <= lk_n && job.lk_head) {                     // the chains at lk_n: head[] of the uploaded state
+        if (kGH) {
+        } else if (c0 <= lk_n && job.lk_head) {              // the chains at lk_n: head[] of the uploaded state
             // (entries may lie inside this chunk, below lk_n: no sweep here, the
             // age test is this one)
             const int hn = (int)wp.mask + 1;                 // hash_size entries were uploaded
@@ -278,8 +294,9 @@ __global__ __launch_bounds__(kLThreads) void k_links(DeflateJob job) {
             }
             ka[e - e0] = h << 13 | (uint32_t)e;
         }
-        links_radix_pass(ka, kb, ms, 13, wcnt, wsum, tid);
-        links_radix_pass(kb, ka, ms, 21, wcnt, wsum, tid);
+        // (the passes' first barrier also ends the reads of stage[] above)
+        links_radix_pass(ka, ka, ms, 13, wcnt, wsum, tid);
+        links_radix_pass(ka, ka, ms, 21, wcnt, wsum, tid);
         // sorted: ka[i] = hash << 13 | e, hashes ascending, e ascending within a hash
         for (int i = tid; i < ms; i += kLThreads) {
             const uint32_t key = ka[i];
@@ -288,22 +305,35 @@ __global__ __launch_bounds__(kLThreads) void k_links(DeflateJob job) {
             uint32_t d;
             if (h == kSkipHash) d = 0;                                       // not inserted (SkipSpec)
             else if (i > 0 && (ka[i - 1] >> 13) == h) d = e - (ka[i - 1] & (kLC - 1));
+            else if (kGH) d = p - ghead[h];
             else d = (p - head[h]) & 0xffffu;
-            kb[e] = (d != 0 && d <= 32767u && d != p) ? d : 0u;               // position 0 is NIL
+            lk[e] = (uint16_t)((d != 0 && d <= 32767u && d != p) ? d : 0u);   // position 0 is NIL
         }
         __syncthreads();
         for (int i = tid; i < ms; i += kLThreads) {
             const uint32_t key = ka[i];
-            if ((key >> 13) != kSkipHash && (i == ms - 1 || (ka[i + 1] >> 13) != (key >> 13)))
-                head[key >> 13] = (uint16_t)(((uint32_t)c0 + (key & (kLC - 1))) & 0xffffu);
+            if ((key >> 13) != kSkipHash && (i == ms - 1 || (ka[i + 1] >> 13) != (key >> 13))) {
+                if (kGH) ghead[key >> 13] = (uint32_t)c0 + (key & (kLC - 1));
+                else head[key >> 13] = (uint16_t)(((uint32_t)c0 + (key & (kLC - 1))) & 0xffffu);
+            }
         }
         if (kSegs) {
             const int w0 = s0 > c0 ? (int)(s0 - c0) : 0, w1 = (int)(s1 - c0 < cnt ? s1 - c0 : cnt);
-            for (int e = tid + w0; e < w1; e += kLThreads) out[c0 + e] = e < m ? (uint16_t)kb[e] : (uint16_t)0;
+            for (int e = tid + w0; e < w1; e += kLThreads) out[c0 + e] = e < m ? lk[e] : (uint16_t)0;
         } else {
-            for (int e = tid + e0; e < cnt; e += kLThreads) out[c0 + e] = e < m ? (uint16_t)kb[e] : (uint16_t)0;
+            for (int e = tid + e0; e < cnt; e += kLThreads) out[c0 + e] = e < m ? lk[e] : (uint16_t)0;
         }
     }
+}
+
+template <int kC, int kH, bool kSegs = false>
+__global__ __launch_bounds__(kLThreads) void k_links(DeflateJob job) {
+    links_body<kC, kH, kSegs, false>(job);
+}
+
+// two workgroups per CU: at most 64 VGPRs (8 waves per SIMD)
+__global__ __launch_bounds__(kLThreads, 8) void k_links_gh(DeflateJob job) {
+    links_body<kLC, 32768, false, true>(job);
 }
 
 // ------------------------------------------------------------------------
@@ -4934,6 +4964,7 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
             break;
         }
         if (job.hbits > 15) hipLaunchKernelGGL((k_links<2048, 65536>), grid, dim3(kLThreads), 0, st, job);
+        else if (job.links_gh && !job.lk_head) hipLaunchKernelGGL(k_links_gh, grid, dim3(kLThreads), 0, st, job);
         else hipLaunchKernelGGL((k_links<kLC, 32768>), grid, dim3(kLThreads), 0, st, job);
         hipLaunchKernelGGL(k_count<false>, grid, dim3(kCntThreads), 0, st, job);
         break;

@@ -19,6 +19,8 @@ constexpr int kSymLimit = 16383;                            // lit_bufsize - 1
 // (few large buffers) must start every segment on a tile boundary, so the
 // host's segment sizes are whole multiples of it.
 constexpr uint32_t kMatchTile = 4096;
+// k_links keeps head[] in the key[] region (32 Ki x 4 B) for buffers this long
+constexpr uint64_t kLinksGhMin = 131072;
 // Buffers are addressed with 32-bit positions inside the kernels: deflate
 // refuses buffers of kMaxBuffer bytes or more (Z_STREAM_ERROR / Z_MEM_ERROR).
 constexpr uint64_t kMaxBuffer = (1ull << 32) - (1ull << 16);
@@ -187,6 +189,10 @@ struct DeflateJob {
     // every buffer of the sub-batch is under 2^31 bytes: k_parse_fast runs on
     // 32-bit positions
     int pos31;
+    // every buffer of the sub-batch has >= kLinksGhMin bytes: k_links keeps its
+    // head[] table (32-bit positions) in the buffer's key[] region, which
+    // k_count overwrites after it, instead of in LDS (two workgroups per CU)
+    int links_gh;
     // deflateInit2_'s windowBits (9..15; 8 is stored as 9, deflate.c:395) and
     // memLevel + 7 = hash_bits (8..16): w_size = 1 << wbits, MAX_DIST = w_size
     // - 262, hash_shift = (hash_bits + 2) / 3, lit_bufsize = 1 << (memLevel + 6)
