@@ -792,7 +792,9 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         for (uint32_t i = a; i < b; i++)
             if (lens[i] >= (1ull << 31) - (1ull << 16)) job.pos31 = 0;
         static const int lgh_env = [] { const char *e = std::getenv("ZGPU_LINKS_GH"); return e ? std::atoi(e) : 1; }();
-        job.links_gh = lgh_env && slow && hbits <= 15;
+        // not in the pipeline: there k_links runs beside k_match, and two
+        // k_links_gh workgroups per CU slow the walks by what they save
+        job.links_gh = lgh_env && slow && hbits <= 15 && (!piped || lgh_env == 2);
         for (uint32_t i = a; i < b && job.links_gh; i++)
             if (lens[i] < kLinksGhMin) job.links_gh = 0;
         job.check = d_check;
