@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: PMC FETCH_SIZE / WRITE_SIZE passes (separate runs) of the C4, C3
 # and C5 launch shapes, copied into profiles/ for bench.py's roofline, then
-# (the C3 / C5 bench lines that read them: tools/r05x.sh)
+# (the C3 / C5 bench lines that read them: tools/jobs/r05x.sh)
 set -o pipefail
 T=${1:-r05y}
 O=gpurun_out/$T
