@@ -403,6 +403,24 @@ def test_fast_levels_lds_parse(zg, level):
             assert st == 0 and z == _syszlib(b, level), (len(b), count)
 
 
+@pytest.mark.parametrize("level", [5, 6, 9])
+def test_links_head_in_key_region_params(zg, level):
+    """k_links_gh (head[] as 32-bit positions in the key region, for batches
+    whose buffers are all >= 128 KiB and whose stages run one after another)
+    under other windowBits / memLevels: hash_bits 8..15 index the same table,
+    memLevel 9 keeps the LDS kernel; streams equal system zlib's, beside a
+    batch with one buffer under 128 KiB (the LDS kernel)."""
+    bufs = [datagen.make("mix", 200000, 91), datagen.make("text", 300001, 92)]
+    for wb, ml in ((9, 1), (10, 5), (13, 7), (15, 8), (15, 9)):
+        got = zg.compress_batch2(bufs, level=level, window_bits=wb, mem_level=ml)
+        for b, (st, z) in zip(bufs, got):
+            assert st == 0 and z == _syszlib(b, level, wb, ml), (len(b), wb, ml)
+    mixed = bufs + [datagen.make("records", 70000, 93)]
+    got = zg.compress_batch(mixed, level=level)
+    for b, (st, z) in zip(mixed, got):
+        assert st == 0 and z == _syszlib(b, level), len(b)
+
+
 def test_wasm_production_entry_points(zg, oracle):
     """The reference's production path: Zlib.compress -> zlib_compress_buffer,
     and the zlib_crc32 / zlib_adler32 exports (src/wasm_module.c:35,66,74),
