@@ -272,8 +272,13 @@ __device__ __attribute__((noinline)) uint32_t codes_used(const uint16_t *lens, i
 }
 
 // kIdx: the streaming inflate()'s consumption index (InflateJob::eidx / bidx)
-template <bool kIdx>
-__global__ __launch_bounds__(64) void k_inflate_decode(InflateJob job) {
+// kW: waves per SIMD the register budget is cut for (0: the compiler's
+// choice, 125 VGPRs = 4 waves; 5: 96 VGPRs and a 64-byte spill).  Batches of
+// 2048 streams or more take kW = 5: the C4 inflate leg 12.27 -> 12.57 GB/s
+// (profiles/r05y2_ab_inflate_five_waves.log); 6 or more waves do not fit.
+// ZGPU_INFL_W5=0 keeps 4 waves everywhere, =2 takes 5 for every batch (tests).
+template <bool kIdx, int kW = 0>
+__global__ __launch_bounds__(64, kW ? kW : 1) void k_inflate_decode(InflateJob job) {
     __shared__ InfLDS S;
     const int lane = threadIdx.x;
     const uint32_t bi = blockIdx.x, g = job.first + bi;
@@ -1023,11 +1028,18 @@ int launch_infl_resolve(uint8_t *out, const uint32_t *sym, uint64_t o0, uint64_t
     return (int)hipGetLastError();
 }
 
+static int infl_w5() {
+    static const int v = [] { const char *e = getenv("ZGPU_INFL_W5"); return e ? atoi(e) : 1; }();
+    return v;
+}
+
 int launch_inflate_stage(int stage, const InflateJob &job, hipStream_t st) {
     if (job.count == 0) return 0;
     switch (stage) {
     case 0:
         if (job.eidx) hipLaunchKernelGGL(k_inflate_decode<true>, dim3(job.count), dim3(64), 0, st, job);
+        else if (infl_w5() == 2 || (infl_w5() == 1 && job.count >= 2048))
+            hipLaunchKernelGGL((k_inflate_decode<false, 5>), dim3(job.count), dim3(64), 0, st, job);
         else hipLaunchKernelGGL(k_inflate_decode<false>, dim3(job.count), dim3(64), 0, st, job);
         break;
     case 1: hipLaunchKernelGGL(k_inflate_copy, dim3(job.count), dim3(64), 0, st, job); break;
