@@ -690,6 +690,7 @@ done:
 // ------------------------------------------------------------------------
 constexpr uint32_t kWin = 40960;       // >= 32768 + kChunk + 258
 constexpr uint32_t kChunk = 4096;
+constexpr uint32_t kLaneCopy = 32;     // matches this short are copied one lane each (k_inflate_copy)
 
 __device__ __attribute__((always_inline)) inline uint32_t wslot(uint32_t p) { return p % kWin; }
 
@@ -725,6 +726,25 @@ __global__ __launch_bounds__(64) void k_inflate_copy(InflateJob job) {
             const uint32_t pos = lo;
             if (pos >= c1) break;
             const uint32_t len = hi & 511u, dist = hi >> 9;
+            // round 5: a run of short matches, one lane each (lane = record mbase + lane).
+            // Lane k leads; a later lane joins while its source ends before the lead's
+            // position (all final bytes: literals or earlier matches), so no lane reads
+            // what another writes, and a lane copies its own bytes in order (a source
+            // overlapping its own destination included)
+            if (len <= kLaneCopy) {
+                const uint32_t ml = (uint32_t)mreg, mh = (uint32_t)(mreg >> 32);
+                const uint32_t lp = ml, ll = mh & 511u, ld = mh >> 9;
+                const bool in_run = lane >= k && mbase + (uint32_t)lane < nm && lp < c1 && ll <= kLaneCopy &&
+                                    (lane == k || lp - ld + ll <= pos);
+                const uint64_t stop_m = __ballot(!in_run && lane >= k);
+                const int end = stop_m ? (int)__builtin_ctzll(stop_m) : 64;     // lanes [k, end)
+                if (lane >= k && lane < end) {
+                    const uint32_t s0 = lp - ld;
+                    for (uint32_t j = 0; j < ll; j++) W[wslot(lp + j)] = W[wslot(s0 + j)];
+                }
+                mi = mbase + (uint32_t)end;
+                continue;
+            }
             const uint32_t s0 = pos - dist;
             if (dist >= len) {
                 for (uint32_t j = (uint32_t)lane; j < len; j += 64) W[wslot(pos + j)] = W[wslot(s0 + j)];
