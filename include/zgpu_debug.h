@@ -20,6 +20,10 @@ int zgpu_debug_stages(const uint8_t *src, size_t n, int level, uint16_t *link,
 /* streams the block-parallel decode of a lone stream finished so far (the
  * others went through the sequential decode) */
 uint64_t zgpu_debug_par_inflates(void);
+/* buffers the segmented lazy parse (k_parse_seg) handed to the sequential one
+ * so far: out[0] lanes that did not meet their neighbour within one segment,
+ * out[1] run-ons longer than the lane's staging room */
+int zgpu_debug_parse_fallbacks(uint64_t *out);
 #ifdef __cplusplus
 }
 #endif

@@ -2073,6 +2073,12 @@ int zgpu_generate_dev(uint8_t *dst, uint64_t len, uint32_t count, int kind, uint
 
 uint64_t zgpu_debug_par_inflates(void) { return g_par_inflates.load(); }
 
+int zgpu_debug_parse_fallbacks(uint64_t *out) {
+    Lease L;
+    if (L.rc) return L.rc;
+    return zgpu::parse_fallback_counts(out) ? ZGPU_STREAM_ERROR : ZGPU_OK;
+}
+
 int zgpu_debug_stages(const uint8_t *src, size_t n, int level, uint16_t *link, uint32_t *rfull,
                       uint32_t *rquart) {
     Lease L;

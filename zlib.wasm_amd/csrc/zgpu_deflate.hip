@@ -1156,10 +1156,16 @@ __device__ uint32_t walk_best0(const uint8_t *in, const uint16_t *lk, uint32_t p
     return (uint32_t)best <= lookahead ? (uint32_t)best : lookahead;
 }
 
+// kT: the staged tile.  The fallback launch after k_parse_seg (only_flagged)
+// takes kT = 256 (2.3 KiB of LDS instead of 36): in the pipeline its
+// workgroups, nearly all of which return at once, then fit beside k_match's
+// 153.6 KiB instead of waiting for CUs it has freed (14-18 ms per sub-batch on
+// the caller's stream, profiles/r05v2_kernel_stats_C4_32768x1MiB_L6.csv).
+template <int kT>
 __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flagged) {
-    __shared__ __attribute__((aligned(16))) uint32_t s_rf[kPT];
-    __shared__ __attribute__((aligned(16))) uint32_t s_rq[kPT];
-    __shared__ __attribute__((aligned(16))) uint8_t s_in[kPT + 16];   // in[t0-16 .. t0+kPT)
+    __shared__ __attribute__((aligned(16))) uint32_t s_rf[kT];
+    __shared__ __attribute__((aligned(16))) uint32_t s_rq[kT];
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[kT + 16];   // in[t0-16 .. t0+kT)
     const int lane = threadIdx.x;
     const uint32_t bi = blockIdx.x;
     const uint32_t g = job.first + bi;
@@ -1200,13 +1206,13 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
 
     uint32_t t0 = p & ~15u;
     while (!done) {
-        stage_words<64, kPT / 4 / 64>(s_rf, rf, t0, kPT, n, lane);
-        if (stage_q) stage_words<64, kPT / 4 / 64>(s_rq, rq, t0, kPT, n, lane);
-        stage_bytes<64, (kPT + 16) / 16 / 64 + 1>(s_in, in, (int64_t)t0 - 16, kPT + 16, n, lane);
+        stage_words<64, kT / 4 / 64>(s_rf, rf, t0, kT, n, lane);
+        if (stage_q) stage_words<64, kT / 4 / 64>(s_rq, rq, t0, kT, n, lane);
+        stage_bytes<64, (kT + 16) / 16 / 64 + 1>(s_in, in, (int64_t)t0 - 16, kT + 16, n, lane);
         __syncthreads();
-        const bool tile_to_end = (uint64_t)t0 + kPT >= n;
+        const bool tile_to_end = (uint64_t)t0 + kT >= n;
         for (;;) {
-            if (!tile_to_end && p + 64 > t0 + kPT) break;         // reload, keep 64 lookahead
+            if (!tile_to_end && p + 64 > t0 + kT) break;         // reload, keep 64 lookahead
             if (p > po.E) { done = true; break; }                 // guard: never parse past the input read
             if (po.E - p < (uint32_t)kMinLookahead) {
                 po.fill(p, lim);
@@ -1395,6 +1401,17 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
 // has more symbols than the lane has state words, is flagged
 // (nblocks = ~0) for k_parse_slow.
 // ------------------------------------------------------------------------
+// buffers k_parse_seg handed to k_parse_slow: [0] a lane did not meet its
+// neighbour within the next segment, [1] a run-on outgrew the lane's state words
+__device__ unsigned long long g_parse_fb[2];
+int parse_fallback_counts(uint64_t *out) {
+    unsigned long long v[2] = {0, 0};
+    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(g_parse_fb), sizeof v) != hipSuccess) return -1;
+    out[0] = v[0];
+    out[1] = v[1];
+    return 0;
+}
+
 constexpr int kSegMin = 512;
 constexpr int kParseLanes = 256;                  // segments (lanes) per buffer
 static_assert(kParseLanes == (int)kParseLanesHost, "host lane groups");
@@ -1603,7 +1620,10 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
     __threadfence_block();
     __syncthreads();
     if (s_fail) {
-        if (lane == 0) job.nblocks[bi] = kParseFallback;
+        if (lane == 0) {
+            job.nblocks[bi] = kParseFallback;
+            atomicAdd(&g_parse_fb[0], 1ull);
+        }
         return;
     }
     // the true parse is lane i's on [y(i-1), y(i)) (lane 0 from 0; y = kEnd: to
@@ -1658,7 +1678,10 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
     __threadfence_block();
     __syncthreads();
     if (s_fail) {
-        if (lane == 0) job.nblocks[bi] = kParseFallback;
+        if (lane == 0) {
+            job.nblocks[bi] = kParseFallback;
+            atomicAdd(&g_parse_fb[1], 1ull);
+        }
         return;
     }
     uint32_t woff = 0, total = 0;
@@ -4952,6 +4975,11 @@ __global__ __launch_bounds__(64) void k_parse_srt(DeflateJob job) {
     if (lane == 0) job.nblocks[bi] = po.nblk;
 }
 
+static bool fb_bigtile() {
+    static const bool v = [] { const char *e = getenv("ZGPU_FB_BIGTILE"); return e && e[0] == '1'; }();
+    return v;
+}
+
 int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipStream_t st) {
     const dim3 grid(job.count);
     switch (stage) {
@@ -4982,9 +5010,12 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
             hipLaunchKernelGGL((k_match<false, false>), mgrid, dim3(kMatchThreads), 0, st, job, wq);
         break;
     }
-    case 2: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 0); break;
+    case 2: hipLaunchKernelGGL(k_parse_slow<kPT>, grid, dim3(64), 0, st, job, 0); break;
     case 5: hipLaunchKernelGGL(k_parse_seg, grid, dim3(kParseLanes), 0, st, job); break;
-    case 6: hipLaunchKernelGGL(k_parse_slow, grid, dim3(64), 0, st, job, 1); break;
+    case 6:                                     // ZGPU_FB_BIGTILE=1 (A/B): the 36 KiB tile here too
+        if (fb_bigtile()) hipLaunchKernelGGL(k_parse_slow<kPT>, grid, dim3(64), 0, st, job, 1);
+        else hipLaunchKernelGGL(k_parse_slow<256>, grid, dim3(64), 0, st, job, 1);
+        break;
     case 3: {
         const bool ev = job.nfl || job.start || job.srec;
         // few buffers (a lone compress2 at L1-3): head / prev / window in LDS, one wave per CU

@@ -430,6 +430,8 @@ size_t checksum_scratch_bytes(uint32_t count);
 //        11 lazy parse of few large buffers (k_pbig*; 6 handles its fallbacks),
 //        12 encode of few large buffers (k_enc_plan, k_enc_scan, k_enc_emit)
 int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipStream_t st);
+// k_parse_seg's fallback counters (zgpu_debug_parse_fallbacks): out[0..1]
+int parse_fallback_counts(uint64_t *out);
 // a18 helpers (zgpu_helpers.hip)
 int launch_slide_hash(uint16_t *head, uint16_t *prev, uint32_t hash_size, uint32_t window_size, uint32_t wsize,
                       hipStream_t st);

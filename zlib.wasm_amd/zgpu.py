@@ -64,7 +64,7 @@ EXPORTED_SYMBOLS = (
     "zlib_stream_total_out", "zlib_slide_hash_simd", "zlib_compare256_simd",
     "zlib_longest_match_simd", "zlib_chunkmemset_simd",
     # include/zgpu_debug.h (test-only)
-    "zgpu_debug_stages", "zgpu_debug_par_inflates",
+    "zgpu_debug_stages", "zgpu_debug_par_inflates", "zgpu_debug_parse_fallbacks",
 )
 
 
