@@ -5013,7 +5013,9 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     case 2: hipLaunchKernelGGL(k_parse_slow<kPT>, grid, dim3(64), 0, st, job, 0); break;
     case 5: hipLaunchKernelGGL(k_parse_seg, grid, dim3(kParseLanes), 0, st, job); break;
     case 6:                                     // ZGPU_FB_BIGTILE=1 (A/B): the 36 KiB tile here too
-        if (fb_bigtile()) hipLaunchKernelGGL(k_parse_slow<kPT>, grid, dim3(64), 0, st, job, 1);
+        // few buffers (no pipeline; a flagged buffer may be 16 MiB or more, where
+        // 256-position tiles would reload 20x as often): the 36 KiB tile
+        if (fb_bigtile() || job.count < 512) hipLaunchKernelGGL(k_parse_slow<kPT>, grid, dim3(64), 0, st, job, 1);
         else hipLaunchKernelGGL(k_parse_slow<256>, grid, dim3(64), 0, st, job, 1);
         break;
     case 3: {
