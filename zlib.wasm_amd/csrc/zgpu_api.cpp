@@ -245,6 +245,7 @@ struct Ctx {
     // sub-batch i+1 runs on `aux` while links/parse/encode run on the caller's
     // stream)
     DevBuf ws_link2, ws_rf2, ws_rq2, ws_state2;
+    DevBuf ws_sym2, ws_blk2;  // k_lzp (the walks and the parse of slot 1 beside the encode of slot 0)
     DevBuf ws_key, ws_key2;   // k_count's walk-length keys (one byte per position)
     DevBuf ws_stg;            // k_parse_seg's symbol staging (caller's stream only)
     DevBuf ws_help;           // the a18 helpers' staging (zlib_*_simd)
@@ -545,36 +546,6 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     const size_t nsub = cuts.size() - 1;
     static const bool no_pipe = std::getenv("ZGPU_NO_PIPELINE") != nullptr;
     const bool piped = slow && nsub > 1 && !no_pipe;
-    if (!c.ws_meta.ensure(16ull * count + 8ull * max_cnt * 2)) return zfail(__LINE__);
-    const size_t ckb = checksum_scratch_bytes(max_cnt);     // trailer checksums of few large buffers
-    void *ck = ckb && c.ws_ck.ensure(ckb) ? c.ws_ck.p : nullptr;
-    if (!c.ws_link.ensure(2 * max_pos + 64)) return zfail(__LINE__);
-    if (!c.ws_sym.ensure(4 * max_pos + 64)) return zfail(__LINE__);
-    if (!c.ws_blk.ensure(sizeof(BlockRec) * max_blk)) return zfail(__LINE__);
-    if ((slow || huff || rle) && !c.ws_rf.ensure(4 * max_pos + 64)) return zfail(__LINE__);
-    // rquart: quarter-budget results (L5-9) and the lazy parse's symbol-start staging (L4-9)
-    if (slow && !c.ws_rq.ensure(4 * max_pos + 64)) return zfail(__LINE__);
-    if (slow && !c.ws_state.ensure(max_pos / 4 + 64)) return zfail(__LINE__);
-    if (slow && !c.ws_key.ensure(max_pos + 64)) return zfail(__LINE__);
-    if (slow && !c.ws_stg.ensure(4 * max_pos + 64)) return zfail(__LINE__);
-    if (piped) {
-        if (!c.ws_key2.ensure(max_pos + 64)) return zfail(__LINE__);
-        if (!c.ws_link2.ensure(2 * max_pos + 64) || !c.ws_rf2.ensure(4 * max_pos + 64) ||
-            !c.ws_rq2.ensure(4 * max_pos + 64) || !c.ws_state2.ensure(max_pos / 4 + 64))
-            return zfail(__LINE__);
-        if (!c.aux && hipStreamCreateWithFlags(&c.aux, hipStreamNonBlocking) != hipSuccess) {
-            c.aux = nullptr;
-            return zfail(__LINE__);
-        }
-        for (int k = 0; k < 2; k++) {
-            if (!c.ev_links[k] && hipEventCreateWithFlags(&c.ev_links[k], hipEventDisableTiming) != hipSuccess)
-                return zfail(__LINE__);
-            if (!c.ev_match[k] && hipEventCreateWithFlags(&c.ev_match[k], hipEventDisableTiming) != hipSuccess)
-                return zfail(__LINE__);
-        }
-    }
-    if (level >= 1 && level <= 3 && !huff && !rle && !c.ws_heads.ensure(4ull * hsize * max_cnt))
-        return zfail(__LINE__);
     // k_match per segment where a sub-batch has too few buffers to fill the GPU
     // one workgroup per buffer (a single zlib.h buffer, say).  The segment is
     // the sub-batch's bytes over the 256 CUs, in whole 4 KiB tiles, at most
@@ -604,6 +575,46 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
                           hipMemcpyAsync(c.ws_seg.p, segs.data(), 4 * segs.size(), hipMemcpyHostToDevice, st) !=
                               hipSuccess))
         return zfail(__LINE__);
+    // k_lzp (round 6, the A/B build only): the walks only where deflate_slow
+    // asks for them, and the parse, in one kernel per buffer, for batch jobs of
+    // levels whose chain is at most kLzpMaxChain (levels 4..7) and no
+    // per-segment match.  Exact, and slower than k_match + k_parse_seg
+    // (DESIGN.md 4.15); ZGPU_LZP=1 in a library built with it.
+    static const int lzp_env = [] { const char *e = std::getenv("ZGPU_LZP"); return e && lzp_built() ? std::atoi(e) : 0; }();
+    const LevelCfg jcfg = tune ? *tune : kLevelCfg[level];
+    const bool lzp = lzp_env && slow && !fs && jcfg.chain >= 4 && jcfg.chain <= kLzpMaxChain && segs.empty();
+    if (!c.ws_meta.ensure(16ull * count + 8ull * max_cnt * 2)) return zfail(__LINE__);
+    const size_t ckb = checksum_scratch_bytes(max_cnt);     // trailer checksums of few large buffers
+    void *ck = ckb && c.ws_ck.ensure(ckb) ? c.ws_ck.p : nullptr;
+    if (!c.ws_link.ensure(2 * max_pos + 64)) return zfail(__LINE__);
+    if (!c.ws_sym.ensure(4 * max_pos + 64)) return zfail(__LINE__);
+    if (!c.ws_blk.ensure(sizeof(BlockRec) * max_blk)) return zfail(__LINE__);
+    if ((slow || huff || rle) && !c.ws_rf.ensure(4 * max_pos + 64)) return zfail(__LINE__);
+    // rquart: quarter-budget results (L5-9; k_lzp: every level)
+    if (slow && !c.ws_rq.ensure(4 * max_pos + 64)) return zfail(__LINE__);
+    if (slow && !lzp && !c.ws_state.ensure(max_pos / 4 + 64)) return zfail(__LINE__);
+    if (slow && !c.ws_key.ensure(max_pos + 64)) return zfail(__LINE__);
+    if (slow && !lzp && !c.ws_stg.ensure(4 * max_pos + 64)) return zfail(__LINE__);
+    if (piped) {
+        if (!c.ws_key2.ensure(max_pos + 64)) return zfail(__LINE__);
+        if (!c.ws_link2.ensure(2 * max_pos + 64) || !c.ws_rq2.ensure(4 * max_pos + 64)) return zfail(__LINE__);
+        if (!c.ws_rf2.ensure(4 * max_pos + 64)) return zfail(__LINE__);
+        if (!lzp && !c.ws_state2.ensure(max_pos / 4 + 64)) return zfail(__LINE__);
+        if (lzp && (!c.ws_sym2.ensure(4 * max_pos + 64) || !c.ws_blk2.ensure(sizeof(BlockRec) * max_blk)))
+            return zfail(__LINE__);
+        if (!c.aux && hipStreamCreateWithFlags(&c.aux, hipStreamNonBlocking) != hipSuccess) {
+            c.aux = nullptr;
+            return zfail(__LINE__);
+        }
+        for (int k = 0; k < 2; k++) {
+            if (!c.ev_links[k] && hipEventCreateWithFlags(&c.ev_links[k], hipEventDisableTiming) != hipSuccess)
+                return zfail(__LINE__);
+            if (!c.ev_match[k] && hipEventCreateWithFlags(&c.ev_match[k], hipEventDisableTiming) != hipSuccess)
+                return zfail(__LINE__);
+        }
+    }
+    if (level >= 1 && level <= 3 && !huff && !rle && !c.ws_heads.ensure(4ull * hsize * max_cnt))
+        return zfail(__LINE__);
     // The sorted-run longest_match (k_bsort / k_bwork / k_match2) for batch
     // jobs at levels 4..9 with hash_bits <= 15 and no per-segment match
     // (ZGPU_MATCH2=0 keeps the chain-walk k_match everywhere).  Per sub-batch:
@@ -611,7 +622,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     // (position-indexed, one slot: all three kernels run on one stream), and
     // a hash table per block.
     static const int match2_env = [] { const char *e = std::getenv("ZGPU_MATCH2"); return e ? std::atoi(e) : 0; }();
-    bool m2 = match2_env == 1 && slow && !fs && hbits <= 15;
+    bool m2 = match2_env == 1 && slow && !fs && hbits <= 15 && !lzp;
     // few large buffers: k_match2 per range of m2_segb blocks (buffer, first
     // block) where the chain walk would go per byte segment (segs)
     std::vector<uint32_t> m2segs;
@@ -741,6 +752,7 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     uint64_t *d_meta = c.ws_meta.as<uint64_t>();
     uint32_t *d_nblk = reinterpret_cast<uint32_t *>(d_meta + 2ull * count);
     uint32_t *d_check = d_nblk + max_cnt;
+    uint32_t *d_nblk2 = d_check + max_cnt;                   // k_lzp's slot 1 (ws_meta holds 4 x max_cnt words)
     if (hipMemcpyAsync(d_meta, meta.data(), 16ull * count, hipMemcpyHostToDevice, st) != hipSuccess)
         return zfail(__LINE__);
     // ZGPU_POISON (debug): fill every workspace with a per-call byte pattern so
@@ -784,10 +796,19 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         job.rfull = (slow || huff || rle) ? (slot ? c.ws_rf2 : c.ws_rf).as<uint32_t>() : nullptr;
         job.rquart = slow ? (slot ? c.ws_rq2 : c.ws_rq).as<uint32_t>() : nullptr;
         job.sym = c.ws_sym.as<uint32_t>();
-        job.stage = slow ? c.ws_stg.as<uint32_t>() : nullptr;
-        job.pstate = slow ? (slot ? c.ws_state2 : c.ws_state).as<uint32_t>() : nullptr;
+        job.stage = slow && !lzp ? c.ws_stg.as<uint32_t>() : nullptr;
+        job.pstate = slow && !lzp ? (slot ? c.ws_state2 : c.ws_state).as<uint32_t>() : nullptr;
         job.blocks = c.ws_blk.as<BlockRec>();
         job.nblocks = d_nblk;
+        static const int lzp_flags = [] { const char *e = std::getenv("ZGPU_LZP_FLAGS"); return e ? std::atoi(e) : 1; }();
+        job.lzp_flags = lzp_flags;
+        if (lzp) {                                      // k_lzp writes the symbols beside the encode: two slots
+            if (slot) {
+                job.sym = c.ws_sym2.as<uint32_t>();
+                job.blocks = c.ws_blk2.as<BlockRec>();
+                job.nblocks = d_nblk2;
+            }
+        }
         job.pos31 = 1;
         for (uint32_t i = a; i < b; i++)
             if (lens[i] >= (1ull << 31) - (1ull << 16)) job.pos31 = 0;
@@ -893,6 +914,8 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             // flush jobs: the sequential lazy parse (the segmented one does not
             // model a flush's effect on the parse)
             if (T.run(3, st, [&] { return launch_deflate_stage(2, job, nullptr, st); })) return zfail(__LINE__);
+        } else if (level >= 4 && lzp) {
+            // parsed by k_lzp with the walks
         } else if (level >= 4) {
             const int ps = job.pgrp ? 11 : 5;                  // few large buffers: k_pbig*
             if (T.run(3, st, [&] { return launch_deflate_stage(ps, job, nullptr, st); })) return zfail(__LINE__);
@@ -936,7 +959,8 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             const DeflateJob job = make_job(s);
             if (slow) {
                 if (T.run(1, st, [&] { return launch_deflate_stage(0, job, nullptr, st); })) return zfail(__LINE__);
-                if (T.run(2, st, [&] { return launch_deflate_stage(1, job, nullptr, st); })) return zfail(__LINE__);
+                if (T.run(2, st, [&] { return launch_deflate_stage(lzp ? 17 : 1, job, nullptr, st); }))
+                    return zfail(__LINE__);
             }
             if (int rc = tail(s, job)) return rc;
         }
@@ -952,7 +976,8 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             if (T.run(1, st, [&] { return launch_deflate_stage(0, job, nullptr, st); })) return zfail(__LINE__);
             if (hipEventRecord(c.ev_links[s & 1], st) != hipSuccess) return zfail(__LINE__);
             if (hipStreamWaitEvent(ax, c.ev_links[s & 1], 0) != hipSuccess) return zfail(__LINE__);
-            if (T.run(2, ax, [&] { return launch_deflate_stage(1, job, nullptr, ax); })) return zfail(__LINE__);
+            if (T.run(2, ax, [&] { return launch_deflate_stage(lzp ? 17 : 1, job, nullptr, ax); }))
+                return zfail(__LINE__);
             if (hipEventRecord(c.ev_match[s & 1], ax) != hipSuccess) return zfail(__LINE__);
             return ZGPU_OK;
         };

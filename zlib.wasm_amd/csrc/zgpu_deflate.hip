@@ -698,15 +698,27 @@ __device__ __attribute__((always_inline)) inline void dwq_steps(DWQ &w, const ch
 // One position's longest_match with deferred compares.  Every lane of the
 // wave that took a position calls this together (the flushes are wave-wide
 // decisions taken with ballots).
+// Out receives the results: out.full(rec, exact) -- the walk's result with the
+// budget cfg.chain, exact = the walk ended before the budget (chain end, the
+// limit or nice), so a longer budget gives the same result -- and, with
+// want_q, out.quart(rec) after chain/4 candidates.
+struct MOutRQ {
+    uint32_t *rf, *rq;
+    int64_t p;
+    __device__ __attribute__((always_inline)) inline void full(uint32_t r, bool) const { rf[p] = r; }
+    __device__ __attribute__((always_inline)) inline void quart(uint32_t r) const { rq[p] = r; }
+    __device__ __attribute__((always_inline)) inline void steps(uint32_t) const {}
+};
+template <typename Out>
 __device__ __attribute__((always_inline)) inline void dwq_walk(const uint32_t *E, int64_t p, int64_t B, int64_t n,
-                                                               const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
+                                                               const LevelCfg &cfg, const Out &out,
                                                                int want_q, int64_t max_dist) {
     const int s = (int)(p - B);
     const uint32_t e0 = E[s];
     const uint32_t d0 = (e0 & 0xffffu) ? (uint32_t)s - (e0 & 0xffffu) : 0xffffu;
     if (d0 > (uint32_t)max_dist) {                 // deflate.c:1955: strstart - hash_head <= MAX_DIST
-        rf[p] = 0;
-        if (want_q) rq[p] = 0;
+        out.full(0u, true);
+        if (want_q) out.quart(0u);
         return;
     }
     const int64_t labs = p > max_dist ? p - max_dist : 0;
@@ -734,7 +746,7 @@ __device__ __attribute__((always_inline)) inline void dwq_walk(const uint32_t *E
             const int m4n = (int)((em & 0xffffu) << 2);
             if (best >= nice || m4n <= limit4 || count >= chain) walking = false;
             if (need_q && count == qc && walking) {
-                rq[p] = match_rec(best, s4, bpos4);
+                out.quart(match_rec(best, s4, bpos4));
                 need_q = false;
             }
             m4 = m4n;
@@ -742,8 +754,9 @@ __device__ __attribute__((always_inline)) inline void dwq_walk(const uint32_t *E
     }
     if (!walking) {
         const uint32_t r = match_rec(best, s4, bpos4);
-        if (need_q) rq[p] = r;
-        rf[p] = r;
+        if (need_q) out.quart(r);
+        out.steps(count);
+        out.full(r, best >= nice || m4 <= limit4);
         return;
     }
     const char *Eb = reinterpret_cast<const char *>(E);
@@ -804,7 +817,7 @@ __device__ __attribute__((always_inline)) inline void dwq_walk(const uint32_t *E
         w.occ = 0;
         const bool fin = !walking;
         if (need_q && (count >= qc || fin)) {          // deflate.c:1390-1392 (chain >>= 2)
-            rq[p] = match_rec(best, s4, bpos4);
+            out.quart(match_rec(best, s4, bpos4));
             need_q = false;
         }
         if (fin) break;
@@ -814,7 +827,8 @@ __device__ __attribute__((always_inline)) inline void dwq_walk(const uint32_t *E
             w.eb = *reinterpret_cast<const uint32_t *>(Eb + w.m4 + w.be4);
         }
     }
-    rf[p] = match_rec(best, s4, bpos4);
+    out.steps(count);
+    out.full(match_rec(best, s4, bpos4), best >= nice || w.m4 <= limit4);
 }
 
 
@@ -964,7 +978,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match(DeflateJob job, int wan
                 // a flush job's search at p sees the input up to the next flush
                 // position only (nice and the compare length are clamped to it)
                 const int64_t nl = kEv ? flush_limit(job, p, n) : n;
-                dwq_walk(E, p, B, nl, c, rf, rq, want_q, max_dist);
+                dwq_walk(E, p, B, nl, c, MOutRQ{rf, rq, p}, want_q, max_dist);
             }
         }
         __syncthreads();
@@ -1536,6 +1550,49 @@ struct SymBuf {
     }
 };
 
+// The block records of a segmented lazy parse (k_parse_seg, k_lzp): the cuts
+// left blk[b].in_end (strstart at the flush) and blk[b].pad (its decision
+// point) for b < ncut; block ncut is the last.  A block is stored-eligible
+// while its start has not slid out of the window: the slides before its flush
+// come from the closed-form schedule (slide_threshold).  Every cut field is
+// read before any record is written; all kT threads of the block call this.
+template <int kT>
+__device__ __attribute__((always_inline)) inline void seg_block_records(BlockRec *blk, uint32_t n, uint32_t total,
+                                                                        uint32_t ncut, const WinP &wp, int lane) {
+    const uint32_t symlim = wp.sym_limit;
+    uint32_t nthr = 0;
+    while (slide_threshold(nthr + 1, n, kMinLookahead - 1, wp) <= (int64_t)n) nthr++;
+    constexpr int kRecs = kT >= 1024 ? 2 : 8;
+    BlockRec r[kRecs];
+    for (uint32_t b0 = 0; b0 <= ncut; b0 += kT * kRecs) {
+#pragma unroll
+        for (int u = 0; u < kRecs; u++) {
+            const uint32_t b = b0 + (uint32_t)u * kT + (uint32_t)lane;
+            if (b > ncut) continue;
+            const bool last = b == ncut;
+            const uint64_t in_end = last ? n : blk[b].in_end;
+            const uint64_t pd = last ? n : blk[b].pad;
+            const uint64_t in_start = b == 0 ? 0 : blk[b - 1].in_end;
+            uint32_t slides = 0;
+            while (slides < nthr && slide_threshold(slides + 1, n, kMinLookahead - 1, wp) <= (int64_t)pd) slides++;
+            r[u].sym_start = b * symlim;
+            r[u].nsym = last ? total - b * symlim : symlim;
+            r[u].in_start = in_start;
+            r[u].in_end = in_end;
+            r[u].flags = (last ? 1u : 0u) | (in_start >= (uint64_t)wp.wsize * slides ? 2u : 0u);
+            r[u].pad = 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kRecs; u++) {
+            const uint32_t b = b0 + (uint32_t)u * kT + (uint32_t)lane;
+            if (b <= ncut) blk[b] = r[u];
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
     const WinP wp = job_win(job);
     const uint32_t symlim = wp.sym_limit;
@@ -1732,39 +1789,642 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
     __threadfence_block();
     __syncthreads();
 
-    // ---- block records (all cut fields read before any record is written)
-    uint32_t nthr = 0;
-    while (slide_threshold(nthr + 1, n, kMinLookahead - 1, wp) <= (int64_t)n) nthr++;
-    constexpr int kRecs = 8;
-    BlockRec r[kRecs];
-    for (uint32_t b0 = 0; b0 <= ncut; b0 += kParseLanes * kRecs) {
+    seg_block_records<kParseLanes>(blk, n, total, ncut, wp, lane);
+    if (lane == 0) job.nblocks[bi] = ncut + 1;
+}
+
+#ifdef ZGPU_LZP
+// ------------------------------------------------------------------------
+// k_lzp — levels 4..7 of a batch job: longest_match where deflate_slow asks
+// for it, and deflate_slow itself, in one kernel (round 6; an A/B build only:
+// make -C zlib.wasm_amd lzp -> libzgpu_lzp.so, ZGPU_LZP=1.  Exact, but 2.7x
+// slower than k_match + k_parse_seg on the bench's sub-batch: DESIGN.md 4.15).
+//
+// k_match walks every position's chain with the full budget, but the lazy
+// parse calls longest_match at about a quarter of the positions
+// (deflate.c:1955-1976) and takes the quartered budget where prev_length >=
+// good_match (:1390-1392).  tools/model/model_walks.c counts 76 chain steps
+// per position for the Silesia-style mix at level 6 against 11 at the parse's
+// call sites.  The sites depend on the results, so this kernel speculates and
+// verifies, tile by tile, with the window in LDS:
+//
+//   1. every position of a tile is walked with the quartered budget (its
+//      result Q(p)); a walk that ends before the budget (chain end, limit,
+//      nice) is exact for the full budget too (kZX);
+//   2. one wave parses the tile (deflate_slow's rules, slow_step) from the
+//      state the previous tile left, taking Q(p) as a guess where the full
+//      result F(p) is needed and unknown, and lists the guessed sites on the
+//      parse's path;
+//   3. the listed sites are walked with the full budget (F), and 2 repeats
+//      until the path uses no guess.  Then the tile's symbols and block cuts
+//      are written as k_parse_seg writes them.
+// The result is deflate_slow's parse exactly: the final path uses the exact
+// result at every decision, and a walk's result is a pure function of the
+// position and its budget.
+//
+// Step s of a workgroup (one buffer) stages tile s and runs two things side
+// by side: the walker waves take the quarter walks of tile s, and the parser
+// wave (wave 15) runs the rounds of tile s-1, whose full walks the walkers
+// take first whenever some are posted (the parser takes them too while it
+// waits).  The window therefore covers tile s-1's history and both tiles:
+// words [0, kZH) before tile s-1, tile s-1, tile s and the compare pad.
+//
+// The parse of a tile (2048 positions) is k_parse_seg's segmented parse on
+// one wave: lane i parses positions [a + 32 i, a + 32 i + 32) from the simple
+// state (lane 0 from the carried state), records the simple states it stands
+// in (2 bits per position), then runs on until it stands in a state a later
+// lane recorded; the stitched path follows those meets from lane 0.
+// ------------------------------------------------------------------------
+constexpr int kZT = 2048;                       // positions per tile
+constexpr int kZH = 32512;                      // window words before the parse tile (>= MAX_DIST, 16-aligned)
+constexpr int kZE = kZH + 2 * kZT + kMPad;      // 36880 words = 144.1 KiB
+constexpr int kZThreads = 1024;
+constexpr int kZParser = kZThreads / 64 - 1;    // the parser wave
+constexpr int kZSeg = kZT / 64;                 // parse positions per lane
+constexpr int kZReq = 512;                      // full-walk request ring (tile offsets)
+constexpr uint32_t kZF = 1u << 30;              // ZQ word: the full-budget result
+constexpr uint32_t kZX = 1u << 31;              // quarter walk ended before its budget: full = quarter
+constexpr uint32_t kZEnd = 0xffffffffu;
+static_assert(kZSeg == 32, "two 16-position state words per lane");
+static_assert(kZT / 2 == kZThreads, "tile staging: 2 words per thread");
+static_assert(kMPad / 4 <= kZThreads && kZH % 16 == 0, "pad staging");
+
+#ifdef ZGPU_LZP_STATS
+// statistics build only (tools/lzp_stats.py): [0] tiles parsed, [1] rounds,
+// [2] full walks requested, [3] quarter walks, [4] quarter steps, [5] full
+// walks, [6] full steps, [7] requests dropped (ring full), [8..15] rounds
+// per tile histogram (1..7, 8+); parser clock (s_memtime) in [16] passes 1-2,
+// [17] stitch + replay, [18] waiting for its full walks, [19] symbols, [20]
+// whole tile; [21] clock of a step (wave 0), [22] walker waves' idle polls,
+// [23] speculative full walks
+__device__ unsigned long long g_zstat[32];
+#define ZSTAT(i, v) atomicAdd(&g_zstat[i], (unsigned long long)(v))
+#define ZCLK() __builtin_amdgcn_s_memtime()
+extern "C" int zgpu_lzp_stats_read(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_zstat), sizeof(g_zstat)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[32] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_zstat), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#else
+#define ZCLK() 0ull
+#endif
+
+// what thread t stages for a tile: words 2t, 2t+1 (bytes, links), the walk
+// keys of positions ts + t and ts + t + 1024, and for t < kMPad/4 four pad words
+struct ZPre {
+    uint32_t b[2], pb[4], lk[2], key[2];
+};
+__device__ __attribute__((always_inline)) inline void zpre_load(ZPre &P, int64_t ts, int64_t n, const uint8_t *in,
+                                                                const uint16_t *L, const uint8_t *K, int tid) {
+    const int64_t q0 = ts + 2 * tid;
+    const uint32_t x0 = ldb(in, q0, n), x1 = ldb(in, q0 + 1, n), x2 = ldb(in, q0 + 2, n);
+    P.b[0] = x0 | x1 << 8;
+    P.b[1] = x1 | x2 << 8;
+    if (tid < kMPad / 4) {
+        const int64_t q1 = ts + kZT + 4 * tid;
+        uint32_t x[5];
 #pragma unroll
-        for (int u = 0; u < kRecs; u++) {
-            const uint32_t b = b0 + (uint32_t)u * kParseLanes + (uint32_t)lane;
-            if (b > ncut) continue;
-            const bool last = b == ncut;
-            const uint64_t in_end = last ? n : blk[b].in_end;
-            const uint64_t pd = last ? n : blk[b].pad;
-            const uint64_t in_start = b == 0 ? 0 : blk[b - 1].in_end;
-            uint32_t slides = 0;
-            while (slides < nthr && slide_threshold(slides + 1, n, kMinLookahead - 1, wp) <= (int64_t)pd) slides++;
-            r[u].sym_start = b * symlim;
-            r[u].nsym = last ? total - b * symlim : symlim;
-            r[u].in_start = in_start;
-            r[u].in_end = in_end;
-            r[u].flags = (last ? 1u : 0u) | (in_start >= (uint64_t)wp.wsize * slides ? 2u : 0u);
-            r[u].pad = 0;
+        for (int u = 0; u < 5; u++) x[u] = ldb(in, q1 + u, n);
+#pragma unroll
+        for (int u = 0; u < 4; u++) P.pb[u] = x[u] | x[u + 1] << 8;
+    }
+    if (q0 + 2 <= n) {
+        const uint32_t v = *reinterpret_cast<const uint32_t *>(L + q0);   // 4-B aligned: ws_off % 64 == 0
+        P.lk[0] = v & 0xffffu;
+        P.lk[1] = v >> 16;
+    } else {
+        P.lk[0] = q0 < n ? (uint32_t)L[q0] : 0u;
+        P.lk[1] = 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+        const int64_t q = ts + tid + u * kZThreads;
+        P.key[u] = q < n ? (uint32_t)K[q] : 0u;
+    }
+}
+// the new tile goes to words [kZH + kZT, kZH + 2 kZT) and its pad after it;
+// the low half of a word is the LDS word index of the position's predecessor
+// (0: none), as in k_match (tile_store<true>)
+__device__ __attribute__((always_inline)) inline void zpre_store(uint32_t *E, const ZPre &P, int tid) {
+    const int w0 = kZH + kZT + 2 * tid;
+    uint2 v;
+    v.x = P.b[0] << 16 | (P.lk[0] ? ((uint32_t)w0 - P.lk[0]) & 0xffffu : 0u);
+    v.y = P.b[1] << 16 | (P.lk[1] ? ((uint32_t)(w0 + 1) - P.lk[1]) & 0xffffu : 0u);
+    *reinterpret_cast<uint2 *>(E + w0) = v;
+    if (tid < kMPad / 4)
+        *reinterpret_cast<uint4 *>(E + kZH + 2 * kZT + 4 * tid) =
+            make_uint4(P.pb[0] << 16, P.pb[1] << 16, P.pb[2] << 16, P.pb[3] << 16);
+}
+// window slide by kZT words: thread t moves the 2-word chunks t + 1024 k in
+// increasing k; the chunk it reads (c + kZT/2 = c + 1024) is the one it writes
+// next, so no chunk is overwritten before it is read.  Predecessor indexes
+// drop by kZT, saturating at 0 (older than the window: beyond every limit).
+__device__ __attribute__((always_inline)) inline void zslide(uint32_t *E, int tid) {
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const us2 d = {(unsigned short)kZT, (unsigned short)0};
+    auto sl = [&](uint32_t w) {
+        return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(us2, w), d));
+    };
+    uint2 *dE = reinterpret_cast<uint2 *>(E);
+    constexpr int kChunks = (kZH + kZT) / 2;
+    static_assert(kZT / 2 == kZThreads, "self-contained slide chains");
+    for (int c = tid; c < kChunks; c += kZThreads) {
+        const uint2 v = dE[c + kZT / 2];
+        dE[c] = make_uint2(sl(v.x), sl(v.y));
+    }
+}
+
+// walk outputs: the quarter walk's result (global, with the exact flag), a
+// full walk's result (LDS, over the parse tile's quarter word)
+// (statistics build: `c` receives the walk's step count)
+struct ZOutQ {
+    uint32_t *dst;
+    mutable uint32_t c = 0;
+    __device__ __attribute__((always_inline)) inline void full(uint32_t r, bool exact) const {
+        *dst = r | (exact ? kZX : 0u);
+    }
+    __device__ __attribute__((always_inline)) inline void quart(uint32_t) const {}
+    __device__ __attribute__((always_inline)) inline void steps(uint32_t k) const { c = k; }
+};
+struct ZOutF {
+    uint32_t *dst;
+    mutable uint32_t c = 0;
+    __device__ __attribute__((always_inline)) inline void full(uint32_t r, bool) const { *dst = r | kZF; }
+    __device__ __attribute__((always_inline)) inline void quart(uint32_t) const {}
+    __device__ __attribute__((always_inline)) inline void steps(uint32_t k) const { c = k; }
+};
+
+struct ZLane {
+    uint32_t p, ml, ms, av;
+};
+// one deflate_slow decision (deflate.c:1946-2027), as slow_step, on the parse
+// tile's results: ZQ[p - a] holds Q(p) (bit kZX: = F(p)) or, once walked,
+// F(p) (bit kZF; Q(p) is then still in the global rq[p]).  A decision that
+// needs F(p) while only the inexact Q(p) is known takes Q(p) and sets guess.
+// Returns 0 (no symbol), 1 (literal at spos), 2 (match at spos, slen); kSym:
+// also the symbol (only the emission needs it: no byte read in the passes).
+// The step is one LDS read and selects: the parse wave's loops are a chain of
+// dependent steps, so its latency, not its issue count, is what costs.
+template <bool kSym>
+__device__ __attribute__((always_inline)) inline uint32_t zstep(ZLane &L, uint32_t n, const uint32_t *ZQ, uint32_t a,
+                                                                const uint32_t *rqg, const uint32_t *E, int64_t B,
+                                                                const LevelCfg &cfg, bool use_q, bool filtered,
+                                                                bool &guess, uint32_t &sym, uint32_t &spos,
+                                                                uint32_t &slen) {
+    const uint32_t p = L.p, pl = L.ml, pm = L.ms;
+    const bool srch = (n - p >= (uint32_t)kMinMatch) & (pl < cfg.lazy);
+    const bool wantq = use_q & (pl >= cfg.good);
+    uint32_t w = ZQ[p - a];
+    if (srch & wantq & ((w & kZF) != 0u)) w = rqg[p];        // the quarter result, under a full one (rare)
+    guess = srch & !wantq & ((w & (kZF | kZX)) == 0u);
+    const uint32_t rl = srch ? (w >> 16) & 0x1ffu : 0u;
+    const bool better = rl > pl;
+    uint32_t ml = better ? rl : (uint32_t)kMinMatch - 1;
+    const uint32_t ms = better ? p - (w & 0xffffu) : pm;
+    const bool drop = (ml <= 5u) & (filtered | ((ml == (uint32_t)kMinMatch) & (p - ms > (uint32_t)kTooFar)));
+    ml = drop ? (uint32_t)kMinMatch - 1 : ml;                  // deflate.c:1964-1975
+    const bool emit = (pl >= (uint32_t)kMinMatch) & (ml <= pl);
+    if (kSym) {
+        sym = emit ? ((p - 1 - pm) << 8) | (pl - kMinMatch) : (E[(int64_t)p - 1 - B] >> 16) & 0xffu;
+        spos = p - 1;
+        slen = emit ? pl : 1u;
+    }
+    const uint32_t code = emit ? 2u : L.av;
+    L.p = emit ? p + pl - 1 : p + 1;
+    L.ms = ms;
+    L.ml = emit ? (uint32_t)kMinMatch - 1 : ml;
+    L.av = emit ? 0u : 1u;
+    return code;
+}
+
+__device__ __attribute__((always_inline)) inline uint32_t lds_ld(const uint32_t *a) {
+    return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__global__ __launch_bounds__(kZThreads) void k_lzp(DeflateJob job) {
+    constexpr int kSortBuckets = 64;
+    __shared__ __attribute__((aligned(16))) uint32_t E[kZE];
+    __shared__ __attribute__((aligned(16))) uint32_t ZQ[kZT];
+    __shared__ uint16_t perm[kZT];
+    __shared__ uint32_t rec[kZT / 16];
+    __shared__ uint16_t req[kZReq];
+    __shared__ uint32_t zst[64];
+    __shared__ int s_hist[kSortBuckets], s_base[kSortBuckets];
+    __shared__ uint32_t sdone[kZT / 32];          // speculative full walks done (results in job.rfull)
+    __shared__ uint32_t c_qnext, c_rhead, c_rtail, c_rdone, c_pdone, c_post, c_total, c_final, c_snext;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint32_t bi = blockIdx.x;
+    const uint32_t g = job.first + bi;
+    const uint32_t n = (uint32_t)job.src_len[g];
+    const uint8_t *in = job.src + job.src_off[g];
+    const uint16_t *Lk = job.link + job.ws_off[bi];
+    const uint8_t *K = job.key + job.ws_off[bi];
+    uint32_t *rqg = job.rquart + job.ws_off[bi];
+    uint32_t *sym = job.sym + job.ws_off[bi];
+    BlockRec *blk = job.blocks + job.blk_off[bi];
+    const LevelCfg cfg = job.cfg;
+    LevelCfg cfgq = cfg;
+    cfgq.chain = cfg.chain >> 2 ? cfg.chain >> 2 : 1u;
+    const WinP wp = job_win(job);
+    const int64_t max_dist = wp.max_dist;
+    const uint32_t symlim = wp.sym_limit;
+    const bool use_q = cfg.good < cfg.lazy;
+    const bool filtered = job.strategy == 1;
+    // the sort key of a quarter walk: k_count's candidate count, capped at the budget
+    const uint32_t kcap = walk_key(cfgq.chain, cfg.chain);
+    const uint32_t S = (n + kZT - 1) / kZT;
+
+    // the parser wave's carried state (uniform): where the parse stands at the
+    // start of the next tile, the symbols written so far
+    uint32_t cp = 0, cml = kMinMatch - 1, cms = 0, cav = 0, symbase = 0, sfinal = 0;
+
+    ZPre P;
+    zpre_load(P, 0, n, in, Lk, K, tid);
+    const bool prio = job.lzp_flags & 1;
+    const bool spec = (job.lzp_flags & 2) && job.rfull;
+    uint32_t *rfs = job.rfull ? job.rfull + job.ws_off[bi] : nullptr;
+#ifdef ZGPU_LZP_STATS
+    unsigned long long st_qw = 0, st_qs = 0, st_fw = 0, st_fs = 0, st_idle = 0, st_sw = 0;
+#endif
+    for (uint32_t s = 0; s <= S; s++) {
+        const uint64_t t_step = ZCLK();
+        const int64_t ts = (int64_t)s * kZT;                 // tile s (quarter walks)
+        const int64_t B = ts - kZT - kZH;                    // word w <-> position B + w
+        const int tile_n = s < S ? (int)((int64_t)n - ts < kZT ? (int64_t)n - ts : kZT) : 0;
+        const uint32_t a = s ? (s - 1) * kZT : 0u;          // tile s-1 (parse) [a, b)
+        const uint32_t b = s ? (a + kZT < n ? a + kZT : n) : 0u;
+        // ---- staging
+        if (s == 0) {
+            for (int i = tid; i < kZH + kZT; i += kZThreads) E[i] = 0;
+        } else {
+            zslide(E, tid);
+            __syncthreads();
+        }
+        if (tile_n) zpre_store(E, P, tid);
+        if (s) {                                            // tile s-1's quarter results
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const uint32_t i = (uint32_t)tid + (uint32_t)u * kZThreads;
+                ZQ[i] = a + i < n ? rqg[a + i] : 0u;
+            }
+        }
+        if (tid < kSortBuckets) s_hist[tid] = 0;
+        if (tid < kZT / 32) sdone[tid] = 0;
+        if (tid == 0) {
+            c_qnext = 0;
+            c_rhead = c_rtail = c_rdone = 0;
+            c_pdone = s ? 0u : 1u;
+            c_snext = 0;
+        }
+        __syncthreads();
+        int bk[2], rk[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int i = tid + u * kZThreads;
+            const uint32_t k = P.key[u] < kcap ? P.key[u] : kcap;
+            bk[u] = kSortBuckets - 1 - (i < tile_n ? (int)(k >> 2) : 0);
+            if (bk[u] < 0) bk[u] = 0;
+            rk[u] = i < tile_n ? atomicAdd(&s_hist[bk[u]], 1) : 0;
+        }
+        __syncthreads();
+        if (tid < 64) {
+            const int v = s_hist[tid];
+            int incl = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(incl, o, 64);
+                if (tid >= o) incl += t;
+            }
+            s_base[tid] = incl - v;
         }
         __syncthreads();
 #pragma unroll
-        for (int u = 0; u < kRecs; u++) {
-            const uint32_t b = b0 + (uint32_t)u * kParseLanes + (uint32_t)lane;
-            if (b <= ncut) blk[b] = r[u];
+        for (int u = 0; u < 2; u++)
+            if (tid + u * kZThreads < tile_n) perm[s_base[bk[u]] + rk[u]] = (uint16_t)(tid + u * kZThreads);
+        __syncthreads();
+        if (s + 1 < S) zpre_load(P, ts + kZT, n, in, Lk, K, tid);     // lands during the walks
+
+        // ---- full walks posted by the parser (tile s-1 offsets), wave-wide
+        // claims of up to 64; returns false when none were pending
+        auto ext_walks = [&](int pr) -> bool {
+            const uint32_t h = ufl(lds_ld(&c_rhead)), t = ufl(lds_ld(&c_rtail));
+            if (h >= t) return false;
+            const uint32_t take = t - h < 64u ? t - h : 64u;
+            uint32_t got = 0;
+            if (lane == 0) got = atomicCAS(&c_rhead, h, h + take) == h;
+            if (!ufl(got)) return true;                      // lost the claim: look again
+            if (prio) __builtin_amdgcn_s_setprio(2);
+            if ((uint32_t)lane < take) {
+                const uint32_t off = req[(h + (uint32_t)lane) % kZReq];
+                const ZOutF o{ZQ + off};
+                dwq_walk(E, (int64_t)a + off, B, n, cfg, o, 0, max_dist);
+#ifdef ZGPU_LZP_STATS
+                st_fw++;
+                st_fs += o.c;
+#endif
+            }
+            if (prio) {
+                if (pr == 3) __builtin_amdgcn_s_setprio(3);
+                else __builtin_amdgcn_s_setprio(0);
+            }
+            __threadfence_block();
+            if (lane == 0) atomicAdd(&c_rdone, take);
+            return true;
+        };
+
+        // ---- the parser wave: rounds over tile s-1, then its symbols
+        if (wave == kZParser && s) {
+            if (prio) __builtin_amdgcn_s_setprio(3);
+            uint64_t t0 = ZCLK(), t_p12 = 0, t_rep = 0, t_wait = 0;
+            const uint32_t x0 = a + (uint32_t)kZSeg * (uint32_t)lane;
+            const uint32_t x1 = x0 + kZSeg < b ? x0 + kZSeg : b;
+            const bool act = x0 < b;
+            const bool tail_tile = b == n;
+            bool gs;
+            uint32_t sv, sp, sl;
+            auto init = [&](ZLane &L) {
+                if (lane == 0) L = ZLane{cp, cml, cms, cav};
+                else L = ZLane{x0, kMinMatch - 1, 0, 0};
+            };
+            auto step = [&](ZLane &L) {
+                return zstep<false>(L, n, ZQ, a, rqg, E, B, cfg, use_q, filtered, gs, sv, sp, sl);
+            };
+            auto step_sym = [&](ZLane &L) {
+                return zstep<true>(L, n, ZQ, a, rqg, E, B, cfg, use_q, filtered, gs, sv, sp, sl);
+            };
+            uint32_t rounds = 0, last = 0, st_p = 0, en = 0, cnt = 0;
+            uint32_t merged = 0;                  // this lane's 32 positions: speculative results taken
+            (void)rounds;
+            bool on = false;
+            for (;;) {
+                rounds++;
+                uint64_t t1 = ZCLK();
+                if (spec) {                       // take the speculative full walks done so far
+                    uint32_t m = lds_ld(&sdone[lane]) & ~merged;
+                    merged |= m;
+                    while (m) {
+                        const uint32_t j = (uint32_t)__builtin_ctz(m);
+                        m &= m - 1;
+                        const uint32_t o = (uint32_t)kZSeg * (uint32_t)lane + j;
+                        if (!(ZQ[o] & kZF)) ZQ[o] = rfs[a + o] | kZF;
+                    }
+                    __threadfence_block();
+                }
+                // pass 1: the own segment, recording the simple states
+                ZLane L;
+                init(L);
+                if (act) {
+                    uint32_t r0 = 0, r1 = 0;
+                    while (L.p < x1) {
+                        const uint32_t o = L.p - x0;
+                        const uint32_t bit = L.ml < (uint32_t)kMinMatch ? 1u << (2 * (o & 15u) + L.av) : 0u;
+                        r0 |= o < 16 ? bit : 0u;
+                        r1 |= o < 16 ? 0u : bit;
+                        step(L);
+                    }
+                    rec[(x0 - a) >> 4] = r0;
+                    rec[((x0 - a) >> 4) + 1] = r1;
+                }
+                __threadfence_block();
+                __builtin_amdgcn_wave_barrier();
+                // pass 2: run on until a later lane's recorded state
+                uint32_t y = kZEnd, tgt = 0, sig = 0;
+                if (act) {
+                    while (L.p < b) {
+                        if (L.p >= x1 && L.ml < (uint32_t)kMinMatch) {
+                            const uint32_t o = L.p - a;
+                            if ((rec[o >> 4] >> (2 * (o & 15u) + L.av)) & 1u) {
+                                y = L.p;
+                                sig = L.av;
+                                tgt = o / kZSeg;
+                                break;
+                            }
+                        }
+                        step(L);
+                    }
+                }
+                {
+                    const uint64_t t2 = ZCLK();
+                    t_p12 += t2 - t1;
+                    t1 = t2;
+                }
+                // stitch: lane 0, then each meet's lane, until a lane reaches b
+                uint32_t cur = 0;
+                uint64_t mask = 0;
+                for (;;) {
+                    mask |= 1ull << cur;
+                    const uint32_t yv = (uint32_t)__builtin_amdgcn_readlane((int)y, (int)cur);
+                    if (yv == kZEnd) break;
+                    const uint32_t j = (uint32_t)__builtin_amdgcn_readlane((int)tgt, (int)cur);
+                    const uint32_t sg = (uint32_t)__builtin_amdgcn_readlane((int)sig, (int)cur);
+                    if (lane == 0) zst[j] = (yv - a) | sg << 16;
+                    cur = j;
+                }
+                last = cur;
+                if (lane == 0) c_post = 0;
+                __threadfence_block();
+                __builtin_amdgcn_wave_barrier();
+                on = (mask >> lane) & 1ull;
+                st_p = lane == 0 ? cp : a + (zst[lane] & 0xffffu);
+                en = (uint32_t)lane == last ? b : y;
+                // replay the path: count the symbols, list the guessed sites
+                const uint32_t tail0 = ufl(lds_ld(&c_rtail));
+                cnt = 0;
+                uint32_t ng = 0;
+                if (on) {
+                    init(L);
+                    while (L.p < en) {
+                        const uint32_t p0 = L.p;
+                        const uint32_t k = step(L);
+                        if (p0 >= st_p) {
+                            cnt += k != 0;
+                            if (gs) {
+                                ng++;
+                                const uint32_t i = atomicAdd(&c_post, 1u);
+                                if (i < (uint32_t)kZReq) req[(tail0 + i) % kZReq] = (uint16_t)(p0 - a);
+                            }
+                        }
+                    }
+                }
+                uint32_t tot = ng;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) tot += __shfl_xor(tot, o, 64);
+                tot = ufl(tot);
+                {
+                    const uint64_t t2 = ZCLK();
+                    t_rep += t2 - t1;
+                    t1 = t2;
+                }
+                if (tot == 0) break;
+                const uint32_t posted = tot < (uint32_t)kZReq ? tot : (uint32_t)kZReq;
+#ifdef ZGPU_LZP_STATS
+                if (lane == 0) {
+                    ZSTAT(2, posted);
+                    ZSTAT(7, tot - posted);
+                }
+#endif
+                __threadfence_block();
+                if (lane == 0) __hip_atomic_store(&c_rtail, tail0 + posted, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                // take full walks until this round's are done
+                for (;;) {
+                    if (ext_walks(3)) continue;
+                    if (ufl(lds_ld(&c_rdone)) >= tail0 + posted) break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                __threadfence_block();
+                t_wait += ZCLK() - t1;
+            }
+            const uint64_t t_emit = ZCLK();
+#ifdef ZGPU_LZP_STATS
+            if (lane == 0) {
+                ZSTAT(0, 1);
+                ZSTAT(1, rounds);
+                ZSTAT(8 + (rounds > 8 ? 7 : rounds - 1), 1);
+            }
+#endif
+            // the symbols: lane i's on the path from st_p to en, in path order
+            uint32_t incl = cnt;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += t;
+            }
+            uint32_t gi = symbase + incl - cnt;
+            ZLane L;
+            init(L);
+            if (on) {
+                while (L.p < en) {
+                    const uint32_t p0 = L.p;
+                    const uint32_t k = step_sym(L);
+                    if (p0 >= st_p && k) {
+                        sym[gi] = sv;
+                        if ((gi + 1) % symlim == 0) {                 // the flush at this symbol (deflate.h:371)
+                            const uint32_t bx = (gi + 1) / symlim - 1;
+                            blk[bx].in_end = (uint64_t)(sp + sl);
+                            blk[bx].pad = sp + 1;                     // its decision point
+                        }
+                        gi++;
+                    }
+                }
+            }
+            uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            const uint32_t np = (uint32_t)__builtin_amdgcn_readlane((int)L.p, (int)last);
+            const uint32_t nml = (uint32_t)__builtin_amdgcn_readlane((int)L.ml, (int)last);
+            const uint32_t nms = (uint32_t)__builtin_amdgcn_readlane((int)L.ms, (int)last);
+            const uint32_t nav = (uint32_t)__builtin_amdgcn_readlane((int)L.av, (int)last);
+            if (tail_tile && nav) {                 // the pending literal at the end, tallied without a flush test
+                if ((uint32_t)lane == last) sym[gi] = (E[(int64_t)n - 1 - B] >> 16) & 0xffu;
+                total++;
+                sfinal = 1;
+            }
+            cp = np; cml = nml; cms = nms; cav = nav;
+            symbase += total;
+            __threadfence_block();
+            if (lane == 0) __hip_atomic_store(&c_pdone, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (prio) __builtin_amdgcn_s_setprio(0);
+#ifdef ZGPU_LZP_STATS
+            if (lane == 0) {
+                const uint64_t t3 = ZCLK();
+                ZSTAT(16, t_p12);
+                ZSTAT(17, t_rep);
+                ZSTAT(18, t_wait);
+                ZSTAT(19, t3 - t_emit);
+                ZSTAT(20, t3 - t0);
+            }
+#else
+            (void)t0; (void)t_p12; (void)t_rep; (void)t_wait; (void)t_emit;
+#endif
+        }
+
+        // ---- walkers (and the parser once its tile is done)
+        for (;;) {
+            if (ext_walks(0)) continue;
+            if (ufl(lds_ld(&c_qnext)) < (uint32_t)tile_n) {
+                uint32_t i0 = 0;
+                if (lane == 0) i0 = atomicAdd(&c_qnext, 64u);
+                i0 = ufl(i0);
+                const uint32_t i = i0 + (uint32_t)lane;
+                if (i < (uint32_t)tile_n) {
+                    const int64_t p = ts + perm[i];
+                    const ZOutQ o{rqg + p};
+                    dwq_walk(E, p, B, n, cfgq, o, 0, max_dist);
+#ifdef ZGPU_LZP_STATS
+                    st_qw++;
+                    st_qs += o.c;
+#endif
+                }
+                continue;
+            }
+            if (ufl(lds_ld(&c_pdone))) break;
+            // idle while the parser works: full walks of the parse tile's inexact
+            // positions (results in rfs, taken by the parser at its next round)
+            if (spec && s && ufl(lds_ld(&c_snext)) < b - a) {
+                uint32_t o0 = 0;
+                if (lane == 0) o0 = atomicAdd(&c_snext, 64u);
+                const uint32_t o = ufl(o0) + (uint32_t)lane;
+                if (o < b - a && !(ZQ[o] & (kZF | kZX))) {
+                    const ZOutQ so{rfs + a + o};
+                    dwq_walk(E, (int64_t)a + o, B, n, cfg, so, 0, max_dist);
+                    __threadfence_block();
+                    atomicOr(&sdone[o >> 5], 1u << (o & 31u));
+#ifdef ZGPU_LZP_STATS
+                    st_sw++;
+#endif
+                }
+                continue;
+            }
+#ifdef ZGPU_LZP_STATS
+            st_idle++;
+#endif
+            __builtin_amdgcn_s_sleep(2);
         }
         __threadfence_block();
         __syncthreads();
+#ifdef ZGPU_LZP_STATS
+        if (tid == 0) ZSTAT(21, ZCLK() - t_step);
+#else
+        (void)t_step;
+#endif
     }
-    if (lane == 0) job.nblocks[bi] = ncut + 1;
+#ifdef ZGPU_LZP_STATS
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        st_qw += __shfl_xor(st_qw, o, 64);
+        st_qs += __shfl_xor(st_qs, o, 64);
+        st_fw += __shfl_xor(st_fw, o, 64);
+        st_fs += __shfl_xor(st_fs, o, 64);
+        st_sw += __shfl_xor(st_sw, o, 64);
+    }
+    if (lane == 0) {
+        ZSTAT(3, st_qw);
+        ZSTAT(4, st_qs);
+        ZSTAT(5, st_fw);
+        ZSTAT(6, st_fs);
+        ZSTAT(22, st_idle);
+        ZSTAT(23, st_sw);
+    }
+#endif
+    if (wave == kZParser && lane == 0) {
+        c_total = symbase;
+        c_final = sfinal;
+    }
+    __syncthreads();
+    const uint32_t total = c_total;
+    const uint32_t ncut = total / symlim - ((c_final && total % symlim == 0) ? 1u : 0u);
+    seg_block_records<kZThreads>(blk, n, total, ncut, wp, tid);
+    if (tid == 0) job.nblocks[bi] = ncut + 1;
+}
+
+#endif  // ZGPU_LZP
+int lzp_built() {
+#ifdef ZGPU_LZP
+    return 1;
+#else
+    return 0;
+#endif
 }
 
 // ------------------------------------------------------------------------
@@ -5105,6 +5765,9 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         else hipLaunchKernelGGL(k_match2<false>, grid, dim3(kM2Threads), 0, st, job, wq);
         break;
     }
+#ifdef ZGPU_LZP
+    case 17: hipLaunchKernelGGL(k_lzp, grid, dim3(kZThreads), 0, st, job); break;   // match + lazy parse (k_lzp)
+#endif
     case 7: hipLaunchKernelGGL(k_parse_huff, grid, dim3(kHuffThreads), 0, st, job); break;
     case 8: hipLaunchKernelGGL(k_parse_rle, grid, dim3(64), 0, st, job); break;
     case 9: hipLaunchKernelGGL(k_count<false>, grid, dim3(kCntThreads), 0, st, job); break;

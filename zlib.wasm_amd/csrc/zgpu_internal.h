@@ -19,6 +19,8 @@ constexpr int kSymLimit = 16383;                            // lit_bufsize - 1
 // (few large buffers) must start every segment on a tile boundary, so the
 // host's segment sizes are whole multiples of it.
 constexpr uint32_t kMatchTile = 4096;
+// k_lzp (match + lazy parse in one kernel) serves batch jobs whose chain budget is at most this (levels 4..7)
+constexpr uint32_t kLzpMaxChain = 256;
 // k_links keeps head[] in the key[] region (32 Ki x 4 B) for buffers this long
 constexpr uint64_t kLinksGhMin = 131072;
 // Buffers are addressed with 32-bit positions inside the kernels: deflate
@@ -302,6 +304,7 @@ struct DeflateJob {
     uint16_t *srt;
     uint16_t *boff;
     uint4 *work;
+    int lzp_flags;           // k_lzp A/B switches (ZGPU_LZP_FLAGS): bit 0 the parser wave at raised priority
 };
 // k_bsort's block (positions) and the stride of its per-block hash table
 constexpr int kSortBlock = 16384;
@@ -432,6 +435,8 @@ size_t checksum_scratch_bytes(uint32_t count);
 int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipStream_t st);
 // k_parse_seg's fallback counters (zgpu_debug_parse_fallbacks): out[0..1]
 int parse_fallback_counts(uint64_t *out);
+// 1 when k_lzp is compiled in (the A/B build, -DZGPU_LZP)
+int lzp_built();
 // a18 helpers (zgpu_helpers.hip)
 int launch_slide_hash(uint16_t *head, uint16_t *prev, uint32_t hash_size, uint32_t window_size, uint32_t wsize,
                       hipStream_t st);
