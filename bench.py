@@ -103,6 +103,8 @@ def parse(argv=None):
                     help="input bytes per deflate sub-batch (workspace ~15 B per byte)")
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="test mode: gloo + oracle instead of the GPU legs (launcher/reduction check)")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="print each rank's HBM / host memory plan for these arguments and exit (no compute)")
     return ap.parse_args(argv)
 
 
@@ -339,11 +341,12 @@ def inflate_leg(a, D, d):
 
 
 def dry_deflate_leg(a, D):
-    """--cpu-dry-run: the oracle compresses this rank's shard of small host
-    buffers (same global-index sharding), so the launcher and the collectives
-    run for real without a GPU."""
+    """--cpu-dry-run: the oracle compresses this rank's shard of host buffers
+    made by the device generator's host twin (oracle/zgen.c: same kind, seed
+    and global indices as the GPU leg), so the launcher, the sharding and the
+    collectives run for real without a GPU, and the per-rank digests can be
+    compared with the compiled reference's (tests/golden/bench_shard_golden_small.json)."""
     import zlib as _z
-    import datagen
     from zhelpers import Oracle
     o = Oracle()
     first, last = shard(D.rank, D.world, a.buffers)
@@ -352,13 +355,85 @@ def dry_deflate_leg(a, D):
     for _ in range(a.steps):
         in_b = out_b = digest = 0
         for g in range(first, last):
-            data = datagen.mix(a.buffer_bytes, g)
+            data = o.generate(a.buffer_bytes, 1, KIND_ID[a.kind], 2025, g)[0]
             z = o.compress(data, a.level)[1]
             in_b += len(data)
             out_b += len(z)
             digest ^= _z.crc32(z)
     return dict(elapsed=time.perf_counter() - t0, in_bytes=in_b, out_bytes=out_b, errors=0,
                 digest=digest, stages={})
+
+
+def dry_digest_check(a, digests):
+    """--cpu-dry-run: every rank's digest against the compiled reference's for
+    the same configuration (tests/golden/make_bench_shard_golden_small.py), if
+    there is one.  Returns (ranks checked, note)."""
+    try:
+        doc = json.load(open(os.path.join(ROOT, "tests", "golden", "bench_shard_golden_small.json")))
+    except OSError:
+        return 0, "no tests/golden/bench_shard_golden_small.json"
+    if (a.kind, a.buffer_bytes, a.buffers, a.level) != (doc["kind"], doc["buffer_bytes"], doc["buffers_per_rank"],
+                                                         doc["level"]):
+        return 0, "no small golden for this configuration"
+    n = 0
+    for r, (dg, ob) in enumerate(digests):
+        want = doc["ranks"].get(str(r))
+        if want is None:
+            continue
+        got = {"out_bytes": int(ob), "stream_crc_xor": "%08x" % (int(dg) & 0xffffffff)}
+        assert got == want, f"rank {r}: dry-run digest {got} != reference {want}"
+        n += 1
+    return n, f"reference {doc.get('reference')}"
+
+
+# Device memory of one rank (bytes), from the library's allocations (DESIGN.md
+# 3): the L4-9 pipelined deflate keeps, per in-flight input byte, link 2 + key
+# 1 + rfull 4 + rquart 4 + pstate 1/4 in two slots and sym 4 + stage 4 in one
+# (30.5 B), every workspace allocated with 1/8 slack (zgpu_api.cpp DevBuf);
+# the inflate leg adds its output and ~2.7 B of match records per in-flight
+# output byte; the checksum legs their inputs.  Workspaces are kept for the
+# context's life, so the legs add up.
+WS_PER_INFLIGHT_BYTE = 30.5 * 1.125
+INFL_WS_PER_INFLIGHT_BYTE = 2.7 * 1.125
+HBM_BYTES_MI355X = 288e9
+
+
+def memory_plan(a, world):
+    n, B = a.buffer_bytes, a.buffers
+    cap = (n + (n >> 12) + (n >> 14) + (n >> 25) + 13 + 15) // 16 * 16       # compressBound, 16-B rounded
+    inflight = min(a.inflight_mb << 20, n * B) if a.level >= 4 else min(4 * (a.inflight_mb << 20), n * B)
+    ws = WS_PER_INFLIGHT_BYTE * inflight if a.level >= 4 else 6.0 * 1.125 * inflight
+    legs = {
+        "deflate_inputs": n * B,
+        "deflate_outputs": cap * B,
+        "deflate_workspace": int(ws),
+        "inflate_outputs": 0 if a.no_inflate else n * B,
+        "inflate_workspace": 0 if a.no_inflate else int(INFL_WS_PER_INFLIGHT_BYTE * min(a.inflight_mb << 20, n * B)),
+        "crc32_inputs": a.crc_buffers * a.crc_bytes,
+        "adler32_inputs": a.adler_buffers * a.adler_bytes,
+    }
+    need = sum(legs.values())
+    have = HBM_BYTES_MI355X
+    src = "MI355X nominal 288 GB"
+    if not a.cpu_dry_run and not a.plan_only and torch.cuda.is_available():
+        have = float(torch.cuda.mem_get_info()[1])
+        src = "torch.cuda.mem_get_info"
+    # host side per rank: the interpreter, torch and the library (~3 GB
+    # resident), the verification sample (<= 64 MiB) and, on rank 0 of a
+    # 1-GPU run, the CPU baseline's sample and outputs
+    host = 3e9 + min(64 << 20, n * B) * 3
+    try:
+        avail = 0
+        for line in open("/proc/meminfo"):
+            if line.startswith("MemAvailable:"):
+                avail = int(line.split()[1]) * 1024
+    except OSError:
+        avail = None
+    return {"hbm_bytes_per_rank": {k: int(v) for k, v in legs.items()}, "hbm_need_per_rank": int(need),
+            "hbm_have_per_rank": int(have), "hbm_source": src, "hbm_fits": need <= have,
+            "host_bytes_per_rank_est": int(host), "host_need_all_ranks_est": int(host * world),
+            "host_available": avail,
+            "host_fits": None if avail is None else host * world <= avail}
 
 
 # ------------------------------------------------------------------ CPU baselines
@@ -610,6 +685,11 @@ def checksum_report(a, c, D, which, tag, cpu=None):
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     a = parse(argv)
+    if a.plan_only:
+        # no launcher, no GPU: the plan of every rank of a --gpus N run
+        plan = memory_plan(a, a.gpus)
+        print(json.dumps({"memory_plan": plan, "n_gpus": a.gpus, "ranks_same_plan": True}), flush=True)
+        return
     maybe_launch(a, argv)
     D = Dist(a)
 
@@ -635,7 +715,11 @@ def main(argv=None):
     assert errors == 0, f"deflate status != Z_OK on {int(errors)} buffers"
 
     # ---- verification on this rank (outside the timed region) ----
-    shard_n, shard_dig, shard_note = (0, False, "cpu dry run") if a.cpu_dry_run else shard_golden_check(a, D, d)
+    if a.cpu_dry_run:
+        dry_ranks, dry_note = dry_digest_check(a, digests)
+        shard_n, shard_dig, shard_note = 0, dry_ranks == D.world, "cpu dry run: " + dry_note
+    else:
+        shard_n, shard_dig, shard_note = shard_golden_check(a, D, d)
     from zhelpers import Oracle
     o = Oracle()
     sample, want = [], []
@@ -724,7 +808,7 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": KIND_DATA[a.kind] if not a.cpu_dry_run else "cpu dry run: tests/datagen.py mix, oracle",
+            "data": KIND_DATA[a.kind] if not a.cpu_dry_run else "cpu dry run: the generator's host twin (oracle/zgen.c), oracle",
             "config": {"workload": f"{KIND_CONFIG[a.kind]}: {a.buffers} x {a.buffer_bytes} B buffers per GPU, "
                                    f"deflate level {a.level}, zlib wrapper, inputs+outputs in HBM",
                        "level": a.level, "buffer_bytes": a.buffer_bytes,
@@ -761,6 +845,7 @@ def main(argv=None):
                          "adler32_values_checked": 0 if ad is None else min(2, ad["B"]),
                          "all_status_ok": True},
             "cpu_baseline": cpu,
+            "memory_plan": memory_plan(a, D.world),
         }
         print(json.dumps(line), flush=True)
     D.close()

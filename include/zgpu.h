@@ -162,6 +162,14 @@ int zgpu_crc32_batch(const uint8_t *const *src, const size_t *len,
 int zgpu_adler32_batch(const uint8_t *const *src, const size_t *len,
                        const uint32_t *init, uint32_t *out, size_t count);
 
+/* The zlib.h checksums crc32()/crc32_z()/adler32()/adler32_z() have no error
+ * return.  When their GPU call fails they return 0, set errno = EIO and keep
+ * the library's error code (ZGPU_ENODEV, ZGPU_MEM_ERROR, ...) for this thread:
+ * zgpu_checksum_error() returns it (ZGPU_OK when none failed since the last
+ * reset; reset != 0 clears it).  ZGPU_CHECKSUM_ERROR=abort ends the process
+ * instead. */
+int zgpu_checksum_error(int reset);
+
 /* ---------------- synthetic workloads (benchmark inputs) ---------------- */
 
 /* Fill `count` buffers of `len` bytes each, laid out back to back at dst

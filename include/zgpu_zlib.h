@@ -173,6 +173,9 @@ int compress(Bytef *dest, uLongf *destLen, const Bytef *source,
 int compress2(Bytef *dest, uLongf *destLen, const Bytef *source,
               uLong sourceLen, int level);                              /* zlib.h:1266 */
 uLong compressBound(uLong sourceLen);                                   /* zlib.h:1282 */
+/* crc32 / crc32_z / adler32 / adler32_z run on the GPU.  A failed GPU call
+ * returns 0 with errno = EIO; zgpu_checksum_error() (zgpu.h) names the
+ * error.  ZGPU_CHECKSUM_ERROR=abort ends the process instead. */
 uLong adler32(uLong adler, const Bytef *buf, uInt len);                 /* zlib.h:1711 */
 uLong adler32_z(uLong adler, const Bytef *buf, size_t len);             /* zlib.h:1731 */
 uLong adler32_combine(uLong adler1, uLong adler2, long len2);           /* zlib.h:1738 */

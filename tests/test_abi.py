@@ -169,29 +169,37 @@ def test_oversize_buffers_refused_before_gpu_work(lib):
 
 def test_checksums_fail_loudly_without_gpu(lib):
     """crc32()/adler32() cannot report errors in zlib's API and there is no CPU
-    path: without a usable GPU a call ends the process with a message naming
-    the call (a returned 0 would be a silently wrong check
-    value); ZGPU_CHECKSUM_ERROR=zero opts into returning 0 with a message on
-    every failed call."""
+    path.  Without a usable GPU a call returns 0, sets errno = EIO, keeps the
+    error code for zgpu_checksum_error() and names the call on stderr
+    (the process is no longer ended); ZGPU_CHECKSUM_ERROR=abort
+    ends it with the message instead."""
     import subprocess
     import sys
-    code = ("import ctypes as C, torch; L = C.CDLL(%r); L.crc32.restype = C.c_ulong; "
+    code = ("import ctypes as C, torch; L = C.CDLL(%r, use_errno=True); L.crc32.restype = C.c_ulong; "
             "L.crc32.argtypes = [C.c_ulong, C.c_char_p, C.c_uint]; "
             "L.adler32.restype = C.c_ulong; L.adler32.argtypes = [C.c_ulong, C.c_char_p, C.c_uint]; "
-            "print(L.crc32(0, b'abc', 3), L.adler32(1, b'abc', 3), flush=True)" % LIB)
+            "print(L.zgpu_checksum_error(0), end=' '); C.set_errno(0); a = L.crc32(0, b'abc', 3); e1 = C.get_errno(); "
+            "s1 = L.zgpu_checksum_error(1); s2 = L.zgpu_checksum_error(0); C.set_errno(0); "
+            "b = L.adler32(1, b'abc', 3); e2 = C.get_errno(); "
+            "print(a, b, e1, e2, s1, s2, L.zgpu_checksum_error(1), flush=True)" % LIB)
     import torch
     if torch.cuda.is_available():
         pytest.skip("a GPU is visible")
+    import errno
     env = dict(os.environ, HIP_VISIBLE_DEVICES="-1")
-    env.pop("ZGPU_CHECKSUM_ERROR", None)              # conftest's setting for the host-side tests
+    env.pop("ZGPU_CHECKSUM_ERROR", None)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr[-500:]
+    v = r.stdout.split()
+    assert v[0] == "0"                                # no failure before the first call
+    assert v[1:3] == ["0", "0"]                       # the documented value
+    assert int(v[3]) == errno.EIO and int(v[4]) == errno.EIO
+    assert int(v[5]) == -100 and v[6] == "0"          # ZGPU_ENODEV, then reset
+    assert int(v[7]) == -100                          # the adler32 failure
+    assert "crc32 of 3 bytes failed" in r.stderr
+    env["ZGPU_CHECKSUM_ERROR"] = "abort"
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0 and "crc32 of 3 bytes failed" in r.stderr, (r.returncode, r.stderr[-500:])
-    assert r.stdout == ""
-    env["ZGPU_CHECKSUM_ERROR"] = "zero"
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
-    assert r.returncode == 0, r.stderr
-    assert r.stdout.split() == ["0", "0"]
-    assert "crc32 of 3 bytes failed" in r.stderr and "adler32 of 3 bytes failed" in r.stderr
 
 
 def test_deflateinit2_params_and_bound_vs_reference_golden(lib):

@@ -108,7 +108,7 @@ def test_bench_gpus_flag_launches_ranks():
     for rank, pr in enumerate(line["per_rank"]):
         ob, dg = 0, 0
         for g in range(rank * per_gpu, (rank + 1) * per_gpu):
-            z = o.compress(datagen.mix(nbytes, g), 6)[1]
+            z = o.compress(o.generate(nbytes, 1, 1, 2025, g)[0], 6)[1]
             ob += len(z)
             dg ^= zlib.crc32(z)
         assert pr["out_bytes"] == ob and pr["stream_crc_xor"] == "%08x" % dg
@@ -126,3 +126,63 @@ def test_bench_rejects_mismatched_world():
                         "--buffers", "1", "--buffer-bytes", "1000"], capture_output=True, text=True,
                        timeout=120, env=env)
     assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stderr + r.stdout)
+
+
+def test_bench_world8_dry_run_matches_reference_digests():
+    """`bench.py --gpus 8 --cpu-dry-run` at a small size: eight gloo ranks
+    (launched by bench.py itself), each compressing its shard of the Silesia-
+    style generator's buffers, reduce and all_gather exactly as on eight GPUs;
+    every rank's digest (sum of stream lengths, XOR of stream CRC-32s) must equal
+    the compiled reference's for the same global indices
+    (tests/golden/bench_shard_golden_small.json, make_bench_shard_golden_small.py)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    g = json.load(open(os.path.join(root, "tests", "golden", "bench_shard_golden_small.json")))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8", "--cpu-dry-run",
+                        "--buffers", str(g["buffers_per_rank"]), "--buffer-bytes", str(g["buffer_bytes"]),
+                        "--steps", "1", "--warmup", "0"], capture_output=True, text=True, timeout=600, env=env,
+                       cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([s for s in r.stdout.splitlines() if s.startswith("{")][-1])
+    assert line["n_gpus"] == 8 and line["config"]["world_size_seen"] == 8
+    assert line["config"]["collective_backend"] == "gloo"
+    assert [p["rank"] for p in line["per_rank"]] == list(range(8))
+    for pr in line["per_rank"]:
+        want = g["ranks"][str(pr["rank"])]
+        assert {"out_bytes": pr["out_bytes"], "stream_crc_xor": pr["stream_crc_xor"]} == want, pr
+    assert line["verified"]["per_rank_digest_vs_reference"] is True
+    total_in = 8 * g["buffers_per_rank"] * g["buffer_bytes"]
+    assert abs(line["compression_ratio"] - total_in / sum(w["out_bytes"] for w in g["ranks"].values())) < 1e-3
+    assert line["memory_plan"]["hbm_fits"] is True
+
+
+def test_bench_memory_plan_per_rank():
+    """`bench.py --gpus 8 --plan-only`: the HBM each rank of the default C4 run
+    holds -- 32 GiB in, 32 GiB out, ~31 B of deflate workspace per in-flight
+    byte (4 GiB), the inflate leg's output and records, the checksum legs'
+    inputs -- must fit an MI355X's 288 GB, and the host side must fit the
+    host; a sub-batch budget twice as large must be reported as not fitting."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+    def plan(*extra):
+        r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8", "--plan-only", *extra],
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return json.loads(r.stdout.strip().splitlines()[-1])["memory_plan"]
+
+    p = plan()
+    legs = p["hbm_bytes_per_rank"]
+    assert legs["deflate_inputs"] == 32768 << 20
+    assert 30 * (4 << 30) < legs["deflate_workspace"] < 36 * (4 << 30)
+    assert p["hbm_need_per_rank"] == sum(legs.values())
+    assert p["hbm_fits"] is True and p["hbm_need_per_rank"] <= 288e9
+    assert p["host_need_all_ranks_est"] == 8 * p["host_bytes_per_rank_est"]
+    assert plan("--inflight-mb", "8192")["hbm_fits"] is False

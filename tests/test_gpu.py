@@ -3,6 +3,7 @@ golden fixtures generated from the compiled reference.  Bit-exact everywhere:
 deflate streams byte for byte, CRC-32 / Adler-32 values exactly."""
 import ctypes as C
 import hashlib
+import os
 import zlib as pyzlib
 
 import numpy as np
@@ -11,6 +12,7 @@ import pytest
 import datagen
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 # ----------------------------- checksums -----------------------------
@@ -377,12 +379,15 @@ def _syszlib(b, level, wbits=15, mem_level=8):
 
 @pytest.mark.parametrize("level", [1, 2, 3])
 def test_fast_levels_lds_parse(zg, level):
-    """Few buffers at L1-3 parse with head[], prev[] and the window in LDS
-    (k_parse_fast<kLds>): 16-bit head entries swept every 16 Ki positions, a
-    32 Ki prev ring and a 32 Ki byte ring filled to p + 262.  Streams equal
-    system zlib's for lone buffers across sweeps and ring wraps, tiny and empty
-    buffers, smaller windows and memLevels, and a batch above the LDS variant's
-    256-buffer limit (the HBM variant) beside one below it."""
+    """Few buffers at L1-3.  Level 1 parses with head[], prev[] and the window
+    in LDS (k_parse_fast<kLds>): 16-bit head entries swept every 16 Ki
+    positions, a 32 Ki prev ring and a 32 Ki byte ring filled to p + 262.
+    Levels 2-3 with at most 16 buffers take the sorted-run parse (k_parse_srt)
+    by default; test_fast_levels_lds_parse_without_srt runs the same cases on
+    k_parse_fast<kLds> there (the path a failed sorted-run allocation takes).
+    Streams equal system zlib's for lone buffers across sweeps and ring wraps,
+    tiny and empty buffers, smaller windows and memLevels, and a batch above the
+    LDS variant's 256-buffer limit (the HBM variant) beside one below it."""
     cases = [[datagen.make("text", 64 * 1024, 81)], [datagen.make("mix", (3 << 20) + 17, 82)],
              [datagen.make("runs", 70000, 83)], [datagen.make("records", (1 << 20) + 1, 84)],
              [b"", b"a", b"ab", b"abc", bytes(300), datagen.make("markup", 32768 + 262, 85)]]
@@ -401,6 +406,30 @@ def test_fast_levels_lds_parse(zg, level):
         got = zg.compress_batch(bufs, level=level)
         for b, (st, z) in zip(bufs, got):
             assert st == 0 and z == _syszlib(b, level), (len(b), count)
+
+
+def test_fast_levels_lds_parse_without_srt():
+    """ZGPU_FAST_SRT is read once per process, so levels 2-3 with few buffers
+    run k_parse_srt in the rest of the suite.  Here a child process with
+    ZGPU_FAST_SRT=0 runs test_fast_levels_lds_parse's cases at levels 2 and 3
+    on k_parse_fast<kLds>, against system zlib."""
+    import subprocess
+    import sys
+    code = (
+        "import sys, zlib; sys.path[:0] = [%r, %r]\n"
+        "import torch, zgpu, datagen\n"
+        "zgpu.load()\n"
+        "for level in (2, 3):\n"
+        "    cases = [[datagen.make('text', 64 * 1024, 81)], [datagen.make('mix', (3 << 20) + 17, 82)],\n"
+        "             [datagen.make('runs', 70000, 83)], [datagen.make('records', (1 << 20) + 1, 84)],\n"
+        "             [b'', b'a', b'ab', b'abc', bytes(300), datagen.make('markup', 32768 + 262, 85)]]\n"
+        "    for bufs in cases:\n"
+        "        for b, (st, z) in zip(bufs, zgpu.compress_batch(bufs, level=level)):\n"
+        "            assert st == 0 and z == zlib.compress(b, level), (len(b), level)\n"
+        "print('ok')\n" % (os.path.join(ROOT, "zlib.wasm_amd"), os.path.join(ROOT, "tests")))
+    env = dict(os.environ, ZGPU_FAST_SRT="0")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
 
 
 @pytest.mark.parametrize("level", [5, 6, 9])

@@ -44,7 +44,7 @@ ok = all(h_dst[i * cap:i * cap + int(dl[i])].numpy().tobytes() ==
          zlib.compress(src[i * n:(i + 1) * n].cpu().numpy().tobytes(), level) for i in range(0, B, B // 8))
 key = "match" if level >= 4 else "parse_greedy"
 import os  # noqa: E402
-print(f"{lib} MATCH2={os.environ.get('ZGPU_MATCH2', '0')}: {key} {stg[key][0] / stg[key][1]:.1f} ms/launch, step {el * 1e3:.1f} ms, exact {ok}",
+print(f"{lib} LZP={os.environ.get('ZGPU_LZP', '0')}: {key} {stg[key][0] / stg[key][1]:.1f} ms/launch, step {el * 1e3:.1f} ms, exact {ok}",
       flush=True)
 print("  stages ms per launch:", {k: round(v[0] / max(v[1], 1) * (v[1] / reps), 2) for k, v in stg.items() if v[1]},
       flush=True)

@@ -4760,8 +4760,9 @@ int launch_tables_upload(const CodeTables *ct, const CrcTables *) {
 }
 
 // ------------------------------------------------------------------------
-// The sorted-run longest_match (round 5): k_bsort, k_bwork, k_match2 for
-// batch jobs at levels 4..9 (hash_bits <= 15).
+// The sorted runs (round 5): k_bsort, k_bwork<true> for k_parse_srt (levels
+// 2..3 of few buffers, hash_bits <= 15).  (Round 5 also walked levels 4..9
+// from them, k_match2: 2x slower than k_match, removed in round 6.)
 //
 // longest_match's candidates for position p are the earlier positions with
 // p's hash, most recent first, while they lie within MAX_DIST (deflate.c
@@ -5002,16 +5003,10 @@ __global__ __launch_bounds__(kBSThreads) void k_bwork(DeflateJob job) {
     }
 }
 
-// k_match2 — levels 4..9, one 1024-thread workgroup per buffer (or per range
-// of blocks of a large buffer).  LDS holds, for the blocks b-2, b-1, b of the
-// current block b, their sorted entries as byte-ring offsets (Sr, 96 KiB) and
-// their bytes (Bw, 48 KiB + pad); between blocks both slide down by one block.
-// A work item (k_bwork) gives a position's three candidate runs; candidate k
-// is Sr[base(k) - k], so the walk needs no link: every candidate's load is
-// independent of the previous one's.  The walk is dwq_walk's (deferred
-// compares, kDU steps per exit test) with the link chase replaced by that
-// index, and it equals longest_match (deflate.c:1356-1497) for every position.
-constexpr int kM2Threads = 1024;
+// The rings of k_parse_srt (levels 2..3 from the sorted runs): the sorted
+// entries and bytes of three blocks.  (k_match2, the sorted-run walk of levels
+// 4..9, measured 2x slower than k_match and left the library in round 6;
+// DESIGN 4.14.)
 constexpr int kM2Pad = 304;                       // bytes past block b: compares read <= 258 + 16 + 3 past a position
 constexpr int kM2Ring = 3 * kSortBlock;
 
@@ -5036,320 +5031,11 @@ __device__ __attribute__((always_inline)) inline void b16(const uint8_t *B, int 
     x2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
     x3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
 }
-// LCP of the scan at s (its first 16 bytes in S) and candidate m, capped at maxcmp
-__device__ __attribute__((always_inline)) inline int blcp16(const uint8_t *B, int m, int s, const Scan16 &S,
-                                                            int maxcmp) {
-    uint32_t a0, a1, a2, a3;
-    b16(B, m, a0, a1, a2, a3);
-    int k = diff16(a0 ^ S.s0, a1 ^ S.s1, a2 ^ S.s2, a3 ^ S.s3);
-    while (k >= 16 && k < maxcmp) {
-        uint32_t c0, c1, c2, c3;
-        b16(B, m + k, a0, a1, a2, a3);
-        b16(B, s + k, c0, c1, c2, c3);
-        const int r = diff16(a0 ^ c0, a1 ^ c1, a2 ^ c2, a3 ^ c3);
-        k += r;
-        if (r < 16) break;
-    }
-    return k < maxcmp ? k : maxcmp;
-}
-
-// One position's longest_match from its work item.  Every lane of the wave
-// calls this together (the flushes are wave-wide decisions taken with ballots).
-//   Sr, B: the rings; vp: the position's ring offset; lim: ring offset of the
-//   limit (candidates must lie above it; the head may equal it, deflate.c
-//   :1955 vs :1492); A0/B1/B2, n0/n01/n012: candidate k is Sr[base(k) - k]
-//   with base A0 for k < n0, B1 for k < n01, B2 below n012 (none after).
-__device__ __attribute__((always_inline)) inline uint32_t m2_cand(const uint16_t *Sr, uint32_t k, int A0, int B1,
-                                                                  int B2, uint32_t n0, uint32_t n01, uint32_t n012) {
-    int idx = k < n0 ? A0 - (int)k : (k < n01 ? B1 - (int)k : B2 - (int)k);
-    idx = idx < 0 ? 0 : idx;
-    const int q = (int)Sr[idx];
-    return k < n012 ? (uint32_t)q : 0xffffffffu;       // none: below every limit (tested as signed)
-}
-// The quick reject with aligned 2-byte reads only (a ds_read_u16 at an odd
-// byte address is split: tools/lds_probe.hip, 6x the cycles of an aligned
-// read).  longest_match rejects a candidate whose bytes best-1, best or 0, 1
-// differ from the scan's (deflate.c:1449-1452); any pair of positions within
-// [0, best] is as sound a filter for "longer than best" (the result is the
-// same: only compares decide), so each test takes the pair at the even byte
-// address next to the one zlib reads -- bytes (best-1, best) or (best-2,
-// best-1), and (0, 1) or (1, 2) -- against the scan's pair at the same offset.
-struct DWQ2 {
-    int occ;
-    int q[kDQ];
-    uint32_t scan01, scan12, scanE1, scanE2;   // the scan's pairs at 0, 1, best-1, best-2
-    int be;            // best - 1
-    bool alive;        // no candidate at or below the limit seen yet
-};
-__device__ __attribute__((always_inline)) inline uint32_t ldu16e(const uint8_t *B, int x) {   // x even
-    return (uint32_t)*reinterpret_cast<const uint16_t *>(B + x);
-}
-__device__ __attribute__((always_inline)) inline void m2_walk(const uint16_t *Sr, const uint8_t *B, int vp, int lim,
-                                                              int A0, int B1, int B2, uint32_t n0, uint32_t n01,
-                                                              uint32_t n012, int64_t p, int64_t n,
-                                                              const LevelCfg &cfg, uint32_t *rf, uint32_t *rq,
-                                                              int want_q) {
-    const int64_t rem = n - p;
-    const int nice = rem < cfg.nice ? (int)rem : cfg.nice;
-    const int maxcmp = rem < kMaxMatch ? (int)rem : kMaxMatch;
-    const uint32_t chain = (uint32_t)cfg.chain;
-    const uint32_t qc = want_q ? chain >> 2 : chain;
-    Scan16 S;
-    b16(B, vp, S.s0, S.s1, S.s2, S.s3);
-    int best = kMinMatch - 1, bq = vp;
-    uint32_t count = 0;
-    bool walking = true, need_q = want_q != 0;
-    auto rec = [&](int bb, int q) { return bb >= kMinMatch ? (((uint32_t)bb << 16) | (uint32_t)(vp - q)) : 0u; };
-#pragma unroll
-    for (int k = 0; k < kD0; k++) {                 // the chain's head, compared by the whole wave
-        if (walking) {
-            const int q = (int)m2_cand(Sr, count, A0, B1, B2, n0, n01, n012);
-            const int len = blcp16(B, q, vp, S, maxcmp);
-            if (len > best) { best = len; bq = q; }
-            count++;
-            const int qn = (int)m2_cand(Sr, count, A0, B1, B2, n0, n01, n012);
-            if (best >= nice || qn <= lim || count >= chain) walking = false;
-            if (need_q && count == qc && walking) {
-                rq[p] = rec(best, bq);
-                need_q = false;
-            }
-        }
-    }
-    if (!walking) {
-        const uint32_t r = rec(best, bq);
-        if (need_q) rq[p] = r;
-        rf[p] = r;
-        return;
-    }
-    DWQ2 w;
-    w.occ = 0;
-#pragma unroll
-    for (int j = 0; j < kDQ; j++) w.q[j] = 0;
-    w.scan01 = S.s0 & 0xffffu;
-    w.scan12 = (S.s0 >> 8) & 0xffffu;
-    w.be = best - 1;
-    w.scanE1 = b4(B, vp + w.be) & 0xffffu;
-    w.scanE2 = b4(B, vp + w.be - 1) & 0xffffu;
-    w.alive = true;
-    count = ufl(count);
-    auto step = [&](uint32_t k) {
-        const int q = (int)m2_cand(Sr, k, A0, B1, B2, n0, n01, n012);
-        const bool in = q > lim;
-        const int qs = in ? q : 0;
-        const int xe = qs + w.be;
-        const uint32_t c01 = ldu16e(B, (qs + 1) & ~1), cE = ldu16e(B, xe & ~1);
-        const uint32_t s01 = (qs & 1) ? w.scan12 : w.scan01, sE = (xe & 1) ? w.scanE2 : w.scanE1;
-        const bool pass = w.alive & in & (c01 == s01) & (cE == sE);
-        w.alive = w.alive & in;
-#pragma unroll
-        for (int j = kDQ - 1; j > 0; j--) w.q[j] = pass ? w.q[j - 1] : w.q[j];
-        w.q[0] = pass ? q : w.q[0];
-        w.occ += pass ? 1 : 0;
-    };
-    for (;;) {
-        const uint32_t end = count < qc ? qc : chain;
-        const int best0 = best;
-        for (;;) {
-            if (end - count >= (uint32_t)kDU) {
-#pragma unroll
-                for (int u = 0; u < kDU; u++) step(count + u);
-                count += kDU;
-            } else {
-                step(count);
-                count += 1;
-            }
-            const uint64_t walkers = __ballot(w.alive), full = __ballot(w.occ >= kDQ - (kDU - 1));
-            if (count >= end || walkers == 0 || full != 0) break;
-        }
-        walking = w.alive && count < chain;
-        if (walking) {                                  // the next candidate must lie above the limit too
-            const int qn = (int)m2_cand(Sr, count, A0, B1, B2, n0, n01, n012);
-            walking = qn > lim;
-        }
-        static_assert(kDQ % 2 == 0, "entries are taken in pairs");
-#pragma unroll
-        for (int j = kDQ - 1; j >= 1; j -= 2) {
-            const bool c1 = j < w.occ, c0 = j - 1 < w.occ;
-            if (__ballot(c0) != 0) {
-                const int l1 = c1 ? blcp16(B, w.q[j], vp, S, maxcmp) : 0;
-                const int l0 = c0 ? blcp16(B, w.q[j - 1], vp, S, maxcmp) : 0;
-                if (c1 && l1 > best) {
-                    best = l1;
-                    bq = w.q[j];
-                    if (l1 >= nice) { walking = false; w.occ = 0; }
-                }
-                if (c0 && j - 1 < w.occ && l0 > best) {
-                    best = l0;
-                    bq = w.q[j - 1];
-                    if (l0 >= nice) { walking = false; w.occ = 0; }
-                }
-            }
-        }
-        w.occ = 0;
-        const bool fin = !walking;
-        if (need_q && (count >= qc || fin)) {          // deflate.c:1390-1392 (chain >>= 2)
-            rq[p] = rec(best, bq);
-            need_q = false;
-        }
-        if (fin) break;
-        if (best != best0) {                           // the quick reject now tests the new best
-            w.be = best - 1;
-            w.scanE1 = b4(B, vp + w.be) & 0xffffu;
-            w.scanE2 = b4(B, vp + w.be - 1) & 0xffffu;
-        }
-    }
-    rf[p] = rec(best, bq);
-}
-
-// What a thread stages of block b: 16 sorted entries, 16 bytes (+ pad).
-struct M2Pre {
-    uint4 s0, s1;
-    uint4 by, pad;
-};
-__device__ __attribute__((always_inline)) inline void m2_prefetch(M2Pre &P, const uint16_t *gS, int m,
-                                                                  const uint8_t *in, int64_t p0, int64_t n, int tid) {
-    const int e = 16 * tid;
-    if (e + 16 <= m) {
-        P.s0 = *reinterpret_cast<const uint4 *>(gS + e);
-        P.s1 = *reinterpret_cast<const uint4 *>(gS + e + 8);
-    } else {
-        uint32_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int j = 0; j < 16; j++)
-            if (e + j < m) v[j >> 1] |= (uint32_t)gS[e + j] << (16 * (j & 1));
-        P.s0 = make_uint4(v[0], v[1], v[2], v[3]);
-        P.s1 = make_uint4(v[4], v[5], v[6], v[7]);
-    }
-    auto ld16 = [&](int64_t x) -> uint4 {
-        if (x >= 0 && x + 16 <= n) {
-            const uintptr_t a = reinterpret_cast<uintptr_t>(in + x);
-            const uint32_t sh = (uint32_t)(a & 3u);
-            const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
-            if (sh == 0) return make_uint4(q[0], q[1], q[2], q[3]);
-            const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
-            return make_uint4(__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
-                              __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh));
-        }
-        uint32_t w[4] = {0, 0, 0, 0};
-        for (int j = 0; j < 16; j++)
-            if (x + j >= 0 && x + j < n) w[j >> 2] |= (uint32_t)in[x + j] << (8 * (j & 3));
-        return make_uint4(w[0], w[1], w[2], w[3]);
-    };
-    P.by = ld16(p0 + e);
-    if (tid < kM2Pad / 16) P.pad = ld16(p0 + kSortBlock + e);
-}
-
-template <bool kSegs = false>
-__global__ __launch_bounds__(kM2Threads) void k_match2(DeflateJob job, int want_q) {
-    __shared__ __attribute__((aligned(16))) uint16_t Sr[kM2Ring];
-    __shared__ __attribute__((aligned(16))) uint8_t Bw[kM2Ring + kM2Pad];
-    __shared__ uint32_t next_c;
-    const int tid = threadIdx.x, lane = tid & 63;
-    // one workgroup per buffer, or (kSegs: job.seg pairs (buffer, first
-    // block), job.seg_len blocks each) per range of blocks; a range first
-    // stages the two blocks before its first one without walking them
-    const uint32_t bi = kSegs ? job.seg[2 * blockIdx.x] : blockIdx.x;
-    const uint32_t g = job.first + bi;
-    const int64_t n = (int64_t)job.src_len[g];
-    const uint8_t *in = job.src + job.src_off[g];
-    const uint32_t nblk = (uint32_t)((n + kSortBlock - 1) / kSortBlock);
-    const uint32_t w0 = kSegs ? job.seg[2 * blockIdx.x + 1] : 0u;
-    const uint32_t w1 = kSegs ? min(nblk, w0 + job.seg_len) : nblk;
-    const uint32_t t0 = w0 >= 2 ? w0 - 2 : 0u;
-    const uint16_t *gS = job.srt + job.ws_off[bi];
-    const uint4 *gW = job.work + job.ws_off[bi];
-    uint32_t *rf = job.rfull + job.ws_off[bi];
-    uint32_t *rq = job.rquart + job.ws_off[bi];
-    const LevelCfg cfg = job.cfg;
-    const int64_t max_dist = job_win(job).max_dist;
-    auto mcount = [&](uint32_t b) -> int {
-        const int64_t r = n - 2 - (int64_t)b * kSortBlock;
-        return r <= 0 ? 0 : (r < kSortBlock ? (int)r : kSortBlock);
-    };
-    M2Pre P;
-    if (t0 < w1) m2_prefetch(P, gS + (size_t)t0 * kSortBlock, mcount(t0), in, (int64_t)t0 * kSortBlock, n, tid);
-    for (uint32_t b = t0; b < w1; b++) {
-        const int64_t p0 = (int64_t)b * kSortBlock;
-        const int m = mcount(b);
-        // slide both rings down one block (b-1 -> slot 0, b -> slot 1); each
-        // thread moves its chunks in increasing order, and a chunk's source is
-        // one this same thread moves later, so nothing is overwritten unread
-        if (b > t0) {
-            uint4 *dS = reinterpret_cast<uint4 *>(Sr);
-            for (int c = tid; c < 2 * kSortBlock / 8; c += kM2Threads) {
-                uint4 v = dS[c + kSortBlock / 8];
-                typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-                auto sub = [](uint32_t x) {
-                    const us2 d = {(unsigned short)kSortBlock, (unsigned short)kSortBlock};
-                    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(us2, x) - d);
-                };
-                v = make_uint4(sub(v.x), sub(v.y), sub(v.z), sub(v.w));
-                dS[c] = v;
-            }
-            uint4 *dB = reinterpret_cast<uint4 *>(Bw);
-            for (int c = tid; c < 2 * kSortBlock / 16; c += kM2Threads) dB[c] = dB[c + kSortBlock / 16];
-            __syncthreads();
-        }
-        // block b into slot 2: entries as ring offsets (2 * kSortBlock + rel)
-        {
-            const uint32_t o = 2u * kSortBlock * 0x10001u;
-            uint4 *dS = reinterpret_cast<uint4 *>(Sr + 2 * kSortBlock + 16 * tid);
-            dS[0] = make_uint4(P.s0.x + o, P.s0.y + o, P.s0.z + o, P.s0.w + o);
-            dS[1] = make_uint4(P.s1.x + o, P.s1.y + o, P.s1.z + o, P.s1.w + o);
-            *reinterpret_cast<uint4 *>(Bw + 2 * kSortBlock + 16 * tid) = P.by;
-            if (tid < kM2Pad / 16) *reinterpret_cast<uint4 *>(Bw + 3 * kSortBlock + 16 * tid) = P.pad;
-        }
-        if (tid == 0) next_c = 0;
-        __syncthreads();
-        if (b + 1 < w1)                                 // lands during the walks
-            m2_prefetch(P, gS + (size_t)(b + 1) * kSortBlock, mcount(b + 1), in, p0 + kSortBlock, n, tid);
-        if (b >= w0) {
-            // positions the sort left out (p > n-3: no INSERT_STRING, no search)
-            for (int64_t x = p0 + m + tid; x < n && x < p0 + kSortBlock; x += kM2Threads) {
-                rf[x] = 0;
-                if (want_q) rq[x] = 0;
-            }
-            const int64_t base = p0 - 2 * kSortBlock;   // absolute position of ring offset 0
-            const uint4 *W = gW + p0;
-            for (;;) {
-                uint32_t c = 0;
-                if (lane == 0) c = atomicAdd(&next_c, 64u);
-                c = ufl(__shfl((int)c, 0, 64));
-                if (c >= (uint32_t)m) break;
-                const uint32_t j = c + lane;
-                if (j >= (uint32_t)m) continue;
-                const uint4 it = W[j];
-                const int i = (int)(it.x & 0xffffu), rel = (int)(it.x >> 16);
-                const uint32_t n0 = it.y & 0xffffu, n1 = it.y >> 16, e1 = it.z & 0xffffu, e2 = it.z >> 16;
-                const uint32_t n2 = it.w;
-                const int64_t p = p0 + rel;
-                const int vp = 2 * kSortBlock + rel;
-                // deflate.c:1955: the head must be within MAX_DIST (and not NIL,
-                // position 0); the chain continues above max(p - MAX_DIST, 0)
-                const int64_t labs = p > max_dist ? p - max_dist : 0;
-                const int lim = (int)(labs - base);
-                const uint32_t n01 = n0 + n1, n012 = n01 + n2;
-                const int A0 = 2 * kSortBlock + i - 1;
-                const int B1 = kSortBlock + (int)e1 - 1 + (int)n0;
-                const int B2 = (int)e2 - 1 + (int)n01;
-                const int h = (int)m2_cand(Sr, 0, A0, B1, B2, n0, n01, n012);
-                const int64_t hq = base + h;
-                if (n012 == 0 || hq < 1 || p - hq > max_dist) {
-                    rf[p] = 0;
-                    if (want_q) rq[p] = 0;
-                    continue;
-                }
-                m2_walk(Sr, Bw, vp, lim, A0, B1, B2, n0, n01, n012, p, n, cfg, rf, rq, want_q);
-            }
-        }
-        __syncthreads();
-    }
-}
-
 // ------------------------------------------------------------------------
 // k_parse_srt — deflate_fast (levels 1..3, deflate.c:1824-1915) of a batch
 // job from the sorted runs (k_bsort, k_bwork<true>).  One wave per buffer,
 // the CU's LDS holding the sorted entries and bytes of the blocks b-2..b of
-// the parse position (as k_match2) and a bitmap of the positions deflate_fast
+// the parse position and a bitmap of the positions deflate_fast
 // has inserted (blocks b-2..b+1).
 //
 // deflate_fast searches the chain of INSERTED positions: a position strictly
@@ -5740,8 +5426,7 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     case 14:                                                // the sorted-run match: sort, work items
         if (job.nsblk) {
             hipLaunchKernelGGL(k_bsort, dim3(job.nsblk), dim3(kBSThreads), 0, st, job);
-            if (job.level >= 4) hipLaunchKernelGGL(k_bwork<false>, dim3(job.nsblk), dim3(kBSThreads), 0, st, job);
-            else hipLaunchKernelGGL(k_bwork<true>, dim3(job.nsblk), dim3(kBSThreads), 0, st, job);
+            hipLaunchKernelGGL(k_bwork<true>, dim3(job.nsblk), dim3(kBSThreads), 0, st, job);
         }
         break;
     case 16:                                                // levels 1..3 from the sorted runs
@@ -5759,12 +5444,6 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
             else hipLaunchKernelGGL(k_parse_srt<int64_t>, grid, dim3(64), 0, st, job);
         }
         break;
-    case 15: {
-        const int wq = (int)(job.cfg.good < job.cfg.lazy) | job.cfg_q;
-        if (job.seg) hipLaunchKernelGGL(k_match2<true>, dim3(job.nseg), dim3(kM2Threads), 0, st, job, wq);
-        else hipLaunchKernelGGL(k_match2<false>, grid, dim3(kM2Threads), 0, st, job, wq);
-        break;
-    }
 #ifdef ZGPU_LZP
     case 17: hipLaunchKernelGGL(k_lzp, grid, dim3(kZThreads), 0, st, job); break;   // match + lazy parse (k_lzp)
 #endif

@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "zgpu_init", "zgpu_info", "zgpu_set_inflight_bytes", "zgpu_deflate_batch_dev",
     "zgpu_deflate_batch_dev_ex", "zgpu_compress_batch_ex",
     "zgpu_crc32_batch_dev", "zgpu_adler32_batch_dev", "zgpu_compress_batch",
-    "zgpu_crc32_batch", "zgpu_adler32_batch", "zgpu_generate_dev", "zgpu_stage_timing",
+    "zgpu_crc32_batch", "zgpu_adler32_batch", "zgpu_checksum_error", "zgpu_generate_dev", "zgpu_stage_timing",
     "zgpu_stage_timing_read", "zgpu_inflate_batch_dev", "zgpu_uncompress_batch",
     "zgpu_deflate_batch_dev2", "zgpu_compress_batch2",
     # include/zgpu_zlib.h
