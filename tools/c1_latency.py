@@ -12,7 +12,9 @@ sys.path.insert(0, 'tests')
 import datagen  # noqa: E402
 import zgpu  # noqa: E402
 
-assert zgpu.load().zgpu_init() == 0
+lib = sys.argv[1] if len(sys.argv) > 1 else None
+assert (zgpu.load(lib) if lib else zgpu.load()).zgpu_init() == 0
+print("library:", lib or "zlib.wasm_amd/libzgpu.so", flush=True)
 for kind in ("text", "mix"):
     data = bytes(datagen.make(kind, 64 * 1024, 7))
     st, z = zgpu.compress2(data, level=6)

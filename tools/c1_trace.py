@@ -8,7 +8,7 @@ import datagen  # noqa: E402
 import zgpu  # noqa: E402
 
 assert zgpu.load().zgpu_init() == 0
-kind = sys.argv[1] if len(sys.argv) > 1 else "runs"
+kind = sys.argv[1] if len(sys.argv) > 1 else "runs"   # datagen kind: text, mix, runs, ...
 data = bytes(datagen.make(kind, 64 * 1024, 7))
 for _ in range(20):
     rc, z = zgpu.compress2(data, level=6)

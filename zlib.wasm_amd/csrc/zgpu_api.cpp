@@ -2084,9 +2084,17 @@ int zgpu_debug_stages(const uint8_t *src, size_t n, int level, uint16_t *link, u
         hipStreamSynchronize(st) != hipSuccess)
         return ZGPU_MEM_ERROR;
     if (link && n && copy_sync(link, job.link, 2 * n, hipMemcpyDeviceToHost, st) != hipSuccess) return ZGPU_MEM_ERROR;
-    if (rfull && n && copy_sync(rfull, job.rfull, 4 * n, hipMemcpyDeviceToHost, st) != hipSuccess) return ZGPU_MEM_ERROR;
-    if (rquart && n && level >= 5 && copy_sync(rquart, job.rquart, 4 * n, hipMemcpyDeviceToHost, st) != hipSuccess)
+    // k_match keeps the quartered budget's result only where it differs from
+    // the full one (bit 31 of rfull); the debug view gives both in full
+    std::vector<uint32_t> rf(n), rq(n);
+    if (n && (copy_sync(rf.data(), job.rfull, 4 * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+              copy_sync(rq.data(), job.rquart, 4 * n, hipMemcpyDeviceToHost, st) != hipSuccess))
         return ZGPU_MEM_ERROR;
+    for (size_t p = 0; p < n; p++) {
+        const uint32_t f = rf[p] & 0x7fffffffu;
+        if (rfull) rfull[p] = f;
+        if (rquart && level >= 5) rquart[p] = (rf[p] >> 31) ? rq[p] : f;
+    }
     return ZGPU_OK;
 }
 
