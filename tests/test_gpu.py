@@ -372,6 +372,31 @@ def test_small_single_buffers_tile_segments(zg, oracle):
         assert rc == 0 and z == oracle.compress(bufs[-1], 6)[1]
 
 
+def test_small_buffers_short_segments_chain(zg, oracle):
+    """Sub-batches of few buffers of at most 64 KiB parse in 256-byte segments
+    (k_pbig1..5), where a lane's run-on may cross up to 8 segments before it
+    meets a later lane's pass 1 and k_pbig3 joins the chain of meets.  Runs
+    of 300..600 bytes and periodic data make the meets skip segments; 64 KiB
+    of zeros never meets within reach (the buffer falls back to k_parse_slow);
+    tiny and ragged sizes give one- and two-lane buffers."""
+    rng = np.random.default_rng(31)
+    runs = bytes(np.repeat(rng.integers(0, 256, 200, dtype=np.uint8), rng.integers(300, 600, 200))[:65536])
+    cases = [[bytes(65536)], [runs], [(b"\x00" * 258 + b"\x01") * 252], [(b"abc" * 21846)[:65536]],
+             [datagen.make("text", 65536, 81)], [datagen.make("mix", 65535, 82)], [datagen.make("random", 65536, 83)],
+             [datagen.make("markup", 40000, 84), datagen.make("records", 65536, 85), datagen.make("runs", 257, 86),
+              datagen.make("text", 256, 87), datagen.make("text", 513, 88)],
+             [datagen.make("runs", 65536, 89), runs[:4097], bytes(5000), datagen.make("text", 30001, 90)]]
+    for bufs in cases:
+        for level in (4, 5, 6, 9):
+            for strategy in (0, 1):
+                got = zg.compress_batch(bufs, level=level, strategy=strategy)
+                for b, (st, z) in zip(bufs, got):
+                    assert st == 0 and z == oracle.compress(b, level, strategy=strategy)[1], \
+                        (len(b), level, strategy)
+        rc, z = zg.compress2(bufs[0], level=6)
+        assert rc == 0 and z == oracle.compress(bufs[0], 6)[1]
+
+
 def _syszlib(b, level, wbits=15, mem_level=8):
     c = pyzlib.compressobj(level, pyzlib.DEFLATED, wbits, mem_level)
     return c.compress(bytes(b)) + c.flush()

@@ -252,7 +252,7 @@ struct Ctx {
     DevBuf ws_help;           // the a18 helpers' staging (zlib_*_simd)
     DevBuf ws_seg;            // k_match segments of sub-batches of few large buffers
     // few large buffers: k_pbig* lane groups and records, k_enc_* block plans
-    DevBuf ws_pg, ws_plane, ws_pbuf, ws_eplan, ws_wind, ws_tl;
+    DevBuf ws_pg, ws_plane, ws_pbuf, ws_eplan, ws_wind, ws_tl, ws_pron;
     DevBuf ws_ck;             // split checksum partials (few large buffers)
     DevBuf ws_srec, ws_snap;  // a streaming job's block records and head[] snapshot
     DevBuf ws_srt, ws_boff, ws_work, ws_bblk;   // the sorted-run parse of levels 2..3 (k_bsort / k_bwork / k_parse_srt)
@@ -657,8 +657,16 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     static const bool no_big = std::getenv("ZGPU_NO_BIGBUF") != nullptr;   // A/B: the one-workgroup stages
     std::vector<uint32_t> pg, plb;
     std::vector<size_t> pg_at(nsub + 1, 0), plb_at(nsub + 1, 0);
-    std::vector<uint32_t> pseg_of(nsub, 0), maxblk_of(nsub, 0);
+    std::vector<uint32_t> pseg_of(nsub, 0), maxblk_of(nsub, 0), preach_of(nsub, 1);
     uint64_t max_lanes = 0;
+    // A sub-batch of small buffers (a lone 64 KiB compress2, say) parses in
+    // 256-byte segments, each buffer one workgroup of at most kParseLanes
+    // lanes, and a lane's run-on may cross kSmallReach segments before it must
+    // meet a later lane's pass 1 (k_pbig3 joins the chain of meets): four times
+    // the lanes of 1 KiB segments, so a quarter of each lane's serial parse,
+    // without the stitch failures short segments would give long matches
+    static const int small_seg = [] { const char *e = std::getenv("ZGPU_PSEG_SMALL"); return e ? std::atoi(e) : 1; }();
+    constexpr uint64_t kSmallSeg = 256, kSmallReach = 8;
     for (size_t sb = 0; sb < nsub; sb++) {
         pg_at[sb] = pg.size() / 2;
         plb_at[sb] = plb.size();
@@ -669,6 +677,12 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         for (uint32_t i = a; i < b; i++) tot += lens[i] - st0;
         uint64_t ps = ((tot + 65535) / 65536 + 15) & ~15ull;
         ps = ps < 1024 ? 1024 : ps > 65536 ? 65536 : ps;
+        uint64_t maxlen = 0;
+        for (uint32_t i = a; i < b; i++) maxlen = std::max<uint64_t>(maxlen, lens[i] - st0);
+        if (small_seg && !fs && tot <= (4ull << 20) && maxlen <= kSmallSeg * kParseLanesHost) {
+            ps = kSmallSeg;
+            preach_of[sb] = (uint32_t)kSmallReach;
+        }
         uint64_t lanes = 0;
         for (uint32_t i = a; i < b; i++) {
             const uint64_t nl = std::max<uint64_t>(1, (lens[i] - st0 + ps - 1) / ps);
@@ -717,7 +731,8 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
         pg.insert(pg.end(), plb.begin(), plb.end());
         if (!c.ws_pg.ensure(4 * pg.size()) ||
             hipMemcpyAsync(c.ws_pg.p, pg.data(), 4 * pg.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
-            !c.ws_plane.ensure(sizeof(PLane) * max_lanes) || !c.ws_pbuf.ensure(sizeof(PBuf) * max_cnt))
+            !c.ws_plane.ensure(sizeof(PLane) * max_lanes) || !c.ws_pbuf.ensure(sizeof(PBuf) * max_cnt) ||
+            !c.ws_pron.ensure(4ull * kRonCap * max_lanes))
             return zfail(__LINE__);
         pg.resize(npg);
     }
@@ -803,6 +818,8 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
             job.npgrp = (uint32_t)(pg_at[s + 1] - pg_at[s]);
             job.plbase = c.ws_pg.as<uint32_t>() + plb_base + plb_at[s];
             job.pseg = pseg_of[s];
+            job.preach = preach_of[s];
+            job.pron = c.ws_pron.as<uint32_t>();
             job.plane = c.ws_plane.as<PLane>();
             job.pbuf = c.ws_pbuf.as<PBuf>();
             if (ntl) {

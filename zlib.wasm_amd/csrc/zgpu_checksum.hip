@@ -166,7 +166,10 @@ __global__ __launch_bounds__(kCkBlock) void k_crc32(const uint8_t *__restrict__ 
 // conflict-free but one block per CU, measured 2 % slower).
 // ------------------------------------------------------------------------
 constexpr int kCsBlock = 1024;
-constexpr int kCsCopyLog = 4;                 // 16 copies per table: 64 KiB, two blocks per CU
+#ifndef ZGPU_CRC_COPY_LOG
+#define ZGPU_CRC_COPY_LOG 4                   // A/B builds: 5 = 32 copies (tools/jobs/r06j.sh)
+#endif
+constexpr int kCsCopyLog = ZGPU_CRC_COPY_LOG; // 16 copies per table: 64 KiB, two blocks per CU
 
 __device__ __attribute__((always_inline)) inline uint32_t s4_at(const uint8_t *T, uint32_t t, uint32_t e,
                                                                 uint32_t loff) {

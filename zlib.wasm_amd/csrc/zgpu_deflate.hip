@@ -1522,15 +1522,57 @@ __device__ __attribute__((always_inline)) inline uint32_t bget(const uint8_t *in
     return (sel4(c.x, c.y, c.z, c.w, o >> 2) >> (8 * (o & 3u))) & 0xffu;
 }
 
-struct SlowLane {
-    uint32_t p, ml, ms, avail;
-    WCache cf, cq;
-    BCache cb;
+// 64-byte lines for the lone-buffer parse (k_pbig1..3): there a wave holds
+// every segment of a buffer and each line a lane leaves is a dependent load of
+// its serial parse; a 64 B line is four positions' worth of a 16 B one
+struct WCache16 {
+    uint32_t base;
+    uint4 a, b, c, d;
 };
+__device__ __attribute__((always_inline)) inline uint32_t sel16(const uint4 &a, const uint4 &b, const uint4 &c,
+                                                                const uint4 &d, uint32_t k) {
+    const uint32_t j = k & 3u;
+    return sel4(sel4(a.x, a.y, a.z, a.w, j), sel4(b.x, b.y, b.z, b.w, j), sel4(c.x, c.y, c.z, c.w, j),
+                sel4(d.x, d.y, d.z, d.w, j), k >> 2);
+}
+__device__ __attribute__((always_inline)) inline uint32_t wget(const uint32_t *a, uint32_t p, WCache16 &c) {
+    const uint32_t b = p & ~15u;
+    if (b != c.base) {
+        const uint4 *q = reinterpret_cast<const uint4 *>(a + b);
+        c.a = q[0]; c.b = q[1]; c.c = q[2]; c.d = q[3];
+        c.base = b;
+    }
+    return sel16(c.a, c.b, c.c, c.d, p & 15u);
+}
+struct BCache64 {
+    uintptr_t base;
+    uint4 a, b, c, d;
+};
+__device__ __attribute__((always_inline)) inline uint32_t bget(const uint8_t *in, uint32_t x, BCache64 &c) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(in + x);
+    const uintptr_t b = a & ~(uintptr_t)63;
+    if (b != c.base) {
+        const uint4 *q = reinterpret_cast<const uint4 *>(b);
+        c.a = q[0]; c.b = q[1]; c.c = q[2]; c.d = q[3];
+        c.base = b;
+    }
+    const uint32_t o = (uint32_t)(a - b);
+    return (sel16(c.a, c.b, c.c, c.d, o >> 2) >> (8 * (o & 3u))) & 0xffu;
+}
+
+template <typename WC, typename BC>
+struct SlowLaneT {
+    uint32_t p, ml, ms, avail;
+    WC cf;
+    BC cb;
+};
+using SlowLane = SlowLaneT<WCache, BCache>;          // k_parse_seg: many lanes in flight hide the loads
+using SlowLaneW = SlowLaneT<WCache16, BCache64>;     // k_pbig*
 
 // one deflate_slow decision (deflate.c:1946-2027) on precomputed results.
 // Returns 0 (no symbol), 1 (literal at spos), 2 (match starting at spos, len).
-__device__ __attribute__((always_inline)) inline int slow_step(SlowLane &L, uint32_t n, const uint32_t *rf, const uint32_t *rq,
+template <typename Lane>
+__device__ __attribute__((always_inline)) inline int slow_step(Lane &L, uint32_t n, const uint32_t *rf, const uint32_t *rq,
                                 const uint8_t *in, const LevelCfg &cfg, bool use_q, bool filtered,
                                 uint32_t &sym, uint32_t &spos, uint32_t &slen) {
     const uint32_t p = L.p;
@@ -1584,9 +1626,10 @@ __device__ inline int64_t slide_threshold(uint32_t k, uint32_t n, int64_t refill
     return a > b ? a : b;
 }
 
-__device__ __attribute__((always_inline)) inline void lane_init(SlowLane &L, uint32_t p, uint32_t avail) {
+template <typename Lane>
+__device__ __attribute__((always_inline)) inline void lane_init(Lane &L, uint32_t p, uint32_t avail) {
     L.p = p; L.ml = kMinMatch - 1; L.ms = 0; L.avail = avail;
-    L.cf.base = L.cq.base = 0xffffffffu;
+    L.cf.base = 0xffffffffu;
     L.cb.base = ~(uintptr_t)0;
 }
 
@@ -1766,7 +1809,7 @@ __global__ __launch_bounds__(kParseLanes) void k_parse_seg(DeflateJob job) {
     const uint32_t rcap = (seg_end - x0 + 15u) >> 4;
     if (mine) {
         L.p = e_p; L.ml = e_ml; L.ms = e_ms; L.avail = e_av;
-        L.cf.base = L.cq.base = 0xffffffffu;
+        L.cf.base = 0xffffffffu;
         L.cb.base = ~(uintptr_t)0;
         while (L.p < end) {
             if (slow_step(L, n, rf, rq, in, cfg, use_q, filtered, sym_v, spos, slen)) {
@@ -2548,7 +2591,7 @@ __global__ __launch_bounds__(kParseLanes) void k_pbig1(DeflateJob job) {
     if (!c.active) return;
     const LevelCfg cfg = job.cfg;
     const bool use_q = cfg.good < cfg.lazy, filtered = job.strategy == 1;
-    SlowLane L;
+    SlowLaneW L;
     uint32_t sym_v, spos, slen;
     const uint32_t x0 = c.xb(c.lane), seg_end = c.seg_end();
     lane_init(L, x0, 0);
@@ -2581,7 +2624,7 @@ __global__ __launch_bounds__(kParseLanes) void k_pbig2(DeflateJob job) {
     const LevelCfg cfg = job.cfg;
     const bool use_q = cfg.good < cfg.lazy, filtered = job.strategy == 1;
     PLane &r = job.plane[c.gl];
-    SlowLane L;
+    SlowLaneW L;
     lane_init(L, r.e_p, r.e_av);
     L.ml = r.e_ml; L.ms = r.e_ms;
     uint32_t sym_v, spos, slen;
@@ -2589,7 +2632,8 @@ __global__ __launch_bounds__(kParseLanes) void k_pbig2(DeflateJob job) {
     bool fail = false;
     if (c.lane + 1 < c.nl) {                          // as k_parse_seg's pass 2
         const uint32_t next_start = c.xb(c.lane + 1);
-        const uint32_t stop = c.lane + 2 >= c.nl ? c.n : c.xb(c.lane + 2);
+        const uint32_t reach = job.preach > 1 ? job.preach : 1u;
+        const uint32_t stop = c.lane + 1 + reach >= c.nl ? c.n : c.xb(c.lane + 1 + reach);
         uint32_t ridx = 0xffffffffu, rw = 0;
         for (;;) {
             if (L.p >= c.n) { y = kEnd; break; }
@@ -2607,28 +2651,77 @@ __global__ __launch_bounds__(kParseLanes) void k_pbig2(DeflateJob job) {
     if (y == kEnd) atomicMin(&job.pbuf[c.bi].first_end, c.lane);
 }
 
+// The lanes whose symbols make the stream: lane 0, then the lane whose segment
+// holds lane 0's meet y(0), then the one holding that lane's meet, ... (the
+// chain of meets); each takes its pass-1 symbols from the previous meet on and
+// its run-on up to its own.  With preach 1 every meet lies in the next segment,
+// so the chain is every lane up to the first whose run-on reached the end.
 __global__ __launch_bounds__(kParseLanes) void k_pbig3(DeflateJob job) {
+    __shared__ uint32_t s_st[kParseLanes], s_p0[kParseLanes];
+    __shared__ uint64_t s_on[kParseLanes / 64];
     const PCtx c = pbig_ctx(job);
-    if (!c.active || job.pbuf[c.bi].fail) return;
+    if (job.pbuf[c.bi].fail) return;                  // uniform: a workgroup's lanes share a buffer
+    const bool chain = job.preach > 1;                // the buffer is this workgroup's (nl <= kParseLanes)
+    const int tid = threadIdx.x;
+    if (chain) {
+        if (tid < 64) {
+            // wave 0: the lanes' next chain lane, 64 at a time in registers, followed with readlane
+            const uint32_t gl0 = job.plbase[c.bi];
+            uint32_t e = 0, prev_y = c.st, prev_sig = 0;
+            bool done = false;
+            for (uint32_t w = 0; w < (uint32_t)kParseLanes; w += 64) {
+                uint64_t on = 0;
+                if (!done && w < c.nl) {
+                    const uint32_t li = w + (uint32_t)tid;
+                    uint32_t y = kEnd, sg = 0;
+                    if (li < c.nl) { y = job.plane[gl0 + li].y; sg = job.plane[gl0 + li].sig; }
+                    const uint32_t nx = y == kEnd ? kEnd : (y - c.st) / c.seg;
+                    while (e < w + 64) {                  // wave-uniform
+                        const uint32_t k = e - w;
+                        on |= 1ull << k;
+                        if (tid == 0) { s_st[e] = prev_y; s_p0[e] = prev_y - prev_sig; }
+                        const uint32_t ye = (uint32_t)__builtin_amdgcn_readlane((int)y, (int)k);
+                        if (ye == kEnd) { done = true; break; }
+                        prev_sig = (uint32_t)__builtin_amdgcn_readlane((int)sg, (int)k);
+                        prev_y = ye;
+                        e = (uint32_t)__builtin_amdgcn_readlane((int)nx, (int)k);
+                    }
+                }
+                if (tid == 0) s_on[w >> 6] = on;
+            }
+        }
+        __syncthreads();
+    }
+    if (!c.active) return;
     const LevelCfg cfg = job.cfg;
     const bool use_q = cfg.good < cfg.lazy, filtered = job.strategy == 1;
     PLane &r = job.plane[c.gl];
-    const bool mine = c.lane <= job.pbuf[c.bi].first_end;
+    bool mine;
+    uint32_t start, p0;
+    if (chain) {
+        mine = (s_on[c.lane >> 6] >> (c.lane & 63u)) & 1u;
+        start = s_st[c.lane];
+        p0 = s_p0[c.lane];
+    } else {
+        mine = c.lane <= job.pbuf[c.bi].first_end;
+        start = c.lane > 0 ? job.plane[c.gl - 1].y : 0u;
+        p0 = c.lane > 0 ? job.plane[c.gl - 1].y - job.plane[c.gl - 1].sig : c.st;
+    }
     const uint32_t x0 = c.xb(c.lane), seg_end = c.seg_end();
-    const uint32_t start = c.lane > 0 ? job.plane[c.gl - 1].y : 0u;
     const uint32_t yend = r.y, end = yend == kEnd ? c.n : yend;
-    SlowLane L;
+    SlowLaneW L;
     uint32_t sym_v, spos, slen;
     uint32_t kstart = 0;
-    if (mine && c.lane > 0) {                         // pass-1 symbols before y(i-1) are not this lane's
+    if (mine && c.lane > 0) {                         // pass-1 symbols before the previous meet are not this lane's
         lane_init(L, x0, 0);
         while (L.p < start)
             if (slow_step(L, c.n, c.rf, c.rq, c.in, cfg, use_q, filtered, sym_v, spos, slen)) kstart++;
     }
     uint32_t rcnt = 0;
-    uint32_t *ron = c.sst + (x0 >> 4);
-    const uint32_t rcap = (seg_end - x0 + 15u) >> 4;
-    if (mine) {                                       // the run-on, staged in the lane's dead state words
+    // the run-on, staged in the lane's dead state words (or its pron slot)
+    uint32_t *ron = chain ? job.pron + (size_t)c.gl * kRonCap : c.sst + (x0 >> 4);
+    const uint32_t rcap = chain ? kRonCap : (seg_end - x0 + 15u) >> 4;
+    if (mine) {
         lane_init(L, r.e_p, r.e_av);
         L.ml = r.e_ml; L.ms = r.e_ms;
         while (L.p < end) {
@@ -2647,6 +2740,7 @@ __global__ __launch_bounds__(kParseLanes) void k_pbig3(DeflateJob job) {
     r.kstart = kstart;
     r.rcnt = rcnt;
     r.cnt = mine ? r.k1 - kstart + rcnt : 0u;
+    r.p0 = p0;
 }
 
 constexpr int kPScanThreads = 1024;
@@ -2686,35 +2780,31 @@ __global__ __launch_bounds__(kPScanThreads) void k_pbig4(DeflateJob job) {
     if (tid == 0) job.pbuf[bi].total = run;
 }
 
-__global__ __launch_bounds__(kParseLanes) void k_pbig5(DeflateJob job) {
-    const PCtx c = pbig_ctx(job);
+// one workgroup per lane group as k_pbig1..3, with kP5Threads threads: the
+// group's lanes are copied by all its waves in turn (lane t by wave t mod
+// waves), where k_parse_seg's compaction has each wave copy its own 64 lanes.
+// A lone buffer's 64..256 lanes are then not one wave's serial chain.
+constexpr int kP5Threads = 1024;
+__global__ __launch_bounds__(kP5Threads) void k_pbig5(DeflateJob job) {
+    const PCtx c = pbig_ctx(job);                     // per-buffer fields only (lane is threadIdx-based)
     const PBuf pb = job.pbuf[c.bi];
     if (pb.fail) return;                              // uniform: a workgroup's lanes share a buffer
-    const int wl = threadIdx.x & 63;
+    const int wl = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t symlim = job_win(job).sym_limit;
     const uint32_t total = pb.total;
     const uint32_t ncut = total / symlim - ((pb.fin && total % symlim == 0) ? 1u : 0u);
-    uint32_t cnt = 0, base = 0, c1 = 0, x0 = 0, kstart = 0, pos0 = c.st;
     const bool filtered = job.strategy == 1;
-    if (c.active) {
-        const PLane &r = job.plane[c.gl];
-        cnt = r.cnt;
-        base = r.base;
-        c1 = cnt - r.rcnt;
-        x0 = c.xb(c.lane);
-        kstart = r.kstart;
-        if (c.lane > 0) {
-            const PLane &q = job.plane[c.gl - 1];
-            pos0 = q.y - q.sig;                       // the lane's symbols tile the input from here
-        }
-    }
-    // as k_parse_seg's compaction: each wave copies its own lanes' symbols
-    for (int j = 0; j < 64; j++) {
-        const uint32_t jc = __shfl(cnt, j, 64), jb = __shfl(base, j, 64);
+    const uint32_t lane0 = job.pgrp[2 * blockIdx.x + 1], gl0 = job.plbase[c.bi];
+    for (uint32_t tl = (uint32_t)wv; tl < (uint32_t)kParseLanes; tl += kP5Threads / 64) {
+        const uint32_t jl = lane0 + tl;
+        if (jl >= c.nl) break;                        // wave-uniform
+        const PLane &r = job.plane[gl0 + jl];
+        const uint32_t jc = r.cnt;
         if (jc == 0) continue;
-        const uint32_t jc1 = __shfl(c1, j, 64), jx = __shfl(x0, j, 64), jk = __shfl(kstart, j, 64);
-        uint32_t run = __shfl(pos0, j, 64);
-        const uint32_t *s1 = c.stg + jx + jk, *s2 = c.sst + (jx >> 4);
+        const uint32_t jb = r.base, jc1 = jc - r.rcnt, jx = c.xb(jl), jk = r.kstart;
+        uint32_t run = r.p0;                          // the lane's symbols tile the input from here
+        const uint32_t *s1 = c.stg + jx + jk;
+        const uint32_t *s2 = job.preach > 1 ? job.pron + (size_t)(gl0 + jl) * kRonCap : c.sst + (jx >> 4);
         for (uint32_t k = 0; k < jc; k += 64) {
             const uint32_t idx = k + (uint32_t)wl;
             const bool have = idx < jc;
@@ -3751,25 +3841,47 @@ __device__ __attribute__((always_inline)) inline uint32_t rget_any(const RHeap &
     default: return rl(H.r[4], j & 63u);
     }
 }
+// Slots past heap_len hold kHInf, a key above every real one (freqs < 2^16
+// with depth and node below), so a sift needs no bounds tests: an absent
+// child is never the smaller one (zlib takes j + 1 only when it exists and is
+// <= heap[j]) and v <= kHInf ends the sift where zlib finds no child.
+constexpr uint32_t kHInf = 0xffffffffu;
+// children j, j + 1 (j even, same register) on heap level L
+template <int L>
+__device__ __attribute__((always_inline)) inline void rget2(const RHeap &H, uint32_t j, uint32_t &a, uint32_t &b) {
+    const uint32_t l = j & 63u;
+    if constexpr (L <= 5) { a = rl(H.r[0], l); b = rl(H.r[0], l + 1); }
+    else if constexpr (L == 6) { a = rl(H.r[1], l); b = rl(H.r[1], l + 1); }
+    else if constexpr (L == 7) {                     // per-register reads (a select of registers would index H)
+        const uint32_t a2 = rl(H.r[2], l), b2 = rl(H.r[2], l + 1), a3 = rl(H.r[3], l), b3 = rl(H.r[3], l + 1);
+        a = (j & 64u) ? a3 : a2;
+        b = (j & 64u) ? b3 : b2;
+    } else {                                         // slots 320.. are past any heap_len (<= 286)
+        a = j < 320u ? rl(H.r[4], l) : kHInf;
+        b = j < 320u ? rl(H.r[4], l + 1) : kHInf;
+    }
+}
 // pqdownheap (trees.c:509-527) of key v entering at node k of level D
 template <int D>
-__device__ __attribute__((always_inline)) inline void r_down(RHeap &H, int heap_len, uint32_t k, uint32_t v) {
+__device__ __attribute__((always_inline)) inline void r_down(RHeap &H, int, uint32_t k, uint32_t v) {
     if constexpr (D < 8) {
-        uint32_t j = k << 1;
-        if ((int)j <= heap_len) {
-            uint32_t hj = rget<D + 1>(H, j);
-            if ((int)j < heap_len) {
-                const uint32_t hj1 = rget<D + 1>(H, j + 1);
-                if (hle(hj1, hj)) { j++; hj = hj1; }
-            }
-            if (!hle(v, hj)) {
-                rset<D>(H, k, hj);
-                r_down<D + 1>(H, heap_len, j, v);
-                return;
-            }
+        const uint32_t j = k << 1;
+        uint32_t a, b;
+        rget2<D + 1>(H, j, a, b);
+        const bool right = hle(b, a);                   // trees.c:515: heap[j+1] <= heap[j]
+        const uint32_t hj = right ? b : a;
+        if (!hle(v, hj)) {
+            rset<D>(H, k, hj);
+            r_down<D + 1>(H, 0, right ? j + 1 : j, v);
+            return;
         }
     }
     rset<D>(H, k, v);
+}
+__device__ __attribute__((always_inline)) inline void rset_any(RHeap &H, uint32_t j, uint32_t v) {
+    const bool me = (threadIdx.x & 63u) == (j & 63u);
+#pragma unroll
+    for (int r = 0; r < 5; r++) H.r[r] = (me && (j >> 6) == (uint32_t)r) ? v : H.r[r];
 }
 __device__ inline void r_down_any(RHeap &H, int heap_len, uint32_t k) {   // build_tree's heapify
     const uint32_t v = rget_any(H, k);
@@ -3814,7 +3926,7 @@ __device__ __attribute__((always_inline)) inline void w_build(TreeRef &t, TreeLD
 #pragma unroll
     for (int r = 0; r < 5; r++) {
         const int j = r * 64 + (int)lane;
-        H.r[r] = (j >= 1 && j <= heap_len) ? hs[j] : 0u;
+        H.r[r] = (j >= 1 && j <= heap_len) ? hs[j] : kHInf;
     }
     for (int k = heap_len / 2; k >= 1; k--) r_down_any(H, heap_len, (uint32_t)k);
     int heap_max = kHeapSize;
@@ -3822,6 +3934,7 @@ __device__ __attribute__((always_inline)) inline void w_build(TreeRef &t, TreeLD
     do {                                               // trees.c:583-604
         const uint32_t kn = rl(H.r[0], 1);
         const uint32_t last = rget_any(H, (uint32_t)heap_len);
+        rset_any(H, (uint32_t)heap_len, kHInf);
         heap_len--;
         r_down<0>(H, heap_len, 1, last);
         const uint32_t km = rl(H.r[0], 1);
@@ -4058,16 +4171,21 @@ __device__ __attribute__((always_inline)) inline void block_plan(const DeflateJo
             const uint32_t i = i0 + 64 * u + (uint32_t)lane;
             v[u] = i < br.nsym ? sym[br.sym_start + i] : 0xffffffffu;
         }
+        // every table lookup of the batch is issued before the first atomic: one
+        // load latency per batch, not one per symbol (a lone block's histogram)
+        uint32_t li[kHU], di[kHU];
+#pragma unroll
+        for (uint32_t u = 0; u < kHU; u++) {
+            const uint32_t dist = v[u] >> 8, lc = v[u] & 0xffu, d = dist - 1u;
+            const bool m = v[u] != 0xffffffffu && dist != 0;
+            li[u] = m ? c_ct.len_code[lc] + 257u : lc;
+            di[u] = m ? (d < 256 ? c_ct.dist_code[d] : c_ct.dist_code[256 + ((d >> 7) & 255u)]) : 0u;
+        }
 #pragma unroll
         for (uint32_t u = 0; u < kHU; u++) {
             if (v[u] == 0xffffffffu) continue;
-            const uint32_t dist = v[u] >> 8, lc = v[u] & 0xffu;
-            if (dist == 0) atomicAdd(&hl[lc], 1u);
-            else {
-                atomicAdd(&hl[c_ct.len_code[lc] + 257], 1u);
-                const uint32_t d = dist - 1;
-                atomicAdd(&hd[d < 256 ? c_ct.dist_code[d] : c_ct.dist_code[256 + (d >> 7)]], 1u);
-            }
+            atomicAdd(&hl[li[u]], 1u);
+            if (v[u] >> 8) atomicAdd(&hd[di[u]], 1u);
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -5455,7 +5573,7 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         hipLaunchKernelGGL(k_pbig2, pg, dim3(kParseLanes), 0, st, job);
         hipLaunchKernelGGL(k_pbig3, pg, dim3(kParseLanes), 0, st, job);
         hipLaunchKernelGGL(k_pbig4, grid, dim3(kPScanThreads), 0, st, job);
-        hipLaunchKernelGGL(k_pbig5, pg, dim3(kParseLanes), 0, st, job);
+        hipLaunchKernelGGL(k_pbig5, pg, dim3(kP5Threads), 0, st, job);
         hipLaunchKernelGGL(k_pbig6, bg, dim3(256), 0, st, job);
         break;
     }
@@ -5465,7 +5583,7 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         hipLaunchKernelGGL(k_pbig2, pg, dim3(kParseLanes), 0, st, job);
         hipLaunchKernelGGL(k_pbig3, pg, dim3(kParseLanes), 0, st, job);
         hipLaunchKernelGGL(k_pbig4, grid, dim3(kPScanThreads), 0, st, job);
-        hipLaunchKernelGGL(k_pbig5, pg, dim3(kParseLanes), 0, st, job);
+        hipLaunchKernelGGL(k_pbig5, pg, dim3(kP5Threads), 0, st, job);
         hipLaunchKernelGGL(k_pbig6s, dim3(1), dim3(256), 0, st, job);
         break;
     }
@@ -5473,7 +5591,8 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         // trees on the whole wave while few blocks are in flight (latency), on
         // one lane when many are (the other waves hide it), as for k_encode
         const dim3 plg((job.maxblk + kEncGroup - 1) / kEncGroup, job.count), eg(job.maxblk, job.count);
-        if ((uint64_t)job.maxblk * job.count < 16384)
+        static const bool plan_lane = std::getenv("ZGPU_PLAN_LANE") != nullptr;   // A/B: one-lane trees always
+        if ((uint64_t)job.maxblk * job.count < 16384 && !plan_lane)
             hipLaunchKernelGGL(k_enc_plan<true>, plg, dim3(kEncThreads), 0, st, job);
         else
             hipLaunchKernelGGL(k_enc_plan1, dim3(job.maxblk, job.count), dim3(64), 0, st, job);

@@ -112,8 +112,9 @@ struct PLane {
     uint32_t k1;                      // pass-1 symbols staged
     uint32_t y, sig;                  // pass 2: where the parse meets the next lane's (~0: the end), pending literal
     uint32_t kstart, rcnt, cnt, base; // pass-1 symbols before y(i-1), run-on symbols, the lane's count, first index
-    uint32_t pad;
+    uint32_t p0;                      // first input position the lane's symbols cover (k_pbig5)
 };
+constexpr uint32_t kRonCap = 64;      // run-on symbols per lane when preach > 1
 struct PBuf { uint32_t fail, first_end, fin, total; };
 constexpr uint32_t kParseLanesHost = 256;   // lanes (segments) per k_pbig* / k_parse_seg workgroup
 
@@ -274,6 +275,12 @@ struct DeflateJob {
     // records a buffer may have
     const uint32_t *pgrp;
     uint32_t npgrp, pseg, maxblk;
+    // preach: segments a lane's run-on may cross before it must meet a later
+    // lane's pass 1 (1: the next one).  Above 1 only when every buffer has at
+    // most kParseLanes lanes (one workgroup each), which k_pbig3 then joins
+    // along the chain of meets; run-on symbols go to pron (kRonCap per lane)
+    uint32_t preach;
+    uint32_t *pron;
     const uint32_t *plbase;
     PLane *plane;
     PBuf *pbuf;
