@@ -90,6 +90,26 @@ def test_stage_links_and_match_vs_oracle(zg, oracle, level, kind, n):
         bad = np.nonzero(rq != oq)[0]
         assert bad.size == 0, f"rquart differ at {bad[:5]}: gpu {rq[bad[:5]]} oracle {oq[bad[:5]]}"
 
+@pytest.mark.parametrize("seg", [4096, 16384, 65536])
+def test_stage_links_and_match_segments_vs_oracle(zg, oracle, seg, monkeypatch):
+    """The per-segment stages of a sub-batch of few large buffers (k_links_seg1
+    for segments up to 16 KiB: head[] at the segment start from one atomicMax
+    pass over the window; k_links<kSegs> and k_match<kSegs> otherwise), per
+    position against the oracle, across segment edges and ragged tails."""
+    monkeypatch.setenv("ZGPU_DEBUG_SEG", str(seg))
+    for kind, n, level in (("text", 70001, 6), ("mix", 150000, 9), ("runs", 65536, 4), ("records", 40000, 6)):
+        data = datagen.make(kind, n, 23)
+        link, rf, rq = zg.debug_stages(data, level)
+        olink = oracle.links(data)
+        bad = np.nonzero(link != olink)[0]
+        assert bad.size == 0, f"{kind} seg {seg}: links differ at {bad[:10]}"
+        of, oq = oracle.match(data, level, olink)
+        bad = np.nonzero(rf != of)[0]
+        assert bad.size == 0, f"{kind} seg {seg}: rfull differ at {bad[:5]}"
+        if level >= 5:
+            assert np.array_equal(rq, oq), f"{kind} seg {seg}: rquart differ"
+
+
 @pytest.mark.parametrize("level", list(range(10)))
 def test_deflate_golden(zg, golden, level):
     cases = [c for c in golden["cases"] if c["n"] <= (1 << 20)]

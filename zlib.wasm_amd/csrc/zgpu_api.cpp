@@ -471,7 +471,8 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
                        uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
                        uint64_t *dst_len, int32_t *status, uint32_t count, int level, int wrap,
                        int strategy, hipStream_t st, const FlushSpec *fs = nullptr, int wbits = 15,
-                       int mem_level = 8, const LevelCfg *tune = nullptr, uint8_t *d_wind = nullptr) {
+                       int mem_level = 8, const LevelCfg *tune = nullptr, uint8_t *d_wind = nullptr,
+                       const uint64_t *host_len = nullptr) {
     if (level == -1) level = 6;
     if (level < 0 || level > 9 || wrap < 0 || wrap > 2 || strategy < 0 || strategy > 4 || wbits < 9 ||
         wbits > 15 || mem_level < 1 || mem_level > 9)
@@ -481,10 +482,15 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     const uint64_t hsize = 1ull << hbits;
     if (fs && (count != 1 || (level == 0) != (fs->plan != nullptr))) return ZGPU_STREAM_ERROR;
     if (count == 0) return ZGPU_OK;
+    // the lengths plan the sub-batches: the host path passes its own copy (a
+    // lone call saves a device-to-host copy and a stream synchronisation)
     std::vector<uint64_t> lens(count);
-    if (hipMemcpyAsync(lens.data(), src_len, 8ull * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
+    if (host_len) {
+        std::memcpy(lens.data(), host_len, 8ull * count);
+    } else if (hipMemcpyAsync(lens.data(), src_len, 8ull * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
+               hipStreamSynchronize(st) != hipSuccess) {
         return zfail(__LINE__);
+    }
     for (uint32_t i = 0; i < count; i++)
         if (lens[i] >= kMaxBuffer) return ZGPU_STREAM_ERROR;   // 32-bit positions in the kernels
 
@@ -1051,11 +1057,17 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
     for (size_t i = 0; i < count; i++)
         if (src_len[i] && hipMemcpyAsync(d_in + so[i], src[i], src_len[i], hipMemcpyHostToDevice, st) != hipSuccess)
             return ZGPU_MEM_ERROR;
-    if (hipMemcpyAsync(d_so, so.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_sl, sl.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_do, dofs.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_dc, dcap.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess)
-        return ZGPU_MEM_ERROR;
+    std::vector<uint64_t> m4;                          // alive until the call returns (the upload's source)
+    {   // d_so, d_sl, d_do, d_dc are consecutive: one upload (a lone call's latency is its copies)
+        m4.reserve(4 * count);
+        m4.insert(m4.end(), so.begin(), so.end());
+        m4.insert(m4.end(), sl.begin(), sl.end());
+        m4.insert(m4.end(), dofs.begin(), dofs.end());
+        m4.insert(m4.end(), dcap.begin(), dcap.end());
+        (void)d_sl; (void)d_dc;
+        if (hipMemcpyAsync(d_so, m4.data(), 32 * count, hipMemcpyHostToDevice, st) != hipSuccess)
+            return ZGPU_MEM_ERROR;
+    }
     FlushSpec fs{};
     if (fh) {
         uint64_t *d_fp = reinterpret_cast<uint64_t *>(d_st + 2 * count);   // 8-aligned
@@ -1118,7 +1130,7 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
     if (wind_out && !c.ws_wind.ensure(count + 64)) return ZGPU_MEM_ERROR;
     int rc = deflate_dev_locked(c, d_in, d_so, d_sl, d_out, d_do, d_dc, d_dl, d_st, (uint32_t)count,
                                 level, wrap, strategy, st, fh ? &fs : nullptr, wbits, mem_level, tune,
-                                wind_out ? c.ws_wind.as<uint8_t>() : nullptr);
+                                wind_out ? c.ws_wind.as<uint8_t>() : nullptr, sl.data());
     if (fh) ZTRACE("chl: ran rc %d\n", rc);
     if (rc) return rc;
     if (wind_out && copy_sync(wind_out, c.ws_wind.p, count, hipMemcpyDeviceToHost, st) != hipSuccess)
@@ -1668,11 +1680,17 @@ int uncompress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_
     for (size_t i = 0; i < count; i++)
         if (src_len[i] && hipMemcpyAsync(d_in + so[i], src[i], src_len[i], hipMemcpyHostToDevice, st) != hipSuccess)
             return ZGPU_MEM_ERROR;
-    if (hipMemcpyAsync(d_so, so.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_sl, sl.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_do, dofs.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(d_dc, dcap.data(), 8 * count, hipMemcpyHostToDevice, st) != hipSuccess)
-        return ZGPU_MEM_ERROR;
+    std::vector<uint64_t> m4;                          // alive until the call returns (the upload's source)
+    {   // d_so, d_sl, d_do, d_dc are consecutive: one upload (a lone call's latency is its copies)
+        m4.reserve(4 * count);
+        m4.insert(m4.end(), so.begin(), so.end());
+        m4.insert(m4.end(), sl.begin(), sl.end());
+        m4.insert(m4.end(), dofs.begin(), dofs.end());
+        m4.insert(m4.end(), dcap.begin(), dcap.end());
+        (void)d_sl; (void)d_dc;
+        if (hipMemcpyAsync(d_so, m4.data(), 32 * count, hipMemcpyHostToDevice, st) != hipSuccess)
+            return ZGPU_MEM_ERROR;
+    }
     int rc = inflate_dev_locked(c, d_in, d_so, d_sl, d_out, d_do, d_dc, d_dl, d_used, d_st, d_stop,
                                 (uint32_t)count, wrap, wbits, st);
     if (rc) return rc;
@@ -2097,6 +2115,21 @@ int zgpu_debug_stages(const uint8_t *src, size_t n, int level, uint16_t *link, u
     job.rquart = c.ws_rq.as<uint32_t>();
     job.key = c.ws_key.as<uint8_t>();
     job.links_gh = n >= kLinksGhMin;                  // as the batch path picks k_links' head[] place
+    // ZGPU_DEBUG_SEG=<bytes> (tests): run the stages per segment of that many
+    // bytes (a multiple of kMatchTile), as a sub-batch of few large buffers does
+    if (const char *dseg = std::getenv("ZGPU_DEBUG_SEG"); dseg && n) {
+        const uint64_t sl = (uint64_t)std::atoll(dseg);
+        if (sl == 0 || sl % kMatchTile) return ZGPU_STREAM_ERROR;
+        std::vector<uint32_t> segs;
+        for (uint64_t o = 0; o < n; o += sl) { segs.push_back(0); segs.push_back((uint32_t)o); }
+        if (!c.ws_seg.ensure(4 * segs.size()) ||
+            copy_sync(c.ws_seg.p, segs.data(), 4 * segs.size(), hipMemcpyHostToDevice, st) != hipSuccess)
+            return ZGPU_MEM_ERROR;
+        job.seg = c.ws_seg.as<uint32_t>();
+        job.nseg = (uint32_t)(segs.size() / 2);
+        job.seg_len = (uint32_t)sl;
+        job.links_gh = 0;
+    }
     if (launch_deflate_stage(0, job, nullptr, st) || launch_deflate_stage(1, job, nullptr, st) ||
         hipStreamSynchronize(st) != hipSuccess)
         return ZGPU_MEM_ERROR;

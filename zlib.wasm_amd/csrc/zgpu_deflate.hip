@@ -337,6 +337,103 @@ __global__ __launch_bounds__(kLThreads, 8) void k_links_gh(DeflateJob job) {
 }
 
 // ------------------------------------------------------------------------
+// k_links_seg1 — k_links for one segment [s0, s1) of a sub-batch of few
+// large buffers (job.seg; hash_bits <= 15, no uploaded chains, segments of at
+// most kLS1Max positions), without walking the 32 Ki window before s0 chunk
+// by chunk.  A link needs from before s0 only head[] as it stands there (the
+// most recent inserted q < s0 per hash, deflate.c:160-163), and that is an
+// order-free maximum: one pass of LDS atomicMax over the window's positions
+// (32 per thread, their bytes loaded at once).  The segment then takes kLS1C
+// positions at a time as k_links does, head[] holding 32-bit positions + 1
+// (0: none, so no sweep).  A lone 64 KiB compress2 walked 5 chunks of 8 Ki
+// per segment in a row before this (107 us).
+// ------------------------------------------------------------------------
+constexpr int kLS1C = 2048;
+constexpr int64_t kLS1Max = 16384;
+__global__ __launch_bounds__(kLThreads) void k_links_seg1(DeflateJob job) {
+    __shared__ uint32_t head[32768];
+    __shared__ uint32_t ka[kLS1C];
+    __shared__ __attribute__((aligned(16))) uint16_t lk[kLS1C + 16];   // first the chunk's bytes
+    uint8_t *const stage = reinterpret_cast<uint8_t *>(lk);
+    __shared__ uint16_t wcnt[kLWaves][256];
+    __shared__ int wsum[kLWaves];
+    const int tid = threadIdx.x;
+    const uint32_t bi = job.seg[2 * blockIdx.x];
+    const uint32_t g = job.first + bi;
+    const int64_t n = (int64_t)job.src_len[g];
+    const uint8_t *in = job.src + job.src_off[g];
+    uint16_t *out = job.link + job.ws_off[bi];
+    const WinP wp = job_win(job);
+    const int64_t s0 = (int64_t)job.seg[2 * blockIdx.x + 1];
+    const int64_t s1 = s0 + (int64_t)job.seg_len < n ? s0 + (int64_t)job.seg_len : n;
+    auto skipped = [&](int64_t p) {                      // huff/rle stretches (SkipSpec): not inserted
+        for (uint32_t k = 0; k < job.sk.n; k++)
+            if ((uint64_t)p >= job.sk.a[k] && (uint64_t)p < job.sk.b[k]) return true;
+        return false;
+    };
+    for (int i = tid; i < 32768; i += kLThreads) head[i] = 0;
+    __syncthreads();
+    {   // the window [max(1, s0 - 32767), s0): q is a candidate of some p >= s0 (position 0 is NIL)
+        const int64_t w0 = s0 - 32767 > 1 ? s0 - 32767 : 1, w1 = s0 < n - 2 ? s0 : n - 2;
+        const int64_t q0 = w0 + 32ll * tid;
+        if (q0 < w1) {
+            uint32_t wb[9];                              // bytes q0 .. q0 + 35
+            const uintptr_t a = reinterpret_cast<uintptr_t>(in + q0);
+            const uint32_t sh = (uint32_t)(a & 3u);
+            const uint32_t *qw = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+            const int64_t lim = n - q0;                  // bytes of the buffer from q0 on
+            uint32_t d[10];
+#pragma unroll
+            for (int j = 0; j < 10; j++)                 // whole words inside the buffer's allocation
+                d[j] = 4ll * j - (int64_t)sh < lim ? qw[j] : 0u;
+#pragma unroll
+            for (int j = 0; j < 9; j++) wb[j] = sh ? __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh) : d[j];
+#pragma unroll
+            for (int j = 0; j < 32; j++) {
+                const int64_t q = q0 + j;
+                if (q >= w1) break;
+                const uint32_t b0 = (wb[j >> 2] >> (8 * (j & 3))) & 0xffu;
+                const uint32_t b1 = (wb[(j + 1) >> 2] >> (8 * ((j + 1) & 3))) & 0xffu;
+                const uint32_t b2 = (wb[(j + 2) >> 2] >> (8 * ((j + 2) & 3))) & 0xffu;
+                if (job.sk.n && skipped(q)) continue;
+                atomicMax(&head[hashp(b0, b1, b2, wp)], (uint32_t)q + 1u);
+            }
+        }
+    }
+    for (int64_t c0 = s0; c0 < s1; c0 += kLS1C) {
+        __syncthreads();
+        stage_bytes<kLThreads, 1>(stage, in, c0, ((kLS1C + 16) / 16) * 16, n, tid);
+        __syncthreads();
+        const int cnt = (int)((s1 - c0) < kLS1C ? (s1 - c0) : kLS1C);
+        const int m = (int)((n - 2 - c0) < cnt ? ((n - 2 - c0) > 0 ? n - 2 - c0 : 0) : cnt);   // p <= n-3
+        for (int e = tid; e < m; e += kLThreads) {
+            uint32_t h = hashp(stage[e], stage[e + 1], stage[e + 2], wp);
+            if (job.sk.n && skipped(c0 + e)) h = kSkipHash;
+            ka[e] = h << 11 | (uint32_t)e;
+        }
+        links_radix_pass(ka, ka, m, 11, wcnt, wsum, tid);
+        links_radix_pass(ka, ka, m, 19, wcnt, wsum, tid);
+        for (int i = tid; i < m; i += kLThreads) {
+            const uint32_t key = ka[i];
+            const uint32_t h = key >> 11, e = key & (kLS1C - 1);
+            const int64_t p = c0 + e;
+            int64_t dd;
+            if (h == kSkipHash) dd = 0;
+            else if (i > 0 && (ka[i - 1] >> 11) == h) dd = e - (ka[i - 1] & (kLS1C - 1));
+            else dd = head[h] ? p - ((int64_t)head[h] - 1) : 0;
+            lk[e] = (uint16_t)(dd > 0 && dd <= 32767 && dd != p ? dd : 0);     // position 0 is NIL
+        }
+        __syncthreads();
+        for (int i = tid; i < m; i += kLThreads) {
+            const uint32_t key = ka[i];
+            if ((key >> 11) != kSkipHash && (i == m - 1 || (ka[i + 1] >> 11) != (key >> 11)))
+                head[key >> 11] = (uint32_t)(c0 + (key & (kLS1C - 1))) + 1u;
+        }
+        for (int e = tid; e < cnt; e += kLThreads) out[c0 + e] = e < m ? lk[e] : (uint16_t)0;
+    }
+}
+
+// ------------------------------------------------------------------------
 // k_count — the order in which k_match walks a tile's positions.  For every
 // position p: the number of earlier positions q in (p - MAX_DIST, p) with the
 // same hash, i.e. the candidates a chain walk from p can visit, capped at the
@@ -383,7 +480,38 @@ __global__ __launch_bounds__(kCntThreads) void k_count(DeflateJob job) {
     const int64_t s1 = kSegs && s0 + (int64_t)job.seg_len < n ? s0 + (int64_t)job.seg_len : n;
     const int64_t c0 = kSegs && s0 > kMaxDist ? (s0 - kMaxDist) / kCntStage * kCntStage : 0;
     for (int i = tid; i < 16384; i += kCntThreads) cnt[i] = 0;
-    for (int64_t t0 = c0; t0 < s1; t0 += kCntStage) {
+    int64_t tstart = c0;
+    if (kSegs && s0 > 0) {
+        // the window of s0, [s0 - MAX_DIST, s0), counted in one pass (32 positions per thread, their
+        // bytes loaded at once) instead of stage after stage from c0 (a lone 64 KiB compress2: 9 stages
+        // per 4 KiB segment); the stages then run from s0, as the window slides over counted positions
+        static_assert(kMaxDist <= 32 * kCntThreads, "one pass");
+        __syncthreads();
+        const int64_t w0 = s0 - kMaxDist > 1 ? s0 - kMaxDist : 1;    // s0's first stage subtracts s0 - MAX_DIST
+        const int64_t q0 = w0 + 32ll * tid;
+        if (q0 < s0) {
+            const uintptr_t a = reinterpret_cast<uintptr_t>(in + q0);
+            const uint32_t sh = (uint32_t)(a & 3u);
+            const uint32_t *qw = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+            const int64_t lim = n - q0;
+            uint32_t d[10], wb[9];
+#pragma unroll
+            for (int j = 0; j < 10; j++) d[j] = 4ll * j - (int64_t)sh < lim ? qw[j] : 0u;
+#pragma unroll
+            for (int j = 0; j < 9; j++) wb[j] = sh ? __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh) : d[j];
+#pragma unroll
+            for (int j = 0; j < 32; j++) {
+                const int64_t q = q0 + j;
+                if (q >= s0 || q + 3 > n) break;
+                const uint32_t h = hash3((wb[j >> 2] >> (8 * (j & 3))) & 0xffu,
+                                         (wb[(j + 1) >> 2] >> (8 * ((j + 1) & 3))) & 0xffu,
+                                         (wb[(j + 2) >> 2] >> (8 * ((j + 2) & 3))) & 0xffu);
+                atomicAdd(&cnt[h >> 1], 1u << ((h & 1u) * 16));
+            }
+        }
+        tstart = s0;
+    }
+    for (int64_t t0 = tstart; t0 < s1; t0 += kCntStage) {
         __syncthreads();
         stage_bytes<kCntThreads, (kCntStage + 16) / 16 / kCntThreads + 1>(s_in, in, t0, kCntStage + 16, n, tid);
         stage_bytes<kCntThreads, (kCntStage + 16) / 16 / kCntThreads + 1>(s_out, in, t0 - kMaxDist,
@@ -393,7 +521,7 @@ __global__ __launch_bounds__(kCntThreads) void k_count(DeflateJob job) {
         for (int64_t p = t0 + tid; p < tend; p += kCntThreads) {
             const int j = (int)(p - t0);
             const int64_t q = p - kMaxDist;                   // leaves p's window
-            if (q >= 1 && q >= c0 && q + 3 <= n) {              // (counted: q >= c0)
+            if (q >= 1 && q >= c0 && q + 3 <= n) {              // (counted: q >= c0, or in s0's window)
                 const uint32_t h = hash3(s_out[j], s_out[j + 1], s_out[j + 2]);
                 atomicSub(&cnt[h >> 1], 1u << ((h & 1u) * 16));
             }
@@ -3897,9 +4025,22 @@ __device__ inline void r_down_any(RHeap &H, int heap_len, uint32_t k) {   // bui
     }
 }
 
+// ZGPU_PLAN_CLOCK (a timing build, tools/plan_clock.py): s_memtime stamps of
+// the first block's tree build in k_enc_plan<true>, written by lane 0 with
+// vector stores; zgpu_plan_clock_read copies them out
+#ifdef ZGPU_PLAN_CLOCK
+__device__ unsigned long long g_pclk[32];
+#define PCLK(i) do { if (pclk && (threadIdx.x & 63u) == 0) pclk[i] = (unsigned long long)__builtin_amdgcn_s_memtime(); } while (0)
+extern "C" int zgpu_plan_clock_read(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pclk), sizeof(g_pclk)) == hipSuccess ? 0 : -1;
+}
+#else
+#define PCLK(i) do { (void)pclk; } while (0)
+#endif
 // Called by all 64 lanes of a wave with wave-uniform arguments; opt_len/static_len stay uniform.
 __device__ __attribute__((always_inline)) inline void w_build(TreeRef &t, TreeLDS &h, int elems, const uint8_t *slen, const uint8_t *extra,
-                        int xbase, int max_length, int64_t &opt_len, int64_t &static_len) {
+                        int xbase, int max_length, int64_t &opt_len, int64_t &static_len,
+                        unsigned long long *pclk = nullptr) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t below = (1ull << lane) - 1ull;
     uint32_t *hs = h.heap;
@@ -3922,6 +4063,7 @@ __device__ __attribute__((always_inline)) inline void w_build(TreeRef &t, TreeLD
     }
     t.max_code = max_code;
     __builtin_amdgcn_wave_barrier();
+    PCLK(10);
     RHeap H;
 #pragma unroll
     for (int r = 0; r < 5; r++) {
@@ -3929,6 +4071,7 @@ __device__ __attribute__((always_inline)) inline void w_build(TreeRef &t, TreeLD
         H.r[r] = (j >= 1 && j <= heap_len) ? hs[j] : kHInf;
     }
     for (int k = heap_len / 2; k >= 1; k--) r_down_any(H, heap_len, (uint32_t)k);
+    PCLK(11);
     int heap_max = kHeapSize;
     uint32_t node = (uint32_t)elems;
     do {                                               // trees.c:583-604
@@ -3954,6 +4097,7 @@ __device__ __attribute__((always_inline)) inline void w_build(TreeRef &t, TreeLD
     const uint32_t rootn = rl(H.r[0], 1) & 1023u;
     if (lane == 0) hs[heap_max] = rl(H.r[0], 1);
     __builtin_amdgcn_wave_barrier();
+    PCLK(12);
 
     // gen_bitlen (trees.c:406-485): depth of every node by pointer jumping; len = min(depth, max_length),
     // overflow = nodes deeper than max_length (a clamped parent pushes its children past it too)
@@ -3985,6 +4129,7 @@ __device__ __attribute__((always_inline)) inline void w_build(TreeRef &t, TreeLD
             if (heap_max + (int)lane + 64 * i < kHeapSize) h.pj[key[i] & 1023u] = pd[i];
         }
     }
+    PCLK(13);
     int overflow = 0;
     int64_t ol = 0, sl = 0;
     uint32_t bc[kMaxBits + 1];
@@ -4047,6 +4192,7 @@ __device__ __attribute__((always_inline)) inline void w_build(TreeRef &t, TreeLD
 #pragma unroll
         for (int b = 0; b <= kMaxBits; b++) bc[b] = h.bl_count[b];
     }
+    PCLK(14);
     // gen_codes (trees.c:589-625): a length's codes go to its symbols in symbol order
     uint32_t next[kMaxBits + 1];
     uint32_t c = 0;
@@ -4156,7 +4302,9 @@ template <bool kWaveTrees, typename TL>
 __device__ __attribute__((always_inline)) inline void block_plan(const DeflateJob &job, const BlockRec br,
                                                                  const uint32_t *sym, TL &T, uint32_t *hl,
                                                                  uint32_t *hd, int lane, int &type, int &lmax,
-                                                                 int &dmax, int &blmax, uint64_t &bits) {
+                                                                 int &dmax, int &blmax, uint64_t &bits,
+                                                                 unsigned long long *pclk = nullptr) {
+    PCLK(0);
     for (int i = lane; i < kLCodes; i += 64) hl[i] = 0;
     if (lane < kDCodes) hd[lane] = 0;
     __builtin_amdgcn_wave_barrier();
@@ -4189,6 +4337,7 @@ __device__ __attribute__((always_inline)) inline void block_plan(const DeflateJo
         }
     }
     __builtin_amdgcn_wave_barrier();
+    PCLK(1);
     for (int i = lane; i < kLCodes; i += 64) T.lfreq[i] = i == kEndBlock ? 1 : (uint16_t)hl[i];
     if (lane < kDCodes) T.dfreq[lane] = (uint16_t)hd[lane];
     if (lane < kBLCodes) T.bfreq[lane] = 0;
@@ -4199,14 +4348,19 @@ __device__ __attribute__((always_inline)) inline void block_plan(const DeflateJo
     TreeRef bt{T.bfreq, T.bdad, T.bcode, T.blen, 0};
     auto cnt = [&](int s, int, int) { T.bfreq[s]++; };
     if constexpr (kWaveTrees) {
-        w_build(lt, T, kLCodes, c_ct.stat_llen, c_ct.xlbits, 257, kMaxBits, opt_len, static_len);
+        PCLK(2);
+        w_build(lt, T, kLCodes, c_ct.stat_llen, c_ct.xlbits, 257, kMaxBits, opt_len, static_len, pclk);
+        PCLK(3);
         w_build(dt, T, kDCodes, c_ct.stat_dlen, c_ct.xdbits, 0, kMaxBits, opt_len, static_len);
+        PCLK(4);
         if (lane == 0) {
             t_rle(T.llen, lt.max_code, cnt);
             t_rle(T.dlen, dt.max_code, cnt);
         }
         __builtin_amdgcn_wave_barrier();
+        PCLK(5);
         w_build(bt, T, kBLCodes, nullptr, c_ct.xblbits, 0, kMaxBLBits, opt_len, static_len);
+        PCLK(6);
     } else if (lane == 0) {
         t_build(lt, T, kLCodes, c_ct.stat_llen, c_ct.xlbits, 257, kMaxBits, opt_len, static_len);
         t_build(dt, T, kDCodes, c_ct.stat_dlen, c_ct.xdbits, 0, kMaxBits, opt_len, static_len);
@@ -4231,6 +4385,7 @@ __device__ __attribute__((always_inline)) inline void block_plan(const DeflateJo
         blmax = max_blindex;
         bits = type == 2 ? (uint64_t)opt_len + 3 : (uint64_t)static_len + 3;
     }
+    PCLK(7);
 }
 
 template <bool kWaveTrees>
@@ -4550,8 +4705,13 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_plan(DeflateJob job) {
     TreeLDS &T = TT[wave];
     int type = 0, lmax = 0, dmax = 0, blmax = 0;
     uint64_t bits = 0;
+#ifdef ZGPU_PLAN_CLOCK
+    unsigned long long *pclk = kb == 0 && bi == 0 ? g_pclk : nullptr;
+#else
+    unsigned long long *pclk = nullptr;
+#endif
     block_plan<kWaveTrees>(job, br, job.sym + job.ws_off[bi], T, HL[wave], HD[wave], lane, type, lmax, dmax, blmax,
-                           bits);
+                           bits, pclk);
     EncPlan &P = job.eplan[job.blk_off[bi] + kb];
     __builtin_amdgcn_wave_barrier();                  // lane 0's tables (t_build) before the copy
     type = __shfl(type, 0, 64);
@@ -4567,6 +4727,7 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_plan(DeflateJob job) {
         if (lane < kDCodes) { P.dcode[lane] = T.dcode[lane]; P.dlen[lane] = T.dlen[lane]; }
         if (lane < kBLCodes) { P.bcode[lane] = T.bcode[lane]; P.blen[lane] = T.blen[lane]; }
     }
+    PCLK(8);
 }
 
 // k_enc_plan for batches (one-lane tree builds): one wave per block and the
@@ -4735,12 +4896,16 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
         for (int i = tid; i < kLCodes; i += kEncThreads) { s_lcode[i] = P.lcode[i]; s_llen[i] = P.llen[i]; }
         if (tid < kDCodes) { s_dcode[tid] = P.dcode[tid]; s_dlen[tid] = P.dlen[tid]; }
         if (tid < kBLCodes) { s_bcode[tid] = P.bcode[tid]; s_blen[tid] = P.blen[tid]; }
+    } else if (type == 1) {                                // static trees (trees.c:292)
+        for (int i = tid; i < kLCodes; i += kEncThreads) { s_lcode[i] = c_ct.stat_lcode[i]; s_llen[i] = c_ct.stat_llen[i]; }
+        if (tid < kDCodes) { s_dcode[tid] = c_ct.stat_dcode[tid]; s_dlen[tid] = 5; }
     }
     if (tid == 0) {
         s_sbase = ((rs + sh) >> 5) << 5;
         s_obit = (k == 0 ? 0 : (int64_t)pl[k].start) + sh;
     }
     __syncthreads();
+
     int64_t sbase = s_sbase;
     auto put = [&](uint64_t v, int nb) {                  // lane 0 only; caller ensures room
         stg_or(stg, s_obit - sbase, v);
@@ -4834,8 +4999,6 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
             copied += take;
         }
     } else {
-        const uint16_t *lcode = type == 1 ? c_ct.stat_lcode : s_lcode;
-        const uint8_t *llen = type == 1 ? c_ct.stat_llen : s_llen;
         // the next batch's symbols are loaded while this one is scanned and placed
         uint32_t nxt = (uint32_t)tid < br.nsym ? sym[br.sym_start + tid] : 0u;
         for (uint32_t base = 0; base < br.nsym + 1; base += kEncThreads) {   // +1: END_BLOCK
@@ -4848,22 +5011,28 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
                 const uint32_t sy = cur;
                 const uint32_t dist = sy >> 8, lc = sy & 0xffu;
                 if (dist == 0) {
-                    v = lcode[lc]; nb = llen[lc];
+                    v = s_lcode[lc]; nb = s_llen[lc];
                 } else {
-                    const uint32_t code = c_ct.len_code[lc];
-                    v = lcode[code + 257]; nb = llen[code + 257];
-                    const int xl = c_ct.xlbits[code];
-                    if (xl) { v |= (uint64_t)(lc - c_ct.len_base[code]) << nb; nb += xl; }
+                    // the codes from LDS and arithmetic, no dependent loads of c_ct per batch.
+                    // _length_code (trees.c:1113-1125): lc < 8 is its own code, 255 is code 28;
+                    // else with b = floor(log2 lc), code 4(b-1) + bits b-1..b-2 of lc, and the
+                    // b-2 bits below are the extra bits
+                    const uint32_t bl = 31u - (uint32_t)__clz((int)(lc | 1u));
+                    const uint32_t lcd = lc < 8 ? lc : lc == 255 ? 28u : 4 * (bl - 1) + ((lc >> (bl - 2)) & 3u);
+                    const uint32_t xl = lc < 8 || lc == 255 ? 0u : bl - 2;
+                    v = s_lcode[lcd + 257]; nb = s_llen[lcd + 257];
+                    v |= (uint64_t)(lc & ((1u << xl) - 1u)) << nb; nb += (int)xl;
+                    // d_code (trees.c:80-85) and its extra bits: for d >= 4, with b = floor(log2 d),
+                    // code 2b + bit b-1 of d, base (2 | that bit) << (b-1), so d - base = d mod 2^(b-1)
                     const uint32_t d = dist - 1;
-                    const uint32_t dc = d < 256 ? c_ct.dist_code[d] : c_ct.dist_code[256 + (d >> 7)];
-                    const uint32_t dcv = type == 1 ? c_ct.stat_dcode[dc] : s_dcode[dc];
-                    const int dl = type == 1 ? 5 : s_dlen[dc];
-                    v |= (uint64_t)dcv << nb; nb += dl;
-                    const int xd = c_ct.xdbits[dc];
-                    if (xd) { v |= (uint64_t)(d - c_ct.dist_base[dc]) << nb; nb += xd; }
+                    const uint32_t b = 31u - (uint32_t)__clz((int)(d | 1u));
+                    const uint32_t dc = d < 4 ? d : 2 * b + ((d >> (b - 1)) & 1u);
+                    const uint32_t xd = d < 4 ? 0u : b - 1;
+                    v |= (uint64_t)s_dcode[dc] << nb; nb += s_dlen[dc];
+                    v |= (uint64_t)(d & ((1u << xd) - 1u)) << nb; nb += (int)xd;
                 }
             } else if (i == br.nsym) {
-                v = lcode[kEndBlock]; nb = llen[kEndBlock];
+                v = s_lcode[kEndBlock]; nb = s_llen[kEndBlock];
             }
             int incl = nb;
 #pragma unroll
@@ -5509,7 +5678,10 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     case 0:
         if (job.seg && !job.lk_head) {                          // few large buffers: per segment
             const dim3 sgrid(job.nseg);
+            static const bool ls1 = [] { const char *e = getenv("ZGPU_LINKS_SEG1"); return !e || e[0] != '0'; }();
             if (job.hbits > 15) hipLaunchKernelGGL((k_links<2048, 65536, true>), sgrid, dim3(kLThreads), 0, st, job);
+            else if (ls1 && (int64_t)job.seg_len <= kLS1Max)
+                hipLaunchKernelGGL(k_links_seg1, sgrid, dim3(kLThreads), 0, st, job);
             else hipLaunchKernelGGL((k_links<kLC, 32768, true>), sgrid, dim3(kLThreads), 0, st, job);
             hipLaunchKernelGGL(k_count<true>, sgrid, dim3(kCntThreads), 0, st, job);
             break;
