@@ -3997,10 +3997,15 @@ __device__ __attribute__((always_inline)) inline void r_down(RHeap &H, int, uint
         uint32_t a, b;
         rget2<D + 1>(H, j, a, b);
         const bool right = hle(b, a);                   // trees.c:515: heap[j+1] <= heap[j]
-        const uint32_t hj = right ? b : a;
+        // j + 1 made opaque: `right ? j + 1 : j` would fold to j | right, and a bool used
+        // past the branch below is kept as a lane mask and rebuilt through VALU ops and a
+        // readfirstlane per level; this way the select stays one s_cselect
+        uint32_t j1 = j + 1;
+        asm volatile("" : "+s"(j1));
+        const uint32_t hj = right ? b : a, jn = right ? j1 : j;
         if (!hle(v, hj)) {
             rset<D>(H, k, hj);
-            r_down<D + 1>(H, 0, right ? j + 1 : j, v);
+            r_down<D + 1>(H, 0, jn, v);
             return;
         }
     }
