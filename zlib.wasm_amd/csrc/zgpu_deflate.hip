@@ -1688,6 +1688,22 @@ __device__ __attribute__((always_inline)) inline uint32_t bget(const uint8_t *in
     return (sel16(c.a, c.b, c.c, c.d, o >> 2) >> (8 * (o & 3u))) & 0xffu;
 }
 
+// reads straight from an LDS copy of [base, ...) (k_pbig1s): no line cache
+struct WDirect { uint32_t base; };
+__device__ __attribute__((always_inline)) inline uint32_t wget(const uint32_t *a, uint32_t p, WDirect &c) {
+    return a[p - c.base];
+}
+struct BDirect { uint32_t base; };
+__device__ __attribute__((always_inline)) inline uint32_t bget(const uint8_t *in, uint32_t x, BDirect &c) {
+    return in[x - c.base];
+}
+__device__ inline void cache_reset(WCache &c) { c.base = 0xffffffffu; }
+__device__ inline void cache_reset(WCache16 &c) { c.base = 0xffffffffu; }
+__device__ inline void cache_reset(BCache &c) { c.base = ~(uintptr_t)0; }
+__device__ inline void cache_reset(BCache64 &c) { c.base = ~(uintptr_t)0; }
+__device__ inline void cache_reset(WDirect &) {}
+__device__ inline void cache_reset(BDirect &) {}
+
 template <typename WC, typename BC>
 struct SlowLaneT {
     uint32_t p, ml, ms, avail;
@@ -1696,6 +1712,7 @@ struct SlowLaneT {
 };
 using SlowLane = SlowLaneT<WCache, BCache>;          // k_parse_seg: many lanes in flight hide the loads
 using SlowLaneW = SlowLaneT<WCache16, BCache64>;     // k_pbig*
+using SlowLaneD = SlowLaneT<WDirect, BDirect>;       // k_pbig1s
 
 // one deflate_slow decision (deflate.c:1946-2027) on precomputed results.
 // Returns 0 (no symbol), 1 (literal at spos), 2 (match starting at spos, len).
@@ -1757,8 +1774,8 @@ __device__ inline int64_t slide_threshold(uint32_t k, uint32_t n, int64_t refill
 template <typename Lane>
 __device__ __attribute__((always_inline)) inline void lane_init(Lane &L, uint32_t p, uint32_t avail) {
     L.p = p; L.ml = kMinMatch - 1; L.ms = 0; L.avail = avail;
-    L.cf.base = 0xffffffffu;
-    L.cb.base = ~(uintptr_t)0;
+    cache_reset(L.cf);
+    cache_reset(L.cb);
 }
 
 // Four symbols buffered in registers and stored as one 16-byte word: a lane's
@@ -2692,10 +2709,10 @@ __device__ inline uint32_t pbig_lanes(uint32_t n, uint32_t seg) {
     const uint32_t k = (n + seg - 1) / seg;
     return k ? k : 1u;
 }
-__device__ inline PCtx pbig_ctx(const DeflateJob &job) {
+__device__ inline PCtx pbig_ctx(const DeflateJob &job, uint32_t grp = blockIdx.x, uint32_t tl = threadIdx.x) {
     PCtx c;
-    c.bi = job.pgrp[2 * blockIdx.x];
-    c.lane = job.pgrp[2 * blockIdx.x + 1] + threadIdx.x;
+    c.bi = job.pgrp[2 * grp];
+    c.lane = job.pgrp[2 * grp + 1] + tl;
     const uint32_t g = job.first + c.bi;
     c.n = (uint32_t)job.src_len[g];
     c.seg = job.pseg;
@@ -2736,6 +2753,65 @@ __global__ __launch_bounds__(kParseLanes) void k_pbig1(DeflateJob job) {
             }
             if (L.ml < (uint32_t)kMinMatch) wcur |= 1u << (2 * (L.p & 15u) + L.avail);
             if (slow_step(L, c.n, c.rf, c.rq, c.in, cfg, use_q, filtered, sym_v, spos, slen)) sb.push(c.stg + x0, sym_v);
+        }
+        c.sst[widx] = wcur;
+        for (uint32_t z = widx + 1; z <= (seg_end - 1) >> 4; z++) c.sst[z] = 0;
+        sb.flush(c.stg + x0);
+    }
+    PLane &r = job.plane[c.gl];
+    r.e_p = L.p; r.e_ml = L.ml; r.e_ms = L.ms; r.e_av = L.avail;
+    r.k1 = sb.k;
+}
+
+// k_pbig1s — k_pbig1 for 256-byte segments (preach > 1), one wave of 64 lanes per workgroup, with the
+// lanes' records and bytes in LDS.  Pass 1 reads only its own segment's rfull words and bytes, so the
+// wave's 64 segments (16 KiB of positions) are copied in once, coalesced, and every step reads LDS.  In
+// k_pbig1 the lanes' record lines come from L2 and nearly every step of the wave waits for some lane's
+// line (a lane crosses a 64-byte line every few steps, and 64 lanes share the wait).
+constexpr int kP1sLanes = 64, kP1sSpan = kP1sLanes * 256;
+__global__ __launch_bounds__(kP1sLanes) void k_pbig1s(DeflateJob job) {
+    __shared__ uint32_t s_rf[kP1sSpan];
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[kP1sSpan + 16];
+    const uint32_t grp = blockIdx.x / (kParseLanes / kP1sLanes), q = blockIdx.x % (kParseLanes / kP1sLanes);
+    const PCtx c = pbig_ctx(job, grp, q * kP1sLanes + threadIdx.x);
+    const uint32_t l0 = c.lane - threadIdx.x;          // the wave's first lane
+    if (l0 >= c.nl) return;                            // uniform: no lane of this wave exists
+    if (c.lane == 0) job.pbuf[c.bi] = PBuf{0u, kEnd, 0u, 0u};
+    const uint32_t X0 = c.xb(l0);
+    const uint32_t X1 = l0 + kP1sLanes >= c.nl ? c.n : c.xb(l0 + kP1sLanes);   // X1 - X0 <= kP1sSpan
+    {   // coalesced 16-byte loads, 16 per thread in flight per batch (X0 is a multiple of 256)
+        const int tid = threadIdx.x;
+        const uint32_t nw = ((X1 - X0) + 3u) & ~3u;
+#pragma unroll 1
+        for (uint32_t b = 0; b < nw; b += 4096)
+            stage_words<kP1sLanes, 16>(s_rf + b, c.rf, (int64_t)X0 + b, (int)(nw - b < 4096 ? nw - b : 4096),
+                                       (int64_t)X1, tid);
+        stage_bytes<kP1sLanes, (kP1sSpan + 16) / 16 / kP1sLanes + 1>(s_in, c.in, X0, (int)(((X1 - X0) + 15u) & ~15u),
+                                                                   (int64_t)c.n, tid);
+    }
+    __syncthreads();
+    if (!c.active) return;
+    const LevelCfg cfg = job.cfg;
+    const bool use_q = cfg.good < cfg.lazy, filtered = job.strategy == 1;
+    SlowLaneD L;
+    L.cf.base = X0;
+    L.cb.base = X0;
+    uint32_t sym_v, spos, slen;
+    const uint32_t x0 = c.xb(c.lane), seg_end = c.seg_end();
+    lane_init(L, x0, 0);
+    SymBuf sb{0, 0, 0, 0, 0};
+    if (x0 < seg_end) {                               // as k_pbig1
+        uint32_t widx = x0 >> 4, wcur = 0;
+        while (L.p < seg_end) {
+            const uint32_t wi = L.p >> 4;
+            if (wi != widx) {
+                c.sst[widx] = wcur;
+                for (uint32_t z = widx + 1; z < wi; z++) c.sst[z] = 0;
+                widx = wi;
+                wcur = 0;
+            }
+            if (L.ml < (uint32_t)kMinMatch) wcur |= 1u << (2 * (L.p & 15u) + L.avail);
+            if (slow_step(L, c.n, s_rf, c.rq, s_in, cfg, use_q, filtered, sym_v, spos, slen)) sb.push(c.stg + x0, sym_v);
         }
         c.sst[widx] = wcur;
         for (uint32_t z = widx + 1; z <= (seg_end - 1) >> 4; z++) c.sst[z] = 0;
@@ -4247,6 +4323,61 @@ __device__ void t_rle(const uint8_t *len, int max_code, Sink sink) {
     }
 }
 
+// scan_tree's counts (trees.c:712-757) by a whole wave.  zlib cuts each maximal run of equal code lengths
+// into pieces on its own: a run starts in the state max_count 7 / min_count 4 (138 / 3 for zeros) whatever
+// precedes it, and its pieces' codes depend only on the run's value v and length L.  Nonzero: L < 4 -> L
+// codes v; L <= 7 -> v + REP_3_6; longer: v + REP_3_6 for the first 7, REP_3_6 per 6 after, and a rest r
+// of 3..5 -> REP_3_6, 1..2 -> r codes v.  Zero: REPZ_11_138 per 138, and a rest of 11..137 -> REPZ_11_138,
+// 3..10 -> REPZ_3_10, 1..2 -> r zeros.  Each run's first lane adds them into bc[19] (LDS).
+__device__ __attribute__((always_inline)) inline void w_rle_count(const uint8_t *len, int max_code, uint32_t *bc) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const int nch = (max_code + 64) >> 6;                       // chunks of 64 entries: 0 .. max_code
+    uint64_t m[5] = {0, 0, 0, 0, 0};                            // run starts per chunk (max_code < 320)
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+        const int n = c * 64 + (int)lane;
+        const bool st = c < nch && n <= max_code && (n == 0 || len[n] != len[n - 1]);
+        m[c] = __ballot(st);
+    }
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+        const int n = c * 64 + (int)lane;
+        if (!((m[c] >> lane) & 1u)) continue;
+        // the next run start after n: later in this chunk, else the first in a later chunk, else max_code + 1
+        const uint64_t above = lane == 63 ? 0ull : m[c] & (~0ull << (lane + 1));
+        int nx = max_code + 1;
+        if (above) nx = c * 64 + (int)__ffsll((long long)above) - 1;
+        else {
+#pragma unroll
+            for (int d = c + 1; d < 5; d++)
+                if (nx == max_code + 1 && m[d]) nx = d * 64 + (int)__ffsll((long long)m[d]) - 1;
+        }
+        const uint32_t L = (uint32_t)(nx - n), v = len[n];
+        if (v != 0) {
+            if (L < 4) atomicAdd(&bc[v], L);
+            else {
+                atomicAdd(&bc[v], 1u);
+                uint32_t rep = 1, lit = 0;
+                if (L > 7) {
+                    const uint32_t R = L - 7, r = R % 6;
+                    rep += R / 6;
+                    if (r >= 3) rep++;
+                    else lit = r;
+                }
+                atomicAdd(&bc[16], rep);
+                if (lit) atomicAdd(&bc[v], lit);
+            }
+        } else {
+            const uint32_t r = L % 138;
+            uint32_t z11 = L / 138;
+            if (r >= 11) z11++;
+            else if (r >= 3) atomicAdd(&bc[17], 1u);
+            else if (r) atomicAdd(&bc[0], r);
+            if (z11) atomicAdd(&bc[18], z11);
+        }
+    }
+}
+
 // Output bit stream, staged in LDS: stg[] holds output bits
 // [sbase, sbase + kStgBits); everything below sbase is in global memory.
 struct Stage {
@@ -4295,6 +4426,30 @@ __device__ __attribute__((always_inline)) inline void stg_flush(Stage &st, int64
         st.sbase += 32ll * full;
         __syncthreads();
     }
+}
+
+// build_bl_tree's tail and _tr_flush_block's choice (trees.c:887-905, 997-1074): the block's type, header
+// fields and length in bits (from its 3-bit header through END_BLOCK; for a stored block the input length
+// is what counts).  One lane, after the three trees.
+template <typename TL>
+__device__ inline void plan_decide(const DeflateJob &job, const BlockRec &br, const TL &T, int64_t opt_len,
+                                   int64_t static_len, int lmax_code, int dmax_code, int &type, int &lmax,
+                                   int &dmax, int &blmax, uint64_t &bits) {
+    int max_blindex;
+    for (max_blindex = kBLCodes - 1; max_blindex >= 3; max_blindex--)
+        if (T.blen[c_ct.bl_order[max_blindex]] != 0) break;
+    opt_len += 3 * ((int64_t)max_blindex + 1) + 5 + 5 + 4;
+    uint64_t opt_lenb = ((uint64_t)opt_len + 3 + 7) >> 3;
+    const uint64_t static_lenb = ((uint64_t)static_len + 3 + 7) >> 3;
+    if (static_lenb <= opt_lenb || job.strategy == 4) opt_lenb = static_lenb;   // trees.c:1035
+    const uint64_t stored_len = br.in_end - br.in_start;
+    if (stored_len + 4 <= opt_lenb && (br.flags & kBlkStored)) type = 0;       // trees.c:1027-1074
+    else if (static_lenb == opt_lenb) type = 1;
+    else type = 2;
+    lmax = lmax_code;
+    dmax = dmax_code;
+    blmax = max_blindex;
+    bits = type == 2 ? (uint64_t)opt_len + 3 : (uint64_t)static_len + 3;
 }
 
 // One block's histogram (_tr_tally's freq updates, deflate.h:354-372), trees
@@ -4358,10 +4513,13 @@ __device__ __attribute__((always_inline)) inline void block_plan(const DeflateJo
         PCLK(3);
         w_build(dt, T, kDCodes, c_ct.stat_dlen, c_ct.xdbits, 0, kMaxBits, opt_len, static_len);
         PCLK(4);
-        if (lane == 0) {
-            t_rle(T.llen, lt.max_code, cnt);
-            t_rle(T.dlen, dt.max_code, cnt);
-        }
+        // the histogram words are dead: they take scan_tree's counts (w_rle_count, all lanes)
+        if (lane < kBLCodes) hl[lane] = 0;
+        __builtin_amdgcn_wave_barrier();
+        w_rle_count(T.llen, lt.max_code, hl);
+        w_rle_count(T.dlen, dt.max_code, hl);
+        __builtin_amdgcn_wave_barrier();
+        if (lane < kBLCodes) T.bfreq[lane] = (uint16_t)hl[lane];
         __builtin_amdgcn_wave_barrier();
         PCLK(5);
         w_build(bt, T, kBLCodes, nullptr, c_ct.xblbits, 0, kMaxBLBits, opt_len, static_len);
@@ -4373,23 +4531,7 @@ __device__ __attribute__((always_inline)) inline void block_plan(const DeflateJo
         t_rle(T.dlen, dt.max_code, cnt);
         t_build(bt, T, kBLCodes, nullptr, c_ct.xblbits, 0, kMaxBLBits, opt_len, static_len);
     }
-    if (lane == 0) {
-        int max_blindex;
-        for (max_blindex = kBLCodes - 1; max_blindex >= 3; max_blindex--)
-            if (T.blen[c_ct.bl_order[max_blindex]] != 0) break;
-        opt_len += 3 * ((int64_t)max_blindex + 1) + 5 + 5 + 4;
-        uint64_t opt_lenb = ((uint64_t)opt_len + 3 + 7) >> 3;
-        const uint64_t static_lenb = ((uint64_t)static_len + 3 + 7) >> 3;
-        if (static_lenb <= opt_lenb || job.strategy == 4) opt_lenb = static_lenb;   // trees.c:1035
-        const uint64_t stored_len = br.in_end - br.in_start;
-        if (stored_len + 4 <= opt_lenb && (br.flags & kBlkStored)) type = 0;       // trees.c:1027-1074
-        else if (static_lenb == opt_lenb) type = 1;
-        else type = 2;
-        lmax = lt.max_code;
-        dmax = dt.max_code;
-        blmax = max_blindex;
-        bits = type == 2 ? (uint64_t)opt_len + 3 : (uint64_t)static_len + 3;
-    }
+    if (lane == 0) plan_decide(job, br, T, opt_len, static_len, lt.max_code, dt.max_code, type, lmax, dmax, blmax, bits);
     PCLK(7);
 }
 
@@ -4733,6 +4875,109 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_plan(DeflateJob job) {
         if (lane < kBLCodes) { P.bcode[lane] = T.bcode[lane]; P.blen[lane] = T.blen[lane]; }
     }
     PCLK(8);
+}
+
+// k_enc_plan2 — the wave trees for sub-batches of few blocks (a lone compress2), two waves per block:
+// the pair splits the block's histogram; wave 0 builds the literal/length tree while wave 1 builds the
+// distance tree (its heap scratch in the pair's second TreeLDS); each counts the code-length runs of its
+// own tree for the bit-length tree (scan_tree, trees.c:712-757; the counts are sums, so their order does
+// not matter); wave 0 then builds the bit-length tree and decides.  Against k_enc_plan<true> (one wave
+// per block) the distance tree and half the histogram leave the critical path.
+constexpr int kPlan2Pairs = kEncThreads / 128;
+__global__ __launch_bounds__(kEncThreads) void k_enc_plan2(DeflateJob job) {
+    static_assert(kEncGroup == 2 * kPlan2Pairs, "a TreeLDS per wave");
+    __shared__ TreeLDS TT[kEncGroup];
+    __shared__ uint32_t HL[kPlan2Pairs][kLCodes], HD[kPlan2Pairs][kDCodes], BC[kPlan2Pairs][kBLCodes];
+    __shared__ int64_t s_len[kPlan2Pairs][2];
+    __shared__ int s_dmax[kPlan2Pairs];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, pair = wave >> 1, wp = wave & 1;
+    const uint32_t bi = blockIdx.y;
+    const uint32_t kb = blockIdx.x * kPlan2Pairs + (uint32_t)pair;
+    const uint32_t nblk = job.nblocks[bi];
+    const bool active = kb < nblk && enc_blocks_ok(job, bi, nblk);   // every wave reaches every barrier
+    BlockRec br{};
+    if (active) br = job.blocks[job.blk_off[bi] + kb];
+    const uint32_t *sym = job.sym + job.ws_off[bi];
+    TreeLDS &T = TT[2 * pair];
+    uint32_t *hl = HL[pair], *hd = HD[pair];
+    for (int i = (wp << 6) | lane; i < kLCodes; i += 128) hl[i] = 0;
+    if (wp == 0 && lane < kDCodes) hd[lane] = 0;
+    if (wp == 1 && lane < kBLCodes) BC[pair][lane] = 0;
+    __syncthreads();
+    if (active) {                                      // the histogram, batches of 512 symbols alternating
+        constexpr uint32_t kHU = 8;
+        for (uint32_t i0 = (uint32_t)wp * 64 * kHU; i0 < br.nsym; i0 += 2 * 64 * kHU) {
+            uint32_t v[kHU], li[kHU], di[kHU];
+#pragma unroll
+            for (uint32_t u = 0; u < kHU; u++) {
+                const uint32_t i = i0 + 64 * u + (uint32_t)lane;
+                v[u] = i < br.nsym ? sym[br.sym_start + i] : 0xffffffffu;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kHU; u++) {
+                const uint32_t dist = v[u] >> 8, lc = v[u] & 0xffu, d = dist - 1u;
+                const bool m = v[u] != 0xffffffffu && dist != 0;
+                li[u] = m ? c_ct.len_code[lc] + 257u : lc;
+                di[u] = m ? (d < 256 ? c_ct.dist_code[d] : c_ct.dist_code[256 + ((d >> 7) & 255u)]) : 0u;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kHU; u++) {
+                if (v[u] == 0xffffffffu) continue;
+                atomicAdd(&hl[li[u]], 1u);
+                if (v[u] >> 8) atomicAdd(&hd[di[u]], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    if (active) {
+        for (int i = (wp << 6) | lane; i < kLCodes; i += 128) T.lfreq[i] = i == kEndBlock ? 1 : (uint16_t)hl[i];
+        if (wp == 0 && lane < kDCodes) T.dfreq[lane] = (uint16_t)hd[lane];
+    }
+    __syncthreads();
+    int64_t opt_len = 0, static_len = 0;
+    TreeRef lt{T.lfreq, T.ldad, T.lcode, T.llen, 0};
+    TreeRef dt{T.dfreq, T.ddad, T.dcode, T.dlen, 0};
+    TreeRef bt{T.bfreq, T.bdad, T.bcode, T.blen, 0};
+    if (active) {
+        if (wp == 0) w_build(lt, T, kLCodes, c_ct.stat_llen, c_ct.xlbits, 257, kMaxBits, opt_len, static_len);
+        else w_build(dt, TT[2 * pair + 1], kDCodes, c_ct.stat_dlen, c_ct.xdbits, 0, kMaxBits, opt_len, static_len);
+        __builtin_amdgcn_wave_barrier();
+        if (wp == 0) {
+            w_rle_count(T.llen, lt.max_code, BC[pair]);
+        } else {
+            w_rle_count(T.dlen, dt.max_code, BC[pair]);
+            if (lane == 0) {
+                s_len[pair][0] = opt_len;
+                s_len[pair][1] = static_len;
+                s_dmax[pair] = dt.max_code;
+            }
+        }
+    }
+    __syncthreads();
+    if (!active || wp != 0) return;
+    if (lane < kBLCodes) T.bfreq[lane] = (uint16_t)BC[pair][lane];
+    opt_len += s_len[pair][0];
+    static_len += s_len[pair][1];
+    __builtin_amdgcn_wave_barrier();
+    w_build(bt, T, kBLCodes, nullptr, c_ct.xblbits, 0, kMaxBLBits, opt_len, static_len);
+    int type = 0, lmax = 0, dmax = 0, blmax = 0;
+    uint64_t bits = 0;
+    if (lane == 0) plan_decide(job, br, T, opt_len, static_len, lt.max_code, s_dmax[pair], type, lmax, dmax, blmax, bits);
+    EncPlan &P = job.eplan[job.blk_off[bi] + kb];
+    __builtin_amdgcn_wave_barrier();                  // lane 0's tables (t_build) before the copy
+    type = __shfl(type, 0, 64);
+    if (lane == 0) {
+        P.type = (uint8_t)type;
+        P.lmax = (uint16_t)lmax;
+        P.dmax = (uint16_t)dmax;
+        P.blmax = (uint16_t)blmax;
+        P.bits = bits;
+    }
+    if (type == 2) {
+        for (int i = lane; i < kLCodes; i += 64) { P.lcode[i] = T.lcode[i]; P.llen[i] = T.llen[i]; }
+        if (lane < kDCodes) { P.dcode[lane] = T.dcode[lane]; P.dlen[lane] = T.dlen[lane]; }
+        if (lane < kBLCodes) { P.bcode[lane] = T.bcode[lane]; P.blen[lane] = T.blen[lane]; }
+    }
 }
 
 // k_enc_plan for batches (one-lane tree builds): one wave per block and the
@@ -5746,7 +5991,10 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     }
     case 11: {
         const dim3 pg(job.npgrp), bg((job.maxblk + 255) / 256, job.count);
-        hipLaunchKernelGGL(k_pbig1, pg, dim3(kParseLanes), 0, st, job);
+        if (job.preach > 1 && job.pseg == 256)             // 256-byte segments: records staged in LDS
+            hipLaunchKernelGGL(k_pbig1s, dim3(job.npgrp * (kParseLanes / kP1sLanes)), dim3(kP1sLanes), 0, st, job);
+        else
+            hipLaunchKernelGGL(k_pbig1, pg, dim3(kParseLanes), 0, st, job);
         hipLaunchKernelGGL(k_pbig2, pg, dim3(kParseLanes), 0, st, job);
         hipLaunchKernelGGL(k_pbig3, pg, dim3(kParseLanes), 0, st, job);
         hipLaunchKernelGGL(k_pbig4, grid, dim3(kPScanThreads), 0, st, job);
@@ -5769,7 +6017,11 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
         // one lane when many are (the other waves hide it), as for k_encode
         const dim3 plg((job.maxblk + kEncGroup - 1) / kEncGroup, job.count), eg(job.maxblk, job.count);
         static const bool plan_lane = std::getenv("ZGPU_PLAN_LANE") != nullptr;   // A/B: one-lane trees always
-        if ((uint64_t)job.maxblk * job.count < 16384 && !plan_lane)
+        static const bool plan_one = std::getenv("ZGPU_PLAN_ONEWAVE") != nullptr;  // A/B: one wave per block
+        const dim3 plg2((job.maxblk + kPlan2Pairs - 1) / kPlan2Pairs, job.count);
+        if ((uint64_t)job.maxblk * job.count < 16384 && !plan_lane && !plan_one)
+            hipLaunchKernelGGL(k_enc_plan2, plg2, dim3(kEncThreads), 0, st, job);
+        else if ((uint64_t)job.maxblk * job.count < 16384 && !plan_lane)
             hipLaunchKernelGGL(k_enc_plan<true>, plg, dim3(kEncThreads), 0, st, job);
         else
             hipLaunchKernelGGL(k_enc_plan1, dim3(job.maxblk, job.count), dim3(64), 0, st, job);
