@@ -672,7 +672,6 @@ int deflate_dev_locked(Ctx &c, const uint8_t *src, const uint64_t *src_off, cons
     // the lanes of 1 KiB segments, so a quarter of each lane's serial parse,
     // without the stitch failures short segments would give long matches
     static const int small_seg = [] { const char *e = std::getenv("ZGPU_PSEG_SMALL"); return e ? std::atoi(e) : 1; }();
-    constexpr uint64_t kSmallSeg = 256, kSmallReach = 8;
     for (size_t sb = 0; sb < nsub; sb++) {
         pg_at[sb] = pg.size() / 2;
         plb_at[sb] = plb.size();
@@ -2534,6 +2533,7 @@ struct internal_state {
     const gz_header *gzhead = nullptr;   // deflateSetHeader: written by the first deflate() call
     bool dict_set = false;               // deflateSetDictionary: the zlib header's FDICT + DICTID
     uint32_t dict_id = 0;
+    size_t dict_len = 0;                 // the dictionary bytes in the window (<= w_size), just before rd
     bool need_dict = false;              // inflate: Z_NEED_DICT answered, waiting for the dictionary
     uint32_t want_dict = 0;              // its DICTID
     gz_header *ihead = nullptr;          // inflateGetHeader: filled as the gzip header arrives
@@ -3423,8 +3423,39 @@ static int deflate_body(z_streamp strm, int flush) {
         }
     }
     bool force_skip = false;
+    const bool slow_fn = s->level >= 4 && s->strategy != Z_HUFFMAN_ONLY && s->strategy != Z_RLE;
     if (!s->header_done) {                                      // deflate.c:1002-1073
+        const size_t before = s->out.size();
         queue_header(s);
+        // a first call whose output space is exactly the header (below) that is not modelled is refused
+        // here, before any output
+        if (s->out_pos == before && strm->avail_out == s->out.size() - before && s->level != 0 && slow_fn &&
+            P - s->rd >= 2) {
+            const char *why = nullptr;
+            const size_t wread = (size_t(2) << s->wbits) - (s->dict_set ? s->dict_len : 0);
+            if (s->dict_set && P - s->rd >= 3) {
+                // with a dictionary the first decision may find a match (history), and the stop at the
+                // first lazy literal moves with the parse; without one (the input's first three bytes
+                // nowhere in the dictionary) the literal comes at the second decision, as with no history
+                const uint8_t *d0 = s->in.data() + (s->rd - s->dict_len - s->in_base);
+                const uint8_t *x = strm->next_in;
+                for (size_t k = 0; k + 3 <= s->dict_len && !why; k++)
+                    if (d0[k] == x[0] && d0[k + 1] == x[1] && d0[k + 2] == x[2])
+                        why = "deflate: a first call whose output space is exactly a preset dictionary's header, "
+                              "with the input's first string in the dictionary, is not modelled";
+            }
+            // more input than fill_window's first read: the later calls' accounting was found to differ
+            // from zlib's for some inputs, so the call is refused instead
+            if (!why && P - s->rd > wread)
+                why = "deflate: a first call whose output space is exactly the header, with more input than "
+                      "fill_window's first read (window_size bytes), is not modelled";
+            if (why) {
+                s->out.resize(before);
+                s->header_done = false;
+                strm->msg = const_cast<char *>(why);
+                return Z_STREAM_ERROR;
+            }
+        }
         drain(strm, s);
         if (s->out_pos < s->out.size()) {
             s->last_flush = -1;
@@ -3440,14 +3471,14 @@ static int deflate_body(z_streamp strm, int flush) {
         // FLUSH_BLOCK cuts the block and returns need_more before the flush's
         // marker.  Without input the flush goes ahead (its marker waits).
         const size_t avail = P - s->rd;
-        const bool slow_fn = s->level >= 4 && s->strategy != Z_HUFFMAN_ONLY && s->strategy != Z_RLE;
-        if (strm->avail_out == 0 && s->level != 0 && !s->dict_set) {
+        if (strm->avail_out == 0 && s->level != 0) {
             // whatever the compress function returns then (need_more, or a marker
             // left pending), deflate() leaves with last_flush = -1: the next call
             // with no input is no Z_BUF_ERROR
             if (avail > 0 || flush != Z_NO_FLUSH) s->last_flush = -1;
             if (avail > 0 && slow_fn && avail >= 2) {
-                P = std::min<size_t>(P, s->rd + (size_t(2) << s->wbits));
+                // fill_window's first read: window_size - strstart (a dictionary's bytes stand before it)
+                P = std::min<size_t>(P, s->rd + (size_t(2) << s->wbits) - (s->dict_set ? s->dict_len : 0));
                 flush = Z_NO_FLUSH;
                 force_skip = true;
             } else if (avail > 0 && flush != Z_NO_FLUSH && flush != Z_FINISH) {
@@ -3734,6 +3765,7 @@ int deflateSetDictionary(z_streamp strm, const Bytef *dictionary, uInt dictLengt
             s->in_base = s->res_S = X;
         }
         s->in.insert(s->in.end(), dictionary, dictionary + dictLength);
+        s->dict_len = dictLength;
         s->res_pos = s->rd = s->rd_seen = s->flush_done = s->ck_pos = X + dictLength;
         s->res_E = X + dictLength;
         s->res_cut = 0;                                 // the last two strings wait as s->insert

@@ -2768,7 +2768,7 @@ __global__ __launch_bounds__(kParseLanes) void k_pbig1(DeflateJob job) {
 // wave's 64 segments (16 KiB of positions) are copied in once, coalesced, and every step reads LDS.  In
 // k_pbig1 the lanes' record lines come from L2 and nearly every step of the wave waits for some lane's
 // line (a lane crosses a 64-byte line every few steps, and 64 lanes share the wait).
-constexpr int kP1sLanes = 64, kP1sSpan = kP1sLanes * 256;
+constexpr int kP1sLanes = 64, kP1sSpan = kP1sLanes * (int)kSmallSeg;
 __global__ __launch_bounds__(kP1sLanes) void k_pbig1s(DeflateJob job) {
     __shared__ uint32_t s_rf[kP1sSpan];
     __shared__ __attribute__((aligned(16))) uint8_t s_in[kP1sSpan + 16];
@@ -2914,12 +2914,14 @@ __global__ __launch_bounds__(kParseLanes) void k_pbig3(DeflateJob job) {
     const uint32_t x0 = c.xb(c.lane), seg_end = c.seg_end();
     const uint32_t yend = r.y, end = yend == kEnd ? c.n : yend;
     SlowLaneW L;
+    const uint32_t *rfp = c.rf;
+    const uint8_t *inp = c.in;
     uint32_t sym_v, spos, slen;
     uint32_t kstart = 0;
     if (mine && c.lane > 0) {                         // pass-1 symbols before the previous meet are not this lane's
         lane_init(L, x0, 0);
         while (L.p < start)
-            if (slow_step(L, c.n, c.rf, c.rq, c.in, cfg, use_q, filtered, sym_v, spos, slen)) kstart++;
+            if (slow_step(L, c.n, rfp, c.rq, inp, cfg, use_q, filtered, sym_v, spos, slen)) kstart++;
     }
     uint32_t rcnt = 0;
     // the run-on, staged in the lane's dead state words (or its pron slot)
@@ -2929,13 +2931,13 @@ __global__ __launch_bounds__(kParseLanes) void k_pbig3(DeflateJob job) {
         lane_init(L, r.e_p, r.e_av);
         L.ml = r.e_ml; L.ms = r.e_ms;
         while (L.p < end) {
-            if (slow_step(L, c.n, c.rf, c.rq, c.in, cfg, use_q, filtered, sym_v, spos, slen)) {
+            if (slow_step(L, c.n, rfp, c.rq, inp, cfg, use_q, filtered, sym_v, spos, slen)) {
                 if (rcnt < rcap) ron[rcnt] = sym_v;
                 rcnt++;
             }
         }
         if (yend == kEnd && L.avail) {                // the final pending literal
-            if (rcnt < rcap) ron[rcnt] = bget(c.in, c.n - 1, L.cb);
+            if (rcnt < rcap) ron[rcnt] = bget(inp, c.n - 1, L.cb);
             rcnt++;
             job.pbuf[c.bi].fin = 1u;
         }
@@ -5120,7 +5122,7 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
     __shared__ uint32_t stg[kEmitStgWords];
     __shared__ uint16_t s_lcode[kLCodes], s_dcode[kDCodes], s_bcode[kBLCodes];
     __shared__ uint8_t s_llen[kLCodes], s_dlen[kDCodes], s_blen[kBLCodes];
-    __shared__ uint32_t wsum[kEncThreads / 64];
+    __shared__ uint32_t wsum2[2][kEncThreads / 64];
     __shared__ int64_t s_obit, s_sbase;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t bi = blockIdx.y, k = blockIdx.x;
@@ -5163,6 +5165,7 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
     };
     // completed words below aligned bit `upto` to global (all of them: fin)
     auto eflush = [&](int64_t upto, bool fin) {
+        __syncthreads();                                   // the staged bits of every thread
         const int64_t rel = upto - sbase;
         const int full = (int)(rel >> 5);
         const int nwords = fin ? (int)((rel + 31) >> 5) : full;
@@ -5249,61 +5252,75 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
             copied += take;
         }
     } else {
-        // the next batch's symbols are loaded while this one is scanned and placed
-        uint32_t nxt = (uint32_t)tid < br.nsym ? sym[br.sym_start + tid] : 0u;
-        for (uint32_t base = 0; base < br.nsym + 1; base += kEncThreads) {   // +1: END_BLOCK
-            const uint32_t i = base + tid;
-            const uint32_t cur = nxt;
-            if (i + kEncThreads < br.nsym) nxt = sym[br.sym_start + i + kEncThreads];
-            uint64_t v = 0;
-            int nb = 0;
-            if (i < br.nsym) {
-                const uint32_t sy = cur;
-                const uint32_t dist = sy >> 8, lc = sy & 0xffu;
-                if (dist == 0) {
-                    v = s_lcode[lc]; nb = s_llen[lc];
-                } else {
-                    // the codes from LDS and arithmetic, no dependent loads of c_ct per batch.
-                    // _length_code (trees.c:1113-1125): lc < 8 is its own code, 255 is code 28;
-                    // else with b = floor(log2 lc), code 4(b-1) + bits b-1..b-2 of lc, and the
-                    // b-2 bits below are the extra bits
-                    const uint32_t bl = 31u - (uint32_t)__clz((int)(lc | 1u));
-                    const uint32_t lcd = lc < 8 ? lc : lc == 255 ? 28u : 4 * (bl - 1) + ((lc >> (bl - 2)) & 3u);
-                    const uint32_t xl = lc < 8 || lc == 255 ? 0u : bl - 2;
-                    v = s_lcode[lcd + 257]; nb = s_llen[lcd + 257];
-                    v |= (uint64_t)(lc & ((1u << xl) - 1u)) << nb; nb += (int)xl;
-                    // d_code (trees.c:80-85) and its extra bits: for d >= 4, with b = floor(log2 d),
-                    // code 2b + bit b-1 of d, base (2 | that bit) << (b-1), so d - base = d mod 2^(b-1)
-                    const uint32_t d = dist - 1;
-                    const uint32_t b = 31u - (uint32_t)__clz((int)(d | 1u));
-                    const uint32_t dc = d < 4 ? d : 2 * b + ((d >> (b - 1)) & 1u);
-                    const uint32_t xd = d < 4 ? 0u : b - 1;
-                    v |= (uint64_t)s_dcode[dc] << nb; nb += s_dlen[dc];
-                    v |= (uint64_t)(d & ((1u << xd) - 1u)) << nb; nb += (int)xd;
-                }
-            } else if (i == br.nsym) {
-                v = s_lcode[kEndBlock]; nb = s_llen[kEndBlock];
+        // a symbol's code (compress_block, trees.c:1105-1135) from LDS and arithmetic, no dependent loads of
+        // c_ct.  _length_code (trees.c:1113-1125): lc < 8 is its own code, 255 is code 28; else with b =
+        // floor(log2 lc), code 4(b-1) + bits b-1..b-2 of lc, and the b-2 bits below are the extra bits.
+        // d_code (trees.c:80-85): for d >= 4, with b = floor(log2 d), code 2b + bit b-1 of d, base (2 | that
+        // bit) << (b-1), so d - base = d mod 2^(b-1)
+        auto code = [&](uint32_t sy, uint64_t &v, int &nb) {
+            const uint32_t dist = sy >> 8, lc = sy & 0xffu;
+            if (dist == 0) {
+                v = s_lcode[lc]; nb = s_llen[lc];
+                return;
             }
+            const uint32_t bl = 31u - (uint32_t)__clz((int)(lc | 1u));
+            const uint32_t lcd = lc < 8 ? lc : lc == 255 ? 28u : 4 * (bl - 1) + ((lc >> (bl - 2)) & 3u);
+            const uint32_t xl = lc < 8 || lc == 255 ? 0u : bl - 2;
+            v = s_lcode[lcd + 257]; nb = s_llen[lcd + 257];
+            v |= (uint64_t)(lc & ((1u << xl) - 1u)) << nb; nb += (int)xl;
+            const uint32_t d = dist - 1;
+            const uint32_t b = 31u - (uint32_t)__clz((int)(d | 1u));
+            const uint32_t dc = d < 4 ? d : 2 * b + ((d >> (b - 1)) & 1u);
+            const uint32_t xd = d < 4 ? 0u : b - 1;
+            v |= (uint64_t)s_dcode[dc] << nb; nb += s_dlen[dc];
+            v |= (uint64_t)(d & ((1u << xd) - 1u)) << nb; nb += (int)xd;
+        };
+        // two symbols per thread (2t, 2t + 1 of a batch of 512: at most 48 bits each, so a batch fits the
+        // staging window after a flush) and one barrier per batch: every thread keeps the bit position,
+        // the wave sums alternate between two slots, and a flush starts with its own barrier.  The next
+        // batch's symbols are loaded while this one is scanned and placed.
+        constexpr uint32_t kBatch = 2 * kEncThreads;
+        static_assert(kBatch * 48 + 64 <= (uint32_t)kEmitStgBits - 32, "a batch fits the window after a flush");
+        const uint32_t i0 = 2u * (uint32_t)tid;
+        uint32_t n0 = i0 < br.nsym ? sym[br.sym_start + i0] : 0u;
+        uint32_t n1 = i0 + 1 < br.nsym ? sym[br.sym_start + i0 + 1] : 0u;
+        int64_t ob = s_obit;
+        int par = 0;
+        for (uint32_t base = 0; base < br.nsym + 1; base += kBatch) {   // +1: END_BLOCK
+            const uint32_t i = base + i0;
+            const uint32_t c0 = n0, c1 = n1;
+            if (i + kBatch < br.nsym) n0 = sym[br.sym_start + i + kBatch];
+            if (i + kBatch + 1 < br.nsym) n1 = sym[br.sym_start + i + kBatch + 1];
+            uint64_t v0 = 0, v1 = 0;
+            int nb0 = 0, nb1 = 0;
+            if (i < br.nsym) code(c0, v0, nb0);
+            else if (i == br.nsym) { v0 = s_lcode[kEndBlock]; nb0 = s_llen[kEndBlock]; }
+            if (i + 1 < br.nsym) code(c1, v1, nb1);
+            else if (i + 1 == br.nsym) { v1 = s_lcode[kEndBlock]; nb1 = s_llen[kEndBlock]; }
+            const int nb = nb0 + nb1;
             int incl = nb;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
                 const int t = __shfl_up(incl, o, 64);
                 if (lane >= o) incl += t;
             }
-            if (lane == 63) wsum[wave] = (uint32_t)incl;
+            if (lane == 63) wsum2[par][wave] = (uint32_t)incl;
             __syncthreads();
             int wpre = 0, total = 0;
             for (int w = 0; w < kEncThreads / 64; w++) {
-                if (w < wave) wpre += (int)wsum[w];
-                total += (int)wsum[w];
+                if (w < wave) wpre += (int)wsum2[par][w];
+                total += (int)wsum2[par][w];
             }
             const int excl = wpre + incl - nb;
-            if (s_obit - sbase + total + 64 > kEmitStgBits) eflush(s_obit, false);
-            if (nb) stg_or(stg, s_obit - sbase + excl, v);
-            __syncthreads();
-            if (tid == 0) s_obit += total;
-            __syncthreads();
+            if (ob - sbase + total + 64 > kEmitStgBits) eflush(ob, false);
+            if (nb0) stg_or(stg, ob - sbase + excl, v0);
+            if (nb1) stg_or(stg, ob - sbase + excl + nb0, v1);
+            ob += total;
+            par ^= 1;
         }
+        __syncthreads();                                   // every symbol placed before the trailer / flush
+        if (tid == 0) s_obit = ob;
+        __syncthreads();
     }
     if (last) {
         if (s_obit - sbase + 160 > kEmitStgBits) eflush(s_obit, false);
@@ -5991,10 +6008,11 @@ int launch_deflate_stage(int stage, const DeflateJob &job, uint32_t *heads, hipS
     }
     case 11: {
         const dim3 pg(job.npgrp), bg((job.maxblk + 255) / 256, job.count);
-        if (job.preach > 1 && job.pseg == 256)             // 256-byte segments: records staged in LDS
-            hipLaunchKernelGGL(k_pbig1s, dim3(job.npgrp * (kParseLanes / kP1sLanes)), dim3(kP1sLanes), 0, st, job);
-        else
-            hipLaunchKernelGGL(k_pbig1, pg, dim3(kParseLanes), 0, st, job);
+        // 256-byte segments: pass 1 from LDS copies (k_pbig1s stages exactly this segment size)
+        const bool staged = job.preach == kSmallReach && job.pseg == kSmallSeg;
+        const dim3 sgq(job.npgrp * (kParseLanes / kP1sLanes));
+        if (staged) hipLaunchKernelGGL(k_pbig1s, sgq, dim3(kP1sLanes), 0, st, job);
+        else hipLaunchKernelGGL(k_pbig1, pg, dim3(kParseLanes), 0, st, job);
         hipLaunchKernelGGL(k_pbig2, pg, dim3(kParseLanes), 0, st, job);
         hipLaunchKernelGGL(k_pbig3, pg, dim3(kParseLanes), 0, st, job);
         hipLaunchKernelGGL(k_pbig4, grid, dim3(kPScanThreads), 0, st, job);

@@ -115,6 +115,9 @@ struct PLane {
     uint32_t p0;                      // first input position the lane's symbols cover (k_pbig5)
 };
 constexpr uint32_t kRonCap = 64;      // run-on symbols per lane when preach > 1
+// sub-batches of small buffers (zgpu_api.cpp): 256-byte segments whose run-ons may cross 8 segments;
+// k_pbig1s stages 64 such segments in LDS
+constexpr uint32_t kSmallSeg = 256, kSmallReach = 8;
 struct PBuf { uint32_t fail, first_end, fin, total; };
 constexpr uint32_t kParseLanesHost = 256;   // lanes (segments) per k_pbig* / k_parse_seg workgroup
 
