@@ -3328,6 +3328,21 @@ int run_items(z_streamp strm, internal_state *s, uint32_t own, bool *full) {
 }
 }  // namespace
 
+// A stop turned into a pause (more input after a call that paused inside a block) applies after the paused
+// block's record.  When the resume point chosen at the end of that call is that record itself, the pause is
+// behind it -- choose_resume's rule for pauses (a pause at the resume record is behind it), which could not
+// see this one, as it was still a stop then -- and the next job must not carry it: the window's read state
+// at the resume point is the record's own (res_E).  A job starting at the pause's block end with the pause
+// among its events produced no records and the stream made no progress (round 6, tools/header_first_probe.py).
+static void drop_pause_behind_resume(internal_state *s, size_t le) {
+    if (s->res_item < 0 || le + 1 != s->ev_type.size() || s->res_pos < s->ev_aux[le]) return;
+    s->ev_pos.pop_back();
+    s->ev_type.pop_back();
+    s->ev_aux.pop_back();
+    s->ev_done = s->ev_type.size();
+    if (s->res_ev > s->ev_type.size()) s->res_ev = s->ev_type.size();
+}
+
 static void stream_trace(const char *where, z_streamp strm, const internal_state *s, int flush) {
     static const bool on = std::getenv("ZGPU_STREAM_TRACE") != nullptr;
     if (!on) return;
@@ -3432,7 +3447,6 @@ static int deflate_body(z_streamp strm, int flush) {
         if (s->out_pos == before && strm->avail_out == s->out.size() - before && s->level != 0 && slow_fn &&
             P - s->rd >= 2) {
             const char *why = nullptr;
-            const size_t wread = (size_t(2) << s->wbits) - (s->dict_set ? s->dict_len : 0);
             if (s->dict_set && P - s->rd >= 3) {
                 // with a dictionary the first decision may find a match (history), and the stop at the
                 // first lazy literal moves with the parse; without one (the input's first three bytes
@@ -3444,11 +3458,6 @@ static int deflate_body(z_streamp strm, int flush) {
                         why = "deflate: a first call whose output space is exactly a preset dictionary's header, "
                               "with the input's first string in the dictionary, is not modelled";
             }
-            // more input than fill_window's first read: the later calls' accounting was found to differ
-            // from zlib's for some inputs, so the call is refused instead
-            if (!why && P - s->rd > wread)
-                why = "deflate: a first call whose output space is exactly the header, with more input than "
-                      "fill_window's first read (window_size bytes), is not modelled";
             if (why) {
                 s->out.resize(before);
                 s->header_done = false;
@@ -3509,6 +3518,7 @@ static int deflate_body(z_streamp strm, int flush) {
                 s->ev_type[le] = kEvPause;
                 s->ev_aux[le] = s->items[s->t - 1].in_end;
                 s->ev_done = le + 1;
+                drop_pause_behind_resume(s, le);
                 s->stale = true;
             } else if (flush == Z_NO_FLUSH) {
                 own = (uint32_t)le;
@@ -3531,6 +3541,7 @@ static int deflate_body(z_streamp strm, int flush) {
                 s->ev_type[le] = kEvPause;
                 s->ev_aux[le] = s->items[s->t - 1].in_end;
                 s->ev_done = le + 1;
+                drop_pause_behind_resume(s, le);
             } else {                                            // Z_FINISH's drain takes over
                 s->ev_pos.pop_back();
                 s->ev_type.pop_back();
