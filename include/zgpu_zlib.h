@@ -52,8 +52,13 @@
  *   - deflatePrime with input pending after a call that did not reach its end,
  *     or after Z_STREAM_END;
  *   - deflateSetDictionary after the stream has ended;
- *   - deflateResetKeep on a stream that has taken input (the window it would
- *     carry into the next stream);
+ *   - deflateResetKeep on a stream that has taken input, except after a
+ *     stream that deflate_slow (levels 4..9, not Z_HUFFMAN_ONLY / Z_RLE) ran
+ *     from its part start to a point with no input pending (the end of
+ *     Z_FINISH, or a flush that took all its input): that window is carried
+ *     into the next stream as the reference carries it; then a preset
+ *     dictionary, or a switch to level 0 or to a deflate_fast level before the
+ *     next input, is refused;
  *   - inflatePrime other than on a raw stream before its first input.
  * inflateUndermine returns Z_DATA_ERROR (as a reference built without
  * INFLATE_ALLOW_INVALID_DISTANCE_TOOFAR_ARRR does).  inflateBack reports a

@@ -261,6 +261,68 @@ def deflate_sessions():
     S.append({"name": "resetkeep-fresh", "ops": [["init", 6, 15, 8, 0], ["resetkeep"],
                                                  ["deflate", sl(m, 0, 100000), Z_FINISH], ["used"], ["reset"],
                                                  ["resetkeep"], ["deflate", sl(t, 0, 100000), Z_FINISH]]})
+    S += resetkeep_sessions()
+    return S
+
+
+def resetkeep_sessions():
+    """deflateResetKeep carrying the window of a deflate_slow stream into the next
+    one (round 6, deflate.c:635-671): after Z_FINISH and after flushes that took
+    all their input, zlib / raw / gzip, window sizes 9-15, old streams long
+    enough to have slid, preset dictionaries, repeated keeps, small output
+    space, parameter changes before the new input"""
+    S = []
+    t = ["text", 100000, 81]
+    m = ["mix", 100000, 82]
+    sl = lambda d, a, b: d + [a, b]
+    K = [["getdict"], ["resetkeep"], ["getdict"]]
+    S.append({"name": "rk-finish-L6", "ops": [["init", 6, 15, 8, 0], ["deflate", sl(t, 0, 30000), Z_FINISH]] + K +
+              [["deflate", sl(t, 30000, 100000), Z_FINISH], ["used"]]})
+    S.append({"name": "rk-raw-L9", "ops": [["init", 9, -15, 8, 0], ["deflate", sl(m, 0, 80000), Z_FINISH]] + K +
+              [["deflate", sl(m, 80000, 100000), Z_FINISH]]})
+    S.append({"name": "rk-gzip-L5", "ops": [["init", 5, 31, 8, 0], ["deflate", sl(t, 0, 50000), Z_FINISH]] + K +
+              [["deflate", sl(t, 50000, 100000), Z_FINISH]]})
+    S.append({"name": "rk-slid-L6", "ops": [["init", 6, 15, 8, 0], ["deflate", sl(m, 0, 100000), Z_NO_FLUSH],
+                                            ["deflate", sl(t, 0, 60000), Z_FINISH]] + K +
+              [["deflate", sl(t, 60000, 100000), Z_FINISH]]})
+    S.append({"name": "rk-slid-L8-raw", "ops": [["init", 8, -15, 8, 0], ["deflate", sl(t, 0, 100000), Z_NO_FLUSH],
+                                                ["deflate", sl(m, 0, 23456), Z_FINISH]] + K +
+              [["deflate", sl(m, 23456, 90000), Z_FINISH]]})
+    for wb, lv, d in ((9, 6, t), (-12, 4, m), (10, 9, m), (-9, 7, t), (13, 5, t), (27, 6, m)):
+        S.append({"name": f"rk-w{wb}-L{lv}", "ops": [["init", lv, wb, 8, 0], ["deflate", sl(d, 0, 40000), Z_FINISH]] +
+                  K + [["deflate", sl(d, 40000, 70000), Z_FINISH]]})
+    for fl in (Z_SYNC_FLUSH, Z_PARTIAL_FLUSH, Z_BLOCK):
+        S.append({"name": f"rk-after-flush{fl}", "ops": [["init", 6, 15, 8, 0], ["deflate", sl(t, 0, 40000), fl]] + K +
+                  [["deflate", sl(t, 40000, 80000), Z_FINISH]]})
+    S.append({"name": "rk-after-full-flush", "ops": [["init", 6, 15, 8, 0], ["deflate", sl(t, 0, 40000), Z_NO_FLUSH],
+                                                     ["deflate", sl(t, 40000, 50000), Z_FULL_FLUSH]] + K +
+              [["deflate", sl(t, 50000, 90000), Z_FINISH]]})
+    S.append({"name": "rk-full-flush-then-finish", "ops": [["init", 6, 15, 8, 0],
+                                                           ["deflate", sl(t, 0, 30000), Z_FULL_FLUSH],
+                                                           ["deflate", sl(t, 30000, 60000), Z_FINISH]] + K +
+              [["deflate", sl(t, 60000, 100000), Z_FINISH]]})
+    S.append({"name": "rk-twice-L7", "ops": [["init", 7, 15, 8, 0], ["deflate", sl(m, 0, 20000), Z_FINISH]] + K +
+              [["deflate", sl(m, 20000, 40000), Z_FINISH]] + K + [["deflate", sl(m, 40000, 70000), Z_FINISH]]})
+    S.append({"name": "rk-small-out", "ops": [["init", 6, 15, 8, 0], ["deflate", sl(t, 0, 30000), Z_FINISH, 700]] +
+              K + [["deflate", sl(t, 30000, 100000), Z_FINISH, 1000]]})
+    S.append({"name": "rk-old-dict", "ops": [["init", 6, 15, 8, 0], ["dict", sl(t, 90000, 99000)],
+                                             ["deflate", sl(t, 0, 30000), Z_FINISH]] + K +
+              [["deflate", sl(t, 30000, 60000), Z_FINISH]]})
+    S.append({"name": "rk-dict-only", "ops": [["init", 6, 15, 8, 0], ["dict", sl(t, 0, 5000)]] + K +
+              [["deflate", sl(t, 5000, 40000), Z_FINISH]]})
+    for lv, st in ((9, 1), (4, 4), (6, 2), (6, 3), (5, 0)):
+        S.append({"name": f"rk-then-params-{lv}-{st}", "ops": [["init", 6, 15, 8, 0],
+                                                               ["deflate", sl(t, 0, 30000), Z_FINISH]] + K +
+                  [["params", lv, st], ["deflate", sl(t, 30000, 100000), Z_FINISH]]})
+    for n in (1, 2, 3, 4):
+        S.append({"name": f"rk-tiny-{n}", "ops": [["init", 6, 15, 8, 0], ["deflate", sl(t, 0, n), Z_FINISH]] + K +
+                  [["deflate", sl(t, n, 5000), Z_FINISH]]})
+    for ml, st in ((1, 0), (9, 1), (5, 4)):
+        S.append({"name": f"rk-m{ml}-s{st}", "ops": [["init", 6, 15, ml, st], ["deflate", sl(m, 0, 50000), Z_FINISH]] +
+                  K + [["deflate", sl(m, 50000, 100000), Z_FINISH]]})
+    S.append({"name": "rk-new-chunks", "ops": [["init", 6, 15, 8, 0], ["deflate", sl(t, 0, 30000), Z_FINISH]] + K +
+              [["deflate", sl(t, 30000, 30100), Z_NO_FLUSH], ["deflate", sl(t, 30100, 45000), Z_SYNC_FLUSH],
+               ["deflate", sl(t, 45000, 100000), Z_FINISH]]})
     return S
 
 

@@ -126,6 +126,37 @@ def test_round4_zlib_h_calls_golden(zg):
     assert not bad
 
 
+def test_resetkeep_refusals(zg):
+    """deflateResetKeep carries a deflate_slow stream's window into the next
+    stream (the api_golden rk-* sessions); the carried states it does not model
+    return Z_STREAM_ERROR with strm->msg and leave the stream as it was: a
+    deflate_fast or deflate_stored stream, input still in the lookahead, a
+    stream whose function changed after data, and after a carried window a
+    preset dictionary or a switch to level 0 or to a deflate_fast level, whose
+    longest_match would start from the prev_length deflate_slow left
+    (zgpu_api.cpp deflateResetKeep, deflateParams)."""
+    L = zg.load()
+    d = datagen.make("text", 60000, 41)
+    fin = lambda a, b: ["deflate", d[a:b], 4]
+    cases = [
+        ([["init", 1, 15, 8, 0], fin(0, 20000), ["resetkeep"]], -2),                   # deflate_fast
+        ([["init", 0, -15, 8, 0], fin(0, 20000), ["resetkeep"]], -2),                  # deflate_stored
+        ([["init", 6, 15, 8, 0], ["deflate", d[:100], 0], ["resetkeep"]], -2),         # lookahead
+        ([["init", 6, 15, 8, 0], ["deflate", d[:20000], 0], ["params", 2, 0],
+          ["deflate", d[20000:30000], 0], ["params", 6, 0], ["deflate", d[30000:31000], 2],
+          ["resetkeep"]], -2),                                                           # mixed functions
+        ([["init", 6, -15, 8, 0], fin(0, 20000), ["resetkeep"], ["dict", d[:3000]]], -2),
+        ([["init", 6, -15, 8, 0], fin(0, 20000), ["resetkeep"], ["params", 0, 0]], -2),
+        ([["init", 6, 15, 8, 0], fin(0, 20000), ["resetkeep"], ["params", 2, 0]], -2),  # deflate_fast next
+    ]
+    for ops, want in cases:
+        rcs, _ = run_zsession(L, ops + [["deflate", d[40000:], 4]])
+        got = rcs[len(ops) - 1]
+        got = got[0] if isinstance(got, (tuple, list)) else got
+        assert got == want, (ops[-1], rcs)
+        assert rcs[-1][-1] == 1 or rcs[-1][-1] == -5, rcs         # the stream goes on (or has ended)
+
+
 def test_params_huff_rle_refusals(zg):
     """deflateParams between deflate_slow or deflate_fast and Z_HUFFMAN_ONLY /
     Z_RLE after data is modelled (test_round4_zlib_h_calls_golden's params-hr-*

@@ -2534,6 +2534,9 @@ struct internal_state {
     bool dict_set = false;               // deflateSetDictionary: the zlib header's FDICT + DICTID
     uint32_t dict_id = 0;
     size_t dict_len = 0;                 // the dictionary bytes in the window (<= w_size), just before rd
+                                         // (deflateResetKeep: the window carried over, < w_size + MAX_DIST)
+    bool carried = false;                // deflateResetKeep carried the last stream's window into this one
+    bool fn_mixed = false;               // deflateParams changed the compress function after data
     bool need_dict = false;              // inflate: Z_NEED_DICT answered, waiting for the dictionary
     uint32_t want_dict = 0;              // its DICTID
     gz_header *ihead = nullptr;          // inflateGetHeader: filled as the gzip header arrives
@@ -3447,7 +3450,7 @@ static int deflate_body(z_streamp strm, int flush) {
         if (s->out_pos == before && strm->avail_out == s->out.size() - before && s->level != 0 && slow_fn &&
             P - s->rd >= 2) {
             const char *why = nullptr;
-            if (s->dict_set && P - s->rd >= 3) {
+            if (s->dict_len > 0 && P - s->rd >= 3) {
                 // with a dictionary the first decision may find a match (history), and the stop at the
                 // first lazy literal moves with the parse; without one (the input's first three bytes
                 // nowhere in the dictionary) the literal comes at the second decision, as with no history
@@ -3487,7 +3490,7 @@ static int deflate_body(z_streamp strm, int flush) {
             if (avail > 0 || flush != Z_NO_FLUSH) s->last_flush = -1;
             if (avail > 0 && slow_fn && avail >= 2) {
                 // fill_window's first read: window_size - strstart (a dictionary's bytes stand before it)
-                P = std::min<size_t>(P, s->rd + (size_t(2) << s->wbits) - (s->dict_set ? s->dict_len : 0));
+                P = std::min<size_t>(P, s->rd + (size_t(2) << s->wbits) - s->dict_len);
                 flush = Z_NO_FLUSH;
                 force_skip = true;
             } else if (avail > 0 && flush != Z_NO_FLUSH && flush != Z_FINISH) {
@@ -3693,17 +3696,80 @@ int fn_of(int level, int strategy) {
 
 // deflateResetKeep (deflate.c:635-671): deflateReset without lm_init, so the
 // next stream keeps the window, the hash chains and strstart of this one and
-// may refer back into it.  Taken where that state is the initial one (nothing
-// compressed or preset since deflateInit / deflateReset), where it is exactly
-// deflateReset; a window carried into a new stream is not modelled
-// (Z_STREAM_ERROR with strm->msg, never a different stream).
+// may refer back into it.  Where that state is the initial one (nothing
+// compressed or preset since deflateInit / deflateReset) it is exactly
+// deflateReset.  After a stream that deflate_slow (levels 4-9, not
+// Z_HUFFMAN_ONLY / Z_RLE) ran from its part start (deflateInit, deflateReset or
+// its last Z_FULL_FLUSH) to a point with nothing left in the lookahead -- the
+// end of Z_FINISH, or a flush call that took all its input -- the carried
+// state is a preset dictionary in all but its bookkeeping:
+//  - deflate_slow hashed every string of the part but the last two, which wait
+//    as s->insert (deflate.c:1941-2027, :2030-2032), as deflateSetDictionary
+//    leaves them (deflate.c:593-605);
+//  - prev_length = match_length = MIN_MATCH-1 and match_available = 0 there
+//    (the flush tail, deflate.c:2030-2040), as after deflateSetDictionary;
+//  - the window holds the part's bytes from the window offset on, strstart =
+//    block_start = their count P (< w_size + MAX_DIST: fill_window slides at
+//    the loop top that ended the parse), so the next stream's part is those P
+//    bytes then its input, in window coordinates, and its slides fall where
+//    the reference's do;
+//  - strm->adler restarts (1, or 0 for gzip) and covers only the new input; a
+//    zlib header carries FDICT with that start value as DICTID, since
+//    deflate.c:1030-1036 tests strstart != 0.
+// Other carried states (deflate_fast's selective hashing, deflate_stored's
+// window, a huffman-only / RLE stretch, input still in the lookahead) are not
+// modelled (Z_STREAM_ERROR with strm->msg, never a different stream).
 int deflateResetKeep(z_streamp strm) {
     if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
     const bool fresh = s->in_base + s->in.size() == 0 && s->rd == 0 && !s->flushed && !s->dict_set &&
                        s->l0_hist.empty() && s->st_strstart == 0 && strm->total_in == 0;
-    if (!fresh) return unsupported(strm, "deflateResetKeep: a window carried into the next stream is not modelled");
-    return deflateReset(strm);
+    if (fresh) return deflateReset(strm);
+    const char *why = "deflateResetKeep: a window carried into the next stream is modelled after deflate_slow "
+                      "(levels 4-9) ran the whole part to a point with no input pending only";
+    if (s->level < 4 || fn_of(s->level, s->strategy) != 2 || s->fn_mixed || !s->hr.empty() || s->level == 0 ||
+        (!s->finished && pending_input(s)) || s->tentative)
+        return unsupported(strm, why);
+    // the window: the part's bytes from the window offset S to the end E.  The parse ended at a loop top
+    // whose fill_window slid once more if strstart >= w_size + MAX_DIST (deflate.c:1535-1545), and every
+    // slide found strstart at least that, so strstart = E below w_size + MAX_DIST, else the one value
+    // in [MAX_DIST, w_size + MAX_DIST) that E reaches by whole slides: a function of E alone
+    const uint64_t W = uint64_t(1) << s->wbits, maxd = W - kMinLookahead;
+    const uint64_t E = std::min<uint64_t>(s->rd, s->in_base + s->in.size());
+    const uint64_t S = E - (E < W + maxd ? E : maxd + (E - maxd) % W);
+    // a one-call stream keeps its last w_size bytes: the older part of the window lies beyond MAX_DIST of
+    // every later position (no candidate, no byte compared; a chain walk stops at the first link below the
+    // limit, whatever string it is), so it only has to hold its place
+    const uint64_t lo = std::max<uint64_t>(S, s->in_base);
+    if (E - lo < std::min<uint64_t>(E - S, W)) return unsupported(strm, why);
+    try {
+        zvec<uint8_t> win(s->al);
+        win.resize((size_t)(lo - S), 0);
+        win.insert(win.end(), s->in.begin() + (std::ptrdiff_t)(lo - s->in_base),
+                   s->in.begin() + (std::ptrdiff_t)(E - s->in_base));
+        const size_t P = win.size();
+        const int rc = deflateReset(strm);
+        if (rc != Z_OK || P == 0) return rc;
+        s = strm->state;
+        s->in.assign(win.begin(), win.end());
+        s->in_base = s->res_S = 0;
+        s->dict_len = P;
+        s->carried = true;
+        s->res_pos = s->rd = s->rd_seen = s->flush_done = s->ck_pos = P;
+        s->res_E = P;
+        s->res_cut = 0;                                 // the last two strings wait as s->insert
+        s->zl_p = s->zl_m = kMinMatch - 1;
+        s->zl_pos = ~0ull;
+        if (s->wrap == 1) {                             // strstart != 0: FDICT, DICTID = adler32 start value
+            s->dict_set = true;
+            s->dict_id = (uint32_t)strm->adler;
+        }
+        s->stale = true;
+        s->flushed = true;                              // the part path (bit and parse offsets)
+        return Z_OK;
+    } catch (const std::bad_alloc &) {
+        return Z_MEM_ERROR;
+    }
 }
 
 // deflateSetDictionary (deflate.c:550-613).  Accepted on a zlib stream
@@ -3723,6 +3789,8 @@ int deflateSetDictionary(z_streamp strm, const Bytef *dictionary, uInt dictLengt
     if (s->wrap == 2 || (s->wrap == 1 && s->last_flush != -2)) return Z_STREAM_ERROR;
     if (s->level != 0 && pending_input(s)) return Z_STREAM_ERROR;        // s->lookahead != 0
     if (s->finished) return unsupported(strm, "deflateSetDictionary: the stream has ended");
+    if (s->carried && dictLength > 0)
+        return unsupported(strm, "deflateSetDictionary: after deflateResetKeep carried a window, not modelled");
     try {
         if (s->wrap == 1) strm->adler = ck_adler32(strm->adler, dictionary, dictLength);
         const uint64_t wsize = uint64_t(1) << s->wbits;
@@ -3897,6 +3965,16 @@ int deflateParams(z_streamp strm, int level, int strategy) {
     // deflate_slow <-> deflate_huff / deflate_rle after data: the stretch the
     // latter parse is left out of the chains (internal_state::hr)
     const int of = fn_of(s->level, s->strategy), nf = fn_of(level, strategy);
+    // deflate_stored after a preset dictionary or a carried window (the bytes wait in the part's input as
+    // history, where deflate_stored_call would take them for data) is not modelled
+    if (!started && level == 0 && s->level != 0 && s->dict_len > 0)
+        return unsupported(strm, "deflateParams: level 0 after a preset dictionary or a carried window is not "
+                                 "modelled");
+    // deflate_fast's longest_match starts from prev_length, which deflate_slow left at 0 when its last
+    // symbol was a match (deflate.c:2008-2015): not known here for a carried window
+    if (!started && s->carried && nf == 1 && of != 1)
+        return unsupported(strm, "deflateParams: a deflate_fast level after deflateResetKeep carried a window is "
+                                 "not modelled");
     const bool enter_hr = started && !s->finished && of < 3 && nf >= 3 && level != 0 && s->level != 0;
     const bool leave_hr = started && !s->finished && of >= 3 && nf < 3 && level != 0 && s->level != 0;
     if (enter_hr) {
@@ -3922,6 +4000,7 @@ int deflateParams(z_streamp strm, int level, int strategy) {
         if (strm->avail_in || pending_input(s)) return Z_BUF_ERROR;
     }
     try {
+        if (started && of != nf) s->fn_mixed = true;
         if (enter_hr) {
             internal_state::HrStretch h{};
             h.a = s->in_base + s->in.size();

@@ -4067,44 +4067,78 @@ __device__ __attribute__((always_inline)) inline void rget2(const RHeap &H, uint
         b = j < 320u ? rl(H.r[4], l + 1) : kHInf;
     }
 }
-// pqdownheap (trees.c:509-527) of key v entering at node k of level D
-template <int D>
-__device__ __attribute__((always_inline)) inline void r_down(RHeap &H, int, uint32_t k, uint32_t v) {
-    if constexpr (D < 8) {
-        const uint32_t j = k << 1;
-        uint32_t a, b;
-        rget2<D + 1>(H, j, a, b);
-        const bool right = hle(b, a);                   // trees.c:515: heap[j+1] <= heap[j]
-        // j + 1 made opaque: `right ? j + 1 : j` would fold to j | right, and a bool used
-        // past the branch below is kept as a lane mask and rebuilt through VALU ops and a
-        // readfirstlane per level; this way the select stays one s_cselect
-        uint32_t j1 = j + 1;
-        asm volatile("" : "+s"(j1));
-        const uint32_t hj = right ? b : a, jn = right ? j1 : j;
-        if (!hle(v, hj)) {
-            rset<D>(H, k, hj);
-            r_down<D + 1>(H, 0, jn, v);
-            return;
-        }
-    }
-    rset<D>(H, k, v);
-}
 __device__ __attribute__((always_inline)) inline void rset_any(RHeap &H, uint32_t j, uint32_t v) {
     const bool me = (threadIdx.x & 63u) == (j & 63u);
 #pragma unroll
     for (int r = 0; r < 5; r++) H.r[r] = (me && (j >> 6) == (uint32_t)r) ? v : H.r[r];
 }
+// pqdownheap (trees.c:509-527) of key v entering at node k of level D.  `live` (~0 or 0) says whether v
+// is still moving down, and a level writes its node only while live.  Reads come from S, the heap as it
+// was when the sift began: a sift writes only nodes above the ones it reads, so the reads never wait on
+// the writes.  Every ZGPU_SIFT_EXIT levels a wave-uniform test ends a sift that has placed v: 1 (a test
+// per level) took the runs block's merges 708k -> 641k clock ticks against the branchy sift it replaced;
+// 2, 3 and 9 levels between tests were slower than that, the levels walked past the placement costing
+// more than the tests (profiles/r06y_plan_clock_onewave_sift_exit_variants.log, r06z_*).
+#ifndef ZGPU_SIFT_EXIT
+#define ZGPU_SIFT_EXIT 1
+#endif
+template <int D>
+__device__ __attribute__((always_inline)) inline void rset_if(RHeap &H, uint32_t k, uint32_t v, uint32_t live) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t t = (k & 63u) | (~live & 64u);          // 64: no lane
+    if constexpr (D <= 5) H.r[0] = lane == t ? v : H.r[0];
+    else if constexpr (D == 6) H.r[1] = lane == t ? v : H.r[1];
+    else if constexpr (D == 7) {
+        const uint32_t hi = (k & 64u) ? t : 64u, lo = (k & 64u) ? 64u : t;
+        H.r[2] = lane == lo ? v : H.r[2];
+        H.r[3] = lane == hi ? v : H.r[3];
+    } else H.r[4] = lane == t ? v : H.r[4];
+}
+template <int D>
+__device__ __attribute__((always_inline)) inline void r_sift(RHeap &H, const RHeap &S, uint32_t k, uint32_t v,
+                                                             uint32_t live) {
+    if constexpr (D < 8) {
+        const uint32_t j = k << 1;
+        uint32_t a, b;
+        rget2<D + 1>(S, j, a, b);
+        const bool right = hle(b, a);                   // trees.c:515: heap[j+1] <= heap[j]
+        uint32_t j1 = j + 1;                            // opaque: jn stays one s_cselect, not VALU ops
+        asm volatile("" : "+s"(j1));
+        const uint32_t hj = right ? b : a, jn = right ? j1 : j;
+        const uint32_t go = hle(v, hj) ? 0u : live;      // trees.c:518: v moves below k
+        rset_if<D>(H, k, go ? hj : v, live);
+        if constexpr ((D + 1) % ZGPU_SIFT_EXIT == 0) {
+            if (go == 0) return;
+        }
+        r_sift<D + 1>(H, S, jn, v, go);
+    } else {
+        rset_if<8>(H, k, v, live);
+    }
+}
+template <int D>
+__device__ __attribute__((always_inline)) inline void r_sift0(RHeap &H, uint32_t k, uint32_t v) {
+    const RHeap S = H;
+    r_sift<D>(H, S, k, v, ~0u);
+}
+// heap[j] for any j < 320 without a branch: one readlane per register and scalar selects
+__device__ __attribute__((always_inline)) inline uint32_t rget_sel(const RHeap &H, uint32_t j) {
+    const uint32_t l = j & 63u, r = j >> 6;
+    const uint32_t v0 = rl(H.r[0], l), v1 = rl(H.r[1], l), v2 = rl(H.r[2], l), v3 = rl(H.r[3], l),
+                   v4 = rl(H.r[4], l);
+    const uint32_t x = r == 0 ? v0 : v1, y = r == 2 ? v2 : v3;
+    return r >= 4 ? v4 : (r >= 2 ? y : x);
+}
 __device__ inline void r_down_any(RHeap &H, int heap_len, uint32_t k) {   // build_tree's heapify
     const uint32_t v = rget_any(H, k);
     switch (31 - __builtin_clz(k)) {
-    case 0: r_down<0>(H, heap_len, k, v); break;
-    case 1: r_down<1>(H, heap_len, k, v); break;
-    case 2: r_down<2>(H, heap_len, k, v); break;
-    case 3: r_down<3>(H, heap_len, k, v); break;
-    case 4: r_down<4>(H, heap_len, k, v); break;
-    case 5: r_down<5>(H, heap_len, k, v); break;
-    case 6: r_down<6>(H, heap_len, k, v); break;
-    default: r_down<7>(H, heap_len, k, v); break;       // k <= heap_len / 2 < 256
+    case 0: r_sift0<0>(H, k, v); break;
+    case 1: r_sift0<1>(H, k, v); break;
+    case 2: r_sift0<2>(H, k, v); break;
+    case 3: r_sift0<3>(H, k, v); break;
+    case 4: r_sift0<4>(H, k, v); break;
+    case 5: r_sift0<5>(H, k, v); break;
+    case 6: r_sift0<6>(H, k, v); break;
+    default: r_sift0<7>(H, k, v); break;                 // k <= heap_len / 2 < 256
     }
 }
 
@@ -4157,12 +4191,16 @@ __device__ __attribute__((always_inline)) inline void w_build(TreeRef &t, TreeLD
     PCLK(11);
     int heap_max = kHeapSize;
     uint32_t node = (uint32_t)elems;
+    uint32_t gidx[5];                                  // the heap slot each lane holds per register
+#pragma unroll
+    for (int r = 0; r < 5; r++) gidx[r] = (uint32_t)(r * 64) + lane;
     do {                                               // trees.c:583-604
         const uint32_t kn = rl(H.r[0], 1);
-        const uint32_t last = rget_any(H, (uint32_t)heap_len);
-        rset_any(H, (uint32_t)heap_len, kHInf);
+        const uint32_t last = rget_sel(H, (uint32_t)heap_len);
+#pragma unroll
+        for (int r = 0; r < 5; r++) H.r[r] = gidx[r] == (uint32_t)heap_len ? kHInf : H.r[r];
         heap_len--;
-        r_down<0>(H, heap_len, 1, last);
+        r_sift0<0>(H, 1, last);
         const uint32_t km = rl(H.r[0], 1);
         heap_max -= 2;
         if (lane == 0) {
@@ -4173,7 +4211,7 @@ __device__ __attribute__((always_inline)) inline void w_build(TreeRef &t, TreeLD
         }
         const uint32_t f = (kn >> 16) + (km >> 16);
         const uint32_t dn = (kn >> 10) & 63u, dm = (km >> 10) & 63u;
-        r_down<0>(H, heap_len, 1, hkey(f, (dn >= dm ? dn : dm) + 1, node));
+        r_sift0<0>(H, 1, hkey(f, (dn >= dm ? dn : dm) + 1, node));
         node++;
     } while (heap_len >= 2);
     heap_max--;
