@@ -49,8 +49,12 @@
  *     between deflate_slow levels (4..9, memLevel <= 8) or deflate_fast
  *     levels (1..3) and those strategies and back to the same function, and
  *     back after a first call of a single byte;
- *   - deflatePrime with input pending after a call that did not reach its end,
- *     or after Z_STREAM_END;
+ *   - deflatePrime after a call that stopped on a full output buffer (or with
+ *     output pending) when its bits complete a byte: the reference writes
+ *     that byte inside its pending output (put_byte at pending_buf[pending])
+ *     and ends the stream with a stale buffer byte; bits that complete none
+ *     are modelled.  Also after a flush call that did not reach its marker,
+ *     and after Z_STREAM_END;
  *   - deflateSetDictionary after the stream has ended;
  *   - deflateResetKeep on a stream that has taken input, except after a
  *     stream that deflate_slow (levels 4..9, not Z_HUFFMAN_ONLY / Z_RLE) ran

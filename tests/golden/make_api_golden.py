@@ -262,7 +262,56 @@ def deflate_sessions():
                                                  ["deflate", sl(m, 0, 100000), Z_FINISH], ["used"], ["reset"],
                                                  ["resetkeep"], ["deflate", sl(t, 0, 100000), Z_FINISH]]})
     S += resetkeep_sessions()
+    S += prime_paused_sessions()
     return S
+
+
+def prime_paused_sessions():
+    """deflatePrime after a deflate() call that stopped on a full output buffer
+    inside its input (round 6, deflate.c:731-757): the bits go after the block
+    the call flushed last.  The next call offers more input, the same input
+    again (the part the last call left), or a flush; primes in a row; every
+    compress function and wrapper.  The reference keeps that call's output
+    pending with pending_out moved on, and deflatePrime's put_byte writes a
+    completed byte at pending_buf[pending] -- inside the output still to go --
+    so only bits that complete no byte (deflatePending's bits + the primed
+    ones < 8, read from the reference here) give a whole stream; the rest are
+    refused (tests/test_gpu_zstream.py::test_prime_after_pause_refusal)."""
+    S = []
+    t = ["text", 300000, 84]
+    m = ["mix", 300000, 85]
+    sl = lambda d, a, b: d + [a, b]
+    ref = Reference()
+    for lv, st, wb, d, out in ((6, 0, 15, t, 1500), (9, 0, -15, m, 3000), (4, 1, 31, t, 700), (2, 0, 15, m, 2000),
+                               (1, 0, -15, t, 5000), (6, 3, 15, m, 1500), (6, 2, -15, t, 4000), (7, 4, 15, m, 30000),
+                               (5, 0, -12, t, 1000), (3, 0, 13, m, 2500), (8, 0, 15, t, 900), (6, 1, -15, m, 6000)):
+        base = [["init", lv, wb, 8, st], ["deflate1", sl(d, 0, 150000), Z_NO_FLUSH, out], ["pending"]]
+        rcs, _ = run_deflate_raw(ref.L, base)
+        k = 7 - rcs[-1][2]                         # bits that complete no byte
+        if k < 1:
+            continue
+        tag = f"L{lv}-s{st}-w{wb}"
+        S.append({"name": f"pp-more-{tag}", "ops": base + [
+            ["prime", k, 0x55], ["pending"], ["deflate", sl(d, 150000, 300000), Z_FINISH, 4000, True]]})
+        S.append({"name": f"pp-flush-{tag}", "ops": base + [
+            ["prime", k, 1], ["deflate1", sl(d, 0, 0), Z_SYNC_FLUSH, 1 << 20, True],
+            ["deflate", sl(d, 150000, 300000), Z_FINISH]]})
+        S.append({"name": f"pp-finish-{tag}", "ops": base + [
+            ["prime", k, 0x2a], ["deflate1", sl(d, 0, 0), Z_FINISH, 1 << 20, True]]})
+        if k >= 2:
+            S.append({"name": f"pp-same-{tag}", "ops": base + [
+                ["prime", k - 1, 0x5a5], ["deflate1", sl(d, 0, 0), Z_NO_FLUSH, out, True], ["prime", 1, 1],
+                ["pending"], ["deflate1", sl(d, 0, 0), Z_NO_FLUSH, 1 << 20, True],
+                ["deflate", sl(d, 150000, 300000), Z_FINISH]]})
+            S.append({"name": f"pp-twice-{tag}", "ops": base + [
+                ["prime", 1, 1], ["prime", k - 1, 0x7f], ["pending"],
+                ["deflate", sl(d, 150000, 200000), Z_SYNC_FLUSH, 0, True], ["deflate", sl(d, 200000, 300000), Z_FINISH]]})
+    return S
+
+
+def run_deflate_raw(L, ops):
+    return run_zsession(L, [[o[0], _slice(o[1])] + o[2:] if o[0] in ("deflate", "dict", "deflate1") else o
+                            for o in ops])
 
 
 def resetkeep_sessions():
@@ -363,7 +412,7 @@ def _slice(spec):
 
 
 def run_deflate(L, sess):
-    ops = [[o[0], _slice(o[1])] + o[2:] if o[0] in ("deflate", "dict") else o for o in sess["ops"]]
+    ops = [[o[0], _slice(o[1])] + o[2:] if o[0] in ("deflate", "dict", "deflate1") else o for o in sess["ops"]]
     rcs, out = run_zsession(L, ops)
     return {"res": json.loads(json.dumps(rcs)), "out": [len(out), hashlib.sha256(out).hexdigest()]}
 

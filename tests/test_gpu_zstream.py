@@ -157,6 +157,26 @@ def test_resetkeep_refusals(zg):
         assert rcs[-1][-1] == 1 or rcs[-1][-1] == -5, rcs         # the stream goes on (or has ended)
 
 
+def test_prime_after_pause_refusal(zg):
+    """deflatePrime after a call that stopped on a full output buffer inside its
+    input is modelled where the bits complete no byte (api_golden pp-*
+    sessions); bits that would complete one are refused: the reference's
+    put_byte writes that byte at pending_buf[pending], inside the output still
+    pending, and its stream ends with a stale buffer byte (zgpu_api.cpp
+    deflatePrime).  The stream goes on as if the call had not been made."""
+    import zlib as pyzlib
+    L = zg.load()
+    d = datagen.make("text", 200000, 42)
+    base = [["init", 6, -15, 8, 0], ["deflate1", d[:150000], 0, 1500], ["pending"]]
+    rcs, _ = run_zsession(L, base)
+    assert rcs[1][2] == 0 and rcs[1][1] > 0, rcs         # stopped on a full output buffer inside its input
+    held = rcs[-1][2]
+    rcs, z = run_zsession(L, base + [["prime", 8 - held, 3], ["deflate", d[150000:], 4, 4000, True]])
+    assert rcs[3] == -2, rcs
+    assert rcs[-1][-1] == 1, rcs
+    assert pyzlib.decompressobj(-15).decompress(z) == d
+
+
 def test_params_huff_rle_refusals(zg):
     """deflateParams between deflate_slow or deflate_fast and Z_HUFFMAN_ONLY /
     Z_RLE after data is modelled (test_round4_zlib_h_calls_golden's params-hr-*

@@ -481,6 +481,9 @@ def run_zsession(L, ops, version=b"1.3.1.1-motley"):
             left = data[len(data) - s.avail_in:] if s.avail_in else b""
         elif k == "bound":
             rcs.append(int(L.deflateBound(C.byref(s), op[1])))
+        elif k == "pending":                     # deflatePending: rc, bytes, bits
+            pn, pb = C.c_uint(0), C.c_int(0)
+            rcs.append([L.deflatePending(C.byref(s), C.byref(pn), C.byref(pb)), pn.value, pb.value])
         elif k == "used":                        # deflateUsed
             b = C.c_int(-99)
             rcs.append([L.deflateUsed(C.byref(s), C.byref(b)), b.value])

@@ -10,9 +10,9 @@ mine = json.load(open("gpurun_out/dbg/rk.json"))
 for s in g["deflate"]:
     if s["name"] not in mine:
         continue
-    ops = [[o[0], _slice(o[1])] + o[2:] if o[0] in ("deflate", "dict") else o for o in s["ops"]]
+    ops = [[o[0], _slice(o[1])] + o[2:] if o[0] in ("deflate", "dict", "deflate1") else o for o in s["ops"]]
     rcs, z = run_zsession(ref.L, ops)
-    k = next(i for i, o in enumerate(ops) if o[0] == "resetkeep")
+    k = next(i for i, o in enumerate(ops) if o[0] in ("resetkeep", "prime"))
     _, z0 = run_zsession(ref.L, ops[:k])
     m = mine[s["name"]]
     zm = bytes.fromhex(m["z"])

@@ -3513,7 +3513,16 @@ static int deflate_body(z_streamp strm, int flush) {
     uint32_t own = ~0u;
     if (s->ev_done < s->ev_type.size()) {                       // the last call did not get to its event
         const size_t le = s->ev_type.size() - 1;
-        if (s->ev_type[le] == 0) {                              // a stop it paused before
+        if (s->ev_type[le] == 0 && P != s->ev_pos[le] && le >= 1 && s->ev_type[le - 1] == kEvPrime &&
+            s->ev_pos[le - 1] == s->ev_pos[le] && s->ev_done == le) {
+            // the stop deflatePrime left due behind its bits (a pause before them stands for the block the
+            // call stopped after): more input, and the reference reads on from there (deflatePrime)
+            s->ev_pos.pop_back();
+            s->ev_type.pop_back();
+            s->ev_aux.pop_back();
+            s->ev_done = s->ev_type.size();
+            s->stale = true;
+        } else if (s->ev_type[le] == 0) {                       // a stop it paused before
             if (P != s->ev_pos[le]) {
                 // more input: the reference goes on from the paused block
                 // reading up to the new end, the stop never comes
@@ -3678,7 +3687,19 @@ int deflatePending(z_streamp strm, unsigned *pending, int *bits) {
     if (!strm || !strm->state || strm->state->inflating) return Z_STREAM_ERROR;
     internal_state *s = strm->state;
     if (pending) *pending = (unsigned)(s->out.size() - s->out_pos);
-    if (bits) *bits = s->finished ? 0 : (int)((s->level == 0 ? s->res_bits : s->proc_bits) & 7);
+    if (bits) {
+        uint64_t b = s->level == 0 ? s->res_bits : s->proc_bits;
+        if (s->prime_due && s->level != 0 && !s->ev_type.empty()) {
+            // deflatePrime's bits no job has written yet are in bi_buf already (deflate.c:745-755)
+            size_t k = s->ev_type.size() - 1;
+            if (s->ev_type[k] == 0 && k > 0 && s->ev_type[k - 1] == kEvPrime) k--;   // its call's stop, due again
+            for (; s->ev_type[k] == kEvPrime; k--) {
+                b += s->ev_aux[k] >> 16;
+                if (k == 0) break;
+            }
+        }
+        *bits = s->finished ? 0 : (int)(b & 7);
+    }
     return Z_OK;
 }
 
@@ -4056,6 +4077,65 @@ int deflatePrime(z_streamp strm, int bits, int value) {
         // progress.  The parse stands at the last call's stop there; the bits
         // become an event at that stop (kEvPrime), which the next job's parse
         // turns into a marker record that k_encode writes.
+        //
+        // After a call that stopped on a full output buffer inside its input
+        // (FLUSH_BLOCK's need_more, its stop still due) the reference stands
+        // right after the block it flushed last: the bits go after that block
+        // and ahead of the next.  The stop becomes the pause the next deflate()
+        // would make of it (the block's end; the parse reads on from there),
+        // the bits an event right after it, which the parse writes as the
+        // pause passes, and the stop is due again behind them (round 6).
+        const size_t le = s->ev_type.empty() ? 0 : s->ev_type.size() - 1;
+        const bool due_stop = s->level != 0 && !s->ev_type.empty() && s->ev_type[le] == 0 && s->ev_done == le;
+        const bool after_pause_prime = due_stop && le >= 1 && s->ev_type[le - 1] == kEvPrime &&
+                                       s->ev_pos[le - 1] == s->ev_pos[le];
+        const bool paused = due_stop && s->t > 0 && s->t <= s->items.size() && s->items[s->t - 1].kind == kItBlock;
+        if (due_stop && (after_pause_prime || paused)) {
+            if (bits == 0) return Z_OK;
+            // The call left output pending with pending_out moved past pending_buf.  deflatePrime's
+            // _tr_flush_bits puts whole bytes at pending_buf[pending] (put_byte indexes by the pending
+            // count, deflate.h), inside the bytes still to go out, and the stream's last pending byte
+            // becomes whatever the buffer held there: only bits that complete no byte keep the stream whole
+            uint32_t held = (uint32_t)(s->proc_bits & 7);
+            for (size_t k = le; k-- > 0 && s->ev_type[k] == kEvPrime && s->ev_pos[k] == s->ev_pos[le];)
+                held += (uint32_t)(s->ev_aux[k] >> 16);
+            if (held + (uint32_t)bits >= 8)
+                return unsupported(strm, "deflatePrime: after a call that stopped on a full output buffer, bits "
+                                         "that complete a byte (the reference writes it into its pending output at "
+                                         "the pending count's offset) are not modelled");
+            try {
+                const uint32_t v = (uint32_t)value & ((1u << bits) - 1u);
+                const uint64_t P0 = s->ev_pos[le];
+                const uint64_t arg = (uint64_t)v | ((uint64_t)bits << 16);
+                if (after_pause_prime) {                        // another deflatePrime there: in front of the stop
+                    s->ev_pos.insert(s->ev_pos.begin() + (std::ptrdiff_t)le, P0);
+                    s->ev_type.insert(s->ev_type.begin() + (std::ptrdiff_t)le, kEvPrime);
+                    s->ev_aux.insert(s->ev_aux.begin() + (std::ptrdiff_t)le, arg);
+                } else {
+                    s->ev_type[le] = kEvPause;
+                    s->ev_aux[le] = s->items[s->t - 1].in_end;
+                    s->ev_pos.push_back(P0);
+                    s->ev_type.push_back(kEvPrime);
+                    s->ev_aux.push_back(arg);
+                    s->ev_pos.push_back(P0);
+                    s->ev_type.push_back(0);
+                    s->ev_aux.push_back(0);
+                    // a pause at the resume point's own block is behind it (drop_pause_behind_resume)
+                    if (s->res_item >= 0 && s->res_pos >= s->ev_aux[le]) {
+                        s->ev_pos.erase(s->ev_pos.begin() + (std::ptrdiff_t)le);
+                        s->ev_type.erase(s->ev_type.begin() + (std::ptrdiff_t)le);
+                        s->ev_aux.erase(s->ev_aux.begin() + (std::ptrdiff_t)le);
+                        if (s->res_ev > le) s->res_ev = le;
+                    }
+                }
+                s->ev_done = s->ev_type.size() - 1;             // the stop is due again
+                s->stale = true;
+                s->prime_due = true;
+                return Z_OK;
+            } catch (const std::bad_alloc &) {
+                return Z_MEM_ERROR;
+            }
+        }
         if (s->level == 0 || s->ev_type.empty() || s->ev_done != s->ev_type.size() || s->tentative ||
             (s->ev_type.back() != 0 && s->ev_type.back() != kEvPrime))
             return unsupported(strm, "deflatePrime: input pending after a call that did not reach its end");
@@ -4074,6 +4154,12 @@ int deflatePrime(z_streamp strm, int bits, int value) {
         }
     }
     if (s->finished) return unsupported(strm, "deflatePrime: after Z_STREAM_END");
+    // output still pending after a call that filled its buffer: a completed byte would go to
+    // pending_buf[pending], inside that output (put_byte, as in the paused case above)
+    if (s->out_pos < s->out.size() && (uint32_t)(s->res_bits & 7) + (uint32_t)bits >= 8)
+        return unsupported(strm, "deflatePrime: with output pending, bits that complete a byte (the reference "
+                                 "writes it into its pending output at the pending count's offset) are not "
+                                 "modelled");
     try {
         uint32_t nb = (uint32_t)(s->res_bits & 7);
         uint64_t acc = (s->res_byte & ((1u << nb) - 1u)) | ((uint64_t)((uint32_t)value & ((1u << bits) - 1u)) << nb);

@@ -1400,6 +1400,11 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
     po.srec = job.srec;
     bool avail = false, done = false;
     FlushEv fe = flush_ev(job);
+    while (fe.prime()) {                       // deflatePrime at the resume point (a pause behind it): bits first
+        if (lane == 0 && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+        po.marker(p, kMarkPrime, lane, fe.prime_arg());
+        fe.i++;
+    }
     uint32_t lim = (uint32_t)fe.limit(n);      // input deflate() has been given
 
     uint32_t t0 = p & ~15u;
@@ -1475,6 +1480,11 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
                             if (fe.pause_at(a)) {
                                 if (lane == 0 && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
                                 fe.i++;
+                                while (fe.prime()) {          // deflatePrime while the call stood here
+                                    if (lane == 0 && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+                                    po.marker(a, kMarkPrime, lane, fe.prime_arg());
+                                    fe.i++;
+                                }
                                 lim = (uint32_t)fe.limit(n);
                             }
                         }
@@ -1532,6 +1542,11 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
                     if (fe.pause_at(p)) {
                         if (lane == 0 && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
                         fe.i++;
+                        while (fe.prime()) {                  // deflatePrime while the call stood here
+                            if (lane == 0 && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+                            po.marker(p, kMarkPrime, lane, fe.prime_arg());
+                            fe.i++;
+                        }
                         lim = (uint32_t)fe.limit(n);
                     }
                 }
@@ -1545,6 +1560,11 @@ __global__ __launch_bounds__(64) void k_parse_slow(DeflateJob job, int only_flag
                     if (fe.pause_at(p)) {
                         if (lane == 0 && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
                         fe.i++;
+                        while (fe.prime()) {                  // deflatePrime while the call stood here
+                            if (lane == 0 && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+                            po.marker(p, kMarkPrime, lane, fe.prime_arg());
+                            fe.i++;
+                        }
                         lim = (uint32_t)fe.limit(n);
                     }
                 }
@@ -3361,6 +3381,11 @@ __global__ __launch_bounds__(64) void k_parse_ev(DeflateJob job) {
     po.block_start = p; po.S = 0; po.E = (int64_t)job.e0 > p ? (int64_t)job.e0 : p;
     po.srec = job.srec;
     FlushEv fe = flush_ev(job);
+    while (fe.prime()) {                       // deflatePrime at the resume point (a pause behind it): bits first
+        if (job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+        po.marker(p, kMarkPrime, fe.prime_arg());
+        fe.i++;
+    }
     int64_t lim = fe.limit(n);
     bool done = false;
     for (;;) {
@@ -3417,6 +3442,11 @@ __global__ __launch_bounds__(64) void k_parse_ev(DeflateJob job) {
             if (fe.pause_at(p)) {
                 if (job.ev_blk) job.ev_blk[fe.i] = po.nblk;
                 fe.i++;
+                while (fe.prime()) {                                  // deflatePrime while the call stood here
+                    if (job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+                    po.marker(p, kMarkPrime, fe.prime_arg());
+                    fe.i++;
+                }
                 lim = fe.limit(n);
             }
         }
@@ -3631,6 +3661,11 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
     const int best0 = kEv ? job.zp0 : kMinMatch - 1;
     uint32_t match_length = kEv ? (uint32_t)job.zm0 : kMinMatch - 1;
     FlushEv fe = flush_ev(job);
+    while (kEv && fe.prime()) {         // deflatePrime at the resume point (a pause behind it): bits first
+        if (lead && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+        po.marker(p, kMarkPrime, fe.prime_arg());
+        fe.i++;
+    }
     P lim = kEv ? (P)fe.limit(n) : n;   // input deflate() has been given
     // s->insert: strings a flush left unhashed (a resumed job starts right
     // after a flush at its window offset + start; none at a block cut)
@@ -3840,6 +3875,11 @@ __global__ __launch_bounds__(64) void k_parse_fast(DeflateJob job, uint32_t *hea
             if (kEv && fe.pause_at(p)) {
                 if (lead && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
                 fe.i++;
+                while (fe.prime()) {                                  // deflatePrime while the call stood here
+                    if (lead && job.ev_blk) job.ev_blk[fe.i] = po.nblk;
+                    po.marker(p, kMarkPrime, fe.prime_arg());
+                    fe.i++;
+                }
                 lim = (P)fe.limit(n);
             }
         }
