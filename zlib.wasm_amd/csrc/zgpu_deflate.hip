@@ -5278,6 +5278,29 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
         }
     };
     if (tid == 0) {
+        // lane 0's header bits go through a register bit writer: whole words are stored to the staging
+        // words (zeroed above, no other writer yet), where put()'s LDS read-modify-write of s_obit and
+        // atomic ORs per call were dependent round trips (a full literal tree's header is ~300 calls)
+        uint64_t acc = 0;
+        int nacc = (int)((s_obit - sbase) & 31);
+        int wi = (int)((s_obit - sbase) >> 5);
+        auto put = [&](uint64_t v, int nb) {              // v < 2^32, nb <= 32
+            acc |= v << nacc;
+            nacc += nb;
+            if (nacc >= 32) {
+                stg[wi++] = (uint32_t)acc;
+                acc >>= 32;
+                nacc -= 32;
+            }
+        };
+        auto align8 = [&] {
+            nacc = (nacc + 7) & ~7;
+            if (nacc >= 32) {
+                stg[wi++] = (uint32_t)acc;
+                acc >>= 32;
+                nacc -= 32;
+            }
+        };
         if (k == 0 && job.bit0) put(job.byte0, (int)job.bit0);   // a resumed streaming job's partial byte
         if (k == 0 && job.wrap == 1) {                     // zlib header (deflate.c:1004-1037)
             uint32_t header = (8u + ((uint32_t)(job.wbits - 8) << 4)) << 8;
@@ -5297,7 +5320,7 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
         const uint64_t stored_len = br.in_end - br.in_start;
         put((uint32_t)(type << 1) + (last ? 1u : 0u), 3);
         if (type == 0) {
-            s_obit = (s_obit + 7) & ~7ll;
+            align8();
             put((uint32_t)stored_len & 0xffffu, 16);
             put((~(uint32_t)stored_len) & 0xffffu, 16);
         } else if (type == 2) {                            // send_all_trees (trees.c:800-824)
@@ -5313,6 +5336,8 @@ __global__ __launch_bounds__(kEncThreads) void k_enc_emit(DeflateJob job) {
             t_rle(s_llen, lcodes - 1, snd);
             t_rle(s_dlen, dcodes - 1, snd);
         }
+        if (nacc > 0) stg[wi] = (uint32_t)acc;
+        s_obit = sbase + 32ll * wi + nacc;
     }
     __syncthreads();
     if (type == 0) {                                       // stored: the raw bytes
