@@ -1186,9 +1186,17 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
     }
     std::vector<uint64_t> ol(count);
     std::vector<int32_t> os(count);
-    if (copy_sync(ol.data(), d_dl, 8 * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        copy_sync(os.data(), d_st, 4 * count, hipMemcpyDeviceToHost, st) != hipSuccess)
+    // the lengths and statuses are consecutive (d_dl, d_st): one copy.  A lone buffer of at most 256 KiB
+    // of output space comes back whole in the same wait (a few KiB more over PCIe against a second round
+    // trip of copy and stream synchronisation; only its reported length is handed on)
+    const bool whole = count == 1 && dcap[0] > 0 && dcap[0] <= (uint64_t(256) << 10);
+    std::vector<uint8_t> lsb(12 * count), stage(whole ? dcap[0] : 0);
+    if (hipMemcpyAsync(lsb.data(), d_dl, 12 * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        (whole && hipMemcpyAsync(stage.data(), d_out + dofs[0], dcap[0], hipMemcpyDeviceToHost, st) != hipSuccess) ||
+        hipStreamSynchronize(st) != hipSuccess)
         return ZGPU_MEM_ERROR;
+    std::memcpy(ol.data(), lsb.data(), 8 * count);
+    std::memcpy(os.data(), lsb.data() + 8 * count, 4 * count);
     for (size_t i = 0; i < count; i++)
         if (ol[i] > dcap[i]) {
             ZTRACE("chl: buffer %zu: %lu bytes reported, capacity %lu\n", i, (unsigned long)ol[i],
@@ -1196,8 +1204,11 @@ int compress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_le
             return ZGPU_MEM_ERROR;
         }
     for (size_t i = 0; i < count; i++) {
-        if (ol[i] && copy_sync(dst[i], d_out + dofs[i], ol[i], hipMemcpyDeviceToHost, st) != hipSuccess)
+        if (whole) {
+            if (ol[i]) std::memcpy(dst[i], stage.data(), ol[i]);
+        } else if (ol[i] && copy_sync(dst[i], d_out + dofs[i], ol[i], hipMemcpyDeviceToHost, st) != hipSuccess) {
             return ZGPU_MEM_ERROR;
+        }
         dst_len[i] = ol[i];
         if (status) status[i] = os[i];
     }
@@ -1696,16 +1707,25 @@ int uncompress_host_locked(Ctx &c, const uint8_t *const *src, const size_t *src_
     std::vector<uint64_t> ol(count), ou(count);
     std::vector<int32_t> os(count);
     std::vector<uint32_t> ostop(count);
-    if (copy_sync(ol.data(), d_dl, 8 * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        copy_sync(ou.data(), d_used, 8 * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        copy_sync(os.data(), d_st, 4 * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        copy_sync(ostop.data(), d_stop, 4 * count, hipMemcpyDeviceToHost, st) != hipSuccess)
+    // the four result arrays in one wait, and a lone stream of at most 256 KiB of output space whole in
+    // the same one (as compress_host_locked)
+    const bool whole = count == 1 && dcap[0] > 0 && dcap[0] <= (uint64_t(256) << 10);
+    std::vector<uint8_t> stage(whole ? dcap[0] : 0);
+    if (hipMemcpyAsync(ol.data(), d_dl, 8 * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(ou.data(), d_used, 8 * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(os.data(), d_st, 4 * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(ostop.data(), d_stop, 4 * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        (whole && hipMemcpyAsync(stage.data(), d_out + dofs[0], dcap[0], hipMemcpyDeviceToHost, st) != hipSuccess) ||
+        hipStreamSynchronize(st) != hipSuccess)
         return ZGPU_MEM_ERROR;
     for (size_t i = 0; i < count; i++)
         if (ol[i] > dcap[i] || ou[i] > sl[i]) return ZGPU_MEM_ERROR;   // device-reported sizes (see compress_host_locked)
     for (size_t i = 0; i < count; i++) {
-        if (ol[i] && copy_sync(dst[i], d_out + dofs[i], ol[i], hipMemcpyDeviceToHost, st) != hipSuccess)
+        if (whole) {
+            if (ol[i]) std::memcpy(dst[i], stage.data(), ol[i]);
+        } else if (ol[i] && copy_sync(dst[i], d_out + dofs[i], ol[i], hipMemcpyDeviceToHost, st) != hipSuccess) {
             return ZGPU_MEM_ERROR;
+        }
         dst_len[i] = ol[i];
         if (src_used) src_used[i] = ou[i];
         if (status) status[i] = os[i];
