@@ -33,9 +33,10 @@
  * 28 level-0 sessions with output buffers from 1 byte up).  After Z_FINISH the
  * caller continues with Z_FINISH until Z_STREAM_END (zlib.h); a flush call
  * that ran out of output space and is given more input instead of the same
- * flush again goes on as the reference does (tests/test_gpu_fuzz.py), except
- * when a preset dictionary's 6-byte zlib header takes all of the first call's
- * output space: the stream stays valid but may differ.
+ * flush again goes on as the reference does (tests/test_gpu_fuzz.py).  A first
+ * call whose output space is exactly the header goes as the reference's does,
+ * with a preset dictionary too, except a flush call whose input's first string
+ * is in the dictionary (refused, below).
  * deflateSetDictionary, deflateSetHeader, deflatePrime, deflateTune and
  * deflateParams give the reference's stream: deflateParams flushes with Z_BLOCK
  * itself when the level's function or the strategy changes (as deflate.c does)
@@ -63,6 +64,10 @@
  *     into the next stream as the reference carries it; then a preset
  *     dictionary, or a switch to level 0 or to a deflate_fast level before the
  *     next input, is refused;
+ *   - a first deflate() flush call whose output space is exactly a preset
+ *     dictionary's 6-byte header, with the input's first three bytes in the
+ *     dictionary (or a Z_NO_FLUSH one whose first read could fill a block
+ *     before its first literal);
  *   - inflatePrime other than on a raw stream before its first input.
  * inflateUndermine returns Z_DATA_ERROR (as a reference built without
  * INFLATE_ALLOW_INVALID_DISTANCE_TOOFAR_ARRR does).  inflateBack reports a

@@ -284,8 +284,10 @@ def _dict_header_sessions():
     """First calls after deflateSetDictionary whose output space is exactly the 6-byte zlib header with
     its DICTID.  deflate_slow then stops at its first lazy literal; where the input's first three bytes
     are nowhere in the dictionary its first decision finds no match and the literal comes at the second,
-    as with no history.  Those sessions (and every deflate_fast / _huff / _rle one) are compared with the
-    system zlib; the others must be refused with strm->msg (returned as `refused`)."""
+    as with no history.  Under Z_NO_FLUSH the stop's place does not matter (the next call goes on from it
+    with the same state), so those are modelled too (round 6), unless the first read could fill a block
+    before the first literal.  Those sessions (and every deflate_fast / _huff / _rle one) are compared
+    with the system zlib; the others must be refused with strm->msg (returned as `refused`)."""
     rng = np.random.default_rng(606)
     data = b"".join(datagen.make(k, 40000, 78) for k in ("text", "mix", "runs"))
     S = []
@@ -313,14 +315,65 @@ def _dict_header_sessions():
                                     break
                         fin = flush == 4
                         slow = level >= 4 and strategy in (0, 1)
-                        # refused: the input's first string in the dictionary
-                        refused = slow and n >= 3 and first in d[-32768:]
+                        # refused: a flush call (or a first read that could fill a block before its first
+                        # literal) whose input's first string is in the dictionary
+                        dl = len(d[-32768:])
+                        refused = slow and n >= 3 and first in d[-32768:] and (flush != 0 or
+                                                                               min(n, 65536 - dl) >= 3 * 16383)
                         S.append((refused, [["init", level, 15, 8, strategy], ["dict", d],
                                             ["deflate1", data[:n], flush, 6],
                                             ["deflate1", b"", flush, 7, True],
                                             ["deflate", b"" if fin else data[n:n + 3000], 4 if fin else 2, None, True],
                                             ["deflate", b"" if fin else data[n + 3000:n + 9000], 4]]))
     return S
+
+
+def _dict_header_no_flush_sessions():
+    """Z_NO_FLUSH first calls after deflateSetDictionary whose output space is exactly the 6-byte header,
+    where the dictionary holds the input's start or all of it (the parse may match to the input's end
+    before its first literal): lazy levels, Z_FILTERED, memLevels 3 / 8 / 9, input sizes around
+    MIN_LOOKAHEAD and up to the first read.  Refused where the first read could fill a block before the
+    first literal (3 bytes a symbol for a whole symbol buffer)."""
+    data = b"".join(datagen.make(k, 40000, 79) for k in ("text", "runs", "mix"))
+    S = []
+    for level in (4, 6, 9):
+        for strategy in (0, 1):
+            for mem in (3, 8, 9):
+                for n in (3, 10, 261, 262, 263, 1000, 5000, 20000, 40000):
+                    for dk in ("prefix", "whole"):
+                        d = data[80000:83000] + (data[:64] if dk == "prefix" else data[:n])
+                        dl = min(len(d), 32768)
+                        refused = n >= 3 and min(n, 65536 - dl) >= 3 * ((1 << (mem + 6)) - 1)
+                        S.append((refused, [["init", level, 15, mem, strategy], ["dict", d],
+                                            ["deflate1", data[:n], 0, 6],
+                                            ["deflate1", b"", 0, 7, True],
+                                            ["deflate", data[n:n + 3000], 2, None, True],
+                                            ["deflate", data[n + 3000:n + 9000], 4]]))
+    return S
+
+
+def test_first_call_dictionary_header_no_flush(zg):
+    """Round 6: a Z_NO_FLUSH first call whose output space is exactly a preset dictionary's header is
+    modelled even when the dictionary holds the input (its first decisions find matches): the call stops
+    at its first lazy literal or at need_more, and the next call goes on from there with the same state,
+    which is the model's stop at need_more.  Every call's status / avail_in / avail_out and the stream
+    equal the system zlib's; the sessions whose first read could fill a block first are refused."""
+    libz = _system_zlib()
+    L = zg.load()
+    bad, n_ref, n_cmp = [], 0, 0
+    for k, (refused, ops) in enumerate(_dict_header_no_flush_sessions()):
+        rg, g = run_zsession(L, ops)
+        if refused:
+            if rg[2][0] != -2 or rg[2][2] != 6:
+                bad.append(("refusal", k, ops[0], len(ops[2][1]), rg[:3]))
+            n_ref += 1
+            continue
+        rz, z = run_zsession(libz, ops)
+        n_cmp += 1
+        if rz != rg or z != g:
+            bad.append((k, ops[0], len(ops[2][1]), rz, rg, len(z), len(g)))
+    assert not bad, (len(bad), bad[:3])
+    assert n_cmp > 0 and n_ref > 0
 
 
 def test_first_call_output_space_is_the_dictionary_header(zg):

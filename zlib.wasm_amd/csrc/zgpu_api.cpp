@@ -3470,16 +3470,24 @@ static int deflate_body(z_streamp strm, int flush) {
         if (s->out_pos == before && strm->avail_out == s->out.size() - before && s->level != 0 && slow_fn &&
             P - s->rd >= 2) {
             const char *why = nullptr;
-            if (s->dict_len > 0 && P - s->rd >= 3) {
-                // with a dictionary the first decision may find a match (history), and the stop at the
-                // first lazy literal moves with the parse; without one (the input's first three bytes
-                // nowhere in the dictionary) the literal comes at the second decision, as with no history
+            // the first fill_window's read: window_size - strstart
+            const size_t first = std::min<size_t>(P - s->rd, (size_t(2) << s->wbits) - s->dict_len);
+            const size_t sym_limit = ((size_t)1 << (s->mem_level + 6)) - 1;
+            if (s->dict_len > 0 && P - s->rd >= 3 && (flush != Z_NO_FLUSH || first >= 3 * sym_limit)) {
+                // With a dictionary the first decision may find a match (history), and the stop at the
+                // first lazy literal moves with the parse.  Under Z_NO_FLUSH that does not matter: the
+                // call stops at that literal or at need_more, whichever comes first, and the loop goes on
+                // from there in the next call with the same state -- the model's stop at need_more -- as
+                // long as no block fills first (less than 3 bytes a symbol for a whole symbol buffer).
+                // A flush call whose input the dictionary covers to its end would act on its flush
+                // instead; without a match at the first decision (the input's first three bytes nowhere
+                // in the dictionary) the literal comes at the second decision, as with no history.
                 const uint8_t *d0 = s->in.data() + (s->rd - s->dict_len - s->in_base);
                 const uint8_t *x = strm->next_in;
                 for (size_t k = 0; k + 3 <= s->dict_len && !why; k++)
                     if (d0[k] == x[0] && d0[k + 1] == x[1] && d0[k + 2] == x[2])
-                        why = "deflate: a first call whose output space is exactly a preset dictionary's header, "
-                              "with the input's first string in the dictionary, is not modelled";
+                        why = "deflate: a first flush call whose output space is exactly a preset dictionary's "
+                              "header, with the input's first string in the dictionary, is not modelled";
             }
             if (why) {
                 s->out.resize(before);
